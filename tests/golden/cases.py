@@ -1,0 +1,49 @@
+"""Access to the golden fixtures (no dependency on /root/reference at run time)."""
+import ast
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+E2E_CASES = ["box40x32_b2x2_s5", "box70x54_b1x1_s20", "box70x54_b3x2_s20",
+             "box48x40_flags000_s10", "box48x40_cart_s10", "bs_b1x1_s60", "bs_b4x2_s60"]
+KERNEL_GEOMS = ["b66x50", "b1x1", "b130x7"]
+KERNEL_NAMES = ["sw_update_ssh", "sw_update_uv", "sw_next_step", "uv_trans_vort", "uv_trans",
+                "uv_diff2", "stress_components", "hh_init", "hh_update", "hh_shift"]
+
+
+def _f(s):
+    return float(str(s).replace("d", "e").replace("D", "e"))
+
+
+def load_e2e(name):
+    """-> dict(basin=..., sw=..., bxy=(bx, by), steps=N, mask=int32 (nx,ny) or None, z=npz)."""
+    z = np.load(os.path.join(HERE, f"e2e_{name}.npz"))
+    b = ast.literal_eval(str(z["meta/basin"]))
+    sw = ast.literal_eval(str(z["meta/sw"]))
+    basin = dict(nx=int(b["nx"]), ny=int(b["ny"]), dxst=_f(b["dxst"]), dyst=_f(b["dyst"]),
+                 rlon=_f(b["rlon"]), rlat=_f(b["rlat"]), curve_grid=int(b["curve"]))
+    mask = None
+    if "in/mask_packed" in z.files:
+        n = basin["nx"] * basin["ny"]
+        mask = np.unpackbits(z["in/mask_packed"])[:n].astype(np.int32).reshape(
+            (basin["nx"], basin["ny"]), order="F")
+    swc = dict(full_free_surface=int(sw["ffs"]), trans_terms=int(sw["trans"]), ksw_lat=int(sw["ksw"]),
+               time_smooth=_f(sw["ts"]))
+    return dict(basin=basin, sw=swc, bxy=tuple(int(v) for v in z["meta/bxy"]), steps=int(z["meta/steps"]),
+                mask=mask, z=z)
+
+
+def e2e_blocks(z):
+    """-> {(bm, bn): info int32[8]} for the blocks in an e2e fixture."""
+    out = {}
+    for k in z.files:
+        if k.endswith("/info"):
+            bm, bn = k[1:].split("/")[0].split("_")
+            out[(int(bm), int(bn))] = z[k]
+    return out
+
+
+def load_kernels(geom):
+    return np.load(os.path.join(HERE, f"kernels_{geom}.npz"))

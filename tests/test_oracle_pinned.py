@@ -1,0 +1,108 @@
+"""Pin the CPU oracle (oracle/sw_oracle.c + oracle/oracle.py) against the compiled
+reference's own outputs (tests/golden, made by tests/golden/gen_golden.py).
+
+Bar: bitwise equality of every output array (halos and untouched cells included)."""
+import ctypes as C
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.golden import cases
+
+# oracle entry point + argument names (same order as the reference kernel, see gen_golden.KERNELS)
+ORC_ARGS = {
+    "sw_update_ssh": ("orc_sw_update_ssh", ["tau"], ["lu", "dx", "dy", "dxh", "dyh", "hhu", "hhv", "sshn",
+                                                     "sshp", "ubrtr", "vbrtr"]),
+    "sw_update_uv": ("orc_sw_update_uv", ["tau"], ["lcu", "lcv", "dxt", "dyt", "dxh", "dyh", "dxb", "dyb",
+                                                   "hhu", "hhu_n", "hhu_p", "hhv", "hhv_n", "hhv_p", "hhh", "ssh",
+                                                   "ubrtr", "ubrtrn", "ubrtrp", "vbrtr", "vbrtrn", "vbrtrp",
+                                                   "r_diss", "rlh_s", "RHSx", "RHSy", "RHSx_adv", "RHSy_adv",
+                                                   "RHSx_dif", "RHSy_dif"]),
+    "sw_next_step": ("orc_sw_next_step", ["time_smooth"], ["lu", "lcu", "lcv", "ssh", "sshn", "sshp", "ubrtr",
+                                                           "ubrtrn", "ubrtrp", "vbrtr", "vbrtrn", "vbrtrp"]),
+    "uv_trans_vort": ("orc_uv_trans_vort", [], ["luu", "dxt", "dyt", "dxb", "dyb", "ubrtr", "vbrtr", "vort"]),
+    "uv_trans": ("orc_uv_trans", [], ["lcu", "lcv", "luu", "dxh", "dyh", "ubrtr", "vbrtr", "vort", "hhq", "hhu",
+                                      "hhv", "hhh", "RHSx_adv", "RHSy_adv"]),
+    "uv_diff2": ("orc_uv_diff2", [], ["lcu", "lcv", "dx", "dy", "dxt", "dyt", "dxh", "dyh", "dxb", "dyb", "mu",
+                                      "str_t", "str_s", "hhq", "hhu", "hhv", "hhh", "RHSx_dif", "RHSy_dif"]),
+    "stress_components": ("orc_stress_components", [], ["lu", "luu", "dx", "dy", "dxt", "dyt", "dxh", "dyh",
+                                                        "dxb", "dyb", "ubrtrp", "vbrtrp", "str_t", "str_s"]),
+    "hh_init": ("orc_hh_init", ["ffs"], ["lu", "llu", "llv", "luh", "dx", "dy", "dxt", "dyt", "dxh", "dyh",
+                                         "dxb", "dyb", "hhq", "hhq_p", "hhq_n", "hhu", "hhu_p", "hhu_n", "hhv",
+                                         "hhv_p", "hhv_n", "hhh", "hhh_p", "hhh_n", "ssh", "sshp", "hhq_rest"]),
+    "hh_update": ("orc_hh_update", [], ["lu", "llu", "llv", "luh", "dx", "dy", "dxt", "dyt", "dxh", "dyh", "dxb",
+                                        "dyb", "hhq_n", "hhu_n", "hhv_n", "hhh_n", "ssh", "hhq_rest"]),
+    "hh_shift": ("orc_hh_shift", ["time_smooth"], ["lu", "llu", "llv", "luh", "hhq", "hhq_p", "hhq_n", "hhu",
+                                                   "hhu_p", "hhu_n", "hhv", "hhv_p", "hhv_n", "hhh", "hhh_p",
+                                                   "hhh_n"]),
+}
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(np.asarray(a).ravel(order="F"))
+    b = np.ascontiguousarray(np.asarray(b).ravel(order="F"))
+    return a.dtype == b.dtype and a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def run_oracle_kernel(z, kname):
+    L = O.lib()
+    geom = [int(v) for v in z["geom"]]
+    work = {k[3:]: z[k].copy(order="F") for k in z.files if k.startswith("in/")}
+    sym, scalars, names = ORC_ARGS[kname]
+    sc = []
+    for s in scalars:
+        if s == "ffs":
+            sc.append(C.c_int(int(z["full_free_surface"])))
+        else:
+            sc.append(C.c_double(float(z[s])))
+    getattr(L, sym)(*geom, *sc, *[work[n].ctypes.data_as(C.c_void_p) for n in names])
+    return work
+
+
+@pytest.mark.parametrize("geom", cases.KERNEL_GEOMS)
+@pytest.mark.parametrize("kname", cases.KERNEL_NAMES)
+def test_oracle_kernel_matches_reference(geom, kname):
+    z = cases.load_kernels(geom)
+    work = run_oracle_kernel(z, kname)
+    outs = [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]
+    assert outs, kname
+    for nm in outs:
+        assert bits_equal(work[nm], z[f"{kname}/{nm}"]), f"{kname}:{nm} differs from the reference"
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a.ravel(order="F")).tobytes()).hexdigest()
+
+
+def build_oracle_model(case):
+    b = case["basin"]
+    basin = O.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"],
+                          rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"])
+    sw = O.SWConfig(**case["sw"])
+    return O.OracleModel(basin, sw, *case["bxy"])
+
+
+@pytest.mark.parametrize("name", cases.E2E_CASES)
+def test_oracle_end_to_end_matches_reference(name):
+    case = cases.load_e2e(name)
+    z = case["z"]
+    m = build_oracle_model(case).init().run(case["steps"])
+    blocks = cases.e2e_blocks(z)
+    assert len(blocks) == len(m.blocks)
+    for k, blk in enumerate(m.blocks):
+        info = blocks[(blk.bm, blk.bn)]
+        assert list(info) == list(blk.args)
+        for nm, a in m.f[k].items():
+            key = f"b{blk.bm}_{blk.bn}/sha/{nm}"
+            if key not in z.files:
+                continue
+            assert _sha(a) == str(z[key]), f"{name}: block ({blk.bm},{blk.bn}) field {nm} differs"
+
+
+def test_uniform_decomposition_sizes():
+    # decomposition.f90:448-482 on BS x-size 285 over 4 blocks: 71/71/71/72
+    assert O.uniform_sizes(285, 4) == [71, 71, 71, 72]
+    assert O.uniform_sizes(159, 2) == [79, 80]
+    assert sum(O.uniform_sizes(1024, 8)) == 1024
