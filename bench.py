@@ -1,0 +1,165 @@
+"""bench.py -- cell-updates/s of the SW barotropic step on the 4096 x 4096 box (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--scaling strong|weak]
+
+One process per GPU (launched by torch.distributed.run for N > 1); the box is split into one
+block per GPU with the reference's block grid (2x1, 2x2, 4x2) and halos are
+exchanged over RCCL inside libocn_sw.  Rank 0 prints ONE JSON line.
+
+value      = interior cells (nx-4)(ny-4) x K / t_loop, t_loop = max over ranks of the K timed steps
+             (barrier + device sync on both sides), inputs resident in HBM.
+roofline   = the dominant stage kernel: algorithmic bytes per launch (SURVEY.md 8a B/cell x cells)
+             / its mean launch time from HIP events on the context stream, vs 8.0 TB/s.
+cpu_baseline = the C restatement (oracle/, 1 core) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "cell-updates/s, SW barotropic step on 4096x4096 box; %HBM BW at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# algorithmic bytes per interior cell per stage (sum = 1136)
+STAGE_BYTES = {"sw_update_ssh": 68, "hh_update": 96, "uv_trans_vort": 44, "uv_trans": 84,
+               "stress_components": 72, "uv_diff2": 96, "sw_update_uv": 200, "sw_next_step": 132,
+               "hh_shift": 176, "hh_init": 168}
+B_ALG = sum(STAGE_BYTES.values())
+
+
+def dims_create(n: int):
+    """MPI_Dims_create(n, 2) as used by the reference (mpp.f90:89): 2 -> 2x1, 4 -> 2x2, 8 -> 4x2."""
+    import math
+    for f in range(int(math.isqrt(n)), 0, -1):
+        if n % f == 0:
+            return n // f, f
+    return n, 1
+
+
+def cpu_baseline(seconds_hint: float = 10.0):
+    """Time the oracle (C restatement, one core) on a bounded sample: 2048^2 box, 6 steps."""
+    from oracle import oracle as O
+    n, steps = 2048, 16
+    om = O.OracleModel(O.BasinConfig(nx=n + 4, ny=n + 4), O.SWConfig(), 1, 1).init()
+    om.run(1)
+    t0 = time.perf_counter()
+    om.run(steps)
+    dt = time.perf_counter() - t0
+    return {"value": n * n * steps / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/sw_oracle.c (gcc -O2 -ffp-contract=off), {n}x{n} box, 1 block, {steps} timed steps "
+                      f"after 1 warm-up step, {dt:.1f} s"}
+
+
+def load_traffic(stage: str, cells: int):
+    """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary (profiles/), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        rec = d["kernels"][stage]
+        if int(rec["cells"]) != cells:
+            return None
+        return float(rec["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=4096, help="box interior size (N x N)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--graph", action="store_true", help="replay steps as hipGraphs (single process)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+    import ocean_model_arch_amd as amd
+
+    torch.cuda.set_device(local_rank)
+    bx, by = dims_create(world)
+    n = args.n
+    nxbox, nybox = (n, n) if args.scaling == "strong" else (n * bx, n * by)
+    basin = amd.BasinConfig(nx=nxbox + 4, ny=nybox + 4)
+    model = amd.OceanModel(basin, amd.SWConfig(), amd.ParallelConfig(bx, by), rank=rank, nranks=world,
+                           device=local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        uid = [amd.make_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        model.attach_comm(uid[0])
+    if args.graph:
+        model.set_graph(True)
+    model.init()
+    model.step(args.warmup, check_every=1).synchronize()
+    model.set_stage_timing(not args.graph)
+    model.stage_times()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    model.step(args.steps, check_every=1)
+    model.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    times = model.stage_times()
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    cells = nxbox * nybox
+    value = cells * args.steps / dt
+    local_cells = model.interior_cells
+    out = None
+    if rank == 0:
+        stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in STAGE_BYTES}
+        roof = None
+        if stage_ms:
+            dom = max(stage_ms, key=lambda s: stage_ms[s])
+            alg = STAGE_BYTES[dom] * local_cells
+            achieved = alg / (stage_ms[dom] * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": load_traffic(dom, local_cells),
+                    "alg_bytes_per_launch": alg, "launch_ms": round(stage_ms[dom], 4)}
+        step_gbs = B_ALG * cells * args.steps / dt / 1e9 / world
+        out = {"metric": METRIC, "value": value, "unit": "cell-updates/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+               "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic (Gaussian SSH hump in a closed flat-bottom box, SURVEY.md 8d)",
+               "config": {"workload": f"{nxbox}x{nybox} box, {bx}x{by} blocks (1 per GPU), sw.par defaults, tau=1s",
+                          "box": [nxbox, nybox], "blocks": [bx, by], "graph": bool(args.graph),
+                          "parallelism": f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else "1 block"},
+               "roofline": roof,
+               "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),
+               "step_alg_gbs_per_gpu": round(step_gbs, 1),
+               "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()}}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+    model.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,244 @@
+/*
+ * ocn_sw.h -- C ABI of the MI355X-native shallow-water barotropic step.
+ *
+ * Drop-in boundary for the reference's kernel and PSy layers
+ * (Andrcraft9/ocean_model_arch; citations are path:line in that tree):
+ *
+ *  - Kernel layer: one entry per SW stage.  Each replaces the Fortran kernel
+ *    `S(nx_start,nx_end,ny_start,ny_end,bnd_x1,bnd_x2,bnd_y1,bnd_y2,[scalars],arrays...)`
+ *    (every argument by reference, explicit-shape arrays) and its CUDA-Fortran twin
+ *    `S_gpu<<<grid,16x16,0,stream(k)>>>` (gpu/kernel/ *_gpu.f90).  Same argument order,
+ *    same meaning, same write set, bitwise-identical results.
+ *  - PSy layer: a model context that owns the per-block device storage of ocean_type /
+ *    grid_type (core/ocean.f90:14-48, core/grid.f90:23-90), runs one stage plus its halo
+ *    sync (envoke, core/kernel_interface.f90:48-119) or the whole step
+ *    (expl_shallow_water, control/shallow_water/shallow_water.f90:22-94), and exchanges
+ *    1-wide 8-direction halos (sync/hybrid_sync, shared/mpp/sync.f90:294-556) between blocks
+ *    of this process and, over RCCL, with blocks of other processes (one block per GPU).
+ *
+ * Conventions
+ *  - Indices are the reference's 1-based global Fortran indices.
+ *  - Arrays are column-major A(bnd_x1:bnd_x2, bnd_y1:bnd_y2); a pointer is the DEVICE
+ *    address of A(bnd_x1,bnd_y1); the leading dimension is ocn_block.pitch elements
+ *    (>= bnd_x2-bnd_x1+1; r4 and r8 arrays of one block share the pitch).
+ *  - `stream` is a hipStream_t passed as an opaque pointer (NULL = default stream).
+ *    Entries are asynchronous on that stream; they never allocate or synchronise.
+ *  - Return value: OCN_OK, or an OCN_ERR_* code (ocn_last_error() describes it).
+ *    The reference kernels return nothing and ignore CUDA status; here every status is
+ *    checked and reported.
+ *  - No torch types; plain pointers and sizes only.
+ */
+#ifndef OCN_SW_H
+#define OCN_SW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCN_ABI_VERSION 1
+
+enum {
+    OCN_OK = 0,
+    OCN_ERR_ARG = 1,       /* bad argument (null pointer, bounds, pitch, id) */
+    OCN_ERR_HIP = 2,       /* HIP runtime error */
+    OCN_ERR_COMM = 3,      /* RCCL error or missing communicator */
+    OCN_ERR_STATE = 4,     /* call out of order (e.g. step before init) */
+    OCN_ERR_BLOWUP = 5     /* check_ssh_err: |ssh| >= 1e4 on a sea point */
+};
+
+/* Block geometry (core/decomposition.f90:40-81, block k of domain_type). */
+typedef struct ocn_block {
+    int32_t nx_start, nx_end, ny_start, ny_end;   /* interior (bnx_start..) */
+    int32_t bnd_x1, bnd_x2, bnd_y1, bnd_y2;       /* array bounds (bbnd_x1..) */
+    int64_t pitch;                                 /* leading dimension, elements */
+} ocn_block;
+
+/* ---------------------------------------------------------------- kernel layer */
+/* kernel/shallow_water/vel_ssh.f90:69  sw_update_ssh_kernel */
+int ocn_sw_update_ssh(const ocn_block *b, double tau,
+                      const float *lu, const float *dx, const float *dy, const float *dxh, const float *dyh,
+                      const double *hhu, const double *hhv, double *sshn, const double *sshp,
+                      const double *ubrtr, const double *vbrtr, void *stream);
+
+/* kernel/shallow_water/depth.f90:101  hh_update_kernel */
+int ocn_hh_update(const ocn_block *b,
+                  const float *lu, const float *llu, const float *llv, const float *luh,
+                  const float *dx, const float *dy, const float *dxt, const float *dyt,
+                  const float *dxh, const float *dyh, const float *dxb, const float *dyb,
+                  double *hqn, double *hun, double *hvn, double *hhn,
+                  const double *sh, const double *h_r, void *stream);
+
+/* vel_ssh.f90:247  uv_trans_vort_kernel (nlev = 1) */
+int ocn_uv_trans_vort(const ocn_block *b, const float *luu,
+                      const float *dxt, const float *dyt, const float *dxb, const float *dyb,
+                      const double *u, const double *v, double *vort, void *stream);
+
+/* vel_ssh.f90:283  uv_trans_kernel (nlev = 1; hq accepted and unused, as in the reference) */
+int ocn_uv_trans(const ocn_block *b, const float *lcu, const float *lcv, const float *luu,
+                 const float *dxh, const float *dyh, const double *u, const double *v,
+                 const double *vort, const double *hq, const double *hu, const double *hv,
+                 const double *hh, double *RHSx, double *RHSy, void *stream);
+
+/* kernel/shallow_water/mixing.f90:14  stress_components_kernel (nlev = 1) */
+int ocn_stress_components(const ocn_block *b, const float *lu, const float *luu,
+                          const float *dx, const float *dy, const float *dxt, const float *dyt,
+                          const float *dxh, const float *dyh, const float *dxb, const float *dyb,
+                          const double *u, const double *v, double *str_t, double *str_s, void *stream);
+
+/* vel_ssh.f90:375  uv_diff2_kernel (nlev = 1; hu/hv accepted and unused, as in the reference) */
+int ocn_uv_diff2(const ocn_block *b, const float *lcu, const float *lcv,
+                 const float *dx, const float *dy, const float *dxt, const float *dyt,
+                 const float *dxh, const float *dyh, const float *dxb, const float *dyb,
+                 const double *mu, const double *str_t, const double *str_s,
+                 const double *hq, const double *hu, const double *hv, const double *hh,
+                 double *RHSx, double *RHSy, void *stream);
+
+/* vel_ssh.f90:108  sw_update_uv */
+int ocn_sw_update_uv(const ocn_block *b, double tau, const float *lcu, const float *lcv,
+                     const float *dxt, const float *dyt, const float *dxh, const float *dyh,
+                     const float *dxb, const float *dyb,
+                     const double *hhu, const double *hhun, const double *hhup,
+                     const double *hhv, const double *hhvn, const double *hhvp,
+                     const double *hhh, const double *ssh,
+                     const double *ubrtr, double *ubrtrn, const double *ubrtrp,
+                     const double *vbrtr, double *vbrtrn, const double *vbrtrp,
+                     const float *rdis, const float *rlh_s,
+                     const double *RHSx, const double *RHSy, const double *RHSx_adv,
+                     const double *RHSy_adv, const double *RHSx_dif, const double *RHSy_dif,
+                     void *stream);
+
+/* vel_ssh.f90:197  sw_next_step (writes interior + halo ring) */
+int ocn_sw_next_step(const ocn_block *b, double time_smooth,
+                     const float *lu, const float *lcu, const float *lcv,
+                     double *ssh, double *sshn, double *sshp,
+                     double *ubrtr, double *ubrtrn, double *ubrtrp,
+                     double *vbrtr, double *vbrtrn, double *vbrtrp, void *stream);
+
+/* depth.f90:164  hh_shift_kernel (time_smooth is a module variable there; an argument here) */
+int ocn_hh_shift(const ocn_block *b, double time_smooth,
+                 const float *lu, const float *llu, const float *llv, const float *luh,
+                 double *hq, double *hqp, double *hqn, double *hu, double *hup, double *hun,
+                 double *hv, double *hvp, double *hvn, double *hh, double *hhp, double *hhn,
+                 void *stream);
+
+/* depth.f90:14  hh_init_kernel (full_free_surface is a module variable there; an argument here) */
+int ocn_hh_init(const ocn_block *b, int32_t full_free_surface,
+                const float *lu, const float *llu, const float *llv, const float *luh,
+                const float *dx, const float *dy, const float *dxt, const float *dyt,
+                const float *dxh, const float *dyh, const float *dxb, const float *dyb,
+                double *hq, double *hqp, double *hqn, double *hu, double *hup, double *hun,
+                double *hv, double *hvp, double *hvn, double *hh, double *hhp, double *hhn,
+                const double *sh, const double *shp, const double *h_r, void *stream);
+
+/* vel_ssh.f90:40  check_ssh_err_kernel: device reduction; *nbad (device int32) += bad points */
+int ocn_check_ssh_err(const ocn_block *b, const float *lu, const double *ssh, int32_t *nbad_device,
+                      void *stream);
+
+/* ---------------------------------------------------------------- PSy layer: model context */
+
+/* Field ids: storage of ocean_type / grid_type restricted to what the SW step touches. */
+enum {
+    /* real(4) */
+    OCN_LU = 0, OCN_LUU, OCN_LUH, OCN_LCU, OCN_LCV, OCN_LLU, OCN_LLV,
+    OCN_DX, OCN_DY, OCN_DXT, OCN_DYT, OCN_DXH, OCN_DYH, OCN_DXB, OCN_DYB, OCN_RLH_S, OCN_R_DISS,
+    OCN_NUM_R4,
+    /* real(8) */
+    OCN_SSH = 32, OCN_SSHN, OCN_SSHP, OCN_UBRTR, OCN_UBRTRN, OCN_UBRTRP, OCN_VBRTR, OCN_VBRTRN, OCN_VBRTRP,
+    OCN_HHQ, OCN_HHQ_P, OCN_HHQ_N, OCN_HHU, OCN_HHU_P, OCN_HHU_N, OCN_HHV, OCN_HHV_P, OCN_HHV_N,
+    OCN_HHH, OCN_HHH_P, OCN_HHH_N, OCN_HHQ_REST, OCN_VORT, OCN_STR_T, OCN_STR_S, OCN_MU,
+    OCN_RHSX, OCN_RHSY, OCN_RHSX_ADV, OCN_RHSY_ADV, OCN_RHSX_DIF, OCN_RHSY_DIF,
+    OCN_FIELD_END
+};
+#define OCN_NUM_R8 (OCN_FIELD_END - OCN_SSH)
+
+/* Stage ids, in the order of expl_shallow_water (shallow_water.f90:36-92). */
+enum {
+    OCN_STAGE_SW_UPDATE_SSH = 0, OCN_STAGE_HH_UPDATE, OCN_STAGE_UV_TRANS_VORT, OCN_STAGE_UV_TRANS,
+    OCN_STAGE_STRESS_COMPONENTS, OCN_STAGE_UV_DIFF2, OCN_STAGE_SW_UPDATE_UV, OCN_STAGE_SW_NEXT_STEP,
+    OCN_STAGE_HH_SHIFT, OCN_STAGE_HH_INIT, OCN_STAGE_CHECK_SSH_ERR, OCN_NUM_STAGES
+};
+
+/* Basin description (configs/basinpar.f90:53-91, basin.par lines 1-18) */
+typedef struct ocn_basin {
+    int32_t nx, ny;
+    double dxst, dyst, rlon, rlat;
+    int32_t curve_grid;                 /* 0 carthesian, 1 undistorted sphere */
+    double rotation_on_lon, rotation_on_lat;
+} ocn_basin;
+
+/* SW switches (configs/sw.f90:34-41, sw.par lines 1-5) */
+typedef struct ocn_sw_params {
+    int32_t full_free_surface, trans_terms, ksw_lat;
+    double time_smooth, lvisc_2;
+} ocn_sw_params;
+
+/* Decomposition request (parallel.par + _DD_MANUAL_BLOCK_GRID_, decomposition.f90:856-858) */
+typedef struct ocn_decomp {
+    int32_t bnx, bny;        /* block grid (total, not per process) */
+    int32_t nranks, rank;    /* processes; blocks are dealt by create_uniform_decomposition */
+    int32_t device;          /* HIP device of this process */
+} ocn_decomp;
+
+/* Per-block information returned to hosts (block k of this process, k = 0..count-1). */
+typedef struct ocn_block_info {
+    ocn_block geom;
+    int32_t bm, bn;                       /* block coordinates in the block grid (1-based) */
+    int32_t nbr_rank[8];                  /* rank of neighbour in dirs 1..8 (kernel_macros.fi:4-12); -1 land, -2 outside */
+    int32_t nbr_k[8];                     /* local index on that rank, or -1 */
+} ocn_block_info;
+
+typedef struct ocn_ctx ocn_ctx;
+
+/* Create a context: decomposes the basin (mask = int32 global (nx,ny) column-major, 0 = sea,
+ * 1 = land, or NULL for the closed box of tools/io.f90:49-59), allocates every field of every
+ * local block on `device` (zero-filled, as data_types.f90:517-533). */
+int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_decomp *dec,
+                   const int32_t *mask, ocn_ctx **out);
+int ocn_ctx_destroy(ocn_ctx *ctx);
+
+int ocn_ctx_block_count(const ocn_ctx *ctx);
+int ocn_ctx_block_info(const ocn_ctx *ctx, int k, ocn_block_info *out);
+/* Device pointer of field `id` of local block k (element (bnd_x1,bnd_y1)); NULL on error. */
+void *ocn_ctx_field(const ocn_ctx *ctx, int k, int id);
+/* Compute stream of the context (hipStream_t). */
+void *ocn_ctx_stream(const ocn_ctx *ctx);
+
+/* RCCL: unique id (128 bytes) made on rank 0, broadcast by the host, then attached. */
+int ocn_comm_unique_id(void *out_id, int32_t nbytes);
+int ocn_ctx_attach_comm(ocn_ctx *ctx, const void *unique_id, int32_t nbytes);
+
+/* Initial state: init_grid_data + init_ocean_data (control/init_data.f90:29-125). */
+int ocn_ctx_init_state(ocn_ctx *ctx);
+
+/* sync(domain, field) for one field over all local blocks (+ remote neighbours). */
+int ocn_ctx_sync(ocn_ctx *ctx, int field_id);
+/* envoke(stage): the stage on every local block, then its sync list (sw_interface.f90). */
+int ocn_ctx_stage(ocn_ctx *ctx, int stage_id, double tau);
+/* expl_shallow_water(tau) x nsteps.  check_every: run check_ssh_err every N steps (0 = never). */
+int ocn_ctx_step(ocn_ctx *ctx, double tau, int32_t nsteps, int32_t check_every);
+/* Wait for the context's stream; returns OCN_ERR_BLOWUP if a check found |ssh| >= 1e4. */
+int ocn_ctx_synchronize(ocn_ctx *ctx);
+
+/* Host <-> device copies of a whole field of local block k (host array: Fortran order,
+ * leading dim bnd_x2-bnd_x1+1, 4 or 8 bytes per element by field kind). Synchronous. */
+int ocn_ctx_download(ocn_ctx *ctx, int k, int field_id, void *host);
+int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
+
+/* Execution options.  OCN_OPT_GRAPH: replay each step as one hipGraph (single-process runs).
+ * OCN_OPT_STAGE_TIMING: bracket every stage's kernels with HIP events on the context stream. */
+int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
+enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3 };
+
+/* Per-stage device time (ms, summed) and launch counts since the last call, from the HIP
+ * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_STAGES entries.  Synchronises. */
+int ocn_ctx_stage_times(ocn_ctx *ctx, double *ms, int64_t *counts);
+
+const char *ocn_last_error(void);
+int ocn_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OCN_SW_H */

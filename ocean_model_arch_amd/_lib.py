@@ -1,0 +1,140 @@
+"""ctypes binding of libocn_sw.so (include/ocn_sw.h).
+
+The HIP library is the product: there is no CPU fallback.  If the shared object is missing
+or cannot be loaded, every entry point raises ``OcnLibraryError`` -- loudly, on purpose.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libocn_sw.so")
+_CSRC = os.path.join(_HERE, "csrc")
+
+OCN_OK, OCN_ERR_ARG, OCN_ERR_HIP, OCN_ERR_COMM, OCN_ERR_STATE, OCN_ERR_BLOWUP = range(6)
+
+# field ids (include/ocn_sw.h)
+R4_NAMES = ["lu", "luu", "luh", "lcu", "lcv", "llu", "llv", "dx", "dy", "dxt", "dyt", "dxh", "dyh",
+            "dxb", "dyb", "rlh_s", "r_diss"]
+R8_NAMES = ["ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp", "vbrtr", "vbrtrn", "vbrtrp",
+            "hhq", "hhq_p", "hhq_n", "hhu", "hhu_p", "hhu_n", "hhv", "hhv_p", "hhv_n",
+            "hhh", "hhh_p", "hhh_n", "hhq_rest", "vort", "str_t", "str_s", "mu",
+            "RHSx", "RHSy", "RHSx_adv", "RHSy_adv", "RHSx_dif", "RHSy_dif"]
+FIELD_ID = {n: i for i, n in enumerate(R4_NAMES)}
+FIELD_ID.update({n: 32 + i for i, n in enumerate(R8_NAMES)})
+
+STAGES = ["sw_update_ssh", "hh_update", "uv_trans_vort", "uv_trans", "stress_components", "uv_diff2",
+          "sw_update_uv", "sw_next_step", "hh_shift", "hh_init", "check_ssh_err"]
+STAGE_ID = {n: i for i, n in enumerate(STAGES)}
+OPT_GRAPH = 1
+OPT_STAGE_TIMING = 3
+
+# exported symbols (every one declared in include/ocn_sw.h)
+KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",
+                  "ocn_stress_components", "ocn_uv_diff2", "ocn_sw_update_uv", "ocn_sw_next_step",
+                  "ocn_hh_shift", "ocn_hh_init", "ocn_check_ssh_err"]
+CTX_SYMBOLS = ["ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
+               "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm",
+               "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
+               "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_set_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version"]
+ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
+
+
+class OcnLibraryError(RuntimeError):
+    pass
+
+
+class OcnError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[ocn error {code}] {msg}")
+        self.code = code
+
+
+class OcnBlock(C.Structure):
+    _fields_ = [("nx_start", C.c_int32), ("nx_end", C.c_int32), ("ny_start", C.c_int32), ("ny_end", C.c_int32),
+                ("bnd_x1", C.c_int32), ("bnd_x2", C.c_int32), ("bnd_y1", C.c_int32), ("bnd_y2", C.c_int32),
+                ("pitch", C.c_int64)]
+
+
+class OcnBasin(C.Structure):
+    _fields_ = [("nx", C.c_int32), ("ny", C.c_int32), ("dxst", C.c_double), ("dyst", C.c_double),
+                ("rlon", C.c_double), ("rlat", C.c_double), ("curve_grid", C.c_int32),
+                ("rotation_on_lon", C.c_double), ("rotation_on_lat", C.c_double)]
+
+
+class OcnSwParams(C.Structure):
+    _fields_ = [("full_free_surface", C.c_int32), ("trans_terms", C.c_int32), ("ksw_lat", C.c_int32),
+                ("time_smooth", C.c_double), ("lvisc_2", C.c_double)]
+
+
+class OcnDecomp(C.Structure):
+    _fields_ = [("bnx", C.c_int32), ("bny", C.c_int32), ("nranks", C.c_int32), ("rank", C.c_int32),
+                ("device", C.c_int32)]
+
+
+class OcnBlockInfo(C.Structure):
+    _fields_ = [("geom", OcnBlock), ("bm", C.c_int32), ("bn", C.c_int32),
+                ("nbr_rank", C.c_int32 * 8), ("nbr_k", C.c_int32 * 8)]
+
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libocn_sw.so in-tree for gfx950 (hipcc; no GPU needed)."""
+    cmd = ["make", "-s", "-f", os.path.join(_CSRC, "Makefile")]
+    if force:
+        cmd.insert(2, "-B")
+    subprocess.check_call(cmd)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OcnLibraryError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                              f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    try:
+        # torch (if used by the host) and this library must share one HIP runtime: import torch first
+        # so its libamdhip64.so.7 is the one resolved.
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    try:
+        L = C.CDLL(LIB_PATH)
+    except OSError as e:
+        raise OcnLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    for name in ALL_SYMBOLS:
+        getattr(L, name)
+    L.ocn_last_error.restype = C.c_char_p
+    L.ocn_ctx_field.restype = C.c_void_p
+    L.ocn_ctx_field.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    L.ocn_ctx_stream.restype = C.c_void_p
+    L.ocn_ctx_stream.argtypes = [C.c_void_p]
+    L.ocn_ctx_create.argtypes = [C.POINTER(OcnBasin), C.POINTER(OcnSwParams), C.POINTER(OcnDecomp), C.c_void_p,
+                                 C.POINTER(C.c_void_p)]
+    for nm in ("ocn_ctx_destroy", "ocn_ctx_init_state", "ocn_ctx_synchronize", "ocn_ctx_block_count"):
+        getattr(L, nm).argtypes = [C.c_void_p]
+    L.ocn_ctx_block_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(OcnBlockInfo)]
+    L.ocn_ctx_sync.argtypes = [C.c_void_p, C.c_int]
+    L.ocn_ctx_stage.argtypes = [C.c_void_p, C.c_int, C.c_double]
+    L.ocn_ctx_step.argtypes = [C.c_void_p, C.c_double, C.c_int32, C.c_int32]
+    L.ocn_ctx_download.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    L.ocn_ctx_upload.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    L.ocn_ctx_set_option.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
+    L.ocn_ctx_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ocn_ctx_attach_comm.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    L.ocn_comm_unique_id.argtypes = [C.c_void_p, C.c_int32]
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = ""):
+    if rc != OCN_OK:
+        msg = lib().ocn_last_error().decode(errors="replace")
+        raise OcnError(rc, f"{what}: {msg}" if what else msg)
+    return rc

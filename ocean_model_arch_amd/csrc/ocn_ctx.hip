@@ -1,0 +1,953 @@
+// ocn_ctx.hip -- PSy layer of the MI355X shallow-water step: model context, decomposition,
+// device storage, initial state, halo exchange (intra-device copies + RCCL), step driver.
+//
+// Reference counterparts (Andrcraft9/ocean_model_arch):
+//   storage        core/data_types.f90:44-144, core/ocean.f90:14-48, core/grid.f90:23-90
+//   decomposition  core/decomposition.f90:427-503 (uniform blocks), :614-669 (block -> rank),
+//                  :672-760 (local numbering, _MPP_SORTED_BLOCKS_), :950-1062 (neighbour maps)
+//   dispatcher     core/kernel_interface.f90:48-119 (envoke) + interface/shallow_water/sw_interface.f90
+//   algorithm      control/shallow_water/shallow_water.f90:22-94 (expl_shallow_water)
+//   halo           shared/mpp/sync.f90:294-556 + syncborder_block2D_gen_all.fi
+//   init           control/init_data.f90:29-125, kernel/service/grid_kernels.f90,
+//                  kernel/service/grid_parameters.f90:80-181, kernel/shallow_water/vel_ssh.f90:15-38
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ocn_internal.h"
+
+namespace ocn {
+
+static thread_local std::string g_last_error;
+
+int set_error(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+int check_hip(hipError_t e, const char *what)
+{
+    if (e == hipSuccess) return OCN_OK;
+    return set_error(OCN_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(call)                                          \
+    do {                                                      \
+        int _rc = check_hip((call), #call);                   \
+        if (_rc) return _rc;                                  \
+    } while (0)
+#define RC(call)                                              \
+    do {                                                      \
+        int _rc = (call);                                     \
+        if (_rc) return _rc;                                  \
+    } while (0)
+
+static inline bool is_r8(int id) { return id >= OCN_SSH && id < OCN_FIELD_END; }
+static inline bool is_r4(int id) { return id >= 0 && id < OCN_NUM_R4; }
+static inline int field_slot(int id) { return is_r4(id) ? id : OCN_NUM_R4 + (id - OCN_SSH); }
+static constexpr int kNumSlots = OCN_NUM_R4 + OCN_NUM_R8;
+
+// ------------------------------------------------------------------ halo segments
+// One strided 1-D run of doubles: dst[i*dst_stride] = src[i*src_stride], i < count.
+struct Seg {
+    const double *src;
+    double *dst;
+    long src_stride, dst_stride;
+    int count;
+};
+
+__global__ __launch_bounds__(256) void k_segments(const Seg *__restrict__ segs, int nseg)
+{
+    const int s = blockIdx.x;
+    if (s >= nseg) return;
+    const Seg g = segs[s];
+    for (int i = threadIdx.x; i < g.count; i += blockDim.x) g.dst[(long)i * g.dst_stride] = g.src[(long)i * g.src_stride];
+}
+
+__global__ void k_fill_r8(double *p, long n, double v)
+{
+    long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// ------------------------------------------------------------------ geometry helpers
+// decomposition.f90:94-290, directions macros/kernel_macros.fi:4-12
+struct Rect { int x0, x1, y0, y1; };
+static Rect boundary_points(const ocn_block &b, int dir)
+{
+    switch (dir) {
+    case 1: return {b.nx_end, b.nx_end, b.ny_start, b.ny_end};
+    case 2: return {b.nx_start, b.nx_start, b.ny_start, b.ny_end};
+    case 3: return {b.nx_start, b.nx_end, b.ny_end, b.ny_end};
+    case 4: return {b.nx_start, b.nx_end, b.ny_start, b.ny_start};
+    case 5: return {b.nx_end, b.nx_end, b.ny_end, b.ny_end};
+    case 6: return {b.nx_end, b.nx_end, b.ny_start, b.ny_start};
+    case 7: return {b.nx_start, b.nx_start, b.ny_end, b.ny_end};
+    default: return {b.nx_start, b.nx_start, b.ny_start, b.ny_start};
+    }
+}
+static Rect halo_points(const ocn_block &b, int dir)
+{
+    switch (dir) {
+    case 1: return {b.nx_end + 1, b.nx_end + 1, b.ny_start, b.ny_end};
+    case 2: return {b.nx_start - 1, b.nx_start - 1, b.ny_start, b.ny_end};
+    case 3: return {b.nx_start, b.nx_end, b.ny_end + 1, b.ny_end + 1};
+    case 4: return {b.nx_start, b.nx_end, b.ny_start - 1, b.ny_start - 1};
+    case 5: return {b.nx_end + 1, b.nx_end + 1, b.ny_end + 1, b.ny_end + 1};
+    case 6: return {b.nx_end + 1, b.nx_end + 1, b.ny_start - 1, b.ny_start - 1};
+    case 7: return {b.nx_start - 1, b.nx_start - 1, b.ny_end + 1, b.ny_end + 1};
+    default: return {b.nx_start - 1, b.nx_start - 1, b.ny_start - 1, b.ny_start - 1};
+    }
+}
+static int inverse_dir(int d)
+{
+    static const int inv[9] = {0, 2, 1, 4, 3, 8, 7, 6, 5};
+    return inv[d];
+}
+static const int kDirDm[9] = {0, 1, -1, 0, 0, 1, 1, -1, -1};
+static const int kDirDn[9] = {0, 0, 0, 1, -1, 1, -1, 1, -1};
+
+// Strip of a Rect inside a block array as (offset, count, stride): a 1-wide rect is a row
+// (stride 1) or a column (stride pitch).
+static void strip(const ocn_block &b, const Rect &r, long &off, int &count, long &stride)
+{
+    off = (long)(r.x0 - b.bnd_x1) + (long)(r.y0 - b.bnd_y1) * (long)b.pitch;
+    if (r.y0 == r.y1) { count = r.x1 - r.x0 + 1; stride = 1; }
+    else { count = r.y1 - r.y0 + 1; stride = (long)b.pitch; }
+}
+
+}  // namespace ocn
+
+using namespace ocn;
+
+// ------------------------------------------------------------------ context
+struct GBlock {            // one block of the global block grid
+    int bm, bn;
+    ocn_block g;           // pitch filled for local blocks only
+    int rank;              // -1 land block (bglob_proc = -1)
+    int k;                 // local index on its rank
+    double weight;         // sea points (bglob_weight)
+};
+
+struct LBlock {
+    ocn_block g;
+    int bm, bn, gid;
+    int nbr_rank[8], nbr_k[8], nbr_gid[8];
+    void *slab = nullptr;
+    std::array<void *, kNumSlots> ptr{};
+    template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
+};
+
+struct HaloPlan {
+    Seg *d_local = nullptr;           // intra-process copies
+    int n_local = 0;
+    // remote: per peer rank, pack segments (into send buffer) and unpack segments (from recv)
+    struct Peer { int rank; long count; double *send, *recv; };
+    std::vector<Peer> peers;
+    Seg *d_pack = nullptr, *d_unpack = nullptr;
+    int n_pack = 0, n_unpack = 0;
+};
+
+struct ocn_ctx {
+    ocn_basin basin;
+    ocn_sw_params sw;
+    ocn_decomp dec;
+    std::vector<int32_t> mask;         // global (nx, ny) column-major
+    int bnx = 1, bny = 1;
+    std::vector<GBlock> gblocks;       // (bm-1) + (bn-1)*bnx
+    std::vector<LBlock> blocks;
+    hipStream_t stream = nullptr;
+    int32_t *d_nbad = nullptr;
+    ncclComm_t comm = nullptr;
+    std::map<std::vector<int>, HaloPlan> plans;
+    bool initialized = false;
+    bool use_graph = false;
+    hipGraphExec_t graph_exec = nullptr;
+    double graph_tau = 0.0;
+    int graph_check = -1;
+    std::vector<void *> allocs;
+    // per-stage HIP-event timing (OCN_OPT_STAGE_TIMING): pending (stage, start, stop) records
+    bool stage_timing = false;
+    struct Rec { int stage; hipEvent_t a, b; };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> event_pool;
+    double stage_ms[OCN_NUM_STAGES] = {0};
+    int64_t stage_n[OCN_NUM_STAGES] = {0};
+};
+
+namespace ocn {
+
+// ------------------------------------------------------------------ decomposition
+// decomposition.f90:448-482: floor(real(remaining)/real(parts_left)) in default real(4)
+static std::vector<int> uniform_sizes(int total, int parts, std::string &err)
+{
+    std::vector<int> s;
+    int acc = 0;
+    for (int i = 1; i <= parts; ++i) {
+        int v = (i == parts) ? total - acc : (int)std::floor((float)(total - acc) / (float)(parts - i + 1));
+        if (v <= 0) { err = "Error in decomposition to uniform blocks: size <= 0"; return {}; }
+        s.push_back(v);
+        acc += v;
+    }
+    return s;
+}
+
+// MPI_Dims_create(n, 2): balanced, non-increasing factors (mpp.f90:89).
+static void dims_create(int n, int &d1, int &d2)
+{
+    d1 = n; d2 = 1;
+    for (int f = (int)std::floor(std::sqrt((double)n)); f >= 1; --f)
+        if (n % f == 0) { d1 = n / f; d2 = f; break; }
+}
+
+static int decompose(ocn_ctx *c)
+{
+    const int nx = c->basin.nx, ny = c->basin.ny;
+    std::string err;
+    auto xs = uniform_sizes(nx - 4, c->bnx, err);
+    auto ys = uniform_sizes(ny - 4, c->bny, err);
+    if (!err.empty()) return set_error(OCN_ERR_ARG, err);
+    int p1, p2;
+    dims_create(c->dec.nranks, p1, p2);
+    if (c->bnx % p1 || c->bny % p2)
+        return set_error(OCN_ERR_ARG, "mod(bnx, p_size(1)) or mod(bny, p_size(2)) not equal 0 (decomposition.f90:628)");
+    const int lbx = c->bnx / p1, lby = c->bny / p2;
+    c->gblocks.assign((size_t)c->bnx * c->bny, GBlock{});
+    int x0 = 0;
+    for (int bm = 1; bm <= c->bnx; ++bm) {
+        int y0 = 0;
+        for (int bn = 1; bn <= c->bny; ++bn) {
+            GBlock &g = c->gblocks[(size_t)(bm - 1) + (size_t)(bn - 1) * c->bnx];
+            g.bm = bm; g.bn = bn;
+            g.g.nx_start = 3 + x0; g.g.nx_end = g.g.nx_start + xs[bm - 1] - 1;
+            g.g.ny_start = 3 + y0; g.g.ny_end = g.g.ny_start + ys[bn - 1] - 1;
+            g.g.bnd_x1 = g.g.nx_start - 2; g.g.bnd_x2 = g.g.nx_end + 2;
+            g.g.bnd_y1 = g.g.ny_start - 2; g.g.bnd_y2 = g.g.ny_end + 2;
+            g.g.pitch = 0;
+            double w = 0.0;
+            for (int i = g.g.nx_start; i <= g.g.nx_end; ++i)
+                for (int j = g.g.ny_start; j <= g.g.ny_end; ++j)
+                    w += 1.0 - (double)c->mask[(size_t)(i - 1) + (size_t)(j - 1) * nx];
+            g.weight = w;
+            // create_uniform_decomposition: process coords (row-major cart), land blocks -> -1
+            const int c1 = (bm - 1) / lbx, c2 = (bn - 1) / lby;
+            g.rank = (w == 0.0) ? -1 : c1 * p2 + c2;
+            g.k = -1;
+            y0 += ys[bn - 1];
+        }
+        x0 += xs[bm - 1];
+    }
+    // local numbering per rank: _MPP_SORTED_BLOCKS_ = MINLOC over weight (column-major order)
+    std::vector<int> next(c->dec.nranks, 0);
+    std::vector<int> order(c->gblocks.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        return c->gblocks[a].weight < c->gblocks[b].weight;
+    });
+    for (int gid : order) {
+        GBlock &g = c->gblocks[gid];
+        if (g.rank >= 0) g.k = next[g.rank]++;
+    }
+    // local blocks of this rank, k order
+    std::vector<int> mine;
+    for (int gid : order)
+        if (c->gblocks[gid].rank == c->dec.rank) mine.push_back(gid);
+    c->blocks.clear();
+    for (int gid : mine) {
+        const GBlock &g = c->gblocks[gid];
+        LBlock lb;
+        lb.g = g.g;
+        lb.bm = g.bm; lb.bn = g.bn; lb.gid = gid;
+        const int w = g.g.bnd_x2 - g.g.bnd_x1 + 1;
+        lb.g.pitch = (int64_t)((w + 63) / 64 * 64);   // 512-B aligned rows for r8
+        for (int d = 1; d <= 8; ++d) {
+            const int m = g.bm + kDirDm[d], n = g.bn + kDirDn[d];
+            if (m < 1 || m > c->bnx || n < 1 || n > c->bny) {
+                lb.nbr_rank[d - 1] = -2; lb.nbr_k[d - 1] = -1; lb.nbr_gid[d - 1] = -1;
+            } else {
+                const int ng = (m - 1) + (n - 1) * c->bnx;
+                lb.nbr_rank[d - 1] = c->gblocks[ng].rank;
+                lb.nbr_k[d - 1] = c->gblocks[ng].k;
+                lb.nbr_gid[d - 1] = c->gblocks[ng].rank >= 0 ? ng : -1;
+            }
+        }
+        c->blocks.push_back(lb);
+    }
+    return OCN_OK;
+}
+
+// ------------------------------------------------------------------ storage
+static int allocate(ocn_ctx *c)
+{
+    for (LBlock &b : c->blocks) {
+        const long rows = b.g.bnd_y2 - b.g.bnd_y1 + 1;
+        const long n = (long)b.g.pitch * rows;
+        // every field padded to a 256-B multiple, based so that A(nx_start, :) rows are
+        // 256-B aligned: base offset shifted by (nx_start - bnd_x1) = 2 elements.
+        const long r8b = ((n * 8 + 16 + 255) / 256) * 256 + 256;
+        const long r4b = ((n * 4 + 8 + 255) / 256) * 256 + 256;
+        const size_t total = (size_t)OCN_NUM_R8 * r8b + (size_t)OCN_NUM_R4 * r4b + 256;
+        HIPCHK(hipMalloc(&b.slab, total));
+        c->allocs.push_back(b.slab);
+        HIPCHK(hipMemsetAsync(b.slab, 0, total, c->stream));
+        char *base = (char *)b.slab;
+        size_t off = 0;
+        for (int id = OCN_SSH; id < OCN_FIELD_END; ++id) {
+            b.ptr[field_slot(id)] = base + off + 256 - 16;
+            off += r8b;
+        }
+        for (int id = 0; id < OCN_NUM_R4; ++id) {
+            b.ptr[field_slot(id)] = base + off + 256 - 8;
+            off += r4b;
+        }
+    }
+    HIPCHK(hipMalloc(&c->d_nbad, 256));
+    c->allocs.push_back(c->d_nbad);
+    HIPCHK(hipMemsetAsync(c->d_nbad, 0, 256, c->stream));
+    return OCN_OK;
+}
+
+// ------------------------------------------------------------------ halo plans
+// syncborder_block2D_gen_all.fi: halo of block k in dir d <- boundary of neighbour in inverse(d).
+// Messages between two processes carry, for every (sending block, dir) pair in global block
+// order and every field of the sync group, the boundary strip in column-major order.
+static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan)
+{
+    std::vector<Seg> local;
+    std::map<int, std::vector<Seg>> pack, unpack;
+    std::map<int, long> send_count, recv_count;
+    // global index of local blocks
+    std::map<int, const LBlock *> by_gid;
+    for (const LBlock &b : c->blocks) by_gid[b.gid] = &b;
+
+    // receiving side: my halos in gid order, dirs 1..8
+    for (auto &kv : by_gid) {
+        const LBlock &b = *kv.second;
+        for (int d = 1; d <= 8; ++d) {
+            const int r = b.nbr_rank[d - 1];
+            if (r < 0) continue;
+            const GBlock &src = c->gblocks[b.nbr_gid[d - 1]];
+            const Rect hr = halo_points(b.g, d);
+            const Rect br = boundary_points(src.g, inverse_dir(d));
+            long hoff; int hcnt; long hstr;
+            strip(b.g, hr, hoff, hcnt, hstr);
+            for (int id : fields) {
+                double *dst = b.f<double>(id) + hoff;
+                if (r == c->dec.rank) {
+                    const LBlock &sb = *by_gid.at(b.nbr_gid[d - 1]);
+                    long soff; int scnt; long sstr;
+                    strip(sb.g, br, soff, scnt, sstr);
+                    local.push_back(Seg{sb.f<double>(id) + soff, dst, sstr, hstr, hcnt});
+                } else {
+                    // offset in the recv buffer from rank r is filled in below (relative index)
+                    unpack[r].push_back(Seg{(const double *)(intptr_t)recv_count[r], dst, 1, hstr, hcnt});
+                    recv_count[r] += hcnt;
+                }
+            }
+        }
+    }
+    // sending side: the remote receivers in gid order, dirs 1..8, where the source is mine.
+    // Enumerate receivers (any rank != mine) that have a neighbour block on my rank.
+    for (size_t gid = 0; gid < c->gblocks.size(); ++gid) {
+        const GBlock &rb = c->gblocks[gid];
+        if (rb.rank < 0 || rb.rank == c->dec.rank) continue;
+        for (int d = 1; d <= 8; ++d) {
+            const int m = rb.bm + kDirDm[d], n = rb.bn + kDirDn[d];
+            if (m < 1 || m > c->bnx || n < 1 || n > c->bny) continue;
+            const int sg = (m - 1) + (n - 1) * c->bnx;
+            if (c->gblocks[sg].rank != c->dec.rank) continue;
+            const LBlock &sb = *by_gid.at(sg);
+            const Rect br = boundary_points(sb.g, inverse_dir(d));
+            long soff; int scnt; long sstr;
+            strip(sb.g, br, soff, scnt, sstr);
+            for (int id : fields) {
+                pack[rb.rank].push_back(Seg{sb.f<double>(id) + soff, (double *)(intptr_t)send_count[rb.rank],
+                                            sstr, 1, scnt});
+                send_count[rb.rank] += scnt;
+            }
+        }
+    }
+    // allocate message buffers and resolve relative offsets
+    std::vector<Seg> all_pack, all_unpack;
+    for (auto &kv : recv_count) {
+        const int r = kv.first;
+        HaloPlan::Peer p{r, kv.second, nullptr, nullptr};
+        if (send_count[r] != kv.second)
+            return set_error(OCN_ERR_STATE, "halo plan: asymmetric message sizes");
+        HIPCHK(hipMalloc(&p.send, sizeof(double) * std::max(1L, p.count)));
+        HIPCHK(hipMalloc(&p.recv, sizeof(double) * std::max(1L, p.count)));
+        c->allocs.push_back(p.send); c->allocs.push_back(p.recv);
+        for (Seg s : pack[r]) { s.dst = p.send + (intptr_t)s.dst; all_pack.push_back(s); }
+        for (Seg s : unpack[r]) { s.src = p.recv + (intptr_t)s.src; all_unpack.push_back(s); }
+        plan.peers.push_back(p);
+    }
+    auto upload = [&](const std::vector<Seg> &v, Seg *&d, int &n) -> int {
+        n = (int)v.size();
+        if (!n) return OCN_OK;
+        HIPCHK(hipMalloc(&d, sizeof(Seg) * v.size()));
+        c->allocs.push_back(d);
+        HIPCHK(hipMemcpy(d, v.data(), sizeof(Seg) * v.size(), hipMemcpyHostToDevice));
+        return OCN_OK;
+    };
+    RC(upload(local, plan.d_local, plan.n_local));
+    RC(upload(all_pack, plan.d_pack, plan.n_pack));
+    RC(upload(all_unpack, plan.d_unpack, plan.n_unpack));
+    return OCN_OK;
+}
+
+static int get_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan *&out)
+{
+    auto it = c->plans.find(fields);
+    if (it == c->plans.end()) {
+        HaloPlan p;
+        RC(build_plan(c, fields, p));
+        it = c->plans.emplace(fields, p).first;
+    }
+    out = &it->second;
+    return OCN_OK;
+}
+
+static int nccl_rc(ncclResult_t r, const char *what)
+{
+    if (r == ncclSuccess) return OCN_OK;
+    return set_error(OCN_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+static int run_sync(ocn_ctx *c, const std::vector<int> &fields)
+{
+    HaloPlan *p;
+    RC(get_plan(c, fields, p));
+    if (!p->peers.empty()) {
+        if (!c->comm) return set_error(OCN_ERR_COMM, "remote neighbours but no RCCL communicator attached");
+        hipLaunchKernelGGL(k_segments, dim3(p->n_pack), dim3(256), 0, c->stream, p->d_pack, p->n_pack);
+        RC(check_launch());
+        RC(nccl_rc(ncclGroupStart(), "ncclGroupStart"));
+        for (auto &peer : p->peers) {
+            RC(nccl_rc(ncclRecv(peer.recv, (size_t)peer.count, ncclDouble, peer.rank, c->comm, c->stream), "ncclRecv"));
+            RC(nccl_rc(ncclSend(peer.send, (size_t)peer.count, ncclDouble, peer.rank, c->comm, c->stream), "ncclSend"));
+        }
+        RC(nccl_rc(ncclGroupEnd(), "ncclGroupEnd"));
+    }
+    if (p->n_local) {
+        hipLaunchKernelGGL(k_segments, dim3(p->n_local), dim3(256), 0, c->stream, p->d_local, p->n_local);
+        RC(check_launch());
+    }
+    if (p->n_unpack) {
+        hipLaunchKernelGGL(k_segments, dim3(p->n_unpack), dim3(256), 0, c->stream, p->d_unpack, p->n_unpack);
+        RC(check_launch());
+    }
+    return OCN_OK;
+}
+
+// ------------------------------------------------------------------ stages (envoke)
+// sync lists: interface/shallow_water/sw_interface.f90 envoke_*_sync
+static const std::vector<int> kSyncSsh = {OCN_SSHN};
+static const std::vector<int> kSyncHhUpdate = {OCN_HHU_N, OCN_HHV_N, OCN_HHH_N};
+static const std::vector<int> kSyncVort = {OCN_VORT};
+static const std::vector<int> kSyncUvTrans = {OCN_HHU_P, OCN_HHV_P, OCN_HHH_P};
+static const std::vector<int> kSyncStress = {OCN_STR_T, OCN_STR_S};
+static const std::vector<int> kSyncUv = {OCN_VBRTRN, OCN_UBRTRN};
+static const std::vector<int> kSyncHhInit = {OCN_HHU, OCN_HHV, OCN_HHH};
+
+static int stage_kernel(ocn_ctx *c, const LBlock &b, int stage, double tau)
+{
+    const ocn_block *g = &b.g;
+    void *s = c->stream;
+#define R4(id) b.f<const float>(id)
+#define R8(id) b.f<double>(id)
+    switch (stage) {
+    case OCN_STAGE_SW_UPDATE_SSH:
+        return ocn_sw_update_ssh(g, tau, R4(OCN_LU), R4(OCN_DX), R4(OCN_DY), R4(OCN_DXH), R4(OCN_DYH),
+                                 R8(OCN_HHU), R8(OCN_HHV), R8(OCN_SSHN), R8(OCN_SSHP), R8(OCN_UBRTR),
+                                 R8(OCN_VBRTR), s);
+    case OCN_STAGE_HH_UPDATE:
+        return ocn_hh_update(g, R4(OCN_LU), R4(OCN_LLU), R4(OCN_LLV), R4(OCN_LUH), R4(OCN_DX), R4(OCN_DY),
+                             R4(OCN_DXT), R4(OCN_DYT), R4(OCN_DXH), R4(OCN_DYH), R4(OCN_DXB), R4(OCN_DYB),
+                             R8(OCN_HHQ_N), R8(OCN_HHU_N), R8(OCN_HHV_N), R8(OCN_HHH_N), R8(OCN_SSH),
+                             R8(OCN_HHQ_REST), s);
+    case OCN_STAGE_UV_TRANS_VORT:
+        return ocn_uv_trans_vort(g, R4(OCN_LUU), R4(OCN_DXT), R4(OCN_DYT), R4(OCN_DXB), R4(OCN_DYB),
+                                 R8(OCN_UBRTR), R8(OCN_VBRTR), R8(OCN_VORT), s);
+    case OCN_STAGE_UV_TRANS:
+        return ocn_uv_trans(g, R4(OCN_LCU), R4(OCN_LCV), R4(OCN_LUU), R4(OCN_DXH), R4(OCN_DYH), R8(OCN_UBRTR),
+                            R8(OCN_VBRTR), R8(OCN_VORT), R8(OCN_HHQ), R8(OCN_HHU), R8(OCN_HHV), R8(OCN_HHH),
+                            R8(OCN_RHSX_ADV), R8(OCN_RHSY_ADV), s);
+    case OCN_STAGE_STRESS_COMPONENTS:
+        return ocn_stress_components(g, R4(OCN_LU), R4(OCN_LUU), R4(OCN_DX), R4(OCN_DY), R4(OCN_DXT),
+                                     R4(OCN_DYT), R4(OCN_DXH), R4(OCN_DYH), R4(OCN_DXB), R4(OCN_DYB),
+                                     R8(OCN_UBRTRP), R8(OCN_VBRTRP), R8(OCN_STR_T), R8(OCN_STR_S), s);
+    case OCN_STAGE_UV_DIFF2:
+        return ocn_uv_diff2(g, R4(OCN_LCU), R4(OCN_LCV), R4(OCN_DX), R4(OCN_DY), R4(OCN_DXT), R4(OCN_DYT),
+                            R4(OCN_DXH), R4(OCN_DYH), R4(OCN_DXB), R4(OCN_DYB), R8(OCN_MU), R8(OCN_STR_T),
+                            R8(OCN_STR_S), R8(OCN_HHQ), R8(OCN_HHU), R8(OCN_HHV), R8(OCN_HHH), R8(OCN_RHSX_DIF),
+                            R8(OCN_RHSY_DIF), s);
+    case OCN_STAGE_SW_UPDATE_UV:
+        return ocn_sw_update_uv(g, tau, R4(OCN_LCU), R4(OCN_LCV), R4(OCN_DXT), R4(OCN_DYT), R4(OCN_DXH),
+                                R4(OCN_DYH), R4(OCN_DXB), R4(OCN_DYB), R8(OCN_HHU), R8(OCN_HHU_N), R8(OCN_HHU_P),
+                                R8(OCN_HHV), R8(OCN_HHV_N), R8(OCN_HHV_P), R8(OCN_HHH), R8(OCN_SSH),
+                                R8(OCN_UBRTR), R8(OCN_UBRTRN), R8(OCN_UBRTRP), R8(OCN_VBRTR), R8(OCN_VBRTRN),
+                                R8(OCN_VBRTRP), R4(OCN_R_DISS), R4(OCN_RLH_S), R8(OCN_RHSX), R8(OCN_RHSY),
+                                R8(OCN_RHSX_ADV), R8(OCN_RHSY_ADV), R8(OCN_RHSX_DIF), R8(OCN_RHSY_DIF), s);
+    case OCN_STAGE_SW_NEXT_STEP:
+        return ocn_sw_next_step(g, c->sw.time_smooth, R4(OCN_LU), R4(OCN_LCU), R4(OCN_LCV), R8(OCN_SSH),
+                                R8(OCN_SSHN), R8(OCN_SSHP), R8(OCN_UBRTR), R8(OCN_UBRTRN), R8(OCN_UBRTRP),
+                                R8(OCN_VBRTR), R8(OCN_VBRTRN), R8(OCN_VBRTRP), s);
+    case OCN_STAGE_HH_SHIFT:
+        return ocn_hh_shift(g, c->sw.time_smooth, R4(OCN_LU), R4(OCN_LLU), R4(OCN_LLV), R4(OCN_LUH),
+                            R8(OCN_HHQ), R8(OCN_HHQ_P), R8(OCN_HHQ_N), R8(OCN_HHU), R8(OCN_HHU_P), R8(OCN_HHU_N),
+                            R8(OCN_HHV), R8(OCN_HHV_P), R8(OCN_HHV_N), R8(OCN_HHH), R8(OCN_HHH_P), R8(OCN_HHH_N), s);
+    case OCN_STAGE_HH_INIT:
+        return ocn_hh_init(g, c->sw.full_free_surface, R4(OCN_LU), R4(OCN_LLU), R4(OCN_LLV), R4(OCN_LUH),
+                           R4(OCN_DX), R4(OCN_DY), R4(OCN_DXT), R4(OCN_DYT), R4(OCN_DXH), R4(OCN_DYH), R4(OCN_DXB),
+                           R4(OCN_DYB), R8(OCN_HHQ), R8(OCN_HHQ_P), R8(OCN_HHQ_N), R8(OCN_HHU), R8(OCN_HHU_P),
+                           R8(OCN_HHU_N), R8(OCN_HHV), R8(OCN_HHV_P), R8(OCN_HHV_N), R8(OCN_HHH), R8(OCN_HHH_P),
+                           R8(OCN_HHH_N), R8(OCN_SSH), R8(OCN_SSHP), R8(OCN_HHQ_REST), s);
+    case OCN_STAGE_CHECK_SSH_ERR:
+        return ocn_check_ssh_err(g, R4(OCN_LU), R8(OCN_SSH), c->d_nbad, s);
+    default:
+        return set_error(OCN_ERR_ARG, "unknown stage id");
+    }
+#undef R4
+#undef R8
+}
+
+static const std::vector<int> *stage_sync(int stage)
+{
+    switch (stage) {
+    case OCN_STAGE_SW_UPDATE_SSH: return &kSyncSsh;
+    case OCN_STAGE_HH_UPDATE: return &kSyncHhUpdate;
+    case OCN_STAGE_UV_TRANS_VORT: return &kSyncVort;
+    case OCN_STAGE_UV_TRANS: return &kSyncUvTrans;
+    case OCN_STAGE_STRESS_COMPONENTS: return &kSyncStress;
+    case OCN_STAGE_SW_UPDATE_UV: return &kSyncUv;
+    case OCN_STAGE_HH_INIT: return &kSyncHhInit;
+    default: return nullptr;   // uv_diff2, sw_next_step, hh_shift, check: empty sync
+    }
+}
+
+// every plan a step can use, built before any graph capture (no hipMalloc while capturing)
+static int prebuild_plans(ocn_ctx *c)
+{
+    HaloPlan *p;
+    for (const std::vector<int> *l : {&kSyncSsh, &kSyncHhUpdate, &kSyncVort, &kSyncUvTrans, &kSyncStress, &kSyncUv,
+                                      &kSyncHhInit})
+        RC(get_plan(c, *l, p));
+    return OCN_OK;
+}
+
+static int get_event(ocn_ctx *c, hipEvent_t &e)
+{
+    if (!c->event_pool.empty()) { e = c->event_pool.back(); c->event_pool.pop_back(); return OCN_OK; }
+    HIPCHK(hipEventCreate(&e));
+    return OCN_OK;
+}
+
+static int envoke(ocn_ctx *c, int stage, double tau)
+{
+    ocn_ctx::Rec rec{stage, nullptr, nullptr};
+    if (c->stage_timing) {
+        RC(get_event(c, rec.a)); RC(get_event(c, rec.b));
+        HIPCHK(hipEventRecord(rec.a, c->stream));
+    }
+    for (const LBlock &b : c->blocks) RC(stage_kernel(c, b, stage, tau));
+    if (c->stage_timing) {
+        HIPCHK(hipEventRecord(rec.b, c->stream));
+        c->recs.push_back(rec);
+    }
+    const std::vector<int> *sl = stage_sync(stage);
+    if (sl) RC(run_sync(c, *sl));
+    return OCN_OK;
+}
+
+// expl_shallow_water (shallow_water.f90:22-94) with the flag gates
+static int one_step(ocn_ctx *c, double tau, bool check)
+{
+    const ocn_sw_params &sw = c->sw;
+    RC(envoke(c, OCN_STAGE_SW_UPDATE_SSH, tau));
+    if (sw.full_free_surface > 0) RC(envoke(c, OCN_STAGE_HH_UPDATE, tau));
+    if (sw.trans_terms > 0) {
+        RC(envoke(c, OCN_STAGE_UV_TRANS_VORT, tau));
+        RC(envoke(c, OCN_STAGE_UV_TRANS, tau));
+    }
+    if (sw.ksw_lat > 0) {
+        RC(envoke(c, OCN_STAGE_STRESS_COMPONENTS, tau));
+        RC(envoke(c, OCN_STAGE_UV_DIFF2, tau));
+    }
+    RC(envoke(c, OCN_STAGE_SW_UPDATE_UV, tau));
+    RC(envoke(c, OCN_STAGE_SW_NEXT_STEP, tau));
+    if (sw.full_free_surface > 0) {
+        RC(envoke(c, OCN_STAGE_HH_SHIFT, tau));
+        RC(envoke(c, OCN_STAGE_HH_INIT, tau));
+    }
+    if (check) RC(envoke(c, OCN_STAGE_CHECK_SSH_ERR, tau));
+    return OCN_OK;
+}
+
+// ------------------------------------------------------------------ host-side initial state
+static const float kPi = 3.1415926f;              // constants.f90:14
+static const double kDPi = 3.14159265358979;      // constants.f90:17
+static const double kLatExtr = 89.99999;          // constants.f90:20
+static const float kRadEarth = 6371000.0f;        // constants.f90:22
+static const float kEarthAngVel = 7.2921159e-5f;  // constants.f90:22
+static double dsind(double x) { return std::sin((x / 180.0) * kDPi); }   // core/math_tools.f90
+static double dcosd(double x) { return std::cos((x / 180.0) * kDPi); }
+
+struct HostBlock {
+    const ocn_block &g;
+    long ld;
+    std::vector<std::vector<float>> r4;
+    explicit HostBlock(const ocn_block &b) : g(b), ld(b.bnd_x2 - b.bnd_x1 + 1)
+    {
+        r4.assign(OCN_NUM_R4, std::vector<float>((size_t)ld * (b.bnd_y2 - b.bnd_y1 + 1), 0.0f));
+    }
+    long I(int m, int n) const { return (long)(m - g.bnd_x1) + (long)(n - g.bnd_y1) * ld; }
+    float &a(int id, int m, int n) { return r4[id][I(m, n)]; }
+};
+
+// grid_kernels.f90:18-92 (lu_init, lu_lv_init), :94-202 (grid_base_init, uniform steps),
+// grid_geo_init_kernel + grid_parameters.f90 (carthesian / spherical metric scaling, Coriolis)
+static void host_grid(const ocn_ctx *c, HostBlock &h)
+{
+    const ocn_block &g = h.g;
+    const int nx = c->basin.nx;
+    for (int n = g.bnd_y1; n <= g.bnd_y2; ++n)
+        for (int m = g.bnd_x1; m <= g.bnd_x2; ++m)
+            if (c->mask[(size_t)(m - 1) + (size_t)(n - 1) * nx] == 0) h.a(OCN_LU, m, n) = 1.0f;
+    for (int n = g.bnd_y1; n <= g.bnd_y2 - 1; ++n)
+        for (int m = g.bnd_x1; m <= g.bnd_x2 - 1; ++m) {
+            const float a = h.a(OCN_LU, m, n), b = h.a(OCN_LU, m + 1, n), cc = h.a(OCN_LU, m, n + 1),
+                        d = h.a(OCN_LU, m + 1, n + 1);
+            if (a + b + cc + d > 0.5f) h.a(OCN_LUH, m, n) = 1.0f;
+            if (a * b * cc * d > 0.5f) h.a(OCN_LUU, m, n) = 1.0f;
+            if (a + b > 0.5f) h.a(OCN_LLU, m, n) = 1.0f;
+            if (a + cc > 0.5f) h.a(OCN_LLV, m, n) = 1.0f;
+            if (a * b > 0.5f) h.a(OCN_LCU, m, n) = 1.0f;
+            if (a * cc > 0.5f) h.a(OCN_LCV, m, n) = 1.0f;
+        }
+    const ocn_basin &bs = c->basin;
+    const int mmm = 3, nnn = 3;
+    std::vector<double> xt(h.ld), xu(h.ld), yt(g.bnd_y2 - g.bnd_y1 + 1), yv(g.bnd_y2 - g.bnd_y1 + 1);
+    for (int m = g.bnd_x1; m <= g.bnd_x2; ++m) xt[m - g.bnd_x1] = bs.rlon + (double)(m - mmm) * bs.dxst;
+    for (int n = g.bnd_y1; n <= g.bnd_y2; ++n) yt[n - g.bnd_y1] = bs.rlat + (double)(n - nnn) * bs.dyst;
+    for (int m = g.bnd_x1; m <= g.bnd_x2 - 1; ++m) xu[m - g.bnd_x1] = (xt[m - g.bnd_x1] + xt[m + 1 - g.bnd_x1]) / 2.0;
+    for (int n = g.bnd_y1; n <= g.bnd_y2 - 1; ++n) yv[n - g.bnd_y1] = (yt[n - g.bnd_y1] + yt[n + 1 - g.bnd_y1]) / 2.0;
+    const float pip180 = kPi / 180.0f;
+    const float sx = (float)bs.dxst * pip180 * kRadEarth;
+    const float sy = (float)bs.dyst * pip180 * kRadEarth;
+    for (int n = g.ny_start - 1; n <= g.ny_end + 1; ++n)
+        for (int m = g.nx_start - 1; m <= g.nx_end + 1; ++m) {
+            for (int id : {OCN_DXT, OCN_DXB, OCN_DX, OCN_DXH}) h.a(id, m, n) = sx;
+            for (int id : {OCN_DYT, OCN_DYB, OCN_DY, OCN_DYH}) h.a(id, m, n) = sy;
+        }
+    std::vector<float> rlh_c(h.r4[OCN_RLH_S].size(), -2.0f * kEarthAngVel);
+    std::fill(h.r4[OCN_RLH_S].begin(), h.r4[OCN_RLH_S].end(), 2.0f * kEarthAngVel);
+    struct Pass { const std::vector<double> *x, *y; int mx, my; bool cor; };
+    const Pass passes[4] = {{&xt, &yt, OCN_DX, OCN_DY, false}, {&xu, &yt, OCN_DXT, OCN_DYH, false},
+                            {&xt, &yv, OCN_DXH, OCN_DYT, false}, {&xu, &yv, OCN_DXB, OCN_DYB, true}};
+    const double sinlat_extr = dsind(kLatExtr);
+    for (const Pass &p : passes)
+        for (int n = g.ny_start - 1; n <= g.ny_end + 1; ++n) {
+            const double y = (*p.y)[n - g.bnd_y1];
+            for (int m = g.nx_start - 1; m <= g.nx_end + 1; ++m) {
+                float &mx = h.a(p.mx, m, n), &my = h.a(p.my, m, n);
+                float &cs = h.a(OCN_RLH_S, m, n);
+                float &cc = rlh_c[h.I(m, n)];
+                if (bs.curve_grid == 0) {
+                    mx = mx * 1.0f; my = my * 1.0f;
+                    if (p.cor) { cs = cs / std::sqrt(2.0f); cc = cc / std::sqrt(2.0f); }
+                } else {
+                    const double lat_mod = std::max(std::min(y, kLatExtr), -kLatExtr);
+                    const double x = (*p.x)[m - g.bnd_x1];
+                    double sin_lat = dsind(y) * dcosd(bs.rotation_on_lat) + dcosd(x) * dcosd(y) * dsind(bs.rotation_on_lat);
+                    sin_lat = std::min(std::max(sin_lat, -sinlat_extr), sinlat_extr);
+                    const double cos_lat = std::sqrt(1.0 - sin_lat * sin_lat);
+                    mx = mx * (float)dcosd(lat_mod);
+                    my = my * 1.0f;
+                    if (p.cor) { cs = cs * (float)sin_lat; cc = cc * (float)cos_lat; }
+                }
+            }
+        }
+}
+
+// vel_ssh.f90:15-38 gaussian_elimination_kernel with sigma = 1, (nx0, ny0) = (nx/2, ny/2)
+static void host_gaussian(const ocn_ctx *c, HostBlock &h, std::vector<double> &ssh)
+{
+    const ocn_block &g = h.g;
+    const int nx0 = c->basin.nx / 2, ny0 = c->basin.ny / 2;
+    const double sigma = 1.0;
+    for (int n = g.ny_start; n <= g.ny_end; ++n)
+        for (int m = g.nx_start; m <= g.nx_end; ++m)
+            if (h.a(OCN_LU, m, n) > 0.5f) {
+                const double dx = (double)(m - nx0) / ((double)nx0 * 0.25);
+                const double dy = (double)(n - ny0) / ((double)ny0 * 0.25);
+                ssh[h.I(m, n)] = (1.0 / (std::sqrt(2.0 * kDPi) * sigma)) *
+                                 std::exp(-((dx * dx + dy * dy) / (2.0 * sigma * sigma)));
+            }
+}
+
+static int upload_field(ocn_ctx *c, const LBlock &b, int id, const void *host, bool async)
+{
+    const size_t es = is_r8(id) ? 8 : 4;
+    const size_t w = (size_t)(b.g.bnd_x2 - b.g.bnd_x1 + 1), rows = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1);
+    if (async)
+        HIPCHK(hipMemcpy2DAsync(b.ptr[field_slot(id)], (size_t)b.g.pitch * es, host, w * es, w * es, rows,
+                                hipMemcpyHostToDevice, c->stream));
+    else
+        HIPCHK(hipMemcpy2D(b.ptr[field_slot(id)], (size_t)b.g.pitch * es, host, w * es, w * es, rows,
+                           hipMemcpyHostToDevice));
+    return OCN_OK;
+}
+
+static int init_state(ocn_ctx *c)
+{
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (const LBlock &b : c->blocks) {
+        HostBlock h(b.g);
+        host_grid(c, h);
+        for (int id = 0; id < OCN_NUM_R4; ++id) RC(upload_field(c, b, id, h.r4[id].data(), false));
+        std::vector<double> r8(h.r4[0].size(), 100.0);      // init_data.f90:112-114 hhq_rest = 100 m
+        RC(upload_field(c, b, OCN_HHQ_REST, r8.data(), false));
+        std::fill(r8.begin(), r8.end(), 0.0);
+        host_gaussian(c, h, r8);
+        RC(upload_field(c, b, OCN_SSH, r8.data(), false));
+    }
+    RC(run_sync(c, {OCN_SSH}));                               // envoke_gaussian_elimination's sync
+    for (const LBlock &b : c->blocks) {                       // sshn = ssh, sshp = ssh (whole arrays)
+        const size_t bytes = (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1) * 8;
+        HIPCHK(hipMemcpyAsync(b.ptr[field_slot(OCN_SSHN)], b.ptr[field_slot(OCN_SSH)], bytes,
+                              hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(b.ptr[field_slot(OCN_SSHP)], b.ptr[field_slot(OCN_SSH)], bytes,
+                              hipMemcpyDeviceToDevice, c->stream));
+    }
+    RC(envoke(c, OCN_STAGE_HH_INIT, 0.0));                    // init_data.f90:60-63
+    for (const LBlock &b : c->blocks) {                       // u = v = 0, mu = lvisc_2 then 0 (:67-77)
+        const long n = (long)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1);
+        for (int id : {OCN_UBRTR, OCN_UBRTRN, OCN_UBRTRP, OCN_VBRTR, OCN_VBRTRN, OCN_VBRTRP, OCN_MU}) {
+            hipLaunchKernelGGL(k_fill_r8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
+                               b.f<double>(id), n, 0.0);
+            RC(check_launch());
+        }
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->initialized = true;
+    return OCN_OK;
+}
+
+}  // namespace ocn
+
+// ================================================================== C ABI (PSy layer)
+extern "C" {
+
+const char *ocn_last_error(void) { return g_last_error.c_str(); }
+int ocn_abi_version(void) { return OCN_ABI_VERSION; }
+
+int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_decomp *dec, const int32_t *mask,
+                   ocn_ctx **out)
+{
+    if (!basin || !sw || !dec || !out) return set_error(OCN_ERR_ARG, "null argument");
+    if (basin->nx < 5 || basin->ny < 5) return set_error(OCN_ERR_ARG, "nx, ny must be >= 5");
+    if (dec->bnx < 1 || dec->bny < 1 || dec->nranks < 1 || dec->rank < 0 || dec->rank >= dec->nranks)
+        return set_error(OCN_ERR_ARG, "bad decomposition request");
+    ocn_ctx *c = new ocn_ctx();
+    c->basin = *basin; c->sw = *sw; c->dec = *dec;
+    c->bnx = dec->bnx; c->bny = dec->bny;
+    const size_t nxy = (size_t)basin->nx * basin->ny;
+    c->mask.assign(nxy, 0);
+    if (mask) {
+        std::memcpy(c->mask.data(), mask, nxy * sizeof(int32_t));
+    } else {   // tools/io.f90:49-59: closed box with a 2-cell land frame
+        for (int n = 1; n <= basin->ny; ++n)
+            for (int m = 1; m <= basin->nx; ++m)
+                c->mask[(size_t)(m - 1) + (size_t)(n - 1) * basin->nx] =
+                    (m < 3 || m > basin->nx - 2 || n < 3 || n > basin->ny - 2) ? 1 : 0;
+    }
+    int rc = check_hip(hipSetDevice(dec->device), "hipSetDevice");
+    if (!rc) rc = check_hip(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!rc) rc = decompose(c);
+    if (!rc) rc = allocate(c);
+    if (!rc) rc = prebuild_plans(c);
+    if (!rc) rc = check_hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    if (rc) { ocn_ctx_destroy(c); return rc; }
+    *out = c;
+    return OCN_OK;
+}
+
+int ocn_ctx_destroy(ocn_ctx *c)
+{
+    if (!c) return OCN_OK;
+    (void)hipSetDevice(c->dec.device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    for (auto &r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->comm) ncclCommDestroy(c->comm);
+    for (void *p : c->allocs) (void)hipFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return OCN_OK;
+}
+
+int ocn_ctx_block_count(const ocn_ctx *c) { return c ? (int)c->blocks.size() : -1; }
+
+int ocn_ctx_block_info(const ocn_ctx *c, int k, ocn_block_info *out)
+{
+    if (!c || !out || k < 0 || k >= (int)c->blocks.size()) return set_error(OCN_ERR_ARG, "bad block index");
+    const LBlock &b = c->blocks[k];
+    out->geom = b.g;
+    out->bm = b.bm; out->bn = b.bn;
+    for (int d = 0; d < 8; ++d) { out->nbr_rank[d] = b.nbr_rank[d]; out->nbr_k[d] = b.nbr_k[d]; }
+    return OCN_OK;
+}
+
+void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
+{
+    if (!c || k < 0 || k >= (int)c->blocks.size() || !(is_r4(id) || is_r8(id))) {
+        set_error(OCN_ERR_ARG, "bad block index or field id");
+        return nullptr;
+    }
+    return c->blocks[k].ptr[field_slot(id)];
+}
+
+void *ocn_ctx_stream(const ocn_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int ocn_comm_unique_id(void *out_id, int32_t nbytes)
+{
+    if (!out_id || nbytes < (int32_t)sizeof(ncclUniqueId)) return set_error(OCN_ERR_ARG, "buffer < 128 bytes");
+    ncclUniqueId id;
+    RC(nccl_rc(ncclGetUniqueId(&id), "ncclGetUniqueId"));
+    std::memcpy(out_id, &id, sizeof(id));
+    return OCN_OK;
+}
+
+int ocn_ctx_attach_comm(ocn_ctx *c, const void *unique_id, int32_t nbytes)
+{
+    if (!c || !unique_id || nbytes < (int32_t)sizeof(ncclUniqueId)) return set_error(OCN_ERR_ARG, "bad unique id");
+    HIPCHK(hipSetDevice(c->dec.device));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    RC(nccl_rc(ncclCommInitRank(&c->comm, c->dec.nranks, id, c->dec.rank), "ncclCommInitRank"));
+    return OCN_OK;
+}
+
+int ocn_ctx_init_state(ocn_ctx *c)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->dec.device));
+    return init_state(c);
+}
+
+int ocn_ctx_sync(ocn_ctx *c, int field_id)
+{
+    if (!c || !is_r8(field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
+    return run_sync(c, {field_id});
+}
+
+int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    if (stage_id < 0 || stage_id >= OCN_NUM_STAGES) return set_error(OCN_ERR_ARG, "bad stage id");
+    return envoke(c, stage_id, tau);
+}
+
+static int capture_step(ocn_ctx *c, double tau, bool check)
+{
+    hipGraph_t graph;
+    HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    int rc = one_step(c, tau, check);
+    hipError_t e = hipStreamEndCapture(c->stream, &graph);
+    if (rc) return rc;
+    HIPCHK(e);
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    e = hipGraphInstantiate(&c->graph_exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    HIPCHK(e);
+    c->graph_tau = tau;
+    c->graph_check = check;
+    return OCN_OK;
+}
+
+int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
+    for (int s = 1; s <= nsteps; ++s) {
+        const bool check = check_every > 0 && (s % check_every == 0);
+        const bool graph_ok = c->use_graph && !c->comm && !c->stage_timing;   // RCCL / events stay outside graphs
+        if (graph_ok) {
+            if (!c->graph_exec || c->graph_tau != tau || c->graph_check != (int)check) RC(capture_step(c, tau, check));
+            HIPCHK(hipGraphLaunch(c->graph_exec, c->stream));
+        } else {
+            RC(one_step(c, tau, check));
+        }
+    }
+    return OCN_OK;
+}
+
+int ocn_ctx_synchronize(ocn_ctx *c)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int32_t nbad = 0;
+    HIPCHK(hipMemcpy(&nbad, c->d_nbad, sizeof(nbad), hipMemcpyDeviceToHost));
+    if (nbad) return set_error(OCN_ERR_BLOWUP, "SIGFPRE predict error: |ssh| >= 1e4 on " + std::to_string(nbad) +
+                                                   " sea points (check_ssh_err_kernel)");
+    return OCN_OK;
+}
+
+int ocn_ctx_stage_times(ocn_ctx *c, double *ms, int64_t *counts)
+{
+    if (!c || !ms || !counts) return set_error(OCN_ERR_ARG, "null argument");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (auto &r : c->recs) {
+        float t = 0.f;
+        HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
+        c->stage_ms[r.stage] += t;
+        c->stage_n[r.stage] += 1;
+        c->event_pool.push_back(r.a); c->event_pool.push_back(r.b);
+    }
+    c->recs.clear();
+    for (int i = 0; i < OCN_NUM_STAGES; ++i) { ms[i] = c->stage_ms[i]; counts[i] = c->stage_n[i]; }
+    for (int i = 0; i < OCN_NUM_STAGES; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
+    return OCN_OK;
+}
+
+int ocn_ctx_download(ocn_ctx *c, int k, int id, void *host)
+{
+    if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !(is_r4(id) || is_r8(id)))
+        return set_error(OCN_ERR_ARG, "download: bad argument");
+    const LBlock &b = c->blocks[k];
+    const size_t es = is_r8(id) ? 8 : 4;
+    const size_t w = (size_t)(b.g.bnd_x2 - b.g.bnd_x1 + 1), rows = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy2D(host, w * es, b.ptr[field_slot(id)], (size_t)b.g.pitch * es, w * es, rows,
+                       hipMemcpyDeviceToHost));
+    return OCN_OK;
+}
+
+int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
+{
+    if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !(is_r4(id) || is_r8(id)))
+        return set_error(OCN_ERR_ARG, "upload: bad argument");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return upload_field(c, c->blocks[k], id, host, false);
+}
+
+int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    switch (key) {
+    case OCN_OPT_GRAPH: c->use_graph = value != 0; return OCN_OK;
+    case OCN_OPT_STAGE_TIMING: c->stage_timing = value != 0; return OCN_OK;
+    default: return set_error(OCN_ERR_ARG, "unknown option");
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+"""OceanModel: host handle on one process's share of the domain (libocn_sw context).
+
+Mirrors the reference's global model state -- ``domain_data`` (core/decomposition.f90),
+``ocean_data`` (core/ocean.f90) and ``grid_data`` (core/grid.f90) -- for the blocks this
+process owns.  Device storage lives in the C++ context; this class only holds the handle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import FIELD_ID, R8_NAMES, STAGE_ID, check, lib
+from .config import BasinConfig, ParallelConfig, SWConfig
+
+
+@dataclass
+class BlockInfo:
+    """domain_type's view of local block k (decomposition.f90:40-81, blocks_info :17-32)."""
+    k: int
+    bm: int
+    bn: int
+    nx_start: int
+    nx_end: int
+    ny_start: int
+    ny_end: int
+    bnd_x1: int
+    bnd_x2: int
+    bnd_y1: int
+    bnd_y2: int
+    pitch: int
+    nbr_rank: tuple
+    nbr_k: tuple
+
+    @property
+    def shape(self):
+        return (self.bnd_x2 - self.bnd_x1 + 1, self.bnd_y2 - self.bnd_y1 + 1)
+
+    @property
+    def cells(self) -> int:
+        return (self.nx_end - self.nx_start + 1) * (self.ny_end - self.ny_start + 1)
+
+    def c_block(self) -> _lib.OcnBlock:
+        return _lib.OcnBlock(self.nx_start, self.nx_end, self.ny_start, self.ny_end,
+                             self.bnd_x1, self.bnd_x2, self.bnd_y1, self.bnd_y2, self.pitch)
+
+
+class OceanModel:
+    """One process's blocks on one GPU.
+
+    ``OceanModel(basin, sw, par, rank=0, nranks=1, device=0)`` decomposes the basin exactly as
+    the reference does (uniform blocks, land blocks dropped, blocks dealt to processes), allocates
+    every field on the device, and ``init()`` builds the reference's initial state
+    (control/init_data.f90).  ``step(n)`` runs expl_shallow_water n times on the device.
+    """
+
+    def __init__(self, basin: BasinConfig, sw: SWConfig = SWConfig(), par: ParallelConfig = ParallelConfig(),
+                 rank: int = 0, nranks: int = 1, device: int = 0):
+        L = lib()
+        self.basin, self.sw, self.par = basin, sw, par
+        self.rank, self.nranks, self.device = rank, nranks, device
+        cb = _lib.OcnBasin(basin.nx, basin.ny, basin.dxst, basin.dyst, basin.rlon, basin.rlat, basin.curve_grid,
+                           basin.rotation_on_lon, basin.rotation_on_lat)
+        cs = _lib.OcnSwParams(sw.full_free_surface, sw.trans_terms, sw.ksw_lat, sw.time_smooth, sw.lvisc_2)
+        cd = _lib.OcnDecomp(par.bppnx, par.bppny, nranks, rank, device)
+        self._mask = None
+        mptr = None
+        if basin.mask is not None:
+            self._mask = np.asfortranarray(basin.mask.astype(np.int32))
+            if self._mask.shape != (basin.nx, basin.ny):
+                raise ValueError(f"mask shape {self._mask.shape} != (nx, ny) = {(basin.nx, basin.ny)}")
+            mptr = self._mask.ctypes.data_as(C.c_void_p)
+        h = C.c_void_p()
+        check(L.ocn_ctx_create(C.byref(cb), C.byref(cs), C.byref(cd), mptr, C.byref(h)), "ocn_ctx_create")
+        self.ctx = h
+        self.blocks: list[BlockInfo] = []
+        for k in range(L.ocn_ctx_block_count(self.ctx)):
+            bi = _lib.OcnBlockInfo()
+            check(L.ocn_ctx_block_info(self.ctx, k, C.byref(bi)), "ocn_ctx_block_info")
+            g = bi.geom
+            self.blocks.append(BlockInfo(k, bi.bm, bi.bn, g.nx_start, g.nx_end, g.ny_start, g.ny_end, g.bnd_x1,
+                                         g.bnd_x2, g.bnd_y1, g.bnd_y2, g.pitch, tuple(bi.nbr_rank),
+                                         tuple(bi.nbr_k)))
+
+    # ---------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "ctx", None):
+            lib().ocn_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def attach_comm(self, unique_id: bytes):
+        """Attach an RCCL communicator (unique id made by ``make_unique_id`` on rank 0)."""
+        buf = C.create_string_buffer(bytes(unique_id), len(unique_id))
+        check(lib().ocn_ctx_attach_comm(self.ctx, buf, len(unique_id)), "ocn_ctx_attach_comm")
+
+    def init(self):
+        check(lib().ocn_ctx_init_state(self.ctx), "ocn_ctx_init_state")
+        return self
+
+    def set_graph(self, on: bool = True):
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_GRAPH, int(on)), "ocn_ctx_set_option")
+        return self
+
+    def set_stage_timing(self, on: bool = True):
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_STAGE_TIMING, int(on)), "ocn_ctx_set_option")
+        return self
+
+    def stage_times(self) -> dict:
+        """{stage: (total_ms, launches)} from HIP events since the last call (synchronises)."""
+        ms = (C.c_double * len(_lib.STAGES))()
+        n = (C.c_int64 * len(_lib.STAGES))()
+        check(lib().ocn_ctx_stage_times(self.ctx, ms, n), "ocn_ctx_stage_times")
+        return {s: (ms[i], n[i]) for i, s in enumerate(_lib.STAGES) if n[i]}
+
+    # ---------------------------------------------------------------- execution
+    def step(self, nsteps: int = 1, tau: float = 1.0, check_every: int = 1):
+        check(lib().ocn_ctx_step(self.ctx, tau, nsteps, check_every), "ocn_ctx_step")
+        return self
+
+    def stage(self, name: str, tau: float = 1.0):
+        check(lib().ocn_ctx_stage(self.ctx, STAGE_ID[name], tau), f"ocn_ctx_stage({name})")
+
+    def sync(self, field: str):
+        check(lib().ocn_ctx_sync(self.ctx, FIELD_ID[field]), f"ocn_ctx_sync({field})")
+
+    def synchronize(self):
+        check(lib().ocn_ctx_synchronize(self.ctx), "ocn_ctx_synchronize")
+        return self
+
+    @property
+    def stream(self) -> int:
+        return lib().ocn_ctx_stream(self.ctx)
+
+    # ---------------------------------------------------------------- data access
+    def field_ptr(self, k: int, name: str) -> int:
+        p = lib().ocn_ctx_field(self.ctx, k, FIELD_ID[name])
+        if not p:
+            raise _lib.OcnError(_lib.OCN_ERR_ARG, f"no field {name} in block {k}")
+        return p
+
+    def download(self, k: int, name: str) -> np.ndarray:
+        b = self.blocks[k]
+        dt = np.float64 if name in R8_NAMES else np.float32
+        a = np.zeros(b.shape, dtype=dt, order="F")
+        check(lib().ocn_ctx_download(self.ctx, k, FIELD_ID[name], a.ctypes.data_as(C.c_void_p)), "download")
+        return a
+
+    def upload(self, k: int, name: str, a: np.ndarray):
+        b = self.blocks[k]
+        dt = np.float64 if name in R8_NAMES else np.float32
+        a = np.asfortranarray(a, dtype=dt)
+        if a.shape != b.shape:
+            raise ValueError(f"{name}: shape {a.shape} != block shape {b.shape}")
+        check(lib().ocn_ctx_upload(self.ctx, k, FIELD_ID[name], a.ctypes.data_as(C.c_void_p)), "upload")
+
+    def state(self, names=None) -> list[dict[str, np.ndarray]]:
+        names = names or list(FIELD_ID)
+        return [{n: self.download(b.k, n) for n in names} for b in self.blocks]
+
+    @property
+    def interior_cells(self) -> int:
+        """(nx-4)(ny-4) share of this process: the cell-updates/s unit of SURVEY.md 8(d)."""
+        return sum(b.cells for b in self.blocks)
+
+
+def make_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    check(lib().ocn_comm_unique_id(buf, 128), "ocn_comm_unique_id")
+    return buf.raw

@@ -1,0 +1,198 @@
+"""GPU parity: the HIP path (libocn_sw.so, through its C ABI) against the reference.
+
+* per-kernel: every kernel-layer entry on the golden random inputs of the compiled
+  reference (tests/golden/kernels_*.npz) -- bitwise, untouched cells included;
+* end-to-end: init + N steps on the golden cases (1 and several blocks on one GPU) against
+  the SHA-256 of every field of every block of the unmodified reference run -- bitwise;
+* larger sizes: against the CPU oracle (pinned to the reference by tests/test_oracle_pinned.py);
+* full size (BASELINE 4096^2): size-independent properties (decomposition invariance,
+  graph == eager, finite & bounded state).
+
+Tolerance: none.  The path computes in fp64 with the reference's evaluation order and
+-ffp-contract=off, so every comparison is bit-for-bit.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from tests.golden import cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a.ravel(order="F")).tobytes()).hexdigest()
+
+
+def bits_equal(a, b):
+    return a.dtype == b.dtype and a.shape == b.shape and \
+        np.ascontiguousarray(a.ravel(order="F")).tobytes() == np.ascontiguousarray(b.ravel(order="F")).tobytes()
+
+
+@pytest.fixture(scope="module")
+def amd():
+    import ocean_model_arch_amd as amd
+    amd.lib()
+    return amd
+
+
+def model_for_geom(amd, z):
+    nxs, nxe, nys, nye, bx1, bx2, by1, by2 = (int(v) for v in z["geom"])
+    assert (nxs, nys, bx1, by1) == (3, 3, 1, 1)
+    m = amd.OceanModel(amd.BasinConfig(nx=bx2, ny=by2))
+    b = m.blocks[0]
+    assert (b.nx_start, b.nx_end, b.ny_start, b.ny_end, b.bnd_x1, b.bnd_x2) == (nxs, nxe, nys, nye, bx1, bx2)
+    return m
+
+
+@pytest.mark.parametrize("geom", cases.KERNEL_GEOMS)
+def test_kernels_match_reference(amd, geom):
+    from ocean_model_arch_amd.kernel_interface import KernelParameters
+    from ocean_model_arch_amd.sw_interface import ShallowWaterInterface
+    z = cases.load_kernels(geom)
+    m = model_for_geom(amd, z)
+    inputs = {k[3:]: z[k] for k in z.files if k.startswith("in/")}
+    iface = ShallowWaterInterface(m)
+    p = KernelParameters(tau=float(z["tau"]), time_smooth=float(z["time_smooth"]))
+    assert int(z["full_free_surface"]) == m.sw.full_free_surface
+    failures = []
+    for kname in cases.KERNEL_NAMES:
+        for nm, a in inputs.items():
+            m.upload(0, nm, a)
+        getattr(iface, f"envoke_{kname}_kernel")(0, p)
+        m.synchronize()
+        outs = [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]
+        for nm in outs:
+            if not bits_equal(m.download(0, nm), z[f"{kname}/{nm}"]):
+                failures.append(f"{kname}:{nm}")
+    m.close()
+    assert not failures, f"{geom}: differs from the reference: {failures}"
+
+
+def build_model(amd, case, graph=False):
+    b = case["basin"]
+    basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
+                            curve_grid=b["curve_grid"], mask=case["mask"])
+    sw = amd.SWConfig(**case["sw"])
+    par = amd.ParallelConfig(bppnx=case["bxy"][0], bppny=case["bxy"][1])
+    m = amd.OceanModel(basin, sw, par)
+    if graph:
+        m.set_graph(True)
+    return m
+
+
+def compare_case(m, case, name):
+    z = case["z"]
+    blocks = cases.e2e_blocks(z)
+    assert len(blocks) == len(m.blocks), name
+    bad = []
+    for b in m.blocks:
+        info = blocks[(b.bm, b.bn)]
+        assert [b.nx_start, b.nx_end, b.ny_start, b.ny_end, b.bnd_x1, b.bnd_x2, b.bnd_y1, b.bnd_y2] == list(info)
+        for key in z.files:
+            pre = f"b{b.bm}_{b.bn}/sha/"
+            if key.startswith(pre):
+                nm = key[len(pre):]
+                if _sha(m.download(b.k, nm)) != str(z[key]):
+                    bad.append(f"({b.bm},{b.bn}):{nm}")
+    return bad
+
+
+@pytest.mark.parametrize("name", cases.E2E_CASES)
+def test_end_to_end_matches_reference(amd, name):
+    case = cases.load_e2e(name)
+    m = build_model(amd, case)
+    m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
+    bad = compare_case(m, case, name)
+    m.close()
+    assert not bad, f"{name}: fields differ from the reference: {bad}"
+
+
+@pytest.mark.parametrize("name", ["box70x54_b3x2_s20", "bs_b1x1_s60"])
+def test_graph_step_matches_reference(amd, name):
+    case = cases.load_e2e(name)
+    m = build_model(amd, case, graph=True)
+    m.init().step(case["steps"], tau=1.0, check_every=0).synchronize()
+    bad = compare_case(m, case, name)
+    m.close()
+    assert not bad, f"{name} (hipGraph): fields differ: {bad}"
+
+
+def test_psykal_host_path_matches_reference(amd):
+    """Reference-shaped host: expl_shallow_water -> envoke -> envoke_<stage>_kernel -> C ABI entry."""
+    from ocean_model_arch_amd.shallow_water import expl_shallow_water
+    from ocean_model_arch_amd.sw_interface import ShallowWaterInterface
+    case = cases.load_e2e("box70x54_b3x2_s20")
+    m = build_model(amd, case)
+    m.init()
+    iface = ShallowWaterInterface(m)
+    for _ in range(case["steps"]):
+        expl_shallow_water(m, 1.0, iface)
+    m.synchronize()
+    bad = compare_case(m, case, "psykal")
+    m.close()
+    assert not bad, bad
+
+
+def _oracle_state(n, bxy, steps):
+    from oracle import oracle as O
+    om = O.OracleModel(O.BasinConfig(nx=n + 4, ny=n + 4), O.SWConfig(), *bxy).init().run(steps)
+    return om
+
+
+@pytest.mark.parametrize("n,bxy,steps", [(256, (1, 1), 10), (1024, (1, 1), 3), (300, (3, 2), 8)])
+def test_larger_boxes_match_oracle(amd, n, bxy, steps):
+    om = _oracle_state(n, bxy, steps)
+    m = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(*bxy))
+    m.init().step(steps).synchronize()
+    bad = []
+    for b in m.blocks:
+        k = [i for i, ob in enumerate(om.blocks) if (ob.bm, ob.bn) == (b.bm, b.bn)][0]
+        for nm, a in om.f[k].items():
+            if nm in ("lu1", "rlh_c"):
+                continue
+            if not bits_equal(m.download(b.k, nm), a):
+                bad.append(f"({b.bm},{b.bn}):{nm}")
+    m.close()
+    assert not bad, bad
+
+
+def _interior(m, nm):
+    """Assemble the global interior of field nm from all blocks."""
+    nx, ny = m.basin.nx, m.basin.ny
+    g = np.full((nx, ny), np.nan)
+    for b in m.blocks:
+        a = m.download(b.k, nm)
+        g[b.nx_start - 1:b.nx_end, b.ny_start - 1:b.ny_end] = \
+            a[b.nx_start - b.bnd_x1:b.nx_end - b.bnd_x1 + 1, b.ny_start - b.bnd_y1:b.ny_end - b.bnd_y1 + 1]
+    return g
+
+
+def test_full_size_decomposition_invariance(amd):
+    """BASELINE box 4096^2: one block vs a 2 x 2 block grid on one GPU give bitwise-identical interiors
+    (the reference's own property: 1 vs 4 vs 8 ranks are bit-identical)."""
+    n, steps = 4096, 3
+    a = amd.OceanModel(amd.box_config(n)).init().step(steps).synchronize()
+    ga = {nm: _interior(a, nm) for nm in ("ssh", "ubrtr", "vbrtr", "sshp", "hhu", "hhh")}
+    a.close()
+    b = amd.OceanModel(amd.box_config(n), par=amd.ParallelConfig(2, 2)).init().step(steps).synchronize()
+    for nm, ref in ga.items():
+        got = _interior(b, nm)
+        assert np.isfinite(ref[2:-2, 2:-2]).all()
+        assert bits_equal(got, ref), nm
+    # the Gaussian hump starts to spread: bounded, nonzero velocities after 3 steps
+    assert 0.0 < np.nanmax(np.abs(ga["ubrtr"])) < 1.0
+    b.close()
+
+
+def test_blowup_is_reported(amd):
+    """check_ssh_err_kernel (vel_ssh.f90:40-67): |ssh| >= 1e4 on a sea point must fail the step."""
+    m = amd.OceanModel(amd.box_config(64)).init()
+    s = m.download(0, "ssh")
+    s[10, 10] = 2.0e4
+    for nm in ("ssh", "sshn", "sshp"):
+        m.upload(0, nm, s)
+    with pytest.raises(amd.OcnError):
+        m.step(1, check_every=1).synchronize()
+    m.close()
