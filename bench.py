@@ -30,6 +30,9 @@ STAGE_BYTES = {"sw_update_ssh": 68, "hh_update": 96, "uv_trans_vort": 44, "uv_tr
                "stress_components": 72, "uv_diff2": 96, "sw_update_uv": 200, "sw_next_step": 132,
                "hh_shift": 176, "hh_init": 168}
 B_ALG = sum(STAGE_BYTES.values())
+# distinct arrays read + written once per interior cell by each fused launch
+FUSED_BYTES = {"fused_a": 180, "fused_b": 252, "fused_c1": 132, "hh_init": 168}
+B_FUSED = sum(FUSED_BYTES.values())
 
 
 def dims_create(n: int):
@@ -77,6 +80,7 @@ def main():
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--graph", action="store_true", help="replay steps as hipGraphs (single process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stages", action="store_true", help="run the 11 reference stages instead of the fused step")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -101,6 +105,7 @@ def main():
         uid = [amd.make_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         model.attach_comm(uid[0])
+    model.set_fused(not args.stages)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -130,27 +135,33 @@ def main():
     local_cells = model.interior_cells
     out = None
     if rank == 0:
-        stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in STAGE_BYTES}
+        kbytes = STAGE_BYTES if args.stages else FUSED_BYTES
+        stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:
             dom = max(stage_ms, key=lambda s: stage_ms[s])
-            alg = STAGE_BYTES[dom] * local_cells
+            alg = kbytes[dom] * local_cells
             achieved = alg / (stage_ms[dom] * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": load_traffic(dom, local_cells),
                     "alg_bytes_per_launch": alg, "launch_ms": round(stage_ms[dom], 4)}
         step_gbs = B_ALG * cells * args.steps / dt / 1e9 / world
+        moved = (B_ALG if args.stages else B_FUSED) * cells * args.steps / dt / 1e9 / world
         out = {"metric": METRIC, "value": value, "unit": "cell-updates/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
                "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
                "data": "synthetic (Gaussian SSH hump in a closed flat-bottom box, SURVEY.md 8d)",
                "config": {"workload": f"{nxbox}x{nybox} box, {bx}x{by} blocks (1 per GPU), sw.par defaults, tau=1s",
                           "box": [nxbox, nybox], "blocks": [bx, by], "graph": bool(args.graph),
+                          "step": "reference stages" if args.stages else "fused groups",
                           "parallelism": f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else "1 block"},
                "roofline": roof,
                "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),
                "step_alg_gbs_per_gpu": round(step_gbs, 1),
+               "step_bytes_per_cell": {"reference_stages_B_alg": B_ALG,
+                                       "this_path": B_ALG if args.stages else B_FUSED},
+               "step_moved_frac": round(moved / HBM_PEAK_GBS, 4),
                "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()}}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()

@@ -226,13 +226,19 @@ int ocn_ctx_synchronize(ocn_ctx *ctx);
 int ocn_ctx_download(ocn_ctx *ctx, int k, int field_id, void *host);
 int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
 
-/* Execution options.  OCN_OPT_GRAPH: replay each step as one hipGraph (single-process runs).
- * OCN_OPT_STAGE_TIMING: bracket every stage's kernels with HIP events on the context stream. */
+/* Execution options.
+ *  OCN_OPT_GRAPH: replay each step as one hipGraph (single-process runs).
+ *  OCN_OPT_STAGE_TIMING: bracket every launch group with HIP events on the context stream.
+ *  OCN_OPT_FUSED (default 1): ocn_ctx_step runs the step as 4 fused launch groups and 3 halo
+ *  syncs (same results and final state bit for bit); 0 = the 11 envoke stages of the reference. */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
-enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3 };
+enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4 };
 
-/* Per-stage device time (ms, summed) and launch counts since the last call, from the HIP
- * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_STAGES entries.  Synchronises. */
+/* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT). */
+enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_NUM_TIMERS };
+
+/* Per-timer device time (ms, summed) and launch counts since the last call, from the HIP
+ * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_TIMERS entries.  Synchronises. */
 int ocn_ctx_stage_times(ocn_ctx *ctx, double *ms, int64_t *counts);
 
 const char *ocn_last_error(void);

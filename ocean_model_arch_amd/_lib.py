@@ -28,8 +28,10 @@ FIELD_ID.update({n: 32 + i for i, n in enumerate(R8_NAMES)})
 STAGES = ["sw_update_ssh", "hh_update", "uv_trans_vort", "uv_trans", "stress_components", "uv_diff2",
           "sw_update_uv", "sw_next_step", "hh_shift", "hh_init", "check_ssh_err"]
 STAGE_ID = {n: i for i, n in enumerate(STAGES)}
+TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"]     # OCN_NUM_TIMERS slots
 OPT_GRAPH = 1
 OPT_STAGE_TIMING = 3
+OPT_FUSED = 4
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",

@@ -50,10 +50,6 @@ int check_hip(hipError_t e, const char *what)
         if (_rc) return _rc;                                  \
     } while (0)
 
-static inline bool is_r8(int id) { return id >= OCN_SSH && id < OCN_FIELD_END; }
-static inline bool is_r4(int id) { return id >= 0 && id < OCN_NUM_R4; }
-static inline int field_slot(int id) { return is_r4(id) ? id : OCN_NUM_R4 + (id - OCN_SSH); }
-static constexpr int kNumSlots = OCN_NUM_R4 + OCN_NUM_R8;
 
 // ------------------------------------------------------------------ halo segments
 // One strided 1-D run of doubles: dst[i*dst_stride] = src[i*src_stride], i < count.
@@ -179,8 +175,10 @@ struct ocn_ctx {
     struct Rec { int stage; hipEvent_t a, b; };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> event_pool;
-    double stage_ms[OCN_NUM_STAGES] = {0};
-    int64_t stage_n[OCN_NUM_STAGES] = {0};
+    double stage_ms[OCN_NUM_TIMERS] = {0};
+    int64_t stage_n[OCN_NUM_TIMERS] = {0};
+    bool fused = true;
+    std::vector<int> sync_a, sync_b;
 };
 
 namespace ocn {
@@ -536,7 +534,18 @@ static const std::vector<int> *stage_sync(int stage)
 // every plan a step can use, built before any graph capture (no hipMalloc while capturing)
 static int prebuild_plans(ocn_ctx *c)
 {
+    // fused-step sync groups (shallow_water.f90 syncs regrouped, see one_step_fused)
+    const ocn_sw_params &sw = c->sw;
+    c->sync_a = {OCN_SSHN};
+    if (sw.full_free_surface > 0) c->sync_a.insert(c->sync_a.end(), {OCN_HHU_N, OCN_HHV_N, OCN_HHH_N});
+    if (sw.trans_terms > 0) c->sync_a.push_back(OCN_VORT);
+    if (sw.ksw_lat > 0) c->sync_a.insert(c->sync_a.end(), {OCN_STR_T, OCN_STR_S});
+    c->sync_b = {};
+    if (sw.trans_terms > 0) c->sync_b = {OCN_HHU_P, OCN_HHV_P, OCN_HHH_P};
+    c->sync_b.insert(c->sync_b.end(), {OCN_VBRTRN, OCN_UBRTRN});
     HaloPlan *p;
+    RC(get_plan(c, c->sync_a, p));
+    RC(get_plan(c, c->sync_b, p));
     for (const std::vector<int> *l : {&kSyncSsh, &kSyncHhUpdate, &kSyncVort, &kSyncUvTrans, &kSyncStress, &kSyncUv,
                                       &kSyncHhInit})
         RC(get_plan(c, *l, p));
@@ -550,18 +559,28 @@ static int get_event(ocn_ctx *c, hipEvent_t &e)
     return OCN_OK;
 }
 
+static int timer_begin(ocn_ctx *c, int id, ocn_ctx::Rec &rec)
+{
+    rec = ocn_ctx::Rec{id, nullptr, nullptr};
+    if (!c->stage_timing) return OCN_OK;
+    RC(get_event(c, rec.a)); RC(get_event(c, rec.b));
+    HIPCHK(hipEventRecord(rec.a, c->stream));
+    return OCN_OK;
+}
+static int timer_end(ocn_ctx *c, ocn_ctx::Rec &rec)
+{
+    if (!c->stage_timing) return OCN_OK;
+    HIPCHK(hipEventRecord(rec.b, c->stream));
+    c->recs.push_back(rec);
+    return OCN_OK;
+}
+
 static int envoke(ocn_ctx *c, int stage, double tau)
 {
-    ocn_ctx::Rec rec{stage, nullptr, nullptr};
-    if (c->stage_timing) {
-        RC(get_event(c, rec.a)); RC(get_event(c, rec.b));
-        HIPCHK(hipEventRecord(rec.a, c->stream));
-    }
+    ocn_ctx::Rec rec;
+    RC(timer_begin(c, stage, rec));
     for (const LBlock &b : c->blocks) RC(stage_kernel(c, b, stage, tau));
-    if (c->stage_timing) {
-        HIPCHK(hipEventRecord(rec.b, c->stream));
-        c->recs.push_back(rec);
-    }
+    RC(timer_end(c, rec));
     const std::vector<int> *sl = stage_sync(stage);
     if (sl) RC(run_sync(c, *sl));
     return OCN_OK;
@@ -588,6 +607,28 @@ static int one_step(ocn_ctx *c, double tau, bool check)
         RC(envoke(c, OCN_STAGE_HH_INIT, tau));
     }
     if (check) RC(envoke(c, OCN_STAGE_CHECK_SSH_ERR, tau));
+    return OCN_OK;
+}
+
+// Fused step (sw_kernels.hip "fused step groups"): 4 launches and 3 halo syncs per step,
+// bitwise the same state as one_step.
+static int one_step_fused(ocn_ctx *c, double tau, bool check)
+{
+    const ocn_sw_params &sw = c->sw;
+    ocn_ctx::Rec rec;
+    RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
+    for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), sw, tau, c->stream));
+    RC(timer_end(c, rec));
+    RC(run_sync(c, c->sync_a));
+    RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
+    for (const LBlock &b : c->blocks) RC(launch_fused_b(&b.g, b.ptr.data(), sw, tau, c->stream));
+    RC(timer_end(c, rec));
+    RC(run_sync(c, c->sync_b));
+    RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
+    for (const LBlock &b : c->blocks)
+        RC(launch_fused_c1(&b.g, b.ptr.data(), sw, check ? c->d_nbad : nullptr, c->stream));
+    RC(timer_end(c, rec));
+    if (sw.full_free_surface > 0) RC(envoke(c, OCN_STAGE_HH_INIT, tau));
     return OCN_OK;
 }
 
@@ -861,7 +902,7 @@ static int capture_step(ocn_ctx *c, double tau, bool check)
 {
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = one_step(c, tau, check);
+    int rc = c->fused ? one_step_fused(c, tau, check) : one_step(c, tau, check);
     hipError_t e = hipStreamEndCapture(c->stream, &graph);
     if (rc) return rc;
     HIPCHK(e);
@@ -884,6 +925,8 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
         if (graph_ok) {
             if (!c->graph_exec || c->graph_tau != tau || c->graph_check != (int)check) RC(capture_step(c, tau, check));
             HIPCHK(hipGraphLaunch(c->graph_exec, c->stream));
+        } else if (c->fused) {
+            RC(one_step_fused(c, tau, check));
         } else {
             RC(one_step(c, tau, check));
         }
@@ -914,8 +957,8 @@ int ocn_ctx_stage_times(ocn_ctx *c, double *ms, int64_t *counts)
         c->event_pool.push_back(r.a); c->event_pool.push_back(r.b);
     }
     c->recs.clear();
-    for (int i = 0; i < OCN_NUM_STAGES; ++i) { ms[i] = c->stage_ms[i]; counts[i] = c->stage_n[i]; }
-    for (int i = 0; i < OCN_NUM_STAGES; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
+    for (int i = 0; i < OCN_NUM_TIMERS; ++i) { ms[i] = c->stage_ms[i]; counts[i] = c->stage_n[i]; }
+    for (int i = 0; i < OCN_NUM_TIMERS; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
     return OCN_OK;
 }
 
@@ -946,6 +989,10 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     switch (key) {
     case OCN_OPT_GRAPH: c->use_graph = value != 0; return OCN_OK;
     case OCN_OPT_STAGE_TIMING: c->stage_timing = value != 0; return OCN_OK;
+    case OCN_OPT_FUSED:
+        if (c->fused != (value != 0) && c->graph_exec) { (void)hipGraphExecDestroy(c->graph_exec); c->graph_exec = nullptr; }
+        c->fused = value != 0;
+        return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -18,6 +18,16 @@
 namespace ocn {
 
 int set_error(int code, const std::string &msg);
+
+inline bool is_r8(int id) { return id >= OCN_SSH && id < OCN_FIELD_END; }
+inline bool is_r4(int id) { return id >= 0 && id < OCN_NUM_R4; }
+inline int field_slot(int id) { return is_r4(id) ? id : OCN_NUM_R4 + (id - OCN_SSH); }
+constexpr int kNumSlots = OCN_NUM_R4 + OCN_NUM_R8;
+
+// Fused step groups (sw_kernels.hip); `ptr` = the block's field table indexed by field_slot().
+int launch_fused_a(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s);
+int launch_fused_b(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s);
+int launch_fused_c1(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, int32_t *nbad, hipStream_t s);
 int check_hip(hipError_t e, const char *what);
 inline int check_launch() { return check_hip(hipGetLastError(), "kernel launch"); }
 

@@ -92,12 +92,9 @@ struct HhUpdate {
     const float *__restrict__ dxh, *__restrict__ dyh, *__restrict__ dxb, *__restrict__ dyb;
     double *__restrict__ hqn, *__restrict__ hun, *__restrict__ hvn, *__restrict__ hhn;
     const double *__restrict__ sh, *__restrict__ h_r;
-    __device__ void operator()(int m, int n) const
+    // the [start-1, end]^2 interpolation part (depth.f90:134-160)
+    __device__ __forceinline__ void interp(int m, int n, long c, double q00) const
     {
-        const long c = I(m, n);
-        const double q00 = h_r[c] + sh[c];
-        hqn[c] = q00;
-        if (m < i0 || m > i1 || n < j0 || n > j1) return;
         const long e = I(m + 1, n), nn = I(m, n + 1), ne = I(m + 1, n + 1);
         const Interp W{I, lu, dx, dy};
         if (llu[c] > 0.5f) {
@@ -115,6 +112,14 @@ struct HhUpdate {
             const double q10 = h_r[e] + sh[e], q01 = h_r[nn] + sh[nn], q11 = h_r[ne] + sh[ne];
             hhn[c] = (W.wt(q00, c) + W.wt(q10, e) + W.wt(q01, nn) + W.wt(q11, ne)) / slu / D(dxb[c]) / D(dyb[c]);
         }
+    }
+    __device__ void operator()(int m, int n) const
+    {
+        const long c = I(m, n);
+        const double q00 = h_r[c] + sh[c];
+        hqn[c] = q00;
+        if (m < i0 || m > i1 || n < j0 || n > j1) return;
+        interp(m, n, c, q00);
     }
 };
 
@@ -199,11 +204,8 @@ struct UvTrans {
     const double *__restrict__ u, *__restrict__ v, *__restrict__ vort;
     const double *__restrict__ hu, *__restrict__ hv, *__restrict__ hh;
     double *__restrict__ RHSx, *__restrict__ RHSy;
-    __device__ void operator()(int m, int n) const
+    __device__ __forceinline__ void eval(int m, int n, long c, bool bu, bool bv, double &rx, double &ry) const
     {
-        const long c = I(m, n);
-        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
-        if (!bu && !bv) return;
         const long e = I(m + 1, n), w = I(m - 1, n), nn = I(m, n + 1), s = I(m, n - 1);
         if (bu) {
             const long se = I(m + 1, n - 1);
@@ -214,8 +216,8 @@ struct UvTrans {
                                 * (u[nn] + u[c]) / 2.0 * D(luu[c]);
             const double fy_m = (v[s] * D(dxh[s]) * hv[s] + v[se] * D(dxh[se]) * hv[se]) / 2.0
                                 * (u[s] + u[c]) / 2.0 * D(luu[s]);
-            RHSx[c] = -(fx_p - fx_m + fy_p - fy_m)
-                      + (vort[c] * hh[c] * (v[e] + v[c]) + vort[s] * hh[s] * (v[se] + v[s])) / 4.0;
+            rx = -(fx_p - fx_m + fy_p - fy_m)
+                 + (vort[c] * hh[c] * (v[e] + v[c]) + vort[s] * hh[s] * (v[se] + v[s])) / 4.0;
         }
         if (bv) {
             const long wn = I(m - 1, n + 1);
@@ -226,9 +228,19 @@ struct UvTrans {
                                 * (v[e] + v[c]) / 2.0;
             const double fx_m = (u[w] * D(dyh[w]) * hu[w] + u[wn] * D(dyh[wn]) * hu[wn]) / 2.0
                                 * (v[w] + v[c]) / 2.0;
-            RHSy[c] = -(fx_p - fx_m + fy_p - fy_m)
-                      - (vort[c] * hh[c] * (u[nn] + u[c]) + vort[w] * hh[w] * (u[wn] + u[w])) / 4.0;
+            ry = -(fx_p - fx_m + fy_p - fy_m)
+                 - (vort[c] * hh[c] * (u[nn] + u[c]) + vort[w] * hh[w] * (u[wn] + u[w])) / 4.0;
         }
+    }
+    __device__ void operator()(int m, int n) const
+    {
+        const long c = I(m, n);
+        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
+        if (!bu && !bv) return;
+        double rx = 0.0, ry = 0.0;
+        eval(m, n, c, bu, bv, rx, ry);
+        if (bu) RHSx[c] = rx;
+        if (bv) RHSy[c] = ry;
     }
 };
 
@@ -270,11 +282,8 @@ struct UvDiff2 {
     const float *__restrict__ dxb, *__restrict__ dyb;
     const double *__restrict__ mu, *__restrict__ str_t, *__restrict__ str_s, *__restrict__ hq, *__restrict__ hh;
     double *__restrict__ RHSx, *__restrict__ RHSy;
-    __device__ void operator()(int m, int n) const
+    __device__ __forceinline__ void eval(int m, int n, long c, bool bu, bool bv, double &rx, double &ry) const
     {
-        const long c = I(m, n);
-        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
-        if (!bu && !bv) return;
         const long e = I(m + 1, n), nn = I(m, n + 1), ne = I(m + 1, n + 1);
         if (bu) {
             const long s = I(m, n - 1), se = I(m + 1, n - 1);
@@ -282,8 +291,8 @@ struct UvDiff2 {
             const double muh_m = (mu[c] + mu[e] + mu[s] + mu[se]) / 4.0;
             const float dy2p = dy[e] * dy[e], dy2 = dy[c] * dy[c];
             const float dxb2 = dxb[c] * dxb[c], dxb2m = dxb[s] * dxb[s];
-            RHSx[c] = (D(dy2p) * mu[e] * hq[e] * str_t[e] - D(dy2) * mu[c] * hq[c] * str_t[c]) / D(dyh[c])
-                      + (D(dxb2) * muh_p * hh[c] * str_s[c] - D(dxb2m) * muh_m * hh[s] * str_s[s]) / D(dxt[c]);
+            rx = (D(dy2p) * mu[e] * hq[e] * str_t[e] - D(dy2) * mu[c] * hq[c] * str_t[c]) / D(dyh[c])
+                 + (D(dxb2) * muh_p * hh[c] * str_s[c] - D(dxb2m) * muh_m * hh[s] * str_s[s]) / D(dxt[c]);
         }
         if (bv) {
             const long w = I(m - 1, n), wn = I(m - 1, n + 1);
@@ -291,9 +300,19 @@ struct UvDiff2 {
             const double muh_m = (mu[c] + mu[w] + mu[nn] + mu[wn]) / 4.0;
             const float dx2p = dx[nn] * dx[nn], dx2 = dx[c] * dx[c];
             const float dyb2 = dyb[c] * dyb[c], dyb2m = dyb[w] * dyb[w];
-            RHSy[c] = -(D(dx2p) * mu[nn] * hq[nn] * str_t[nn] - D(dx2) * mu[c] * hq[c] * str_t[c]) / D(dxh[c])
-                      + (D(dyb2) * muh_p * hh[c] * str_s[c] - D(dyb2m) * muh_m * hh[w] * str_s[w]) / D(dyt[c]);
+            ry = -(D(dx2p) * mu[nn] * hq[nn] * str_t[nn] - D(dx2) * mu[c] * hq[c] * str_t[c]) / D(dxh[c])
+                 + (D(dyb2) * muh_p * hh[c] * str_s[c] - D(dyb2m) * muh_m * hh[w] * str_s[w]) / D(dyt[c]);
         }
+    }
+    __device__ void operator()(int m, int n) const
+    {
+        const long c = I(m, n);
+        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
+        if (!bu && !bv) return;
+        double rx = 0.0, ry = 0.0;
+        eval(m, n, c, bu, bv, rx, ry);
+        if (bu) RHSx[c] = rx;
+        if (bv) RHSy[c] = ry;
     }
 };
 
@@ -311,11 +330,10 @@ struct SwUpdateUv {
     const float *__restrict__ rdis, *__restrict__ rlh_s;
     const double *__restrict__ RHSx, *__restrict__ RHSy, *__restrict__ RHSx_adv, *__restrict__ RHSy_adv;
     const double *__restrict__ RHSx_dif, *__restrict__ RHSy_dif;
-    __device__ void operator()(int m, int n) const
+    // rxa/rxd/rya/ryd: RHSx_adv, RHSx_dif, RHSy_adv, RHSy_dif at this point (used under lcu / lcv)
+    __device__ __forceinline__ void eval(int m, int n, long c, bool bu, bool bv, double rxa, double rxd,
+                                         double rya, double ryd) const
     {
-        const long c = I(m, n);
-        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
-        if (!bu && !bv) return;
         const double g = D(OCN_FREE_FALL_ACC);
         if (bu) {
             const long e = I(m + 1, n), s = I(m, n - 1), se = I(m + 1, n - 1);
@@ -326,7 +344,7 @@ struct SwUpdateUv {
             const double fric = D(rd) / 2.0 * ubrtrp[c] * D(dxt[c]) * D(dyh[c]) * hhu[c];
             const double c1 = D(rlh_s[c]) * hhh[c] * D(dxb[c]) * D(dyb[c]) * (vbrtr[e] + vbrtr[c]);
             const double c2 = D(rlh_s[s]) * hhh[s] * D(dxb[s]) * D(dyb[s]) * (vbrtr[se] + vbrtr[s]);
-            const double grx = RHSx[c] + slx + RHSx_dif[c] + RHSx_adv[c] - fric + (c1 + c2) / 4.0;
+            const double grx = RHSx[c] + slx + rxd + rxa - fric + (c1 + c2) / 4.0;
             ubrtrn[c] = (ubrtrp[c] * bp0 + grx) / (bp);
         }
         if (bv) {
@@ -338,9 +356,19 @@ struct SwUpdateUv {
             const double fric = D(rd) / 2.0 * vbrtrp[c] * D(dxh[c]) * D(dyt[c]) * hhv[c];
             const double c1 = D(rlh_s[c]) * hhh[c] * D(dxb[c]) * D(dyb[c]) * (ubrtr[nn] + ubrtr[c]);
             const double c2 = D(rlh_s[w]) * hhh[w] * D(dxb[w]) * D(dyb[w]) * (ubrtr[wn] + ubrtr[w]);
-            const double gry = RHSy[c] + sly + RHSy_dif[c] + RHSy_adv[c] - fric - (c1 + c2) / 4.0;
+            const double gry = RHSy[c] + sly + ryd + rya - fric - (c1 + c2) / 4.0;
             vbrtrn[c] = (vbrtrp[c] * bp0 + gry) / (bp);
         }
+    }
+    __device__ void operator()(int m, int n) const
+    {
+        const long c = I(m, n);
+        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
+        if (!bu && !bv) return;
+        double rxa = 0.0, rxd = 0.0, rya = 0.0, ryd = 0.0;
+        if (bu) { rxa = RHSx_adv[c]; rxd = RHSx_dif[c]; }
+        if (bv) { rya = RHSy_adv[c]; ryd = RHSy_dif[c]; }
+        eval(m, n, c, bu, bv, rxa, rxd, rya, ryd);
     }
 };
 
@@ -415,6 +443,93 @@ struct CheckSshErr {
     }
 };
 
+// ================================================================== fused step groups
+// The step's 10 stages regrouped into 4 launches with the same results, write sets and halo
+// state as the stage-by-stage reference order (shallow_water.f90:36-92):
+//   A  = a1 sw_update_ssh + a2 hh_update + a3 uv_trans_vort + a5 stress_components
+//        (mutually independent: none reads another's output) -> one sync of their 7 fields.
+//        hh_update's whole-array hqn = h_r + ssh is not stored: its only readers are hh_shift's
+//        hq/hqp updates, which hh_init overwrites whole-array later in the same step.
+//   B  = a4 uv_trans + a6 uv_diff2 + a7 sw_update_uv: sw_update_uv reads RHS*_adv / RHS*_dif
+//        only at its own point, so they are passed in registers (and still stored) -> sync
+//        of u/v (and uv_trans's lazy hh*_p sync, whose halos nothing in B reads).
+//   C1 = a8 sw_next_step + a9 hh_shift on the outer ring only (on [start-1,end]^2 its
+//        outputs are dead: hh_init overwrites them) + check_ssh_err.
+//   C2 = a10 hh_init (unchanged) -> sync hhu/hhv/hhh.
+struct FusedA {
+    int sx, sy;
+    bool do_hh, do_vort, do_stress;
+    SwUpdateSsh a1; HhUpdate a2; UvTransVort a3; StressComponents a5;
+    __device__ void operator()(int m, int n) const
+    {
+        if (m >= sx && n >= sy) {
+            a1(m, n);
+            if (do_vort) a3(m, n);
+            if (do_stress) a5(m, n);
+        }
+        if (do_hh) {
+            const long c = a2.I(m, n);
+            a2.interp(m, n, c, a2.h_r[c] + a2.sh[c]);
+        }
+    }
+};
+
+struct FusedB {
+    bool do_adv, do_dif;
+    UvTrans a4; UvDiff2 a6; SwUpdateUv a7;
+    __device__ void operator()(int m, int n) const
+    {
+        const long c = a7.I(m, n);
+        const bool bu = a7.lcu[c] > 0.5f, bv = a7.lcv[c] > 0.5f;
+        if (!bu && !bv) return;
+        double rxa = 0.0, rya = 0.0, rxd = 0.0, ryd = 0.0;
+        if (do_adv) {
+            a4.eval(m, n, c, bu, bv, rxa, rya);
+            if (bu) a4.RHSx[c] = rxa;
+            if (bv) a4.RHSy[c] = rya;
+        } else {
+            if (bu) rxa = a7.RHSx_adv[c];
+            if (bv) rya = a7.RHSy_adv[c];
+        }
+        if (do_dif) {
+            a6.eval(m, n, c, bu, bv, rxd, ryd);
+            if (bu) a6.RHSx[c] = rxd;
+            if (bv) a6.RHSy[c] = ryd;
+        } else {
+            if (bu) rxd = a7.RHSx_dif[c];
+            if (bv) ryd = a7.RHSy_dif[c];
+        }
+        a7.eval(m, n, c, bu, bv, rxa, rxd, rya, ryd);
+    }
+};
+
+struct FusedC1 {
+    int sx, ex, sy, ey;
+    bool do_hh;
+    int *nbad;
+    SwNextStep a8; HhShift a9;
+    __device__ void operator()(int m, int n) const
+    {
+        a8(m, n);
+        if (do_hh && (m == ex + 1 || n == ey + 1)) a9(m, n);
+        if (nbad && m >= sx && m <= ex && n >= sy && n <= ey) {
+            const long c = a8.I(m, n);
+            if (a8.lu[c] > 0.5f) {
+                const double x = a8.ssh[c];
+                if (!(x < 10000.0 && x > -10000.0)) atomicAdd(nbad, 1);
+            }
+        }
+    }
+};
+
+#define CHECK(...)                                                \
+    do {                                                          \
+        int _rc = check_block(b);                                 \
+        if (_rc) return _rc;                                      \
+        _rc = nonnull({__VA_ARGS__});                             \
+        if (_rc) return _rc;                                      \
+    } while (0)
+
 // ================================================================== C ABI (kernel layer)
 static int check_block(const ocn_block *b)
 {
@@ -436,13 +551,72 @@ static int nonnull(std::initializer_list<const void *> ps)
     return OCN_OK;
 }
 
-#define CHECK(...)                                                \
-    do {                                                          \
-        int _rc = check_block(b);                                 \
-        if (_rc) return _rc;                                      \
-        _rc = nonnull({__VA_ARGS__});                             \
-        if (_rc) return _rc;                                      \
-    } while (0)
+#define RC_K(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
+
+// ------------------------------------------------------------------ fused launches
+#define F4(id) ((const float *)ptr[field_slot(id)])
+#define F8(id) ((double *)ptr[field_slot(id)])
+
+static SwUpdateSsh mk_a1(const ocn_block *b, void *const *ptr, double tau)
+{
+    return SwUpdateSsh{geo(b), tau, F4(OCN_LU), F4(OCN_DX), F4(OCN_DY), F4(OCN_DXH), F4(OCN_DYH), F8(OCN_HHU),
+                       F8(OCN_HHV), F8(OCN_SSHN), F8(OCN_SSHP), F8(OCN_UBRTR), F8(OCN_VBRTR)};
+}
+static HhUpdate mk_a2(const ocn_block *b, void *const *ptr)
+{
+    return HhUpdate{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end,
+                    F4(OCN_LU), F4(OCN_LLU), F4(OCN_LLV), F4(OCN_LUH), F4(OCN_DX), F4(OCN_DY), F4(OCN_DXT),
+                    F4(OCN_DYT), F4(OCN_DXH), F4(OCN_DYH), F4(OCN_DXB), F4(OCN_DYB), F8(OCN_HHQ_N), F8(OCN_HHU_N),
+                    F8(OCN_HHV_N), F8(OCN_HHH_N), F8(OCN_SSH), F8(OCN_HHQ_REST)};
+}
+
+int launch_fused_a(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s)
+{
+    RC_K(check_block(b));
+    FusedA k{b->nx_start, b->ny_start, sw.full_free_surface > 0, sw.trans_terms > 0, sw.ksw_lat > 0,
+             mk_a1(b, ptr, tau), mk_a2(b, ptr),
+             UvTransVort{geo(b), F4(OCN_LUU), F4(OCN_DXT), F4(OCN_DYT), F4(OCN_DXB), F4(OCN_DYB), F8(OCN_UBRTR),
+                         F8(OCN_VBRTR), F8(OCN_VORT)},
+             StressComponents{geo(b), F4(OCN_LU), F4(OCN_LUU), F4(OCN_DX), F4(OCN_DY), F4(OCN_DXT), F4(OCN_DYT),
+                              F4(OCN_DXH), F4(OCN_DYH), F4(OCN_DXB), F4(OCN_DYB), F8(OCN_UBRTRP), F8(OCN_VBRTRP),
+                              F8(OCN_STR_T), F8(OCN_STR_S)}};
+    const int o = k.do_hh ? 1 : 0;
+    return launch_range(b->nx_start - o, b->nx_end, b->ny_start - o, b->ny_end, k, s);
+}
+
+int launch_fused_b(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s)
+{
+    RC_K(check_block(b));
+    FusedB k{sw.trans_terms > 0, sw.ksw_lat > 0,
+             UvTrans{geo(b), F4(OCN_LCU), F4(OCN_LCV), F4(OCN_LUU), F4(OCN_DXH), F4(OCN_DYH), F8(OCN_UBRTR),
+                     F8(OCN_VBRTR), F8(OCN_VORT), F8(OCN_HHU), F8(OCN_HHV), F8(OCN_HHH), F8(OCN_RHSX_ADV),
+                     F8(OCN_RHSY_ADV)},
+             UvDiff2{geo(b), F4(OCN_LCU), F4(OCN_LCV), F4(OCN_DX), F4(OCN_DY), F4(OCN_DXT), F4(OCN_DYT), F4(OCN_DXH),
+                     F4(OCN_DYH), F4(OCN_DXB), F4(OCN_DYB), F8(OCN_MU), F8(OCN_STR_T), F8(OCN_STR_S), F8(OCN_HHQ),
+                     F8(OCN_HHH), F8(OCN_RHSX_DIF), F8(OCN_RHSY_DIF)},
+             SwUpdateUv{geo(b), tau, F4(OCN_LCU), F4(OCN_LCV), F4(OCN_DXT), F4(OCN_DYT), F4(OCN_DXH), F4(OCN_DYH),
+                        F4(OCN_DXB), F4(OCN_DYB), F8(OCN_HHU), F8(OCN_HHU_N), F8(OCN_HHU_P), F8(OCN_HHV),
+                        F8(OCN_HHV_N), F8(OCN_HHV_P), F8(OCN_HHH), F8(OCN_SSH), F8(OCN_UBRTR), F8(OCN_UBRTRN),
+                        F8(OCN_UBRTRP), F8(OCN_VBRTR), F8(OCN_VBRTRN), F8(OCN_VBRTRP), F4(OCN_R_DISS),
+                        F4(OCN_RLH_S), F8(OCN_RHSX), F8(OCN_RHSY), F8(OCN_RHSX_ADV), F8(OCN_RHSY_ADV),
+                        F8(OCN_RHSX_DIF), F8(OCN_RHSY_DIF)}};
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, s);
+}
+
+int launch_fused_c1(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, int32_t *nbad, hipStream_t s)
+{
+    RC_K(check_block(b));
+    FusedC1 k{b->nx_start, b->nx_end, b->ny_start, b->ny_end, sw.full_free_surface > 0, (int *)nbad,
+              SwNextStep{geo(b), sw.time_smooth, F4(OCN_LU), F4(OCN_LCU), F4(OCN_LCV), F8(OCN_SSH), F8(OCN_SSHN),
+                         F8(OCN_SSHP), F8(OCN_UBRTR), F8(OCN_UBRTRN), F8(OCN_UBRTRP), F8(OCN_VBRTR),
+                         F8(OCN_VBRTRN), F8(OCN_VBRTRP)},
+              HhShift{geo(b), sw.time_smooth, F4(OCN_LU), F4(OCN_LLU), F4(OCN_LLV), F4(OCN_LUH), F8(OCN_HHQ),
+                      F8(OCN_HHQ_P), F8(OCN_HHQ_N), F8(OCN_HHU), F8(OCN_HHU_P), F8(OCN_HHU_N), F8(OCN_HHV),
+                      F8(OCN_HHV_P), F8(OCN_HHV_N), F8(OCN_HHH), F8(OCN_HHH_P), F8(OCN_HHH_N)}};
+    return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, s);
+}
+#undef F4
+#undef F8
 
 }  // namespace ocn
 

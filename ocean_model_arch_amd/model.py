@@ -115,10 +115,15 @@ class OceanModel:
 
     def stage_times(self) -> dict:
         """{stage: (total_ms, launches)} from HIP events since the last call (synchronises)."""
-        ms = (C.c_double * len(_lib.STAGES))()
-        n = (C.c_int64 * len(_lib.STAGES))()
+        ms = (C.c_double * len(_lib.TIMERS))()
+        n = (C.c_int64 * len(_lib.TIMERS))()
         check(lib().ocn_ctx_stage_times(self.ctx, ms, n), "ocn_ctx_stage_times")
-        return {s: (ms[i], n[i]) for i, s in enumerate(_lib.STAGES) if n[i]}
+        return {s: (ms[i], n[i]) for i, s in enumerate(_lib.TIMERS) if n[i]}
+
+    def set_fused(self, on: bool = True):
+        """Fused step groups (default) or the reference's 11 envoke stages; same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FUSED, int(on)), "ocn_ctx_set_option")
+        return self
 
     # ---------------------------------------------------------------- execution
     def step(self, nsteps: int = 1, tau: float = 1.0, check_every: int = 1):

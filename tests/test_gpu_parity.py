@@ -70,13 +70,14 @@ def test_kernels_match_reference(amd, geom):
     assert not failures, f"{geom}: differs from the reference: {failures}"
 
 
-def build_model(amd, case, graph=False):
+def build_model(amd, case, graph=False, fused=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"])
     sw = amd.SWConfig(**case["sw"])
     par = amd.ParallelConfig(bppnx=case["bxy"][0], bppny=case["bxy"][1])
     m = amd.OceanModel(basin, sw, par)
+    m.set_fused(fused)
     if graph:
         m.set_graph(True)
     return m
@@ -99,10 +100,12 @@ def compare_case(m, case, name):
     return bad
 
 
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "stages"])
 @pytest.mark.parametrize("name", cases.E2E_CASES)
-def test_end_to_end_matches_reference(amd, name):
+def test_end_to_end_matches_reference(amd, name, fused):
+    """fused = the 4-launch step (default); stages = the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    m = build_model(amd, case)
+    m = build_model(amd, case, fused=fused)
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     bad = compare_case(m, case, name)
     m.close()
@@ -141,10 +144,11 @@ def _oracle_state(n, bxy, steps):
     return om
 
 
-@pytest.mark.parametrize("n,bxy,steps", [(256, (1, 1), 10), (1024, (1, 1), 3), (300, (3, 2), 8)])
-def test_larger_boxes_match_oracle(amd, n, bxy, steps):
+@pytest.mark.parametrize("n,bxy,steps,fused", [(256, (1, 1), 10, True), (1024, (1, 1), 3, True),
+                                                (300, (3, 2), 8, True), (300, (3, 2), 8, False)])
+def test_larger_boxes_match_oracle(amd, n, bxy, steps, fused):
     om = _oracle_state(n, bxy, steps)
-    m = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(*bxy))
+    m = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(*bxy)).set_fused(fused)
     m.init().step(steps).synchronize()
     bad = []
     for b in m.blocks:
