@@ -191,6 +191,29 @@ typedef struct ocn_block_info {
 
 typedef struct ocn_ctx ocn_ctx;
 
+/* Host-only (no GPU needed): the blocks rank dec->rank owns, as ocn_ctx_create would make them.
+ * Writes min(count, cap) entries; *count = number of blocks. */
+int ocn_decompose(const ocn_basin *basin, const ocn_decomp *dec, const int32_t *mask,
+                  ocn_block_info *out, int32_t cap, int32_t *count);
+
+/* Host-only schedule of one halo exchange of the real(8) fields `field_ids` for rank dec->rank:
+ * the copies/messages ocn_ctx_sync performs (syncborder_block2D_gen_all.fi semantics).
+ * LOCAL: strip src of local block k_src -> strip dst of local block k.
+ * SEND : strip src of local block k_src -> message to `peer` at element `offset`.
+ * RECV : message from `peer` at element `offset` -> strip dst of local block k.
+ * Rects are inclusive global 1-based indices; strips are walked column-major. */
+enum { OCN_HALO_LOCAL = 0, OCN_HALO_SEND = 1, OCN_HALO_RECV = 2 };
+typedef struct ocn_halo_msg {
+    int32_t kind, peer, k, k_src, field;
+    int32_t dst_x0, dst_x1, dst_y0, dst_y1;
+    int32_t src_x0, src_x1, src_y0, src_y1;
+    int32_t count;
+    int64_t offset;
+} ocn_halo_msg;
+int ocn_halo_schedule(const ocn_basin *basin, const ocn_decomp *dec, const int32_t *mask,
+                      const int32_t *field_ids, int32_t nfields, ocn_halo_msg *out, int32_t cap,
+                      int32_t *count);
+
 /* Create a context: decomposes the basin (mask = int32 global (nx,ny) column-major, 0 = sea,
  * 1 = land, or NULL for the closed box of tools/io.f90:49-59), allocates every field of every
  * local block on `device` (zero-filled, as data_types.f90:517-533). */

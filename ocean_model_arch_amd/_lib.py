@@ -37,7 +37,7 @@ OPT_FUSED = 4
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",
                   "ocn_stress_components", "ocn_uv_diff2", "ocn_sw_update_uv", "ocn_sw_next_step",
                   "ocn_hh_shift", "ocn_hh_init", "ocn_check_ssh_err"]
-CTX_SYMBOLS = ["ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
+CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
                "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm",
                "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
                "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_set_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version"]
@@ -80,6 +80,15 @@ class OcnBlockInfo(C.Structure):
     _fields_ = [("geom", OcnBlock), ("bm", C.c_int32), ("bn", C.c_int32),
                 ("nbr_rank", C.c_int32 * 8), ("nbr_k", C.c_int32 * 8)]
 
+
+class OcnHaloMsg(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("peer", C.c_int32), ("k", C.c_int32), ("k_src", C.c_int32),
+                ("field", C.c_int32), ("dst_x0", C.c_int32), ("dst_x1", C.c_int32), ("dst_y0", C.c_int32),
+                ("dst_y1", C.c_int32), ("src_x0", C.c_int32), ("src_x1", C.c_int32), ("src_y0", C.c_int32),
+                ("src_y1", C.c_int32), ("count", C.c_int32), ("offset", C.c_int64)]
+
+
+HALO_LOCAL, HALO_SEND, HALO_RECV = 0, 1, 2
 
 _lib = None
 
@@ -131,6 +140,10 @@ def lib() -> C.CDLL:
     L.ocn_ctx_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ocn_ctx_attach_comm.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     L.ocn_comm_unique_id.argtypes = [C.c_void_p, C.c_int32]
+    L.ocn_decompose.argtypes = [C.POINTER(OcnBasin), C.POINTER(OcnDecomp), C.c_void_p, C.POINTER(OcnBlockInfo),
+                                C.c_int32, C.POINTER(C.c_int32)]
+    L.ocn_halo_schedule.argtypes = [C.POINTER(OcnBasin), C.POINTER(OcnDecomp), C.c_void_p, C.POINTER(C.c_int32),
+                                    C.c_int32, C.POINTER(OcnHaloMsg), C.c_int32, C.POINTER(C.c_int32)]
     _lib = L
     return L
 

@@ -317,43 +317,49 @@ static int allocate(ocn_ctx *c)
 // syncborder_block2D_gen_all.fi: halo of block k in dir d <- boundary of neighbour in inverse(d).
 // Messages between two processes carry, for every (sending block, dir) pair in global block
 // order and every field of the sync group, the boundary strip in column-major order.
-static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan)
-{
-    std::vector<Seg> local;
-    std::map<int, std::vector<Seg>> pack, unpack;
-    std::map<int, long> send_count, recv_count;
-    // global index of local blocks
-    std::map<int, const LBlock *> by_gid;
-    for (const LBlock &b : c->blocks) by_gid[b.gid] = &b;
+// Host-only schedule of one halo exchange (no device pointers): every entry copies the
+// 1-wide strip `src` of local block ks (local copy or send) into the strip `dst` of local block
+// k (local copy or receive).  Message layout between two processes: for every (receiving
+// block, dir) in global block order, every field of the group, the sender's boundary strip in
+// column-major order -- enumerated identically on both sides from global knowledge.
+struct PlanEntry {
+    int kind;          // OCN_HALO_LOCAL / OCN_HALO_SEND / OCN_HALO_RECV
+    int peer;          // rank (send/recv), own rank for local
+    int k, ks;         // destination / source local block (-1 where not applicable)
+    int field;
+    Rect dst, src;
+    long buf_off;      // element offset in the peer's message (send/recv)
+    int count;
+};
 
+static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::vector<PlanEntry> &out)
+{
+    out.clear();
+    std::map<int, int> k_of_gid;
+    for (size_t k = 0; k < c->blocks.size(); ++k) k_of_gid[c->blocks[k].gid] = (int)k;
+    std::map<int, long> send_count, recv_count;
     // receiving side: my halos in gid order, dirs 1..8
-    for (auto &kv : by_gid) {
-        const LBlock &b = *kv.second;
+    for (auto &kv : k_of_gid) {
+        const int k = kv.second;
+        const LBlock &b = c->blocks[k];
         for (int d = 1; d <= 8; ++d) {
             const int r = b.nbr_rank[d - 1];
             if (r < 0) continue;
             const GBlock &src = c->gblocks[b.nbr_gid[d - 1]];
             const Rect hr = halo_points(b.g, d);
             const Rect br = boundary_points(src.g, inverse_dir(d));
-            long hoff; int hcnt; long hstr;
-            strip(b.g, hr, hoff, hcnt, hstr);
+            const int cnt = (hr.x1 - hr.x0 + 1) * (hr.y1 - hr.y0 + 1);
             for (int id : fields) {
-                double *dst = b.f<double>(id) + hoff;
-                if (r == c->dec.rank) {
-                    const LBlock &sb = *by_gid.at(b.nbr_gid[d - 1]);
-                    long soff; int scnt; long sstr;
-                    strip(sb.g, br, soff, scnt, sstr);
-                    local.push_back(Seg{sb.f<double>(id) + soff, dst, sstr, hstr, hcnt});
-                } else {
-                    // offset in the recv buffer from rank r is filled in below (relative index)
-                    unpack[r].push_back(Seg{(const double *)(intptr_t)recv_count[r], dst, 1, hstr, hcnt});
-                    recv_count[r] += hcnt;
+                if (r == c->dec.rank)
+                    out.push_back(PlanEntry{OCN_HALO_LOCAL, r, k, k_of_gid.at(b.nbr_gid[d - 1]), id, hr, br, 0, cnt});
+                else {
+                    out.push_back(PlanEntry{OCN_HALO_RECV, r, k, -1, id, hr, br, recv_count[r], cnt});
+                    recv_count[r] += cnt;
                 }
             }
         }
     }
-    // sending side: the remote receivers in gid order, dirs 1..8, where the source is mine.
-    // Enumerate receivers (any rank != mine) that have a neighbour block on my rank.
+    // sending side: remote receivers in gid order, dirs 1..8, whose source block is mine
     for (size_t gid = 0; gid < c->gblocks.size(); ++gid) {
         const GBlock &rb = c->gblocks[gid];
         if (rb.rank < 0 || rb.rank == c->dec.rank) continue;
@@ -362,30 +368,56 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
             if (m < 1 || m > c->bnx || n < 1 || n > c->bny) continue;
             const int sg = (m - 1) + (n - 1) * c->bnx;
             if (c->gblocks[sg].rank != c->dec.rank) continue;
-            const LBlock &sb = *by_gid.at(sg);
-            const Rect br = boundary_points(sb.g, inverse_dir(d));
-            long soff; int scnt; long sstr;
-            strip(sb.g, br, soff, scnt, sstr);
+            const int ks = k_of_gid.at(sg);
+            const Rect br = boundary_points(c->blocks[ks].g, inverse_dir(d));
+            const Rect hr = halo_points(rb.g, d);
+            const int cnt = (br.x1 - br.x0 + 1) * (br.y1 - br.y0 + 1);
             for (int id : fields) {
-                pack[rb.rank].push_back(Seg{sb.f<double>(id) + soff, (double *)(intptr_t)send_count[rb.rank],
-                                            sstr, 1, scnt});
-                send_count[rb.rank] += scnt;
+                out.push_back(PlanEntry{OCN_HALO_SEND, rb.rank, -1, ks, id, hr, br, send_count[rb.rank], cnt});
+                send_count[rb.rank] += cnt;
             }
         }
     }
-    // allocate message buffers and resolve relative offsets
-    std::vector<Seg> all_pack, all_unpack;
-    for (auto &kv : recv_count) {
-        const int r = kv.first;
-        HaloPlan::Peer p{r, kv.second, nullptr, nullptr};
-        if (send_count[r] != kv.second)
-            return set_error(OCN_ERR_STATE, "halo plan: asymmetric message sizes");
+    for (auto &kv : recv_count)
+        if (send_count[kv.first] != kv.second) return set_error(OCN_ERR_STATE, "halo plan: asymmetric message sizes");
+    for (auto &kv : send_count)
+        if (recv_count[kv.first] != kv.second) return set_error(OCN_ERR_STATE, "halo plan: asymmetric message sizes");
+    return OCN_OK;
+}
+
+static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan)
+{
+    std::vector<PlanEntry> entries;
+    RC(plan_entries(c, fields, entries));
+    std::map<int, long> msg;                       // peer -> message length
+    for (const PlanEntry &e : entries)
+        if (e.kind == OCN_HALO_RECV) msg[e.peer] = std::max(msg[e.peer], e.buf_off + e.count);
+    std::map<int, HaloPlan::Peer> peers;
+    for (auto &kv : msg) {
+        HaloPlan::Peer p{kv.first, kv.second, nullptr, nullptr};
         HIPCHK(hipMalloc(&p.send, sizeof(double) * std::max(1L, p.count)));
         HIPCHK(hipMalloc(&p.recv, sizeof(double) * std::max(1L, p.count)));
         c->allocs.push_back(p.send); c->allocs.push_back(p.recv);
-        for (Seg s : pack[r]) { s.dst = p.send + (intptr_t)s.dst; all_pack.push_back(s); }
-        for (Seg s : unpack[r]) { s.src = p.recv + (intptr_t)s.src; all_unpack.push_back(s); }
+        peers[kv.first] = p;
         plan.peers.push_back(p);
+    }
+    std::vector<Seg> local, pack, unpack;
+    for (const PlanEntry &e : entries) {
+        long doff, soff, dstr, sstr; int dcnt, scnt;
+        if (e.kind == OCN_HALO_LOCAL) {
+            const LBlock &db = c->blocks[e.k], &sb = c->blocks[e.ks];
+            strip(db.g, e.dst, doff, dcnt, dstr);
+            strip(sb.g, e.src, soff, scnt, sstr);
+            local.push_back(Seg{sb.f<double>(e.field) + soff, db.f<double>(e.field) + doff, sstr, dstr, dcnt});
+        } else if (e.kind == OCN_HALO_RECV) {
+            const LBlock &db = c->blocks[e.k];
+            strip(db.g, e.dst, doff, dcnt, dstr);
+            unpack.push_back(Seg{peers.at(e.peer).recv + e.buf_off, db.f<double>(e.field) + doff, 1, dstr, dcnt});
+        } else {
+            const LBlock &sb = c->blocks[e.ks];
+            strip(sb.g, e.src, soff, scnt, sstr);
+            pack.push_back(Seg{sb.f<double>(e.field) + soff, peers.at(e.peer).send + e.buf_off, sstr, 1, scnt});
+        }
     }
     auto upload = [&](const std::vector<Seg> &v, Seg *&d, int &n) -> int {
         n = (int)v.size();
@@ -396,8 +428,8 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
         return OCN_OK;
     };
     RC(upload(local, plan.d_local, plan.n_local));
-    RC(upload(all_pack, plan.d_pack, plan.n_pack));
-    RC(upload(all_unpack, plan.d_unpack, plan.n_unpack));
+    RC(upload(pack, plan.d_pack, plan.n_pack));
+    RC(upload(unpack, plan.d_unpack, plan.n_unpack));
     return OCN_OK;
 }
 
@@ -784,6 +816,21 @@ static int init_state(ocn_ctx *c)
 
 }  // namespace ocn
 
+static void set_mask(ocn_ctx *c, const int32_t *mask)
+{
+    const ocn_basin *basin = &c->basin;
+    const size_t nxy = (size_t)basin->nx * basin->ny;
+    c->mask.assign(nxy, 0);
+    if (mask) {
+        std::memcpy(c->mask.data(), mask, nxy * sizeof(int32_t));
+    } else {   // tools/io.f90:49-59: closed box with a 2-cell land frame
+        for (int n = 1; n <= basin->ny; ++n)
+            for (int m = 1; m <= basin->nx; ++m)
+                c->mask[(size_t)(m - 1) + (size_t)(n - 1) * basin->nx] =
+                    (m < 3 || m > basin->nx - 2 || n < 3 || n > basin->ny - 2) ? 1 : 0;
+    }
+}
+
 // ================================================================== C ABI (PSy layer)
 extern "C" {
 
@@ -800,16 +847,7 @@ int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_de
     ocn_ctx *c = new ocn_ctx();
     c->basin = *basin; c->sw = *sw; c->dec = *dec;
     c->bnx = dec->bnx; c->bny = dec->bny;
-    const size_t nxy = (size_t)basin->nx * basin->ny;
-    c->mask.assign(nxy, 0);
-    if (mask) {
-        std::memcpy(c->mask.data(), mask, nxy * sizeof(int32_t));
-    } else {   // tools/io.f90:49-59: closed box with a 2-cell land frame
-        for (int n = 1; n <= basin->ny; ++n)
-            for (int m = 1; m <= basin->nx; ++m)
-                c->mask[(size_t)(m - 1) + (size_t)(n - 1) * basin->nx] =
-                    (m < 3 || m > basin->nx - 2 || n < 3 || n > basin->ny - 2) ? 1 : 0;
-    }
+    set_mask(c, mask);
     int rc = check_hip(hipSetDevice(dec->device), "hipSetDevice");
     if (!rc) rc = check_hip(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
     if (!rc) rc = decompose(c);
@@ -818,6 +856,62 @@ int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_de
     if (!rc) rc = check_hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     if (rc) { ocn_ctx_destroy(c); return rc; }
     *out = c;
+    return OCN_OK;
+}
+
+// host-only context (decomposition only, no device) for the query entry points
+static int host_ctx(const ocn_basin *basin, const ocn_decomp *dec, const int32_t *mask, ocn_ctx *&c)
+{
+    if (!basin || !dec) return set_error(OCN_ERR_ARG, "null argument");
+    if (basin->nx < 5 || basin->ny < 5) return set_error(OCN_ERR_ARG, "nx, ny must be >= 5");
+    if (dec->bnx < 1 || dec->bny < 1 || dec->nranks < 1 || dec->rank < 0 || dec->rank >= dec->nranks)
+        return set_error(OCN_ERR_ARG, "bad decomposition request");
+    c = new ocn_ctx();
+    c->basin = *basin; c->dec = *dec; c->bnx = dec->bnx; c->bny = dec->bny;
+    set_mask(c, mask);
+    const int rc = decompose(c);
+    if (rc) { delete c; c = nullptr; }
+    return rc;
+}
+
+int ocn_decompose(const ocn_basin *basin, const ocn_decomp *dec, const int32_t *mask, ocn_block_info *out,
+                  int32_t cap, int32_t *count)
+{
+    ocn_ctx *c = nullptr;
+    RC(host_ctx(basin, dec, mask, c));
+    const int n = (int)c->blocks.size();
+    if (count) *count = n;
+    for (int k = 0; k < n && k < cap && out; ++k) {
+        const LBlock &b = c->blocks[k];
+        out[k].geom = b.g; out[k].bm = b.bm; out[k].bn = b.bn;
+        for (int d = 0; d < 8; ++d) { out[k].nbr_rank[d] = b.nbr_rank[d]; out[k].nbr_k[d] = b.nbr_k[d]; }
+    }
+    delete c;
+    return OCN_OK;
+}
+
+int ocn_halo_schedule(const ocn_basin *basin, const ocn_decomp *dec, const int32_t *mask, const int32_t *field_ids,
+                      int32_t nfields, ocn_halo_msg *out, int32_t cap, int32_t *count)
+{
+    if (!field_ids || nfields < 1) return set_error(OCN_ERR_ARG, "no fields");
+    std::vector<int> fields(field_ids, field_ids + nfields);
+    for (int id : fields)
+        if (!is_r8(id)) return set_error(OCN_ERR_ARG, "halo exchange is defined for real(8) fields");
+    ocn_ctx *c = nullptr;
+    RC(host_ctx(basin, dec, mask, c));
+    std::vector<PlanEntry> es;
+    const int rc = plan_entries(c, fields, es);
+    delete c;
+    RC(rc);
+    if (count) *count = (int32_t)es.size();
+    for (size_t i = 0; i < es.size() && (int32_t)i < cap && out; ++i) {
+        const PlanEntry &e = es[i];
+        ocn_halo_msg &o = out[i];
+        o.kind = e.kind; o.peer = e.peer; o.k = e.k; o.k_src = e.ks; o.field = e.field;
+        o.dst_x0 = e.dst.x0; o.dst_x1 = e.dst.x1; o.dst_y0 = e.dst.y0; o.dst_y1 = e.dst.y1;
+        o.src_x0 = e.src.x0; o.src_x1 = e.src.x1; o.src_y0 = e.src.y0; o.src_y1 = e.src.y1;
+        o.offset = e.buf_off; o.count = e.count;
+    }
     return OCN_OK;
 }
 
