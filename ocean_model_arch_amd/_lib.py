@@ -10,7 +10,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libocn_sw.so")
+# OCN_LIB_PATH selects an alternative build (performance variants); default: the in-tree build.
+LIB_PATH = os.environ.get("OCN_LIB_PATH") or os.path.join(_HERE, "libocn_sw.so")
 _CSRC = os.path.join(_HERE, "csrc")
 
 OCN_OK, OCN_ERR_ARG, OCN_ERR_HIP, OCN_ERR_COMM, OCN_ERR_STATE, OCN_ERR_BLOWUP = range(6)

@@ -12,6 +12,11 @@
 #define OCN_ROWS 32
 #endif
 
+// Minimum waves per SIMD requested from the register allocator for the stencil kernels.
+#ifndef OCN_LB_WAVES
+#define OCN_LB_WAVES 1
+#endif
+
 // shared/constants.f90:23  FreeFallAcc = 9.8 (real(4))
 #define OCN_FREE_FALL_ACC 9.8f
 

@@ -11,6 +11,14 @@
 // 4 thread-rows march down the strip in steps of 4 so the n-1 / n+1 rows a thread needs
 // were just touched by its own workgroup (L1/L2 hits).  Each array is therefore streamed
 // from HBM about once per stage; the +-1 neighbours come from cache.
+//
+// Code shape for memory-level parallelism: every operand is loaded unconditionally (all
+// addresses are inside the block array), values are computed unconditionally, and only the
+// stores are predicated by the reference's masks.  Masks therefore never serialise a second
+// round of loads behind the mask load, and all loads of a cell can be in flight together.
+// Offsets are 32-bit element indices from a wave-uniform base (the kernel-argument pointer),
+// so loads use the SGPR-base + 32-bit VGPR-offset form instead of a 64-bit VGPR address
+// per array.
 #include <hip/hip_runtime.h>
 
 #include "ocn_internal.h"
@@ -19,7 +27,7 @@ namespace ocn {
 
 // ------------------------------------------------------------------ launch scaffolding
 template <typename Body>
-__global__ __launch_bounds__(256) void k_range(int m0, int m1, int n0, int n1, Body body)
+__global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range(int m0, int m1, int n0, int n1, Body body)
 {
     const int m = m0 + (int)blockIdx.x * 64 + (int)threadIdx.x;
     if (m > m1) return;
@@ -38,17 +46,43 @@ static int launch_range(int m0, int m1, int n0, int n1, const Body &body, hipStr
     return check_launch();
 }
 
+// Optional scheduling hint (OCN_SCHED_LOADS_FIRST): ask the LLVM scheduler to place the
+// cell's global loads ahead of its arithmetic, so a wave keeps all of them in flight.
+#ifdef OCN_SCHED_LOADS_FIRST
+#define OCN_LOADS_FIRST()                                                         \
+    do {                                                                          \
+        __builtin_amdgcn_sched_group_barrier(0x020, OCN_SCHED_LOADS_FIRST, 0);    \
+        __builtin_amdgcn_sched_group_barrier(0x002, 4000, 0);                     \
+    } while (0)
+#else
+#define OCN_LOADS_FIRST() do { } while (0)
+#endif
+
+// Element index of A(m, n) in a block array: 32-bit (the host checks pitch * rows < 2^31).
 struct Geo {
     int bx1, by1;
-    long p;
-    __device__ __forceinline__ long operator()(int m, int n) const
+    unsigned p;
+    __device__ __forceinline__ unsigned operator()(int m, int n) const
     {
-        return (long)(m - bx1) + (long)(n - by1) * p;
+        return (unsigned)(m - bx1) + (unsigned)(n - by1) * p;
     }
 };
-static inline Geo geo(const ocn_block *b) { return Geo{b->bnd_x1, b->bnd_y1, (long)b->pitch}; }
+static inline Geo geo(const ocn_block *b) { return Geo{b->bnd_x1, b->bnd_y1, (unsigned)b->pitch}; }
 
 #define D(x) ((double)(x))
+
+// Loads / stores through a 32-bit byte offset from the (wave-uniform) array base: the compiler
+// then emits the SGPR-base + 32-bit VGPR-offset global_load/store form (no 64-bit address
+// arithmetic per array).  Block arrays hold < 2^29 elements, so every r8 byte offset fits 32 bits (checked on the host).
+template <class T> __device__ __forceinline__ T ld(const T *__restrict__ p, unsigned i)
+{
+    return *(const T *)((const char *)p + i * (unsigned)sizeof(T));
+}
+template <class T> __device__ __forceinline__ void st(T *__restrict__ p, unsigned i, T v)
+{
+    *(T *)((char *)p + i * (unsigned)sizeof(T)) = v;
+}
+
 
 // ------------------------------------------------------------------ a1 sw_update_ssh
 // vel_ssh.f90:69-106
@@ -60,26 +94,43 @@ struct SwUpdateSsh {
     const double *__restrict__ sshp, *__restrict__ ubrtr, *__restrict__ vbrtr;
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        if (!(lu[c] > 0.5f)) return;
-        const long w = I(m - 1, n), s = I(m, n - 1);
-        const double t1 = ubrtr[c] * hhu[c] * D(dyh[c]);
-        const double t2 = ubrtr[w] * hhu[w] * D(dyh[w]);
-        const double t3 = vbrtr[c] * hhv[c] * D(dxh[c]);
-        const double t4 = vbrtr[s] * hhv[s] * D(dxh[s]);
-        const float area = dx[c] * dy[c];
+        const unsigned c = I(m, n), w = c - 1, s = c - I.p;
+        const double t1 = ld(ubrtr, c) * ld(hhu, c) * D(ld(dyh, c));
+        const double t2 = ld(ubrtr, w) * ld(hhu, w) * D(ld(dyh, w));
+        const double t3 = ld(vbrtr, c) * ld(hhv, c) * D(ld(dxh, c));
+        const double t4 = ld(vbrtr, s) * ld(hhv, s) * D(ld(dxh, s));
+        const float area = ld(dx, c) * ld(dy, c);
         const double div = (t1 - t2 + t3 - t4) / D(area);
-        sshn[c] = sshp[c] + 2.0 * tau * (-div);
+        const double r = ld(sshp, c) + 2.0 * tau * (-div);
+        if (ld(lu, c) > 0.5f) st(sshn, c, r);
     }
 };
 
 // ------------------------------------------------------------------ T->U/V/H interpolation
-// kernel/shallow_water/depth.f90:56-97; hq(m,n) = h_r + sh * f recomputed at each point
-// (the whole-array assignment precedes the loop in the reference, so every read sees it).
+// kernel/shallow_water/depth.f90:56-97 for one level given its values at the four corners
+// (m,n), (m+1,n), (m,n+1), (m+1,n+1).
 struct Interp {
-    Geo I;
     const float *__restrict__ lu, *__restrict__ dx, *__restrict__ dy;
-    __device__ __forceinline__ double wt(double h, long i) const { return h * D(dx[i]) * D(dy[i]) * D(lu[i]); }
+    const float *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxh, *__restrict__ dyh;
+    const float *__restrict__ dxb, *__restrict__ dyb;
+    // per-corner weights dx*dy*lu (products evaluated per use, as the reference does)
+    __device__ __forceinline__ double wt(double h, unsigned i) const { return h * D(ld(dx, i)) * D(ld(dy, i)) * D(ld(lu, i)); }
+    __device__ __forceinline__ double u(double h00, double h10, unsigned c, unsigned e) const
+    {
+        const double slu = D(ld(lu, c) + ld(lu, e));
+        return (wt(h00, c) + wt(h10, e)) / slu / D(ld(dxt, c)) / D(ld(dyh, c));
+    }
+    __device__ __forceinline__ double v(double h00, double h01, unsigned c, unsigned nn) const
+    {
+        const double slu = D(ld(lu, c) + ld(lu, nn));
+        return (wt(h00, c) + wt(h01, nn)) / slu / D(ld(dxh, c)) / D(ld(dyt, c));
+    }
+    __device__ __forceinline__ double h(double h00, double h10, double h01, double h11, unsigned c, unsigned e,
+                                        unsigned nn, unsigned ne) const
+    {
+        const double slu = D(ld(lu, c) + ld(lu, e) + ld(lu, nn) + ld(lu, ne));
+        return (wt(h00, c) + wt(h10, e) + wt(h01, nn) + wt(h11, ne)) / slu / D(ld(dxb, c)) / D(ld(dyb, c));
+    }
 };
 
 // ------------------------------------------------------------------ a2 hh_update
@@ -87,39 +138,29 @@ struct Interp {
 // interpolation part runs on [start-1, end]^2.
 struct HhUpdate {
     Geo I; int i0, i1, j0, j1;
-    const float *__restrict__ lu, *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
-    const float *__restrict__ dx, *__restrict__ dy, *__restrict__ dxt, *__restrict__ dyt;
-    const float *__restrict__ dxh, *__restrict__ dyh, *__restrict__ dxb, *__restrict__ dyb;
+    Interp W;
+    const float *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
     double *__restrict__ hqn, *__restrict__ hun, *__restrict__ hvn, *__restrict__ hhn;
     const double *__restrict__ sh, *__restrict__ h_r;
-    // the [start-1, end]^2 interpolation part (depth.f90:134-160)
-    __device__ __forceinline__ void interp(int m, int n, long c, double q00) const
+    // the [start-1, end]^2 interpolation part (depth.f90:134-160); q = h_r + sh at each corner
+    __device__ __forceinline__ void interp(unsigned c, double q00) const
     {
-        const long e = I(m + 1, n), nn = I(m, n + 1), ne = I(m + 1, n + 1);
-        const Interp W{I, lu, dx, dy};
-        if (llu[c] > 0.5f) {
-            const double slu = D(lu[c] + lu[e]);
-            const double q10 = h_r[e] + sh[e];
-            hun[c] = (W.wt(q00, c) + W.wt(q10, e)) / slu / D(dxt[c]) / D(dyh[c]);
-        }
-        if (llv[c] > 0.5f) {
-            const double slu = D(lu[c] + lu[nn]);
-            const double q01 = h_r[nn] + sh[nn];
-            hvn[c] = (W.wt(q00, c) + W.wt(q01, nn)) / slu / D(dxh[c]) / D(dyt[c]);
-        }
-        if (luh[c] > 0.5f) {
-            const double slu = D(lu[c] + lu[e] + lu[nn] + lu[ne]);
-            const double q10 = h_r[e] + sh[e], q01 = h_r[nn] + sh[nn], q11 = h_r[ne] + sh[ne];
-            hhn[c] = (W.wt(q00, c) + W.wt(q10, e) + W.wt(q01, nn) + W.wt(q11, ne)) / slu / D(dxb[c]) / D(dyb[c]);
-        }
+        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1;
+        const double q10 = ld(h_r, e) + ld(sh, e), q01 = ld(h_r, nn) + ld(sh, nn), q11 = ld(h_r, ne) + ld(sh, ne);
+        const double xu = W.u(q00, q10, c, e);
+        const double xv = W.v(q00, q01, c, nn);
+        const double xh = W.h(q00, q10, q01, q11, c, e, nn, ne);
+        if (ld(llu, c) > 0.5f) st(hun, c, xu);
+        if (ld(llv, c) > 0.5f) st(hvn, c, xv);
+        if (ld(luh, c) > 0.5f) st(hhn, c, xh);
     }
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        const double q00 = h_r[c] + sh[c];
-        hqn[c] = q00;
+        const unsigned c = I(m, n);
+        const double q00 = ld(h_r, c) + ld(sh, c);
+        st(hqn, c, q00);
         if (m < i0 || m > i1 || n < j0 || n > j1) return;
-        interp(m, n, c, q00);
+        interp(c, q00);
     }
 };
 
@@ -128,9 +169,8 @@ struct HhUpdate {
 // three levels interpolated on [start-1, end]^2.
 struct HhInit {
     Geo I; int i0, i1, j0, j1; double f;
-    const float *__restrict__ lu, *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
-    const float *__restrict__ dx, *__restrict__ dy, *__restrict__ dxt, *__restrict__ dyt;
-    const float *__restrict__ dxh, *__restrict__ dyh, *__restrict__ dxb, *__restrict__ dyb;
+    Interp W;
+    const float *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
     double *__restrict__ hq, *__restrict__ hqp, *__restrict__ hqn;
     double *__restrict__ hu, *__restrict__ hup, *__restrict__ hun;
     double *__restrict__ hv, *__restrict__ hvp, *__restrict__ hvn;
@@ -138,42 +178,23 @@ struct HhInit {
     const double *__restrict__ sh, *__restrict__ shp, *__restrict__ h_r;
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        const double r00 = h_r[c];
-        const double a00 = r00 + sh[c] * f, b00 = r00 + shp[c] * f;
-        hq[c] = a00; hqp[c] = b00; hqn[c] = r00;
+        OCN_LOADS_FIRST();
+        const unsigned c = I(m, n);
+        const double r00 = ld(h_r, c);
+        const double a00 = r00 + ld(sh, c) * f, b00 = r00 + ld(shp, c) * f;
+        st(hq, c, a00); st(hqp, c, b00); st(hqn, c, r00);
         if (m < i0 || m > i1 || n < j0 || n > j1) return;
-        const long e = I(m + 1, n), nn = I(m, n + 1), ne = I(m + 1, n + 1);
-        const Interp W{I, lu, dx, dy};
-        const bool bu = llu[c] > 0.5f, bv = llv[c] > 0.5f, bh = luh[c] > 0.5f;
-        if (bu) {
-            const double slu = D(lu[c] + lu[e]);
-            const double r10 = h_r[e];
-            const double a10 = r10 + sh[e] * f, b10 = r10 + shp[e] * f;
-            const double x = D(dxt[c]), y = D(dyh[c]);
-            hu[c] = (W.wt(a00, c) + W.wt(a10, e)) / slu / x / y;
-            hup[c] = (W.wt(b00, c) + W.wt(b10, e)) / slu / x / y;
-            hun[c] = (W.wt(r00, c) + W.wt(r10, e)) / slu / x / y;
-        }
-        if (bv) {
-            const double slu = D(lu[c] + lu[nn]);
-            const double r01 = h_r[nn];
-            const double a01 = r01 + sh[nn] * f, b01 = r01 + shp[nn] * f;
-            const double x = D(dxh[c]), y = D(dyt[c]);
-            hv[c] = (W.wt(a00, c) + W.wt(a01, nn)) / slu / x / y;
-            hvp[c] = (W.wt(b00, c) + W.wt(b01, nn)) / slu / x / y;
-            hvn[c] = (W.wt(r00, c) + W.wt(r01, nn)) / slu / x / y;
-        }
-        if (bh) {
-            const double slu = D(lu[c] + lu[e] + lu[nn] + lu[ne]);
-            const double r10 = h_r[e], r01 = h_r[nn], r11 = h_r[ne];
-            const double a10 = r10 + sh[e] * f, a01 = r01 + sh[nn] * f, a11 = r11 + sh[ne] * f;
-            const double b10 = r10 + shp[e] * f, b01 = r01 + shp[nn] * f, b11 = r11 + shp[ne] * f;
-            const double x = D(dxb[c]), y = D(dyb[c]);
-            hh[c] = (W.wt(a00, c) + W.wt(a10, e) + W.wt(a01, nn) + W.wt(a11, ne)) / slu / x / y;
-            hhp[c] = (W.wt(b00, c) + W.wt(b10, e) + W.wt(b01, nn) + W.wt(b11, ne)) / slu / x / y;
-            hhn[c] = (W.wt(r00, c) + W.wt(r10, e) + W.wt(r01, nn) + W.wt(r11, ne)) / slu / x / y;
-        }
+        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1;
+        const double r10 = ld(h_r, e), r01 = ld(h_r, nn), r11 = ld(h_r, ne);
+        const double a10 = r10 + ld(sh, e) * f, a01 = r01 + ld(sh, nn) * f, a11 = r11 + ld(sh, ne) * f;
+        const double b10 = r10 + ld(shp, e) * f, b01 = r01 + ld(shp, nn) * f, b11 = r11 + ld(shp, ne) * f;
+        const double u0 = W.u(a00, a10, c, e), u1 = W.u(b00, b10, c, e), u2 = W.u(r00, r10, c, e);
+        const double v0 = W.v(a00, a01, c, nn), v1 = W.v(b00, b01, c, nn), v2 = W.v(r00, r01, c, nn);
+        const double h0 = W.h(a00, a10, a01, a11, c, e, nn, ne), h1 = W.h(b00, b10, b01, b11, c, e, nn, ne),
+                     h2 = W.h(r00, r10, r01, r11, c, e, nn, ne);
+        if (ld(llu, c) > 0.5f) { st(hu, c, u0); st(hup, c, u1); st(hun, c, u2); }
+        if (ld(llv, c) > 0.5f) { st(hv, c, v0); st(hvp, c, v1); st(hvn, c, v2); }
+        if (ld(luh, c) > 0.5f) { st(hh, c, h0); st(hhp, c, h1); st(hhn, c, h2); }
     }
 };
 
@@ -186,13 +207,12 @@ struct UvTransVort {
     double *__restrict__ vort;
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        if (!(luu[c] > 0.5f)) return;
-        const long e = I(m + 1, n), nn = I(m, n + 1);
-        const double a = v[e] * D(dyt[e]) - v[c] * D(dyt[c]);
-        const double b = u[nn] * D(dxt[nn]) - u[c] * D(dxt[c]);
-        const double d = (v[e] - v[c]) * D(dyb[c]) - (u[nn] - u[c]) * D(dxb[c]);
-        vort[c] = a - b - d;
+        const unsigned c = I(m, n), e = c + 1, nn = c + I.p;
+        const double a = ld(v, e) * D(ld(dyt, e)) - ld(v, c) * D(ld(dyt, c));
+        const double b = ld(u, nn) * D(ld(dxt, nn)) - ld(u, c) * D(ld(dxt, c));
+        const double d = (ld(v, e) - ld(v, c)) * D(ld(dyb, c)) - (ld(u, nn) - ld(u, c)) * D(ld(dxb, c));
+        const double r = a - b - d;
+        if (ld(luu, c) > 0.5f) st(vort, c, r);
     }
 };
 
@@ -204,43 +224,39 @@ struct UvTrans {
     const double *__restrict__ u, *__restrict__ v, *__restrict__ vort;
     const double *__restrict__ hu, *__restrict__ hv, *__restrict__ hh;
     double *__restrict__ RHSx, *__restrict__ RHSy;
-    __device__ __forceinline__ void eval(int m, int n, long c, bool bu, bool bv, double &rx, double &ry) const
+    __device__ __forceinline__ void eval(unsigned c, double &rx, double &ry) const
     {
-        const long e = I(m + 1, n), w = I(m - 1, n), nn = I(m, n + 1), s = I(m, n - 1);
-        if (bu) {
-            const long se = I(m + 1, n - 1);
-            const double fu_c = u[c] * D(dyh[c]) * hu[c];
-            const double fx_p = (fu_c + u[e] * D(dyh[e]) * hu[e]) / 2.0 * (u[c] + u[e]) / 2.0;
-            const double fx_m = (fu_c + u[w] * D(dyh[w]) * hu[w]) / 2.0 * (u[c] + u[w]) / 2.0;
-            const double fy_p = (v[c] * D(dxh[c]) * hv[c] + v[e] * D(dxh[e]) * hv[e]) / 2.0
-                                * (u[nn] + u[c]) / 2.0 * D(luu[c]);
-            const double fy_m = (v[s] * D(dxh[s]) * hv[s] + v[se] * D(dxh[se]) * hv[se]) / 2.0
-                                * (u[s] + u[c]) / 2.0 * D(luu[s]);
+        const unsigned e = c + 1, w = c - 1, nn = c + I.p, s = c - I.p, se = s + 1, wn = nn - 1;
+        {
+            const double fu_c = ld(u, c) * D(ld(dyh, c)) * ld(hu, c);
+            const double fx_p = (fu_c + ld(u, e) * D(ld(dyh, e)) * ld(hu, e)) / 2.0 * (ld(u, c) + ld(u, e)) / 2.0;
+            const double fx_m = (fu_c + ld(u, w) * D(ld(dyh, w)) * ld(hu, w)) / 2.0 * (ld(u, c) + ld(u, w)) / 2.0;
+            const double fy_p = (ld(v, c) * D(ld(dxh, c)) * ld(hv, c) + ld(v, e) * D(ld(dxh, e)) * ld(hv, e)) / 2.0
+                                * (ld(u, nn) + ld(u, c)) / 2.0 * D(ld(luu, c));
+            const double fy_m = (ld(v, s) * D(ld(dxh, s)) * ld(hv, s) + ld(v, se) * D(ld(dxh, se)) * ld(hv, se)) / 2.0
+                                * (ld(u, s) + ld(u, c)) / 2.0 * D(ld(luu, s));
             rx = -(fx_p - fx_m + fy_p - fy_m)
-                 + (vort[c] * hh[c] * (v[e] + v[c]) + vort[s] * hh[s] * (v[se] + v[s])) / 4.0;
+                 + (ld(vort, c) * ld(hh, c) * (ld(v, e) + ld(v, c)) + ld(vort, s) * ld(hh, s) * (ld(v, se) + ld(v, s))) / 4.0;
         }
-        if (bv) {
-            const long wn = I(m - 1, n + 1);
-            const double fv_c = v[c] * D(dxh[c]) * hv[c];
-            const double fy_p = (fv_c + v[nn] * D(dxh[nn]) * hv[nn]) / 2.0 * (v[c] + v[nn]) / 2.0;
-            const double fy_m = (fv_c + v[s] * D(dxh[s]) * hv[s]) / 2.0 * (v[c] + v[s]) / 2.0;
-            const double fx_p = (u[c] * D(dyh[c]) * hu[c] + u[nn] * D(dyh[nn]) * hu[nn]) / 2.0
-                                * (v[e] + v[c]) / 2.0;
-            const double fx_m = (u[w] * D(dyh[w]) * hu[w] + u[wn] * D(dyh[wn]) * hu[wn]) / 2.0
-                                * (v[w] + v[c]) / 2.0;
+        {
+            const double fv_c = ld(v, c) * D(ld(dxh, c)) * ld(hv, c);
+            const double fy_p = (fv_c + ld(v, nn) * D(ld(dxh, nn)) * ld(hv, nn)) / 2.0 * (ld(v, c) + ld(v, nn)) / 2.0;
+            const double fy_m = (fv_c + ld(v, s) * D(ld(dxh, s)) * ld(hv, s)) / 2.0 * (ld(v, c) + ld(v, s)) / 2.0;
+            const double fx_p = (ld(u, c) * D(ld(dyh, c)) * ld(hu, c) + ld(u, nn) * D(ld(dyh, nn)) * ld(hu, nn)) / 2.0
+                                * (ld(v, e) + ld(v, c)) / 2.0;
+            const double fx_m = (ld(u, w) * D(ld(dyh, w)) * ld(hu, w) + ld(u, wn) * D(ld(dyh, wn)) * ld(hu, wn)) / 2.0
+                                * (ld(v, w) + ld(v, c)) / 2.0;
             ry = -(fx_p - fx_m + fy_p - fy_m)
-                 - (vort[c] * hh[c] * (u[nn] + u[c]) + vort[w] * hh[w] * (u[wn] + u[w])) / 4.0;
+                 - (ld(vort, c) * ld(hh, c) * (ld(u, nn) + ld(u, c)) + ld(vort, w) * ld(hh, w) * (ld(u, wn) + ld(u, w))) / 4.0;
         }
     }
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
-        if (!bu && !bv) return;
-        double rx = 0.0, ry = 0.0;
-        eval(m, n, c, bu, bv, rx, ry);
-        if (bu) RHSx[c] = rx;
-        if (bv) RHSy[c] = ry;
+        const unsigned c = I(m, n);
+        double rx, ry;
+        eval(c, rx, ry);
+        if (ld(lcu, c) > 0.5f) st(RHSx, c, rx);
+        if (ld(lcv, c) > 0.5f) st(RHSy, c, ry);
     }
 };
 
@@ -255,21 +271,17 @@ struct StressComponents {
     double *__restrict__ str_t, *__restrict__ str_s;
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        if (lu[c] > 0.5f) {
-            const long w = I(m - 1, n), s = I(m, n - 1);
-            const float r1 = dy[c] / dx[c];
-            const float r2 = dx[c] / dy[c];
-            str_t[c] = D(r1) * (u[c] / D(dyh[c]) - u[w] / D(dyh[w]))
-                       - D(r2) * (v[c] / D(dxh[c]) - v[s] / D(dxh[s]));
-        }
-        if (luu[c] > 0.5f) {
-            const long e = I(m + 1, n), nn = I(m, n + 1);
-            const float r1 = dxb[c] / dyb[c];
-            const float r2 = dyb[c] / dxb[c];
-            str_s[c] = D(r1) * (u[nn] / D(dxt[nn]) - u[c] / D(dxt[c]))
-                       + D(r2) * (v[e] / D(dyt[e]) - v[c] / D(dyt[c]));
-        }
+        const unsigned c = I(m, n), w = c - 1, s = c - I.p, e = c + 1, nn = c + I.p;
+        const float r1 = ld(dy, c) / ld(dx, c);
+        const float r2 = ld(dx, c) / ld(dy, c);
+        const double vt = D(r1) * (ld(u, c) / D(ld(dyh, c)) - ld(u, w) / D(ld(dyh, w)))
+                          - D(r2) * (ld(v, c) / D(ld(dxh, c)) - ld(v, s) / D(ld(dxh, s)));
+        const float q1 = ld(dxb, c) / ld(dyb, c);
+        const float q2 = ld(dyb, c) / ld(dxb, c);
+        const double vs = D(q1) * (ld(u, nn) / D(ld(dxt, nn)) - ld(u, c) / D(ld(dxt, c)))
+                          + D(q2) * (ld(v, e) / D(ld(dyt, e)) - ld(v, c) / D(ld(dyt, c)));
+        if (ld(lu, c) > 0.5f) st(str_t, c, vt);
+        if (ld(luu, c) > 0.5f) st(str_s, c, vs);
     }
 };
 
@@ -282,37 +294,33 @@ struct UvDiff2 {
     const float *__restrict__ dxb, *__restrict__ dyb;
     const double *__restrict__ mu, *__restrict__ str_t, *__restrict__ str_s, *__restrict__ hq, *__restrict__ hh;
     double *__restrict__ RHSx, *__restrict__ RHSy;
-    __device__ __forceinline__ void eval(int m, int n, long c, bool bu, bool bv, double &rx, double &ry) const
+    __device__ __forceinline__ void eval(unsigned c, double &rx, double &ry) const
     {
-        const long e = I(m + 1, n), nn = I(m, n + 1), ne = I(m + 1, n + 1);
-        if (bu) {
-            const long s = I(m, n - 1), se = I(m + 1, n - 1);
-            const double muh_p = (mu[c] + mu[e] + mu[nn] + mu[ne]) / 4.0;
-            const double muh_m = (mu[c] + mu[e] + mu[s] + mu[se]) / 4.0;
-            const float dy2p = dy[e] * dy[e], dy2 = dy[c] * dy[c];
-            const float dxb2 = dxb[c] * dxb[c], dxb2m = dxb[s] * dxb[s];
-            rx = (D(dy2p) * mu[e] * hq[e] * str_t[e] - D(dy2) * mu[c] * hq[c] * str_t[c]) / D(dyh[c])
-                 + (D(dxb2) * muh_p * hh[c] * str_s[c] - D(dxb2m) * muh_m * hh[s] * str_s[s]) / D(dxt[c]);
+        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1, s = c - I.p, se = s + 1, w = c - 1, wn = nn - 1;
+        {
+            const double muh_p = (ld(mu, c) + ld(mu, e) + ld(mu, nn) + ld(mu, ne)) / 4.0;
+            const double muh_m = (ld(mu, c) + ld(mu, e) + ld(mu, s) + ld(mu, se)) / 4.0;
+            const float dy2p = ld(dy, e) * ld(dy, e), dy2 = ld(dy, c) * ld(dy, c);
+            const float dxb2 = ld(dxb, c) * ld(dxb, c), dxb2m = ld(dxb, s) * ld(dxb, s);
+            rx = (D(dy2p) * ld(mu, e) * ld(hq, e) * ld(str_t, e) - D(dy2) * ld(mu, c) * ld(hq, c) * ld(str_t, c)) / D(ld(dyh, c))
+                 + (D(dxb2) * muh_p * ld(hh, c) * ld(str_s, c) - D(dxb2m) * muh_m * ld(hh, s) * ld(str_s, s)) / D(ld(dxt, c));
         }
-        if (bv) {
-            const long w = I(m - 1, n), wn = I(m - 1, n + 1);
-            const double muh_p = (mu[c] + mu[e] + mu[nn] + mu[ne]) / 4.0;
-            const double muh_m = (mu[c] + mu[w] + mu[nn] + mu[wn]) / 4.0;
-            const float dx2p = dx[nn] * dx[nn], dx2 = dx[c] * dx[c];
-            const float dyb2 = dyb[c] * dyb[c], dyb2m = dyb[w] * dyb[w];
-            ry = -(D(dx2p) * mu[nn] * hq[nn] * str_t[nn] - D(dx2) * mu[c] * hq[c] * str_t[c]) / D(dxh[c])
-                 + (D(dyb2) * muh_p * hh[c] * str_s[c] - D(dyb2m) * muh_m * hh[w] * str_s[w]) / D(dyt[c]);
+        {
+            const double muh_p = (ld(mu, c) + ld(mu, e) + ld(mu, nn) + ld(mu, ne)) / 4.0;
+            const double muh_m = (ld(mu, c) + ld(mu, w) + ld(mu, nn) + ld(mu, wn)) / 4.0;
+            const float dx2p = ld(dx, nn) * ld(dx, nn), dx2 = ld(dx, c) * ld(dx, c);
+            const float dyb2 = ld(dyb, c) * ld(dyb, c), dyb2m = ld(dyb, w) * ld(dyb, w);
+            ry = -(D(dx2p) * ld(mu, nn) * ld(hq, nn) * ld(str_t, nn) - D(dx2) * ld(mu, c) * ld(hq, c) * ld(str_t, c)) / D(ld(dxh, c))
+                 + (D(dyb2) * muh_p * ld(hh, c) * ld(str_s, c) - D(dyb2m) * muh_m * ld(hh, w) * ld(str_s, w)) / D(ld(dyt, c));
         }
     }
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
-        if (!bu && !bv) return;
-        double rx = 0.0, ry = 0.0;
-        eval(m, n, c, bu, bv, rx, ry);
-        if (bu) RHSx[c] = rx;
-        if (bv) RHSy[c] = ry;
+        const unsigned c = I(m, n);
+        double rx, ry;
+        eval(c, rx, ry);
+        if (ld(lcu, c) > 0.5f) st(RHSx, c, rx);
+        if (ld(lcv, c) > 0.5f) st(RHSy, c, ry);
     }
 };
 
@@ -330,45 +338,46 @@ struct SwUpdateUv {
     const float *__restrict__ rdis, *__restrict__ rlh_s;
     const double *__restrict__ RHSx, *__restrict__ RHSy, *__restrict__ RHSx_adv, *__restrict__ RHSy_adv;
     const double *__restrict__ RHSx_dif, *__restrict__ RHSy_dif;
-    // rxa/rxd/rya/ryd: RHSx_adv, RHSx_dif, RHSy_adv, RHSy_dif at this point (used under lcu / lcv)
-    __device__ __forceinline__ void eval(int m, int n, long c, bool bu, bool bv, double rxa, double rxd,
-                                         double rya, double ryd) const
+    // rxa/rxd/rya/ryd: RHSx_adv, RHSx_dif, RHSy_adv, RHSy_dif at this point
+    __device__ __forceinline__ void eval(unsigned c, double rxa, double rxd, double rya, double ryd, double &un,
+                                         double &vn) const
     {
         const double g = D(OCN_FREE_FALL_ACC);
-        if (bu) {
-            const long e = I(m + 1, n), s = I(m, n - 1), se = I(m + 1, n - 1);
-            const double bp = hhun[c] * D(dxt[c]) * D(dyh[c]) / 2.0 / tau;
-            const double bp0 = hhup[c] * D(dxt[c]) * D(dyh[c]) / 2.0 / tau;
-            const double slx = -(g * (ssh[e] - ssh[c]) * D(dyh[c]) * hhu[c]);
-            const float rd = rdis[c] + rdis[e];
-            const double fric = D(rd) / 2.0 * ubrtrp[c] * D(dxt[c]) * D(dyh[c]) * hhu[c];
-            const double c1 = D(rlh_s[c]) * hhh[c] * D(dxb[c]) * D(dyb[c]) * (vbrtr[e] + vbrtr[c]);
-            const double c2 = D(rlh_s[s]) * hhh[s] * D(dxb[s]) * D(dyb[s]) * (vbrtr[se] + vbrtr[s]);
-            const double grx = RHSx[c] + slx + rxd + rxa - fric + (c1 + c2) / 4.0;
-            ubrtrn[c] = (ubrtrp[c] * bp0 + grx) / (bp);
+        const unsigned e = c + 1, s = c - I.p, se = s + 1, nn = c + I.p, w = c - 1, wn = nn - 1;
+        {
+            const double bp = ld(hhun, c) * D(ld(dxt, c)) * D(ld(dyh, c)) / 2.0 / tau;
+            const double bp0 = ld(hhup, c) * D(ld(dxt, c)) * D(ld(dyh, c)) / 2.0 / tau;
+            const double slx = -(g * (ld(ssh, e) - ld(ssh, c)) * D(ld(dyh, c)) * ld(hhu, c));
+            const float rd = ld(rdis, c) + ld(rdis, e);
+            const double fric = D(rd) / 2.0 * ld(ubrtrp, c) * D(ld(dxt, c)) * D(ld(dyh, c)) * ld(hhu, c);
+            const double c1 = D(ld(rlh_s, c)) * ld(hhh, c) * D(ld(dxb, c)) * D(ld(dyb, c)) * (ld(vbrtr, e) + ld(vbrtr, c));
+            const double c2 = D(ld(rlh_s, s)) * ld(hhh, s) * D(ld(dxb, s)) * D(ld(dyb, s)) * (ld(vbrtr, se) + ld(vbrtr, s));
+            const double grx = ld(RHSx, c) + slx + rxd + rxa - fric + (c1 + c2) / 4.0;
+            un = (ld(ubrtrp, c) * bp0 + grx) / (bp);
         }
-        if (bv) {
-            const long nn = I(m, n + 1), w = I(m - 1, n), wn = I(m - 1, n + 1);
-            const double bp = hhvn[c] * D(dyt[c]) * D(dxh[c]) / 2.0 / tau;
-            const double bp0 = hhvp[c] * D(dyt[c]) * D(dxh[c]) / 2.0 / tau;
-            const double sly = -(g * (ssh[nn] - ssh[c]) * D(dxh[c]) * hhv[c]);
-            const float rd = rdis[c] + rdis[nn];
-            const double fric = D(rd) / 2.0 * vbrtrp[c] * D(dxh[c]) * D(dyt[c]) * hhv[c];
-            const double c1 = D(rlh_s[c]) * hhh[c] * D(dxb[c]) * D(dyb[c]) * (ubrtr[nn] + ubrtr[c]);
-            const double c2 = D(rlh_s[w]) * hhh[w] * D(dxb[w]) * D(dyb[w]) * (ubrtr[wn] + ubrtr[w]);
-            const double gry = RHSy[c] + sly + ryd + rya - fric - (c1 + c2) / 4.0;
-            vbrtrn[c] = (vbrtrp[c] * bp0 + gry) / (bp);
+        {
+            const double bp = ld(hhvn, c) * D(ld(dyt, c)) * D(ld(dxh, c)) / 2.0 / tau;
+            const double bp0 = ld(hhvp, c) * D(ld(dyt, c)) * D(ld(dxh, c)) / 2.0 / tau;
+            const double sly = -(g * (ld(ssh, nn) - ld(ssh, c)) * D(ld(dxh, c)) * ld(hhv, c));
+            const float rd = ld(rdis, c) + ld(rdis, nn);
+            const double fric = D(rd) / 2.0 * ld(vbrtrp, c) * D(ld(dxh, c)) * D(ld(dyt, c)) * ld(hhv, c);
+            const double c1 = D(ld(rlh_s, c)) * ld(hhh, c) * D(ld(dxb, c)) * D(ld(dyb, c)) * (ld(ubrtr, nn) + ld(ubrtr, c));
+            const double c2 = D(ld(rlh_s, w)) * ld(hhh, w) * D(ld(dxb, w)) * D(ld(dyb, w)) * (ld(ubrtr, wn) + ld(ubrtr, w));
+            const double gry = ld(RHSy, c) + sly + ryd + rya - fric - (c1 + c2) / 4.0;
+            vn = (ld(vbrtrp, c) * bp0 + gry) / (bp);
         }
+    }
+    __device__ __forceinline__ void store(unsigned c, double un, double vn) const
+    {
+        if (ld(lcu, c) > 0.5f) st(ubrtrn, c, un);
+        if (ld(lcv, c) > 0.5f) st(vbrtrn, c, vn);
     }
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        const bool bu = lcu[c] > 0.5f, bv = lcv[c] > 0.5f;
-        if (!bu && !bv) return;
-        double rxa = 0.0, rxd = 0.0, rya = 0.0, ryd = 0.0;
-        if (bu) { rxa = RHSx_adv[c]; rxd = RHSx_dif[c]; }
-        if (bv) { rya = RHSy_adv[c]; ryd = RHSy_dif[c]; }
-        eval(m, n, c, bu, bv, rxa, rxd, rya, ryd);
+        const unsigned c = I(m, n);
+        double un, vn;
+        eval(c, ld(RHSx_adv, c), ld(RHSx_dif, c), ld(RHSy_adv, c), ld(RHSy_dif, c), un, vn);
+        store(c, un, vn);
     }
 };
 
@@ -380,25 +389,22 @@ struct SwNextStep {
     double *__restrict__ ssh, *__restrict__ sshn, *__restrict__ sshp;
     double *__restrict__ u, *__restrict__ un, *__restrict__ up;
     double *__restrict__ v, *__restrict__ vn, *__restrict__ vp;
-    __device__ void operator()(int m, int n) const
+    // returns the ssh value after the update (for check_ssh_err)
+    __device__ __forceinline__ double step(unsigned i) const
     {
-        const long i = I(m, n);
-        if (lu[i] > 0.5f) {
-            const double x = ssh[i], xn = sshn[i];
-            sshp[i] = x + ts * (xn - 2.0 * x + sshp[i]) / 2.0;
-            ssh[i] = xn;
-        }
-        if (lcu[i] > 0.5f) {
-            const double x = u[i], xn = un[i];
-            up[i] = x + ts * (xn - 2.0 * x + up[i]) / 2.0;
-            u[i] = xn;
-        }
-        if (lcv[i] > 0.5f) {
-            const double x = v[i], xn = vn[i];
-            vp[i] = x + ts * (xn - 2.0 * x + vp[i]) / 2.0;
-            v[i] = xn;
-        }
+        const double x = ld(ssh, i), xn = ld(sshn, i), xp = ld(sshp, i);
+        const double a = ld(u, i), an = ld(un, i), ap = ld(up, i);
+        const double b = ld(v, i), bn = ld(vn, i), bp = ld(vp, i);
+        const double fx = x + ts * (xn - 2.0 * x + xp) / 2.0;
+        const double fa = a + ts * (an - 2.0 * a + ap) / 2.0;
+        const double fb = b + ts * (bn - 2.0 * b + bp) / 2.0;
+        const bool bl = ld(lu, i) > 0.5f;
+        if (bl) { st(sshp, i, fx); st(ssh, i, xn); }
+        if (ld(lcu, i) > 0.5f) { st(up, i, fa); st(u, i, an); }
+        if (ld(lcv, i) > 0.5f) { st(vp, i, fb); st(v, i, bn); }
+        return bl ? xn : x;
     }
+    __device__ void operator()(int m, int n) const { (void)step(I(m, n)); }
 };
 
 // ------------------------------------------------------------------ a9 hh_shift
@@ -410,36 +416,34 @@ struct HhShift {
     double *__restrict__ hu, *__restrict__ hup, *__restrict__ hun;
     double *__restrict__ hv, *__restrict__ hvp, *__restrict__ hvn;
     double *__restrict__ hh, *__restrict__ hhp, *__restrict__ hhn;
-    __device__ static __forceinline__ void shift(double *x, double *xp, const double *xn, long i, double ts)
+    __device__ static __forceinline__ void shift(bool mask, double *x, double *xp, const double *xn, unsigned i,
+                                                 double ts)
     {
-        const double a = x[i], an = xn[i];
-        xp[i] = a + ts * (an - 2.0 * a + xp[i]) / 2.0;
-        x[i] = an;
+        const double a = ld(x, i), an = ld(xn, i), ap = ld(xp, i);
+        const double f = a + ts * (an - 2.0 * a + ap) / 2.0;
+        if (mask) { st(xp, i, f); st(x, i, an); }
     }
     __device__ void operator()(int m, int n) const
     {
-        const long i = I(m, n);
-        if (llu[i] > 0.5f) shift(hu, hup, hun, i, ts);
-        if (llv[i] > 0.5f) shift(hv, hvp, hvn, i, ts);
-        if (lu[i] > 0.5f) shift(hq, hqp, hqn, i, ts);
-        if (luh[i] > 0.5f) shift(hh, hhp, hhn, i, ts);
+        const unsigned i = I(m, n);
+        shift(ld(llu, i) > 0.5f, hu, hup, hun, i, ts);
+        shift(ld(llv, i) > 0.5f, hv, hvp, hvn, i, ts);
+        shift(ld(lu, i) > 0.5f, hq, hqp, hqn, i, ts);
+        shift(ld(luh, i) > 0.5f, hh, hhp, hhn, i, ts);
     }
 };
 
 // ------------------------------------------------------------------ check_ssh_err
-// vel_ssh.f90:40-67 as a device reduction (one atomic per wave with bad points).
+// vel_ssh.f90:40-67 as a device reduction (one atomic per thread with a bad point; the
+// count only needs to be non-zero).
 struct CheckSshErr {
     Geo I;
     const float *__restrict__ lu; const double *__restrict__ ssh; int *nbad;
     __device__ void operator()(int m, int n) const
     {
-        const long c = I(m, n);
-        bool bad = false;
-        if (lu[c] > 0.5f) {
-            const double s = ssh[c];
-            bad = !(s < 10000.0 && s > -10000.0);
-        }
-        if (bad) atomicAdd(nbad, 1);
+        const unsigned c = I(m, n);
+        const double s = ld(ssh, c);
+        if (ld(lu, c) > 0.5f && !(s < 10000.0 && s > -10000.0)) atomicAdd(nbad, 1);
     }
 };
 
@@ -462,14 +466,15 @@ struct FusedA {
     SwUpdateSsh a1; HhUpdate a2; UvTransVort a3; StressComponents a5;
     __device__ void operator()(int m, int n) const
     {
+        OCN_LOADS_FIRST();
         if (m >= sx && n >= sy) {
             a1(m, n);
             if (do_vort) a3(m, n);
             if (do_stress) a5(m, n);
         }
         if (do_hh) {
-            const long c = a2.I(m, n);
-            a2.interp(m, n, c, a2.h_r[c] + a2.sh[c]);
+            const unsigned c = a2.I(m, n);
+            a2.interp(c, ld(a2.h_r, c) + ld(a2.sh, c));
         }
     }
 };
@@ -479,27 +484,26 @@ struct FusedB {
     UvTrans a4; UvDiff2 a6; SwUpdateUv a7;
     __device__ void operator()(int m, int n) const
     {
-        const long c = a7.I(m, n);
-        const bool bu = a7.lcu[c] > 0.5f, bv = a7.lcv[c] > 0.5f;
-        if (!bu && !bv) return;
-        double rxa = 0.0, rya = 0.0, rxd = 0.0, ryd = 0.0;
-        if (do_adv) {
-            a4.eval(m, n, c, bu, bv, rxa, rya);
-            if (bu) a4.RHSx[c] = rxa;
-            if (bv) a4.RHSy[c] = rya;
-        } else {
-            if (bu) rxa = a7.RHSx_adv[c];
-            if (bv) rya = a7.RHSy_adv[c];
+        OCN_LOADS_FIRST();
+        const unsigned c = a7.I(m, n);
+        double rxa, rya, rxd, ryd;
+        if (do_adv) a4.eval(c, rxa, rya);
+        else { rxa = ld(a7.RHSx_adv, c); rya = ld(a7.RHSy_adv, c); }
+        if (do_dif) a6.eval(c, rxd, ryd);
+        else { rxd = ld(a7.RHSx_dif, c); ryd = ld(a7.RHSy_dif, c); }
+        double un, vn;
+        a7.eval(c, rxa, rxd, rya, ryd, un, vn);
+        const bool bu = ld(a7.lcu, c) > 0.5f, bv = ld(a7.lcv, c) > 0.5f;
+        if (bu) {
+            if (do_adv) st(a4.RHSx, c, rxa);
+            if (do_dif) st(a6.RHSx, c, rxd);
+            st(a7.ubrtrn, c, un);
         }
-        if (do_dif) {
-            a6.eval(m, n, c, bu, bv, rxd, ryd);
-            if (bu) a6.RHSx[c] = rxd;
-            if (bv) a6.RHSy[c] = ryd;
-        } else {
-            if (bu) rxd = a7.RHSx_dif[c];
-            if (bv) ryd = a7.RHSy_dif[c];
+        if (bv) {
+            if (do_adv) st(a4.RHSy, c, rya);
+            if (do_dif) st(a6.RHSy, c, ryd);
+            st(a7.vbrtrn, c, vn);
         }
-        a7.eval(m, n, c, bu, bv, rxa, rxd, rya, ryd);
     }
 };
 
@@ -510,15 +514,11 @@ struct FusedC1 {
     SwNextStep a8; HhShift a9;
     __device__ void operator()(int m, int n) const
     {
-        a8(m, n);
+        const unsigned c = a8.I(m, n);
+        const double x = a8.step(c);
         if (do_hh && (m == ex + 1 || n == ey + 1)) a9(m, n);
-        if (nbad && m >= sx && m <= ex && n >= sy && n <= ey) {
-            const long c = a8.I(m, n);
-            if (a8.lu[c] > 0.5f) {
-                const double x = a8.ssh[c];
-                if (!(x < 10000.0 && x > -10000.0)) atomicAdd(nbad, 1);
-            }
-        }
+        if (nbad && m >= sx && m <= ex && n >= sy && n <= ey && ld(a8.lu, c) > 0.5f && !(x < 10000.0 && x > -10000.0))
+            atomicAdd(nbad, 1);
     }
 };
 
@@ -541,6 +541,8 @@ static int check_block(const ocn_block *b)
         return set_error(OCN_ERR_ARG, "array bounds must include a 1-wide halo ring");
     if (b->pitch < (int64_t)(b->bnd_x2 - b->bnd_x1 + 1))
         return set_error(OCN_ERR_ARG, "pitch smaller than bnd_x2-bnd_x1+1");
+    if (b->pitch * (int64_t)(b->bnd_y2 - b->bnd_y1 + 1) >= (int64_t(1) << 29))
+        return set_error(OCN_ERR_ARG, "block array of 2^29 elements or more (32-bit byte offsets of r8 fields)");
     return OCN_OK;
 }
 
@@ -565,9 +567,10 @@ static SwUpdateSsh mk_a1(const ocn_block *b, void *const *ptr, double tau)
 static HhUpdate mk_a2(const ocn_block *b, void *const *ptr)
 {
     return HhUpdate{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end,
-                    F4(OCN_LU), F4(OCN_LLU), F4(OCN_LLV), F4(OCN_LUH), F4(OCN_DX), F4(OCN_DY), F4(OCN_DXT),
-                    F4(OCN_DYT), F4(OCN_DXH), F4(OCN_DYH), F4(OCN_DXB), F4(OCN_DYB), F8(OCN_HHQ_N), F8(OCN_HHU_N),
-                    F8(OCN_HHV_N), F8(OCN_HHH_N), F8(OCN_SSH), F8(OCN_HHQ_REST)};
+                    Interp{F4(OCN_LU), F4(OCN_DX), F4(OCN_DY), F4(OCN_DXT), F4(OCN_DYT), F4(OCN_DXH), F4(OCN_DYH),
+                           F4(OCN_DXB), F4(OCN_DYB)},
+                    F4(OCN_LLU), F4(OCN_LLV), F4(OCN_LUH), F8(OCN_HHQ_N), F8(OCN_HHU_N), F8(OCN_HHV_N),
+                    F8(OCN_HHH_N), F8(OCN_SSH), F8(OCN_HHQ_REST)};
 }
 
 int launch_fused_a(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s)
@@ -640,7 +643,7 @@ int ocn_hh_update(const ocn_block *b, const float *lu, const float *llu, const f
 {
     CHECK(lu, llu, llv, luh, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, hqn, hun, hvn, hhn, sh, h_r);
     HhUpdate k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end,
-               lu, llu, llv, luh, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, hqn, hun, hvn, hhn, sh, h_r};
+               Interp{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh, hqn, hun, hvn, hhn, sh, h_r};
     return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream);
 }
 
@@ -728,7 +731,7 @@ int ocn_hh_init(const ocn_block *b, int32_t full_free_surface, const float *lu, 
     CHECK(lu, llu, llv, luh, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh,
           hhp, hhn, sh, shp, h_r);
     HhInit k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)full_free_surface,
-             lu, llu, llv, luh, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb,
+             Interp{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh,
              hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn, sh, shp, h_r};
     return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream);
 }
