@@ -58,6 +58,36 @@ def cpu_baseline(seconds_hint: float = 10.0):
                       f"after 1 warm-up step, {dt:.1f} s"}
 
 
+def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for):
+    """Run-time check of the N > 1 path: a 512^2 box on the N-GPU block grid (RCCL halos) for
+    5 steps; rank 0 recomputes the same block grid inside one process on its GPU (device-local
+    halo copies, the path tests/test_gpu_parity.py pins to the reference) and compares every
+    rank's block bit for bit.  Returns True/False on rank 0, None elsewhere."""
+    import numpy as np
+    n, steps = 512, 5
+    m = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(bx, by), rank=rank, nranks=world,
+                       device=local_rank)
+    m.attach_comm(uid_for())
+    m.init().step(steps).synchronize()
+    mine = {(b.bm, b.bn): {f: m.download(b.k, f) for f in ("ssh", "ubrtr", "vbrtr", "hhu", "str_s")}
+            for b in m.blocks}
+    m.close()
+    gathered = [None] * world if rank == 0 else None
+    dist.gather_object(mine, gathered, dst=0)
+    if rank != 0:
+        return None
+    ref = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(bx, by), device=local_rank)
+    ref.init().step(steps).synchronize()
+    ok = True
+    for b in ref.blocks:
+        for part in gathered:
+            if (b.bm, b.bn) in part:
+                for f, a in part[(b.bm, b.bn)].items():
+                    ok &= a.tobytes() == ref.download(b.k, f).tobytes()
+    ref.close()
+    return bool(ok)
+
+
 def load_traffic(stage: str, cells: int):
     """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary (profiles/), or None."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -100,11 +130,16 @@ def main():
     basin = amd.BasinConfig(nx=nxbox + 4, ny=nybox + 4)
     model = amd.OceanModel(basin, amd.SWConfig(), amd.ParallelConfig(bx, by), rank=rank, nranks=world,
                            device=local_rank)
+    parity = None
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        uid = [amd.make_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        model.attach_comm(uid[0])
+
+        def uid_for():
+            uid = [amd.make_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            return uid[0]
+        model.attach_comm(uid_for())
+        parity = multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for)
     model.set_fused(not args.stages)
     if args.graph:
         model.set_graph(True)
@@ -163,6 +198,8 @@ def main():
                                        "this_path": B_ALG if args.stages else B_FUSED},
                "step_moved_frac": round(moved / HBM_PEAK_GBS, 4),
                "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()}}
+        if world > 1:
+            out["multi_gpu_parity_512"] = parity
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
     model.close()

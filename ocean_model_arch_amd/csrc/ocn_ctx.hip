@@ -982,12 +982,14 @@ int ocn_ctx_init_state(ocn_ctx *c)
 int ocn_ctx_sync(ocn_ctx *c, int field_id)
 {
     if (!c || !is_r8(field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
+    HIPCHK(hipSetDevice(c->dec.device));
     return run_sync(c, {field_id});
 }
 
 int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->dec.device));
     if (stage_id < 0 || stage_id >= OCN_NUM_STAGES) return set_error(OCN_ERR_ARG, "bad stage id");
     return envoke(c, stage_id, tau);
 }
@@ -1012,6 +1014,7 @@ static int capture_step(ocn_ctx *c, double tau, bool check)
 int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->dec.device));
     if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
     for (int s = 1; s <= nsteps; ++s) {
         const bool check = check_every > 0 && (s % check_every == 0);
@@ -1031,6 +1034,7 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
 int ocn_ctx_synchronize(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->dec.device));
     HIPCHK(hipStreamSynchronize(c->stream));
     int32_t nbad = 0;
     HIPCHK(hipMemcpy(&nbad, c->d_nbad, sizeof(nbad), hipMemcpyDeviceToHost));

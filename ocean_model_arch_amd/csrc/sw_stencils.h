@@ -1,0 +1,611 @@
+// sw_stencils.h -- the per-cell arithmetic of the SW step stages (functors), shared by the
+// HIP kernels (sw_kernels.hip, compiled for gfx950) and the host-side memory-safety /
+// parity harness (tests/native/stencil_host.cpp, compiled with g++ -fsanitize=address).
+// Each functor restates one reference loop nest (kernel/shallow_water/*.f90) bit for bit.
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/ocn_sw.h"
+
+#ifndef OCN_HD
+#define OCN_HD __device__
+#endif
+#ifndef OCN_INLINE
+#define OCN_INLINE __forceinline__
+#endif
+#ifndef OCN_ATOMIC_INC
+#define OCN_ATOMIC_INC(p) atomicAdd((p), 1)
+#endif
+#ifndef OCN_FREE_FALL_ACC
+#define OCN_FREE_FALL_ACC 9.8f   // shared/constants.f90:23 FreeFallAcc = 9.8 (real(4))
+#endif
+
+namespace ocn {
+
+// Element index of A(m, n) in a block array: 32-bit (the host checks pitch * rows < 2^31).
+struct Geo {
+    int bx1, by1;
+    unsigned p;
+    OCN_HD OCN_INLINE unsigned operator()(int m, int n) const
+    {
+        return (unsigned)(m - bx1) + (unsigned)(n - by1) * p;
+    }
+};
+
+#define D(x) ((double)(x))
+
+// Loads / stores through a 32-bit byte offset from the (wave-uniform) array base: the compiler
+// then emits the SGPR-base + 32-bit VGPR-offset global_load/store form (no 64-bit address
+// arithmetic per array).  Block arrays hold < 2^29 elements, so every r8 byte offset fits 32 bits (checked on the host).
+#ifdef OCN_HOST_BOUNDS_CHECK   // host harness only: every access checked against the block size
+extern unsigned ocn_host_limit;
+void ocn_host_oob(unsigned i);
+#define OCN_CHECK_INDEX(i) do { if ((i) >= ocn_host_limit) ocn_host_oob(i); } while (0)
+#else
+#define OCN_CHECK_INDEX(i) do { } while (0)
+#endif
+
+template <class T> OCN_HD OCN_INLINE T ld(const T *__restrict__ p, unsigned i)
+{
+    OCN_CHECK_INDEX(i);
+    return *(const T *)((const char *)p + i * (unsigned)sizeof(T));
+}
+template <class T> OCN_HD OCN_INLINE void st(T *__restrict__ p, unsigned i, T v)
+{
+    OCN_CHECK_INDEX(i);
+    *(T *)((char *)p + i * (unsigned)sizeof(T)) = v;
+}
+
+
+// ------------------------------------------------------------------ a1 sw_update_ssh
+// vel_ssh.f90:69-106
+struct SwUpdateSsh {
+    Geo I; double tau;
+    const float *__restrict__ lu, *__restrict__ dx, *__restrict__ dy, *__restrict__ dxh, *__restrict__ dyh;
+    const double *__restrict__ hhu, *__restrict__ hhv;
+    double *__restrict__ sshn;
+    const double *__restrict__ sshp, *__restrict__ ubrtr, *__restrict__ vbrtr;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n), w = c - 1, s = c - I.p;
+        const double t1 = ld(ubrtr, c) * ld(hhu, c) * D(ld(dyh, c));
+        const double t2 = ld(ubrtr, w) * ld(hhu, w) * D(ld(dyh, w));
+        const double t3 = ld(vbrtr, c) * ld(hhv, c) * D(ld(dxh, c));
+        const double t4 = ld(vbrtr, s) * ld(hhv, s) * D(ld(dxh, s));
+        const float area = ld(dx, c) * ld(dy, c);
+        const double div = (t1 - t2 + t3 - t4) / D(area);
+        const double r = ld(sshp, c) + 2.0 * tau * (-div);
+        if (ld(lu, c) > 0.5f) st(sshn, c, r);
+    }
+};
+
+// ------------------------------------------------------------------ T->U/V/H interpolation
+// kernel/shallow_water/depth.f90:56-97 for one level given its values at the four corners
+// (m,n), (m+1,n), (m,n+1), (m+1,n+1).
+struct Interp {
+    const float *__restrict__ lu, *__restrict__ dx, *__restrict__ dy;
+    const float *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxh, *__restrict__ dyh;
+    const float *__restrict__ dxb, *__restrict__ dyb;
+    // per-corner weights dx*dy*lu (products evaluated per use, as the reference does)
+    OCN_HD OCN_INLINE double wt(double h, unsigned i) const { return h * D(ld(dx, i)) * D(ld(dy, i)) * D(ld(lu, i)); }
+    OCN_HD OCN_INLINE double u(double h00, double h10, unsigned c, unsigned e) const
+    {
+        const double slu = D(ld(lu, c) + ld(lu, e));
+        return (wt(h00, c) + wt(h10, e)) / slu / D(ld(dxt, c)) / D(ld(dyh, c));
+    }
+    OCN_HD OCN_INLINE double v(double h00, double h01, unsigned c, unsigned nn) const
+    {
+        const double slu = D(ld(lu, c) + ld(lu, nn));
+        return (wt(h00, c) + wt(h01, nn)) / slu / D(ld(dxh, c)) / D(ld(dyt, c));
+    }
+    OCN_HD OCN_INLINE double h(double h00, double h10, double h01, double h11, unsigned c, unsigned e,
+                                        unsigned nn, unsigned ne) const
+    {
+        const double slu = D(ld(lu, c) + ld(lu, e) + ld(lu, nn) + ld(lu, ne));
+        return (wt(h00, c) + wt(h10, e) + wt(h01, nn) + wt(h11, ne)) / slu / D(ld(dxb, c)) / D(ld(dyb, c));
+    }
+};
+
+// ------------------------------------------------------------------ a2 hh_update
+// depth.f90:101-162.  Thread grid = whole bnd range (hqn = h_r + sh, :129); the
+// interpolation part runs on [start-1, end]^2.
+struct HhUpdate {
+    Geo I; int i0, i1, j0, j1;
+    Interp W;
+    const float *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
+    double *__restrict__ hqn, *__restrict__ hun, *__restrict__ hvn, *__restrict__ hhn;
+    const double *__restrict__ sh, *__restrict__ h_r;
+    // the [start-1, end]^2 interpolation part (depth.f90:134-160); q = h_r + sh at each corner
+    OCN_HD OCN_INLINE void interp(unsigned c, double q00) const
+    {
+        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1;
+        const double q10 = ld(h_r, e) + ld(sh, e), q01 = ld(h_r, nn) + ld(sh, nn), q11 = ld(h_r, ne) + ld(sh, ne);
+        const double xu = W.u(q00, q10, c, e);
+        const double xv = W.v(q00, q01, c, nn);
+        const double xh = W.h(q00, q10, q01, q11, c, e, nn, ne);
+        if (ld(llu, c) > 0.5f) st(hun, c, xu);
+        if (ld(llv, c) > 0.5f) st(hvn, c, xv);
+        if (ld(luh, c) > 0.5f) st(hhn, c, xh);
+    }
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n);
+        const double q00 = ld(h_r, c) + ld(sh, c);
+        st(hqn, c, q00);
+        if (m < i0 || m > i1 || n < j0 || n > j1) return;
+        interp(c, q00);
+    }
+};
+
+// ------------------------------------------------------------------ a10 hh_init
+// depth.f90:14-99: hq = h_r + sh*ffs, hqp = h_r + shp*ffs, hqn = h_r (whole array), then the
+// three levels interpolated on [start-1, end]^2.
+struct HhInit {
+    Geo I; int i0, i1, j0, j1; double f;
+    Interp W;
+    const float *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
+    double *__restrict__ hq, *__restrict__ hqp, *__restrict__ hqn;
+    double *__restrict__ hu, *__restrict__ hup, *__restrict__ hun;
+    double *__restrict__ hv, *__restrict__ hvp, *__restrict__ hvn;
+    double *__restrict__ hh, *__restrict__ hhp, *__restrict__ hhn;
+    const double *__restrict__ sh, *__restrict__ shp, *__restrict__ h_r;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n);
+        const double r00 = ld(h_r, c);
+        const double a00 = r00 + ld(sh, c) * f, b00 = r00 + ld(shp, c) * f;
+        st(hq, c, a00); st(hqp, c, b00); st(hqn, c, r00);
+        if (m < i0 || m > i1 || n < j0 || n > j1) return;
+        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1;
+        const double r10 = ld(h_r, e), r01 = ld(h_r, nn), r11 = ld(h_r, ne);
+        const double a10 = r10 + ld(sh, e) * f, a01 = r01 + ld(sh, nn) * f, a11 = r11 + ld(sh, ne) * f;
+        const double b10 = r10 + ld(shp, e) * f, b01 = r01 + ld(shp, nn) * f, b11 = r11 + ld(shp, ne) * f;
+        const double u0 = W.u(a00, a10, c, e), u1 = W.u(b00, b10, c, e), u2 = W.u(r00, r10, c, e);
+        const double v0 = W.v(a00, a01, c, nn), v1 = W.v(b00, b01, c, nn), v2 = W.v(r00, r01, c, nn);
+        const double h0 = W.h(a00, a10, a01, a11, c, e, nn, ne), h1 = W.h(b00, b10, b01, b11, c, e, nn, ne),
+                     h2 = W.h(r00, r10, r01, r11, c, e, nn, ne);
+        if (ld(llu, c) > 0.5f) { st(hu, c, u0); st(hup, c, u1); st(hun, c, u2); }
+        if (ld(llv, c) > 0.5f) { st(hv, c, v0); st(hvp, c, v1); st(hvn, c, v2); }
+        if (ld(luh, c) > 0.5f) { st(hh, c, h0); st(hhp, c, h1); st(hhn, c, h2); }
+    }
+};
+
+// ------------------------------------------------------------------ a3 uv_trans_vort
+// vel_ssh.f90:247-281
+struct UvTransVort {
+    Geo I;
+    const float *__restrict__ luu, *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxb, *__restrict__ dyb;
+    const double *__restrict__ u, *__restrict__ v;
+    double *__restrict__ vort;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n), e = c + 1, nn = c + I.p;
+        const double a = ld(v, e) * D(ld(dyt, e)) - ld(v, c) * D(ld(dyt, c));
+        const double b = ld(u, nn) * D(ld(dxt, nn)) - ld(u, c) * D(ld(dxt, c));
+        const double d = (ld(v, e) - ld(v, c)) * D(ld(dyb, c)) - (ld(u, nn) - ld(u, c)) * D(ld(dxb, c));
+        const double r = a - b - d;
+        if (ld(luu, c) > 0.5f) st(vort, c, r);
+    }
+};
+
+// ------------------------------------------------------------------ a4 uv_trans
+// vel_ssh.f90:283-373
+struct UvTrans {
+    Geo I;
+    const float *__restrict__ lcu, *__restrict__ lcv, *__restrict__ luu, *__restrict__ dxh, *__restrict__ dyh;
+    const double *__restrict__ u, *__restrict__ v, *__restrict__ vort;
+    const double *__restrict__ hu, *__restrict__ hv, *__restrict__ hh;
+    double *__restrict__ RHSx, *__restrict__ RHSy;
+    OCN_HD OCN_INLINE void eval(unsigned c, double &rx, double &ry) const
+    {
+        const unsigned e = c + 1, w = c - 1, nn = c + I.p, s = c - I.p, se = s + 1, wn = nn - 1;
+        {
+            const double fu_c = ld(u, c) * D(ld(dyh, c)) * ld(hu, c);
+            const double fx_p = (fu_c + ld(u, e) * D(ld(dyh, e)) * ld(hu, e)) / 2.0 * (ld(u, c) + ld(u, e)) / 2.0;
+            const double fx_m = (fu_c + ld(u, w) * D(ld(dyh, w)) * ld(hu, w)) / 2.0 * (ld(u, c) + ld(u, w)) / 2.0;
+            const double fy_p = (ld(v, c) * D(ld(dxh, c)) * ld(hv, c) + ld(v, e) * D(ld(dxh, e)) * ld(hv, e)) / 2.0
+                                * (ld(u, nn) + ld(u, c)) / 2.0 * D(ld(luu, c));
+            const double fy_m = (ld(v, s) * D(ld(dxh, s)) * ld(hv, s) + ld(v, se) * D(ld(dxh, se)) * ld(hv, se)) / 2.0
+                                * (ld(u, s) + ld(u, c)) / 2.0 * D(ld(luu, s));
+            rx = -(fx_p - fx_m + fy_p - fy_m)
+                 + (ld(vort, c) * ld(hh, c) * (ld(v, e) + ld(v, c)) + ld(vort, s) * ld(hh, s) * (ld(v, se) + ld(v, s))) / 4.0;
+        }
+        {
+            const double fv_c = ld(v, c) * D(ld(dxh, c)) * ld(hv, c);
+            const double fy_p = (fv_c + ld(v, nn) * D(ld(dxh, nn)) * ld(hv, nn)) / 2.0 * (ld(v, c) + ld(v, nn)) / 2.0;
+            const double fy_m = (fv_c + ld(v, s) * D(ld(dxh, s)) * ld(hv, s)) / 2.0 * (ld(v, c) + ld(v, s)) / 2.0;
+            const double fx_p = (ld(u, c) * D(ld(dyh, c)) * ld(hu, c) + ld(u, nn) * D(ld(dyh, nn)) * ld(hu, nn)) / 2.0
+                                * (ld(v, e) + ld(v, c)) / 2.0;
+            const double fx_m = (ld(u, w) * D(ld(dyh, w)) * ld(hu, w) + ld(u, wn) * D(ld(dyh, wn)) * ld(hu, wn)) / 2.0
+                                * (ld(v, w) + ld(v, c)) / 2.0;
+            ry = -(fx_p - fx_m + fy_p - fy_m)
+                 - (ld(vort, c) * ld(hh, c) * (ld(u, nn) + ld(u, c)) + ld(vort, w) * ld(hh, w) * (ld(u, wn) + ld(u, w))) / 4.0;
+        }
+    }
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n);
+        double rx, ry;
+        eval(c, rx, ry);
+        if (ld(lcu, c) > 0.5f) st(RHSx, c, rx);
+        if (ld(lcv, c) > 0.5f) st(RHSy, c, ry);
+    }
+};
+
+// ------------------------------------------------------------------ a5 stress_components
+// mixing.f90:14-58
+struct StressComponents {
+    Geo I;
+    const float *__restrict__ lu, *__restrict__ luu, *__restrict__ dx, *__restrict__ dy;
+    const float *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxh, *__restrict__ dyh;
+    const float *__restrict__ dxb, *__restrict__ dyb;
+    const double *__restrict__ u, *__restrict__ v;
+    double *__restrict__ str_t, *__restrict__ str_s;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n), w = c - 1, s = c - I.p, e = c + 1, nn = c + I.p;
+        const float r1 = ld(dy, c) / ld(dx, c);
+        const float r2 = ld(dx, c) / ld(dy, c);
+        const double vt = D(r1) * (ld(u, c) / D(ld(dyh, c)) - ld(u, w) / D(ld(dyh, w)))
+                          - D(r2) * (ld(v, c) / D(ld(dxh, c)) - ld(v, s) / D(ld(dxh, s)));
+        const float q1 = ld(dxb, c) / ld(dyb, c);
+        const float q2 = ld(dyb, c) / ld(dxb, c);
+        const double vs = D(q1) * (ld(u, nn) / D(ld(dxt, nn)) - ld(u, c) / D(ld(dxt, c)))
+                          + D(q2) * (ld(v, e) / D(ld(dyt, e)) - ld(v, c) / D(ld(dyt, c)));
+        if (ld(lu, c) > 0.5f) st(str_t, c, vt);
+        if (ld(luu, c) > 0.5f) st(str_s, c, vs);
+    }
+};
+
+// ------------------------------------------------------------------ a6 uv_diff2
+// vel_ssh.f90:375-452
+struct UvDiff2 {
+    Geo I;
+    const float *__restrict__ lcu, *__restrict__ lcv, *__restrict__ dx, *__restrict__ dy;
+    const float *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxh, *__restrict__ dyh;
+    const float *__restrict__ dxb, *__restrict__ dyb;
+    const double *__restrict__ mu, *__restrict__ str_t, *__restrict__ str_s, *__restrict__ hq, *__restrict__ hh;
+    double *__restrict__ RHSx, *__restrict__ RHSy;
+    OCN_HD OCN_INLINE void eval(unsigned c, double &rx, double &ry) const
+    {
+        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1, s = c - I.p, se = s + 1, w = c - 1, wn = nn - 1;
+        {
+            const double muh_p = (ld(mu, c) + ld(mu, e) + ld(mu, nn) + ld(mu, ne)) / 4.0;
+            const double muh_m = (ld(mu, c) + ld(mu, e) + ld(mu, s) + ld(mu, se)) / 4.0;
+            const float dy2p = ld(dy, e) * ld(dy, e), dy2 = ld(dy, c) * ld(dy, c);
+            const float dxb2 = ld(dxb, c) * ld(dxb, c), dxb2m = ld(dxb, s) * ld(dxb, s);
+            rx = (D(dy2p) * ld(mu, e) * ld(hq, e) * ld(str_t, e) - D(dy2) * ld(mu, c) * ld(hq, c) * ld(str_t, c)) / D(ld(dyh, c))
+                 + (D(dxb2) * muh_p * ld(hh, c) * ld(str_s, c) - D(dxb2m) * muh_m * ld(hh, s) * ld(str_s, s)) / D(ld(dxt, c));
+        }
+        {
+            const double muh_p = (ld(mu, c) + ld(mu, e) + ld(mu, nn) + ld(mu, ne)) / 4.0;
+            const double muh_m = (ld(mu, c) + ld(mu, w) + ld(mu, nn) + ld(mu, wn)) / 4.0;
+            const float dx2p = ld(dx, nn) * ld(dx, nn), dx2 = ld(dx, c) * ld(dx, c);
+            const float dyb2 = ld(dyb, c) * ld(dyb, c), dyb2m = ld(dyb, w) * ld(dyb, w);
+            ry = -(D(dx2p) * ld(mu, nn) * ld(hq, nn) * ld(str_t, nn) - D(dx2) * ld(mu, c) * ld(hq, c) * ld(str_t, c)) / D(ld(dxh, c))
+                 + (D(dyb2) * muh_p * ld(hh, c) * ld(str_s, c) - D(dyb2m) * muh_m * ld(hh, w) * ld(str_s, w)) / D(ld(dyt, c));
+        }
+    }
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n);
+        double rx, ry;
+        eval(c, rx, ry);
+        if (ld(lcu, c) > 0.5f) st(RHSx, c, rx);
+        if (ld(lcv, c) > 0.5f) st(RHSy, c, ry);
+    }
+};
+
+// ------------------------------------------------------------------ a7 sw_update_uv
+// vel_ssh.f90:108-195
+struct SwUpdateUv {
+    Geo I; double tau;
+    const float *__restrict__ lcu, *__restrict__ lcv, *__restrict__ dxt, *__restrict__ dyt;
+    const float *__restrict__ dxh, *__restrict__ dyh, *__restrict__ dxb, *__restrict__ dyb;
+    const double *__restrict__ hhu, *__restrict__ hhun, *__restrict__ hhup;
+    const double *__restrict__ hhv, *__restrict__ hhvn, *__restrict__ hhvp;
+    const double *__restrict__ hhh, *__restrict__ ssh;
+    const double *__restrict__ ubrtr; double *__restrict__ ubrtrn; const double *__restrict__ ubrtrp;
+    const double *__restrict__ vbrtr; double *__restrict__ vbrtrn; const double *__restrict__ vbrtrp;
+    const float *__restrict__ rdis, *__restrict__ rlh_s;
+    const double *__restrict__ RHSx, *__restrict__ RHSy, *__restrict__ RHSx_adv, *__restrict__ RHSy_adv;
+    const double *__restrict__ RHSx_dif, *__restrict__ RHSy_dif;
+    // rxa/rxd/rya/ryd: RHSx_adv, RHSx_dif, RHSy_adv, RHSy_dif at this point
+    OCN_HD OCN_INLINE void eval(unsigned c, double rxa, double rxd, double rya, double ryd, double &un,
+                                         double &vn) const
+    {
+        const double g = D(OCN_FREE_FALL_ACC);
+        const unsigned e = c + 1, s = c - I.p, se = s + 1, nn = c + I.p, w = c - 1, wn = nn - 1;
+        {
+            const double bp = ld(hhun, c) * D(ld(dxt, c)) * D(ld(dyh, c)) / 2.0 / tau;
+            const double bp0 = ld(hhup, c) * D(ld(dxt, c)) * D(ld(dyh, c)) / 2.0 / tau;
+            const double slx = -(g * (ld(ssh, e) - ld(ssh, c)) * D(ld(dyh, c)) * ld(hhu, c));
+            const float rd = ld(rdis, c) + ld(rdis, e);
+            const double fric = D(rd) / 2.0 * ld(ubrtrp, c) * D(ld(dxt, c)) * D(ld(dyh, c)) * ld(hhu, c);
+            const double c1 = D(ld(rlh_s, c)) * ld(hhh, c) * D(ld(dxb, c)) * D(ld(dyb, c)) * (ld(vbrtr, e) + ld(vbrtr, c));
+            const double c2 = D(ld(rlh_s, s)) * ld(hhh, s) * D(ld(dxb, s)) * D(ld(dyb, s)) * (ld(vbrtr, se) + ld(vbrtr, s));
+            const double grx = ld(RHSx, c) + slx + rxd + rxa - fric + (c1 + c2) / 4.0;
+            un = (ld(ubrtrp, c) * bp0 + grx) / (bp);
+        }
+        {
+            const double bp = ld(hhvn, c) * D(ld(dyt, c)) * D(ld(dxh, c)) / 2.0 / tau;
+            const double bp0 = ld(hhvp, c) * D(ld(dyt, c)) * D(ld(dxh, c)) / 2.0 / tau;
+            const double sly = -(g * (ld(ssh, nn) - ld(ssh, c)) * D(ld(dxh, c)) * ld(hhv, c));
+            const float rd = ld(rdis, c) + ld(rdis, nn);
+            const double fric = D(rd) / 2.0 * ld(vbrtrp, c) * D(ld(dxh, c)) * D(ld(dyt, c)) * ld(hhv, c);
+            const double c1 = D(ld(rlh_s, c)) * ld(hhh, c) * D(ld(dxb, c)) * D(ld(dyb, c)) * (ld(ubrtr, nn) + ld(ubrtr, c));
+            const double c2 = D(ld(rlh_s, w)) * ld(hhh, w) * D(ld(dxb, w)) * D(ld(dyb, w)) * (ld(ubrtr, wn) + ld(ubrtr, w));
+            const double gry = ld(RHSy, c) + sly + ryd + rya - fric - (c1 + c2) / 4.0;
+            vn = (ld(vbrtrp, c) * bp0 + gry) / (bp);
+        }
+    }
+    OCN_HD OCN_INLINE void store(unsigned c, double un, double vn) const
+    {
+        if (ld(lcu, c) > 0.5f) st(ubrtrn, c, un);
+        if (ld(lcv, c) > 0.5f) st(vbrtrn, c, vn);
+    }
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n);
+        double un, vn;
+        eval(c, ld(RHSx_adv, c), ld(RHSx_dif, c), ld(RHSy_adv, c), ld(RHSy_dif, c), un, vn);
+        store(c, un, vn);
+    }
+};
+
+// ------------------------------------------------------------------ a8 sw_next_step
+// vel_ssh.f90:197-245 (interior + halo ring)
+struct SwNextStep {
+    Geo I; double ts;
+    const float *__restrict__ lu, *__restrict__ lcu, *__restrict__ lcv;
+    double *__restrict__ ssh, *__restrict__ sshn, *__restrict__ sshp;
+    double *__restrict__ u, *__restrict__ un, *__restrict__ up;
+    double *__restrict__ v, *__restrict__ vn, *__restrict__ vp;
+    // returns the ssh value after the update (for check_ssh_err)
+    OCN_HD OCN_INLINE double step(unsigned i) const
+    {
+        const double x = ld(ssh, i), xn = ld(sshn, i), xp = ld(sshp, i);
+        const double a = ld(u, i), an = ld(un, i), ap = ld(up, i);
+        const double b = ld(v, i), bn = ld(vn, i), bp = ld(vp, i);
+        const double fx = x + ts * (xn - 2.0 * x + xp) / 2.0;
+        const double fa = a + ts * (an - 2.0 * a + ap) / 2.0;
+        const double fb = b + ts * (bn - 2.0 * b + bp) / 2.0;
+        const bool bl = ld(lu, i) > 0.5f;
+        if (bl) { st(sshp, i, fx); st(ssh, i, xn); }
+        if (ld(lcu, i) > 0.5f) { st(up, i, fa); st(u, i, an); }
+        if (ld(lcv, i) > 0.5f) { st(vp, i, fb); st(v, i, bn); }
+        return bl ? xn : x;
+    }
+    OCN_HD void operator()(int m, int n) const { (void)step(I(m, n)); }
+};
+
+// ------------------------------------------------------------------ a9 hh_shift
+// depth.f90:164-211 (interior + halo ring)
+struct HhShift {
+    Geo I; double ts;
+    const float *__restrict__ lu, *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
+    double *__restrict__ hq, *__restrict__ hqp, *__restrict__ hqn;
+    double *__restrict__ hu, *__restrict__ hup, *__restrict__ hun;
+    double *__restrict__ hv, *__restrict__ hvp, *__restrict__ hvn;
+    double *__restrict__ hh, *__restrict__ hhp, *__restrict__ hhn;
+    OCN_HD static OCN_INLINE void shift(bool mask, double *x, double *xp, const double *xn, unsigned i,
+                                                 double ts)
+    {
+        const double a = ld(x, i), an = ld(xn, i), ap = ld(xp, i);
+        const double f = a + ts * (an - 2.0 * a + ap) / 2.0;
+        if (mask) { st(xp, i, f); st(x, i, an); }
+    }
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned i = I(m, n);
+        shift(ld(llu, i) > 0.5f, hu, hup, hun, i, ts);
+        shift(ld(llv, i) > 0.5f, hv, hvp, hvn, i, ts);
+        shift(ld(lu, i) > 0.5f, hq, hqp, hqn, i, ts);
+        shift(ld(luh, i) > 0.5f, hh, hhp, hhn, i, ts);
+    }
+};
+
+// ------------------------------------------------------------------ check_ssh_err
+// vel_ssh.f90:40-67 as a device reduction (one atomic per thread with a bad point; the
+// count only needs to be non-zero).
+struct CheckSshErr {
+    Geo I;
+    const float *__restrict__ lu; const double *__restrict__ ssh; int *nbad;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = I(m, n);
+        const double s = ld(ssh, c);
+        if (ld(lu, c) > 0.5f && !(s < 10000.0 && s > -10000.0)) OCN_ATOMIC_INC(nbad);
+    }
+};
+
+// ================================================================== fused step groups
+// The step's 10 stages regrouped into 4 launches with the same results, write sets and halo
+// state as the stage-by-stage reference order (shallow_water.f90:36-92):
+//   A  = a1 sw_update_ssh + a2 hh_update + a3 uv_trans_vort + a5 stress_components
+//        (mutually independent: none reads another's output) -> one sync of their 7 fields.
+//        hh_update's whole-array hqn = h_r + ssh is not stored: its only readers are hh_shift's
+//        hq/hqp updates, which hh_init overwrites whole-array later in the same step.
+//   B  = a4 uv_trans + a6 uv_diff2 + a7 sw_update_uv: sw_update_uv reads RHS*_adv / RHS*_dif
+//        only at its own point, so they are passed in registers (and still stored) -> sync
+//        of u/v (and uv_trans's lazy hh*_p sync, whose halos nothing in B reads).
+//   C1 = a8 sw_next_step + a9 hh_shift on the outer ring only (on [start-1,end]^2 its
+//        outputs are dead: hh_init overwrites them) + check_ssh_err.
+//   C2 = a10 hh_init (unchanged) -> sync hhu/hhv/hhh.
+struct FusedA {
+    int sx, sy;
+    bool do_hh, do_vort, do_stress;
+    SwUpdateSsh a1; HhUpdate a2; UvTransVort a3; StressComponents a5;
+    OCN_HD void operator()(int m, int n) const
+    {
+        if (m >= sx && n >= sy) {
+            a1(m, n);
+            if (do_vort) a3(m, n);
+            if (do_stress) a5(m, n);
+        }
+        if (do_hh) {
+            const unsigned c = a2.I(m, n);
+            a2.interp(c, ld(a2.h_r, c) + ld(a2.sh, c));
+        }
+    }
+};
+
+struct FusedB {
+    bool do_adv, do_dif;
+    UvTrans a4; UvDiff2 a6; SwUpdateUv a7;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = a7.I(m, n);
+        double rxa, rya, rxd, ryd;
+        if (do_adv) a4.eval(c, rxa, rya);
+        else { rxa = ld(a7.RHSx_adv, c); rya = ld(a7.RHSy_adv, c); }
+        if (do_dif) a6.eval(c, rxd, ryd);
+        else { rxd = ld(a7.RHSx_dif, c); ryd = ld(a7.RHSy_dif, c); }
+        double un, vn;
+        a7.eval(c, rxa, rxd, rya, ryd, un, vn);
+        const bool bu = ld(a7.lcu, c) > 0.5f, bv = ld(a7.lcv, c) > 0.5f;
+        if (bu) {
+            if (do_adv) st(a4.RHSx, c, rxa);
+            if (do_dif) st(a6.RHSx, c, rxd);
+            st(a7.ubrtrn, c, un);
+        }
+        if (bv) {
+            if (do_adv) st(a4.RHSy, c, rya);
+            if (do_dif) st(a6.RHSy, c, ryd);
+            st(a7.vbrtrn, c, vn);
+        }
+    }
+};
+
+struct FusedC1 {
+    int sx, ex, sy, ey;
+    bool do_hh;
+    int *nbad;
+    SwNextStep a8; HhShift a9;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const unsigned c = a8.I(m, n);
+        const double x = a8.step(c);
+        if (do_hh && (m == ex + 1 || n == ey + 1)) a9(m, n);
+        if (nbad && m >= sx && m <= ex && n >= sy && n <= ey && ld(a8.lu, c) > 0.5f && !(x < 10000.0 && x > -10000.0))
+            OCN_ATOMIC_INC(nbad);
+    }
+};
+
+
+// ------------------------------------------------------------------ functor makers
+// Built from a block's field table (`ptr`, indexed by ocn_field_slot) -- used by the fused
+// launches and by the host harness, so both run exactly the same functors over the same ranges.
+inline int ocn_field_slot(int id) { return id < OCN_NUM_R4 ? id : OCN_NUM_R4 + (id - OCN_SSH); }
+inline Geo geo(const ocn_block *b) { return Geo{b->bnd_x1, b->bnd_y1, (unsigned)b->pitch}; }
+
+struct Range { int m0, m1, n0, n1; };
+inline Range range_interior(const ocn_block *b) { return {b->nx_start, b->nx_end, b->ny_start, b->ny_end}; }
+inline Range range_ring(const ocn_block *b)
+{
+    return {b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1};
+}
+inline Range range_bnd(const ocn_block *b) { return {b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2}; }
+inline Range range_fused_a(const ocn_block *b, const ocn_sw_params &sw)
+{
+    const int o = sw.full_free_surface > 0 ? 1 : 0;
+    return {b->nx_start - o, b->nx_end, b->ny_start - o, b->ny_end};
+}
+
+#define OCN_F4(id) ((const float *)ptr[ocn_field_slot(id)])
+#define OCN_F8(id) ((double *)ptr[ocn_field_slot(id)])
+
+inline Interp make_interp(void *const *ptr)
+{
+    return Interp{OCN_F4(OCN_LU), OCN_F4(OCN_DX), OCN_F4(OCN_DY), OCN_F4(OCN_DXT), OCN_F4(OCN_DYT),
+                  OCN_F4(OCN_DXH), OCN_F4(OCN_DYH), OCN_F4(OCN_DXB), OCN_F4(OCN_DYB)};
+}
+inline SwUpdateSsh make_sw_update_ssh(const ocn_block *b, void *const *ptr, double tau)
+{
+    return SwUpdateSsh{geo(b), tau, OCN_F4(OCN_LU), OCN_F4(OCN_DX), OCN_F4(OCN_DY), OCN_F4(OCN_DXH),
+                       OCN_F4(OCN_DYH), OCN_F8(OCN_HHU), OCN_F8(OCN_HHV), OCN_F8(OCN_SSHN), OCN_F8(OCN_SSHP),
+                       OCN_F8(OCN_UBRTR), OCN_F8(OCN_VBRTR)};
+}
+inline HhUpdate make_hh_update(const ocn_block *b, void *const *ptr)
+{
+    return HhUpdate{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, make_interp(ptr),
+                    OCN_F4(OCN_LLU), OCN_F4(OCN_LLV), OCN_F4(OCN_LUH), OCN_F8(OCN_HHQ_N), OCN_F8(OCN_HHU_N),
+                    OCN_F8(OCN_HHV_N), OCN_F8(OCN_HHH_N), OCN_F8(OCN_SSH), OCN_F8(OCN_HHQ_REST)};
+}
+inline UvTransVort make_uv_trans_vort(const ocn_block *b, void *const *ptr)
+{
+    return UvTransVort{geo(b), OCN_F4(OCN_LUU), OCN_F4(OCN_DXT), OCN_F4(OCN_DYT), OCN_F4(OCN_DXB), OCN_F4(OCN_DYB),
+                       OCN_F8(OCN_UBRTR), OCN_F8(OCN_VBRTR), OCN_F8(OCN_VORT)};
+}
+inline UvTrans make_uv_trans(const ocn_block *b, void *const *ptr)
+{
+    return UvTrans{geo(b), OCN_F4(OCN_LCU), OCN_F4(OCN_LCV), OCN_F4(OCN_LUU), OCN_F4(OCN_DXH), OCN_F4(OCN_DYH),
+                   OCN_F8(OCN_UBRTR), OCN_F8(OCN_VBRTR), OCN_F8(OCN_VORT), OCN_F8(OCN_HHU), OCN_F8(OCN_HHV),
+                   OCN_F8(OCN_HHH), OCN_F8(OCN_RHSX_ADV), OCN_F8(OCN_RHSY_ADV)};
+}
+inline StressComponents make_stress_components(const ocn_block *b, void *const *ptr)
+{
+    return StressComponents{geo(b), OCN_F4(OCN_LU), OCN_F4(OCN_LUU), OCN_F4(OCN_DX), OCN_F4(OCN_DY),
+                            OCN_F4(OCN_DXT), OCN_F4(OCN_DYT), OCN_F4(OCN_DXH), OCN_F4(OCN_DYH), OCN_F4(OCN_DXB),
+                            OCN_F4(OCN_DYB), OCN_F8(OCN_UBRTRP), OCN_F8(OCN_VBRTRP), OCN_F8(OCN_STR_T),
+                            OCN_F8(OCN_STR_S)};
+}
+inline UvDiff2 make_uv_diff2(const ocn_block *b, void *const *ptr)
+{
+    return UvDiff2{geo(b), OCN_F4(OCN_LCU), OCN_F4(OCN_LCV), OCN_F4(OCN_DX), OCN_F4(OCN_DY), OCN_F4(OCN_DXT),
+                   OCN_F4(OCN_DYT), OCN_F4(OCN_DXH), OCN_F4(OCN_DYH), OCN_F4(OCN_DXB), OCN_F4(OCN_DYB),
+                   OCN_F8(OCN_MU), OCN_F8(OCN_STR_T), OCN_F8(OCN_STR_S), OCN_F8(OCN_HHQ), OCN_F8(OCN_HHH),
+                   OCN_F8(OCN_RHSX_DIF), OCN_F8(OCN_RHSY_DIF)};
+}
+inline SwUpdateUv make_sw_update_uv(const ocn_block *b, void *const *ptr, double tau)
+{
+    return SwUpdateUv{geo(b), tau, OCN_F4(OCN_LCU), OCN_F4(OCN_LCV), OCN_F4(OCN_DXT), OCN_F4(OCN_DYT),
+                      OCN_F4(OCN_DXH), OCN_F4(OCN_DYH), OCN_F4(OCN_DXB), OCN_F4(OCN_DYB), OCN_F8(OCN_HHU),
+                      OCN_F8(OCN_HHU_N), OCN_F8(OCN_HHU_P), OCN_F8(OCN_HHV), OCN_F8(OCN_HHV_N), OCN_F8(OCN_HHV_P),
+                      OCN_F8(OCN_HHH), OCN_F8(OCN_SSH), OCN_F8(OCN_UBRTR), OCN_F8(OCN_UBRTRN), OCN_F8(OCN_UBRTRP),
+                      OCN_F8(OCN_VBRTR), OCN_F8(OCN_VBRTRN), OCN_F8(OCN_VBRTRP), OCN_F4(OCN_R_DISS),
+                      OCN_F4(OCN_RLH_S), OCN_F8(OCN_RHSX), OCN_F8(OCN_RHSY), OCN_F8(OCN_RHSX_ADV),
+                      OCN_F8(OCN_RHSY_ADV), OCN_F8(OCN_RHSX_DIF), OCN_F8(OCN_RHSY_DIF)};
+}
+inline SwNextStep make_sw_next_step(const ocn_block *b, void *const *ptr, double ts)
+{
+    return SwNextStep{geo(b), ts, OCN_F4(OCN_LU), OCN_F4(OCN_LCU), OCN_F4(OCN_LCV), OCN_F8(OCN_SSH),
+                      OCN_F8(OCN_SSHN), OCN_F8(OCN_SSHP), OCN_F8(OCN_UBRTR), OCN_F8(OCN_UBRTRN), OCN_F8(OCN_UBRTRP),
+                      OCN_F8(OCN_VBRTR), OCN_F8(OCN_VBRTRN), OCN_F8(OCN_VBRTRP)};
+}
+inline HhShift make_hh_shift(const ocn_block *b, void *const *ptr, double ts)
+{
+    return HhShift{geo(b), ts, OCN_F4(OCN_LU), OCN_F4(OCN_LLU), OCN_F4(OCN_LLV), OCN_F4(OCN_LUH), OCN_F8(OCN_HHQ),
+                   OCN_F8(OCN_HHQ_P), OCN_F8(OCN_HHQ_N), OCN_F8(OCN_HHU), OCN_F8(OCN_HHU_P), OCN_F8(OCN_HHU_N),
+                   OCN_F8(OCN_HHV), OCN_F8(OCN_HHV_P), OCN_F8(OCN_HHV_N), OCN_F8(OCN_HHH), OCN_F8(OCN_HHH_P),
+                   OCN_F8(OCN_HHH_N)};
+}
+inline HhInit make_hh_init(const ocn_block *b, void *const *ptr, int ffs)
+{
+    return HhInit{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)ffs, make_interp(ptr),
+                  OCN_F4(OCN_LLU), OCN_F4(OCN_LLV), OCN_F4(OCN_LUH), OCN_F8(OCN_HHQ), OCN_F8(OCN_HHQ_P),
+                  OCN_F8(OCN_HHQ_N), OCN_F8(OCN_HHU), OCN_F8(OCN_HHU_P), OCN_F8(OCN_HHU_N), OCN_F8(OCN_HHV),
+                  OCN_F8(OCN_HHV_P), OCN_F8(OCN_HHV_N), OCN_F8(OCN_HHH), OCN_F8(OCN_HHH_P), OCN_F8(OCN_HHH_N),
+                  OCN_F8(OCN_SSH), OCN_F8(OCN_SSHP), OCN_F8(OCN_HHQ_REST)};
+}
+inline FusedA make_fused_a(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau)
+{
+    return FusedA{b->nx_start, b->ny_start, sw.full_free_surface > 0, sw.trans_terms > 0, sw.ksw_lat > 0,
+                  make_sw_update_ssh(b, ptr, tau), make_hh_update(b, ptr), make_uv_trans_vort(b, ptr),
+                  make_stress_components(b, ptr)};
+}
+inline FusedB make_fused_b(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau)
+{
+    return FusedB{sw.trans_terms > 0, sw.ksw_lat > 0, make_uv_trans(b, ptr), make_uv_diff2(b, ptr),
+                  make_sw_update_uv(b, ptr, tau)};
+}
+inline FusedC1 make_fused_c1(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, int32_t *nbad)
+{
+    return FusedC1{b->nx_start, b->nx_end, b->ny_start, b->ny_end, sw.full_free_surface > 0, (int *)nbad,
+                   make_sw_next_step(b, ptr, sw.time_smooth), make_hh_shift(b, ptr, sw.time_smooth)};
+}
+#undef OCN_F4
+#undef OCN_F8
+
+}  // namespace ocn

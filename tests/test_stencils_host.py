@@ -1,0 +1,149 @@
+"""The product's stencil functors (ocean_model_arch_amd/csrc/sw_stencils.h -- the code the HIP
+kernels run) executed on the host by tests/native/stencil_host.cpp with every array access
+bounds-checked, against the compiled reference's golden outputs.
+
+Catches, on the CPU and before anything reaches the GPU: out-of-bounds accesses (a GPU memory
+fault), write-set mistakes, arithmetic-order mistakes, and errors in the fused regrouping of
+the step (fused A/B/C1 + hh_init with three halo exchanges must give the reference's state bit
+for bit).  Halo exchanges between blocks use the oracle's block copies."""
+import ctypes as C
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.golden import cases
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "tests", "native", "libstencil_host.so")
+
+R4 = ["lu", "luu", "luh", "lcu", "lcv", "llu", "llv", "dx", "dy", "dxt", "dyt", "dxh", "dyh", "dxb", "dyb",
+      "rlh_s", "r_diss"]
+R8 = ["ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp", "vbrtr", "vbrtrn", "vbrtrp", "hhq", "hhq_p", "hhq_n",
+      "hhu", "hhu_p", "hhu_n", "hhv", "hhv_p", "hhv_n", "hhh", "hhh_p", "hhh_n", "hhq_rest", "vort", "str_t",
+      "str_s", "mu", "RHSx", "RHSy", "RHSx_adv", "RHSy_adv", "RHSx_dif", "RHSy_dif"]
+STAGE = {n: i for i, n in enumerate(cases.KERNEL_NAMES)}
+STAGE_IDS = {"sw_update_ssh": 0, "hh_update": 1, "uv_trans_vort": 2, "uv_trans": 3, "stress_components": 4,
+             "uv_diff2": 5, "sw_update_uv": 6, "sw_next_step": 7, "hh_shift": 8, "hh_init": 9}
+FUSED_A, FUSED_B, FUSED_C1, CHECK = 11, 12, 13, 10
+
+
+class Block(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("nx_start", "nx_end", "ny_start", "ny_end", "bnd_x1", "bnd_x2",
+                                         "bnd_y1", "bnd_y2")] + [("pitch", C.c_int64)]
+
+
+class SwParams(C.Structure):
+    _fields_ = [("full_free_surface", C.c_int32), ("trans_terms", C.c_int32), ("ksw_lat", C.c_int32),
+                ("time_smooth", C.c_double), ("lvisc_2", C.c_double)]
+
+
+@pytest.fixture(scope="module")
+def hst():
+    subprocess.check_call(["make", "-s", "-f", os.path.join(REPO, "tests", "native", "Makefile")], cwd=REPO)
+    L = C.CDLL(LIB)
+    L.hst_stage.restype = C.c_long
+    L.hst_stage.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.POINTER(SwParams), C.c_double,
+                            C.POINTER(C.c_int32)]
+    return L
+
+
+def table(arrs):
+    t = (C.c_void_p * (len(R4) + len(R8)))()
+    for i, n in enumerate(R4 + R8):
+        t[i] = arrs[n].ctypes.data
+    return t
+
+
+def blk(g):
+    nxs, nxe, nys, nye, bx1, bx2, by1, by2 = (int(v) for v in g)
+    return Block(nxs, nxe, nys, nye, bx1, bx2, by1, by2, bx2 - bx1 + 1)
+
+
+def bits_equal(a, b):
+    return np.ascontiguousarray(a.ravel(order="F")).tobytes() == np.ascontiguousarray(b.ravel(order="F")).tobytes()
+
+
+@pytest.mark.parametrize("geom", cases.KERNEL_GEOMS)
+def test_stage_functors_match_reference(hst, geom):
+    z = cases.load_kernels(geom)
+    b = blk(z["geom"])
+    sw = SwParams(int(z["full_free_surface"]), 1, 1, float(z["time_smooth"]), 1000.0)
+    bad = []
+    for kname in cases.KERNEL_NAMES:
+        arrs = {k[3:]: z[k].copy(order="F") for k in z.files if k.startswith("in/")}
+        nbad = C.c_int32(0)
+        oob = hst.hst_stage(STAGE_IDS[kname], C.byref(b), table(arrs), C.byref(sw), float(z["tau"]), C.byref(nbad))
+        assert oob == 0, f"{kname}: {oob} out-of-bounds accesses"
+        for nm in [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]:
+            if not bits_equal(arrs[nm], z[f"{kname}/{nm}"]):
+                bad.append(f"{kname}:{nm}")
+    assert not bad, bad
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a.ravel(order="F")).tobytes()).hexdigest()
+
+
+def host_step(hst, om, fused, nbad):
+    sw_o = om.sw
+    sw = SwParams(sw_o.full_free_surface, sw_o.trans_terms, sw_o.ksw_lat, sw_o.time_smooth, sw_o.lvisc_2)
+    blocks = [(Block(*b.args, b.bx2 - b.bx1 + 1), table(om.f[k])) for k, b in enumerate(om.blocks)]
+
+    def each(stage, tau=1.0):
+        for b, t in blocks:
+            oob = hst.hst_stage(stage, C.byref(b), t, C.byref(sw), tau, C.byref(nbad))
+            assert oob == 0, f"stage {stage}: {oob} out-of-bounds accesses"
+
+    if fused:
+        each(FUSED_A)
+        sa = ["sshn"] + (["hhu_n", "hhv_n", "hhh_n"] if sw.full_free_surface > 0 else []) + \
+             (["vort"] if sw.trans_terms > 0 else []) + (["str_t", "str_s"] if sw.ksw_lat > 0 else [])
+        for f in sa:
+            om.sync(f)
+        each(FUSED_B)
+        for f in (["hhu_p", "hhv_p", "hhh_p"] if sw.trans_terms > 0 else []) + ["vbrtrn", "ubrtrn"]:
+            om.sync(f)
+        each(FUSED_C1)
+        if sw.full_free_surface > 0:
+            each(STAGE_IDS["hh_init"])
+            for f in ("hhu", "hhv", "hhh"):
+                om.sync(f)
+    else:
+        syncs = {"sw_update_ssh": ["sshn"], "hh_update": ["hhu_n", "hhv_n", "hhh_n"], "uv_trans_vort": ["vort"],
+                 "uv_trans": ["hhu_p", "hhv_p", "hhh_p"], "stress_components": ["str_t", "str_s"],
+                 "sw_update_uv": ["vbrtrn", "ubrtrn"], "hh_init": ["hhu", "hhv", "hhh"]}
+        order = ["sw_update_ssh"] + (["hh_update"] if sw.full_free_surface > 0 else []) + \
+                (["uv_trans_vort", "uv_trans"] if sw.trans_terms > 0 else []) + \
+                (["stress_components", "uv_diff2"] if sw.ksw_lat > 0 else []) + ["sw_update_uv", "sw_next_step"] + \
+                (["hh_shift", "hh_init"] if sw.full_free_surface > 0 else [])
+        for st in order:
+            each(STAGE_IDS[st])
+            for f in syncs.get(st, []):
+                om.sync(f)
+        each(CHECK)
+
+
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "stages"])
+@pytest.mark.parametrize("name", cases.E2E_CASES)
+def test_host_step_matches_reference(hst, name, fused):
+    case = cases.load_e2e(name)
+    b = case["basin"]
+    om = O.OracleModel(O.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"],
+                                     rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"]),
+                       O.SWConfig(**case["sw"]), *case["bxy"]).init()
+    nbad = C.c_int32(0)
+    for _ in range(case["steps"]):
+        host_step(hst, om, fused, nbad)
+    assert nbad.value == 0
+    z = case["z"]
+    bad = []
+    for k, blkk in enumerate(om.blocks):
+        for nm, a in om.f[k].items():
+            key = f"b{blkk.bm}_{blkk.bn}/sha/{nm}"
+            if key in z.files and _sha(a) != str(z[key]):
+                bad.append(f"({blkk.bm},{blkk.bn}):{nm}")
+    assert not bad, f"{name}: {bad}"
