@@ -9,7 +9,7 @@
 
 // Rows of a block strip owned by one 64x4 workgroup (see sw_kernels.hip).
 #ifndef OCN_ROWS
-#define OCN_ROWS 32
+#define OCN_ROWS 8
 #endif
 
 // Minimum waves per SIMD requested from the register allocator for the stencil kernels.
