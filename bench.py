@@ -30,9 +30,18 @@ STAGE_BYTES = {"sw_update_ssh": 68, "hh_update": 96, "uv_trans_vort": 44, "uv_tr
                "stress_components": 72, "uv_diff2": 96, "sw_update_uv": 200, "sw_next_step": 132,
                "hh_shift": 176, "hh_init": 168}
 B_ALG = sum(STAGE_BYTES.values())
-# distinct arrays read + written once per interior cell by each fused launch
-FUSED_BYTES = {"fused_a": 180, "fused_b": 252, "fused_c1": 132, "hh_init": 168}
-B_FUSED = sum(FUSED_BYTES.values())
+# distinct arrays read + written once per interior cell by each fused launch (DESIGN.md "bytes"):
+# real(4) masks/metrics as 2-D arrays, or compact (1 mask byte per point, metrics per row);
+# steps other than the last of an ocn_ctx_step call skip dead stores (FusedB RHS*_adv/_dif,
+# HhInit hqp/hqn/hun/hvn/hhn), FULL_EXTRA more bytes on the last step.
+FUSED_BYTES = {False: {"fused_a": 180, "fused_b": 220, "fused_c1": 132, "hh_init": 128},
+               True: {"fused_a": 129, "fused_b": 169, "fused_c1": 121, "hh_init": 81}}
+FULL_EXTRA = {"fused_b": 32, "hh_init": 40}
+
+
+def fused_bytes(compact: bool, steps: int):
+    """Mean bytes per interior cell per launch over one ocn_ctx_step call of `steps` steps."""
+    return {k: v + FULL_EXTRA.get(k, 0) / steps for k, v in FUSED_BYTES[compact].items()}
 
 
 def dims_create(n: int):
@@ -88,13 +97,13 @@ def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for):
     return bool(ok)
 
 
-def load_traffic(stage: str, cells: int):
+def load_traffic(stage: str, cells: int, compact: bool):
     """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary (profiles/), or None."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
         rec = d["kernels"][stage]
-        if int(rec["cells"]) != cells:
+        if int(rec["cells"]) != cells or bool(rec.get("compact")) != compact:
             return None
         return float(rec["hbm_bytes_per_launch"])
     except Exception:
@@ -111,6 +120,7 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay steps as hipGraphs (single process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stages", action="store_true", help="run the 11 reference stages instead of the fused step")
+    ap.add_argument("--no-compact", action="store_true", help="fused step on the 2-D real(4) arrays")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -141,6 +151,7 @@ def main():
         model.attach_comm(uid_for())
         parity = multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for)
     model.set_fused(not args.stages)
+    model.set_compact(not args.no_compact)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -160,6 +171,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     times = model.stage_times()
+    compact = model.compact_active
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -170,7 +182,8 @@ def main():
     local_cells = model.interior_cells
     out = None
     if rank == 0:
-        kbytes = STAGE_BYTES if args.stages else FUSED_BYTES
+        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps)
+        b_path = sum(kbytes.values())
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:
@@ -179,10 +192,10 @@ def main():
             achieved = alg / (stage_ms[dom] * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": load_traffic(dom, local_cells),
-                    "alg_bytes_per_launch": alg, "launch_ms": round(stage_ms[dom], 4)}
+                    "traffic": load_traffic(dom, local_cells, compact),
+                    "alg_bytes_per_launch": int(alg), "launch_ms": round(stage_ms[dom], 4)}
         step_gbs = B_ALG * cells * args.steps / dt / 1e9 / world
-        moved = (B_ALG if args.stages else B_FUSED) * cells * args.steps / dt / 1e9 / world
+        moved = b_path * cells * args.steps / dt / 1e9 / world
         out = {"metric": METRIC, "value": value, "unit": "cell-updates/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
                "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
@@ -190,12 +203,13 @@ def main():
                "config": {"workload": f"{nxbox}x{nybox} box, {bx}x{by} blocks (1 per GPU), sw.par defaults, tau=1s",
                           "box": [nxbox, nybox], "blocks": [bx, by], "graph": bool(args.graph),
                           "step": "reference stages" if args.stages else "fused groups",
+                          "static_fields": "compact" if compact else "2-D arrays",
                           "parallelism": f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else "1 block"},
                "roofline": roof,
                "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),
                "step_alg_gbs_per_gpu": round(step_gbs, 1),
                "step_bytes_per_cell": {"reference_stages_B_alg": B_ALG,
-                                       "this_path": B_ALG if args.stages else B_FUSED},
+                                       "this_path": round(b_path, 1)},
                "step_moved_frac": round(moved / HBM_PEAK_GBS, 4),
                "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()}}
         if world > 1:

@@ -253,9 +253,17 @@ int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
  *  OCN_OPT_GRAPH: replay each step as one hipGraph (single-process runs).
  *  OCN_OPT_STAGE_TIMING: bracket every launch group with HIP events on the context stream.
  *  OCN_OPT_FUSED (default 1): ocn_ctx_step runs the step as 4 fused launch groups and 3 halo
- *  syncs (same results and final state bit for bit); 0 = the 11 envoke stages of the reference. */
+ *  syncs (same results and final state bit for bit); 0 = the 11 envoke stages of the reference.
+ *  OCN_OPT_COMPACT (default 1): the fused step reads the real(4) masks as one bit-packed byte
+ *  per point and the grid metrics as one value per row, when that is exact for the current
+ *  real(4) fields (checked when they were last set; same results bit for bit).  Handing out a
+ *  real(4) pointer with ocn_ctx_field disables this until it is set to 1 again, which also
+ *  rebuilds the tables from the fields at the next ocn_ctx_step.
+ * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
+ * the compact tables. */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
-enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4 };
+int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
+enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT). */
 enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_NUM_TIMERS };

@@ -139,6 +139,8 @@ struct LBlock {
     int nbr_rank[8], nbr_k[8], nbr_gid[8];
     void *slab = nullptr;
     std::array<void *, kNumSlots> ptr{};
+    uint8_t *bits = nullptr;           // compact static fields (sw_stencils.h): mask bytes
+    float *rows = nullptr;             // and metric row tables
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
@@ -166,9 +168,8 @@ struct ocn_ctx {
     std::map<std::vector<int>, HaloPlan> plans;
     bool initialized = false;
     bool use_graph = false;
-    hipGraphExec_t graph_exec = nullptr;
-    double graph_tau = 0.0;
-    int graph_check = -1;
+    struct Graph { hipGraphExec_t exec; double tau; bool check, last, compact; };
+    std::vector<Graph> graphs;         // one captured step per (tau, check, last step, compact)
     std::vector<void *> allocs;
     // per-stage HIP-event timing (OCN_OPT_STAGE_TIMING): pending (stage, start, stop) records
     bool stage_timing = false;
@@ -179,6 +180,11 @@ struct ocn_ctx {
     int64_t stage_n[OCN_NUM_TIMERS] = {0};
     bool fused = true;
     std::vector<int> sync_a, sync_b;
+    // compact static fields: requested (OCN_OPT_COMPACT), in use, stale (real(4) fields
+    // changed since they were built), or unusable because raw real(4) pointers were handed out
+    bool compact_req = true, compact = false, static_dirty = true;
+    mutable bool r4_escaped = false;
+    int32_t *d_flags = nullptr;
 };
 
 namespace ocn {
@@ -307,9 +313,18 @@ static int allocate(ocn_ctx *c)
             off += r4b;
         }
     }
+    for (LBlock &b : c->blocks) {
+        const size_t n = (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1);
+        const size_t nrow = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1) * (OCN_NUM_R4 - OCN_DX);   // metric row tables
+        HIPCHK(hipMalloc(&b.bits, n));
+        c->allocs.push_back(b.bits);
+        HIPCHK(hipMalloc(&b.rows, nrow * sizeof(float)));
+        c->allocs.push_back(b.rows);
+    }
     HIPCHK(hipMalloc(&c->d_nbad, 256));
     c->allocs.push_back(c->d_nbad);
     HIPCHK(hipMemsetAsync(c->d_nbad, 0, 256, c->stream));
+    c->d_flags = c->d_nbad + 32;
     return OCN_OK;
 }
 
@@ -642,25 +657,54 @@ static int one_step(ocn_ctx *c, double tau, bool check)
     return OCN_OK;
 }
 
+// (Re)builds the compact static fields when the real(4) fields may have changed, and decides
+// whether the fused step reads them (sw_stencils.h "compact static fields").  Synchronises
+// only when a rebuild was needed (once after init / an upload of a real(4) field).
+static int prepare_static(ocn_ctx *c)
+{
+    if (!c->compact_req || c->r4_escaped) { c->compact = false; return OCN_OK; }
+    if (!c->static_dirty) return OCN_OK;
+    HIPCHK(hipMemsetAsync(c->d_flags, 0, sizeof(int32_t), c->stream));
+    for (const LBlock &b : c->blocks) RC(launch_prepare(&b.g, b.ptr.data(), b.bits, b.rows, c->d_flags, c->stream));
+    int32_t flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->compact = flags == 0;
+    c->static_dirty = false;
+    return OCN_OK;
+}
+
 // Fused step (sw_kernels.hip "fused step groups"): 4 launches and 3 halo syncs per step,
-// bitwise the same state as one_step.
-static int one_step_fused(ocn_ctx *c, double tau, bool check)
+// bitwise the same state as one_step.  last = false skips stores no later kernel reads
+// (sw_stencils.h FusedB / HhInit `full`); the last step of every ocn_ctx_step call leaves the
+// full state.
+static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
 {
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
+    auto cp = [c](const LBlock &b, Compact &t) -> const Compact * {
+        t = Compact{b.bits, b.rows};
+        return c->compact ? &t : nullptr;
+    };
+    Compact t;
     RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-    for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), sw, tau, c->stream));
+    for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), sw, tau, c->stream));
     RC(timer_end(c, rec));
     RC(run_sync(c, c->sync_a));
     RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
-    for (const LBlock &b : c->blocks) RC(launch_fused_b(&b.g, b.ptr.data(), sw, tau, c->stream));
+    for (const LBlock &b : c->blocks) RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), sw, tau, last, c->stream));
     RC(timer_end(c, rec));
     RC(run_sync(c, c->sync_b));
     RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
     for (const LBlock &b : c->blocks)
-        RC(launch_fused_c1(&b.g, b.ptr.data(), sw, check ? c->d_nbad : nullptr, c->stream));
+        RC(launch_fused_c1(&b.g, b.ptr.data(), cp(b, t), sw, check ? c->d_nbad : nullptr, c->stream));
     RC(timer_end(c, rec));
-    if (sw.full_free_surface > 0) RC(envoke(c, OCN_STAGE_HH_INIT, tau));
+    if (sw.full_free_surface > 0) {
+        RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
+        for (const LBlock &b : c->blocks) RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), sw, last, c->stream));
+        RC(timer_end(c, rec));
+        RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
+    }
     return OCN_OK;
 }
 
@@ -786,6 +830,7 @@ static int init_state(ocn_ctx *c)
         HostBlock h(b.g);
         host_grid(c, h);
         for (int id = 0; id < OCN_NUM_R4; ++id) RC(upload_field(c, b, id, h.r4[id].data(), false));
+        c->static_dirty = true;
         std::vector<double> r8(h.r4[0].size(), 100.0);      // init_data.f90:112-114 hhq_rest = 100 m
         RC(upload_field(c, b, OCN_HHQ_REST, r8.data(), false));
         std::fill(r8.begin(), r8.end(), 0.0);
@@ -920,7 +965,7 @@ int ocn_ctx_destroy(ocn_ctx *c)
     if (!c) return OCN_OK;
     (void)hipSetDevice(c->dec.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    for (auto &g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto &r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -948,6 +993,7 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
         set_error(OCN_ERR_ARG, "bad block index or field id");
         return nullptr;
     }
+    if (is_r4(id)) c->r4_escaped = true;   // may be written behind our back: no compact tables
     return c->blocks[k].ptr[field_slot(id)];
 }
 
@@ -994,20 +1040,38 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     return envoke(c, stage_id, tau);
 }
 
-static int capture_step(ocn_ctx *c, double tau, bool check)
+static void drop_graphs(ocn_ctx *c)
 {
+    for (auto &g : c->graphs) (void)hipGraphExecDestroy(g.exec);
+    c->graphs.clear();
+}
+
+static int run_step(ocn_ctx *c, double tau, bool check, bool last)
+{
+    return c->fused ? one_step_fused(c, tau, check, last) : one_step(c, tau, check);
+}
+
+// one step as a replayed hipGraph, captured once per (tau, check, last, compact)
+static int graph_step(ocn_ctx *c, double tau, bool check, bool last)
+{
+    for (const auto &g : c->graphs)
+        if (g.tau == tau && g.check == check && g.last == last && g.compact == c->compact) {
+            HIPCHK(hipGraphLaunch(g.exec, c->stream));
+            return OCN_OK;
+        }
+    if (c->graphs.size() >= 8) drop_graphs(c);
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = c->fused ? one_step_fused(c, tau, check) : one_step(c, tau, check);
+    int rc = run_step(c, tau, check, last);
     hipError_t e = hipStreamEndCapture(c->stream, &graph);
     if (rc) return rc;
     HIPCHK(e);
-    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
-    e = hipGraphInstantiate(&c->graph_exec, graph, nullptr, nullptr, 0);
+    hipGraphExec_t exec;
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     HIPCHK(e);
-    c->graph_tau = tau;
-    c->graph_check = check;
+    c->graphs.push_back(ocn_ctx::Graph{exec, tau, check, last, c->compact});
+    HIPCHK(hipGraphLaunch(exec, c->stream));
     return OCN_OK;
 }
 
@@ -1016,17 +1080,13 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
     if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
+    if (c->fused) RC(prepare_static(c));
+    const bool graph_ok = c->use_graph && !c->comm && !c->stage_timing;   // RCCL / events stay outside graphs
     for (int s = 1; s <= nsteps; ++s) {
         const bool check = check_every > 0 && (s % check_every == 0);
-        const bool graph_ok = c->use_graph && !c->comm && !c->stage_timing;   // RCCL / events stay outside graphs
-        if (graph_ok) {
-            if (!c->graph_exec || c->graph_tau != tau || c->graph_check != (int)check) RC(capture_step(c, tau, check));
-            HIPCHK(hipGraphLaunch(c->graph_exec, c->stream));
-        } else if (c->fused) {
-            RC(one_step_fused(c, tau, check));
-        } else {
-            RC(one_step(c, tau, check));
-        }
+        const bool last = s == nsteps;
+        if (graph_ok) RC(graph_step(c, tau, check, last));
+        else RC(run_step(c, tau, check, last));
     }
     return OCN_OK;
 }
@@ -1078,6 +1138,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !(is_r4(id) || is_r8(id)))
         return set_error(OCN_ERR_ARG, "upload: bad argument");
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (is_r4(id)) c->static_dirty = true;
     return upload_field(c, c->blocks[k], id, host, false);
 }
 
@@ -1088,9 +1149,26 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     case OCN_OPT_GRAPH: c->use_graph = value != 0; return OCN_OK;
     case OCN_OPT_STAGE_TIMING: c->stage_timing = value != 0; return OCN_OK;
     case OCN_OPT_FUSED:
-        if (c->fused != (value != 0) && c->graph_exec) { (void)hipGraphExecDestroy(c->graph_exec); c->graph_exec = nullptr; }
+        if (c->fused != (value != 0)) drop_graphs(c);
         c->fused = value != 0;
         return OCN_OK;
+    case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
+        c->compact_req = value != 0;
+        c->r4_escaped = false;
+        c->static_dirty = true;
+        return OCN_OK;
+    default: return set_error(OCN_ERR_ARG, "unknown option");
+    }
+}
+
+int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
+{
+    if (!c || !value) return set_error(OCN_ERR_ARG, "null argument");
+    switch (key) {
+    case OCN_OPT_GRAPH: *value = c->use_graph; return OCN_OK;
+    case OCN_OPT_STAGE_TIMING: *value = c->stage_timing; return OCN_OK;
+    case OCN_OPT_FUSED: *value = c->fused; return OCN_OK;
+    case OCN_OPT_COMPACT: *value = c->fused && c->compact; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -29,10 +29,25 @@ inline bool is_r4(int id) { return id >= 0 && id < OCN_NUM_R4; }
 inline int field_slot(int id) { return is_r4(id) ? id : OCN_NUM_R4 + (id - OCN_SSH); }
 constexpr int kNumSlots = OCN_NUM_R4 + OCN_NUM_R8;
 
-// Fused step groups (sw_kernels.hip); `ptr` = the block's field table indexed by field_slot().
-int launch_fused_a(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s);
-int launch_fused_b(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s);
-int launch_fused_c1(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, int32_t *nbad, hipStream_t s);
+// A block's compact static fields (sw_stencils.h): mask bytes (pitch x rows) and metric rows.
+struct Compact {
+    const uint8_t *bits;
+    const float *rows;
+};
+
+// Fused step groups (sw_kernels.hip); `ptr` = the block's field table indexed by field_slot(),
+// `cp` = its compact tables or nullptr for the 2-D real(4) arrays.
+int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, double tau,
+                   hipStream_t s);
+int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, double tau,
+                   bool full, hipStream_t s);
+int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw,
+                    int32_t *nbad, hipStream_t s);
+int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, bool full,
+                    hipStream_t s);
+// Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
+// they cannot be used into *flags (device int).
+int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s);
 int check_hip(hipError_t e, const char *what);
 inline int check_launch() { return check_hip(hipGetLastError(), "kernel launch"); }
 

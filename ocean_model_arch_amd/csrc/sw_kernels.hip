@@ -34,7 +34,9 @@ __global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range(int m0, int m1, int
     if (m > m1) return;
     const int nb = n0 + (int)blockIdx.y * OCN_ROWS;
     const int ne = min(n1, nb + OCN_ROWS - 1);
-    for (int n = nb + (int)threadIdx.y; n <= ne; n += 4) body(m, n);
+    // a wave is one 64-lane thread-row: its row index is wave-uniform (scalar registers)
+    const int ty = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
+    for (int n = nb + ty; n <= ne; n += 4) body(m, n);
 }
 
 template <typename Body>
@@ -81,28 +83,74 @@ static int nonnull(std::initializer_list<const void *> ps)
 #define RC_K(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
 
 // ------------------------------------------------------------------ fused launches
-int launch_fused_a(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s)
+// cp == nullptr: the real(4) fields are read from the 2-D arrays; otherwise from the block's
+// compact tables (sw_stencils.h "compact static fields", built by launch_prepare).
+template <template <bool> class Make, typename... A>
+static int launch_fused(const Range &r, const ocn_block *b, void *const *ptr, const Compact *cp, hipStream_t s,
+                        A... a)
 {
     RC_K(check_block(b));
-    const FusedA k = make_fused_a(b, ptr, sw, tau);
-    const Range r = range_fused_a(b, sw);
-    return launch_range(r.m0, r.m1, r.n0, r.n1, k, s);
+    if (cp) {
+        const Tab<true> t{ptr, cp->bits, cp->rows, block_rows(b)};
+        return launch_range(r.m0, r.m1, r.n0, r.n1, Make<true>::make(b, t, a...), s);
+    }
+    const Tab<false> t{ptr};
+    return launch_range(r.m0, r.m1, r.n0, r.n1, Make<false>::make(b, t, a...), s);
+}
+template <bool C> struct MkA {
+    static FusedA<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau)
+    {
+        return make_fused_a(b, t, sw, tau);
+    }
+};
+template <bool C> struct MkB {
+    static FusedB<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau, bool full)
+    {
+        return make_fused_b(b, t, sw, tau, full);
+    }
+};
+template <bool C> struct MkC1 {
+    static FusedC1<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, int32_t *nbad)
+    {
+        return make_fused_c1(b, t, sw, nbad);
+    }
+};
+template <bool C> struct MkC2 {
+    static HhInit<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, bool full)
+    {
+        return make_hh_init(b, t, sw.full_free_surface, full);
+    }
+};
+
+int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, double tau,
+                   hipStream_t s)
+{
+    return launch_fused<MkA>(range_fused_a(b, sw), b, ptr, cp, s, sw, tau);
 }
 
-int launch_fused_b(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau, hipStream_t s)
+int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, double tau,
+                   bool full, hipStream_t s)
 {
-    RC_K(check_block(b));
-    const FusedB k = make_fused_b(b, ptr, sw, tau);
-    const Range r = range_interior(b);
-    return launch_range(r.m0, r.m1, r.n0, r.n1, k, s);
+    return launch_fused<MkB>(range_interior(b), b, ptr, cp, s, sw, tau, full);
 }
 
-int launch_fused_c1(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, int32_t *nbad, hipStream_t s)
+int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw,
+                    int32_t *nbad, hipStream_t s)
+{
+    return launch_fused<MkC1>(range_ring(b), b, ptr, cp, s, sw, nbad);
+}
+
+int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, bool full,
+                    hipStream_t s)
+{
+    return launch_fused<MkC2>(range_bnd(b), b, ptr, cp, s, sw, full);
+}
+
+int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s)
 {
     RC_K(check_block(b));
-    const FusedC1 k = make_fused_c1(b, ptr, sw, nbad);
-    const Range r = range_ring(b);
-    return launch_range(r.m0, r.m1, r.n0, r.n1, k, s);
+    const Range r = range_bnd(b);
+    return launch_range(r.m0, r.m1, r.n0, r.n1, make_prepare(b, ptr, bits, rows, (int *)flags), s);
 }
 
 }  // namespace ocn
@@ -116,7 +164,7 @@ int ocn_sw_update_ssh(const ocn_block *b, double tau, const float *lu, const flo
                       const double *sshp, const double *ubrtr, const double *vbrtr, void *stream)
 {
     CHECK(lu, dx, dy, dxh, dyh, hhu, hhv, sshn, sshp, ubrtr, vbrtr);
-    SwUpdateSsh k{geo(b), tau, lu, dx, dy, dxh, dyh, hhu, hhv, sshn, sshp, ubrtr, vbrtr};
+    SwUpdateSsh<false> k{geo(b), tau, lu, dx, dy, dxh, dyh, hhu, hhv, sshn, sshp, ubrtr, vbrtr};
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
 }
 
@@ -126,8 +174,8 @@ int ocn_hh_update(const ocn_block *b, const float *lu, const float *llu, const f
                   double *hhn, const double *sh, const double *h_r, void *stream)
 {
     CHECK(lu, llu, llv, luh, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, hqn, hun, hvn, hhn, sh, h_r);
-    HhUpdate k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end,
-               Interp{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh, hqn, hun, hvn, hhn, sh, h_r};
+    HhUpdate<false> k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end,
+               Interp<false>{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh, hqn, hun, hvn, hhn, sh, h_r};
     return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream);
 }
 
@@ -135,7 +183,7 @@ int ocn_uv_trans_vort(const ocn_block *b, const float *luu, const float *dxt, co
                       const float *dyb, const double *u, const double *v, double *vort, void *stream)
 {
     CHECK(luu, dxt, dyt, dxb, dyb, u, v, vort);
-    UvTransVort k{geo(b), luu, dxt, dyt, dxb, dyb, u, v, vort};
+    UvTransVort<false> k{geo(b), luu, dxt, dyt, dxb, dyb, u, v, vort};
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
 }
 
@@ -145,7 +193,7 @@ int ocn_uv_trans(const ocn_block *b, const float *lcu, const float *lcv, const f
 {
     (void)hq;
     CHECK(lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy);
-    UvTrans k{geo(b), lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy};
+    UvTrans<false> k{geo(b), lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy};
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
 }
 
@@ -155,7 +203,7 @@ int ocn_stress_components(const ocn_block *b, const float *lu, const float *luu,
                           void *stream)
 {
     CHECK(lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s);
-    StressComponents k{geo(b), lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s};
+    StressComponents<false> k{geo(b), lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s};
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
 }
 
@@ -166,7 +214,7 @@ int ocn_uv_diff2(const ocn_block *b, const float *lcu, const float *lcv, const f
 {
     (void)hu; (void)hv;
     CHECK(lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy);
-    UvDiff2 k{geo(b), lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy};
+    UvDiff2<false> k{geo(b), lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy};
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
 }
 
@@ -181,7 +229,7 @@ int ocn_sw_update_uv(const ocn_block *b, double tau, const float *lcu, const flo
 {
     CHECK(lcu, lcv, dxt, dyt, dxh, dyh, dxb, dyb, hhu, hhun, hhup, hhv, hhvn, hhvp, hhh, ssh, ubrtr, ubrtrn,
           ubrtrp, vbrtr, vbrtrn, vbrtrp, rdis, rlh_s, RHSx, RHSy, RHSx_adv, RHSy_adv, RHSx_dif, RHSy_dif);
-    SwUpdateUv k{geo(b), tau, lcu, lcv, dxt, dyt, dxh, dyh, dxb, dyb, hhu, hhun, hhup, hhv, hhvn, hhvp, hhh, ssh,
+    SwUpdateUv<false> k{geo(b), tau, lcu, lcv, dxt, dyt, dxh, dyh, dxb, dyb, hhu, hhun, hhup, hhv, hhvn, hhvp, hhh, ssh,
                  ubrtr, ubrtrn, ubrtrp, vbrtr, vbrtrn, vbrtrp, rdis, rlh_s, RHSx, RHSy, RHSx_adv, RHSy_adv,
                  RHSx_dif, RHSy_dif};
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
@@ -192,7 +240,7 @@ int ocn_sw_next_step(const ocn_block *b, double time_smooth, const float *lu, co
                      double *vbrtr, double *vbrtrn, double *vbrtrp, void *stream)
 {
     CHECK(lu, lcu, lcv, ssh, sshn, sshp, ubrtr, ubrtrn, ubrtrp, vbrtr, vbrtrn, vbrtrp);
-    SwNextStep k{geo(b), time_smooth, lu, lcu, lcv, ssh, sshn, sshp, ubrtr, ubrtrn, ubrtrp, vbrtr, vbrtrn, vbrtrp};
+    SwNextStep<false> k{geo(b), time_smooth, lu, lcu, lcv, ssh, sshn, sshp, ubrtr, ubrtrn, ubrtrp, vbrtr, vbrtrn, vbrtrp};
     return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream);
 }
 
@@ -201,7 +249,7 @@ int ocn_hh_shift(const ocn_block *b, double time_smooth, const float *lu, const 
                  double *hv, double *hvp, double *hvn, double *hh, double *hhp, double *hhn, void *stream)
 {
     CHECK(lu, llu, llv, luh, hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn);
-    HhShift k{geo(b), time_smooth, lu, llu, llv, luh, hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn};
+    HhShift<false> k{geo(b), time_smooth, lu, llu, llv, luh, hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn};
     return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream);
 }
 
@@ -214,8 +262,8 @@ int ocn_hh_init(const ocn_block *b, int32_t full_free_surface, const float *lu, 
 {
     CHECK(lu, llu, llv, luh, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh,
           hhp, hhn, sh, shp, h_r);
-    HhInit k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)full_free_surface,
-             Interp{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh,
+    HhInit<false> k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)full_free_surface, true,
+             Interp<false>{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh,
              hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn, sh, shp, h_r};
     return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream);
 }
@@ -223,7 +271,7 @@ int ocn_hh_init(const ocn_block *b, int32_t full_free_surface, const float *lu, 
 int ocn_check_ssh_err(const ocn_block *b, const float *lu, const double *ssh, int32_t *nbad_device, void *stream)
 {
     CHECK(lu, ssh, nbad_device);
-    CheckSshErr k{geo(b), lu, ssh, (int *)nbad_device};
+    CheckSshErr<false> k{geo(b), lu, ssh, (int *)nbad_device};
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
 }
 

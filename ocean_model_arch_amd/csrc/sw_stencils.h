@@ -1,7 +1,15 @@
 // sw_stencils.h -- the per-cell arithmetic of the SW step stages (functors), shared by the
 // HIP kernels (sw_kernels.hip, compiled for gfx950) and the host-side memory-safety /
-// parity harness (tests/native/stencil_host.cpp, compiled with g++ -fsanitize=address).
+// parity harness (tests/native/stencil_host.cpp).
 // Each functor restates one reference loop nest (kernel/shallow_water/*.f90) bit for bit.
+//
+// Every functor is a template on C ("compact static fields"):
+//   C = false  the real(4) masks and grid metrics are the reference's 2-D block arrays;
+//   C = true   the 7 masks are bits of one byte per point and the 10 metric fields that are
+//              constant along each row over [nx_start-1, nx_end+1] are one value per row
+//              (built by Prepare below; exact -- masks hold only 0.0/1.0, row values are
+//              the array's own bit patterns -- and used only when that was verified).
+// The arithmetic is identical in both; only where a real(4) operand is read from differs.
 #pragma once
 
 #include <stdint.h>
@@ -17,20 +25,33 @@
 #ifndef OCN_ATOMIC_INC
 #define OCN_ATOMIC_INC(p) atomicAdd((p), 1)
 #endif
+#ifndef OCN_ATOMIC_OR
+#define OCN_ATOMIC_OR(p, v) atomicOr((p), (v))
+#endif
 #ifndef OCN_FREE_FALL_ACC
 #define OCN_FREE_FALL_ACC 9.8f   // shared/constants.f90:23 FreeFallAcc = 9.8 (real(4))
 #endif
 
 namespace ocn {
 
-// Element index of A(m, n) in a block array: 32-bit (the host checks pitch * rows < 2^31).
+// A point of a block array: element index of A(m, n) (32-bit; the host checks pitch * rows
+// < 2^29) and row index n - bnd_y1.
+struct Pt {
+    unsigned c, r;
+};
+
 struct Geo {
     int bx1, by1;
     unsigned p;
-    OCN_HD OCN_INLINE unsigned operator()(int m, int n) const
+    OCN_HD OCN_INLINE Pt operator()(int m, int n) const
     {
-        return (unsigned)(m - bx1) + (unsigned)(n - by1) * p;
+        const unsigned r = (unsigned)(n - by1);
+        return Pt{(unsigned)(m - bx1) + r * p, r};
     }
+    OCN_HD OCN_INLINE Pt e(Pt q) const { return Pt{q.c + 1, q.r}; }
+    OCN_HD OCN_INLINE Pt w(Pt q) const { return Pt{q.c - 1, q.r}; }
+    OCN_HD OCN_INLINE Pt n(Pt q) const { return Pt{q.c + p, q.r + 1}; }
+    OCN_HD OCN_INLINE Pt s(Pt q) const { return Pt{q.c - p, q.r - 1}; }
 };
 
 #define D(x) ((double)(x))
@@ -56,19 +77,40 @@ template <class T> OCN_HD OCN_INLINE void st(T *__restrict__ p, unsigned i, T v)
     OCN_CHECK_INDEX(i);
     *(T *)((char *)p + i * (unsigned)sizeof(T)) = v;
 }
+template <class T> OCN_HD OCN_INLINE T ld(const T *__restrict__ p, Pt q) { return ld(p, q.c); }
+template <class T> OCN_HD OCN_INLINE void st(T *__restrict__ p, Pt q, T v) { st(p, q.c, v); }
 
+// real(4) mask (lu, luu, luh, lcu, lcv, llu, llv) and grid-metric fields
+template <bool C> struct Msk;
+template <> struct Msk<false> { const float *__restrict__ a; };
+template <> struct Msk<true> { const uint8_t *__restrict__ a; unsigned bit; };
+template <bool C> struct Met;
+template <> struct Met<false> { const float *__restrict__ a; };
+template <> struct Met<true> { const float *__restrict__ a; };   // indexed by row
+
+OCN_HD OCN_INLINE float ld(const Msk<false> &f, Pt q) { return ld(f.a, q.c); }
+OCN_HD OCN_INLINE float ld(const Msk<true> &f, Pt q) { return (ld(f.a, q.c) & f.bit) ? 1.0f : 0.0f; }
+OCN_HD OCN_INLINE float ld(const Met<false> &f, Pt q) { return ld(f.a, q.c); }
+OCN_HD OCN_INLINE float ld(const Met<true> &f, Pt q) { return ld(f.a, q.r); }
+
+OCN_HD OCN_INLINE uint32_t fbits(float f)
+{
+    uint32_t u;
+    __builtin_memcpy(&u, &f, sizeof(u));
+    return u;
+}
 
 // ------------------------------------------------------------------ a1 sw_update_ssh
 // vel_ssh.f90:69-106
-struct SwUpdateSsh {
+template <bool C> struct SwUpdateSsh {
     Geo I; double tau;
-    const float *__restrict__ lu, *__restrict__ dx, *__restrict__ dy, *__restrict__ dxh, *__restrict__ dyh;
+    Msk<C> lu; Met<C> dx, dy, dxh, dyh;
     const double *__restrict__ hhu, *__restrict__ hhv;
     double *__restrict__ sshn;
     const double *__restrict__ sshp, *__restrict__ ubrtr, *__restrict__ vbrtr;
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n), w = c - 1, s = c - I.p;
+        const Pt c = I(m, n), w = I.w(c), s = I.s(c);
         const double t1 = ld(ubrtr, c) * ld(hhu, c) * D(ld(dyh, c));
         const double t2 = ld(ubrtr, w) * ld(hhu, w) * D(ld(dyh, w));
         const double t3 = ld(vbrtr, c) * ld(hhv, c) * D(ld(dxh, c));
@@ -83,24 +125,21 @@ struct SwUpdateSsh {
 // ------------------------------------------------------------------ T->U/V/H interpolation
 // kernel/shallow_water/depth.f90:56-97 for one level given its values at the four corners
 // (m,n), (m+1,n), (m,n+1), (m+1,n+1).
-struct Interp {
-    const float *__restrict__ lu, *__restrict__ dx, *__restrict__ dy;
-    const float *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxh, *__restrict__ dyh;
-    const float *__restrict__ dxb, *__restrict__ dyb;
+template <bool C> struct Interp {
+    Msk<C> lu; Met<C> dx, dy, dxt, dyt, dxh, dyh, dxb, dyb;
     // per-corner weights dx*dy*lu (products evaluated per use, as the reference does)
-    OCN_HD OCN_INLINE double wt(double h, unsigned i) const { return h * D(ld(dx, i)) * D(ld(dy, i)) * D(ld(lu, i)); }
-    OCN_HD OCN_INLINE double u(double h00, double h10, unsigned c, unsigned e) const
+    OCN_HD OCN_INLINE double wt(double h, Pt i) const { return h * D(ld(dx, i)) * D(ld(dy, i)) * D(ld(lu, i)); }
+    OCN_HD OCN_INLINE double u(double h00, double h10, Pt c, Pt e) const
     {
         const double slu = D(ld(lu, c) + ld(lu, e));
         return (wt(h00, c) + wt(h10, e)) / slu / D(ld(dxt, c)) / D(ld(dyh, c));
     }
-    OCN_HD OCN_INLINE double v(double h00, double h01, unsigned c, unsigned nn) const
+    OCN_HD OCN_INLINE double v(double h00, double h01, Pt c, Pt nn) const
     {
         const double slu = D(ld(lu, c) + ld(lu, nn));
         return (wt(h00, c) + wt(h01, nn)) / slu / D(ld(dxh, c)) / D(ld(dyt, c));
     }
-    OCN_HD OCN_INLINE double h(double h00, double h10, double h01, double h11, unsigned c, unsigned e,
-                                        unsigned nn, unsigned ne) const
+    OCN_HD OCN_INLINE double h(double h00, double h10, double h01, double h11, Pt c, Pt e, Pt nn, Pt ne) const
     {
         const double slu = D(ld(lu, c) + ld(lu, e) + ld(lu, nn) + ld(lu, ne));
         return (wt(h00, c) + wt(h10, e) + wt(h01, nn) + wt(h11, ne)) / slu / D(ld(dxb, c)) / D(ld(dyb, c));
@@ -110,16 +149,16 @@ struct Interp {
 // ------------------------------------------------------------------ a2 hh_update
 // depth.f90:101-162.  Thread grid = whole bnd range (hqn = h_r + sh, :129); the
 // interpolation part runs on [start-1, end]^2.
-struct HhUpdate {
+template <bool C> struct HhUpdate {
     Geo I; int i0, i1, j0, j1;
-    Interp W;
-    const float *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
+    Interp<C> W;
+    Msk<C> llu, llv, luh;
     double *__restrict__ hqn, *__restrict__ hun, *__restrict__ hvn, *__restrict__ hhn;
     const double *__restrict__ sh, *__restrict__ h_r;
     // the [start-1, end]^2 interpolation part (depth.f90:134-160); q = h_r + sh at each corner
-    OCN_HD OCN_INLINE void interp(unsigned c, double q00) const
+    OCN_HD OCN_INLINE void interp(Pt c, double q00) const
     {
-        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1;
+        const Pt e = I.e(c), nn = I.n(c), ne = I.e(nn);
         const double q10 = ld(h_r, e) + ld(sh, e), q01 = ld(h_r, nn) + ld(sh, nn), q11 = ld(h_r, ne) + ld(sh, ne);
         const double xu = W.u(q00, q10, c, e);
         const double xv = W.v(q00, q01, c, nn);
@@ -130,7 +169,7 @@ struct HhUpdate {
     }
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n);
+        const Pt c = I(m, n);
         const double q00 = ld(h_r, c) + ld(sh, c);
         st(hqn, c, q00);
         if (m < i0 || m > i1 || n < j0 || n > j1) return;
@@ -141,10 +180,17 @@ struct HhUpdate {
 // ------------------------------------------------------------------ a10 hh_init
 // depth.f90:14-99: hq = h_r + sh*ffs, hqp = h_r + shp*ffs, hqn = h_r (whole array), then the
 // three levels interpolated on [start-1, end]^2.
-struct HhInit {
-    Geo I; int i0, i1, j0, j1; double f;
-    Interp W;
-    const float *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
+// full = false (fused step, every step of an ocn_ctx_step call but the last) skips stores
+// whose values no later kernel reads before they are rewritten:
+//   hqn = h_r and hun/hvn/hhn = interp(h_r): hqn is never changed by the fused step (fused A
+//     does not store hh_update's hqn), and hun/hvn/hhn are rewritten on exactly these points
+//     by the next step's hh_update before anything reads them;
+//   hqp: read only by hh_shift's hq/hqp update, whose results this kernel overwrites
+//     whole-array one launch later.
+template <bool C> struct HhInit {
+    Geo I; int i0, i1, j0, j1; double f; bool full;
+    Interp<C> W;
+    Msk<C> llu, llv, luh;
     double *__restrict__ hq, *__restrict__ hqp, *__restrict__ hqn;
     double *__restrict__ hu, *__restrict__ hup, *__restrict__ hun;
     double *__restrict__ hv, *__restrict__ hvp, *__restrict__ hvn;
@@ -152,35 +198,42 @@ struct HhInit {
     const double *__restrict__ sh, *__restrict__ shp, *__restrict__ h_r;
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n);
+        const Pt c = I(m, n);
         const double r00 = ld(h_r, c);
         const double a00 = r00 + ld(sh, c) * f, b00 = r00 + ld(shp, c) * f;
-        st(hq, c, a00); st(hqp, c, b00); st(hqn, c, r00);
+        st(hq, c, a00);
+        if (full) { st(hqp, c, b00); st(hqn, c, r00); }
         if (m < i0 || m > i1 || n < j0 || n > j1) return;
-        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1;
+        const Pt e = I.e(c), nn = I.n(c), ne = I.e(nn);
         const double r10 = ld(h_r, e), r01 = ld(h_r, nn), r11 = ld(h_r, ne);
         const double a10 = r10 + ld(sh, e) * f, a01 = r01 + ld(sh, nn) * f, a11 = r11 + ld(sh, ne) * f;
         const double b10 = r10 + ld(shp, e) * f, b01 = r01 + ld(shp, nn) * f, b11 = r11 + ld(shp, ne) * f;
-        const double u0 = W.u(a00, a10, c, e), u1 = W.u(b00, b10, c, e), u2 = W.u(r00, r10, c, e);
-        const double v0 = W.v(a00, a01, c, nn), v1 = W.v(b00, b01, c, nn), v2 = W.v(r00, r01, c, nn);
-        const double h0 = W.h(a00, a10, a01, a11, c, e, nn, ne), h1 = W.h(b00, b10, b01, b11, c, e, nn, ne),
-                     h2 = W.h(r00, r10, r01, r11, c, e, nn, ne);
-        if (ld(llu, c) > 0.5f) { st(hu, c, u0); st(hup, c, u1); st(hun, c, u2); }
-        if (ld(llv, c) > 0.5f) { st(hv, c, v0); st(hvp, c, v1); st(hvn, c, v2); }
-        if (ld(luh, c) > 0.5f) { st(hh, c, h0); st(hhp, c, h1); st(hhn, c, h2); }
+        const double u0 = W.u(a00, a10, c, e), u1 = W.u(b00, b10, c, e);
+        const double v0 = W.v(a00, a01, c, nn), v1 = W.v(b00, b01, c, nn);
+        const double h0 = W.h(a00, a10, a01, a11, c, e, nn, ne), h1 = W.h(b00, b10, b01, b11, c, e, nn, ne);
+        const bool bu = ld(llu, c) > 0.5f, bv = ld(llv, c) > 0.5f, bh = ld(luh, c) > 0.5f;
+        if (bu) { st(hu, c, u0); st(hup, c, u1); }
+        if (bv) { st(hv, c, v0); st(hvp, c, v1); }
+        if (bh) { st(hh, c, h0); st(hhp, c, h1); }
+        if (full) {
+            const double u2 = W.u(r00, r10, c, e), v2 = W.v(r00, r01, c, nn), h2 = W.h(r00, r10, r01, r11, c, e, nn, ne);
+            if (bu) st(hun, c, u2);
+            if (bv) st(hvn, c, v2);
+            if (bh) st(hhn, c, h2);
+        }
     }
 };
 
 // ------------------------------------------------------------------ a3 uv_trans_vort
 // vel_ssh.f90:247-281
-struct UvTransVort {
+template <bool C> struct UvTransVort {
     Geo I;
-    const float *__restrict__ luu, *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxb, *__restrict__ dyb;
+    Msk<C> luu; Met<C> dxt, dyt, dxb, dyb;
     const double *__restrict__ u, *__restrict__ v;
     double *__restrict__ vort;
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n), e = c + 1, nn = c + I.p;
+        const Pt c = I(m, n), e = I.e(c), nn = I.n(c);
         const double a = ld(v, e) * D(ld(dyt, e)) - ld(v, c) * D(ld(dyt, c));
         const double b = ld(u, nn) * D(ld(dxt, nn)) - ld(u, c) * D(ld(dxt, c));
         const double d = (ld(v, e) - ld(v, c)) * D(ld(dyb, c)) - (ld(u, nn) - ld(u, c)) * D(ld(dxb, c));
@@ -191,15 +244,15 @@ struct UvTransVort {
 
 // ------------------------------------------------------------------ a4 uv_trans
 // vel_ssh.f90:283-373
-struct UvTrans {
+template <bool C> struct UvTrans {
     Geo I;
-    const float *__restrict__ lcu, *__restrict__ lcv, *__restrict__ luu, *__restrict__ dxh, *__restrict__ dyh;
+    Msk<C> lcu, lcv, luu; Met<C> dxh, dyh;
     const double *__restrict__ u, *__restrict__ v, *__restrict__ vort;
     const double *__restrict__ hu, *__restrict__ hv, *__restrict__ hh;
     double *__restrict__ RHSx, *__restrict__ RHSy;
-    OCN_HD OCN_INLINE void eval(unsigned c, double &rx, double &ry) const
+    OCN_HD OCN_INLINE void eval(Pt c, double &rx, double &ry) const
     {
-        const unsigned e = c + 1, w = c - 1, nn = c + I.p, s = c - I.p, se = s + 1, wn = nn - 1;
+        const Pt e = I.e(c), w = I.w(c), nn = I.n(c), s = I.s(c), se = I.e(s), wn = I.w(nn);
         {
             const double fu_c = ld(u, c) * D(ld(dyh, c)) * ld(hu, c);
             const double fx_p = (fu_c + ld(u, e) * D(ld(dyh, e)) * ld(hu, e)) / 2.0 * (ld(u, c) + ld(u, e)) / 2.0;
@@ -225,7 +278,7 @@ struct UvTrans {
     }
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n);
+        const Pt c = I(m, n);
         double rx, ry;
         eval(c, rx, ry);
         if (ld(lcu, c) > 0.5f) st(RHSx, c, rx);
@@ -235,16 +288,14 @@ struct UvTrans {
 
 // ------------------------------------------------------------------ a5 stress_components
 // mixing.f90:14-58
-struct StressComponents {
+template <bool C> struct StressComponents {
     Geo I;
-    const float *__restrict__ lu, *__restrict__ luu, *__restrict__ dx, *__restrict__ dy;
-    const float *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxh, *__restrict__ dyh;
-    const float *__restrict__ dxb, *__restrict__ dyb;
+    Msk<C> lu, luu; Met<C> dx, dy, dxt, dyt, dxh, dyh, dxb, dyb;
     const double *__restrict__ u, *__restrict__ v;
     double *__restrict__ str_t, *__restrict__ str_s;
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n), w = c - 1, s = c - I.p, e = c + 1, nn = c + I.p;
+        const Pt c = I(m, n), w = I.w(c), s = I.s(c), e = I.e(c), nn = I.n(c);
         const float r1 = ld(dy, c) / ld(dx, c);
         const float r2 = ld(dx, c) / ld(dy, c);
         const double vt = D(r1) * (ld(u, c) / D(ld(dyh, c)) - ld(u, w) / D(ld(dyh, w)))
@@ -260,16 +311,14 @@ struct StressComponents {
 
 // ------------------------------------------------------------------ a6 uv_diff2
 // vel_ssh.f90:375-452
-struct UvDiff2 {
+template <bool C> struct UvDiff2 {
     Geo I;
-    const float *__restrict__ lcu, *__restrict__ lcv, *__restrict__ dx, *__restrict__ dy;
-    const float *__restrict__ dxt, *__restrict__ dyt, *__restrict__ dxh, *__restrict__ dyh;
-    const float *__restrict__ dxb, *__restrict__ dyb;
+    Msk<C> lcu, lcv; Met<C> dx, dy, dxt, dyt, dxh, dyh, dxb, dyb;
     const double *__restrict__ mu, *__restrict__ str_t, *__restrict__ str_s, *__restrict__ hq, *__restrict__ hh;
     double *__restrict__ RHSx, *__restrict__ RHSy;
-    OCN_HD OCN_INLINE void eval(unsigned c, double &rx, double &ry) const
+    OCN_HD OCN_INLINE void eval(Pt c, double &rx, double &ry) const
     {
-        const unsigned e = c + 1, nn = c + I.p, ne = nn + 1, s = c - I.p, se = s + 1, w = c - 1, wn = nn - 1;
+        const Pt e = I.e(c), nn = I.n(c), ne = I.e(nn), s = I.s(c), se = I.e(s), w = I.w(c), wn = I.w(nn);
         {
             const double muh_p = (ld(mu, c) + ld(mu, e) + ld(mu, nn) + ld(mu, ne)) / 4.0;
             const double muh_m = (ld(mu, c) + ld(mu, e) + ld(mu, s) + ld(mu, se)) / 4.0;
@@ -289,7 +338,7 @@ struct UvDiff2 {
     }
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n);
+        const Pt c = I(m, n);
         double rx, ry;
         eval(c, rx, ry);
         if (ld(lcu, c) > 0.5f) st(RHSx, c, rx);
@@ -299,24 +348,22 @@ struct UvDiff2 {
 
 // ------------------------------------------------------------------ a7 sw_update_uv
 // vel_ssh.f90:108-195
-struct SwUpdateUv {
+template <bool C> struct SwUpdateUv {
     Geo I; double tau;
-    const float *__restrict__ lcu, *__restrict__ lcv, *__restrict__ dxt, *__restrict__ dyt;
-    const float *__restrict__ dxh, *__restrict__ dyh, *__restrict__ dxb, *__restrict__ dyb;
+    Msk<C> lcu, lcv; Met<C> dxt, dyt, dxh, dyh, dxb, dyb;
     const double *__restrict__ hhu, *__restrict__ hhun, *__restrict__ hhup;
     const double *__restrict__ hhv, *__restrict__ hhvn, *__restrict__ hhvp;
     const double *__restrict__ hhh, *__restrict__ ssh;
     const double *__restrict__ ubrtr; double *__restrict__ ubrtrn; const double *__restrict__ ubrtrp;
     const double *__restrict__ vbrtr; double *__restrict__ vbrtrn; const double *__restrict__ vbrtrp;
-    const float *__restrict__ rdis, *__restrict__ rlh_s;
+    Met<C> rdis, rlh_s;
     const double *__restrict__ RHSx, *__restrict__ RHSy, *__restrict__ RHSx_adv, *__restrict__ RHSy_adv;
     const double *__restrict__ RHSx_dif, *__restrict__ RHSy_dif;
     // rxa/rxd/rya/ryd: RHSx_adv, RHSx_dif, RHSy_adv, RHSy_dif at this point
-    OCN_HD OCN_INLINE void eval(unsigned c, double rxa, double rxd, double rya, double ryd, double &un,
-                                         double &vn) const
+    OCN_HD OCN_INLINE void eval(Pt c, double rxa, double rxd, double rya, double ryd, double &un, double &vn) const
     {
         const double g = D(OCN_FREE_FALL_ACC);
-        const unsigned e = c + 1, s = c - I.p, se = s + 1, nn = c + I.p, w = c - 1, wn = nn - 1;
+        const Pt e = I.e(c), s = I.s(c), se = I.e(s), nn = I.n(c), w = I.w(c), wn = I.w(nn);
         {
             const double bp = ld(hhun, c) * D(ld(dxt, c)) * D(ld(dyh, c)) / 2.0 / tau;
             const double bp0 = ld(hhup, c) * D(ld(dxt, c)) * D(ld(dyh, c)) / 2.0 / tau;
@@ -340,30 +387,26 @@ struct SwUpdateUv {
             vn = (ld(vbrtrp, c) * bp0 + gry) / (bp);
         }
     }
-    OCN_HD OCN_INLINE void store(unsigned c, double un, double vn) const
-    {
-        if (ld(lcu, c) > 0.5f) st(ubrtrn, c, un);
-        if (ld(lcv, c) > 0.5f) st(vbrtrn, c, vn);
-    }
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n);
+        const Pt c = I(m, n);
         double un, vn;
         eval(c, ld(RHSx_adv, c), ld(RHSx_dif, c), ld(RHSy_adv, c), ld(RHSy_dif, c), un, vn);
-        store(c, un, vn);
+        if (ld(lcu, c) > 0.5f) st(ubrtrn, c, un);
+        if (ld(lcv, c) > 0.5f) st(vbrtrn, c, vn);
     }
 };
 
 // ------------------------------------------------------------------ a8 sw_next_step
 // vel_ssh.f90:197-245 (interior + halo ring)
-struct SwNextStep {
+template <bool C> struct SwNextStep {
     Geo I; double ts;
-    const float *__restrict__ lu, *__restrict__ lcu, *__restrict__ lcv;
+    Msk<C> lu, lcu, lcv;
     double *__restrict__ ssh, *__restrict__ sshn, *__restrict__ sshp;
     double *__restrict__ u, *__restrict__ un, *__restrict__ up;
     double *__restrict__ v, *__restrict__ vn, *__restrict__ vp;
     // returns the ssh value after the update (for check_ssh_err)
-    OCN_HD OCN_INLINE double step(unsigned i) const
+    OCN_HD OCN_INLINE double step(Pt i) const
     {
         const double x = ld(ssh, i), xn = ld(sshn, i), xp = ld(sshp, i);
         const double a = ld(u, i), an = ld(un, i), ap = ld(up, i);
@@ -382,15 +425,14 @@ struct SwNextStep {
 
 // ------------------------------------------------------------------ a9 hh_shift
 // depth.f90:164-211 (interior + halo ring)
-struct HhShift {
+template <bool C> struct HhShift {
     Geo I; double ts;
-    const float *__restrict__ lu, *__restrict__ llu, *__restrict__ llv, *__restrict__ luh;
+    Msk<C> lu, llu, llv, luh;
     double *__restrict__ hq, *__restrict__ hqp, *__restrict__ hqn;
     double *__restrict__ hu, *__restrict__ hup, *__restrict__ hun;
     double *__restrict__ hv, *__restrict__ hvp, *__restrict__ hvn;
     double *__restrict__ hh, *__restrict__ hhp, *__restrict__ hhn;
-    OCN_HD static OCN_INLINE void shift(bool mask, double *x, double *xp, const double *xn, unsigned i,
-                                                 double ts)
+    OCN_HD static OCN_INLINE void shift(bool mask, double *x, double *xp, const double *xn, Pt i, double ts)
     {
         const double a = ld(x, i), an = ld(xn, i), ap = ld(xp, i);
         const double f = a + ts * (an - 2.0 * a + ap) / 2.0;
@@ -398,7 +440,7 @@ struct HhShift {
     }
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned i = I(m, n);
+        const Pt i = I(m, n);
         shift(ld(llu, i) > 0.5f, hu, hup, hun, i, ts);
         shift(ld(llv, i) > 0.5f, hv, hvp, hvn, i, ts);
         shift(ld(lu, i) > 0.5f, hq, hqp, hqn, i, ts);
@@ -409,12 +451,12 @@ struct HhShift {
 // ------------------------------------------------------------------ check_ssh_err
 // vel_ssh.f90:40-67 as a device reduction (one atomic per thread with a bad point; the
 // count only needs to be non-zero).
-struct CheckSshErr {
+template <bool C> struct CheckSshErr {
     Geo I;
-    const float *__restrict__ lu; const double *__restrict__ ssh; int *nbad;
+    Msk<C> lu; const double *__restrict__ ssh; int *nbad;
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = I(m, n);
+        const Pt c = I(m, n);
         const double s = ld(ssh, c);
         if (ld(lu, c) > 0.5f && !(s < 10000.0 && s > -10000.0)) OCN_ATOMIC_INC(nbad);
     }
@@ -428,15 +470,19 @@ struct CheckSshErr {
 //        hh_update's whole-array hqn = h_r + ssh is not stored: its only readers are hh_shift's
 //        hq/hqp updates, which hh_init overwrites whole-array later in the same step.
 //   B  = a4 uv_trans + a6 uv_diff2 + a7 sw_update_uv: sw_update_uv reads RHS*_adv / RHS*_dif
-//        only at its own point, so they are passed in registers (and still stored) -> sync
-//        of u/v (and uv_trans's lazy hh*_p sync, whose halos nothing in B reads).
+//        only at its own point, so they are passed in registers -> sync of u/v (and
+//        uv_trans's lazy hh*_p sync, whose halos nothing in B reads).  They have no other
+//        reader, so they are stored only when `full` (the last step of a call).
 //   C1 = a8 sw_next_step + a9 hh_shift on the outer ring only (on [start-1,end]^2 its
 //        outputs are dead: hh_init overwrites them) + check_ssh_err.
-//   C2 = a10 hh_init (unchanged) -> sync hhu/hhv/hhh.
-struct FusedA {
+//   C2 = a10 hh_init (full = false except on the last step of a call) -> sync hhu/hhv/hhh.
+// "full" launches (the last step of every ocn_ctx_step call) store everything the reference
+// stores; the others skip stores nobody reads (FusedB, HhInit), so the state after each call
+// is the reference's bit for bit.
+template <bool C> struct FusedA {
     int sx, sy;
     bool do_hh, do_vort, do_stress;
-    SwUpdateSsh a1; HhUpdate a2; UvTransVort a3; StressComponents a5;
+    SwUpdateSsh<C> a1; HhUpdate<C> a2; UvTransVort<C> a3; StressComponents<C> a5;
     OCN_HD void operator()(int m, int n) const
     {
         if (m >= sx && n >= sy) {
@@ -445,18 +491,18 @@ struct FusedA {
             if (do_stress) a5(m, n);
         }
         if (do_hh) {
-            const unsigned c = a2.I(m, n);
+            const Pt c = a2.I(m, n);
             a2.interp(c, ld(a2.h_r, c) + ld(a2.sh, c));
         }
     }
 };
 
-struct FusedB {
-    bool do_adv, do_dif;
-    UvTrans a4; UvDiff2 a6; SwUpdateUv a7;
+template <bool C> struct FusedB {
+    bool do_adv, do_dif, full;
+    UvTrans<C> a4; UvDiff2<C> a6; SwUpdateUv<C> a7;
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = a7.I(m, n);
+        const Pt c = a7.I(m, n);
         double rxa, rya, rxd, ryd;
         if (do_adv) a4.eval(c, rxa, rya);
         else { rxa = ld(a7.RHSx_adv, c); rya = ld(a7.RHSy_adv, c); }
@@ -466,26 +512,26 @@ struct FusedB {
         a7.eval(c, rxa, rxd, rya, ryd, un, vn);
         const bool bu = ld(a7.lcu, c) > 0.5f, bv = ld(a7.lcv, c) > 0.5f;
         if (bu) {
-            if (do_adv) st(a4.RHSx, c, rxa);
-            if (do_dif) st(a6.RHSx, c, rxd);
+            if (do_adv && full) st(a4.RHSx, c, rxa);
+            if (do_dif && full) st(a6.RHSx, c, rxd);
             st(a7.ubrtrn, c, un);
         }
         if (bv) {
-            if (do_adv) st(a4.RHSy, c, rya);
-            if (do_dif) st(a6.RHSy, c, ryd);
+            if (do_adv && full) st(a4.RHSy, c, rya);
+            if (do_dif && full) st(a6.RHSy, c, ryd);
             st(a7.vbrtrn, c, vn);
         }
     }
 };
 
-struct FusedC1 {
+template <bool C> struct FusedC1 {
     int sx, ex, sy, ey;
     bool do_hh;
     int *nbad;
-    SwNextStep a8; HhShift a9;
+    SwNextStep<C> a8; HhShift<C> a9;
     OCN_HD void operator()(int m, int n) const
     {
-        const unsigned c = a8.I(m, n);
+        const Pt c = a8.I(m, n);
         const double x = a8.step(c);
         if (do_hh && (m == ex + 1 || n == ey + 1)) a9(m, n);
         if (nbad && m >= sx && m <= ex && n >= sy && n <= ey && ld(a8.lu, c) > 0.5f && !(x < 10000.0 && x > -10000.0))
@@ -493,12 +539,51 @@ struct FusedC1 {
     }
 };
 
+// ================================================================== compact static fields
+// Mask bits: bit (1 << id) for the mask ids OCN_LU..OCN_LLV (0..6).  Row tables: for the
+// metric ids OCN_DX..OCN_R_DISS, rows[(id - OCN_DX) * nrows + (n - bnd_y1)].
+constexpr int kNumMasks = OCN_DX;                         // OCN_LU..OCN_LLV
+constexpr int kNumRowFields = OCN_NUM_R4 - OCN_DX;        // OCN_DX..OCN_R_DISS
+enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2 };
+
+// Thread grid = whole bnd range.  Mask bytes everywhere; row values from column nx_start-1
+// for the rows [ny_start-1, ny_end+1] the stencils read; every point of [nx_start-1,
+// nx_end+1] on those rows must carry the same bit pattern, and every mask value must be
+// exactly 0.0f or 1.0f -- otherwise `flags` records why and the caller keeps the 2-D path.
+struct Prepare {
+    Geo I; int ms, me, ns, ne;
+    const float *__restrict__ r4[OCN_NUM_R4];
+    uint8_t *__restrict__ bits; float *__restrict__ rows; unsigned nrows; int *flags;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const Pt q = I(m, n);
+        unsigned b = 0;
+        bool bad = false;
+        for (int id = 0; id < kNumMasks; ++id) {
+            const uint32_t v = fbits(ld(r4[id], q));
+            if (v == 0x3f800000u) b |= 1u << id;
+            else if (v != 0u) bad = true;
+        }
+        st(bits, q, (uint8_t)b);
+        if (bad) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_MASK_NOT_BINARY);
+        if (m < ms || m > me || n < ns || n > ne) return;
+        const Pt q0 = I(ms, n);
+        bool vary = false;
+        for (int k = 0; k < kNumRowFields; ++k) {
+            const float v = ld(r4[OCN_DX + k], q);
+            vary |= fbits(v) != fbits(ld(r4[OCN_DX + k], q0));
+            if (m == ms) st(rows, (unsigned)k * nrows + q.r, v);
+        }
+        if (vary) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_METRIC_NOT_ROW_CONSTANT);
+    }
+};
 
 // ------------------------------------------------------------------ functor makers
 // Built from a block's field table (`ptr`, indexed by ocn_field_slot) -- used by the fused
 // launches and by the host harness, so both run exactly the same functors over the same ranges.
 inline int ocn_field_slot(int id) { return id < OCN_NUM_R4 ? id : OCN_NUM_R4 + (id - OCN_SSH); }
 inline Geo geo(const ocn_block *b) { return Geo{b->bnd_x1, b->bnd_y1, (unsigned)b->pitch}; }
+inline unsigned block_rows(const ocn_block *b) { return (unsigned)(b->bnd_y2 - b->bnd_y1 + 1); }
 
 struct Range { int m0, m1, n0, n1; };
 inline Range range_interior(const ocn_block *b) { return {b->nx_start, b->nx_end, b->ny_start, b->ny_end}; }
@@ -513,99 +598,119 @@ inline Range range_fused_a(const ocn_block *b, const ocn_sw_params &sw)
     return {b->nx_start - o, b->nx_end, b->ny_start - o, b->ny_end};
 }
 
-#define OCN_F4(id) ((const float *)ptr[ocn_field_slot(id)])
-#define OCN_F8(id) ((double *)ptr[ocn_field_slot(id)])
+inline Prepare make_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int *flags)
+{
+    Prepare k{geo(b), b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, {}, bits, rows,
+              block_rows(b), flags};
+    for (int id = 0; id < OCN_NUM_R4; ++id) k.r4[id] = (const float *)ptr[ocn_field_slot(id)];
+    return k;
+}
 
-inline Interp make_interp(void *const *ptr)
+// Field table of one block: real(8) arrays from `ptr`; masks / metrics from `ptr` (C = false)
+// or from the compact tables (C = true).
+template <bool C> struct Tab;
+template <> struct Tab<false> {
+    void *const *ptr;
+    Msk<false> m(int id) const { return {(const float *)ptr[ocn_field_slot(id)]}; }
+    Met<false> g(int id) const { return {(const float *)ptr[ocn_field_slot(id)]}; }
+    double *f(int id) const { return (double *)ptr[ocn_field_slot(id)]; }
+};
+template <> struct Tab<true> {
+    void *const *ptr;
+    const uint8_t *bits; const float *rows; unsigned nrows;
+    Msk<true> m(int id) const { return {bits, 1u << id}; }
+    Met<true> g(int id) const { return {rows + (size_t)(id - OCN_DX) * nrows}; }
+    double *f(int id) const { return (double *)ptr[ocn_field_slot(id)]; }
+};
+
+template <bool C> Interp<C> make_interp(const Tab<C> &t)
 {
-    return Interp{OCN_F4(OCN_LU), OCN_F4(OCN_DX), OCN_F4(OCN_DY), OCN_F4(OCN_DXT), OCN_F4(OCN_DYT),
-                  OCN_F4(OCN_DXH), OCN_F4(OCN_DYH), OCN_F4(OCN_DXB), OCN_F4(OCN_DYB)};
+    return Interp<C>{t.m(OCN_LU), t.g(OCN_DX), t.g(OCN_DY), t.g(OCN_DXT), t.g(OCN_DYT), t.g(OCN_DXH),
+                     t.g(OCN_DYH), t.g(OCN_DXB), t.g(OCN_DYB)};
 }
-inline SwUpdateSsh make_sw_update_ssh(const ocn_block *b, void *const *ptr, double tau)
+template <bool C> SwUpdateSsh<C> make_sw_update_ssh(const ocn_block *b, const Tab<C> &t, double tau)
 {
-    return SwUpdateSsh{geo(b), tau, OCN_F4(OCN_LU), OCN_F4(OCN_DX), OCN_F4(OCN_DY), OCN_F4(OCN_DXH),
-                       OCN_F4(OCN_DYH), OCN_F8(OCN_HHU), OCN_F8(OCN_HHV), OCN_F8(OCN_SSHN), OCN_F8(OCN_SSHP),
-                       OCN_F8(OCN_UBRTR), OCN_F8(OCN_VBRTR)};
+    return SwUpdateSsh<C>{geo(b), tau, t.m(OCN_LU), t.g(OCN_DX), t.g(OCN_DY), t.g(OCN_DXH), t.g(OCN_DYH),
+                          t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_SSHN), t.f(OCN_SSHP), t.f(OCN_UBRTR), t.f(OCN_VBRTR)};
 }
-inline HhUpdate make_hh_update(const ocn_block *b, void *const *ptr)
+template <bool C> HhUpdate<C> make_hh_update(const ocn_block *b, const Tab<C> &t)
 {
-    return HhUpdate{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, make_interp(ptr),
-                    OCN_F4(OCN_LLU), OCN_F4(OCN_LLV), OCN_F4(OCN_LUH), OCN_F8(OCN_HHQ_N), OCN_F8(OCN_HHU_N),
-                    OCN_F8(OCN_HHV_N), OCN_F8(OCN_HHH_N), OCN_F8(OCN_SSH), OCN_F8(OCN_HHQ_REST)};
+    return HhUpdate<C>{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, make_interp(t),
+                       t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LUH), t.f(OCN_HHQ_N), t.f(OCN_HHU_N), t.f(OCN_HHV_N),
+                       t.f(OCN_HHH_N), t.f(OCN_SSH), t.f(OCN_HHQ_REST)};
 }
-inline UvTransVort make_uv_trans_vort(const ocn_block *b, void *const *ptr)
+template <bool C> UvTransVort<C> make_uv_trans_vort(const ocn_block *b, const Tab<C> &t)
 {
-    return UvTransVort{geo(b), OCN_F4(OCN_LUU), OCN_F4(OCN_DXT), OCN_F4(OCN_DYT), OCN_F4(OCN_DXB), OCN_F4(OCN_DYB),
-                       OCN_F8(OCN_UBRTR), OCN_F8(OCN_VBRTR), OCN_F8(OCN_VORT)};
+    return UvTransVort<C>{geo(b), t.m(OCN_LUU), t.g(OCN_DXT), t.g(OCN_DYT), t.g(OCN_DXB), t.g(OCN_DYB),
+                          t.f(OCN_UBRTR), t.f(OCN_VBRTR), t.f(OCN_VORT)};
 }
-inline UvTrans make_uv_trans(const ocn_block *b, void *const *ptr)
+template <bool C> UvTrans<C> make_uv_trans(const ocn_block *b, const Tab<C> &t)
 {
-    return UvTrans{geo(b), OCN_F4(OCN_LCU), OCN_F4(OCN_LCV), OCN_F4(OCN_LUU), OCN_F4(OCN_DXH), OCN_F4(OCN_DYH),
-                   OCN_F8(OCN_UBRTR), OCN_F8(OCN_VBRTR), OCN_F8(OCN_VORT), OCN_F8(OCN_HHU), OCN_F8(OCN_HHV),
-                   OCN_F8(OCN_HHH), OCN_F8(OCN_RHSX_ADV), OCN_F8(OCN_RHSY_ADV)};
+    return UvTrans<C>{geo(b), t.m(OCN_LCU), t.m(OCN_LCV), t.m(OCN_LUU), t.g(OCN_DXH), t.g(OCN_DYH),
+                      t.f(OCN_UBRTR), t.f(OCN_VBRTR), t.f(OCN_VORT), t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_HHH),
+                      t.f(OCN_RHSX_ADV), t.f(OCN_RHSY_ADV)};
 }
-inline StressComponents make_stress_components(const ocn_block *b, void *const *ptr)
+template <bool C> StressComponents<C> make_stress_components(const ocn_block *b, const Tab<C> &t)
 {
-    return StressComponents{geo(b), OCN_F4(OCN_LU), OCN_F4(OCN_LUU), OCN_F4(OCN_DX), OCN_F4(OCN_DY),
-                            OCN_F4(OCN_DXT), OCN_F4(OCN_DYT), OCN_F4(OCN_DXH), OCN_F4(OCN_DYH), OCN_F4(OCN_DXB),
-                            OCN_F4(OCN_DYB), OCN_F8(OCN_UBRTRP), OCN_F8(OCN_VBRTRP), OCN_F8(OCN_STR_T),
-                            OCN_F8(OCN_STR_S)};
+    return StressComponents<C>{geo(b), t.m(OCN_LU), t.m(OCN_LUU), t.g(OCN_DX), t.g(OCN_DY), t.g(OCN_DXT),
+                               t.g(OCN_DYT), t.g(OCN_DXH), t.g(OCN_DYH), t.g(OCN_DXB), t.g(OCN_DYB),
+                               t.f(OCN_UBRTRP), t.f(OCN_VBRTRP), t.f(OCN_STR_T), t.f(OCN_STR_S)};
 }
-inline UvDiff2 make_uv_diff2(const ocn_block *b, void *const *ptr)
+template <bool C> UvDiff2<C> make_uv_diff2(const ocn_block *b, const Tab<C> &t)
 {
-    return UvDiff2{geo(b), OCN_F4(OCN_LCU), OCN_F4(OCN_LCV), OCN_F4(OCN_DX), OCN_F4(OCN_DY), OCN_F4(OCN_DXT),
-                   OCN_F4(OCN_DYT), OCN_F4(OCN_DXH), OCN_F4(OCN_DYH), OCN_F4(OCN_DXB), OCN_F4(OCN_DYB),
-                   OCN_F8(OCN_MU), OCN_F8(OCN_STR_T), OCN_F8(OCN_STR_S), OCN_F8(OCN_HHQ), OCN_F8(OCN_HHH),
-                   OCN_F8(OCN_RHSX_DIF), OCN_F8(OCN_RHSY_DIF)};
+    return UvDiff2<C>{geo(b), t.m(OCN_LCU), t.m(OCN_LCV), t.g(OCN_DX), t.g(OCN_DY), t.g(OCN_DXT), t.g(OCN_DYT),
+                      t.g(OCN_DXH), t.g(OCN_DYH), t.g(OCN_DXB), t.g(OCN_DYB), t.f(OCN_MU), t.f(OCN_STR_T),
+                      t.f(OCN_STR_S), t.f(OCN_HHQ), t.f(OCN_HHH), t.f(OCN_RHSX_DIF), t.f(OCN_RHSY_DIF)};
 }
-inline SwUpdateUv make_sw_update_uv(const ocn_block *b, void *const *ptr, double tau)
+template <bool C> SwUpdateUv<C> make_sw_update_uv(const ocn_block *b, const Tab<C> &t, double tau)
 {
-    return SwUpdateUv{geo(b), tau, OCN_F4(OCN_LCU), OCN_F4(OCN_LCV), OCN_F4(OCN_DXT), OCN_F4(OCN_DYT),
-                      OCN_F4(OCN_DXH), OCN_F4(OCN_DYH), OCN_F4(OCN_DXB), OCN_F4(OCN_DYB), OCN_F8(OCN_HHU),
-                      OCN_F8(OCN_HHU_N), OCN_F8(OCN_HHU_P), OCN_F8(OCN_HHV), OCN_F8(OCN_HHV_N), OCN_F8(OCN_HHV_P),
-                      OCN_F8(OCN_HHH), OCN_F8(OCN_SSH), OCN_F8(OCN_UBRTR), OCN_F8(OCN_UBRTRN), OCN_F8(OCN_UBRTRP),
-                      OCN_F8(OCN_VBRTR), OCN_F8(OCN_VBRTRN), OCN_F8(OCN_VBRTRP), OCN_F4(OCN_R_DISS),
-                      OCN_F4(OCN_RLH_S), OCN_F8(OCN_RHSX), OCN_F8(OCN_RHSY), OCN_F8(OCN_RHSX_ADV),
-                      OCN_F8(OCN_RHSY_ADV), OCN_F8(OCN_RHSX_DIF), OCN_F8(OCN_RHSY_DIF)};
+    return SwUpdateUv<C>{geo(b), tau, t.m(OCN_LCU), t.m(OCN_LCV), t.g(OCN_DXT), t.g(OCN_DYT), t.g(OCN_DXH),
+                         t.g(OCN_DYH), t.g(OCN_DXB), t.g(OCN_DYB), t.f(OCN_HHU), t.f(OCN_HHU_N), t.f(OCN_HHU_P),
+                         t.f(OCN_HHV), t.f(OCN_HHV_N), t.f(OCN_HHV_P), t.f(OCN_HHH), t.f(OCN_SSH), t.f(OCN_UBRTR),
+                         t.f(OCN_UBRTRN), t.f(OCN_UBRTRP), t.f(OCN_VBRTR), t.f(OCN_VBRTRN), t.f(OCN_VBRTRP),
+                         t.g(OCN_R_DISS), t.g(OCN_RLH_S), t.f(OCN_RHSX), t.f(OCN_RHSY), t.f(OCN_RHSX_ADV),
+                         t.f(OCN_RHSY_ADV), t.f(OCN_RHSX_DIF), t.f(OCN_RHSY_DIF)};
 }
-inline SwNextStep make_sw_next_step(const ocn_block *b, void *const *ptr, double ts)
+template <bool C> SwNextStep<C> make_sw_next_step(const ocn_block *b, const Tab<C> &t, double ts)
 {
-    return SwNextStep{geo(b), ts, OCN_F4(OCN_LU), OCN_F4(OCN_LCU), OCN_F4(OCN_LCV), OCN_F8(OCN_SSH),
-                      OCN_F8(OCN_SSHN), OCN_F8(OCN_SSHP), OCN_F8(OCN_UBRTR), OCN_F8(OCN_UBRTRN), OCN_F8(OCN_UBRTRP),
-                      OCN_F8(OCN_VBRTR), OCN_F8(OCN_VBRTRN), OCN_F8(OCN_VBRTRP)};
+    return SwNextStep<C>{geo(b), ts, t.m(OCN_LU), t.m(OCN_LCU), t.m(OCN_LCV), t.f(OCN_SSH), t.f(OCN_SSHN),
+                         t.f(OCN_SSHP), t.f(OCN_UBRTR), t.f(OCN_UBRTRN), t.f(OCN_UBRTRP), t.f(OCN_VBRTR),
+                         t.f(OCN_VBRTRN), t.f(OCN_VBRTRP)};
 }
-inline HhShift make_hh_shift(const ocn_block *b, void *const *ptr, double ts)
+template <bool C> HhShift<C> make_hh_shift(const ocn_block *b, const Tab<C> &t, double ts)
 {
-    return HhShift{geo(b), ts, OCN_F4(OCN_LU), OCN_F4(OCN_LLU), OCN_F4(OCN_LLV), OCN_F4(OCN_LUH), OCN_F8(OCN_HHQ),
-                   OCN_F8(OCN_HHQ_P), OCN_F8(OCN_HHQ_N), OCN_F8(OCN_HHU), OCN_F8(OCN_HHU_P), OCN_F8(OCN_HHU_N),
-                   OCN_F8(OCN_HHV), OCN_F8(OCN_HHV_P), OCN_F8(OCN_HHV_N), OCN_F8(OCN_HHH), OCN_F8(OCN_HHH_P),
-                   OCN_F8(OCN_HHH_N)};
+    return HhShift<C>{geo(b), ts, t.m(OCN_LU), t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LUH), t.f(OCN_HHQ),
+                      t.f(OCN_HHQ_P), t.f(OCN_HHQ_N), t.f(OCN_HHU), t.f(OCN_HHU_P), t.f(OCN_HHU_N), t.f(OCN_HHV),
+                      t.f(OCN_HHV_P), t.f(OCN_HHV_N), t.f(OCN_HHH), t.f(OCN_HHH_P), t.f(OCN_HHH_N)};
 }
-inline HhInit make_hh_init(const ocn_block *b, void *const *ptr, int ffs)
+template <bool C> HhInit<C> make_hh_init(const ocn_block *b, const Tab<C> &t, int ffs, bool full)
 {
-    return HhInit{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)ffs, make_interp(ptr),
-                  OCN_F4(OCN_LLU), OCN_F4(OCN_LLV), OCN_F4(OCN_LUH), OCN_F8(OCN_HHQ), OCN_F8(OCN_HHQ_P),
-                  OCN_F8(OCN_HHQ_N), OCN_F8(OCN_HHU), OCN_F8(OCN_HHU_P), OCN_F8(OCN_HHU_N), OCN_F8(OCN_HHV),
-                  OCN_F8(OCN_HHV_P), OCN_F8(OCN_HHV_N), OCN_F8(OCN_HHH), OCN_F8(OCN_HHH_P), OCN_F8(OCN_HHH_N),
-                  OCN_F8(OCN_SSH), OCN_F8(OCN_SSHP), OCN_F8(OCN_HHQ_REST)};
+    return HhInit<C>{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)ffs, full,
+                     make_interp(t), t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LUH), t.f(OCN_HHQ), t.f(OCN_HHQ_P),
+                     t.f(OCN_HHQ_N), t.f(OCN_HHU), t.f(OCN_HHU_P), t.f(OCN_HHU_N), t.f(OCN_HHV), t.f(OCN_HHV_P),
+                     t.f(OCN_HHV_N), t.f(OCN_HHH), t.f(OCN_HHH_P), t.f(OCN_HHH_N), t.f(OCN_SSH), t.f(OCN_SSHP),
+                     t.f(OCN_HHQ_REST)};
 }
-inline FusedA make_fused_a(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau)
+template <bool C> CheckSshErr<C> make_check_ssh_err(const ocn_block *b, const Tab<C> &t, int32_t *nbad)
 {
-    return FusedA{b->nx_start, b->ny_start, sw.full_free_surface > 0, sw.trans_terms > 0, sw.ksw_lat > 0,
-                  make_sw_update_ssh(b, ptr, tau), make_hh_update(b, ptr), make_uv_trans_vort(b, ptr),
-                  make_stress_components(b, ptr)};
+    return CheckSshErr<C>{geo(b), t.m(OCN_LU), t.f(OCN_SSH), (int *)nbad};
 }
-inline FusedB make_fused_b(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, double tau)
+template <bool C> FusedA<C> make_fused_a(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau)
 {
-    return FusedB{sw.trans_terms > 0, sw.ksw_lat > 0, make_uv_trans(b, ptr), make_uv_diff2(b, ptr),
-                  make_sw_update_uv(b, ptr, tau)};
+    return FusedA<C>{b->nx_start, b->ny_start, sw.full_free_surface > 0, sw.trans_terms > 0, sw.ksw_lat > 0,
+                     make_sw_update_ssh(b, t, tau), make_hh_update(b, t), make_uv_trans_vort(b, t),
+                     make_stress_components(b, t)};
 }
-inline FusedC1 make_fused_c1(const ocn_block *b, void *const *ptr, const ocn_sw_params &sw, int32_t *nbad)
+template <bool C>
+FusedB<C> make_fused_b(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau, bool full)
 {
-    return FusedC1{b->nx_start, b->nx_end, b->ny_start, b->ny_end, sw.full_free_surface > 0, (int *)nbad,
-                   make_sw_next_step(b, ptr, sw.time_smooth), make_hh_shift(b, ptr, sw.time_smooth)};
+    return FusedB<C>{sw.trans_terms > 0, sw.ksw_lat > 0, full, make_uv_trans(b, t), make_uv_diff2(b, t),
+                     make_sw_update_uv(b, t, tau)};
 }
-#undef OCN_F4
-#undef OCN_F8
+template <bool C> FusedC1<C> make_fused_c1(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, int32_t *nbad)
+{
+    return FusedC1<C>{b->nx_start, b->nx_end, b->ny_start, b->ny_end, sw.full_free_surface > 0, (int *)nbad,
+                      make_sw_next_step(b, t, sw.time_smooth), make_hh_shift(b, t, sw.time_smooth)};
+}
 
 }  // namespace ocn

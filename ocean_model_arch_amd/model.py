@@ -125,6 +125,22 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FUSED, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_compact(self, on: bool = True):
+        """Compact static fields for the fused step (bit-packed masks, per-row metrics) when exact
+        for the current real(4) fields; re-arms them after raw real(4) pointers were handed out."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_COMPACT, int(on)), "ocn_ctx_set_option")
+        return self
+
+    def option(self, key: int) -> int:
+        v = C.c_int64(0)
+        check(lib().ocn_ctx_get_option(self.ctx, key, C.byref(v)), "ocn_ctx_get_option")
+        return v.value
+
+    @property
+    def compact_active(self) -> bool:
+        """Whether the last step() read the compact static fields."""
+        return bool(self.option(_lib.OPT_COMPACT))
+
     # ---------------------------------------------------------------- execution
     def step(self, nsteps: int = 1, tau: float = 1.0, check_every: int = 1):
         check(lib().ocn_ctx_step(self.ctx, tau, nsteps, check_every), "ocn_ctx_step")

@@ -16,7 +16,7 @@ for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recu
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "")
-            m = re.search(r"k_range<ocn::(\w+)>|ocn::(\w+)\(", name)
+            m = re.search(r"k_range<ocn::(\w+(?:<\w+>)?)>|ocn::(\w+)\(", name)
             k = (m.group(1) or m.group(2)) if m else name[:60]
             vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
 out = {}

@@ -70,7 +70,7 @@ def test_kernels_match_reference(amd, geom):
     assert not failures, f"{geom}: differs from the reference: {failures}"
 
 
-def build_model(amd, case, graph=False, fused=True):
+def build_model(amd, case, graph=False, fused=True, compact=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"])
@@ -78,6 +78,7 @@ def build_model(amd, case, graph=False, fused=True):
     par = amd.ParallelConfig(bppnx=case["bxy"][0], bppny=case["bxy"][1])
     m = amd.OceanModel(basin, sw, par)
     m.set_fused(fused)
+    m.set_compact(compact)
     if graph:
         m.set_graph(True)
     return m
@@ -100,16 +101,68 @@ def compare_case(m, case, name):
     return bad
 
 
-@pytest.mark.parametrize("fused", [True, False], ids=["fused", "stages"])
+@pytest.mark.parametrize("mode", ["compact", "fused", "stages"])
 @pytest.mark.parametrize("name", cases.E2E_CASES)
-def test_end_to_end_matches_reference(amd, name, fused):
-    """fused = the 4-launch step (default); stages = the reference's 11 envoke stages."""
+def test_end_to_end_matches_reference(amd, name, mode):
+    """compact = the 4-launch step reading the compact static fields (default); fused = the same
+    on the 2-D real(4) arrays; stages = the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    m = build_model(amd, case, fused=fused)
+    m = build_model(amd, case, fused=mode != "stages", compact=mode == "compact")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
+    assert m.compact_active == (mode == "compact")
     bad = compare_case(m, case, name)
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["stream", "graph"])
+def test_split_step_calls_match_reference(amd, graph):
+    """The run split over several ocn_ctx_step calls (each call's last step writes hh_init's
+    time-invariant levels): same final state as one call and as the reference."""
+    name = "box70x54_b3x2_s20"
+    case = cases.load_e2e(name)
+    m = build_model(amd, case, graph=graph).init()
+    for n in (7, 1, 12):
+        m.step(n, tau=1.0, check_every=0)
+    m.synchronize()
+    bad = compare_case(m, case, name)
+    m.close()
+    assert not bad, f"{name}: fields differ from the reference: {bad}"
+
+
+@pytest.mark.parametrize("what", ["metric", "mask"])
+def test_compact_fallback_is_exact(amd, what):
+    """real(4) fields the compact tables cannot represent (a metric varying along a row, a mask
+    value other than 0/1): the fused step must detect it, read the 2-D arrays, and still match
+    the oracle run on the same modified fields bit for bit."""
+    from oracle import oracle as O
+    n, bxy, steps = 96, (2, 1), 6
+    om = O.OracleModel(O.BasinConfig(nx=n + 4, ny=n + 4), O.SWConfig(), *bxy).init()
+    m = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(*bxy)).init()
+    for b in m.blocks:
+        k = [i for i, ob in enumerate(om.blocks) if (ob.bm, ob.bn) == (b.bm, b.bn)][0]
+        if what == "metric":
+            a = om.f[k]["dx"]
+            a *= (1.0 + 1.0e-4 * np.arange(a.shape[0], dtype=np.float32))[:, None]
+            nm = "dx"
+        else:
+            a = om.f[k]["lu"]
+            a[a.shape[0] // 2, a.shape[1] // 2] = 0.75
+            nm = "lu"
+        m.upload(b.k, nm, a)
+    m.step(steps).synchronize()
+    assert not m.compact_active
+    om.run(steps)
+    bad = []
+    for b in m.blocks:
+        k = [i for i, ob in enumerate(om.blocks) if (ob.bm, ob.bn) == (b.bm, b.bn)][0]
+        for nm, a in om.f[k].items():
+            if nm in ("lu1", "rlh_c"):
+                continue
+            if not bits_equal(m.download(b.k, nm), a):
+                bad.append(f"({b.bm},{b.bn}):{nm}")
+    m.close()
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("name", ["box70x54_b3x2_s20", "bs_b1x1_s60"])

@@ -46,8 +46,10 @@ def hst():
     subprocess.check_call(["make", "-s", "-f", os.path.join(REPO, "tests", "native", "Makefile")], cwd=REPO)
     L = C.CDLL(LIB)
     L.hst_stage.restype = C.c_long
-    L.hst_stage.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.POINTER(SwParams), C.c_double,
-                            C.POINTER(C.c_int32)]
+    L.hst_stage.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(SwParams),
+                            C.c_double, C.POINTER(C.c_int32), C.c_int]
+    L.hst_prepare.restype = C.c_int
+    L.hst_prepare.argtypes = [C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p]
     return L
 
 
@@ -76,7 +78,8 @@ def test_stage_functors_match_reference(hst, geom):
     for kname in cases.KERNEL_NAMES:
         arrs = {k[3:]: z[k].copy(order="F") for k in z.files if k.startswith("in/")}
         nbad = C.c_int32(0)
-        oob = hst.hst_stage(STAGE_IDS[kname], C.byref(b), table(arrs), C.byref(sw), float(z["tau"]), C.byref(nbad))
+        oob = hst.hst_stage(STAGE_IDS[kname], C.byref(b), table(arrs), None, None, C.byref(sw), float(z["tau"]),
+                            C.byref(nbad), 1)
         assert oob == 0, f"{kname}: {oob} out-of-bounds accesses"
         for nm in [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]:
             if not bits_equal(arrs[nm], z[f"{kname}/{nm}"]):
@@ -88,28 +91,47 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a.ravel(order="F")).tobytes()).hexdigest()
 
 
-def host_step(hst, om, fused, nbad):
+N_ROW_FIELDS = len(R4) - 7          # dx .. r_diss
+
+
+def compact_tables(hst, om):
+    """Host-built compact static fields (sw_stencils.h Prepare) of every block; rows the
+    stencils must not read are NaN so that a wrong row index cannot go unnoticed."""
+    out = []
+    for k, b in enumerate(om.blocks):
+        blk_ = Block(*b.args, b.bx2 - b.bx1 + 1)
+        shape = om.f[k]["lu"].shape
+        bits = np.zeros(shape[0] * shape[1], dtype=np.uint8)
+        rows = np.full(N_ROW_FIELDS * shape[1], np.nan, dtype=np.float32)
+        flags = hst.hst_prepare(C.byref(blk_), table(om.f[k]), bits.ctypes.data, rows.ctypes.data)
+        out.append((bits, rows, flags))
+    return out
+
+
+def host_step(hst, om, mode, nbad, last=True, tabs=None):
     sw_o = om.sw
     sw = SwParams(sw_o.full_free_surface, sw_o.trans_terms, sw_o.ksw_lat, sw_o.time_smooth, sw_o.lvisc_2)
     blocks = [(Block(*b.args, b.bx2 - b.bx1 + 1), table(om.f[k])) for k, b in enumerate(om.blocks)]
+    compact = mode == "compact"
 
-    def each(stage, tau=1.0):
-        for b, t in blocks:
-            oob = hst.hst_stage(stage, C.byref(b), t, C.byref(sw), tau, C.byref(nbad))
+    def each(stage, tau=1.0, full=1):
+        for k, (b, t) in enumerate(blocks):
+            bits, rows = (tabs[k][0].ctypes.data, tabs[k][1].ctypes.data) if compact else (None, None)
+            oob = hst.hst_stage(stage, C.byref(b), t, bits, rows, C.byref(sw), tau, C.byref(nbad), full)
             assert oob == 0, f"stage {stage}: {oob} out-of-bounds accesses"
 
-    if fused:
+    if mode != "stages":
         each(FUSED_A)
         sa = ["sshn"] + (["hhu_n", "hhv_n", "hhh_n"] if sw.full_free_surface > 0 else []) + \
              (["vort"] if sw.trans_terms > 0 else []) + (["str_t", "str_s"] if sw.ksw_lat > 0 else [])
         for f in sa:
             om.sync(f)
-        each(FUSED_B)
+        each(FUSED_B, full=int(last))
         for f in (["hhu_p", "hhv_p", "hhh_p"] if sw.trans_terms > 0 else []) + ["vbrtrn", "ubrtrn"]:
             om.sync(f)
         each(FUSED_C1)
         if sw.full_free_surface > 0:
-            each(STAGE_IDS["hh_init"])
+            each(STAGE_IDS["hh_init"], full=int(last))
             for f in ("hhu", "hhv", "hhh"):
                 om.sync(f)
     else:
@@ -127,17 +149,24 @@ def host_step(hst, om, fused, nbad):
         each(CHECK)
 
 
-@pytest.mark.parametrize("fused", [True, False], ids=["fused", "stages"])
+@pytest.mark.parametrize("mode", ["compact", "fused", "stages"])
 @pytest.mark.parametrize("name", cases.E2E_CASES)
-def test_host_step_matches_reference(hst, name, fused):
+def test_host_step_matches_reference(hst, name, mode):
+    """The whole run as one ocn_ctx_step call: hh_init's time-invariant stores are skipped on
+    every step but the last (fused modes); "compact" reads masks / metrics from the compact
+    tables, which must be exact for these grids (no curvilinear metrics)."""
     case = cases.load_e2e(name)
     b = case["basin"]
     om = O.OracleModel(O.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"],
                                      rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"]),
                        O.SWConfig(**case["sw"]), *case["bxy"]).init()
     nbad = C.c_int32(0)
-    for _ in range(case["steps"]):
-        host_step(hst, om, fused, nbad)
+    tabs = None
+    if mode == "compact":
+        tabs = compact_tables(hst, om)
+        assert all(t[2] == 0 for t in tabs), [t[2] for t in tabs]
+    for s in range(case["steps"]):
+        host_step(hst, om, mode, nbad, last=s == case["steps"] - 1, tabs=tabs)
     assert nbad.value == 0
     z = case["z"]
     bad = []
@@ -147,3 +176,34 @@ def test_host_step_matches_reference(hst, name, fused):
             if key in z.files and _sha(a) != str(z[key]):
                 bad.append(f"({blkk.bm},{blkk.bn}):{nm}")
     assert not bad, f"{name}: {bad}"
+
+
+@pytest.mark.parametrize("what,flag", [("none", 0), ("metric", 2), ("mask", 1)])
+def test_compact_tables_detect_inexact_fields(hst, what, flag):
+    """Prepare must refuse (flags) real(4) fields the compact tables cannot hold exactly: a metric
+    that varies along a row inside [nx_start-1, nx_end+1], a mask value other than 0.0 / 1.0."""
+    om = O.OracleModel(O.BasinConfig(nx=40, ny=36), O.SWConfig(), 2, 1).init()
+    for k in range(len(om.blocks)):
+        if what == "metric":
+            om.f[k]["dyh"][3, 4] = np.nextafter(om.f[k]["dyh"][3, 4], np.float32(2e9))
+        elif what == "mask":
+            om.f[k]["llv"][5, 5] = 0.5
+    flags = [t[2] for t in compact_tables(hst, om)]
+    assert flags == [flag] * len(om.blocks)
+
+
+def test_compact_row_window_is_what_the_stencils_read(hst):
+    """A metric varying only outside [nx_start-1, nx_end+1] (the outer halo column, never read)
+    keeps the compact tables usable, and the run stays bitwise equal to the 2-D path."""
+    om = O.OracleModel(O.BasinConfig(nx=40, ny=36), O.SWConfig(), 1, 1).init()
+    om.f[0]["dx"][0, :] *= np.float32(3.0)          # column bnd_x1 = nx_start - 2
+    tabs = compact_tables(hst, om)
+    assert tabs[0][2] == 0
+    ref = O.OracleModel(O.BasinConfig(nx=40, ny=36), O.SWConfig(), 1, 1).init()
+    ref.f[0]["dx"][0, :] *= np.float32(3.0)
+    nbad = C.c_int32(0)
+    for s in range(4):
+        host_step(hst, om, "compact", nbad, last=s == 3, tabs=tabs)
+        host_step(hst, ref, "stages", nbad)
+    for nm in ref.f[0]:
+        assert bits_equal(om.f[0][nm], ref.f[0][nm]), nm
