@@ -31,6 +31,7 @@ STAGES = ["sw_update_ssh", "hh_update", "uv_trans_vort", "uv_trans", "stress_com
 STAGE_ID = {n: i for i, n in enumerate(STAGES)}
 TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"]     # OCN_NUM_TIMERS slots
 OPT_GRAPH = 1
+OPT_OVERLAP = 2
 OPT_STAGE_TIMING = 3
 OPT_FUSED = 4
 OPT_COMPACT = 5

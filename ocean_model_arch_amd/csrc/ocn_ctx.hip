@@ -163,6 +163,9 @@ struct ocn_ctx {
     std::vector<GBlock> gblocks;       // (bm-1) + (bn-1)*bnx
     std::vector<LBlock> blocks;
     hipStream_t stream = nullptr;
+    hipStream_t comm_stream = nullptr;  // halo exchanges overlapped with interior compute
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool overlap = true;
     int32_t *d_nbad = nullptr;
     ncclComm_t comm = nullptr;
     std::map<std::vector<int>, HaloPlan> plans;
@@ -466,27 +469,28 @@ static int nccl_rc(ncclResult_t r, const char *what)
     return set_error(OCN_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-static int run_sync(ocn_ctx *c, const std::vector<int> &fields)
+static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stream = nullptr)
 {
     HaloPlan *p;
     RC(get_plan(c, fields, p));
+    if (!stream) stream = c->stream;
     if (!p->peers.empty()) {
         if (!c->comm) return set_error(OCN_ERR_COMM, "remote neighbours but no RCCL communicator attached");
-        hipLaunchKernelGGL(k_segments, dim3(p->n_pack), dim3(256), 0, c->stream, p->d_pack, p->n_pack);
+        hipLaunchKernelGGL(k_segments, dim3(p->n_pack), dim3(256), 0, stream, p->d_pack, p->n_pack);
         RC(check_launch());
         RC(nccl_rc(ncclGroupStart(), "ncclGroupStart"));
         for (auto &peer : p->peers) {
-            RC(nccl_rc(ncclRecv(peer.recv, (size_t)peer.count, ncclDouble, peer.rank, c->comm, c->stream), "ncclRecv"));
-            RC(nccl_rc(ncclSend(peer.send, (size_t)peer.count, ncclDouble, peer.rank, c->comm, c->stream), "ncclSend"));
+            RC(nccl_rc(ncclRecv(peer.recv, (size_t)peer.count, ncclDouble, peer.rank, c->comm, stream), "ncclRecv"));
+            RC(nccl_rc(ncclSend(peer.send, (size_t)peer.count, ncclDouble, peer.rank, c->comm, stream), "ncclSend"));
         }
         RC(nccl_rc(ncclGroupEnd(), "ncclGroupEnd"));
     }
     if (p->n_local) {
-        hipLaunchKernelGGL(k_segments, dim3(p->n_local), dim3(256), 0, c->stream, p->d_local, p->n_local);
+        hipLaunchKernelGGL(k_segments, dim3(p->n_local), dim3(256), 0, stream, p->d_local, p->n_local);
         RC(check_launch());
     }
     if (p->n_unpack) {
-        hipLaunchKernelGGL(k_segments, dim3(p->n_unpack), dim3(256), 0, c->stream, p->d_unpack, p->n_unpack);
+        hipLaunchKernelGGL(k_segments, dim3(p->n_unpack), dim3(256), 0, stream, p->d_unpack, p->n_unpack);
         RC(check_launch());
     }
     return OCN_OK;
@@ -678,6 +682,35 @@ static int prepare_static(ocn_ctx *c)
 // bitwise the same state as one_step.  last = false skips stores no later kernel reads
 // (sw_stencils.h FusedB / HhInit `full`); the last step of every ocn_ctx_step call leaves the
 // full state.
+//
+// With halo exchanges to do (several blocks or ranks) and OCN_OPT_OVERLAP, each exchange runs
+// on the comm stream while the compute stream works on points that neither feed it nor read
+// its halos (sw_stencils.h frame_rects):
+//   A.frame | fork: sync A || A.inner, B.inner | join | B.frame | fork: sync B || C1.inner |
+//   join | C1.frame | C2.frame | fork: sync C2 || C2.inner | join
+// Every halo write of an exchange lands on points the concurrent inner launches neither read
+// nor write, and every value it sends was produced by the frame launch before the fork.
+static bool has_exchange(ocn_ctx *c)
+{
+    HaloPlan *p = nullptr;
+    if (get_plan(c, c->sync_a, p) || !p) return false;
+    return p->n_local > 0 || !p->peers.empty();
+}
+
+static int fork_sync(ocn_ctx *c, const std::vector<int> &fields)
+{
+    HIPCHK(hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
+    RC(run_sync(c, fields, c->comm_stream));
+    HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
+    return OCN_OK;
+}
+static int join_sync(ocn_ctx *c)
+{
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    return OCN_OK;
+}
+
 static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
 {
     const ocn_sw_params &sw = c->sw;
@@ -687,23 +720,58 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
         return c->compact ? &t : nullptr;
     };
     Compact t;
-    RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-    for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), sw, tau, c->stream));
-    RC(timer_end(c, rec));
-    RC(run_sync(c, c->sync_a));
-    RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
-    for (const LBlock &b : c->blocks) RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), sw, tau, last, c->stream));
-    RC(timer_end(c, rec));
-    RC(run_sync(c, c->sync_b));
-    RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
-    for (const LBlock &b : c->blocks)
-        RC(launch_fused_c1(&b.g, b.ptr.data(), cp(b, t), sw, check ? c->d_nbad : nullptr, c->stream));
-    RC(timer_end(c, rec));
-    if (sw.full_free_surface > 0) {
-        RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-        for (const LBlock &b : c->blocks) RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), sw, last, c->stream));
+    int32_t *nbad = check ? c->d_nbad : nullptr;
+    hipStream_t s = c->stream;
+    const bool ffs = sw.full_free_surface > 0;
+    if (!(c->overlap && has_exchange(c))) {
+        RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
+        for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, s));
         RC(timer_end(c, rec));
-        RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
+        RC(run_sync(c, c->sync_a));
+        RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, last, s));
+        RC(timer_end(c, rec));
+        RC(run_sync(c, c->sync_b));
+        RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
+        for (const LBlock &b : c->blocks) RC(launch_fused_c1(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, nbad, s));
+        RC(timer_end(c, rec));
+        if (ffs) {
+            RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
+            for (const LBlock &b : c->blocks)
+                RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, last, s));
+            RC(timer_end(c, rec));
+            RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
+        }
+        return OCN_OK;
+    }
+    RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
+    for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, tau, s));
+    RC(fork_sync(c, c->sync_a));
+    for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, tau, s));
+    RC(timer_end(c, rec));
+    RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
+    for (const LBlock &b : c->blocks)
+        RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, tau, last, s));
+    RC(join_sync(c));
+    for (const LBlock &b : c->blocks)
+        RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, tau, last, s));
+    RC(fork_sync(c, c->sync_b));
+    RC(timer_end(c, rec));
+    RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
+    for (const LBlock &b : c->blocks) RC(launch_fused_c1(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, nbad, s));
+    RC(join_sync(c));
+    for (const LBlock &b : c->blocks) RC(launch_fused_c1(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, nbad, s));
+    RC(timer_end(c, rec));
+    if (ffs) {
+        RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, last, s));
+        RC(fork_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, last, s));
+        RC(join_sync(c));
+        RC(timer_end(c, rec));
     }
     return OCN_OK;
 }
@@ -895,6 +963,9 @@ int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_de
     set_mask(c, mask);
     int rc = check_hip(hipSetDevice(dec->device), "hipSetDevice");
     if (!rc) rc = check_hip(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!rc) rc = check_hip(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming), "hipEventCreate");
+    if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming), "hipEventCreate");
     if (!rc) rc = decompose(c);
     if (!rc) rc = allocate(c);
     if (!rc) rc = prebuild_plans(c);
@@ -970,6 +1041,10 @@ int ocn_ctx_destroy(ocn_ctx *c)
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
     for (void *p : c->allocs) (void)hipFree(p);
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return OCN_OK;
@@ -1152,6 +1227,10 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         if (c->fused != (value != 0)) drop_graphs(c);
         c->fused = value != 0;
         return OCN_OK;
+    case OCN_OPT_OVERLAP:
+        if (c->overlap != (value != 0)) drop_graphs(c);
+        c->overlap = value != 0;
+        return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -1168,6 +1247,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_GRAPH: *value = c->use_graph; return OCN_OK;
     case OCN_OPT_STAGE_TIMING: *value = c->stage_timing; return OCN_OK;
     case OCN_OPT_FUSED: *value = c->fused; return OCN_OK;
+    case OCN_OPT_OVERLAP: *value = c->overlap; return OCN_OK;
     case OCN_OPT_COMPACT: *value = c->fused && c->compact; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }

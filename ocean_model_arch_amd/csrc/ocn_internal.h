@@ -36,15 +36,17 @@ struct Compact {
 };
 
 // Fused step groups (sw_kernels.hip); `ptr` = the block's field table indexed by field_slot(),
-// `cp` = its compact tables or nullptr for the 2-D real(4) arrays.
-int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, double tau,
-                   hipStream_t s);
-int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, double tau,
-                   bool full, hipStream_t s);
-int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw,
+// `cp` = its compact tables or nullptr for the 2-D real(4) arrays, `part` = which part of the
+// launch range (sw_stencils.h frame_rects: the halo-overlap split).
+enum { OCN_PART_ALL = 0, OCN_PART_FRAME = 1, OCN_PART_INNER = 2 };
+int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
+                   double tau, hipStream_t s);
+int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
+                   double tau, bool full, hipStream_t s);
+int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
                     int32_t *nbad, hipStream_t s);
-int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, bool full,
-                    hipStream_t s);
+int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
+                    bool full, hipStream_t s);
 // Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
 // they cannot be used into *flags (device int).
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s);

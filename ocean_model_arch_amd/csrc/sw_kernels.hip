@@ -49,6 +49,35 @@ static int launch_range(int m0, int m1, int n0, int n1, const Body &body, hipStr
     return check_launch();
 }
 
+// the frame part of a split range (sw_stencils.h frame_rects): one thread per point
+template <typename Body>
+__global__ __launch_bounds__(256) void k_frame(Rects q, int total, Body body)
+{
+    const int t = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (t >= total) return;
+    int m, n;
+    frame_point(q, t, m, n);
+    body(m, n);
+}
+
+// part: OCN_PART_ALL = R, OCN_PART_FRAME = R minus `inner`, OCN_PART_INNER = R clipped to `inner`
+template <typename Body>
+static int launch_part(const Range &r, const Range &inner, int part, const Body &body, hipStream_t s)
+{
+    if (part == OCN_PART_INNER) {
+        const Range i = range_clip(r, inner);
+        return launch_range(i.m0, i.m1, i.n0, i.n1, body, s);
+    }
+    if (part == OCN_PART_FRAME) {
+        const Rects q = frame_rects(r, inner);
+        const int total = q.total();
+        if (total == 0) return OCN_OK;
+        hipLaunchKernelGGL(k_frame<Body>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, q, total, body);
+        return check_launch();
+    }
+    return launch_range(r.m0, r.m1, r.n0, r.n1, body, s);
+}
+
 #define CHECK(...)                                                \
     do {                                                          \
         int _rc = check_block(b);                                 \
@@ -86,16 +115,16 @@ static int nonnull(std::initializer_list<const void *> ps)
 // cp == nullptr: the real(4) fields are read from the 2-D arrays; otherwise from the block's
 // compact tables (sw_stencils.h "compact static fields", built by launch_prepare).
 template <template <bool> class Make, typename... A>
-static int launch_fused(const Range &r, const ocn_block *b, void *const *ptr, const Compact *cp, hipStream_t s,
-                        A... a)
+static int launch_fused(const Range &r, const Range &inner, int part, const ocn_block *b, void *const *ptr,
+                        const Compact *cp, hipStream_t s, A... a)
 {
     RC_K(check_block(b));
     if (cp) {
         const Tab<true> t{ptr, cp->bits, cp->rows, block_rows(b)};
-        return launch_range(r.m0, r.m1, r.n0, r.n1, Make<true>::make(b, t, a...), s);
+        return launch_part(r, inner, part, Make<true>::make(b, t, a...), s);
     }
     const Tab<false> t{ptr};
-    return launch_range(r.m0, r.m1, r.n0, r.n1, Make<false>::make(b, t, a...), s);
+    return launch_part(r, inner, part, Make<false>::make(b, t, a...), s);
 }
 template <bool C> struct MkA {
     static FusedA<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau)
@@ -122,28 +151,28 @@ template <bool C> struct MkC2 {
     }
 };
 
-int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, double tau,
-                   hipStream_t s)
+int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
+                   double tau, hipStream_t s)
 {
-    return launch_fused<MkA>(range_fused_a(b, sw), b, ptr, cp, s, sw, tau);
+    return launch_fused<MkA>(range_fused_a(b, sw), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, tau);
 }
 
-int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, double tau,
-                   bool full, hipStream_t s)
+int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
+                   double tau, bool full, hipStream_t s)
 {
-    return launch_fused<MkB>(range_interior(b), b, ptr, cp, s, sw, tau, full);
+    return launch_fused<MkB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, tau, full);
 }
 
-int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw,
+int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
                     int32_t *nbad, hipStream_t s)
 {
-    return launch_fused<MkC1>(range_ring(b), b, ptr, cp, s, sw, nbad);
+    return launch_fused<MkC1>(range_ring(b), range_interior(b), part, b, ptr, cp, s, sw, nbad);
 }
 
-int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, const ocn_sw_params &sw, bool full,
-                    hipStream_t s)
+int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
+                    bool full, hipStream_t s)
 {
-    return launch_fused<MkC2>(range_bnd(b), b, ptr, cp, s, sw, full);
+    return launch_fused<MkC2>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, full);
 }
 
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s)

@@ -598,6 +598,53 @@ inline Range range_fused_a(const ocn_block *b, const ocn_sw_params &sw)
     return {b->nx_start - o, b->nx_end, b->ny_start - o, b->ny_end};
 }
 
+// Halo-overlap split of a launch range R (OCN_OPT_OVERLAP): the "inner" part is R clipped to
+// a rectangle whose points neither read halo values nor produce values a neighbour receives;
+// the "frame" is the rest of R, as up to four rectangles (bottom, top, left, right).
+//   fused A, fused B, hh_init: inner = [start+1, end-1]^2 (stencils reach +-1 only inside the
+//     interior; the interior's outer lines are what neighbours receive);
+//   fused C1 (pointwise): inner = [start, end]^2 (only the halo ring reads exchanged values).
+struct Rects {
+    int m0[4], n0[4], w[4], h[4];
+    int total() const { return w[0] * h[0] + w[1] * h[1] + w[2] * h[2] + w[3] * h[3]; }
+};
+inline Range range_clip(const Range &r, const Range &i)
+{
+    return {i.m0 > r.m0 ? i.m0 : r.m0, i.m1 < r.m1 ? i.m1 : r.m1, i.n0 > r.n0 ? i.n0 : r.n0,
+            i.n1 < r.n1 ? i.n1 : r.n1};
+}
+inline bool range_empty(const Range &r) { return r.m1 < r.m0 || r.n1 < r.n0; }
+inline Rects frame_rects(const Range &r, const Range &inner)
+{
+    Rects q{};
+    const Range i = range_clip(r, inner);
+    if (range_empty(r)) return q;
+    if (range_empty(i)) {
+        q.m0[0] = r.m0; q.n0[0] = r.n0; q.w[0] = r.m1 - r.m0 + 1; q.h[0] = r.n1 - r.n0 + 1;
+        return q;
+    }
+    const int w = r.m1 - r.m0 + 1;
+    q.m0[0] = r.m0; q.n0[0] = r.n0;     q.w[0] = w;             q.h[0] = i.n0 - r.n0;   // bottom
+    q.m0[1] = r.m0; q.n0[1] = i.n1 + 1; q.w[1] = w;             q.h[1] = r.n1 - i.n1;   // top
+    q.m0[2] = r.m0; q.n0[2] = i.n0;     q.w[2] = i.m0 - r.m0;   q.h[2] = i.n1 - i.n0 + 1;   // left
+    q.m0[3] = i.m1 + 1; q.n0[3] = i.n0; q.w[3] = r.m1 - i.m1;   q.h[3] = i.n1 - i.n0 + 1;   // right
+    return q;
+}
+// point t (0 <= t < total) of the frame
+inline OCN_HD void frame_point(const Rects &q, int t, int &m, int &n)
+{
+    for (int k = 0; k < 4; ++k) {
+        const int cnt = q.w[k] * q.h[k];
+        if (t < cnt) { m = q.m0[k] + t % q.w[k]; n = q.n0[k] + t / q.w[k]; return; }
+        t -= cnt;
+    }
+    m = n = 0;
+}
+inline Range inner_interior_shrunk(const ocn_block *b)
+{
+    return {b->nx_start + 1, b->nx_end - 1, b->ny_start + 1, b->ny_end - 1};
+}
+
 inline Prepare make_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int *flags)
 {
     Prepare k{geo(b), b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, {}, bits, rows,

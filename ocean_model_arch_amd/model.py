@@ -125,6 +125,11 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FUSED, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_overlap(self, on: bool = True):
+        """Overlap halo exchanges (comm stream) with the interior part of the fused launches (default)."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_OVERLAP, int(on)), "ocn_ctx_set_option")
+        return self
+
     def set_compact(self, on: bool = True):
         """Compact static fields for the fused step (bit-packed masks, per-row metrics) when exact
         for the current real(4) fields; re-arms them after raw real(4) pointers were handed out."""

@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #define OCN_HD
 #define OCN_INLINE inline
@@ -32,8 +33,20 @@ template <class K> static void run(const Range &r, const K &k)
         for (int m = r.m0; m <= r.m1; ++m) k(m, n);
 }
 
+// part 0 = whole range, 1 = frame (frame_rects, in the device kernel's point order), 2 = inner
+template <class K> static void run_part(const Range &r, const Range &inner, int part, const K &k)
+{
+    if (part == 2) { run(range_clip(r, inner), k); return; }
+    if (part == 1) {
+        const Rects q = frame_rects(r, inner);
+        for (int t = 0, n = q.total(); t < n; ++t) { int m, nn; frame_point(q, t, m, nn); k(m, nn); }
+        return;
+    }
+    run(r, k);
+}
+
 template <bool C> static void run_stage(int stage, const ocn_block *b, const Tab<C> &t, const ocn_sw_params *sw,
-                                        double tau, int32_t *nbad, bool full)
+                                        double tau, int32_t *nbad, bool full, int part)
 {
     switch (stage) {
     case OCN_STAGE_SW_UPDATE_SSH: run(range_interior(b), make_sw_update_ssh(b, t, tau)); break;
@@ -45,26 +58,50 @@ template <bool C> static void run_stage(int stage, const ocn_block *b, const Tab
     case OCN_STAGE_SW_UPDATE_UV: run(range_interior(b), make_sw_update_uv(b, t, tau)); break;
     case OCN_STAGE_SW_NEXT_STEP: run(range_ring(b), make_sw_next_step(b, t, sw->time_smooth)); break;
     case OCN_STAGE_HH_SHIFT: run(range_ring(b), make_hh_shift(b, t, sw->time_smooth)); break;
-    case OCN_STAGE_HH_INIT: run(range_bnd(b), make_hh_init(b, t, sw->full_free_surface, full)); break;
+    case OCN_STAGE_HH_INIT:
+        run_part(range_bnd(b), inner_interior_shrunk(b), part, make_hh_init(b, t, sw->full_free_surface, full));
+        break;
     case OCN_STAGE_CHECK_SSH_ERR: run(range_interior(b), make_check_ssh_err(b, t, nbad)); break;
-    case 11: run(range_fused_a(b, *sw), make_fused_a(b, t, *sw, tau)); break;
-    case 12: run(range_interior(b), make_fused_b(b, t, *sw, tau, full)); break;
-    case 13: run(range_ring(b), make_fused_c1(b, t, *sw, nbad)); break;
+    case 11: run_part(range_fused_a(b, *sw), inner_interior_shrunk(b), part, make_fused_a(b, t, *sw, tau)); break;
+    case 12: run_part(range_interior(b), inner_interior_shrunk(b), part, make_fused_b(b, t, *sw, tau, full)); break;
+    case 13: run_part(range_ring(b), range_interior(b), part, make_fused_c1(b, t, *sw, nbad)); break;
     default: g_oob = -1;
     }
 }
 
 // stage: 0..9 = OCN_STAGE_* (reference stages), 10 = check_ssh_err, 11/12/13 = fused A/B/C1.
 // bits/rows: the block's compact tables (hst_prepare) or nullptr for the 2-D real(4) arrays;
-// full: HhInit::full.  Returns the number of out-of-bounds accesses detected (0 = clean).
+// full: FusedB / HhInit `full`; part: the halo-overlap split (fused A/B/C1, hh_init).
+// Returns the number of out-of-bounds accesses detected (0 = clean).
 extern "C" long hst_stage(int stage, const ocn_block *b, void *const *ptr, const uint8_t *bits, const float *rows,
-                          const ocn_sw_params *sw, double tau, int32_t *nbad, int full)
+                          const ocn_sw_params *sw, double tau, int32_t *nbad, int full, int part)
 {
     g_oob = 0;
     ocn_host_limit = (unsigned)(b->pitch * (int64_t)(b->bnd_y2 - b->bnd_y1 + 1));
-    if (bits) run_stage(stage, b, Tab<true>{ptr, bits, rows, block_rows(b)}, sw, tau, nbad, full != 0);
-    else run_stage(stage, b, Tab<false>{ptr}, sw, tau, nbad, full != 0);
+    if (bits) run_stage(stage, b, Tab<true>{ptr, bits, rows, block_rows(b)}, sw, tau, nbad, full != 0, part);
+    else run_stage(stage, b, Tab<false>{ptr}, sw, tau, nbad, full != 0, part);
     return g_oob;
+}
+
+// Frame/inner split of a range: 1 if every point of r is in exactly one of the two parts.
+extern "C" int hst_split_ok(int m0, int m1, int n0, int n1, int i0, int i1, int j0, int j1)
+{
+    const Range r{m0, m1, n0, n1}, inner{i0, i1, j0, j1};
+    const int w = m1 - m0 + 1, h = n1 - n0 + 1;
+    if (w <= 0 || h <= 0) return frame_rects(r, inner).total() == 0;
+    std::vector<int> hit((size_t)w * h, 0);
+    auto mark = [&](int m, int n) {
+        if (m < m0 || m > m1 || n < n0 || n > n1) { hit[0] += 100; return; }
+        ++hit[(size_t)(m - m0) + (size_t)(n - n0) * w];
+    };
+    const Rects q = frame_rects(r, inner);
+    for (int t = 0, n = q.total(); t < n; ++t) { int m, nn; frame_point(q, t, m, nn); mark(m, nn); }
+    const Range i = range_clip(r, inner);
+    for (int n = i.n0; n <= i.n1; ++n)
+        for (int m = i.m0; m <= i.m1; ++m) mark(m, n);
+    for (int v : hit)
+        if (v != 1) return 0;
+    return 1;
 }
 
 // The compact tables of a block (Prepare, thread grid = bnd range); returns the OCN_COMPACT_* flags.

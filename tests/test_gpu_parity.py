@@ -70,7 +70,7 @@ def test_kernels_match_reference(amd, geom):
     assert not failures, f"{geom}: differs from the reference: {failures}"
 
 
-def build_model(amd, case, graph=False, fused=True, compact=True):
+def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"])
@@ -79,6 +79,7 @@ def build_model(amd, case, graph=False, fused=True, compact=True):
     m = amd.OceanModel(basin, sw, par)
     m.set_fused(fused)
     m.set_compact(compact)
+    m.set_overlap(overlap)
     if graph:
         m.set_graph(True)
     return m
@@ -101,15 +102,17 @@ def compare_case(m, case, name):
     return bad
 
 
-@pytest.mark.parametrize("mode", ["compact", "fused", "stages"])
+@pytest.mark.parametrize("mode", ["compact", "fused", "stages", "serial"])
 @pytest.mark.parametrize("name", cases.E2E_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
-    """compact = the 4-launch step reading the compact static fields (default); fused = the same
-    on the 2-D real(4) arrays; stages = the reference's 11 envoke stages."""
+    """compact = the 4-launch step reading the compact static fields, halo exchanges overlapped
+    with inner launches when there are several blocks (the default); fused = the same on the 2-D
+    real(4) arrays; serial = compact without the overlap; stages = the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    m = build_model(amd, case, fused=mode != "stages", compact=mode == "compact")
+    m = build_model(amd, case, fused=mode != "stages", compact=mode in ("compact", "serial"),
+                    overlap=mode != "serial")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
-    assert m.compact_active == (mode == "compact")
+    assert m.compact_active == (mode in ("compact", "serial"))
     bad = compare_case(m, case, name)
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"

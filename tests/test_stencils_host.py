@@ -47,7 +47,8 @@ def hst():
     L = C.CDLL(LIB)
     L.hst_stage.restype = C.c_long
     L.hst_stage.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(SwParams),
-                            C.c_double, C.POINTER(C.c_int32), C.c_int]
+                            C.c_double, C.POINTER(C.c_int32), C.c_int, C.c_int]
+    L.hst_split_ok.argtypes = [C.c_int] * 8
     L.hst_prepare.restype = C.c_int
     L.hst_prepare.argtypes = [C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p]
     return L
@@ -79,7 +80,7 @@ def test_stage_functors_match_reference(hst, geom):
         arrs = {k[3:]: z[k].copy(order="F") for k in z.files if k.startswith("in/")}
         nbad = C.c_int32(0)
         oob = hst.hst_stage(STAGE_IDS[kname], C.byref(b), table(arrs), None, None, C.byref(sw), float(z["tau"]),
-                            C.byref(nbad), 1)
+                            C.byref(nbad), 1, 0)
         assert oob == 0, f"{kname}: {oob} out-of-bounds accesses"
         for nm in [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]:
             if not bits_equal(arrs[nm], z[f"{kname}/{nm}"]):
@@ -112,14 +113,42 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None):
     sw_o = om.sw
     sw = SwParams(sw_o.full_free_surface, sw_o.trans_terms, sw_o.ksw_lat, sw_o.time_smooth, sw_o.lvisc_2)
     blocks = [(Block(*b.args, b.bx2 - b.bx1 + 1), table(om.f[k])) for k, b in enumerate(om.blocks)]
-    compact = mode == "compact"
+    compact = mode in ("compact", "overlap_early", "overlap_late")
 
-    def each(stage, tau=1.0, full=1):
+    def each(stage, tau=1.0, full=1, part=0):
         for k, (b, t) in enumerate(blocks):
             bits, rows = (tabs[k][0].ctypes.data, tabs[k][1].ctypes.data) if compact else (None, None)
-            oob = hst.hst_stage(stage, C.byref(b), t, bits, rows, C.byref(sw), tau, C.byref(nbad), full)
+            oob = hst.hst_stage(stage, C.byref(b), t, bits, rows, C.byref(sw), tau, C.byref(nbad), full, part)
             assert oob == 0, f"stage {stage}: {oob} out-of-bounds accesses"
 
+    def syncs(names):
+        for f in names:
+            om.sync(f)
+
+    sa = ["sshn"] + (["hhu_n", "hhv_n", "hhh_n"] if sw.full_free_surface > 0 else []) + \
+         (["vort"] if sw.trans_terms > 0 else []) + (["str_t", "str_s"] if sw.ksw_lat > 0 else [])
+    sb = (["hhu_p", "hhv_p", "hhh_p"] if sw.trans_terms > 0 else []) + ["vbrtrn", "ubrtrn"]
+    if mode in ("overlap_early", "overlap_late"):
+        # ocn_ctx.hip one_step_fused with OCN_OPT_OVERLAP: each exchange runs concurrently with
+        # the inner launches; emulate it completing as early and as late as possible
+        early = mode == "overlap_early"
+        FR, IN = 1, 2
+        each(FUSED_A, part=FR)
+        if early: syncs(sa)
+        each(FUSED_A, part=IN)
+        each(FUSED_B, full=int(last), part=IN)
+        if not early: syncs(sa)
+        each(FUSED_B, full=int(last), part=FR)
+        if early: syncs(sb)
+        each(FUSED_C1, part=IN)
+        if not early: syncs(sb)
+        each(FUSED_C1, part=FR)
+        if sw.full_free_surface > 0:
+            each(STAGE_IDS["hh_init"], full=int(last), part=FR)
+            if early: syncs(["hhu", "hhv", "hhh"])
+            each(STAGE_IDS["hh_init"], full=int(last), part=IN)
+            if not early: syncs(["hhu", "hhv", "hhh"])
+        return
     if mode != "stages":
         each(FUSED_A)
         sa = ["sshn"] + (["hhu_n", "hhv_n", "hhh_n"] if sw.full_free_surface > 0 else []) + \
@@ -149,7 +178,7 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None):
         each(CHECK)
 
 
-@pytest.mark.parametrize("mode", ["compact", "fused", "stages"])
+@pytest.mark.parametrize("mode", ["compact", "fused", "stages", "overlap_early", "overlap_late"])
 @pytest.mark.parametrize("name", cases.E2E_CASES)
 def test_host_step_matches_reference(hst, name, mode):
     """The whole run as one ocn_ctx_step call: hh_init's time-invariant stores are skipped on
@@ -162,7 +191,7 @@ def test_host_step_matches_reference(hst, name, mode):
                        O.SWConfig(**case["sw"]), *case["bxy"]).init()
     nbad = C.c_int32(0)
     tabs = None
-    if mode == "compact":
+    if mode in ("compact", "overlap_early", "overlap_late"):
         tabs = compact_tables(hst, om)
         assert all(t[2] == 0 for t in tabs), [t[2] for t in tabs]
     for s in range(case["steps"]):
@@ -207,3 +236,11 @@ def test_compact_row_window_is_what_the_stencils_read(hst):
         host_step(hst, ref, "stages", nbad)
     for nm in ref.f[0]:
         assert bits_equal(om.f[0][nm], ref.f[0][nm]), nm
+
+
+@pytest.mark.parametrize("r,inner", [((1, 40, 1, 30), (3, 38, 3, 28)), ((2, 9, 2, 9), (3, 8, 3, 8)),
+                                     ((5, 6, 5, 6), (6, 5, 6, 5)), ((0, 63, 0, 0), (1, 62, 1, -1)),
+                                     ((3, 70, 3, 70), (0, 100, 0, 100)), ((3, 70, 3, 70), (10, 20, 50, 60))])
+def test_frame_inner_split_partitions_the_range(hst, r, inner):
+    """The halo-overlap split: frame + inner cover every point of the launch range exactly once."""
+    assert hst.hst_split_ok(*r, *inner) == 1
