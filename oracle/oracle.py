@@ -83,6 +83,15 @@ class SWConfig:
     ksw_lat: int = 1
     time_smooth: float = 0.5
     lvisc_2: float = 1.0e3
+    use_tracers: int = 0
+    tracer_num: int = 1
+
+
+def tracer_fields(sw: SWConfig) -> list[str]:
+    """core/ocean.f90:38-41, 90-100: flux_x, flux_y and ff1/ff1p/ff1n per tracer (1-based)."""
+    if sw.use_tracers <= 0:
+        return []
+    return ["flux_x", "flux_y"] + [f"{p}_{k}" for k in range(1, sw.tracer_num + 1) for p in ("ff1", "ff1p", "ff1n")]
 
 
 def read_mask_file(path: str, nx: int, ny: int) -> np.ndarray:
@@ -174,7 +183,7 @@ class OracleModel:
             d = {}
             for name in R4_FIELDS + AUX_R4:
                 d[name] = np.zeros(b.shape, dtype=np.float32, order="F")
-            for name in R8_FIELDS:
+            for name in R8_FIELDS + tracer_fields(sw):
                 d[name] = np.zeros(b.shape, dtype=np.float64, order="F")
             self.f.append(d)
         self.L = lib()
@@ -244,12 +253,24 @@ class OracleModel:
                 f[nm][...] = 0.0
             f["mu"][...] = self.sw.lvisc_2
             f["mu"][...] = 0.0
+        if self.sw.use_tracers > 0:                    # init_data.f90:80-90
+            for t in range(1, self.sw.tracer_num + 1):
+                for k, b in enumerate(self.blocks):
+                    L.orc_gaussian_elimination(*b.args, _p(self.f[k]["lu"]), _p(self.f[k][f"ff1_{t}"]),
+                                               C.c_double(0.5), bc.nx // 2, bc.ny // 2)
+                self.sync(f"ff1_{t}")
+                for f in self.f:
+                    f[f"ff1n_{t}"][...] = f[f"ff1_{t}"]; f[f"ff1p_{t}"][...] = f[f"ff1_{t}"]
+            for f in self.f:
+                f["flux_x"][...] = 0.0; f["flux_y"][...] = 0.0
 
     # ---------------------------------------------------------------- stages (a1..a10)
-    def _each(self, fn, *names, scalars=()):
+    def _each(self, fn, *names, scalars=(), tau=None):
+        """fn(bounds, scalars..., arrays...) per block; the names "TAU" / "ONE" pass tau / 1.0d0 by value."""
         for k, b in enumerate(self.blocks):
             f = self.f[k]
-            fn(*b.args, *scalars, *[_p(f[n]) for n in names])
+            fn(*b.args, *scalars, *[C.c_double(tau) if n == "TAU" else C.c_double(1.0) if n == "ONE" else _p(f[n])
+                                    for n in names])
 
     def stage_sw_update_ssh(self, tau):
         self._each(self.L.orc_sw_update_ssh, "lu", "dx", "dy", "dxh", "dyh", "hhu", "hhv",
@@ -306,6 +327,32 @@ class OracleModel:
         for nm in ("hhu", "hhv", "hhh"):
             self.sync(nm)
 
+    # ---------------------------------------------------------------- tracers (control/tracer.f90)
+    def stage_tran_diff_fluxes(self, t: int):
+        """interface/tracer/tracer_interface.f90:28-59 (factor_mu = 1.0d0) + sync flux_x, flux_y."""
+        self._each(self.L.orc_tran_diff_fluxes, "lcu", "lcv", "dxt", "dyt", "dxh", "dyh", "hhu", "hhv",
+                   f"ff1_{t}", f"ff1p_{t}", "ubrtr", "vbrtr", "mu", "ONE", "flux_x", "flux_y")
+        self.sync("flux_x"); self.sync("flux_y")
+
+    def stage_tran_diff_tracer(self, t: int, tau: float):
+        """tracer_interface.f90:61-86 + sync ff1n."""
+        self._each(self.L.orc_tran_diff_tracer, "lu", "dx", "dy", "TAU", "hhq_n", "hhq_p", "flux_x", "flux_y",
+                   f"ff1p_{t}", f"ff1n_{t}", tau=tau)
+        self.sync(f"ff1n_{t}")
+
+    def stage_tracer_next_step(self, t: int):
+        """tracer_interface.f90:88-104 (no sync)."""
+        self._each(self.L.orc_tracer_next_step, "lu", f"ff1n_{t}", f"ff1p_{t}", f"ff1_{t}",
+                   scalars=(C.c_double(self.sw.time_smooth),))
+
+    def expl_tracer(self, tau: float = 1.0):
+        """control/tracer.f90:33-62."""
+        if self.sw.use_tracers > 0:
+            for t in range(1, self.sw.tracer_num + 1):
+                self.stage_tran_diff_fluxes(t)
+                self.stage_tran_diff_tracer(t, tau)
+                self.stage_tracer_next_step(t)
+
     def check_ssh_err(self) -> int:
         bad = 0
         for k, b in enumerate(self.blocks):
@@ -313,7 +360,7 @@ class OracleModel:
         return bad
 
     def step(self, tau: float = 1.0):
-        """control/shallow_water/shallow_water.f90:22-94 (expl_shallow_water)."""
+        """One model time step (model.f90:146-160): expl_shallow_water (shallow_water.f90:22-94), then expl_tracer."""
         sw = self.sw
         self.stage_sw_update_ssh(tau)
         if sw.full_free_surface > 0:
@@ -331,6 +378,7 @@ class OracleModel:
             self.stage_hh_init()
         if self.check_ssh_err():
             raise FloatingPointError("SIGFPRE predict error (check_ssh_err_kernel)")
+        self.expl_tracer(tau)                          # model.f90:156
 
     def run(self, steps: int, tau: float = 1.0):
         for _ in range(steps):

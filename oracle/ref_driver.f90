@@ -2,10 +2,11 @@
 !
 ! Drives the unmodified, compiled reference (oracle/_ref, see oracle/ref.mk) through
 ! exactly the init sequence of model.f90:47-91 (mpp_init, basin.par/sw.par/parallel.par,
-! read_global_mask, domain init, init_grid_data, init_ocean_data) and then NSTEPS calls of
-! expl_shallow_water(tau) (control/shallow_water/shallow_water.f90:22), with tau = 1 s
-! (ocean_run.par line 2).  Afterwards every field the SW step touches is dumped, per
-! block, with its bounds, as raw little-endian stream records into DUMPFILE.
+! read_global_mask, domain init, init_grid_data, init_ocean_data) and then NSTEPS model steps
+! (model.f90:146-160: expl_shallow_water(tau), control/shallow_water/shallow_water.f90:22,
+! then expl_tracer(tau), control/tracer.f90:33), with tau = 1 s (ocean_run.par line 2).
+! Afterwards every field the step touches is dumped, per block, with its bounds, as raw
+! little-endian stream records into DUMPFILE (header: block count, tracer count).
 !
 ! usage (in a directory holding basin.par, sw.par, parallel.par):
 !     ref_driver NSTEPS DUMPFILE
@@ -13,7 +14,7 @@ program ref_driver
     use kind_module, only: wp8 => SHR_KIND_R8, wp4 => SHR_KIND_R4
     use mpp_module
     use config_basinpar_module, only: load_config_basinpar_from_file
-    use config_sw_module, only: load_config_sw_from_file
+    use config_sw_module, only: load_config_sw_from_file, use_tracers, tracer_num
     use config_parallel_module, only: load_config_parallel_from_file_and_cmd
     use decomposition_module, only: domain_data
     use mpp_sync_module, only: mpp_sync_init
@@ -22,10 +23,11 @@ program ref_driver
     use io_module, only: read_global_mask
     use init_data_module, only: init_grid_data, init_ocean_data
     use shallow_water_module, only: expl_shallow_water
+    use tracer_control_module, only: expl_tracer
     use data_types_module, only: data2D_real8_type, data2D_real4_type
     implicit none
 
-    integer :: nsteps, step, k, ierr
+    integer :: nsteps, step, k, ierr, t, ntr
     character(len=256) :: arg, dumpfile
     real(wp8) :: tau
     integer, parameter :: u = 77
@@ -51,12 +53,15 @@ program ref_driver
     !$omp parallel default(shared) private(step)
     do step = 1, nsteps
         call expl_shallow_water(tau)
+        call expl_tracer(tau)
     enddo
     !$omp end parallel
 
     if (mpp_rank == 0) then
         open(u, file=trim(dumpfile), access='stream', form='unformatted', status='replace')
-        write(u) domain_data%bcount
+        ntr = 0
+        if (use_tracers > 0) ntr = tracer_num
+        write(u) domain_data%bcount, ntr
         do k = 1, domain_data%bcount
             write(u) domain_data%bindx(k, 1), domain_data%bindx(k, 2),                    &
                      domain_data%bnx_start(k), domain_data%bnx_end(k),                    &
@@ -93,6 +98,13 @@ program ref_driver
                      ocean_data%RHSx%block(k)%field, ocean_data%RHSy%block(k)%field,      &
                      ocean_data%RHSx_adv%block(k)%field, ocean_data%RHSy_adv%block(k)%field, &
                      ocean_data%RHSx_dif%block(k)%field, ocean_data%RHSy_dif%block(k)%field
+            if (ntr > 0) then
+                write(u) ocean_data%flux_x%block(k)%field, ocean_data%flux_y%block(k)%field
+                do t = 1, ntr
+                    write(u) ocean_data%ff1(t)%block(k)%field, ocean_data%ff1p(t)%block(k)%field,  &
+                             ocean_data%ff1n(t)%block(k)%field
+                enddo
+            endif
         enddo
         close(u)
     endif

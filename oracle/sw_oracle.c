@@ -403,6 +403,68 @@ void orc_hh_shift(BND_ARGS, double ts, const float *lu, const float *llu, const 
 /* ------------------------------------------------------------------------- */
 /* Grid setup (runs once).                                                   */
 
+/* ---------------------------------------------------------------- tracers
+ * kernel/tracer/leapfrog_tracer.f90:13-92 tran_diff_fluxes_kernel (interior; flux_x on lcu,
+ * flux_y on lcv; flux_gm = 0.0d0 is still added, so -0.0 sums become +0.0). */
+void orc_tran_diff_fluxes(BND_ARGS, const float *lcu, const float *lcv, const float *dxt, const float *dyt,
+                          const float *dxh, const float *dyh, const double *hhu, const double *hhv,
+                          const double *ff, const double *ffp, const double *uu, const double *vv,
+                          const double *mu, double factor_mu, double *flux_x, double *flux_y)
+{
+    (void)ffp; (void)by2;
+    for (int n = nys; n <= nye; ++n)
+        for (int m = nxs; m <= nxe; ++m) {
+            const long c = I(m, n), e = I(m + 1, n), nn = I(m, n + 1);
+            if (lcu[c] > 0.5f) {
+                const double dfdx = ff[e] - ff[c];
+                const double mu_1d = (mu[c] + mu[e]) / 2.0 * factor_mu * (double)dyh[c] / (double)dxt[c];
+                const double flux_diff = mu_1d * hhu[c] * dfdx;
+                const double flux_adv = -uu[c] * hhu[c] * (double)dyh[c] * (ff[c] + ff[e]) / 2.0;
+                flux_x[c] = flux_adv + flux_diff + 0.0;
+            }
+            if (lcv[c] > 0.5f) {
+                const double dfdy = ff[nn] - ff[c];
+                const double mu_1d = (mu[c] + mu[nn]) / 2.0 * factor_mu * (double)dxh[c] / (double)dyt[c];
+                const double flux_diff = mu_1d * hhv[c] * dfdy;
+                const double flux_adv = -vv[c] * hhv[c] * (double)dxh[c] * (ff[c] + ff[nn]) / 2.0;
+                flux_y[c] = flux_adv + flux_diff + 0.0;
+            }
+        }
+}
+
+/* leapfrog_tracer.f90:94-136 tran_diff_tracer_kernel (interior, lu). */
+void orc_tran_diff_tracer(BND_ARGS, const float *lu, const float *dx, const float *dy, double tau,
+                          const double *hhqn, const double *hhqp, const double *flux_x, const double *flux_y,
+                          const double *ffp, double *ffn)
+{
+    (void)by2;
+    for (int n = nys; n <= nye; ++n)
+        for (int m = nxs; m <= nxe; ++m) {
+            const long c = I(m, n);
+            if (lu[c] > 0.5f) {
+                const double bp = hhqn[c] * (double)dx[c] * (double)dy[c] / tau / 2.0;
+                const double bp0 = hhqp[c] * (double)dx[c] * (double)dy[c] / tau / 2.0;
+                const double rhs = flux_x[c] - flux_x[I(m - 1, n)] + flux_y[c] - flux_y[I(m, n - 1)];
+                const double eta = bp0 * ffp[c] + rhs;
+                ffn[c] = eta / bp;
+            }
+        }
+}
+
+/* leapfrog_tracer.f90:138-168 tracer_next_step_kernel (interior + halo ring, lu). */
+void orc_tracer_next_step(BND_ARGS, double ts, const float *lu, const double *ffn, double *ffp, double *ff)
+{
+    (void)by2;
+    for (int n = nys - 1; n <= nye + 1; ++n)
+        for (int m = nxs - 1; m <= nxe + 1; ++m) {
+            const long c = I(m, n);
+            if (lu[c] > 0.5f) {
+                ffp[c] = ff[c] + ts * (ffn[c] - 2.0 * ff[c] + ffp[c]) / 2.0;
+                ff[c] = ffn[c];
+            }
+        }
+}
+
 /* kernel/service/grid_kernels.f90:18-38  lu_init_kernel: mask is global (nx, ny) column-major */
 void orc_lu_init(int bx1, int bx2, int by1, int by2, int nx, const int32_t *mask, float *lu, float *lu1)
 {

@@ -8,9 +8,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 E2E_CASES = ["box40x32_b2x2_s5", "box70x54_b1x1_s20", "box70x54_b3x2_s20",
              "box48x40_flags000_s10", "box48x40_cart_s10", "bs_b1x1_s60", "bs_b4x2_s60"]
+TRACER_E2E_CASES = ["box40x32_tr2_s5", "box70x54_b3x2_tr_s20", "bs_b4x2_tr_s60"]
 KERNEL_GEOMS = ["b66x50", "b1x1", "b130x7"]
 KERNEL_NAMES = ["sw_update_ssh", "sw_update_uv", "sw_next_step", "uv_trans_vort", "uv_trans",
                 "uv_diff2", "stress_components", "hh_init", "hh_update", "hh_shift"]
+TRACER_KERNEL_NAMES = ["tran_diff_fluxes", "tran_diff_tracer", "tracer_next_step"]
 
 
 def _f(s):
@@ -31,6 +33,8 @@ def load_e2e(name):
             (basin["nx"], basin["ny"]), order="F")
     swc = dict(full_free_surface=int(sw["ffs"]), trans_terms=int(sw["trans"]), ksw_lat=int(sw["ksw"]),
                time_smooth=_f(sw["ts"]))
+    if int(sw.get("tr", 0)) > 0:
+        swc.update(use_tracers=int(sw["tr"]), tracer_num=int(sw["trn"]))
     return dict(basin=basin, sw=swc, bxy=tuple(int(v) for v in z["meta/bxy"]), steps=int(z["meta/steps"]),
                 mask=mask, z=z)
 

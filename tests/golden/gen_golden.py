@@ -101,6 +101,19 @@ KERNELS = {
                    ("dxb", "r4"), ("dyb", "r4"),
                    ("hhq_n", "r8o"), ("hhu_n", "r8o"), ("hhv_n", "r8o"), ("hhh_n", "r8o"),
                    ("ssh", "r8"), ("hhq_rest", "r8")]),
+    # kernel/tracer/leapfrog_tracer.f90:13 (factor_mu passed as 1.0d0 by tracer_interface.f90:47)
+    "tran_diff_fluxes": ("_QMtracer_modulePtran_diff_fluxes_kernel", [],
+                         [("lcu", "r4"), ("lcv", "r4"), ("dxt", "r4"), ("dyt", "r4"), ("dxh", "r4"), ("dyh", "r4"),
+                          ("hhu", "r8"), ("hhv", "r8"), ("ff1", "r8"), ("ff1p", "r8"), ("ubrtr", "r8"),
+                          ("vbrtr", "r8"), ("mu", "r8"), ("factor_mu", "f64"), ("flux_x", "r8o"),
+                          ("flux_y", "r8o")]),
+    # leapfrog_tracer.f90:94
+    "tran_diff_tracer": ("_QMtracer_modulePtran_diff_tracer_kernel", [],
+                         [("lu", "r4"), ("dx", "r4"), ("dy", "r4"), ("tau", "f64"), ("hhq_n", "r8"),
+                          ("hhq_p", "r8"), ("flux_x", "r8"), ("flux_y", "r8"), ("ff1p", "r8"), ("ff1n", "r8o")]),
+    # leapfrog_tracer.f90:138
+    "tracer_next_step": ("_QMtracer_modulePtracer_next_step_kernel", ["time_smooth"],
+                         [("lu", "r4"), ("ff1n", "r8"), ("ff1p", "r8o"), ("ff1", "r8o")]),
     # depth.f90:164 (module var time_smooth)
     "hh_shift": ("_QMdepth_modulePhh_shift_kernel", [],
                  [("lu", "r4"), ("llu", "r4"), ("llv", "r4"), ("luh", "r4"),
@@ -148,6 +161,11 @@ def random_state(rng: np.random.Generator, shape, ref) -> dict[str, np.ndarray]:
     s["str_t"] = f8(-1.0e-4, 1.0e-4)
     s["str_s"] = f8(-1.0e-4, 1.0e-4)
     s["mu"] = f8(0.0, 1.0e3)
+    # tracer state (drawn last: the inputs of the SW kernels above are unchanged by it)
+    for nm in ("ff1", "ff1p", "ff1n"):
+        s[nm] = f8(0.0, 0.5)
+    for nm in ("flux_x", "flux_y"):
+        s[nm] = f8(-1.0e-3, 1.0e-3)
     return s
 
 
@@ -158,7 +176,8 @@ def gen_kernels(ref, tag, geom, seed):
     rng = np.random.default_rng(seed)
     state = random_state(rng, shape, ref)
     out = {"geom": np.array([nxs, nxe, nys, nye, bx1, bx2, by1, by2], np.int32),
-           "tau": np.float64(1.0), "time_smooth": np.float64(0.5), "full_free_surface": np.int32(1)}
+           "tau": np.float64(1.0), "time_smooth": np.float64(0.5), "full_free_surface": np.int32(1),
+           "factor_mu": np.float64(0.7)}
     for nm, a in state.items():
         out["in/" + nm] = a
     C.c_double.in_dll(ref, "_QMconfig_sw_moduleEtime_smooth").value = 0.5
@@ -171,6 +190,8 @@ def gen_kernels(ref, tag, geom, seed):
         for nm, kind in args:
             if kind == "int":
                 cargs.append(C.byref(C.c_int(1)))
+            elif kind == "f64":
+                cargs.append(C.byref(C.c_double(float(out[nm]))))
             else:
                 cargs.append(work[nm].ctypes.data_as(C.c_void_p))
         getattr(ref, sym)(*cargs)
@@ -209,8 +230,8 @@ SW_TMPL = """{ffs} : full free surface
 {ksw} : ksw_lat
 {ts} : time smooth
 1.0d+03 : lvisc_2
-0 : tracers
-1 : tracer num
+{tr} : tracers
+{trn} : tracer num
 none : ssh init
 """
 PAR_TMPL = """0 : mod
@@ -238,8 +259,12 @@ CASES = {
     "box48x40_cart_s10": (dict(BOX, nx=48, ny=40, curve=0), dict(SW_DEFAULT, ts="0.25d0"), (1, 1), 10, True),
     "bs_b1x1_s60": (BS, SW_DEFAULT, (1, 1), 60, False),
     "bs_b4x2_s60": (BS, SW_DEFAULT, (4, 2), 60, False),
+    # tracers (config 5 = BS + 1 tracer on 4x2 blocks)
+    "box40x32_tr2_s5": (dict(BOX, nx=40, ny=32), dict(SW_DEFAULT, tr=1, trn=2), (2, 1), 5, True),
+    "box70x54_b3x2_tr_s20": (dict(BOX, nx=70, ny=54), dict(SW_DEFAULT, tr=1, trn=1), (3, 2), 20, False),
+    "bs_b4x2_tr_s60": (BS, dict(SW_DEFAULT, tr=1, trn=1), (4, 2), 60, False),
 }
-PROGNOSTIC = ["ssh", "sshp", "ubrtr", "ubrtrp", "vbrtr", "vbrtrp"]
+PROGNOSTIC = ["ssh", "sshp", "ubrtr", "ubrtrp", "vbrtr", "vbrtrp", "ff1_1", "ff1p_1"]
 
 
 def digest(a: np.ndarray) -> str:
@@ -250,7 +275,7 @@ def gen_e2e(name, basin, sw, bxy, steps, full):
     d = tempfile.mkdtemp()
     try:
         open(os.path.join(d, "basin.par"), "w").write(BASIN_TMPL.format(**basin))
-        open(os.path.join(d, "sw.par"), "w").write(SW_TMPL.format(**sw))
+        open(os.path.join(d, "sw.par"), "w").write(SW_TMPL.format(**dict(dict(tr=0, trn=1), **sw)))
         open(os.path.join(d, "parallel.par"), "w").write(PAR_TMPL.format(bx=bxy[0], by=bxy[1]))
         env = dict(os.environ, OMP_NUM_THREADS="1")
         subprocess.check_call([REFDRV, str(steps), "dump.bin"], cwd=d, env=env,
@@ -278,14 +303,17 @@ def gen_e2e(name, basin, sw, bxy, steps, full):
     print("wrote", path, os.path.getsize(path))
 
 
-def main():
+def main(which):
+    """which: nothing = everything; otherwise "kernels" and/or e2e case names."""
     subprocess.check_call(["make", "-s", "-f", os.path.join(REPO, "oracle", "ref.mk")], cwd=REPO)
     ref = C.CDLL(REFLIB)
-    for i, (tag, geom) in enumerate(GEOMS.items()):
-        gen_kernels(ref, tag, geom, 1234 + i)
+    if not which or "kernels" in which:
+        for i, (tag, geom) in enumerate(GEOMS.items()):
+            gen_kernels(ref, tag, geom, 1234 + i)
     for name, (basin, sw, bxy, steps, full) in CASES.items():
-        gen_e2e(name, basin, sw, bxy, steps, full)
+        if not which or name in which:
+            gen_e2e(name, basin, sw, bxy, steps, full)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -20,7 +20,7 @@ def read_dump(path):
         pos += a.nbytes
         return a
 
-    bcount = int(take("<i4", 1)[0])
+    bcount, ntr = (int(v) for v in take("<i4", 2))
     out = []
     for _ in range(bcount):
         bm, bn, nxs, nxe, nys, nye, bx1, bx2, by1, by2 = (int(v) for v in take("<i4", 10))
@@ -29,7 +29,10 @@ def read_dump(path):
         f = {}
         for name in R4_FIELDS:
             f[name] = take("<f4", n).reshape(shape, order="F").copy(order="F")
-        for name in R8_FIELDS:
+        names = list(R8_FIELDS)
+        if ntr > 0:
+            names += ["flux_x", "flux_y"] + [f"{p}_{t}" for t in range(1, ntr + 1) for p in ("ff1", "ff1p", "ff1n")]
+        for name in names:
             f[name] = take("<f8", n).reshape(shape, order="F").copy(order="F")
         out.append((dict(bm=bm, bn=bn, nxs=nxs, nxe=nxe, nys=nys, nye=nye,
                          bx1=bx1, bx2=bx2, by1=by1, by2=by2), f))

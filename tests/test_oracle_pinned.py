@@ -34,6 +34,13 @@ ORC_ARGS = {
                                          "hhv_p", "hhv_n", "hhh", "hhh_p", "hhh_n", "ssh", "sshp", "hhq_rest"]),
     "hh_update": ("orc_hh_update", [], ["lu", "llu", "llv", "luh", "dx", "dy", "dxt", "dyt", "dxh", "dyh", "dxb",
                                         "dyb", "hhq_n", "hhu_n", "hhv_n", "hhh_n", "ssh", "hhq_rest"]),
+    # kernel/tracer/leapfrog_tracer.f90; "@x" = the fixture's scalar x passed in place
+    "tran_diff_fluxes": ("orc_tran_diff_fluxes", [], ["lcu", "lcv", "dxt", "dyt", "dxh", "dyh", "hhu", "hhv", "ff1",
+                                                     "ff1p", "ubrtr", "vbrtr", "mu", "@factor_mu", "flux_x",
+                                                     "flux_y"]),
+    "tran_diff_tracer": ("orc_tran_diff_tracer", [], ["lu", "dx", "dy", "@tau", "hhq_n", "hhq_p", "flux_x", "flux_y",
+                                                     "ff1p", "ff1n"]),
+    "tracer_next_step": ("orc_tracer_next_step", ["time_smooth"], ["lu", "ff1n", "ff1p", "ff1"]),
     "hh_shift": ("orc_hh_shift", ["time_smooth"], ["lu", "llu", "llv", "luh", "hhq", "hhq_p", "hhq_n", "hhu",
                                                    "hhu_p", "hhu_n", "hhv", "hhv_p", "hhv_n", "hhh", "hhh_p",
                                                    "hhh_n"]),
@@ -57,12 +64,13 @@ def run_oracle_kernel(z, kname):
             sc.append(C.c_int(int(z["full_free_surface"])))
         else:
             sc.append(C.c_double(float(z[s])))
-    getattr(L, sym)(*geom, *sc, *[work[n].ctypes.data_as(C.c_void_p) for n in names])
+    getattr(L, sym)(*geom, *sc, *[C.c_double(float(z[n[1:]])) if n[0] == "@" else work[n].ctypes.data_as(C.c_void_p)
+                                  for n in names])
     return work
 
 
 @pytest.mark.parametrize("geom", cases.KERNEL_GEOMS)
-@pytest.mark.parametrize("kname", cases.KERNEL_NAMES)
+@pytest.mark.parametrize("kname", cases.KERNEL_NAMES + cases.TRACER_KERNEL_NAMES)
 def test_oracle_kernel_matches_reference(geom, kname):
     z = cases.load_kernels(geom)
     work = run_oracle_kernel(z, kname)
@@ -84,13 +92,14 @@ def build_oracle_model(case):
     return O.OracleModel(basin, sw, *case["bxy"])
 
 
-@pytest.mark.parametrize("name", cases.E2E_CASES)
+@pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
 def test_oracle_end_to_end_matches_reference(name):
     case = cases.load_e2e(name)
     z = case["z"]
     m = build_oracle_model(case).init().run(case["steps"])
     blocks = cases.e2e_blocks(z)
     assert len(blocks) == len(m.blocks)
+    checked = set()
     for k, blk in enumerate(m.blocks):
         info = blocks[(blk.bm, blk.bn)]
         assert list(info) == list(blk.args)
@@ -99,6 +108,9 @@ def test_oracle_end_to_end_matches_reference(name):
             if key not in z.files:
                 continue
             assert _sha(a) == str(z[key]), f"{name}: block ({blk.bm},{blk.bn}) field {nm} differs"
+            checked.add(nm)
+    if case["sw"].get("use_tracers", 0) > 0:
+        assert {"flux_x", "flux_y", "ff1_1", "ff1p_1", "ff1n_1"} <= checked
 
 
 def test_uniform_decomposition_sizes():
