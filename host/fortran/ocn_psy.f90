@@ -44,7 +44,7 @@ module ocn_psy
     type(ocn_block), allocatable, public :: blk(:)
     type(ocn_sw_params), public :: sw_params
 
-    public :: psy_init, envoke, expl_shallow_water, fld
+    public :: psy_init, envoke, expl_shallow_water, expl_tracer, fld
 
 contains
 
@@ -230,7 +230,66 @@ contains
         type(sync_parameters_type), intent(in) :: sp
     end subroutine
 
+    ! ------------------------------------------------------------- tracer wrappers
+    ! interface/tracer/tracer_interface.f90 (tracer = param%data_id)
+    subroutine envoke_tran_diff_fluxes_kernel(k, param)    ! tracer_interface.f90:28
+        integer, intent(in) :: k
+        type(kernel_parameters_type), intent(in) :: param
+        integer(c_int) :: t
+        t = OCN_TRACER_BASE + 3 * (param%data_id - 1)
+        call ocn_check(ocn_tran_diff_fluxes(blk(k), fld(k, OCN_LCU), fld(k, OCN_LCV), fld(k, OCN_DXT),          &
+                       fld(k, OCN_DYT), fld(k, OCN_DXH), fld(k, OCN_DYH), fld(k, OCN_HHU), fld(k, OCN_HHV),       &
+                       fld(k, t), fld(k, t + 1), fld(k, OCN_UBRTR), fld(k, OCN_VBRTR), fld(k, OCN_MU), 1.0d0,    &
+                       fld(k, OCN_FLUX_X), fld(k, OCN_FLUX_Y), ocn_ctx_stream(ctx)), 'tran_diff_fluxes')
+    end subroutine
+    subroutine envoke_tran_diff_fluxes_sync(k, sp)
+        integer, intent(in) :: k
+        type(sync_parameters_type), intent(in) :: sp
+        call ocn_check(ocn_ctx_sync(ctx, OCN_FLUX_X), 'sync'); call ocn_check(ocn_ctx_sync(ctx, OCN_FLUX_Y), 'sync')
+    end subroutine
+
+    subroutine envoke_tran_diff_tracer_kernel(k, param)    ! tracer_interface.f90:61
+        integer, intent(in) :: k
+        type(kernel_parameters_type), intent(in) :: param
+        integer(c_int) :: t
+        t = OCN_TRACER_BASE + 3 * (param%data_id - 1)
+        call ocn_check(ocn_tran_diff_tracer(blk(k), fld(k, OCN_LU), fld(k, OCN_DX), fld(k, OCN_DY), param%tau,   &
+                       fld(k, OCN_HHQ_N), fld(k, OCN_HHQ_P), fld(k, OCN_FLUX_X), fld(k, OCN_FLUX_Y),             &
+                       fld(k, t + 1), fld(k, t + 2), ocn_ctx_stream(ctx)), 'tran_diff_tracer')
+    end subroutine
+    subroutine envoke_tran_diff_tracer_sync(k, sp)
+        integer, intent(in) :: k
+        type(sync_parameters_type), intent(in) :: sp
+        call ocn_check(ocn_ctx_sync(ctx, int(OCN_TRACER_BASE + 3 * (sp%data_id - 1) + 2, c_int)), 'sync ff1n')
+    end subroutine
+
+    subroutine envoke_tracer_next_step_kernel(k, param)    ! tracer_interface.f90:88
+        integer, intent(in) :: k
+        type(kernel_parameters_type), intent(in) :: param
+        integer(c_int) :: t
+        t = OCN_TRACER_BASE + 3 * (param%data_id - 1)
+        call ocn_check(ocn_tracer_next_step(blk(k), param%time_smooth, fld(k, OCN_LU), fld(k, t + 2),             &
+                       fld(k, t + 1), fld(k, t), ocn_ctx_stream(ctx)), 'tracer_next_step')
+    end subroutine
+
     ! ------------------------------------------------------------- algorithm layer
+    ! control/tracer.f90:33-62
+    subroutine expl_tracer(tau)
+        real(c_double), intent(in) :: tau
+        type(kernel_parameters_type) :: p
+        integer :: k
+        if (sw_params%use_tracers <= 0) return
+        do k = 1, sw_params%tracer_num
+            call p%clear()
+            p%tau = tau
+            p%time_smooth = sw_params%time_smooth
+            p%data_id = k
+            call envoke(envoke_tran_diff_fluxes_kernel, envoke_tran_diff_fluxes_sync, p)
+            call envoke(envoke_tran_diff_tracer_kernel, envoke_tran_diff_tracer_sync, p)
+            call envoke(envoke_tracer_next_step_kernel, envoke_empty_sync, p)
+        enddo
+    end subroutine
+
     ! control/shallow_water/shallow_water.f90:22-94
     subroutine expl_shallow_water(tau)
         real(c_double), intent(in) :: tau

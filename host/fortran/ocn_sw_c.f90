@@ -24,7 +24,12 @@ module ocn_sw_c
                                  OCN_STR_T = 55, OCN_STR_S = 56, OCN_MU = 57, OCN_RHSX = 58, OCN_RHSY = 59,     &
                                  OCN_RHSX_ADV = 60, OCN_RHSY_ADV = 61, OCN_RHSX_DIF = 62, OCN_RHSY_DIF = 63,    &
                                  OCN_FIELD_END = 64
+    ! tracer storage (core/ocean.f90:38-41): flux_x, flux_y, then ff1/ff1p/ff1n of tracer k at
+    ! OCN_TRACER_BASE + 3*(k-1) + 0/1/2
+    integer(c_int), parameter :: OCN_FLUX_X = 64, OCN_FLUX_Y = 65, OCN_TRACER_BASE = 66
     integer(c_int), parameter :: OCN_STAGE_CHECK_SSH_ERR = 10
+    integer(c_int), parameter :: OCN_TSTAGE_TRAN_DIFF_FLUXES = 0, OCN_TSTAGE_TRAN_DIFF_TRACER = 1, &
+                                 OCN_TSTAGE_TRACER_NEXT_STEP = 2
 
     type, bind(C) :: ocn_block
         integer(c_int32_t) :: nx_start, nx_end, ny_start, ny_end
@@ -42,6 +47,7 @@ module ocn_sw_c
     type, bind(C) :: ocn_sw_params
         integer(c_int32_t) :: full_free_surface, trans_terms, ksw_lat
         real(c_double) :: time_smooth, lvisc_2
+        integer(c_int32_t) :: use_tracers, tracer_num
     end type
 
     type, bind(C) :: ocn_decomp
@@ -195,6 +201,37 @@ module ocn_sw_c
         end function
         type(c_ptr) function ocn_last_error() bind(C, name='ocn_last_error')
             import :: c_ptr
+        end function
+        ! kernel/tracer/leapfrog_tracer.f90:13, :94, :138
+        integer(c_int) function ocn_tran_diff_fluxes(b, lcu, lcv, dxt, dyt, dxh, dyh, hhu, hhv, ff, ffp, uu, vv, &
+                                                     mu, factor_mu, flux_x, flux_y, stream)                    &
+                                                     bind(C, name='ocn_tran_diff_fluxes')
+            import :: c_int, c_double, c_ptr, ocn_block
+            type(ocn_block), intent(in) :: b
+            type(c_ptr), value :: lcu, lcv, dxt, dyt, dxh, dyh, hhu, hhv, ff, ffp, uu, vv, mu
+            real(c_double), value :: factor_mu
+            type(c_ptr), value :: flux_x, flux_y, stream
+        end function
+        integer(c_int) function ocn_tran_diff_tracer(b, lu, dx, dy, tau, hhqn, hhqp, flux_x, flux_y, ffp, ffn,  &
+                                                     stream) bind(C, name='ocn_tran_diff_tracer')
+            import :: c_int, c_double, c_ptr, ocn_block
+            type(ocn_block), intent(in) :: b
+            type(c_ptr), value :: lu, dx, dy
+            real(c_double), value :: tau
+            type(c_ptr), value :: hhqn, hhqp, flux_x, flux_y, ffp, ffn, stream
+        end function
+        integer(c_int) function ocn_tracer_next_step(b, time_smooth, lu, ffn, ffp, ff, stream) &
+                                                     bind(C, name='ocn_tracer_next_step')
+            import :: c_int, c_double, c_ptr, ocn_block
+            type(ocn_block), intent(in) :: b
+            real(c_double), value :: time_smooth
+            type(c_ptr), value :: lu, ffn, ffp, ff, stream
+        end function
+        integer(c_int) function ocn_ctx_tracer_stage(ctx, stage, tracer, tau) bind(C, name='ocn_ctx_tracer_stage')
+            import :: c_int, c_double, c_ptr
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: stage, tracer
+            real(c_double), value :: tau
         end function
     end interface
 

@@ -5,7 +5,7 @@
 !     ocn_sw_driver NSTEPS DUMPFILE [native]
 ! Reads the positional .par files (first lexeme per line, readpar semantics), builds the model
 ! (decomposition + init_grid_data + init_ocean_data on the device), runs NSTEPS of
-! expl_shallow_water through the Fortran PSy layer (or, with "native", ocn_ctx_step), and
+! expl_shallow_water + expl_tracer through the Fortran PSy layer (or, with "native", ocn_ctx_step), and
 ! writes every field of every block in the oracle/ref_driver.f90 dump format.
 program ocn_sw_driver
     use iso_c_binding
@@ -13,7 +13,7 @@ program ocn_sw_driver
     use ocn_psy
     implicit none
 
-    integer :: nsteps, step, k, id, u, nx, ny, nlo
+    integer :: nsteps, step, k, id, u, nx, ny, nlo, ntr
     character(len=512) :: arg, dumpfile, maskfile
     character(len=256) :: lines(32)
     type(ocn_basin) :: basin
@@ -43,6 +43,7 @@ program ocn_sw_driver
     call read_par('sw.par', lines, nlo)
     read(lines(1), *) sw%full_free_surface; read(lines(2), *) sw%trans_terms; read(lines(3), *) sw%ksw_lat
     read(lines(4), *) sw%time_smooth; read(lines(5), *) sw%lvisc_2
+    read(lines(6), *) sw%use_tracers; read(lines(7), *) sw%tracer_num
     ! parallel.par (configs/parallel.f90:34-37), _DD_MANUAL_BLOCK_GRID_
     call read_par('parallel.par', lines, nlo)
     read(lines(3), *) dec%bnx; read(lines(4), *) dec%bny
@@ -62,14 +63,17 @@ program ocn_sw_driver
     if (native) then
         call ocn_check(ocn_ctx_step(c, 1.0d0, int(nsteps, c_int32_t), 1_c_int32_t), 'ocn_ctx_step')
     else
-        do step = 1, nsteps
+        do step = 1, nsteps                       ! model.f90:146-160
             call expl_shallow_water(1.0d0)
+            call expl_tracer(1.0d0)
         enddo
     endif
     call ocn_check(ocn_ctx_synchronize(c), 'ocn_ctx_synchronize')
 
     open(newunit=u, file=trim(dumpfile), access='stream', form='unformatted', status='replace')
-    write(u) int(bcount, c_int32_t)
+    ntr = 0
+    if (sw%use_tracers > 0) ntr = sw%tracer_num
+    write(u) int(bcount, c_int32_t), int(ntr, c_int32_t)
     do k = 1, bcount
         call ocn_check(ocn_ctx_block_info(c, int(k - 1, c_int), info), 'block_info')
         write(u) info%bm, info%bn, info%geom%nx_start, info%geom%nx_end, info%geom%ny_start, info%geom%ny_end, &
@@ -80,7 +84,7 @@ program ocn_sw_driver
             call ocn_check(ocn_ctx_download(c, int(k - 1, c_int), int(r4_order(id), c_int), c_loc(a4)), 'download')
             write(u) a4
         enddo
-        do id = OCN_SSH, OCN_FIELD_END - 1
+        do id = OCN_SSH, OCN_FIELD_END - 1 + merge(2 + 3 * ntr, 0, ntr > 0)   ! + flux_x, flux_y, ff1/ff1p/ff1n
             call ocn_check(ocn_ctx_download(c, int(k - 1, c_int), int(id, c_int), c_loc(a8)), 'download')
             write(u) a8
         enddo

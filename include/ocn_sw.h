@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define OCN_ABI_VERSION 1
+#define OCN_ABI_VERSION 2
 
 enum {
     OCN_OK = 0,
@@ -136,6 +136,22 @@ int ocn_hh_init(const ocn_block *b, int32_t full_free_surface,
 int ocn_check_ssh_err(const ocn_block *b, const float *lu, const double *ssh, int32_t *nbad_device,
                       void *stream);
 
+/* kernel/tracer/leapfrog_tracer.f90:13  tran_diff_fluxes_kernel (flux_x on lcu, flux_y on lcv) */
+int ocn_tran_diff_fluxes(const ocn_block *b, const float *lcu, const float *lcv,
+                         const float *dxt, const float *dyt, const float *dxh, const float *dyh,
+                         const double *hhu, const double *hhv, const double *ff, const double *ffp,
+                         const double *uu, const double *vv, const double *mu, double factor_mu,
+                         double *flux_x, double *flux_y, void *stream);
+
+/* leapfrog_tracer.f90:94  tran_diff_tracer_kernel */
+int ocn_tran_diff_tracer(const ocn_block *b, const float *lu, const float *dx, const float *dy, double tau,
+                         const double *hhqn, const double *hhqp, const double *flux_x, const double *flux_y,
+                         const double *ffp, double *ffn, void *stream);
+
+/* leapfrog_tracer.f90:138  tracer_next_step_kernel (writes interior + halo ring) */
+int ocn_tracer_next_step(const ocn_block *b, double time_smooth, const float *lu, const double *ffn,
+                         double *ffp, double *ff, void *stream);
+
 /* ---------------------------------------------------------------- PSy layer: model context */
 
 /* Field ids: storage of ocean_type / grid_type restricted to what the SW step touches. */
@@ -149,9 +165,15 @@ enum {
     OCN_HHQ, OCN_HHQ_P, OCN_HHQ_N, OCN_HHU, OCN_HHU_P, OCN_HHU_N, OCN_HHV, OCN_HHV_P, OCN_HHV_N,
     OCN_HHH, OCN_HHH_P, OCN_HHH_N, OCN_HHQ_REST, OCN_VORT, OCN_STR_T, OCN_STR_S, OCN_MU,
     OCN_RHSX, OCN_RHSY, OCN_RHSX_ADV, OCN_RHSY_ADV, OCN_RHSX_DIF, OCN_RHSY_DIF,
-    OCN_FIELD_END
+    OCN_FIELD_END,
+    /* real(8) tracer storage (core/ocean.f90:38-41), present when ocn_sw_params.use_tracers > 0 */
+    OCN_FLUX_X = OCN_FIELD_END, OCN_FLUX_Y, OCN_TRACER_BASE
 };
 #define OCN_NUM_R8 (OCN_FIELD_END - OCN_SSH)
+/* ff1(k), ff1p(k), ff1n(k) of tracer k = 1..tracer_num */
+#define OCN_FF1(k) (OCN_TRACER_BASE + 3 * ((k) - 1))
+#define OCN_FF1P(k) (OCN_TRACER_BASE + 3 * ((k) - 1) + 1)
+#define OCN_FF1N(k) (OCN_TRACER_BASE + 3 * ((k) - 1) + 2)
 
 /* Stage ids, in the order of expl_shallow_water (shallow_water.f90:36-92). */
 enum {
@@ -159,6 +181,8 @@ enum {
     OCN_STAGE_STRESS_COMPONENTS, OCN_STAGE_UV_DIFF2, OCN_STAGE_SW_UPDATE_UV, OCN_STAGE_SW_NEXT_STEP,
     OCN_STAGE_HH_SHIFT, OCN_STAGE_HH_INIT, OCN_STAGE_CHECK_SSH_ERR, OCN_NUM_STAGES
 };
+/* Tracer stage ids, in the order of expl_tracer (control/tracer.f90:42-58). */
+enum { OCN_TSTAGE_TRAN_DIFF_FLUXES = 0, OCN_TSTAGE_TRAN_DIFF_TRACER, OCN_TSTAGE_TRACER_NEXT_STEP, OCN_NUM_TSTAGES };
 
 /* Basin description (configs/basinpar.f90:53-91, basin.par lines 1-18) */
 typedef struct ocn_basin {
@@ -168,10 +192,11 @@ typedef struct ocn_basin {
     double rotation_on_lon, rotation_on_lat;
 } ocn_basin;
 
-/* SW switches (configs/sw.f90:34-41, sw.par lines 1-5) */
+/* SW switches (configs/sw.f90:34-41, sw.par lines 1-7) */
 typedef struct ocn_sw_params {
     int32_t full_free_surface, trans_terms, ksw_lat;
     double time_smooth, lvisc_2;
+    int32_t use_tracers, tracer_num;
 } ocn_sw_params;
 
 /* Decomposition request (parallel.par + _DD_MANUAL_BLOCK_GRID_, decomposition.f90:856-858) */
@@ -239,7 +264,11 @@ int ocn_ctx_init_state(ocn_ctx *ctx);
 int ocn_ctx_sync(ocn_ctx *ctx, int field_id);
 /* envoke(stage): the stage on every local block, then its sync list (sw_interface.f90). */
 int ocn_ctx_stage(ocn_ctx *ctx, int stage_id, double tau);
-/* expl_shallow_water(tau) x nsteps.  check_every: run check_ssh_err every N steps (0 = never). */
+/* envoke of tracer stage `stage_id` (OCN_TSTAGE_*) for tracer k (1-based, data_id), then its
+ * sync list (interface/tracer/tracer_interface.f90). */
+int ocn_ctx_tracer_stage(ocn_ctx *ctx, int stage_id, int tracer, double tau);
+/* nsteps model steps (model.f90:146-160): expl_shallow_water(tau), then expl_tracer(tau) when
+ * use_tracers > 0.  check_every: run check_ssh_err every N steps (0 = never). */
 int ocn_ctx_step(ocn_ctx *ctx, double tau, int32_t nsteps, int32_t check_every);
 /* Wait for the context's stream; returns OCN_ERR_BLOWUP if a check found |ssh| >= 1e4. */
 int ocn_ctx_synchronize(ocn_ctx *ctx);
@@ -265,8 +294,10 @@ int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5 };
 
-/* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT). */
-enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_NUM_TIMERS };
+/* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
+ * three tracer stages (summed over tracers). */
+enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_TIMER_TRACER,
+       OCN_NUM_TIMERS = OCN_TIMER_TRACER + OCN_NUM_TSTAGES };
 
 /* Per-timer device time (ms, summed) and launch counts since the last call, from the HIP
  * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_TIMERS entries.  Synchronises. */

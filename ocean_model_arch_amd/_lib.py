@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import re
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -23,13 +24,49 @@ R8_NAMES = ["ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp", "vbrtr", "vbrtrn
             "hhq", "hhq_p", "hhq_n", "hhu", "hhu_p", "hhu_n", "hhv", "hhv_p", "hhv_n",
             "hhh", "hhh_p", "hhh_n", "hhq_rest", "vort", "str_t", "str_s", "mu",
             "RHSx", "RHSy", "RHSx_adv", "RHSy_adv", "RHSx_dif", "RHSy_dif"]
-FIELD_ID = {n: i for i, n in enumerate(R4_NAMES)}
+OCN_FIELD_END = 32 + len(R8_NAMES)
+OCN_TRACER_BASE = OCN_FIELD_END + 2        # OCN_FLUX_X, OCN_FLUX_Y, then ff1/ff1p/ff1n per tracer
+MAX_TRACERS = 64
+_TRACER_RE = re.compile(r"^(ff1|ff1p|ff1n)_([0-9]+)$")
+
+
+def tracer_names(tracer_num: int) -> list[str]:
+    """core/ocean.f90:38-41: flux_x, flux_y, then ff1_k, ff1p_k, ff1n_k for k = 1..tracer_num."""
+    return ["flux_x", "flux_y"] + [f"{p}_{k}" for k in range(1, tracer_num + 1) for p in ("ff1", "ff1p", "ff1n")]
+
+
+class _FieldIds(dict):
+    """name -> field id; tracer names (ff1_3, ...) resolve on demand (OCN_FF1(k) etc.)."""
+    def __missing__(self, name):
+        m = _TRACER_RE.match(name)
+        if not m or not 1 <= int(m.group(2)) <= MAX_TRACERS:
+            raise KeyError(name)
+        return OCN_TRACER_BASE + 3 * (int(m.group(2)) - 1) + ("ff1", "ff1p", "ff1n").index(m.group(1))
+
+    def name(self, fid: int) -> str:
+        for k, v in self.items():
+            if v == fid:
+                return k
+        t = fid - OCN_TRACER_BASE
+        if 0 <= t < 3 * MAX_TRACERS:
+            return f"{('ff1', 'ff1p', 'ff1n')[t % 3]}_{t // 3 + 1}"
+        raise KeyError(fid)
+
+
+FIELD_ID = _FieldIds({n: i for i, n in enumerate(R4_NAMES)})
 FIELD_ID.update({n: 32 + i for i, n in enumerate(R8_NAMES)})
+FIELD_ID.update({"flux_x": OCN_FIELD_END, "flux_y": OCN_FIELD_END + 1})
+
+
+def is_r8_name(name: str) -> bool:
+    return name not in R4_NAMES
 
 STAGES = ["sw_update_ssh", "hh_update", "uv_trans_vort", "uv_trans", "stress_components", "uv_diff2",
           "sw_update_uv", "sw_next_step", "hh_shift", "hh_init", "check_ssh_err"]
 STAGE_ID = {n: i for i, n in enumerate(STAGES)}
-TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"]     # OCN_NUM_TIMERS slots
+TSTAGES = ["tran_diff_fluxes", "tran_diff_tracer", "tracer_next_step"]
+TSTAGE_ID = {n: i for i, n in enumerate(TSTAGES)}
+TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES     # OCN_NUM_TIMERS slots
 OPT_GRAPH = 1
 OPT_OVERLAP = 2
 OPT_STAGE_TIMING = 3
@@ -39,10 +76,11 @@ OPT_COMPACT = 5
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",
                   "ocn_stress_components", "ocn_uv_diff2", "ocn_sw_update_uv", "ocn_sw_next_step",
-                  "ocn_hh_shift", "ocn_hh_init", "ocn_check_ssh_err"]
+                  "ocn_hh_shift", "ocn_hh_init", "ocn_check_ssh_err", "ocn_tran_diff_fluxes",
+                  "ocn_tran_diff_tracer", "ocn_tracer_next_step"]
 CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
                "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm",
-               "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
+               "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
                "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version"]
 ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
 
@@ -71,7 +109,8 @@ class OcnBasin(C.Structure):
 
 class OcnSwParams(C.Structure):
     _fields_ = [("full_free_surface", C.c_int32), ("trans_terms", C.c_int32), ("ksw_lat", C.c_int32),
-                ("time_smooth", C.c_double), ("lvisc_2", C.c_double)]
+                ("time_smooth", C.c_double), ("lvisc_2", C.c_double), ("use_tracers", C.c_int32),
+                ("tracer_num", C.c_int32)]
 
 
 class OcnDecomp(C.Structure):

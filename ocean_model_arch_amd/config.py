@@ -56,20 +56,22 @@ class BasinConfig:
 
 @dataclass
 class SWConfig:
-    """configs/sw.f90:34-41 (sw.par lines 1-5); defaults = the shipped sw.par."""
+    """configs/sw.f90:34-41 (sw.par lines 1-7); defaults = the shipped sw.par."""
     full_free_surface: int = 1
     trans_terms: int = 1
     ksw_lat: int = 1
     time_smooth: float = 0.5
     lvisc_2: float = 1.0e3
+    use_tracers: int = 0
+    tracer_num: int = 1
 
     @classmethod
     def from_par(cls, path: str) -> "SWConfig":
         c = _lexemes(path)
-        if int(c[5]) > 0:
-            raise NotImplementedError("use_tracers > 0: tracer stages are not part of this build yet")
+        if len(c) > 7 and c[7].strip().lower() != "none":
+            raise NotImplementedError("ssh_init_file_name other than 'none' is not supported")
         return cls(full_free_surface=int(c[0]), trans_terms=int(c[1]), ksw_lat=int(c[2]),
-                   time_smooth=_real(c[3]), lvisc_2=_real(c[4]))
+                   time_smooth=_real(c[3]), lvisc_2=_real(c[4]), use_tracers=int(c[5]), tracer_num=int(c[6]))
 
 
 @dataclass

@@ -138,7 +138,7 @@ struct LBlock {
     int bm, bn, gid;
     int nbr_rank[8], nbr_k[8], nbr_gid[8];
     void *slab = nullptr;
-    std::array<void *, kNumSlots> ptr{};
+    std::vector<void *> ptr;           // field table, indexed by field_slot(id)
     uint8_t *bits = nullptr;           // compact static fields (sw_stencils.h): mask bytes
     float *rows = nullptr;             // and metric row tables
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
@@ -191,6 +191,14 @@ struct ocn_ctx {
 };
 
 namespace ocn {
+
+// real(8) fields of a context: the SW set, then flux_x, flux_y and ff1/ff1p/ff1n per tracer
+static int num_r8(const ocn_ctx *c)
+{
+    return OCN_NUM_R8 + (c->sw.use_tracers > 0 ? 2 + 3 * c->sw.tracer_num : 0);
+}
+static bool has_r8(const ocn_ctx *c, int id) { return id >= OCN_SSH && id < OCN_SSH + num_r8(c); }
+static bool has_field(const ocn_ctx *c, int id) { return is_r4(id) || has_r8(c, id); }
 
 // ------------------------------------------------------------------ decomposition
 // decomposition.f90:448-482: floor(real(remaining)/real(parts_left)) in default real(4)
@@ -301,13 +309,15 @@ static int allocate(ocn_ctx *c)
         // 256-B aligned: base offset shifted by (nx_start - bnd_x1) = 2 elements.
         const long r8b = ((n * 8 + 16 + 255) / 256) * 256 + 256;
         const long r4b = ((n * 4 + 8 + 255) / 256) * 256 + 256;
-        const size_t total = (size_t)OCN_NUM_R8 * r8b + (size_t)OCN_NUM_R4 * r4b + 256;
+        const int nr8 = num_r8(c);
+        const size_t total = (size_t)nr8 * r8b + (size_t)OCN_NUM_R4 * r4b + 256;
         HIPCHK(hipMalloc(&b.slab, total));
         c->allocs.push_back(b.slab);
         HIPCHK(hipMemsetAsync(b.slab, 0, total, c->stream));
         char *base = (char *)b.slab;
         size_t off = 0;
-        for (int id = OCN_SSH; id < OCN_FIELD_END; ++id) {
+        b.ptr.assign((size_t)(OCN_NUM_R4 + nr8), nullptr);
+        for (int id = OCN_SSH; id < OCN_SSH + nr8; ++id) {
             b.ptr[field_slot(id)] = base + off + 256 - 16;
             off += r8b;
         }
@@ -597,6 +607,13 @@ static int prebuild_plans(ocn_ctx *c)
     HaloPlan *p;
     RC(get_plan(c, c->sync_a, p));
     RC(get_plan(c, c->sync_b, p));
+    if (sw.use_tracers > 0) {
+        RC(get_plan(c, {OCN_FLUX_X, OCN_FLUX_Y}, p));
+        for (int k = 1; k <= sw.tracer_num; ++k) {
+            RC(get_plan(c, {OCN_FF1N(k)}, p));
+            RC(get_plan(c, {OCN_FF1(k)}, p));
+        }
+    }
     for (const std::vector<int> *l : {&kSyncSsh, &kSyncHhUpdate, &kSyncVort, &kSyncUvTrans, &kSyncStress, &kSyncUv,
                                       &kSyncHhInit})
         RC(get_plan(c, *l, p));
@@ -723,6 +740,7 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
     int32_t *nbad = check ? c->d_nbad : nullptr;
     hipStream_t s = c->stream;
     const bool ffs = sw.full_free_surface > 0;
+    const bool full_c2 = last || sw.use_tracers > 0;   // tracers read hh_init's hhq_p every step
     if (!(c->overlap && has_exchange(c))) {
         RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
         for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, s));
@@ -739,7 +757,7 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
         if (ffs) {
             RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
             for (const LBlock &b : c->blocks)
-                RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, last, s));
+                RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, full_c2, s));
             RC(timer_end(c, rec));
             RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
         }
@@ -766,13 +784,40 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
     if (ffs) {
         RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
         for (const LBlock &b : c->blocks)
-            RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, last, s));
+            RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, full_c2, s));
         RC(fork_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
         for (const LBlock &b : c->blocks)
-            RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, last, s));
+            RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, full_c2, s));
         RC(join_sync(c));
         RC(timer_end(c, rec));
     }
+    return OCN_OK;
+}
+
+// ------------------------------------------------------------------ tracers
+// expl_tracer (control/tracer.f90:33-62): for every tracer, envoke of the three tracer stages
+// with the syncs of interface/tracer/tracer_interface.f90 (flux_x, flux_y; ff1n; none).
+static const std::vector<int> kSyncFlux = {OCN_FLUX_X, OCN_FLUX_Y};
+
+static int tracer_stage(ocn_ctx *c, int stage, int k, double tau, bool compact)
+{
+    ocn_ctx::Rec rec;
+    RC(timer_begin(c, OCN_TIMER_TRACER + stage, rec));
+    for (const LBlock &b : c->blocks) {
+        const Compact t{b.bits, b.rows};
+        RC(launch_tracer(&b.g, b.ptr.data(), compact ? &t : nullptr, stage, k, tau, c->sw.time_smooth, c->stream));
+    }
+    RC(timer_end(c, rec));
+    if (stage == OCN_TSTAGE_TRAN_DIFF_FLUXES) RC(run_sync(c, kSyncFlux));
+    if (stage == OCN_TSTAGE_TRAN_DIFF_TRACER) RC(run_sync(c, {OCN_FF1N(k)}));
+    return OCN_OK;
+}
+
+static int expl_tracer(ocn_ctx *c, double tau, bool compact)
+{
+    if (c->sw.use_tracers <= 0) return OCN_OK;
+    for (int k = 1; k <= c->sw.tracer_num; ++k)
+        for (int stage = 0; stage < OCN_NUM_TSTAGES; ++stage) RC(tracer_stage(c, stage, k, tau, compact));
     return OCN_OK;
 }
 
@@ -862,12 +907,12 @@ static void host_grid(const ocn_ctx *c, HostBlock &h)
         }
 }
 
-// vel_ssh.f90:15-38 gaussian_elimination_kernel with sigma = 1, (nx0, ny0) = (nx/2, ny/2)
-static void host_gaussian(const ocn_ctx *c, HostBlock &h, std::vector<double> &ssh)
+// vel_ssh.f90:15-38 gaussian_elimination_kernel, (nx0, ny0) = (nx/2, ny/2); sigma = 1 for ssh,
+// 0.5 for tracers (init_data.f90:48, 83)
+static void host_gaussian(const ocn_ctx *c, HostBlock &h, std::vector<double> &ssh, double sigma = 1.0)
 {
     const ocn_block &g = h.g;
     const int nx0 = c->basin.nx / 2, ny0 = c->basin.ny / 2;
-    const double sigma = 1.0;
     for (int n = g.ny_start; n <= g.ny_end; ++n)
         for (int m = g.nx_start; m <= g.nx_end; ++m)
             if (h.a(OCN_LU, m, n) > 0.5f) {
@@ -880,7 +925,7 @@ static void host_gaussian(const ocn_ctx *c, HostBlock &h, std::vector<double> &s
 
 static int upload_field(ocn_ctx *c, const LBlock &b, int id, const void *host, bool async)
 {
-    const size_t es = is_r8(id) ? 8 : 4;
+    const size_t es = is_r4(id) ? 4 : 8;
     const size_t w = (size_t)(b.g.bnd_x2 - b.g.bnd_x1 + 1), rows = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1);
     if (async)
         HIPCHK(hipMemcpy2DAsync(b.ptr[field_slot(id)], (size_t)b.g.pitch * es, host, w * es, w * es, rows,
@@ -922,6 +967,33 @@ static int init_state(ocn_ctx *c)
             RC(check_launch());
         }
     }
+    if (c->sw.use_tracers > 0) {                              // init_data.f90:80-90
+        for (int k = 1; k <= c->sw.tracer_num; ++k) {
+            for (const LBlock &b : c->blocks) {
+                HostBlock h(b.g);
+                host_grid(c, h);
+                std::vector<double> r8(h.r4[0].size(), 0.0);
+                host_gaussian(c, h, r8, 0.5);
+                RC(upload_field(c, b, OCN_FF1(k), r8.data(), false));
+            }
+            RC(run_sync(c, {OCN_FF1(k)}));
+            for (const LBlock &b : c->blocks) {
+                const size_t bytes = (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1) * 8;
+                HIPCHK(hipMemcpyAsync(b.ptr[field_slot(OCN_FF1N(k))], b.ptr[field_slot(OCN_FF1(k))], bytes,
+                                      hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(hipMemcpyAsync(b.ptr[field_slot(OCN_FF1P(k))], b.ptr[field_slot(OCN_FF1(k))], bytes,
+                                      hipMemcpyDeviceToDevice, c->stream));
+            }
+        }
+        for (const LBlock &b : c->blocks) {
+            const long n = (long)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1);
+            for (int id : {OCN_FLUX_X, OCN_FLUX_Y}) {
+                hipLaunchKernelGGL(k_fill_r8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
+                                   b.f<double>(id), n, 0.0);
+                RC(check_launch());
+            }
+        }
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->initialized = true;
     return OCN_OK;
@@ -957,6 +1029,8 @@ int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_de
     if (basin->nx < 5 || basin->ny < 5) return set_error(OCN_ERR_ARG, "nx, ny must be >= 5");
     if (dec->bnx < 1 || dec->bny < 1 || dec->nranks < 1 || dec->rank < 0 || dec->rank >= dec->nranks)
         return set_error(OCN_ERR_ARG, "bad decomposition request");
+    if (sw->use_tracers > 0 && (sw->tracer_num < 1 || sw->tracer_num > kMaxTracers))
+        return set_error(OCN_ERR_ARG, "tracer_num must be 1.." + std::to_string(kMaxTracers));
     ocn_ctx *c = new ocn_ctx();
     c->basin = *basin; c->sw = *sw; c->dec = *dec;
     c->bnx = dec->bnx; c->bny = dec->bny;
@@ -1012,7 +1086,8 @@ int ocn_halo_schedule(const ocn_basin *basin, const ocn_decomp *dec, const int32
     if (!field_ids || nfields < 1) return set_error(OCN_ERR_ARG, "no fields");
     std::vector<int> fields(field_ids, field_ids + nfields);
     for (int id : fields)
-        if (!is_r8(id)) return set_error(OCN_ERR_ARG, "halo exchange is defined for real(8) fields");
+        if (id < OCN_SSH || id >= OCN_TRACER_BASE + 3 * kMaxTracers)
+            return set_error(OCN_ERR_ARG, "halo exchange is defined for real(8) fields");
     ocn_ctx *c = nullptr;
     RC(host_ctx(basin, dec, mask, c));
     std::vector<PlanEntry> es;
@@ -1064,7 +1139,7 @@ int ocn_ctx_block_info(const ocn_ctx *c, int k, ocn_block_info *out)
 
 void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
 {
-    if (!c || k < 0 || k >= (int)c->blocks.size() || !(is_r4(id) || is_r8(id))) {
+    if (!c || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id)) {
         set_error(OCN_ERR_ARG, "bad block index or field id");
         return nullptr;
     }
@@ -1102,7 +1177,7 @@ int ocn_ctx_init_state(ocn_ctx *c)
 
 int ocn_ctx_sync(ocn_ctx *c, int field_id)
 {
-    if (!c || !is_r8(field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
+    if (!c || !has_r8(c, field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
     HIPCHK(hipSetDevice(c->dec.device));
     return run_sync(c, {field_id});
 }
@@ -1121,9 +1196,11 @@ static void drop_graphs(ocn_ctx *c)
     c->graphs.clear();
 }
 
+// one model step (model.f90:146-160): expl_shallow_water, then expl_tracer
 static int run_step(ocn_ctx *c, double tau, bool check, bool last)
 {
-    return c->fused ? one_step_fused(c, tau, check, last) : one_step(c, tau, check);
+    RC(c->fused ? one_step_fused(c, tau, check, last) : one_step(c, tau, check));
+    return expl_tracer(c, tau, c->fused && c->compact);
 }
 
 // one step as a replayed hipGraph, captured once per (tau, check, last, compact)
@@ -1148,6 +1225,16 @@ static int graph_step(ocn_ctx *c, double tau, bool check, bool last)
     c->graphs.push_back(ocn_ctx::Graph{exec, tau, check, last, c->compact});
     HIPCHK(hipGraphLaunch(exec, c->stream));
     return OCN_OK;
+}
+
+int ocn_ctx_tracer_stage(ocn_ctx *c, int stage_id, int tracer, double tau)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->dec.device));
+    if (c->sw.use_tracers <= 0 || tracer < 1 || tracer > c->sw.tracer_num)
+        return set_error(OCN_ERR_ARG, "no such tracer (use_tracers / tracer_num)");
+    if (stage_id < 0 || stage_id >= OCN_NUM_TSTAGES) return set_error(OCN_ERR_ARG, "bad tracer stage id");
+    return tracer_stage(c, stage_id, tracer, tau, false);
 }
 
 int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
@@ -1197,10 +1284,10 @@ int ocn_ctx_stage_times(ocn_ctx *c, double *ms, int64_t *counts)
 
 int ocn_ctx_download(ocn_ctx *c, int k, int id, void *host)
 {
-    if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !(is_r4(id) || is_r8(id)))
+    if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
         return set_error(OCN_ERR_ARG, "download: bad argument");
     const LBlock &b = c->blocks[k];
-    const size_t es = is_r8(id) ? 8 : 4;
+    const size_t es = is_r4(id) ? 4 : 8;
     const size_t w = (size_t)(b.g.bnd_x2 - b.g.bnd_x1 + 1), rows = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1);
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy2D(host, w * es, b.ptr[field_slot(id)], (size_t)b.g.pitch * es, w * es, rows,
@@ -1210,7 +1297,7 @@ int ocn_ctx_download(ocn_ctx *c, int k, int id, void *host)
 
 int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
 {
-    if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !(is_r4(id) || is_r8(id)))
+    if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
         return set_error(OCN_ERR_ARG, "upload: bad argument");
     HIPCHK(hipStreamSynchronize(c->stream));
     if (is_r4(id)) c->static_dirty = true;

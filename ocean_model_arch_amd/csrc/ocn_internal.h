@@ -24,10 +24,11 @@ namespace ocn {
 
 int set_error(int code, const std::string &msg);
 
-inline bool is_r8(int id) { return id >= OCN_SSH && id < OCN_FIELD_END; }
+inline bool is_r8(int id) { return id >= OCN_SSH && id < OCN_FIELD_END; }   // SW fields (tracers: ctx_has_field)
 inline bool is_r4(int id) { return id >= 0 && id < OCN_NUM_R4; }
 inline int field_slot(int id) { return is_r4(id) ? id : OCN_NUM_R4 + (id - OCN_SSH); }
-constexpr int kNumSlots = OCN_NUM_R4 + OCN_NUM_R8;
+constexpr int kNumSlots = OCN_NUM_R4 + OCN_NUM_R8;   // without tracer fields
+constexpr int kMaxTracers = 64;
 
 // A block's compact static fields (sw_stencils.h): mask bytes (pitch x rows) and metric rows.
 struct Compact {
@@ -47,6 +48,9 @@ int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, int
                     int32_t *nbad, hipStream_t s);
 int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
                     bool full, hipStream_t s);
+// Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
+int launch_tracer(const ocn_block *b, void *const *ptr, const Compact *cp, int stage, int k, double tau, double ts,
+                  hipStream_t s);
 // Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
 // they cannot be used into *flags (device int).
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s);

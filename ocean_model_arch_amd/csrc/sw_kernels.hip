@@ -175,6 +175,32 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, int
     return launch_fused<MkC2>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, full);
 }
 
+// tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block
+int launch_tracer(const ocn_block *b, void *const *ptr, const Compact *cp, int stage, int k, double tau, double ts,
+                  hipStream_t s)
+{
+    RC_K(check_block(b));
+    auto go = [&](const auto &t) -> int {
+        switch (stage) {
+        case OCN_TSTAGE_TRAN_DIFF_FLUXES: {
+            const Range r = range_interior(b);
+            return launch_range(r.m0, r.m1, r.n0, r.n1, make_tran_diff_fluxes(b, t, k), s);
+        }
+        case OCN_TSTAGE_TRAN_DIFF_TRACER: {
+            const Range r = range_interior(b);
+            return launch_range(r.m0, r.m1, r.n0, r.n1, make_tran_diff_tracer(b, t, k, tau), s);
+        }
+        case OCN_TSTAGE_TRACER_NEXT_STEP: {
+            const Range r = range_ring(b);
+            return launch_range(r.m0, r.m1, r.n0, r.n1, make_tracer_next_step(b, t, k, ts), s);
+        }
+        default: return set_error(OCN_ERR_ARG, "bad tracer stage id");
+        }
+    };
+    if (cp) return go(Tab<true>{ptr, cp->bits, cp->rows, block_rows(b)});
+    return go(Tab<false>{ptr});
+}
+
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s)
 {
     RC_K(check_block(b));
@@ -295,6 +321,34 @@ int ocn_hh_init(const ocn_block *b, int32_t full_free_surface, const float *lu, 
              Interp<false>{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh,
              hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn, sh, shp, h_r};
     return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream);
+}
+
+int ocn_tran_diff_fluxes(const ocn_block *b, const float *lcu, const float *lcv, const float *dxt, const float *dyt,
+                         const float *dxh, const float *dyh, const double *hhu, const double *hhv, const double *ff,
+                         const double *ffp, const double *uu, const double *vv, const double *mu, double factor_mu,
+                         double *flux_x, double *flux_y, void *stream)
+{
+    (void)ffp;   // passed and unused by the reference kernel ("Try ff instead of ffp")
+    CHECK(lcu, lcv, dxt, dyt, dxh, dyh, hhu, hhv, ff, uu, vv, mu, flux_x, flux_y);
+    TranDiffFluxes<false> k{geo(b), factor_mu, lcu, lcv, dxt, dyt, dxh, dyh, hhu, hhv, ff, uu, vv, mu, flux_x, flux_y};
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+}
+
+int ocn_tran_diff_tracer(const ocn_block *b, const float *lu, const float *dx, const float *dy, double tau,
+                         const double *hhqn, const double *hhqp, const double *flux_x, const double *flux_y,
+                         const double *ffp, double *ffn, void *stream)
+{
+    CHECK(lu, dx, dy, hhqn, hhqp, flux_x, flux_y, ffp, ffn);
+    TranDiffTracer<false> k{geo(b), tau, lu, dx, dy, hhqn, hhqp, flux_x, flux_y, ffp, ffn};
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+}
+
+int ocn_tracer_next_step(const ocn_block *b, double time_smooth, const float *lu, const double *ffn, double *ffp,
+                         double *ff, void *stream)
+{
+    CHECK(lu, ffn, ffp, ff);
+    TracerNextStep<false> k{geo(b), time_smooth, lu, ffn, ffp, ff};
+    return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream);
 }
 
 int ocn_check_ssh_err(const ocn_block *b, const float *lu, const double *ssh, int32_t *nbad_device, void *stream)

@@ -462,6 +462,60 @@ template <bool C> struct CheckSshErr {
     }
 };
 
+// ================================================================== tracers
+// kernel/tracer/leapfrog_tracer.f90:13-92 tran_diff_fluxes_kernel (interior).  flux_gm = 0.0d0
+// is still added (x + 0.0 turns -0.0 into +0.0, as the reference does).
+template <bool C> struct TranDiffFluxes {
+    Geo I; double factor_mu;
+    Msk<C> lcu, lcv; Met<C> dxt, dyt, dxh, dyh;
+    const double *__restrict__ hhu, *__restrict__ hhv, *__restrict__ ff;
+    const double *__restrict__ uu, *__restrict__ vv, *__restrict__ mu;
+    double *__restrict__ flux_x, *__restrict__ flux_y;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const Pt c = I(m, n), e = I.e(c), nn = I.n(c);
+        const double fc = ld(ff, c), fe = ld(ff, e), fn = ld(ff, nn);
+        const double mc = ld(mu, c);
+        const double mux = (mc + ld(mu, e)) / 2.0 * factor_mu * D(ld(dyh, c)) / D(ld(dxt, c));
+        const double fx = -ld(uu, c) * ld(hhu, c) * D(ld(dyh, c)) * (fc + fe) / 2.0 + mux * ld(hhu, c) * (fe - fc) + 0.0;
+        const double muy = (mc + ld(mu, nn)) / 2.0 * factor_mu * D(ld(dxh, c)) / D(ld(dyt, c));
+        const double fy = -ld(vv, c) * ld(hhv, c) * D(ld(dxh, c)) * (fc + fn) / 2.0 + muy * ld(hhv, c) * (fn - fc) + 0.0;
+        if (ld(lcu, c) > 0.5f) st(flux_x, c, fx);
+        if (ld(lcv, c) > 0.5f) st(flux_y, c, fy);
+    }
+};
+
+// leapfrog_tracer.f90:94-136 tran_diff_tracer_kernel (interior)
+template <bool C> struct TranDiffTracer {
+    Geo I; double tau;
+    Msk<C> lu; Met<C> dx, dy;
+    const double *__restrict__ hhqn, *__restrict__ hhqp, *__restrict__ flux_x, *__restrict__ flux_y;
+    const double *__restrict__ ffp; double *__restrict__ ffn;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const Pt c = I(m, n), w = I.w(c), s = I.s(c);
+        const double bp = ld(hhqn, c) * D(ld(dx, c)) * D(ld(dy, c)) / tau / 2.0;
+        const double bp0 = ld(hhqp, c) * D(ld(dx, c)) * D(ld(dy, c)) / tau / 2.0;
+        const double rhs = ld(flux_x, c) - ld(flux_x, w) + ld(flux_y, c) - ld(flux_y, s);
+        const double eta = bp0 * ld(ffp, c) + rhs;
+        if (ld(lu, c) > 0.5f) st(ffn, c, eta / bp);
+    }
+};
+
+// leapfrog_tracer.f90:138-168 tracer_next_step_kernel (interior + halo ring)
+template <bool C> struct TracerNextStep {
+    Geo I; double ts;
+    Msk<C> lu;
+    const double *__restrict__ ffn; double *__restrict__ ffp, *__restrict__ ff;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const Pt c = I(m, n);
+        const double x = ld(ff, c), xn = ld(ffn, c), xp = ld(ffp, c);
+        const double f = x + ts * (xn - 2.0 * x + xp) / 2.0;
+        if (ld(lu, c) > 0.5f) { st(ffp, c, f); st(ff, c, xn); }
+    }
+};
+
 // ================================================================== fused step groups
 // The step's 10 stages regrouped into 4 launches with the same results, write sets and halo
 // state as the stage-by-stage reference order (shallow_water.f90:36-92):
@@ -741,6 +795,23 @@ template <bool C> HhInit<C> make_hh_init(const ocn_block *b, const Tab<C> &t, in
 template <bool C> CheckSshErr<C> make_check_ssh_err(const ocn_block *b, const Tab<C> &t, int32_t *nbad)
 {
     return CheckSshErr<C>{geo(b), t.m(OCN_LU), t.f(OCN_SSH), (int *)nbad};
+}
+// tracer k (1-based); the PSy layer passes factor_mu = 1.0d0 (tracer_interface.f90:47)
+template <bool C>
+TranDiffFluxes<C> make_tran_diff_fluxes(const ocn_block *b, const Tab<C> &t, int k, double factor_mu = 1.0)
+{
+    return TranDiffFluxes<C>{geo(b), factor_mu, t.m(OCN_LCU), t.m(OCN_LCV), t.g(OCN_DXT), t.g(OCN_DYT), t.g(OCN_DXH),
+                             t.g(OCN_DYH), t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_FF1(k)), t.f(OCN_UBRTR),
+                             t.f(OCN_VBRTR), t.f(OCN_MU), t.f(OCN_FLUX_X), t.f(OCN_FLUX_Y)};
+}
+template <bool C> TranDiffTracer<C> make_tran_diff_tracer(const ocn_block *b, const Tab<C> &t, int k, double tau)
+{
+    return TranDiffTracer<C>{geo(b), tau, t.m(OCN_LU), t.g(OCN_DX), t.g(OCN_DY), t.f(OCN_HHQ_N), t.f(OCN_HHQ_P),
+                             t.f(OCN_FLUX_X), t.f(OCN_FLUX_Y), t.f(OCN_FF1P(k)), t.f(OCN_FF1N(k))};
+}
+template <bool C> TracerNextStep<C> make_tracer_next_step(const ocn_block *b, const Tab<C> &t, int k, double ts)
+{
+    return TracerNextStep<C>{geo(b), ts, t.m(OCN_LU), t.f(OCN_FF1N(k)), t.f(OCN_FF1P(k)), t.f(OCN_FF1(k))};
 }
 template <bool C> FusedA<C> make_fused_a(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau)
 {

@@ -12,7 +12,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import FIELD_ID, R8_NAMES, STAGE_ID, check, lib
+from ._lib import FIELD_ID, R4_NAMES, R8_NAMES, STAGE_ID, TSTAGE_ID, check, is_r8_name, lib, tracer_names
 from .config import BasinConfig, ParallelConfig, SWConfig
 
 
@@ -63,7 +63,10 @@ class OceanModel:
         self.rank, self.nranks, self.device = rank, nranks, device
         cb = _lib.OcnBasin(basin.nx, basin.ny, basin.dxst, basin.dyst, basin.rlon, basin.rlat, basin.curve_grid,
                            basin.rotation_on_lon, basin.rotation_on_lat)
-        cs = _lib.OcnSwParams(sw.full_free_surface, sw.trans_terms, sw.ksw_lat, sw.time_smooth, sw.lvisc_2)
+        cs = _lib.OcnSwParams(sw.full_free_surface, sw.trans_terms, sw.ksw_lat, sw.time_smooth, sw.lvisc_2,
+                              sw.use_tracers, sw.tracer_num)
+        # ocean_type / grid_type fields this model holds (core/ocean.f90, core/grid.f90)
+        self.field_names = R4_NAMES + R8_NAMES + (tracer_names(sw.tracer_num) if sw.use_tracers > 0 else [])
         cd = _lib.OcnDecomp(par.bppnx, par.bppny, nranks, rank, device)
         self._mask = None
         mptr = None
@@ -154,6 +157,10 @@ class OceanModel:
     def stage(self, name: str, tau: float = 1.0):
         check(lib().ocn_ctx_stage(self.ctx, STAGE_ID[name], tau), f"ocn_ctx_stage({name})")
 
+    def tracer_stage(self, name: str, tracer: int, tau: float = 1.0):
+        """envoke of one tracer stage for tracer `tracer` (1-based data_id), with its sync."""
+        check(lib().ocn_ctx_tracer_stage(self.ctx, TSTAGE_ID[name], tracer, tau), f"ocn_ctx_tracer_stage({name})")
+
     def sync(self, field: str):
         check(lib().ocn_ctx_sync(self.ctx, FIELD_ID[field]), f"ocn_ctx_sync({field})")
 
@@ -174,21 +181,21 @@ class OceanModel:
 
     def download(self, k: int, name: str) -> np.ndarray:
         b = self.blocks[k]
-        dt = np.float64 if name in R8_NAMES else np.float32
+        dt = np.float64 if is_r8_name(name) else np.float32
         a = np.zeros(b.shape, dtype=dt, order="F")
         check(lib().ocn_ctx_download(self.ctx, k, FIELD_ID[name], a.ctypes.data_as(C.c_void_p)), "download")
         return a
 
     def upload(self, k: int, name: str, a: np.ndarray):
         b = self.blocks[k]
-        dt = np.float64 if name in R8_NAMES else np.float32
+        dt = np.float64 if is_r8_name(name) else np.float32
         a = np.asfortranarray(a, dtype=dt)
         if a.shape != b.shape:
             raise ValueError(f"{name}: shape {a.shape} != block shape {b.shape}")
         check(lib().ocn_ctx_upload(self.ctx, k, FIELD_ID[name], a.ctypes.data_as(C.c_void_p)), "upload")
 
     def state(self, names=None) -> list[dict[str, np.ndarray]]:
-        names = names or list(FIELD_ID)
+        names = names or self.field_names
         return [{n: self.download(b.k, n) for n in names} for b in self.blocks]
 
     @property

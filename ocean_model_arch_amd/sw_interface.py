@@ -67,7 +67,7 @@ class ShallowWaterInterface:
         self._fn = {st: getattr(L, sym) for st, (sym, _, _) in KERNEL_ARGS.items()}
         self._cblocks = [b.c_block() for b in model.blocks]
         # device pointers resolved once per block (storage never moves)
-        self._ptrs = [{nm: C.c_void_p(model.field_ptr(b.k, nm)) for nm in model_fields()} for b in model.blocks]
+        self._ptrs = [{nm: C.c_void_p(model.field_ptr(b.k, nm)) for nm in model.field_names} for b in model.blocks]
         for st in KERNEL_ARGS:
             setattr(self, f"envoke_{st}_kernel", self._make_kernel(st))
             setattr(self, f"envoke_{st}_sync", self._make_sync(st))
@@ -100,7 +100,3 @@ class ShallowWaterInterface:
         sync.__name__ = f"envoke_{stage}_sync"
         return sync
 
-
-def model_fields():
-    from ._lib import FIELD_ID
-    return list(FIELD_ID)

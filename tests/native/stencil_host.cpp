@@ -104,6 +104,26 @@ extern "C" int hst_split_ok(int m0, int m1, int n0, int n1, int i0, int i1, int 
     return 1;
 }
 
+// Tracer stage (OCN_TSTAGE_*) of tracer k: ptr must hold the tracer slots (flux_x, flux_y,
+// ff1/ff1p/ff1n per tracer) after the SW ones.
+extern "C" long hst_tracer(int stage, const ocn_block *b, void *const *ptr, const uint8_t *bits, const float *rows,
+                           int k, double tau, double ts, double factor_mu)
+{
+    g_oob = 0;
+    ocn_host_limit = (unsigned)(b->pitch * (int64_t)(b->bnd_y2 - b->bnd_y1 + 1));
+    auto go = [&](const auto &t) {
+        switch (stage) {
+        case OCN_TSTAGE_TRAN_DIFF_FLUXES: run(range_interior(b), make_tran_diff_fluxes(b, t, k, factor_mu)); break;
+        case OCN_TSTAGE_TRAN_DIFF_TRACER: run(range_interior(b), make_tran_diff_tracer(b, t, k, tau)); break;
+        case OCN_TSTAGE_TRACER_NEXT_STEP: run(range_ring(b), make_tracer_next_step(b, t, k, ts)); break;
+        default: g_oob = -1;
+        }
+    };
+    if (bits) go(Tab<true>{ptr, bits, rows, block_rows(b)});
+    else go(Tab<false>{ptr});
+    return g_oob;
+}
+
 // The compact tables of a block (Prepare, thread grid = bnd range); returns the OCN_COMPACT_* flags.
 extern "C" int hst_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows)
 {

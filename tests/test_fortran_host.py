@@ -54,7 +54,8 @@ def write_case(d, case):
     s = case["sw"]
     open(os.path.join(d, "sw.par"), "w").write(
         f"{s['full_free_surface']} : ffs\n{s['trans_terms']} : trans\n{s['ksw_lat']} : ksw\n"
-        f"{s['time_smooth']!r} : ts\n1000.0 : lvisc\n0 : tracers\n1 : n\nnone : ssh\n")
+        f"{s['time_smooth']!r} : ts\n1000.0 : lvisc\n{s.get('use_tracers', 0)} : tracers\n"
+        f"{s.get('tracer_num', 1)} : n\nnone : ssh\n")
     bx, by = case["bxy"]
     open(os.path.join(d, "parallel.par"), "w").write(f"0 : m\nnone : f\n{bx} : bx\n{by} : by\n0\n0\nnone\n0\n0\n")
 
@@ -67,7 +68,8 @@ def test_fortran_host_builds():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,mode", [("box70x54_b3x2_s20", "psy"), ("bs_b4x2_s60", "psy"),
-                                       ("box48x40_flags000_s10", "native"), ("bs_b1x1_s60", "native")])
+                                       ("box48x40_flags000_s10", "native"), ("bs_b1x1_s60", "native"),
+                                       ("box40x32_tr2_s5", "psy"), ("bs_b4x2_tr_s60", "native")])
 def test_fortran_host_matches_reference(tmp_path, name, mode):
     case = cases.load_e2e(name)
     write_case(str(tmp_path), case)

@@ -52,7 +52,7 @@ def test_kernels_match_reference(amd, geom):
     from ocean_model_arch_amd.sw_interface import ShallowWaterInterface
     z = cases.load_kernels(geom)
     m = model_for_geom(amd, z)
-    inputs = {k[3:]: z[k] for k in z.files if k.startswith("in/")}
+    inputs = {k[3:]: z[k] for k in z.files if k.startswith("in/") and k[3:] in m.field_names}
     iface = ShallowWaterInterface(m)
     p = KernelParameters(tau=float(z["tau"]), time_smooth=float(z["time_smooth"]))
     assert int(z["full_free_surface"]) == m.sw.full_free_surface
@@ -65,6 +65,47 @@ def test_kernels_match_reference(amd, geom):
         outs = [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]
         for nm in outs:
             if not bits_equal(m.download(0, nm), z[f"{kname}/{nm}"]):
+                failures.append(f"{kname}:{nm}")
+    m.close()
+    assert not failures, f"{geom}: differs from the reference: {failures}"
+
+
+TRACER_IN = {"ff1": "ff1_1", "ff1p": "ff1p_1", "ff1n": "ff1n_1", "flux_x": "flux_x", "flux_y": "flux_y"}
+
+
+@pytest.mark.parametrize("geom", cases.KERNEL_GEOMS)
+def test_tracer_kernels_match_reference(amd, geom):
+    """ocn_tran_diff_fluxes / ocn_tran_diff_tracer / ocn_tracer_next_step (kernel layer, called
+    through the C ABI with the fixture's scalars, factor_mu = 0.7) on the reference's outputs."""
+    import ctypes as C
+    z = cases.load_kernels(geom)
+    nxs, nxe, nys, nye, bx1, bx2, by1, by2 = (int(v) for v in z["geom"])
+    m = amd.OceanModel(amd.BasinConfig(nx=bx2, ny=by2), amd.SWConfig(use_tracers=1, tracer_num=1))
+    L = amd.lib()
+    blk = m.blocks[0].c_block()
+    inputs = {TRACER_IN.get(k[3:], k[3:]): z[k] for k in z.files if k.startswith("in/")}
+    P = lambda nm: C.c_void_p(m.field_ptr(0, nm))      # noqa: E731
+    calls = {
+        "tran_diff_fluxes": lambda: L.ocn_tran_diff_fluxes(
+            C.byref(blk), *[P(n) for n in ("lcu", "lcv", "dxt", "dyt", "dxh", "dyh", "hhu", "hhv", "ff1_1", "ff1p_1",
+                                           "ubrtr", "vbrtr", "mu")], C.c_double(float(z["factor_mu"])),
+            P("flux_x"), P("flux_y"), C.c_void_p(m.stream)),
+        "tran_diff_tracer": lambda: L.ocn_tran_diff_tracer(
+            C.byref(blk), P("lu"), P("dx"), P("dy"), C.c_double(float(z["tau"])),
+            *[P(n) for n in ("hhq_n", "hhq_p", "flux_x", "flux_y", "ff1p_1", "ff1n_1")], C.c_void_p(m.stream)),
+        "tracer_next_step": lambda: L.ocn_tracer_next_step(
+            C.byref(blk), C.c_double(float(z["time_smooth"])), P("lu"), P("ff1n_1"), P("ff1p_1"), P("ff1_1"),
+            C.c_void_p(m.stream)),
+    }
+    failures = []
+    for kname in cases.TRACER_KERNEL_NAMES:
+        for nm, a in inputs.items():
+            m.upload(0, nm, a)
+        assert calls[kname]() == 0, kname
+        m.synchronize()
+        for key in [k for k in z.files if k.startswith(kname + "/")]:
+            nm = key.split("/", 1)[1]
+            if not bits_equal(m.download(0, TRACER_IN.get(nm, nm)), z[key]):
                 failures.append(f"{kname}:{nm}")
     m.close()
     assert not failures, f"{geom}: differs from the reference: {failures}"
@@ -103,7 +144,7 @@ def compare_case(m, case, name):
 
 
 @pytest.mark.parametrize("mode", ["compact", "fused", "stages", "serial"])
-@pytest.mark.parametrize("name", cases.E2E_CASES)
+@pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the 4-launch step reading the compact static fields, halo exchanges overlapped
     with inner launches when there are several blocks (the default); fused = the same on the 2-D
@@ -190,6 +231,25 @@ def test_psykal_host_path_matches_reference(amd):
         expl_shallow_water(m, 1.0, iface)
     m.synchronize()
     bad = compare_case(m, case, "psykal")
+    m.close()
+    assert not bad, bad
+
+
+def test_psykal_tracer_path_matches_reference(amd):
+    """expl_shallow_water + expl_tracer through the Python PSy layers (tracer_interface mirror)."""
+    from ocean_model_arch_amd.shallow_water import expl_shallow_water
+    from ocean_model_arch_amd.sw_interface import ShallowWaterInterface
+    from ocean_model_arch_amd.tracer import expl_tracer
+    from ocean_model_arch_amd.tracer_interface import TracerInterface
+    case = cases.load_e2e("box70x54_b3x2_tr_s20")
+    m = build_model(amd, case)
+    m.init()
+    iface, tiface = ShallowWaterInterface(m), TracerInterface(m)
+    for _ in range(case["steps"]):
+        expl_shallow_water(m, 1.0, iface)
+        expl_tracer(m, 1.0, tiface)
+    m.synchronize()
+    bad = compare_case(m, case, "psykal tracers")
     m.close()
     assert not bad, bad
 

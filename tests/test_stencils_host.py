@@ -49,14 +49,23 @@ def hst():
     L.hst_stage.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(SwParams),
                             C.c_double, C.POINTER(C.c_int32), C.c_int, C.c_int]
     L.hst_split_ok.argtypes = [C.c_int] * 8
+    L.hst_tracer.restype = C.c_long
+    L.hst_tracer.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_double,
+                             C.c_double, C.c_double]
     L.hst_prepare.restype = C.c_int
     L.hst_prepare.argtypes = [C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p]
     return L
 
 
-def table(arrs):
-    t = (C.c_void_p * (len(R4) + len(R8)))()
-    for i, n in enumerate(R4 + R8):
+def table(arrs, ntr=0, kernel_names=False):
+    """Field table indexed like ocn_field_slot: the SW fields, then (tracers) flux_x, flux_y and
+    ff1/ff1p/ff1n per tracer (named ff1, ff1p, ff1n in the kernel fixtures)."""
+    names = R4 + R8
+    if ntr:
+        names = names + ["flux_x", "flux_y"] + (["ff1", "ff1p", "ff1n"] if kernel_names else
+                                                [f"{p}_{k}" for k in range(1, ntr + 1) for p in ("ff1", "ff1p", "ff1n")])
+    t = (C.c_void_p * len(names))()
+    for i, n in enumerate(names):
         t[i] = arrs[n].ctypes.data
     return t
 
@@ -68,6 +77,22 @@ def blk(g):
 
 def bits_equal(a, b):
     return np.ascontiguousarray(a.ravel(order="F")).tobytes() == np.ascontiguousarray(b.ravel(order="F")).tobytes()
+
+
+@pytest.mark.parametrize("geom", cases.KERNEL_GEOMS)
+def test_tracer_functors_match_reference(hst, geom):
+    z = cases.load_kernels(geom)
+    b = blk(z["geom"])
+    bad = []
+    for st, kname in enumerate(cases.TRACER_KERNEL_NAMES):
+        arrs = {k[3:]: z[k].copy(order="F") for k in z.files if k.startswith("in/")}
+        oob = hst.hst_tracer(st, C.byref(b), table(arrs, 1, True), None, None, 1, float(z["tau"]),
+                             float(z["time_smooth"]), float(z["factor_mu"]))
+        assert oob == 0, f"{kname}: {oob} out-of-bounds accesses"
+        for nm in [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]:
+            if not bits_equal(arrs[nm], z[f"{kname}/{nm}"]):
+                bad.append(f"{kname}:{nm}")
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("geom", cases.KERNEL_GEOMS)
@@ -112,8 +137,20 @@ def compact_tables(hst, om):
 def host_step(hst, om, mode, nbad, last=True, tabs=None):
     sw_o = om.sw
     sw = SwParams(sw_o.full_free_surface, sw_o.trans_terms, sw_o.ksw_lat, sw_o.time_smooth, sw_o.lvisc_2)
-    blocks = [(Block(*b.args, b.bx2 - b.bx1 + 1), table(om.f[k])) for k, b in enumerate(om.blocks)]
+    ntr = sw_o.tracer_num if sw_o.use_tracers > 0 else 0
+    blocks = [(Block(*b.args, b.bx2 - b.bx1 + 1), table(om.f[k], ntr)) for k, b in enumerate(om.blocks)]
     compact = mode in ("compact", "overlap_early", "overlap_late")
+
+    def tracers():
+        """expl_tracer (control/tracer.f90:33-62) after the SW step."""
+        for t in range(1, ntr + 1):
+            for st, sync in ((0, ["flux_x", "flux_y"]), (1, [f"ff1n_{t}"]), (2, [])):
+                for k, (b, tb) in enumerate(blocks):
+                    bits, rows = (tabs[k][0].ctypes.data, tabs[k][1].ctypes.data) if compact else (None, None)
+                    oob = hst.hst_tracer(st, C.byref(b), tb, bits, rows, t, 1.0, sw_o.time_smooth, 1.0)
+                    assert oob == 0, f"tracer stage {st}: {oob} out-of-bounds accesses"
+                for f in sync:
+                    om.sync(f)
 
     def each(stage, tau=1.0, full=1, part=0):
         for k, (b, t) in enumerate(blocks):
@@ -144,10 +181,11 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None):
         if not early: syncs(sb)
         each(FUSED_C1, part=FR)
         if sw.full_free_surface > 0:
-            each(STAGE_IDS["hh_init"], full=int(last), part=FR)
+            each(STAGE_IDS["hh_init"], full=int(last or ntr > 0), part=FR)
             if early: syncs(["hhu", "hhv", "hhh"])
-            each(STAGE_IDS["hh_init"], full=int(last), part=IN)
+            each(STAGE_IDS["hh_init"], full=int(last or ntr > 0), part=IN)
             if not early: syncs(["hhu", "hhv", "hhh"])
+        tracers()
         return
     if mode != "stages":
         each(FUSED_A)
@@ -160,7 +198,7 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None):
             om.sync(f)
         each(FUSED_C1)
         if sw.full_free_surface > 0:
-            each(STAGE_IDS["hh_init"], full=int(last))
+            each(STAGE_IDS["hh_init"], full=int(last or ntr > 0))      # tracers read hhq_p every step
             for f in ("hhu", "hhv", "hhh"):
                 om.sync(f)
     else:
@@ -176,10 +214,11 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None):
             for f in syncs.get(st, []):
                 om.sync(f)
         each(CHECK)
+    tracers()
 
 
 @pytest.mark.parametrize("mode", ["compact", "fused", "stages", "overlap_early", "overlap_late"])
-@pytest.mark.parametrize("name", cases.E2E_CASES)
+@pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
 def test_host_step_matches_reference(hst, name, mode):
     """The whole run as one ocn_ctx_step call: hh_init's time-invariant stores are skipped on
     every step but the last (fused modes); "compact" reads masks / metrics from the compact
