@@ -171,7 +171,7 @@ struct ocn_ctx {
     std::map<std::vector<int>, HaloPlan> plans;
     bool initialized = false;
     bool use_graph = false;
-    struct Graph { hipGraphExec_t exec; double tau; bool check, last, compact; };
+    struct Graph { hipGraphExec_t exec; double tau; bool check, first, last, compact; };
     std::vector<Graph> graphs;         // one captured step per (tau, check, last step, compact)
     std::vector<void *> allocs;
     // per-stage HIP-event timing (OCN_OPT_STAGE_TIMING): pending (stage, start, stop) records
@@ -182,7 +182,7 @@ struct ocn_ctx {
     double stage_ms[OCN_NUM_TIMERS] = {0};
     int64_t stage_n[OCN_NUM_TIMERS] = {0};
     bool fused = true;
-    std::vector<int> sync_a, sync_b;
+    std::vector<int> sync_a, sync_a_reuse, sync_b;
     // compact static fields: requested (OCN_OPT_COMPACT), in use, stale (real(4) fields
     // changed since they were built), or unusable because raw real(4) pointers were handed out
     bool compact_req = true, compact = false, static_dirty = true;
@@ -601,11 +601,15 @@ static int prebuild_plans(ocn_ctx *c)
     if (sw.full_free_surface > 0) c->sync_a.insert(c->sync_a.end(), {OCN_HHU_N, OCN_HHV_N, OCN_HHH_N});
     if (sw.trans_terms > 0) c->sync_a.push_back(OCN_VORT);
     if (sw.ksw_lat > 0) c->sync_a.insert(c->sync_a.end(), {OCN_STR_T, OCN_STR_S});
+    c->sync_a_reuse.clear();
+    for (int id : c->sync_a)
+        if (id != OCN_HHU_N && id != OCN_HHV_N && id != OCN_HHH_N) c->sync_a_reuse.push_back(id);
     c->sync_b = {};
     if (sw.trans_terms > 0) c->sync_b = {OCN_HHU_P, OCN_HHV_P, OCN_HHH_P};
     c->sync_b.insert(c->sync_b.end(), {OCN_VBRTRN, OCN_UBRTRN});
     HaloPlan *p;
     RC(get_plan(c, c->sync_a, p));
+    RC(get_plan(c, c->sync_a_reuse, p));
     RC(get_plan(c, c->sync_b, p));
     if (sw.use_tracers > 0) {
         RC(get_plan(c, {OCN_FLUX_X, OCN_FLUX_Y}, p));
@@ -728,7 +732,7 @@ static int join_sync(ocn_ctx *c)
     return OCN_OK;
 }
 
-static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
+static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool last)
 {
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
@@ -741,14 +745,19 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
     hipStream_t s = c->stream;
     const bool ffs = sw.full_free_surface > 0;
     const bool full_c2 = last || sw.use_tracers > 0;   // tracers read hh_init's hhq_p every step
+    // sw_stencils.h "reuse" steps: hun/hvn/hhn are hh_init's hu/hv/hh of the previous step.  Not
+    // on the first step of a call (the host may have changed ssh since) nor on the last one.
+    const bool reuse = sw.full_free_surface == 1 && !first && !last;
+    const std::vector<int> &sync_a = reuse ? c->sync_a_reuse : c->sync_a;
     if (!(c->overlap && has_exchange(c))) {
         RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-        for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, s));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, reuse, s));
         RC(timer_end(c, rec));
-        RC(run_sync(c, c->sync_a));
+        RC(run_sync(c, sync_a));
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
         for (const LBlock &b : c->blocks)
-            RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, last, s));
+            RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, last, reuse, s));
         RC(timer_end(c, rec));
         RC(run_sync(c, c->sync_b));
         RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
@@ -764,16 +773,18 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool last)
         return OCN_OK;
     }
     RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-    for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, tau, s));
-    RC(fork_sync(c, c->sync_a));
-    for (const LBlock &b : c->blocks) RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, tau, s));
+    for (const LBlock &b : c->blocks)
+        RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, tau, reuse, s));
+    RC(fork_sync(c, sync_a));
+    for (const LBlock &b : c->blocks)
+        RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, tau, reuse, s));
     RC(timer_end(c, rec));
     RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
     for (const LBlock &b : c->blocks)
-        RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, tau, last, s));
+        RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, tau, last, reuse, s));
     RC(join_sync(c));
     for (const LBlock &b : c->blocks)
-        RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, tau, last, s));
+        RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, tau, last, reuse, s));
     RC(fork_sync(c, c->sync_b));
     RC(timer_end(c, rec));
     RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
@@ -1197,24 +1208,24 @@ static void drop_graphs(ocn_ctx *c)
 }
 
 // one model step (model.f90:146-160): expl_shallow_water, then expl_tracer
-static int run_step(ocn_ctx *c, double tau, bool check, bool last)
+static int run_step(ocn_ctx *c, double tau, bool check, bool first, bool last)
 {
-    RC(c->fused ? one_step_fused(c, tau, check, last) : one_step(c, tau, check));
+    RC(c->fused ? one_step_fused(c, tau, check, first, last) : one_step(c, tau, check));
     return expl_tracer(c, tau, c->fused && c->compact);
 }
 
-// one step as a replayed hipGraph, captured once per (tau, check, last, compact)
-static int graph_step(ocn_ctx *c, double tau, bool check, bool last)
+// one step as a replayed hipGraph, captured once per (tau, check, first, last, compact)
+static int graph_step(ocn_ctx *c, double tau, bool check, bool first, bool last)
 {
     for (const auto &g : c->graphs)
-        if (g.tau == tau && g.check == check && g.last == last && g.compact == c->compact) {
+        if (g.tau == tau && g.check == check && g.first == first && g.last == last && g.compact == c->compact) {
             HIPCHK(hipGraphLaunch(g.exec, c->stream));
             return OCN_OK;
         }
     if (c->graphs.size() >= 8) drop_graphs(c);
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = run_step(c, tau, check, last);
+    int rc = run_step(c, tau, check, first, last);
     hipError_t e = hipStreamEndCapture(c->stream, &graph);
     if (rc) return rc;
     HIPCHK(e);
@@ -1222,7 +1233,7 @@ static int graph_step(ocn_ctx *c, double tau, bool check, bool last)
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     HIPCHK(e);
-    c->graphs.push_back(ocn_ctx::Graph{exec, tau, check, last, c->compact});
+    c->graphs.push_back(ocn_ctx::Graph{exec, tau, check, first, last, c->compact});
     HIPCHK(hipGraphLaunch(exec, c->stream));
     return OCN_OK;
 }
@@ -1246,9 +1257,9 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
     const bool graph_ok = c->use_graph && !c->comm && !c->stage_timing;   // RCCL / events stay outside graphs
     for (int s = 1; s <= nsteps; ++s) {
         const bool check = check_every > 0 && (s % check_every == 0);
-        const bool last = s == nsteps;
-        if (graph_ok) RC(graph_step(c, tau, check, last));
-        else RC(run_step(c, tau, check, last));
+        const bool first = s == 1, last = s == nsteps;
+        if (graph_ok) RC(graph_step(c, tau, check, first, last));
+        else RC(run_step(c, tau, check, first, last));
     }
     return OCN_OK;
 }

@@ -7,10 +7,19 @@
 
 #include "../../include/ocn_sw.h"
 
-// Rows of a block strip owned by one 64x4 workgroup (see sw_kernels.hip).
+// Stencil tile of one 256-thread workgroup (sw_kernels.hip k_range): OCN_TW columns (a
+// multiple of 64) x OCN_ROWS rows; OCN_XCD_REMAP = XCD-banded tile order.
+#ifndef OCN_TW
+#define OCN_TW 64
+#endif
 #ifndef OCN_ROWS
 #define OCN_ROWS 8
 #endif
+#ifndef OCN_XCD_REMAP
+#define OCN_XCD_REMAP 0
+#endif
+#define OCN_WY (256 / OCN_TW)
+static_assert(OCN_TW % 64 == 0 && 256 % OCN_TW == 0, "OCN_TW must be 64, 128 or 256");
 
 // Minimum waves per SIMD requested from the register allocator for the stencil kernels.
 #ifndef OCN_LB_WAVES
@@ -41,9 +50,9 @@ struct Compact {
 // launch range (sw_stencils.h frame_rects: the halo-overlap split).
 enum { OCN_PART_ALL = 0, OCN_PART_FRAME = 1, OCN_PART_INNER = 2 };
 int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                   double tau, hipStream_t s);
+                   double tau, bool reuse, hipStream_t s);
 int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                   double tau, bool full, hipStream_t s);
+                   double tau, bool full, bool reuse, hipStream_t s);
 int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
                     int32_t *nbad, hipStream_t s);
 int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,

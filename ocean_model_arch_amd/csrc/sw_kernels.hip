@@ -27,25 +27,41 @@
 namespace ocn {
 
 // ------------------------------------------------------------------ launch scaffolding
+// A workgroup owns a tile of OCN_TW columns x OCN_ROWS rows: OCN_TW lanes across (a multiple
+// of the 64-lane wave), OCN_WY = 256 / OCN_TW waves stacked vertically that step through the
+// tile rows together.  Tile t = (t % ntx, t / ntx).  With OCN_XCD_REMAP the linear workgroup
+// id is remapped so that each of the 8 XCDs (workgroups are dealt round-robin, id % 8) works
+// on one contiguous band of tiles: horizontally adjacent tiles then run back to back on the
+// same XCD and their shared +-1 columns / rows are L2 hits instead of refetches.
 template <typename Body>
-__global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range(int m0, int m1, int n0, int n1, Body body)
+__global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range(int m0, int m1, int n0, int n1, int ntx, int ntiles,
+                                                             Body body)
 {
-    const int m = m0 + (int)blockIdx.x * 64 + (int)threadIdx.x;
+    int tile = (int)blockIdx.x;
+#if OCN_XCD_REMAP
+    const int per = (ntiles + 7) / 8;
+    tile = (tile % 8) * per + tile / 8;
+    if (tile >= ntiles) return;
+#endif
+    const int tx = tile % ntx, ty = tile / ntx;
+    const int m = m0 + tx * OCN_TW + (int)threadIdx.x;
     if (m > m1) return;
-    const int nb = n0 + (int)blockIdx.y * OCN_ROWS;
+    const int nb = n0 + ty * OCN_ROWS;
     const int ne = min(n1, nb + OCN_ROWS - 1);
-    // a wave is one 64-lane thread-row: its row index is wave-uniform (scalar registers)
-    const int ty = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
-    for (int n = nb + ty; n <= ne; n += 4) body(m, n);
+    // every wave is one thread-row: its row index is wave-uniform (scalar registers)
+    const int wy = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
+    for (int n = nb + wy; n <= ne; n += OCN_WY) body(m, n);
 }
 
 template <typename Body>
 static int launch_range(int m0, int m1, int n0, int n1, const Body &body, hipStream_t s)
 {
     if (m1 < m0 || n1 < n0) return OCN_OK;
-    dim3 block(64, 4);
-    dim3 grid((unsigned)((m1 - m0 + 64) / 64), (unsigned)((n1 - n0 + OCN_ROWS) / OCN_ROWS));
-    hipLaunchKernelGGL(k_range<Body>, grid, block, 0, s, m0, m1, n0, n1, body);
+    const int ntx = (m1 - m0 + OCN_TW) / OCN_TW, nty = (n1 - n0 + OCN_ROWS) / OCN_ROWS;
+    const int ntiles = ntx * nty;
+    const int nblocks = OCN_XCD_REMAP ? 8 * ((ntiles + 7) / 8) : ntiles;
+    hipLaunchKernelGGL(k_range<Body>, dim3((unsigned)nblocks), dim3(OCN_TW, OCN_WY), 0, s, m0, m1, n0, n1, ntx,
+                       ntiles, body);
     return check_launch();
 }
 
@@ -127,15 +143,15 @@ static int launch_fused(const Range &r, const Range &inner, int part, const ocn_
     return launch_part(r, inner, part, Make<false>::make(b, t, a...), s);
 }
 template <bool C> struct MkA {
-    static FusedA<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau)
+    static FusedA<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau, bool reuse)
     {
-        return make_fused_a(b, t, sw, tau);
+        return make_fused_a(b, t, sw, tau, reuse);
     }
 };
 template <bool C> struct MkB {
-    static FusedB<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau, bool full)
+    static FusedB<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau, bool full, bool reuse)
     {
-        return make_fused_b(b, t, sw, tau, full);
+        return make_fused_b(b, t, sw, tau, full, reuse);
     }
 };
 template <bool C> struct MkC1 {
@@ -152,15 +168,16 @@ template <bool C> struct MkC2 {
 };
 
 int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                   double tau, hipStream_t s)
+                   double tau, bool reuse, hipStream_t s)
 {
-    return launch_fused<MkA>(range_fused_a(b, sw), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, tau);
+    return launch_fused<MkA>(range_fused_a(b, sw, reuse), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, tau,
+                             reuse);
 }
 
 int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                   double tau, bool full, hipStream_t s)
+                   double tau, bool full, bool reuse, hipStream_t s)
 {
-    return launch_fused<MkB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, tau, full);
+    return launch_fused<MkB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, tau, full, reuse);
 }
 
 int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,

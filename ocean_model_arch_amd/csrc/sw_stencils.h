@@ -530,6 +530,12 @@ template <bool C> struct TracerNextStep {
 //   C1 = a8 sw_next_step + a9 hh_shift on the outer ring only (on [start-1,end]^2 its
 //        outputs are dead: hh_init overwrites them) + check_ssh_err.
 //   C2 = a10 hh_init (full = false except on the last step of a call) -> sync hhu/hhv/hhh.
+// "reuse" steps (full_free_surface == 1, neither the first nor the last step of a call): a2's
+// hun/hvn/hhn = interp(h_r + ssh) are bit for bit hh_init's hu/hv/hh = interp(h_r + ssh*1.0)
+// of the previous step (same ssh -- nothing writes it in between -- same masks, same range,
+// same arithmetic), so A skips a2 and B reads hhu/hhv where a7 reads hhu_n/hhv_n.  Their other
+// readers only see them on the halo ring, whose results are overwritten before use (see
+// ocn_ctx.hip one_step_fused); the last step of a call recomputes and stores them.
 // "full" launches (the last step of every ocn_ctx_step call) store everything the reference
 // stores; the others skip stores nobody reads (FusedB, HhInit), so the state after each call
 // is the reference's bit for bit.
@@ -646,9 +652,9 @@ inline Range range_ring(const ocn_block *b)
     return {b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1};
 }
 inline Range range_bnd(const ocn_block *b) { return {b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2}; }
-inline Range range_fused_a(const ocn_block *b, const ocn_sw_params &sw)
+inline Range range_fused_a(const ocn_block *b, const ocn_sw_params &sw, bool reuse = false)
 {
-    const int o = sw.full_free_surface > 0 ? 1 : 0;
+    const int o = sw.full_free_surface > 0 && !reuse ? 1 : 0;
     return {b->nx_start - o, b->nx_end, b->ny_start - o, b->ny_end};
 }
 
@@ -813,17 +819,21 @@ template <bool C> TracerNextStep<C> make_tracer_next_step(const ocn_block *b, co
 {
     return TracerNextStep<C>{geo(b), ts, t.m(OCN_LU), t.f(OCN_FF1N(k)), t.f(OCN_FF1P(k)), t.f(OCN_FF1(k))};
 }
-template <bool C> FusedA<C> make_fused_a(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau)
+template <bool C>
+FusedA<C> make_fused_a(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau, bool reuse = false)
 {
-    return FusedA<C>{b->nx_start, b->ny_start, sw.full_free_surface > 0, sw.trans_terms > 0, sw.ksw_lat > 0,
+    return FusedA<C>{b->nx_start, b->ny_start, sw.full_free_surface > 0 && !reuse, sw.trans_terms > 0, sw.ksw_lat > 0,
                      make_sw_update_ssh(b, t, tau), make_hh_update(b, t), make_uv_trans_vort(b, t),
                      make_stress_components(b, t)};
 }
 template <bool C>
-FusedB<C> make_fused_b(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau, bool full)
+FusedB<C> make_fused_b(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau, bool full,
+                       bool reuse = false)
 {
-    return FusedB<C>{sw.trans_terms > 0, sw.ksw_lat > 0, full, make_uv_trans(b, t), make_uv_diff2(b, t),
-                     make_sw_update_uv(b, t, tau)};
+    FusedB<C> k{sw.trans_terms > 0, sw.ksw_lat > 0, full, make_uv_trans(b, t), make_uv_diff2(b, t),
+                make_sw_update_uv(b, t, tau)};
+    if (reuse) { k.a7.hhun = k.a7.hhu; k.a7.hhvn = k.a7.hhv; }
+    return k;
 }
 template <bool C> FusedC1<C> make_fused_c1(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, int32_t *nbad)
 {

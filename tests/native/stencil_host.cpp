@@ -46,7 +46,7 @@ template <class K> static void run_part(const Range &r, const Range &inner, int 
 }
 
 template <bool C> static void run_stage(int stage, const ocn_block *b, const Tab<C> &t, const ocn_sw_params *sw,
-                                        double tau, int32_t *nbad, bool full, int part)
+                                        double tau, int32_t *nbad, bool full, bool reuse, int part)
 {
     switch (stage) {
     case OCN_STAGE_SW_UPDATE_SSH: run(range_interior(b), make_sw_update_ssh(b, t, tau)); break;
@@ -62,8 +62,12 @@ template <bool C> static void run_stage(int stage, const ocn_block *b, const Tab
         run_part(range_bnd(b), inner_interior_shrunk(b), part, make_hh_init(b, t, sw->full_free_surface, full));
         break;
     case OCN_STAGE_CHECK_SSH_ERR: run(range_interior(b), make_check_ssh_err(b, t, nbad)); break;
-    case 11: run_part(range_fused_a(b, *sw), inner_interior_shrunk(b), part, make_fused_a(b, t, *sw, tau)); break;
-    case 12: run_part(range_interior(b), inner_interior_shrunk(b), part, make_fused_b(b, t, *sw, tau, full)); break;
+    case 11:
+        run_part(range_fused_a(b, *sw, reuse), inner_interior_shrunk(b), part, make_fused_a(b, t, *sw, tau, reuse));
+        break;
+    case 12:
+        run_part(range_interior(b), inner_interior_shrunk(b), part, make_fused_b(b, t, *sw, tau, full, reuse));
+        break;
     case 13: run_part(range_ring(b), range_interior(b), part, make_fused_c1(b, t, *sw, nbad)); break;
     default: g_oob = -1;
     }
@@ -71,15 +75,16 @@ template <bool C> static void run_stage(int stage, const ocn_block *b, const Tab
 
 // stage: 0..9 = OCN_STAGE_* (reference stages), 10 = check_ssh_err, 11/12/13 = fused A/B/C1.
 // bits/rows: the block's compact tables (hst_prepare) or nullptr for the 2-D real(4) arrays;
-// full: FusedB / HhInit `full`; part: the halo-overlap split (fused A/B/C1, hh_init).
-// Returns the number of out-of-bounds accesses detected (0 = clean).
+// flags: bit 0 = FusedB / HhInit `full`, bit 1 = fused A/B "reuse"; part: the halo-overlap
+// split (fused A/B/C1, hh_init).  Returns the number of out-of-bounds accesses (0 = clean).
 extern "C" long hst_stage(int stage, const ocn_block *b, void *const *ptr, const uint8_t *bits, const float *rows,
-                          const ocn_sw_params *sw, double tau, int32_t *nbad, int full, int part)
+                          const ocn_sw_params *sw, double tau, int32_t *nbad, int flags, int part)
 {
     g_oob = 0;
     ocn_host_limit = (unsigned)(b->pitch * (int64_t)(b->bnd_y2 - b->bnd_y1 + 1));
-    if (bits) run_stage(stage, b, Tab<true>{ptr, bits, rows, block_rows(b)}, sw, tau, nbad, full != 0, part);
-    else run_stage(stage, b, Tab<false>{ptr}, sw, tau, nbad, full != 0, part);
+    const bool full = flags & 1, reuse = (flags & 2) != 0;
+    if (bits) run_stage(stage, b, Tab<true>{ptr, bits, rows, block_rows(b)}, sw, tau, nbad, full, reuse, part);
+    else run_stage(stage, b, Tab<false>{ptr}, sw, tau, nbad, full, reuse, part);
     return g_oob;
 }
 

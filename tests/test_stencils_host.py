@@ -134,7 +134,7 @@ def compact_tables(hst, om):
     return out
 
 
-def host_step(hst, om, mode, nbad, last=True, tabs=None):
+def host_step(hst, om, mode, nbad, last=True, tabs=None, first=True):
     sw_o = om.sw
     sw = SwParams(sw_o.full_free_surface, sw_o.trans_terms, sw_o.ksw_lat, sw_o.time_smooth, sw_o.lvisc_2)
     ntr = sw_o.tracer_num if sw_o.use_tracers > 0 else 0
@@ -162,7 +162,11 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None):
         for f in names:
             om.sync(f)
 
-    sa = ["sshn"] + (["hhu_n", "hhv_n", "hhh_n"] if sw.full_free_surface > 0 else []) + \
+    # ocn_ctx.hip one_step_fused: "reuse" steps skip hh_update (hun/hvn/hhn = previous hu/hv/hh)
+    reuse = sw.full_free_surface == 1 and not first and not last
+    fa = 2 * int(reuse)
+    fb = int(last) | 2 * int(reuse)
+    sa = ["sshn"] + (["hhu_n", "hhv_n", "hhh_n"] if sw.full_free_surface > 0 and not reuse else []) + \
          (["vort"] if sw.trans_terms > 0 else []) + (["str_t", "str_s"] if sw.ksw_lat > 0 else [])
     sb = (["hhu_p", "hhv_p", "hhh_p"] if sw.trans_terms > 0 else []) + ["vbrtrn", "ubrtrn"]
     if mode in ("overlap_early", "overlap_late"):
@@ -170,12 +174,12 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None):
         # the inner launches; emulate it completing as early and as late as possible
         early = mode == "overlap_early"
         FR, IN = 1, 2
-        each(FUSED_A, part=FR)
+        each(FUSED_A, full=fa, part=FR)
         if early: syncs(sa)
-        each(FUSED_A, part=IN)
-        each(FUSED_B, full=int(last), part=IN)
+        each(FUSED_A, full=fa, part=IN)
+        each(FUSED_B, full=fb, part=IN)
         if not early: syncs(sa)
-        each(FUSED_B, full=int(last), part=FR)
+        each(FUSED_B, full=fb, part=FR)
         if early: syncs(sb)
         each(FUSED_C1, part=IN)
         if not early: syncs(sb)
@@ -188,12 +192,10 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None):
         tracers()
         return
     if mode != "stages":
-        each(FUSED_A)
-        sa = ["sshn"] + (["hhu_n", "hhv_n", "hhh_n"] if sw.full_free_surface > 0 else []) + \
-             (["vort"] if sw.trans_terms > 0 else []) + (["str_t", "str_s"] if sw.ksw_lat > 0 else [])
+        each(FUSED_A, full=fa)
         for f in sa:
             om.sync(f)
-        each(FUSED_B, full=int(last))
+        each(FUSED_B, full=fb)
         for f in (["hhu_p", "hhv_p", "hhh_p"] if sw.trans_terms > 0 else []) + ["vbrtrn", "ubrtrn"]:
             om.sync(f)
         each(FUSED_C1)
@@ -234,7 +236,7 @@ def test_host_step_matches_reference(hst, name, mode):
         tabs = compact_tables(hst, om)
         assert all(t[2] == 0 for t in tabs), [t[2] for t in tabs]
     for s in range(case["steps"]):
-        host_step(hst, om, mode, nbad, last=s == case["steps"] - 1, tabs=tabs)
+        host_step(hst, om, mode, nbad, last=s == case["steps"] - 1, tabs=tabs, first=s == 0)
     assert nbad.value == 0
     z = case["z"]
     bad = []
@@ -271,7 +273,7 @@ def test_compact_row_window_is_what_the_stencils_read(hst):
     ref.f[0]["dx"][0, :] *= np.float32(3.0)
     nbad = C.c_int32(0)
     for s in range(4):
-        host_step(hst, om, "compact", nbad, last=s == 3, tabs=tabs)
+        host_step(hst, om, "compact", nbad, last=s == 3, tabs=tabs, first=s == 0)
         host_step(hst, ref, "stages", nbad)
     for nm in ref.f[0]:
         assert bits_equal(om.f[0][nm], ref.f[0][nm]), nm
