@@ -732,6 +732,8 @@ static int join_sync(ocn_ctx *c)
     return OCN_OK;
 }
 
+// block b's launch arguments: geometry, field table, compact tables (or nullptr)
+#define FT(b) &(b).g, (b).ptr.data(), (int)(b).ptr.size(), cp(b, t)
 static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool last)
 {
     const ocn_sw_params &sw = c->sw;
@@ -752,21 +754,21 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool l
     if (!(c->overlap && has_exchange(c))) {
         RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
         for (const LBlock &b : c->blocks)
-            RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, reuse, s));
+            RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
         RC(timer_end(c, rec));
         RC(run_sync(c, sync_a));
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
         for (const LBlock &b : c->blocks)
-            RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, tau, last, reuse, s));
+            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, last, reuse, s));
         RC(timer_end(c, rec));
         RC(run_sync(c, c->sync_b));
         RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
-        for (const LBlock &b : c->blocks) RC(launch_fused_c1(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, nbad, s));
+        for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_ALL, sw, nbad, s));
         RC(timer_end(c, rec));
         if (ffs) {
             RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
             for (const LBlock &b : c->blocks)
-                RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_ALL, sw, full_c2, s));
+                RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, full_c2, s));
             RC(timer_end(c, rec));
             RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
         }
@@ -774,36 +776,37 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool l
     }
     RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
     for (const LBlock &b : c->blocks)
-        RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, tau, reuse, s));
+        RC(launch_fused_a(FT(b), OCN_PART_FRAME, sw, tau, reuse, s));
     RC(fork_sync(c, sync_a));
     for (const LBlock &b : c->blocks)
-        RC(launch_fused_a(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, tau, reuse, s));
+        RC(launch_fused_a(FT(b), OCN_PART_INNER, sw, tau, reuse, s));
     RC(timer_end(c, rec));
     RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
     for (const LBlock &b : c->blocks)
-        RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, tau, last, reuse, s));
+        RC(launch_fused_b(FT(b), OCN_PART_INNER, sw, tau, last, reuse, s));
     RC(join_sync(c));
     for (const LBlock &b : c->blocks)
-        RC(launch_fused_b(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, tau, last, reuse, s));
+        RC(launch_fused_b(FT(b), OCN_PART_FRAME, sw, tau, last, reuse, s));
     RC(fork_sync(c, c->sync_b));
     RC(timer_end(c, rec));
     RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
-    for (const LBlock &b : c->blocks) RC(launch_fused_c1(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, nbad, s));
+    for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_INNER, sw, nbad, s));
     RC(join_sync(c));
-    for (const LBlock &b : c->blocks) RC(launch_fused_c1(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, nbad, s));
+    for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_FRAME, sw, nbad, s));
     RC(timer_end(c, rec));
     if (ffs) {
         RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
         for (const LBlock &b : c->blocks)
-            RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_FRAME, sw, full_c2, s));
+            RC(launch_fused_c2(FT(b), OCN_PART_FRAME, sw, full_c2, s));
         RC(fork_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
         for (const LBlock &b : c->blocks)
-            RC(launch_fused_c2(&b.g, b.ptr.data(), cp(b, t), OCN_PART_INNER, sw, full_c2, s));
+            RC(launch_fused_c2(FT(b), OCN_PART_INNER, sw, full_c2, s));
         RC(join_sync(c));
         RC(timer_end(c, rec));
     }
     return OCN_OK;
 }
+#undef FT
 
 // ------------------------------------------------------------------ tracers
 // expl_tracer (control/tracer.f90:33-62): for every tracer, envoke of the three tracer stages
@@ -816,7 +819,8 @@ static int tracer_stage(ocn_ctx *c, int stage, int k, double tau, bool compact)
     RC(timer_begin(c, OCN_TIMER_TRACER + stage, rec));
     for (const LBlock &b : c->blocks) {
         const Compact t{b.bits, b.rows};
-        RC(launch_tracer(&b.g, b.ptr.data(), compact ? &t : nullptr, stage, k, tau, c->sw.time_smooth, c->stream));
+        RC(launch_tracer(&b.g, b.ptr.data(), (int)b.ptr.size(), compact ? &t : nullptr, stage, k, tau, c->sw.time_smooth,
+                          c->stream));
     }
     RC(timer_end(c, rec));
     if (stage == OCN_TSTAGE_TRAN_DIFF_FLUXES) RC(run_sync(c, kSyncFlux));

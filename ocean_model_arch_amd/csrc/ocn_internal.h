@@ -16,7 +16,7 @@
 #define OCN_ROWS 8
 #endif
 #ifndef OCN_XCD_REMAP
-#define OCN_XCD_REMAP 0
+#define OCN_XCD_REMAP 1
 #endif
 #define OCN_WY (256 / OCN_TW)
 static_assert(OCN_TW % 64 == 0 && 256 % OCN_TW == 0, "OCN_TW must be 64, 128 or 256");
@@ -49,17 +49,17 @@ struct Compact {
 // `cp` = its compact tables or nullptr for the 2-D real(4) arrays, `part` = which part of the
 // launch range (sw_stencils.h frame_rects: the halo-overlap split).
 enum { OCN_PART_ALL = 0, OCN_PART_FRAME = 1, OCN_PART_INNER = 2 };
-int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                   double tau, bool reuse, hipStream_t s);
-int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                   double tau, bool full, bool reuse, hipStream_t s);
-int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                    int32_t *nbad, hipStream_t s);
-int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                    bool full, hipStream_t s);
+int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                   const ocn_sw_params &sw, double tau, bool reuse, hipStream_t s);
+int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                   const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s);
+int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s);
+int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                    const ocn_sw_params &sw, bool full, hipStream_t s);
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
-int launch_tracer(const ocn_block *b, void *const *ptr, const Compact *cp, int stage, int k, double tau, double ts,
-                  hipStream_t s);
+int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
+                  double ts, hipStream_t s);
 // Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
 // they cannot be used into *flags (device int).
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s);

@@ -130,92 +130,60 @@ static int nonnull(std::initializer_list<const void *> ps)
 // ------------------------------------------------------------------ fused launches
 // cp == nullptr: the real(4) fields are read from the 2-D arrays; otherwise from the block's
 // compact tables (sw_stencils.h "compact static fields", built by launch_prepare).
-template <template <bool> class Make, typename... A>
+template <template <bool> class K, typename... A>
 static int launch_fused(const Range &r, const Range &inner, int part, const ocn_block *b, void *const *ptr,
-                        const Compact *cp, hipStream_t s, A... a)
+                        int nptr, const Compact *cp, int tracer, hipStream_t s, A... a)
 {
     RC_K(check_block(b));
-    if (cp) {
-        const Tab<true> t{ptr, cp->bits, cp->rows, block_rows(b)};
-        return launch_part(r, inner, part, Make<true>::make(b, t, a...), s);
-    }
-    const Tab<false> t{ptr};
-    return launch_part(r, inner, part, Make<false>::make(b, t, a...), s);
-}
-template <bool C> struct MkA {
-    static FusedA<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau, bool reuse)
-    {
-        return make_fused_a(b, t, sw, tau, reuse);
-    }
-};
-template <bool C> struct MkB {
-    static FusedB<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, double tau, bool full, bool reuse)
-    {
-        return make_fused_b(b, t, sw, tau, full, reuse);
-    }
-};
-template <bool C> struct MkC1 {
-    static FusedC1<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, int32_t *nbad)
-    {
-        return make_fused_c1(b, t, sw, nbad);
-    }
-};
-template <bool C> struct MkC2 {
-    static HhInit<C> make(const ocn_block *b, const Tab<C> &t, ocn_sw_params sw, bool full)
-    {
-        return make_hh_init(b, t, sw.full_free_surface, full);
-    }
-};
-
-int launch_fused_a(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                   double tau, bool reuse, hipStream_t s)
-{
-    return launch_fused<MkA>(range_fused_a(b, sw, reuse), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, tau,
-                             reuse);
+    if (cp)
+        return launch_part(r, inner, part,
+                           K<true>{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), tracer), a...}, s);
+    return launch_part(r, inner, part, K<false>{*b, make_tab<false>(ptr, nptr, nullptr, nullptr, 0, tracer), a...},
+                       s);
 }
 
-int launch_fused_b(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                   double tau, bool full, bool reuse, hipStream_t s)
+int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                   const ocn_sw_params &sw, double tau, bool reuse, hipStream_t s)
 {
-    return launch_fused<MkB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, tau, full, reuse);
+    return launch_fused<KFusedA>(range_fused_a(b, sw, reuse), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s,
+                                 sw, tau, reuse);
 }
 
-int launch_fused_c1(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                    int32_t *nbad, hipStream_t s)
+int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                   const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s)
 {
-    return launch_fused<MkC1>(range_ring(b), range_interior(b), part, b, ptr, cp, s, sw, nbad);
+    return launch_fused<KFusedB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s, sw, tau,
+                                 full, reuse);
 }
 
-int launch_fused_c2(const ocn_block *b, void *const *ptr, const Compact *cp, int part, const ocn_sw_params &sw,
-                    bool full, hipStream_t s)
+int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s)
 {
-    return launch_fused<MkC2>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, cp, s, sw, full);
+    return launch_fused<KFusedC1>(range_ring(b), range_interior(b), part, b, ptr, nptr, cp, 0, s, sw, nbad);
 }
 
-// tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block
-int launch_tracer(const ocn_block *b, void *const *ptr, const Compact *cp, int stage, int k, double tau, double ts,
-                  hipStream_t s)
+int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                    const ocn_sw_params &sw, bool full, hipStream_t s)
 {
-    RC_K(check_block(b));
-    auto go = [&](const auto &t) -> int {
-        switch (stage) {
-        case OCN_TSTAGE_TRAN_DIFF_FLUXES: {
-            const Range r = range_interior(b);
-            return launch_range(r.m0, r.m1, r.n0, r.n1, make_tran_diff_fluxes(b, t, k), s);
-        }
-        case OCN_TSTAGE_TRAN_DIFF_TRACER: {
-            const Range r = range_interior(b);
-            return launch_range(r.m0, r.m1, r.n0, r.n1, make_tran_diff_tracer(b, t, k, tau), s);
-        }
-        case OCN_TSTAGE_TRACER_NEXT_STEP: {
-            const Range r = range_ring(b);
-            return launch_range(r.m0, r.m1, r.n0, r.n1, make_tracer_next_step(b, t, k, ts), s);
-        }
-        default: return set_error(OCN_ERR_ARG, "bad tracer stage id");
-        }
-    };
-    if (cp) return go(Tab<true>{ptr, cp->bits, cp->rows, block_rows(b)});
-    return go(Tab<false>{ptr});
+    return launch_fused<KHhInit>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s,
+                                 (int)sw.full_free_surface, full);
+}
+
+// tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy
+// layer passes it (tracer_interface.f90:47)
+int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
+                  double ts, hipStream_t s)
+{
+    const Range ri = range_interior(b), rr = range_ring(b);
+    switch (stage) {
+    case OCN_TSTAGE_TRAN_DIFF_FLUXES:
+        return launch_fused<KTranDiffFluxes>(ri, ri, OCN_PART_ALL, b, ptr, nptr, cp, k, s, 1.0);
+    case OCN_TSTAGE_TRAN_DIFF_TRACER:
+        return launch_fused<KTranDiffTracer>(ri, ri, OCN_PART_ALL, b, ptr, nptr, cp, k, s, tau);
+    case OCN_TSTAGE_TRACER_NEXT_STEP:
+        return launch_fused<KTracerNextStep>(rr, rr, OCN_PART_ALL, b, ptr, nptr, cp, k, s, ts);
+    default: return set_error(OCN_ERR_ARG, "bad tracer stage id");
+    }
 }
 
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s)

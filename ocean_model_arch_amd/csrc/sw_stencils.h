@@ -17,7 +17,7 @@
 #include "../../include/ocn_sw.h"
 
 #ifndef OCN_HD
-#define OCN_HD __device__
+#define OCN_HD __host__ __device__
 #endif
 #ifndef OCN_INLINE
 #define OCN_INLINE __forceinline__
@@ -642,8 +642,8 @@ struct Prepare {
 // Built from a block's field table (`ptr`, indexed by ocn_field_slot) -- used by the fused
 // launches and by the host harness, so both run exactly the same functors over the same ranges.
 inline int ocn_field_slot(int id) { return id < OCN_NUM_R4 ? id : OCN_NUM_R4 + (id - OCN_SSH); }
-inline Geo geo(const ocn_block *b) { return Geo{b->bnd_x1, b->bnd_y1, (unsigned)b->pitch}; }
-inline unsigned block_rows(const ocn_block *b) { return (unsigned)(b->bnd_y2 - b->bnd_y1 + 1); }
+OCN_HD inline Geo geo(const ocn_block *b) { return Geo{b->bnd_x1, b->bnd_y1, (unsigned)b->pitch}; }
+OCN_HD inline unsigned block_rows(const ocn_block *b) { return (unsigned)(b->bnd_y2 - b->bnd_y1 + 1); }
 
 struct Range { int m0, m1, n0, n1; };
 inline Range range_interior(const ocn_block *b) { return {b->nx_start, b->nx_end, b->ny_start, b->ny_end}; }
@@ -713,63 +713,90 @@ inline Prepare make_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits,
     return k;
 }
 
-// Field table of one block: real(8) arrays from `ptr`; masks / metrics from `ptr` (C = false)
-// or from the compact tables (C = true).
-template <bool C> struct Tab;
-template <> struct Tab<false> {
-    void *const *ptr;
-    Msk<false> m(int id) const { return {(const float *)ptr[ocn_field_slot(id)]}; }
-    Met<false> g(int id) const { return {(const float *)ptr[ocn_field_slot(id)]}; }
-    double *f(int id) const { return (double *)ptr[ocn_field_slot(id)]; }
-};
-template <> struct Tab<true> {
-    void *const *ptr;
+// Field table of one block, passed BY VALUE to the fused kernels, which build their stage
+// functors on the device from it (the K* wrappers below): every distinct array pointer then
+// occupies one kernel-argument slot and one SGPR pair, however many stages read it.  Slots:
+// the SW fields (ocn_field_slot order), flux_x, flux_y, and ff1/ff1p/ff1n of ONE tracer.
+// Masks / metrics come from the 2-D arrays (C = false) or from the compact tables (C = true).
+constexpr int kTabSlots = OCN_NUM_R4 + OCN_NUM_R8 + 5;
+OCN_HD inline int tab_slot(int id)
+{
+    return id < OCN_NUM_R4 ? id
+           : id < OCN_TRACER_BASE ? OCN_NUM_R4 + (id - OCN_SSH)
+                                  : OCN_NUM_R4 + OCN_NUM_R8 + 2 + (id - OCN_TRACER_BASE) % 3;
+}
+template <bool C> struct Tab {
+    const void *p[kTabSlots];
     const uint8_t *bits; const float *rows; unsigned nrows;
-    Msk<true> m(int id) const { return {bits, 1u << id}; }
-    Met<true> g(int id) const { return {rows + (size_t)(id - OCN_DX) * nrows}; }
-    double *f(int id) const { return (double *)ptr[ocn_field_slot(id)]; }
+    OCN_HD OCN_INLINE Msk<C> m(int id) const
+    {
+        if constexpr (C) return Msk<C>{bits, 1u << id};
+        else return Msk<C>{(const float *)p[id]};
+    }
+    OCN_HD OCN_INLINE Met<C> g(int id) const
+    {
+        if constexpr (C) return Met<C>{rows + (unsigned)(id - OCN_DX) * nrows};
+        else return Met<C>{(const float *)p[id]};
+    }
+    OCN_HD OCN_INLINE double *f(int id) const { return (double *)p[tab_slot(id)]; }
 };
+// host: the table of a block from its storage `ptr` (indexed by ocn_field_slot, `nptr` entries:
+// SW fields, then flux_x, flux_y, ff1/ff1p/ff1n per tracer), holding tracer `tracer`'s fields
+template <bool C>
+inline Tab<C> make_tab(void *const *ptr, int nptr, const uint8_t *bits, const float *rows, unsigned nrows,
+                       int tracer = 0)
+{
+    Tab<C> t{};
+    for (int i = 0; i < OCN_NUM_R4 + OCN_NUM_R8 + 2 && i < nptr; ++i) t.p[i] = ptr[i];
+    if (tracer > 0)
+        for (int w = 0; w < 3; ++w) {
+            const int slot = ocn_field_slot(OCN_FF1(tracer) + w);
+            t.p[OCN_NUM_R4 + OCN_NUM_R8 + 2 + w] = slot < nptr ? ptr[slot] : nullptr;
+        }
+    t.bits = bits; t.rows = rows; t.nrows = nrows;
+    return t;
+}
 
-template <bool C> Interp<C> make_interp(const Tab<C> &t)
+template <bool C> OCN_HD inline Interp<C> make_interp(const Tab<C> &t)
 {
     return Interp<C>{t.m(OCN_LU), t.g(OCN_DX), t.g(OCN_DY), t.g(OCN_DXT), t.g(OCN_DYT), t.g(OCN_DXH),
                      t.g(OCN_DYH), t.g(OCN_DXB), t.g(OCN_DYB)};
 }
-template <bool C> SwUpdateSsh<C> make_sw_update_ssh(const ocn_block *b, const Tab<C> &t, double tau)
+template <bool C> OCN_HD inline SwUpdateSsh<C> make_sw_update_ssh(const ocn_block *b, const Tab<C> &t, double tau)
 {
     return SwUpdateSsh<C>{geo(b), tau, t.m(OCN_LU), t.g(OCN_DX), t.g(OCN_DY), t.g(OCN_DXH), t.g(OCN_DYH),
                           t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_SSHN), t.f(OCN_SSHP), t.f(OCN_UBRTR), t.f(OCN_VBRTR)};
 }
-template <bool C> HhUpdate<C> make_hh_update(const ocn_block *b, const Tab<C> &t)
+template <bool C> OCN_HD inline HhUpdate<C> make_hh_update(const ocn_block *b, const Tab<C> &t)
 {
     return HhUpdate<C>{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, make_interp(t),
                        t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LUH), t.f(OCN_HHQ_N), t.f(OCN_HHU_N), t.f(OCN_HHV_N),
                        t.f(OCN_HHH_N), t.f(OCN_SSH), t.f(OCN_HHQ_REST)};
 }
-template <bool C> UvTransVort<C> make_uv_trans_vort(const ocn_block *b, const Tab<C> &t)
+template <bool C> OCN_HD inline UvTransVort<C> make_uv_trans_vort(const ocn_block *b, const Tab<C> &t)
 {
     return UvTransVort<C>{geo(b), t.m(OCN_LUU), t.g(OCN_DXT), t.g(OCN_DYT), t.g(OCN_DXB), t.g(OCN_DYB),
                           t.f(OCN_UBRTR), t.f(OCN_VBRTR), t.f(OCN_VORT)};
 }
-template <bool C> UvTrans<C> make_uv_trans(const ocn_block *b, const Tab<C> &t)
+template <bool C> OCN_HD inline UvTrans<C> make_uv_trans(const ocn_block *b, const Tab<C> &t)
 {
     return UvTrans<C>{geo(b), t.m(OCN_LCU), t.m(OCN_LCV), t.m(OCN_LUU), t.g(OCN_DXH), t.g(OCN_DYH),
                       t.f(OCN_UBRTR), t.f(OCN_VBRTR), t.f(OCN_VORT), t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_HHH),
                       t.f(OCN_RHSX_ADV), t.f(OCN_RHSY_ADV)};
 }
-template <bool C> StressComponents<C> make_stress_components(const ocn_block *b, const Tab<C> &t)
+template <bool C> OCN_HD inline StressComponents<C> make_stress_components(const ocn_block *b, const Tab<C> &t)
 {
     return StressComponents<C>{geo(b), t.m(OCN_LU), t.m(OCN_LUU), t.g(OCN_DX), t.g(OCN_DY), t.g(OCN_DXT),
                                t.g(OCN_DYT), t.g(OCN_DXH), t.g(OCN_DYH), t.g(OCN_DXB), t.g(OCN_DYB),
                                t.f(OCN_UBRTRP), t.f(OCN_VBRTRP), t.f(OCN_STR_T), t.f(OCN_STR_S)};
 }
-template <bool C> UvDiff2<C> make_uv_diff2(const ocn_block *b, const Tab<C> &t)
+template <bool C> OCN_HD inline UvDiff2<C> make_uv_diff2(const ocn_block *b, const Tab<C> &t)
 {
     return UvDiff2<C>{geo(b), t.m(OCN_LCU), t.m(OCN_LCV), t.g(OCN_DX), t.g(OCN_DY), t.g(OCN_DXT), t.g(OCN_DYT),
                       t.g(OCN_DXH), t.g(OCN_DYH), t.g(OCN_DXB), t.g(OCN_DYB), t.f(OCN_MU), t.f(OCN_STR_T),
                       t.f(OCN_STR_S), t.f(OCN_HHQ), t.f(OCN_HHH), t.f(OCN_RHSX_DIF), t.f(OCN_RHSY_DIF)};
 }
-template <bool C> SwUpdateUv<C> make_sw_update_uv(const ocn_block *b, const Tab<C> &t, double tau)
+template <bool C> OCN_HD inline SwUpdateUv<C> make_sw_update_uv(const ocn_block *b, const Tab<C> &t, double tau)
 {
     return SwUpdateUv<C>{geo(b), tau, t.m(OCN_LCU), t.m(OCN_LCV), t.g(OCN_DXT), t.g(OCN_DYT), t.g(OCN_DXH),
                          t.g(OCN_DYH), t.g(OCN_DXB), t.g(OCN_DYB), t.f(OCN_HHU), t.f(OCN_HHU_N), t.f(OCN_HHU_P),
@@ -778,19 +805,19 @@ template <bool C> SwUpdateUv<C> make_sw_update_uv(const ocn_block *b, const Tab<
                          t.g(OCN_R_DISS), t.g(OCN_RLH_S), t.f(OCN_RHSX), t.f(OCN_RHSY), t.f(OCN_RHSX_ADV),
                          t.f(OCN_RHSY_ADV), t.f(OCN_RHSX_DIF), t.f(OCN_RHSY_DIF)};
 }
-template <bool C> SwNextStep<C> make_sw_next_step(const ocn_block *b, const Tab<C> &t, double ts)
+template <bool C> OCN_HD inline SwNextStep<C> make_sw_next_step(const ocn_block *b, const Tab<C> &t, double ts)
 {
     return SwNextStep<C>{geo(b), ts, t.m(OCN_LU), t.m(OCN_LCU), t.m(OCN_LCV), t.f(OCN_SSH), t.f(OCN_SSHN),
                          t.f(OCN_SSHP), t.f(OCN_UBRTR), t.f(OCN_UBRTRN), t.f(OCN_UBRTRP), t.f(OCN_VBRTR),
                          t.f(OCN_VBRTRN), t.f(OCN_VBRTRP)};
 }
-template <bool C> HhShift<C> make_hh_shift(const ocn_block *b, const Tab<C> &t, double ts)
+template <bool C> OCN_HD inline HhShift<C> make_hh_shift(const ocn_block *b, const Tab<C> &t, double ts)
 {
     return HhShift<C>{geo(b), ts, t.m(OCN_LU), t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LUH), t.f(OCN_HHQ),
                       t.f(OCN_HHQ_P), t.f(OCN_HHQ_N), t.f(OCN_HHU), t.f(OCN_HHU_P), t.f(OCN_HHU_N), t.f(OCN_HHV),
                       t.f(OCN_HHV_P), t.f(OCN_HHV_N), t.f(OCN_HHH), t.f(OCN_HHH_P), t.f(OCN_HHH_N)};
 }
-template <bool C> HhInit<C> make_hh_init(const ocn_block *b, const Tab<C> &t, int ffs, bool full)
+template <bool C> OCN_HD inline HhInit<C> make_hh_init(const ocn_block *b, const Tab<C> &t, int ffs, bool full)
 {
     return HhInit<C>{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)ffs, full,
                      make_interp(t), t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LUH), t.f(OCN_HHQ), t.f(OCN_HHQ_P),
@@ -798,36 +825,36 @@ template <bool C> HhInit<C> make_hh_init(const ocn_block *b, const Tab<C> &t, in
                      t.f(OCN_HHV_N), t.f(OCN_HHH), t.f(OCN_HHH_P), t.f(OCN_HHH_N), t.f(OCN_SSH), t.f(OCN_SSHP),
                      t.f(OCN_HHQ_REST)};
 }
-template <bool C> CheckSshErr<C> make_check_ssh_err(const ocn_block *b, const Tab<C> &t, int32_t *nbad)
+template <bool C> OCN_HD inline CheckSshErr<C> make_check_ssh_err(const ocn_block *b, const Tab<C> &t, int32_t *nbad)
 {
     return CheckSshErr<C>{geo(b), t.m(OCN_LU), t.f(OCN_SSH), (int *)nbad};
 }
 // tracer k (1-based); the PSy layer passes factor_mu = 1.0d0 (tracer_interface.f90:47)
 template <bool C>
-TranDiffFluxes<C> make_tran_diff_fluxes(const ocn_block *b, const Tab<C> &t, int k, double factor_mu = 1.0)
+OCN_HD inline TranDiffFluxes<C> make_tran_diff_fluxes(const ocn_block *b, const Tab<C> &t, int k, double factor_mu = 1.0)
 {
     return TranDiffFluxes<C>{geo(b), factor_mu, t.m(OCN_LCU), t.m(OCN_LCV), t.g(OCN_DXT), t.g(OCN_DYT), t.g(OCN_DXH),
                              t.g(OCN_DYH), t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_FF1(k)), t.f(OCN_UBRTR),
                              t.f(OCN_VBRTR), t.f(OCN_MU), t.f(OCN_FLUX_X), t.f(OCN_FLUX_Y)};
 }
-template <bool C> TranDiffTracer<C> make_tran_diff_tracer(const ocn_block *b, const Tab<C> &t, int k, double tau)
+template <bool C> OCN_HD inline TranDiffTracer<C> make_tran_diff_tracer(const ocn_block *b, const Tab<C> &t, int k, double tau)
 {
     return TranDiffTracer<C>{geo(b), tau, t.m(OCN_LU), t.g(OCN_DX), t.g(OCN_DY), t.f(OCN_HHQ_N), t.f(OCN_HHQ_P),
                              t.f(OCN_FLUX_X), t.f(OCN_FLUX_Y), t.f(OCN_FF1P(k)), t.f(OCN_FF1N(k))};
 }
-template <bool C> TracerNextStep<C> make_tracer_next_step(const ocn_block *b, const Tab<C> &t, int k, double ts)
+template <bool C> OCN_HD inline TracerNextStep<C> make_tracer_next_step(const ocn_block *b, const Tab<C> &t, int k, double ts)
 {
     return TracerNextStep<C>{geo(b), ts, t.m(OCN_LU), t.f(OCN_FF1N(k)), t.f(OCN_FF1P(k)), t.f(OCN_FF1(k))};
 }
 template <bool C>
-FusedA<C> make_fused_a(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau, bool reuse = false)
+OCN_HD inline FusedA<C> make_fused_a(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau, bool reuse = false)
 {
     return FusedA<C>{b->nx_start, b->ny_start, sw.full_free_surface > 0 && !reuse, sw.trans_terms > 0, sw.ksw_lat > 0,
                      make_sw_update_ssh(b, t, tau), make_hh_update(b, t), make_uv_trans_vort(b, t),
                      make_stress_components(b, t)};
 }
 template <bool C>
-FusedB<C> make_fused_b(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau, bool full,
+OCN_HD inline FusedB<C> make_fused_b(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, double tau, bool full,
                        bool reuse = false)
 {
     FusedB<C> k{sw.trans_terms > 0, sw.ksw_lat > 0, full, make_uv_trans(b, t), make_uv_diff2(b, t),
@@ -835,10 +862,43 @@ FusedB<C> make_fused_b(const ocn_block *b, const Tab<C> &t, const ocn_sw_params 
     if (reuse) { k.a7.hhun = k.a7.hhu; k.a7.hhvn = k.a7.hhv; }
     return k;
 }
-template <bool C> FusedC1<C> make_fused_c1(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, int32_t *nbad)
+template <bool C> OCN_HD inline FusedC1<C> make_fused_c1(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, int32_t *nbad)
 {
     return FusedC1<C>{b->nx_start, b->nx_end, b->ny_start, b->ny_end, sw.full_free_surface > 0, (int *)nbad,
                       make_sw_next_step(b, t, sw.time_smooth), make_hh_shift(b, t, sw.time_smooth)};
 }
+
+// ------------------------------------------------------------------ launch functors
+// What the fused / tracer kernels receive: the block, its field table and the scalars.  The
+// stage functors are built on the device inside operator(), so each distinct array is one
+// kernel-argument pointer however many stages read it (no duplicated pointers, no SGPR spills).
+template <bool C> struct KFusedA {
+    ocn_block b; Tab<C> t; ocn_sw_params sw; double tau; bool reuse;
+    OCN_HD void operator()(int m, int n) const { make_fused_a(&b, t, sw, tau, reuse)(m, n); }
+};
+template <bool C> struct KFusedB {
+    ocn_block b; Tab<C> t; ocn_sw_params sw; double tau; bool full, reuse;
+    OCN_HD void operator()(int m, int n) const { make_fused_b(&b, t, sw, tau, full, reuse)(m, n); }
+};
+template <bool C> struct KFusedC1 {
+    ocn_block b; Tab<C> t; ocn_sw_params sw; int32_t *nbad;
+    OCN_HD void operator()(int m, int n) const { make_fused_c1(&b, t, sw, nbad)(m, n); }
+};
+template <bool C> struct KHhInit {
+    ocn_block b; Tab<C> t; int ffs; bool full;
+    OCN_HD void operator()(int m, int n) const { make_hh_init(&b, t, ffs, full)(m, n); }
+};
+template <bool C> struct KTranDiffFluxes {      // t holds the tracer's fields
+    ocn_block b; Tab<C> t; double factor_mu;
+    OCN_HD void operator()(int m, int n) const { make_tran_diff_fluxes(&b, t, 1, factor_mu)(m, n); }
+};
+template <bool C> struct KTranDiffTracer {
+    ocn_block b; Tab<C> t; double tau;
+    OCN_HD void operator()(int m, int n) const { make_tran_diff_tracer(&b, t, 1, tau)(m, n); }
+};
+template <bool C> struct KTracerNextStep {
+    ocn_block b; Tab<C> t; double ts;
+    OCN_HD void operator()(int m, int n) const { make_tracer_next_step(&b, t, 1, ts)(m, n); }
+};
 
 }  // namespace ocn

@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #define OCN_HD
@@ -58,17 +59,18 @@ template <bool C> static void run_stage(int stage, const ocn_block *b, const Tab
     case OCN_STAGE_SW_UPDATE_UV: run(range_interior(b), make_sw_update_uv(b, t, tau)); break;
     case OCN_STAGE_SW_NEXT_STEP: run(range_ring(b), make_sw_next_step(b, t, sw->time_smooth)); break;
     case OCN_STAGE_HH_SHIFT: run(range_ring(b), make_hh_shift(b, t, sw->time_smooth)); break;
-    case OCN_STAGE_HH_INIT:
-        run_part(range_bnd(b), inner_interior_shrunk(b), part, make_hh_init(b, t, sw->full_free_surface, full));
+    case OCN_STAGE_HH_INIT:   // as the fused C2 launch (KHhInit); full = true is the reference kernel
+        run_part(range_bnd(b), inner_interior_shrunk(b), part, KHhInit<C>{*b, t, sw->full_free_surface, full});
         break;
     case OCN_STAGE_CHECK_SSH_ERR: run(range_interior(b), make_check_ssh_err(b, t, nbad)); break;
+    // the fused launch functors exactly as sw_kernels.hip passes them (stage functors built inside)
     case 11:
-        run_part(range_fused_a(b, *sw, reuse), inner_interior_shrunk(b), part, make_fused_a(b, t, *sw, tau, reuse));
+        run_part(range_fused_a(b, *sw, reuse), inner_interior_shrunk(b), part, KFusedA<C>{*b, t, *sw, tau, reuse});
         break;
     case 12:
-        run_part(range_interior(b), inner_interior_shrunk(b), part, make_fused_b(b, t, *sw, tau, full, reuse));
+        run_part(range_interior(b), inner_interior_shrunk(b), part, KFusedB<C>{*b, t, *sw, tau, full, reuse});
         break;
-    case 13: run_part(range_ring(b), range_interior(b), part, make_fused_c1(b, t, *sw, nbad)); break;
+    case 13: run_part(range_ring(b), range_interior(b), part, KFusedC1<C>{*b, t, *sw, nbad}); break;
     default: g_oob = -1;
     }
 }
@@ -77,14 +79,15 @@ template <bool C> static void run_stage(int stage, const ocn_block *b, const Tab
 // bits/rows: the block's compact tables (hst_prepare) or nullptr for the 2-D real(4) arrays;
 // flags: bit 0 = FusedB / HhInit `full`, bit 1 = fused A/B "reuse"; part: the halo-overlap
 // split (fused A/B/C1, hh_init).  Returns the number of out-of-bounds accesses (0 = clean).
-extern "C" long hst_stage(int stage, const ocn_block *b, void *const *ptr, const uint8_t *bits, const float *rows,
-                          const ocn_sw_params *sw, double tau, int32_t *nbad, int flags, int part)
+extern "C" long hst_stage(int stage, const ocn_block *b, void *const *ptr, int nptr, const uint8_t *bits,
+                          const float *rows, const ocn_sw_params *sw, double tau, int32_t *nbad, int flags, int part)
 {
     g_oob = 0;
     ocn_host_limit = (unsigned)(b->pitch * (int64_t)(b->bnd_y2 - b->bnd_y1 + 1));
     const bool full = flags & 1, reuse = (flags & 2) != 0;
-    if (bits) run_stage(stage, b, Tab<true>{ptr, bits, rows, block_rows(b)}, sw, tau, nbad, full, reuse, part);
-    else run_stage(stage, b, Tab<false>{ptr}, sw, tau, nbad, full, reuse, part);
+    if (bits)
+        run_stage(stage, b, make_tab<true>(ptr, nptr, bits, rows, block_rows(b)), sw, tau, nbad, full, reuse, part);
+    else run_stage(stage, b, make_tab<false>(ptr, nptr, nullptr, nullptr, 0), sw, tau, nbad, full, reuse, part);
     return g_oob;
 }
 
@@ -111,21 +114,23 @@ extern "C" int hst_split_ok(int m0, int m1, int n0, int n1, int i0, int i1, int 
 
 // Tracer stage (OCN_TSTAGE_*) of tracer k: ptr must hold the tracer slots (flux_x, flux_y,
 // ff1/ff1p/ff1n per tracer) after the SW ones.
-extern "C" long hst_tracer(int stage, const ocn_block *b, void *const *ptr, const uint8_t *bits, const float *rows,
-                           int k, double tau, double ts, double factor_mu)
+extern "C" long hst_tracer(int stage, const ocn_block *b, void *const *ptr, int nptr, const uint8_t *bits,
+                           const float *rows, int k, double tau, double ts, double factor_mu)
 {
     g_oob = 0;
     ocn_host_limit = (unsigned)(b->pitch * (int64_t)(b->bnd_y2 - b->bnd_y1 + 1));
     auto go = [&](const auto &t) {
-        switch (stage) {
-        case OCN_TSTAGE_TRAN_DIFF_FLUXES: run(range_interior(b), make_tran_diff_fluxes(b, t, k, factor_mu)); break;
-        case OCN_TSTAGE_TRAN_DIFF_TRACER: run(range_interior(b), make_tran_diff_tracer(b, t, k, tau)); break;
-        case OCN_TSTAGE_TRACER_NEXT_STEP: run(range_ring(b), make_tracer_next_step(b, t, k, ts)); break;
+        using T = std::decay_t<decltype(t)>;
+        constexpr bool C = std::is_same_v<T, Tab<true>>;
+        switch (stage) {   // the launch functors of sw_kernels.hip launch_tracer
+        case OCN_TSTAGE_TRAN_DIFF_FLUXES: run(range_interior(b), KTranDiffFluxes<C>{*b, t, factor_mu}); break;
+        case OCN_TSTAGE_TRAN_DIFF_TRACER: run(range_interior(b), KTranDiffTracer<C>{*b, t, tau}); break;
+        case OCN_TSTAGE_TRACER_NEXT_STEP: run(range_ring(b), KTracerNextStep<C>{*b, t, ts}); break;
         default: g_oob = -1;
         }
     };
-    if (bits) go(Tab<true>{ptr, bits, rows, block_rows(b)});
-    else go(Tab<false>{ptr});
+    if (bits) go(make_tab<true>(ptr, nptr, bits, rows, block_rows(b), k));
+    else go(make_tab<false>(ptr, nptr, nullptr, nullptr, 0, k));
     return g_oob;
 }
 

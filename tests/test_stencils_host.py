@@ -46,12 +46,12 @@ def hst():
     subprocess.check_call(["make", "-s", "-f", os.path.join(REPO, "tests", "native", "Makefile")], cwd=REPO)
     L = C.CDLL(LIB)
     L.hst_stage.restype = C.c_long
-    L.hst_stage.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(SwParams),
-                            C.c_double, C.POINTER(C.c_int32), C.c_int, C.c_int]
+    L.hst_stage.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                            C.POINTER(SwParams), C.c_double, C.POINTER(C.c_int32), C.c_int, C.c_int]
     L.hst_split_ok.argtypes = [C.c_int] * 8
     L.hst_tracer.restype = C.c_long
-    L.hst_tracer.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_double,
-                             C.c_double, C.c_double]
+    L.hst_tracer.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                             C.c_double, C.c_double, C.c_double]
     L.hst_prepare.restype = C.c_int
     L.hst_prepare.argtypes = [C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p]
     return L
@@ -86,7 +86,8 @@ def test_tracer_functors_match_reference(hst, geom):
     bad = []
     for st, kname in enumerate(cases.TRACER_KERNEL_NAMES):
         arrs = {k[3:]: z[k].copy(order="F") for k in z.files if k.startswith("in/")}
-        oob = hst.hst_tracer(st, C.byref(b), table(arrs, 1, True), None, None, 1, float(z["tau"]),
+        t = table(arrs, 1, True)
+        oob = hst.hst_tracer(st, C.byref(b), t, len(t), None, None, 1, float(z["tau"]),
                              float(z["time_smooth"]), float(z["factor_mu"]))
         assert oob == 0, f"{kname}: {oob} out-of-bounds accesses"
         for nm in [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]:
@@ -104,7 +105,8 @@ def test_stage_functors_match_reference(hst, geom):
     for kname in cases.KERNEL_NAMES:
         arrs = {k[3:]: z[k].copy(order="F") for k in z.files if k.startswith("in/")}
         nbad = C.c_int32(0)
-        oob = hst.hst_stage(STAGE_IDS[kname], C.byref(b), table(arrs), None, None, C.byref(sw), float(z["tau"]),
+        t = table(arrs)
+        oob = hst.hst_stage(STAGE_IDS[kname], C.byref(b), t, len(t), None, None, C.byref(sw), float(z["tau"]),
                             C.byref(nbad), 1, 0)
         assert oob == 0, f"{kname}: {oob} out-of-bounds accesses"
         for nm in [k.split("/", 1)[1] for k in z.files if k.startswith(kname + "/")]:
@@ -147,7 +149,7 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None, first=True):
             for st, sync in ((0, ["flux_x", "flux_y"]), (1, [f"ff1n_{t}"]), (2, [])):
                 for k, (b, tb) in enumerate(blocks):
                     bits, rows = (tabs[k][0].ctypes.data, tabs[k][1].ctypes.data) if compact else (None, None)
-                    oob = hst.hst_tracer(st, C.byref(b), tb, bits, rows, t, 1.0, sw_o.time_smooth, 1.0)
+                    oob = hst.hst_tracer(st, C.byref(b), tb, len(tb), bits, rows, t, 1.0, sw_o.time_smooth, 1.0)
                     assert oob == 0, f"tracer stage {st}: {oob} out-of-bounds accesses"
                 for f in sync:
                     om.sync(f)
@@ -155,7 +157,7 @@ def host_step(hst, om, mode, nbad, last=True, tabs=None, first=True):
     def each(stage, tau=1.0, full=1, part=0):
         for k, (b, t) in enumerate(blocks):
             bits, rows = (tabs[k][0].ctypes.data, tabs[k][1].ctypes.data) if compact else (None, None)
-            oob = hst.hst_stage(stage, C.byref(b), t, bits, rows, C.byref(sw), tau, C.byref(nbad), full, part)
+            oob = hst.hst_stage(stage, C.byref(b), t, len(t), bits, rows, C.byref(sw), tau, C.byref(nbad), full, part)
             assert oob == 0, f"stage {stage}: {oob} out-of-bounds accesses"
 
     def syncs(names):
