@@ -30,18 +30,30 @@ STAGE_BYTES = {"sw_update_ssh": 68, "hh_update": 96, "uv_trans_vort": 44, "uv_tr
                "stress_components": 72, "uv_diff2": 96, "sw_update_uv": 200, "sw_next_step": 132,
                "hh_shift": 176, "hh_init": 168}
 B_ALG = sum(STAGE_BYTES.values())
-# distinct arrays read + written once per interior cell by each fused launch (DESIGN.md "bytes"):
-# real(4) masks/metrics as 2-D arrays, or compact (1 mask byte per point, metrics per row);
-# steps other than the last of an ocn_ctx_step call skip dead stores (FusedB RHS*_adv/_dif,
-# HhInit hqp/hqn/hun/hvn/hhn), FULL_EXTRA more bytes on the last step.
-FUSED_BYTES = {False: {"fused_a": 180, "fused_b": 220, "fused_c1": 132, "hh_init": 128},
-               True: {"fused_a": 129, "fused_b": 169, "fused_c1": 121, "hh_init": 81}}
-FULL_EXTRA = {"fused_b": 32, "hh_init": 40}
+# Distinct arrays read + written once per interior cell by each fused launch, for
+# the bench's sw.par (all three flags on), as (compact static fields, 2-D real(4) arrays).  An
+# ocn_ctx_step call of K steps runs its first step plain, steps 2..K-1 as "reuse" steps (fused A
+# skips hh_update, fused B reads hhu/hhv for hhu_n/hhv_n) and its last step "full" (fused B and
+# hh_init store the values only the host reads).  K = 1: one plain + full step.
+FUSED_BYTES = {
+    "fused_a": {"first": (129, 180), "mid": (89, 128), "last": (129, 180)},
+    "fused_b": {"first": (169, 220), "mid": (153, 204), "last": (201, 252)},
+    "fused_c1": {"first": (121, 132), "mid": (121, 132), "last": (121, 132)},
+    "hh_init": {"first": (81, 128), "mid": (81, 128), "last": (121, 168)},
+}
 
 
 def fused_bytes(compact: bool, steps: int):
     """Mean bytes per interior cell per launch over one ocn_ctx_step call of `steps` steps."""
-    return {k: v + FULL_EXTRA.get(k, 0) / steps for k, v in FUSED_BYTES[compact].items()}
+    i = 0 if compact else 1
+    out = {}
+    for k, kinds in FUSED_BYTES.items():
+        if steps == 1:
+            v = kinds["last"][i]
+        else:
+            v = (kinds["first"][i] + (steps - 2) * kinds["mid"][i] + kinds["last"][i]) / steps
+        out[k] = v
+    return out
 
 
 def dims_create(n: int):
@@ -121,6 +133,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stages", action="store_true", help="run the 11 reference stages instead of the fused step")
     ap.add_argument("--no-compact", action="store_true", help="fused step on the 2-D real(4) arrays")
+    ap.add_argument("--no-march", action="store_true", help="one thread per point in every launch (no register march)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -152,6 +165,7 @@ def main():
         parity = multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for)
     model.set_fused(not args.stages)
     model.set_compact(not args.no_compact)
+    model.set_march(not args.no_march)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -204,6 +218,7 @@ def main():
                           "box": [nxbox, nybox], "blocks": [bx, by], "graph": bool(args.graph),
                           "step": "reference stages" if args.stages else "fused groups",
                           "static_fields": "compact" if compact else "2-D arrays",
+                          "march": bool(compact and not args.stages and not args.no_march),
                           "parallelism": f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else "1 block"},
                "roofline": roof,
                "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),

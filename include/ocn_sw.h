@@ -288,11 +288,14 @@ int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
  *  real(4) fields (checked when they were last set; same results bit for bit).  Handing out a
  *  real(4) pointer with ocn_ctx_field disables this until it is set to 1 again, which also
  *  rebuilds the tables from the fields at the next ocn_ctx_step.
+ *  OCN_OPT_MARCH (default 1): with the compact tables, the stencil launches that have a
+ *  register-march form (fused B) run as one (same results bit for bit); 0 = one thread per point.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables. */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
-enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5 };
+enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
+       OCN_OPT_MARCH = 6 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers). */

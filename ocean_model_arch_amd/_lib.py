@@ -72,6 +72,7 @@ OPT_OVERLAP = 2
 OPT_STAGE_TIMING = 3
 OPT_FUSED = 4
 OPT_COMPACT = 5
+OPT_MARCH = 6
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",

@@ -186,6 +186,7 @@ struct ocn_ctx {
     // compact static fields: requested (OCN_OPT_COMPACT), in use, stale (real(4) fields
     // changed since they were built), or unusable because raw real(4) pointers were handed out
     bool compact_req = true, compact = false, static_dirty = true;
+    bool march = true;   // OCN_OPT_MARCH
     mutable bool r4_escaped = false;
     int32_t *d_flags = nullptr;
 };
@@ -739,7 +740,7 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool l
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
     auto cp = [c](const LBlock &b, Compact &t) -> const Compact * {
-        t = Compact{b.bits, b.rows};
+        t = Compact{b.bits, b.rows, c->march};
         return c->compact ? &t : nullptr;
     };
     Compact t;
@@ -1333,6 +1334,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         if (c->overlap != (value != 0)) drop_graphs(c);
         c->overlap = value != 0;
         return OCN_OK;
+    case OCN_OPT_MARCH: c->march = value != 0; return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -1351,6 +1353,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_FUSED: *value = c->fused; return OCN_OK;
     case OCN_OPT_OVERLAP: *value = c->overlap; return OCN_OK;
     case OCN_OPT_COMPACT: *value = c->fused && c->compact; return OCN_OK;
+    case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

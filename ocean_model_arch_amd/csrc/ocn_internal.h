@@ -39,10 +39,12 @@ inline int field_slot(int id) { return is_r4(id) ? id : OCN_NUM_R4 + (id - OCN_S
 constexpr int kNumSlots = OCN_NUM_R4 + OCN_NUM_R8;   // without tracer fields
 constexpr int kMaxTracers = 64;
 
-// A block's compact static fields (sw_stencils.h): mask bytes (pitch x rows) and metric rows.
+// A block's compact static fields (sw_stencils.h): mask bytes (pitch x rows) and metric rows;
+// march: run the stencil launches that have one as register marches (sw_kernels.hip k_march).
 struct Compact {
     const uint8_t *bits;
     const float *rows;
+    bool march;
 };
 
 // Fused step groups (sw_kernels.hip); `ptr` = the block's field table indexed by field_slot(),

@@ -94,6 +94,194 @@ static int launch_part(const Range &r, const Range &inner, int part, const Body 
     return launch_range(r.m0, r.m1, r.n0, r.n1, body, s);
 }
 
+// ------------------------------------------------------------------ register march
+// For stencils over many arrays the k_range mapping issues one load instruction per
+// (array, neighbour): fused B issues 76 per cell, and the L1/TA path -- not HBM -- limits it
+// (SQ_WAIT_INST_ANY ~70 % of wave time; profiles/r01b).  The march mapping loads each array
+// once per cell instead:
+//   * a wave owns 64 consecutive columns and marches down kMarchRows rows; lanes 1..62 produce
+//     output, lanes 0 and 63 only load the m-1 / m+1 neighbour columns;
+//   * the n-1 / n / n+1 rows of an array stay in registers and rotate as the wave moves down, so
+//     each iteration loads only row n+1 (or row n for arrays read at n-1 and n);
+//   * m+1 / m-1 neighbours come from the adjacent lane (DPP wave_shl:1 / wave_shr:1);
+//   * the per-row metrics of the compact tables are wave-uniform (scalar loads).
+// Four waves of a workgroup sit side by side (248 output columns); XCD-banded tile order as
+// k_range.  Whole waves stay active through the loop (the lane shifts need every lane).
+constexpr int kMarchCols = 62;
+#ifndef OCN_MARCH_ROWS
+#define OCN_MARCH_ROWS 16
+#endif
+
+__device__ __forceinline__ double lane_shift(double x, int dx)   // x of lane + dx, dx in {-1, 0, 1}
+{
+    if (dx == 0) return x;
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    if (dx > 0) {   // wave_shl:1: lane i <- lane i+1
+        lo = __builtin_amdgcn_mov_dpp(lo, 0x130, 0xf, 0xf, false);
+        hi = __builtin_amdgcn_mov_dpp(hi, 0x130, 0xf, 0xf, false);
+    } else {        // wave_shr:1: lane i <- lane i-1
+        lo = __builtin_amdgcn_mov_dpp(lo, 0x138, 0xf, 0xf, false);
+        hi = __builtin_amdgcn_mov_dpp(hi, 0x138, 0xf, 0xf, false);
+    }
+    return __hiloint2double(hi, lo);
+}
+
+// Never defined: a view access outside the rows a march keeps fails to link.
+extern "C" __device__ void ocn_march_bad_access();
+
+// rows n-1 (s), n (c), n+1 (nn) of one r8 array at this lane's column; S / N: whether s / nn are kept
+template <bool S, bool N> struct Rows {
+    double s, c, nn;
+    __device__ __forceinline__ double at(int dx, int dy) const
+    {
+        if ((dy < 0 && !S) || (dy > 0 && !N) || dy < -1 || dy > 1) ocn_march_bad_access();
+        return lane_shift(dy < 0 ? s : dy == 0 ? c : nn, dx);
+    }
+    __device__ __forceinline__ void rotate() { s = c; c = nn; }
+};
+
+// value of an array read only at (m, n)
+struct Here {
+    double v;
+    __device__ __forceinline__ double at(int dx, int dy) const
+    {
+        if (dx != 0 || dy != 0) ocn_march_bad_access();
+        return v;
+    }
+};
+
+template <class Body>
+__global__ __launch_bounds__(256) void k_march(int m0, int m1, int n0, int n1, int ntx, int ntiles, Body body)
+{
+    int tile = (int)blockIdx.x;
+#if OCN_XCD_REMAP
+    const int per = (ntiles + 7) / 8;
+    tile = (tile % 8) * per + tile / 8;
+    if (tile >= ntiles) return;
+#endif
+    const int tx = tile % ntx, ty = tile / ntx;
+    const int lane = (int)threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int mw = m0 + (tx * 4 + wave) * kMarchCols;   // first output column of this wave
+    if (mw > m1) return;                                 // wave-uniform
+    const int m = mw - 1 + lane;                         // loaded column (m1 + 1 at most is read)
+    const bool out = lane >= 1 && lane <= kMarchCols && m <= m1;
+    const int nb = n0 + ty * OCN_MARCH_ROWS, ne = min(n1, nb + OCN_MARCH_ROWS - 1);
+    body.march(min(m, m1 + 1), out, nb, ne);
+}
+
+template <typename Body>
+static int launch_march(int m0, int m1, int n0, int n1, const Body &body, hipStream_t s)
+{
+    if (m1 < m0 || n1 < n0) return OCN_OK;
+    const int wg_cols = 4 * kMarchCols;
+    const int ntx = (m1 - m0 + wg_cols) / wg_cols, nty = (n1 - n0 + OCN_MARCH_ROWS) / OCN_MARCH_ROWS;
+    const int ntiles = ntx * nty;
+    const int nblocks = OCN_XCD_REMAP ? 8 * ((ntiles + 7) / 8) : ntiles;
+    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, m0, m1, n0, n1, ntx, ntiles, body);
+    return check_launch();
+}
+
+// The view of fused B's three stages (sw_stencils.h uv_trans_math / uv_diff2_math /
+// sw_update_uv_math) over the march registers.  Accessor names follow the stage functors; an
+// array named twice there (u = ubrtr, hu = hhu, hh = hhh) is one register set here.
+struct MarchViewB {
+    Rows<true, true> rU, rV, rHV, rMU;                 // ubrtr, vbrtr, hhv, mu
+    Rows<false, true> rHU, rHQ, rSTT, rSSH;            // hhu, hhq, str_t, ssh
+    Rows<true, false> rVORT, rHH, rSTS;                // vort, hhh, str_s
+    Here hhun_, hhup_, hhvn_, hhvp_, ubrtrp_, vbrtrp_, rhsx_, rhsy_;
+    unsigned bits_s, bits_c;                           // mask bytes at (m, n-1), (m, n)
+    float g[kNumRowFields][3];                         // metric rows n-1, n, n+1 (compact tables)
+    double tau;
+    __device__ __forceinline__ double quot(double a, double b, int, int) const { return a / b; }
+    __device__ __forceinline__ double qtau(double a) const { return a / tau; }
+#define OCN_MV(name, reg) \
+    __device__ __forceinline__ double name(int dx, int dy) const { return reg.at(dx, dy); }
+    OCN_MV(u, rU) OCN_MV(ubrtr, rU) OCN_MV(v, rV) OCN_MV(vbrtr, rV) OCN_MV(hu, rHU) OCN_MV(hhu, rHU)
+    OCN_MV(hv, rHV) OCN_MV(hhv, rHV) OCN_MV(hh, rHH) OCN_MV(hhh, rHH) OCN_MV(mu, rMU) OCN_MV(hq, rHQ)
+    OCN_MV(vort, rVORT) OCN_MV(str_t, rSTT) OCN_MV(str_s, rSTS) OCN_MV(ssh, rSSH)
+    OCN_MV(hhun, hhun_) OCN_MV(hhup, hhup_) OCN_MV(hhvn, hhvn_) OCN_MV(hhvp, hhvp_) OCN_MV(ubrtrp, ubrtrp_)
+    OCN_MV(vbrtrp, vbrtrp_) OCN_MV(RHSx, rhsx_) OCN_MV(RHSy, rhsy_)
+#undef OCN_MV
+#define OCN_MG(name, id) \
+    __device__ __forceinline__ float name(int, int dy) const { return g[id - OCN_DX][dy + 1]; }
+    OCN_MG(dx, OCN_DX) OCN_MG(dy, OCN_DY) OCN_MG(dxt, OCN_DXT) OCN_MG(dyt, OCN_DYT) OCN_MG(dxh, OCN_DXH)
+    OCN_MG(dyh, OCN_DYH) OCN_MG(dxb, OCN_DXB) OCN_MG(dyb, OCN_DYB) OCN_MG(rlh_s, OCN_RLH_S) OCN_MG(rdis, OCN_R_DISS)
+#undef OCN_MG
+    __device__ __forceinline__ float luu(int dx, int dy) const
+    {
+        if (dx != 0 || dy < -1 || dy > 0) ocn_march_bad_access();
+        return ((dy < 0 ? bits_s : bits_c) & (1u << OCN_LUU)) ? 1.0f : 0.0f;
+    }
+};
+
+// fused B (sw_stencils.h FusedB) as a register march; compact static fields only
+struct MarchFusedB {
+    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; bool full, reuse;
+    __device__ void march(int m, bool out, int nb, int ne) const
+    {
+        const FusedB<true> k = make_fused_b(&b, t, sw, tau, full, reuse);
+        const UvTrans<true> &a4 = k.a4;
+        const UvDiff2<true> &a6 = k.a6;
+        const SwUpdateUv<true> &a7 = k.a7;
+        const Geo I = a7.I;
+        const unsigned nrows = t.nrows;
+        auto row_met = [&](int id, int n) { return t.rows[(unsigned)(id - OCN_DX) * nrows + (unsigned)(n - b.bnd_y1)]; };
+        MarchViewB x;
+        x.tau = tau;
+        {
+            const Pt s = I(m, nb - 1), c = I(m, nb);
+            x.rU.s = ld(a7.ubrtr, s); x.rU.c = ld(a7.ubrtr, c);
+            x.rV.s = ld(a7.vbrtr, s); x.rV.c = ld(a7.vbrtr, c);
+            x.rHV.s = ld(a7.hhv, s); x.rHV.c = ld(a7.hhv, c);
+            x.rMU.s = ld(a6.mu, s); x.rMU.c = ld(a6.mu, c);
+            x.rHU.c = ld(a7.hhu, c); x.rHQ.c = ld(a6.hq, c); x.rSTT.c = ld(a6.str_t, c); x.rSSH.c = ld(a7.ssh, c);
+            x.rVORT.c = ld(a4.vort, s); x.rHH.c = ld(a7.hhh, s); x.rSTS.c = ld(a6.str_s, s);
+            x.bits_c = ld(t.bits, s);
+            for (int id = OCN_DX; id < OCN_NUM_R4; ++id) {
+                x.g[id - OCN_DX][1] = row_met(id, nb - 1);
+                x.g[id - OCN_DX][2] = row_met(id, nb);
+            }
+        }
+        for (int n = nb; n <= ne; ++n) {
+            const Pt c = I(m, n), cn = I(m, n + 1);
+            // rotate the rows kept at n-1 / n; load row n+1 (or n)
+            x.rVORT.s = x.rVORT.c; x.rHH.s = x.rHH.c; x.rSTS.s = x.rSTS.c; x.bits_s = x.bits_c;
+            for (int r = 0; r < kNumRowFields; ++r) { x.g[r][0] = x.g[r][1]; x.g[r][1] = x.g[r][2]; }
+            x.rU.nn = ld(a7.ubrtr, cn); x.rV.nn = ld(a7.vbrtr, cn); x.rHV.nn = ld(a7.hhv, cn); x.rMU.nn = ld(a6.mu, cn);
+            x.rHU.nn = ld(a7.hhu, cn); x.rHQ.nn = ld(a6.hq, cn); x.rSTT.nn = ld(a6.str_t, cn); x.rSSH.nn = ld(a7.ssh, cn);
+            x.rVORT.c = ld(a4.vort, c); x.rHH.c = ld(a7.hhh, c); x.rSTS.c = ld(a6.str_s, c);
+            x.bits_c = ld(t.bits, c);
+            for (int id = OCN_DX; id < OCN_NUM_R4; ++id) x.g[id - OCN_DX][2] = row_met(id, n + 1);
+            x.hhun_.v = ld(a7.hhun, c); x.hhup_.v = ld(a7.hhup, c); x.hhvn_.v = ld(a7.hhvn, c);
+            x.hhvp_.v = ld(a7.hhvp, c); x.ubrtrp_.v = ld(a7.ubrtrp, c); x.vbrtrp_.v = ld(a7.vbrtrp, c);
+            x.rhsx_.v = ld(a7.RHSx, c); x.rhsy_.v = ld(a7.RHSy, c);
+
+            double rxa, rya, rxd, ryd;
+            if (k.do_adv) uv_trans_math(x, rxa, rya);
+            else { rxa = ld(a7.RHSx_adv, c); rya = ld(a7.RHSy_adv, c); }
+            if (k.do_dif) uv_diff2_math(x, rxd, ryd);
+            else { rxd = ld(a7.RHSx_dif, c); ryd = ld(a7.RHSy_dif, c); }
+            double un, vn;
+            sw_update_uv_math(x, rxa, rxd, rya, ryd, un, vn);
+            if (out) {
+                if (x.bits_c & (1u << OCN_LCU)) {
+                    if (k.do_adv && k.full) st(a4.RHSx, c, rxa);
+                    if (k.do_dif && k.full) st(a6.RHSx, c, rxd);
+                    st(a7.ubrtrn, c, un);
+                }
+                if (x.bits_c & (1u << OCN_LCV)) {
+                    if (k.do_adv && k.full) st(a4.RHSy, c, rya);
+                    if (k.do_dif && k.full) st(a6.RHSy, c, ryd);
+                    st(a7.vbrtrn, c, vn);
+                }
+            }
+            x.rU.rotate(); x.rV.rotate(); x.rHV.rotate(); x.rMU.rotate();
+            x.rHU.rotate(); x.rHQ.rotate(); x.rSTT.rotate(); x.rSSH.rotate();
+        }
+    }
+};
+
 #define CHECK(...)                                                \
     do {                                                          \
         int _rc = check_block(b);                                 \
@@ -152,6 +340,13 @@ int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s)
 {
+    if (cp && cp->march && part != OCN_PART_FRAME) {
+        RC_K(check_block(b));
+        const Range r = part == OCN_PART_INNER ? range_clip(range_interior(b), inner_interior_shrunk(b))
+                                               : range_interior(b);
+        const MarchFusedB k{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0), sw, tau, full, reuse};
+        return launch_march(r.m0, r.m1, r.n0, r.n1, k, s);
+    }
     return launch_fused<KFusedB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s, sw, tau,
                                  full, reuse);
 }

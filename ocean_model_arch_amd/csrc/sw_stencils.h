@@ -52,6 +52,11 @@ struct Geo {
     OCN_HD OCN_INLINE Pt w(Pt q) const { return Pt{q.c - 1, q.r}; }
     OCN_HD OCN_INLINE Pt n(Pt q) const { return Pt{q.c + p, q.r + 1}; }
     OCN_HD OCN_INLINE Pt s(Pt q) const { return Pt{q.c - p, q.r - 1}; }
+    // A(m + dx, n + dy) for constant dx, dy (folded after inlining)
+    OCN_HD OCN_INLINE Pt at(Pt q, int dx, int dy) const
+    {
+        return Pt{q.c + (unsigned)dx + (unsigned)dy * p, q.r + (unsigned)dy};
+    }
 };
 
 #define D(x) ((double)(x))
@@ -242,40 +247,61 @@ template <bool C> struct UvTransVort {
     }
 };
 
+// ------------------------------------------------------------------ views
+// The arithmetic of the stages fused into launch B (a4, a6, a7) is written against a "view"
+// x: x.u(dx, dy) is u(m+dx, n+dy) of the reference loop, x.dyh(dx, dy) the real(4) metric
+// there, x.quot(a, b, id, dy) = a / b for b = D(metric id at row n+dy), x.qtau(a) = a / tau.
+// The pointer views below load every operand from its block array (the stage kernels, the
+// k_range fused kernel and the host harness); the register march of sw_kernels.hip supplies
+// the same values from registers.  Same expressions, same evaluation order, same results.
+#define OCN_VIEW_LD(name) \
+    OCN_HD OCN_INLINE auto name(int dx, int dy) const { return ld(k.name, k.I.at(c, dx, dy)); }
+#define OCN_VIEW_PTR_COMMON(K)                                                                         \
+    const K &k; Pt c;                                                                                  \
+    OCN_HD OCN_INLINE double quot(double a, double b, int, int) const { return a / b; }
+
 // ------------------------------------------------------------------ a4 uv_trans
 // vel_ssh.f90:283-373
+template <class X> OCN_HD OCN_INLINE void uv_trans_math(const X &x, double &rx, double &ry)
+{
+    {
+        const double fu_c = x.u(0, 0) * D(x.dyh(0, 0)) * x.hu(0, 0);
+        const double fx_p = (fu_c + x.u(1, 0) * D(x.dyh(1, 0)) * x.hu(1, 0)) / 2.0 * (x.u(0, 0) + x.u(1, 0)) / 2.0;
+        const double fx_m = (fu_c + x.u(-1, 0) * D(x.dyh(-1, 0)) * x.hu(-1, 0)) / 2.0 * (x.u(0, 0) + x.u(-1, 0)) / 2.0;
+        const double fy_p = (x.v(0, 0) * D(x.dxh(0, 0)) * x.hv(0, 0) + x.v(1, 0) * D(x.dxh(1, 0)) * x.hv(1, 0)) / 2.0
+                            * (x.u(0, 1) + x.u(0, 0)) / 2.0 * D(x.luu(0, 0));
+        const double fy_m = (x.v(0, -1) * D(x.dxh(0, -1)) * x.hv(0, -1) + x.v(1, -1) * D(x.dxh(1, -1)) * x.hv(1, -1)) / 2.0
+                            * (x.u(0, -1) + x.u(0, 0)) / 2.0 * D(x.luu(0, -1));
+        rx = -(fx_p - fx_m + fy_p - fy_m)
+             + (x.vort(0, 0) * x.hh(0, 0) * (x.v(1, 0) + x.v(0, 0))
+                + x.vort(0, -1) * x.hh(0, -1) * (x.v(1, -1) + x.v(0, -1))) / 4.0;
+    }
+    {
+        const double fv_c = x.v(0, 0) * D(x.dxh(0, 0)) * x.hv(0, 0);
+        const double fy_p = (fv_c + x.v(0, 1) * D(x.dxh(0, 1)) * x.hv(0, 1)) / 2.0 * (x.v(0, 0) + x.v(0, 1)) / 2.0;
+        const double fy_m = (fv_c + x.v(0, -1) * D(x.dxh(0, -1)) * x.hv(0, -1)) / 2.0 * (x.v(0, 0) + x.v(0, -1)) / 2.0;
+        const double fx_p = (x.u(0, 0) * D(x.dyh(0, 0)) * x.hu(0, 0) + x.u(0, 1) * D(x.dyh(0, 1)) * x.hu(0, 1)) / 2.0
+                            * (x.v(1, 0) + x.v(0, 0)) / 2.0;
+        const double fx_m = (x.u(-1, 0) * D(x.dyh(-1, 0)) * x.hu(-1, 0) + x.u(-1, 1) * D(x.dyh(-1, 1)) * x.hu(-1, 1)) / 2.0
+                            * (x.v(-1, 0) + x.v(0, 0)) / 2.0;
+        ry = -(fx_p - fx_m + fy_p - fy_m)
+             - (x.vort(0, 0) * x.hh(0, 0) * (x.u(0, 1) + x.u(0, 0))
+                + x.vort(-1, 0) * x.hh(-1, 0) * (x.u(-1, 1) + x.u(-1, 0))) / 4.0;
+    }
+}
+
 template <bool C> struct UvTrans {
     Geo I;
     Msk<C> lcu, lcv, luu; Met<C> dxh, dyh;
     const double *__restrict__ u, *__restrict__ v, *__restrict__ vort;
     const double *__restrict__ hu, *__restrict__ hv, *__restrict__ hh;
     double *__restrict__ RHSx, *__restrict__ RHSy;
-    OCN_HD OCN_INLINE void eval(Pt c, double &rx, double &ry) const
-    {
-        const Pt e = I.e(c), w = I.w(c), nn = I.n(c), s = I.s(c), se = I.e(s), wn = I.w(nn);
-        {
-            const double fu_c = ld(u, c) * D(ld(dyh, c)) * ld(hu, c);
-            const double fx_p = (fu_c + ld(u, e) * D(ld(dyh, e)) * ld(hu, e)) / 2.0 * (ld(u, c) + ld(u, e)) / 2.0;
-            const double fx_m = (fu_c + ld(u, w) * D(ld(dyh, w)) * ld(hu, w)) / 2.0 * (ld(u, c) + ld(u, w)) / 2.0;
-            const double fy_p = (ld(v, c) * D(ld(dxh, c)) * ld(hv, c) + ld(v, e) * D(ld(dxh, e)) * ld(hv, e)) / 2.0
-                                * (ld(u, nn) + ld(u, c)) / 2.0 * D(ld(luu, c));
-            const double fy_m = (ld(v, s) * D(ld(dxh, s)) * ld(hv, s) + ld(v, se) * D(ld(dxh, se)) * ld(hv, se)) / 2.0
-                                * (ld(u, s) + ld(u, c)) / 2.0 * D(ld(luu, s));
-            rx = -(fx_p - fx_m + fy_p - fy_m)
-                 + (ld(vort, c) * ld(hh, c) * (ld(v, e) + ld(v, c)) + ld(vort, s) * ld(hh, s) * (ld(v, se) + ld(v, s))) / 4.0;
-        }
-        {
-            const double fv_c = ld(v, c) * D(ld(dxh, c)) * ld(hv, c);
-            const double fy_p = (fv_c + ld(v, nn) * D(ld(dxh, nn)) * ld(hv, nn)) / 2.0 * (ld(v, c) + ld(v, nn)) / 2.0;
-            const double fy_m = (fv_c + ld(v, s) * D(ld(dxh, s)) * ld(hv, s)) / 2.0 * (ld(v, c) + ld(v, s)) / 2.0;
-            const double fx_p = (ld(u, c) * D(ld(dyh, c)) * ld(hu, c) + ld(u, nn) * D(ld(dyh, nn)) * ld(hu, nn)) / 2.0
-                                * (ld(v, e) + ld(v, c)) / 2.0;
-            const double fx_m = (ld(u, w) * D(ld(dyh, w)) * ld(hu, w) + ld(u, wn) * D(ld(dyh, wn)) * ld(hu, wn)) / 2.0
-                                * (ld(v, w) + ld(v, c)) / 2.0;
-            ry = -(fx_p - fx_m + fy_p - fy_m)
-                 - (ld(vort, c) * ld(hh, c) * (ld(u, nn) + ld(u, c)) + ld(vort, w) * ld(hh, w) * (ld(u, wn) + ld(u, w))) / 4.0;
-        }
-    }
+    struct View {
+        OCN_VIEW_PTR_COMMON(UvTrans)
+        OCN_VIEW_LD(u) OCN_VIEW_LD(v) OCN_VIEW_LD(vort) OCN_VIEW_LD(hu) OCN_VIEW_LD(hv) OCN_VIEW_LD(hh)
+        OCN_VIEW_LD(dxh) OCN_VIEW_LD(dyh) OCN_VIEW_LD(luu)
+    };
+    OCN_HD OCN_INLINE void eval(Pt c, double &rx, double &ry) const { uv_trans_math(View{*this, c}, rx, ry); }
     OCN_HD void operator()(int m, int n) const
     {
         const Pt c = I(m, n);
@@ -311,31 +337,42 @@ template <bool C> struct StressComponents {
 
 // ------------------------------------------------------------------ a6 uv_diff2
 // vel_ssh.f90:375-452
+template <class X> OCN_HD OCN_INLINE void uv_diff2_math(const X &x, double &rx, double &ry)
+{
+    {
+        const double muh_p = (x.mu(0, 0) + x.mu(1, 0) + x.mu(0, 1) + x.mu(1, 1)) / 4.0;
+        const double muh_m = (x.mu(0, 0) + x.mu(1, 0) + x.mu(0, -1) + x.mu(1, -1)) / 4.0;
+        const float dy2p = x.dy(1, 0) * x.dy(1, 0), dy2 = x.dy(0, 0) * x.dy(0, 0);
+        const float dxb2 = x.dxb(0, 0) * x.dxb(0, 0), dxb2m = x.dxb(0, -1) * x.dxb(0, -1);
+        rx = x.quot(D(dy2p) * x.mu(1, 0) * x.hq(1, 0) * x.str_t(1, 0) - D(dy2) * x.mu(0, 0) * x.hq(0, 0) * x.str_t(0, 0),
+                    D(x.dyh(0, 0)), OCN_DYH, 0)
+             + x.quot(D(dxb2) * muh_p * x.hh(0, 0) * x.str_s(0, 0) - D(dxb2m) * muh_m * x.hh(0, -1) * x.str_s(0, -1),
+                      D(x.dxt(0, 0)), OCN_DXT, 0);
+    }
+    {
+        const double muh_p = (x.mu(0, 0) + x.mu(1, 0) + x.mu(0, 1) + x.mu(1, 1)) / 4.0;
+        const double muh_m = (x.mu(0, 0) + x.mu(-1, 0) + x.mu(0, 1) + x.mu(-1, 1)) / 4.0;
+        const float dx2p = x.dx(0, 1) * x.dx(0, 1), dx2 = x.dx(0, 0) * x.dx(0, 0);
+        const float dyb2 = x.dyb(0, 0) * x.dyb(0, 0), dyb2m = x.dyb(-1, 0) * x.dyb(-1, 0);
+        ry = x.quot(-(D(dx2p) * x.mu(0, 1) * x.hq(0, 1) * x.str_t(0, 1) - D(dx2) * x.mu(0, 0) * x.hq(0, 0) * x.str_t(0, 0)),
+                    D(x.dxh(0, 0)), OCN_DXH, 0)
+             + x.quot(D(dyb2) * muh_p * x.hh(0, 0) * x.str_s(0, 0) - D(dyb2m) * muh_m * x.hh(-1, 0) * x.str_s(-1, 0),
+                      D(x.dyt(0, 0)), OCN_DYT, 0);
+    }
+}
+
 template <bool C> struct UvDiff2 {
     Geo I;
     Msk<C> lcu, lcv; Met<C> dx, dy, dxt, dyt, dxh, dyh, dxb, dyb;
     const double *__restrict__ mu, *__restrict__ str_t, *__restrict__ str_s, *__restrict__ hq, *__restrict__ hh;
     double *__restrict__ RHSx, *__restrict__ RHSy;
-    OCN_HD OCN_INLINE void eval(Pt c, double &rx, double &ry) const
-    {
-        const Pt e = I.e(c), nn = I.n(c), ne = I.e(nn), s = I.s(c), se = I.e(s), w = I.w(c), wn = I.w(nn);
-        {
-            const double muh_p = (ld(mu, c) + ld(mu, e) + ld(mu, nn) + ld(mu, ne)) / 4.0;
-            const double muh_m = (ld(mu, c) + ld(mu, e) + ld(mu, s) + ld(mu, se)) / 4.0;
-            const float dy2p = ld(dy, e) * ld(dy, e), dy2 = ld(dy, c) * ld(dy, c);
-            const float dxb2 = ld(dxb, c) * ld(dxb, c), dxb2m = ld(dxb, s) * ld(dxb, s);
-            rx = (D(dy2p) * ld(mu, e) * ld(hq, e) * ld(str_t, e) - D(dy2) * ld(mu, c) * ld(hq, c) * ld(str_t, c)) / D(ld(dyh, c))
-                 + (D(dxb2) * muh_p * ld(hh, c) * ld(str_s, c) - D(dxb2m) * muh_m * ld(hh, s) * ld(str_s, s)) / D(ld(dxt, c));
-        }
-        {
-            const double muh_p = (ld(mu, c) + ld(mu, e) + ld(mu, nn) + ld(mu, ne)) / 4.0;
-            const double muh_m = (ld(mu, c) + ld(mu, w) + ld(mu, nn) + ld(mu, wn)) / 4.0;
-            const float dx2p = ld(dx, nn) * ld(dx, nn), dx2 = ld(dx, c) * ld(dx, c);
-            const float dyb2 = ld(dyb, c) * ld(dyb, c), dyb2m = ld(dyb, w) * ld(dyb, w);
-            ry = -(D(dx2p) * ld(mu, nn) * ld(hq, nn) * ld(str_t, nn) - D(dx2) * ld(mu, c) * ld(hq, c) * ld(str_t, c)) / D(ld(dxh, c))
-                 + (D(dyb2) * muh_p * ld(hh, c) * ld(str_s, c) - D(dyb2m) * muh_m * ld(hh, w) * ld(str_s, w)) / D(ld(dyt, c));
-        }
-    }
+    struct View {
+        OCN_VIEW_PTR_COMMON(UvDiff2)
+        OCN_VIEW_LD(mu) OCN_VIEW_LD(str_t) OCN_VIEW_LD(str_s) OCN_VIEW_LD(hq) OCN_VIEW_LD(hh)
+        OCN_VIEW_LD(dx) OCN_VIEW_LD(dy) OCN_VIEW_LD(dxt) OCN_VIEW_LD(dyt) OCN_VIEW_LD(dxh) OCN_VIEW_LD(dyh)
+        OCN_VIEW_LD(dxb) OCN_VIEW_LD(dyb)
+    };
+    OCN_HD OCN_INLINE void eval(Pt c, double &rx, double &ry) const { uv_diff2_math(View{*this, c}, rx, ry); }
     OCN_HD void operator()(int m, int n) const
     {
         const Pt c = I(m, n);
@@ -347,7 +384,38 @@ template <bool C> struct UvDiff2 {
 };
 
 // ------------------------------------------------------------------ a7 sw_update_uv
-// vel_ssh.f90:108-195
+// vel_ssh.f90:108-195.  rxa/rxd/rya/ryd: RHSx_adv, RHSx_dif, RHSy_adv, RHSy_dif at this point.
+template <class X>
+OCN_HD OCN_INLINE void sw_update_uv_math(const X &x, double rxa, double rxd, double rya, double ryd, double &un,
+                                         double &vn)
+{
+    const double g = D(OCN_FREE_FALL_ACC);
+    {
+        const double bp = x.qtau(x.hhun(0, 0) * D(x.dxt(0, 0)) * D(x.dyh(0, 0)) / 2.0);
+        const double bp0 = x.qtau(x.hhup(0, 0) * D(x.dxt(0, 0)) * D(x.dyh(0, 0)) / 2.0);
+        const double slx = -(g * (x.ssh(1, 0) - x.ssh(0, 0)) * D(x.dyh(0, 0)) * x.hhu(0, 0));
+        const float rd = x.rdis(0, 0) + x.rdis(1, 0);
+        const double fric = D(rd) / 2.0 * x.ubrtrp(0, 0) * D(x.dxt(0, 0)) * D(x.dyh(0, 0)) * x.hhu(0, 0);
+        const double c1 = D(x.rlh_s(0, 0)) * x.hhh(0, 0) * D(x.dxb(0, 0)) * D(x.dyb(0, 0)) * (x.vbrtr(1, 0) + x.vbrtr(0, 0));
+        const double c2 = D(x.rlh_s(0, -1)) * x.hhh(0, -1) * D(x.dxb(0, -1)) * D(x.dyb(0, -1))
+                          * (x.vbrtr(1, -1) + x.vbrtr(0, -1));
+        const double grx = x.RHSx(0, 0) + slx + rxd + rxa - fric + (c1 + c2) / 4.0;
+        un = (x.ubrtrp(0, 0) * bp0 + grx) / (bp);
+    }
+    {
+        const double bp = x.qtau(x.hhvn(0, 0) * D(x.dyt(0, 0)) * D(x.dxh(0, 0)) / 2.0);
+        const double bp0 = x.qtau(x.hhvp(0, 0) * D(x.dyt(0, 0)) * D(x.dxh(0, 0)) / 2.0);
+        const double sly = -(g * (x.ssh(0, 1) - x.ssh(0, 0)) * D(x.dxh(0, 0)) * x.hhv(0, 0));
+        const float rd = x.rdis(0, 0) + x.rdis(0, 1);
+        const double fric = D(rd) / 2.0 * x.vbrtrp(0, 0) * D(x.dxh(0, 0)) * D(x.dyt(0, 0)) * x.hhv(0, 0);
+        const double c1 = D(x.rlh_s(0, 0)) * x.hhh(0, 0) * D(x.dxb(0, 0)) * D(x.dyb(0, 0)) * (x.ubrtr(0, 1) + x.ubrtr(0, 0));
+        const double c2 = D(x.rlh_s(-1, 0)) * x.hhh(-1, 0) * D(x.dxb(-1, 0)) * D(x.dyb(-1, 0))
+                          * (x.ubrtr(-1, 1) + x.ubrtr(-1, 0));
+        const double gry = x.RHSy(0, 0) + sly + ryd + rya - fric - (c1 + c2) / 4.0;
+        vn = (x.vbrtrp(0, 0) * bp0 + gry) / (bp);
+    }
+}
+
 template <bool C> struct SwUpdateUv {
     Geo I; double tau;
     Msk<C> lcu, lcv; Met<C> dxt, dyt, dxh, dyh, dxb, dyb;
@@ -359,33 +427,18 @@ template <bool C> struct SwUpdateUv {
     Met<C> rdis, rlh_s;
     const double *__restrict__ RHSx, *__restrict__ RHSy, *__restrict__ RHSx_adv, *__restrict__ RHSy_adv;
     const double *__restrict__ RHSx_dif, *__restrict__ RHSy_dif;
-    // rxa/rxd/rya/ryd: RHSx_adv, RHSx_dif, RHSy_adv, RHSy_dif at this point
+    struct View {
+        OCN_VIEW_PTR_COMMON(SwUpdateUv)
+        OCN_HD OCN_INLINE double qtau(double a) const { return a / k.tau; }
+        OCN_VIEW_LD(hhu) OCN_VIEW_LD(hhun) OCN_VIEW_LD(hhup) OCN_VIEW_LD(hhv) OCN_VIEW_LD(hhvn) OCN_VIEW_LD(hhvp)
+        OCN_VIEW_LD(hhh) OCN_VIEW_LD(ssh) OCN_VIEW_LD(ubrtr) OCN_VIEW_LD(ubrtrp) OCN_VIEW_LD(vbrtr) OCN_VIEW_LD(vbrtrp)
+        OCN_VIEW_LD(RHSx) OCN_VIEW_LD(RHSy)
+        OCN_VIEW_LD(dxt) OCN_VIEW_LD(dyt) OCN_VIEW_LD(dxh) OCN_VIEW_LD(dyh) OCN_VIEW_LD(dxb) OCN_VIEW_LD(dyb)
+        OCN_VIEW_LD(rdis) OCN_VIEW_LD(rlh_s)
+    };
     OCN_HD OCN_INLINE void eval(Pt c, double rxa, double rxd, double rya, double ryd, double &un, double &vn) const
     {
-        const double g = D(OCN_FREE_FALL_ACC);
-        const Pt e = I.e(c), s = I.s(c), se = I.e(s), nn = I.n(c), w = I.w(c), wn = I.w(nn);
-        {
-            const double bp = ld(hhun, c) * D(ld(dxt, c)) * D(ld(dyh, c)) / 2.0 / tau;
-            const double bp0 = ld(hhup, c) * D(ld(dxt, c)) * D(ld(dyh, c)) / 2.0 / tau;
-            const double slx = -(g * (ld(ssh, e) - ld(ssh, c)) * D(ld(dyh, c)) * ld(hhu, c));
-            const float rd = ld(rdis, c) + ld(rdis, e);
-            const double fric = D(rd) / 2.0 * ld(ubrtrp, c) * D(ld(dxt, c)) * D(ld(dyh, c)) * ld(hhu, c);
-            const double c1 = D(ld(rlh_s, c)) * ld(hhh, c) * D(ld(dxb, c)) * D(ld(dyb, c)) * (ld(vbrtr, e) + ld(vbrtr, c));
-            const double c2 = D(ld(rlh_s, s)) * ld(hhh, s) * D(ld(dxb, s)) * D(ld(dyb, s)) * (ld(vbrtr, se) + ld(vbrtr, s));
-            const double grx = ld(RHSx, c) + slx + rxd + rxa - fric + (c1 + c2) / 4.0;
-            un = (ld(ubrtrp, c) * bp0 + grx) / (bp);
-        }
-        {
-            const double bp = ld(hhvn, c) * D(ld(dyt, c)) * D(ld(dxh, c)) / 2.0 / tau;
-            const double bp0 = ld(hhvp, c) * D(ld(dyt, c)) * D(ld(dxh, c)) / 2.0 / tau;
-            const double sly = -(g * (ld(ssh, nn) - ld(ssh, c)) * D(ld(dxh, c)) * ld(hhv, c));
-            const float rd = ld(rdis, c) + ld(rdis, nn);
-            const double fric = D(rd) / 2.0 * ld(vbrtrp, c) * D(ld(dxh, c)) * D(ld(dyt, c)) * ld(hhv, c);
-            const double c1 = D(ld(rlh_s, c)) * ld(hhh, c) * D(ld(dxb, c)) * D(ld(dyb, c)) * (ld(ubrtr, nn) + ld(ubrtr, c));
-            const double c2 = D(ld(rlh_s, w)) * ld(hhh, w) * D(ld(dxb, w)) * D(ld(dyb, w)) * (ld(ubrtr, wn) + ld(ubrtr, w));
-            const double gry = ld(RHSy, c) + sly + ryd + rya - fric - (c1 + c2) / 4.0;
-            vn = (ld(vbrtrp, c) * bp0 + gry) / (bp);
-        }
+        sw_update_uv_math(View{*this, c}, rxa, rxd, rya, ryd, un, vn);
     }
     OCN_HD void operator()(int m, int n) const
     {

@@ -139,6 +139,12 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_COMPACT, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_march(self, on: bool = True):
+        """Register-march form of the stencil launches that have one (default; needs the compact
+        static fields); same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MARCH, int(on)), "ocn_ctx_set_option")
+        return self
+
     def option(self, key: int) -> int:
         v = C.c_int64(0)
         check(lib().ocn_ctx_get_option(self.ctx, key, C.byref(v)), "ocn_ctx_get_option")

@@ -1,0 +1,53 @@
+"""HBM bytes per launch of the fused-step kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+over bench.py (scripts/pmc.sh), written as the JSON bench.py reads for roofline.traffic.
+
+    python scripts/pmc_traffic.py <pmc dir> <stenbench pmc dir> <cells> [--compact] > profiles/pmc_traffic.json
+
+FETCH_SIZE on gfx950 under-counts wide streaming reads (MI355X_MICROARCH.md 'HBM': half the
+bytes at 16 B/lane); our kernels read 8 B/lane.  The read scale is therefore calibrated on the
+stencil microbenchmark's pointwise kernel k_bench<0,0> (scripts/stenbench.hip), whose reads are
+exactly 20 arrays x 4094^2 x 8 B in the same 64 x 4-thread, 8-B-per-lane pattern.  WRITE_SIZE
+reads exactly for streaming stores.  Counter values are KiB."""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+STAGE = {"KFusedA": "fused_a", "KFusedB": "fused_b", "MarchFusedB": "fused_b", "KFusedC1": "fused_c1",
+         "KHhInit": "hh_init", "MarchHhInit": "hh_init", "MarchFusedA": "fused_a"}
+
+
+def means(root):
+    vals = defaultdict(lambda: defaultdict(list))
+    for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recursive=True):
+        for row in csv.DictReader(open(path)):
+            vals[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]) * 1024.0)
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in vals.items()}
+
+
+def main():
+    pmc, sten, cells = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    compact = "--compact" in sys.argv
+    cal = [v for k, v in means(sten).items() if "k_bench<0, 0>" in k][0]
+    exact_read = 20 * 4094 * 4094 * 8.0
+    scale = exact_read / cal["FETCH_SIZE"]
+    out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py; read scale {scale:.4f} "
+                     f"calibrated on stenbench k_bench<0,0> ({exact_read:.0f} B read exactly)",
+           "fetch_scale": scale, "kernels": {}}
+    for k, d in means(pmc).items():
+        m = re.search(r"ocn::(\w+)", k.replace("k_range<ocn::", "").replace("k_march<ocn::", ""))
+        name = m.group(1) if m else k
+        stage = STAGE.get(name)
+        if not stage or "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+            continue
+        rd, wr = d["FETCH_SIZE"] * scale, d["WRITE_SIZE"]
+        out["kernels"][stage] = {"kernel": name, "cells": cells, "compact": compact, "fetch_bytes": round(rd),
+                                 "write_bytes": round(wr), "hbm_bytes_per_launch": round(rd + wr)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

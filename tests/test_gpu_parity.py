@@ -111,7 +111,7 @@ def test_tracer_kernels_match_reference(amd, geom):
     assert not failures, f"{geom}: differs from the reference: {failures}"
 
 
-def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True):
+def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True, march=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"])
@@ -121,6 +121,7 @@ def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True):
     m.set_fused(fused)
     m.set_compact(compact)
     m.set_overlap(overlap)
+    m.set_march(march)
     if graph:
         m.set_graph(True)
     return m
@@ -143,17 +144,20 @@ def compare_case(m, case, name):
     return bad
 
 
-@pytest.mark.parametrize("mode", ["compact", "fused", "stages", "serial"])
+@pytest.mark.parametrize("mode", ["compact", "pointwise", "fused", "stages", "serial"])
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
-    """compact = the 4-launch step reading the compact static fields, halo exchanges overlapped
-    with inner launches when there are several blocks (the default); fused = the same on the 2-D
-    real(4) arrays; serial = compact without the overlap; stages = the reference's 11 envoke stages."""
+    """compact = the 4-launch step reading the compact static fields, fused B as a register
+    march, halo exchanges overlapped with inner launches when there are several blocks (the
+    default); pointwise = compact with every launch one thread per point; fused = the 4-launch
+    step on the 2-D real(4) arrays; serial = compact without the overlap; stages = the
+    reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    m = build_model(amd, case, fused=mode != "stages", compact=mode in ("compact", "serial"),
-                    overlap=mode != "serial")
+    compact = mode in ("compact", "serial", "pointwise")
+    m = build_model(amd, case, fused=mode != "stages", compact=compact, overlap=mode != "serial",
+                    march=mode != "pointwise")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
-    assert m.compact_active == (mode in ("compact", "serial"))
+    assert m.compact_active == compact
     bad = compare_case(m, case, name)
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
