@@ -308,8 +308,9 @@ static int allocate(ocn_ctx *c)
         const long n = (long)b.g.pitch * rows;
         // every field padded to a 256-B multiple, based so that A(nx_start, :) rows are
         // 256-B aligned: base offset shifted by (nx_start - bnd_x1) = 2 elements.
-        const long r8b = ((n * 8 + 16 + 255) / 256) * 256 + 256;
-        const long r4b = ((n * 4 + 8 + 255) / 256) * 256 + 256;
+        // OCN_FIELD_SKEW (bytes, multiple of 256): extra gap between consecutive fields
+        const long r8b = ((n * 8 + 16 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW;
+        const long r4b = ((n * 4 + 8 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW;
         const int nr8 = num_r8(c);
         const size_t total = (size_t)nr8 * r8b + (size_t)OCN_NUM_R4 * r4b + 256;
         HIPCHK(hipMalloc(&b.slab, total));

@@ -21,6 +21,11 @@
 #define OCN_WY (256 / OCN_TW)
 static_assert(OCN_TW % 64 == 0 && 256 % OCN_TW == 0, "OCN_TW must be 64, 128 or 256");
 
+#ifndef OCN_FIELD_SKEW
+#define OCN_FIELD_SKEW 0
+#endif
+static_assert(OCN_FIELD_SKEW % 256 == 0, "OCN_FIELD_SKEW must keep fields 256-B aligned");
+
 // Minimum waves per SIMD requested from the register allocator for the stencil kernels.
 #ifndef OCN_LB_WAVES
 #define OCN_LB_WAVES 1

@@ -99,45 +99,68 @@ static int launch_part(const Range &r, const Range &inner, int part, const Body 
 // (array, neighbour): fused B issues 76 per cell, and the L1/TA path -- not HBM -- limits it
 // (SQ_WAIT_INST_ANY ~70 % of wave time; profiles/r01b).  The march mapping loads each array
 // once per cell instead:
-//   * a wave owns 64 consecutive columns and marches down kMarchRows rows; lanes 1..62 produce
-//     output, lanes 0 and 63 only load the m-1 / m+1 neighbour columns;
+//   * a wave owns 64 consecutive columns and marches down OCN_MARCH_ROWS rows;
 //   * the n-1 / n / n+1 rows of an array stay in registers and rotate as the wave moves down, so
 //     each iteration loads only row n+1 (or row n for arrays read at n-1 and n);
 //   * m+1 / m-1 neighbours come from the adjacent lane (DPP wave_shl:1 / wave_shr:1);
 //   * the per-row metrics of the compact tables are wave-uniform (scalar loads).
-// Four waves of a workgroup sit side by side (248 output columns); XCD-banded tile order as
-// k_range.  Whole waves stay active through the loop (the lane shifts need every lane).
-constexpr int kMarchCols = 62;
+// Two lane layouts (Body::kAligned):
+//   * aligned: the 64 columns of a wave start on a 512-B boundary (A(nx_start + 64 j, n)) and all
+//     64 lanes produce output, so every store writes whole 128-B lines.  Lane 0's m-1 and lane
+//     63's m+1 neighbours come from one extra load per (array, row) with only those two lanes
+//     active ("edge" values, merged in by the DPP move's bound control).  Partial-line stores
+//     cost HBM bandwidth (scripts/mixbench.hip: write-only streams 5.3 TB/s aligned, 3.6 TB/s
+//     with 62-column waves offset by one column), so the store-heavy launches use this layout;
+//   * offset: lanes 1..62 produce output and lanes 0 / 63 only load the m-1 / m+1 columns (no
+//     edge loads, fewer registers; fused B, which stores two arrays).
+// Four waves of a workgroup sit side by side; XCD-banded tile order as k_range.  Whole waves
+// stay active through the loop (the lane shifts need every lane).
+constexpr int kMarchCols = 62;   // output columns of an offset-layout wave
 #ifndef OCN_MARCH_ROWS
-#define OCN_MARCH_ROWS 16
+#define OCN_MARCH_ROWS 8
 #endif
 
-__device__ __forceinline__ double lane_shift(double x, int dx)   // x of lane + dx, dx in {-1, 0, 1}
+// x of lane + dx (dx in {-1, 0, 1}); the lane without a source (0 for -1, 63 for +1) gets e
+__device__ __forceinline__ int dpp_shift(int x, int e, int dx)
+{
+    if (dx > 0) return __builtin_amdgcn_update_dpp(e, x, 0x130, 0xf, 0xf, false);   // wave_shl:1
+    return __builtin_amdgcn_update_dpp(e, x, 0x138, 0xf, 0xf, false);               // wave_shr:1
+}
+__device__ __forceinline__ double lane_shift(double x, double e, int dx)
 {
     if (dx == 0) return x;
-    int lo = __double2loint(x), hi = __double2hiint(x);
-    if (dx > 0) {   // wave_shl:1: lane i <- lane i+1
-        lo = __builtin_amdgcn_mov_dpp(lo, 0x130, 0xf, 0xf, false);
-        hi = __builtin_amdgcn_mov_dpp(hi, 0x130, 0xf, 0xf, false);
-    } else {        // wave_shr:1: lane i <- lane i-1
-        lo = __builtin_amdgcn_mov_dpp(lo, 0x138, 0xf, 0xf, false);
-        hi = __builtin_amdgcn_mov_dpp(hi, 0x138, 0xf, 0xf, false);
-    }
+    const int lo = dpp_shift(__double2loint(x), __double2loint(e), dx);
+    const int hi = dpp_shift(__double2hiint(x), __double2hiint(e), dx);
     return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ unsigned lane_shift(unsigned x, unsigned e, int dx)
+{
+    return dx == 0 ? x : (unsigned)dpp_shift((int)x, (int)e, dx);
 }
 
 // Never defined: a view access outside the rows a march keeps fails to link.
 extern "C" __device__ void ocn_march_bad_access();
 
-// rows n-1 (s), n (c), n+1 (nn) of one r8 array at this lane's column; S / N: whether s / nn are kept
-template <bool S, bool N> struct Rows {
-    double s, c, nn;
-    __device__ __forceinline__ double at(int dx, int dy) const
+// Rows n-1 (s), n (c), n+1 (nn) of one array at this lane's column; S / N: whether s / nn are
+// kept; E: the rows' edge values es / ec / enn are kept (aligned layout, arrays read at m+-1).
+template <class T, bool S, bool N, bool E = false> struct Rows {
+    T s, c, nn, es, ec, enn;
+    __device__ __forceinline__ T at(int dx, int dy) const
     {
         if ((dy < 0 && !S) || (dy > 0 && !N) || dy < -1 || dy > 1) ocn_march_bad_access();
-        return lane_shift(dy < 0 ? s : dy == 0 ? c : nn, dx);
+        const T v = dy < 0 ? s : dy == 0 ? c : nn;
+        const T e = dy < 0 ? es : dy == 0 ? ec : enn;
+        return lane_shift(v, E ? e : v, dx);
     }
-    __device__ __forceinline__ void rotate() { s = c; c = nn; }
+    __device__ __forceinline__ void rotate() { s = c; c = nn; es = ec; ec = enn; }
+};
+template <bool S, bool N, bool E = false> using RowsD = Rows<double, S, N, E>;
+// mask bytes of the compact tables: bit id of the byte
+template <bool S, bool N, bool E = false> struct BitRows : Rows<unsigned, S, N, E> {
+    __device__ __forceinline__ float mask(int id, int dx, int dy) const
+    {
+        return (this->at(dx, dy) >> id) & 1u ? 1.0f : 0.0f;
+    }
 };
 
 // value of an array read only at (m, n)
@@ -150,8 +173,53 @@ struct Here {
     }
 };
 
+// per-row metrics of the compact tables (wave-uniform) for rows n-1, n, n+1
+struct MetRows {
+    float g[kNumRowFields][3];
+    __device__ __forceinline__ float at(int id, int dy) const
+    {
+        if (dy < -1 || dy > 1) ocn_march_bad_access();
+        return g[id - OCN_DX][dy + 1];
+    }
+    // rows n-1 <- n <- n+1 = next (one value per metric field)
+    __device__ __forceinline__ void shift(const float *next)
+    {
+        for (int k = 0; k < kNumRowFields; ++k) { g[k][0] = g[k][1]; g[k][1] = g[k][2]; g[k][2] = next[k]; }
+    }
+    // rows n-1 and n before the first row of a march (table rows[(id - OCN_DX) * nrows + r])
+    __device__ __forceinline__ void preload(const float *rows, unsigned nrows, unsigned r_prev, unsigned r_cur)
+    {
+        for (int k = 0; k < kNumRowFields; ++k) {
+            g[k][1] = ld(rows, (unsigned)k * nrows + r_prev);
+            g[k][2] = ld(rows, (unsigned)k * nrows + r_cur);
+        }
+    }
+    __device__ __forceinline__ static void load(float *q, const float *rows, unsigned nrows, unsigned r)
+    {
+        for (int k = 0; k < kNumRowFields; ++k) q[k] = ld(rows, (unsigned)k * nrows + r);
+    }
+};
+#define OCN_MV(name, reg) \
+    __device__ __forceinline__ double name(int dx, int dy) const { return reg.at(dx, dy); }
+#define OCN_MG(name, id) \
+    __device__ __forceinline__ float name(int, int dy) const { return met.at(id, dy); }
+#define OCN_MG_ALL                                                                                         \
+    OCN_MG(dx, OCN_DX) OCN_MG(dy, OCN_DY) OCN_MG(dxt, OCN_DXT) OCN_MG(dyt, OCN_DYT) OCN_MG(dxh, OCN_DXH)     \
+    OCN_MG(dyh, OCN_DYH) OCN_MG(dxb, OCN_DXB) OCN_MG(dyb, OCN_DYB)
+
+// One lane of a march: its loaded column m, its edge column me (aligned layout: lane 0 m-1,
+// lane 63 m+1, both clamped into the block array), whether it is an edge lane, whether it
+// produces output.
+struct Lane { int m, me; bool edge, out; };
+
+// Loaded columns are clamped to [mlo, mhi] (inside the block array); a lane whose column was
+// clamped never produces output and its value is read by no output lane.
+#ifndef OCN_MARCH_LB
+#define OCN_MARCH_LB 1   // minimum waves per SIMD asked of the register allocator
+#endif
 template <class Body>
-__global__ __launch_bounds__(256) void k_march(int m0, int m1, int n0, int n1, int ntx, int ntiles, Body body)
+__global__ __launch_bounds__(256, OCN_MARCH_LB) void k_march(int m0, int m1, int n0, int n1, int w0, int ntx,
+                                                             int ntiles, int mlo, int mhi, Body body)
 {
     int tile = (int)blockIdx.x;
 #if OCN_XCD_REMAP
@@ -162,52 +230,90 @@ __global__ __launch_bounds__(256) void k_march(int m0, int m1, int n0, int n1, i
     const int tx = tile % ntx, ty = tile / ntx;
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int mw = m0 + (tx * 4 + wave) * kMarchCols;   // first output column of this wave
-    if (mw > m1) return;                                 // wave-uniform
-    const int m = mw - 1 + lane;                         // loaded column (m1 + 1 at most is read)
-    const bool out = lane >= 1 && lane <= kMarchCols && m <= m1;
+    constexpr int cols = Body::kAligned ? 64 : kMarchCols;
+    const int mw = w0 + (tx * 4 + wave) * cols;   // first output column of this wave
+    if (mw > m1) return;                          // wave-uniform
+    Lane L;
+    if (Body::kAligned) {
+        const int m = mw + lane;
+        L.out = m >= m0 && m <= m1;
+        L.m = min(max(m, mlo), mhi);
+        L.me = min(max(lane == 0 ? m - 1 : m + 1, mlo), mhi);
+        L.edge = lane == 0 || lane == 63;
+    } else {
+        const int m = mw - 1 + lane;
+        L.out = lane >= 1 && lane <= kMarchCols && m <= m1;
+        L.m = L.me = min(max(m, mlo), mhi);
+        L.edge = false;
+    }
     const int nb = n0 + ty * OCN_MARCH_ROWS, ne = min(n1, nb + OCN_MARCH_ROWS - 1);
-    body.march(min(m, m1 + 1), out, nb, ne);
+    body.march(L, nb, ne);
 }
 
 template <typename Body>
-static int launch_march(int m0, int m1, int n0, int n1, const Body &body, hipStream_t s)
+static int launch_march(const ocn_block *b, const Range &r, const Body &body, hipStream_t s)
 {
-    if (m1 < m0 || n1 < n0) return OCN_OK;
-    const int wg_cols = 4 * kMarchCols;
-    const int ntx = (m1 - m0 + wg_cols) / wg_cols, nty = (n1 - n0 + OCN_MARCH_ROWS) / OCN_MARCH_ROWS;
+    if (range_empty(r)) return OCN_OK;
+    int w0 = r.m0, cols = kMarchCols, mlo = max(r.m0 - 1, b->bnd_x1), mhi = min(r.m1 + 1, b->bnd_x2);
+    if (Body::kAligned) {   // waves start at nx_start + 64 j (256-B aligned rows, ocn_ctx.hip allocate)
+        const int d = r.m0 - b->nx_start;
+        w0 = b->nx_start + 64 * (d >= 0 ? d / 64 : -((63 - d) / 64));
+        cols = 64;
+        mlo = b->bnd_x1;
+        mhi = b->bnd_x2;
+    }
+    const int wg_cols = 4 * cols;
+    const int ntx = (r.m1 - w0 + wg_cols) / wg_cols, nty = (r.n1 - r.n0 + OCN_MARCH_ROWS) / OCN_MARCH_ROWS;
     const int ntiles = ntx * nty;
     const int nblocks = OCN_XCD_REMAP ? 8 * ((ntiles + 7) / 8) : ntiles;
-    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, m0, m1, n0, n1, ntx, ntiles, body);
+    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, r.m0, r.m1, r.n0, r.n1, w0, ntx,
+                       ntiles, mlo, mhi, body);
     return check_launch();
+}
+
+// Software pipelining of the marches (OCN_MARCH_PF = 1): the loads a row needs ("batch" of
+// row n: the arrays' row n+1 or n values, its mask bytes and metric row n+1) are issued one
+// iteration ahead, so a wave's loads for row n+1 are in flight while it computes row n.
+#ifndef OCN_MARCH_PF
+#define OCN_MARCH_PF 0
+#endif
+
+// The march loop shared by every march body F: F::Batch holds one row's loads, F::load fills it,
+// F::row consumes it (rotate the kept rows, compute, store).
+template <class F, class V>
+__device__ __forceinline__ void march_rows(const F &k, V &x, const Lane &L, int nb, int ne)
+{
+    typename F::Batch cur, nxt;
+    k.load(cur, L, nb);
+    for (int n = nb; n <= ne; ++n) {
+        if (OCN_MARCH_PF && n < ne) k.load(nxt, L, n + 1);   // wave-uniform branch
+        k.row(x, cur, L, n);
+        if (n < ne) {
+            if (!OCN_MARCH_PF) k.load(nxt, L, n + 1);
+            cur = nxt;
+        }
+    }
 }
 
 // The view of fused B's three stages (sw_stencils.h uv_trans_math / uv_diff2_math /
 // sw_update_uv_math) over the march registers.  Accessor names follow the stage functors; an
 // array named twice there (u = ubrtr, hu = hhu, hh = hhh) is one register set here.
 struct MarchViewB {
-    Rows<true, true> rU, rV, rHV, rMU;                 // ubrtr, vbrtr, hhv, mu
-    Rows<false, true> rHU, rHQ, rSTT, rSSH;            // hhu, hhq, str_t, ssh
-    Rows<true, false> rVORT, rHH, rSTS;                // vort, hhh, str_s
+    RowsD<true, true> rU, rV, rHV, rMU;                // ubrtr, vbrtr, hhv, mu
+    RowsD<false, true> rHU, rHQ, rSTT, rSSH;           // hhu, hhq, str_t, ssh
+    RowsD<true, false> rVORT, rHH, rSTS;               // vort, hhh, str_s
     Here hhun_, hhup_, hhvn_, hhvp_, ubrtrp_, vbrtrp_, rhsx_, rhsy_;
     unsigned bits_s, bits_c;                           // mask bytes at (m, n-1), (m, n)
-    float g[kNumRowFields][3];                         // metric rows n-1, n, n+1 (compact tables)
+    MetRows met;                                       // metric rows n-1, n, n+1 (compact tables)
     double tau;
     __device__ __forceinline__ double quot(double a, double b, int, int) const { return a / b; }
     __device__ __forceinline__ double qtau(double a) const { return a / tau; }
-#define OCN_MV(name, reg) \
-    __device__ __forceinline__ double name(int dx, int dy) const { return reg.at(dx, dy); }
     OCN_MV(u, rU) OCN_MV(ubrtr, rU) OCN_MV(v, rV) OCN_MV(vbrtr, rV) OCN_MV(hu, rHU) OCN_MV(hhu, rHU)
     OCN_MV(hv, rHV) OCN_MV(hhv, rHV) OCN_MV(hh, rHH) OCN_MV(hhh, rHH) OCN_MV(mu, rMU) OCN_MV(hq, rHQ)
     OCN_MV(vort, rVORT) OCN_MV(str_t, rSTT) OCN_MV(str_s, rSTS) OCN_MV(ssh, rSSH)
     OCN_MV(hhun, hhun_) OCN_MV(hhup, hhup_) OCN_MV(hhvn, hhvn_) OCN_MV(hhvp, hhvp_) OCN_MV(ubrtrp, ubrtrp_)
     OCN_MV(vbrtrp, vbrtrp_) OCN_MV(RHSx, rhsx_) OCN_MV(RHSy, rhsy_)
-#undef OCN_MV
-#define OCN_MG(name, id) \
-    __device__ __forceinline__ float name(int, int dy) const { return g[id - OCN_DX][dy + 1]; }
-    OCN_MG(dx, OCN_DX) OCN_MG(dy, OCN_DY) OCN_MG(dxt, OCN_DXT) OCN_MG(dyt, OCN_DYT) OCN_MG(dxh, OCN_DXH)
-    OCN_MG(dyh, OCN_DYH) OCN_MG(dxb, OCN_DXB) OCN_MG(dyb, OCN_DYB) OCN_MG(rlh_s, OCN_RLH_S) OCN_MG(rdis, OCN_R_DISS)
-#undef OCN_MG
+    OCN_MG_ALL OCN_MG(rlh_s, OCN_RLH_S) OCN_MG(rdis, OCN_R_DISS)
     __device__ __forceinline__ float luu(int dx, int dy) const
     {
         if (dx != 0 || dy < -1 || dy > 0) ocn_march_bad_access();
@@ -215,47 +321,40 @@ struct MarchViewB {
     }
 };
 
-// fused B (sw_stencils.h FusedB) as a register march; compact static fields only
+// fused B (sw_stencils.h FusedB) as a register march (offset layout); compact static fields only
 struct MarchFusedB {
+    static constexpr bool kAligned = false;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; bool full, reuse;
-    __device__ void march(int m, bool out, int nb, int ne) const
-    {
-        const FusedB<true> k = make_fused_b(&b, t, sw, tau, full, reuse);
-        const UvTrans<true> &a4 = k.a4;
-        const UvDiff2<true> &a6 = k.a6;
-        const SwUpdateUv<true> &a7 = k.a7;
-        const Geo I = a7.I;
-        const unsigned nrows = t.nrows;
-        auto row_met = [&](int id, int n) { return t.rows[(unsigned)(id - OCN_DX) * nrows + (unsigned)(n - b.bnd_y1)]; };
-        MarchViewB x;
-        x.tau = tau;
+    using View = MarchViewB;
+    struct Fn {
+        FusedB<true> k; const Tab<true> &t;
+        // row n: ubrtr, vbrtr, hhv, mu, hhu, hhq, str_t, ssh at n+1; vort, hhh, str_s, mask bytes
+        // and the pointwise operands at n; metric row n+1
+        struct Batch { double nn[8], c[3], h[8]; unsigned bits; float g[kNumRowFields]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
         {
-            const Pt s = I(m, nb - 1), c = I(m, nb);
-            x.rU.s = ld(a7.ubrtr, s); x.rU.c = ld(a7.ubrtr, c);
-            x.rV.s = ld(a7.vbrtr, s); x.rV.c = ld(a7.vbrtr, c);
-            x.rHV.s = ld(a7.hhv, s); x.rHV.c = ld(a7.hhv, c);
-            x.rMU.s = ld(a6.mu, s); x.rMU.c = ld(a6.mu, c);
-            x.rHU.c = ld(a7.hhu, c); x.rHQ.c = ld(a6.hq, c); x.rSTT.c = ld(a6.str_t, c); x.rSSH.c = ld(a7.ssh, c);
-            x.rVORT.c = ld(a4.vort, s); x.rHH.c = ld(a7.hhh, s); x.rSTS.c = ld(a6.str_s, s);
-            x.bits_c = ld(t.bits, s);
-            for (int id = OCN_DX; id < OCN_NUM_R4; ++id) {
-                x.g[id - OCN_DX][1] = row_met(id, nb - 1);
-                x.g[id - OCN_DX][2] = row_met(id, nb);
-            }
+            const SwUpdateUv<true> &a7 = k.a7;
+            const Pt c = a7.I(L.m, n), cn = a7.I(L.m, n + 1);
+            q.nn[0] = ld(a7.ubrtr, cn); q.nn[1] = ld(a7.vbrtr, cn); q.nn[2] = ld(a7.hhv, cn);
+            q.nn[3] = ld(k.a6.mu, cn); q.nn[4] = ld(a7.hhu, cn); q.nn[5] = ld(k.a6.hq, cn);
+            q.nn[6] = ld(k.a6.str_t, cn); q.nn[7] = ld(a7.ssh, cn);
+            q.c[0] = ld(k.a4.vort, c); q.c[1] = ld(a7.hhh, c); q.c[2] = ld(k.a6.str_s, c);
+            q.bits = ld(t.bits, c);
+            q.h[0] = ld(a7.hhun, c); q.h[1] = ld(a7.hhup, c); q.h[2] = ld(a7.hhvn, c); q.h[3] = ld(a7.hhvp, c);
+            q.h[4] = ld(a7.ubrtrp, c); q.h[5] = ld(a7.vbrtrp, c); q.h[6] = ld(a7.RHSx, c); q.h[7] = ld(a7.RHSy, c);
+            MetRows::load(q.g, t.rows, t.nrows, cn.r);
         }
-        for (int n = nb; n <= ne; ++n) {
-            const Pt c = I(m, n), cn = I(m, n + 1);
-            // rotate the rows kept at n-1 / n; load row n+1 (or n)
+        __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
+        {
+            const SwUpdateUv<true> &a7 = k.a7;
+            const Pt c = a7.I(L.m, n);
             x.rVORT.s = x.rVORT.c; x.rHH.s = x.rHH.c; x.rSTS.s = x.rSTS.c; x.bits_s = x.bits_c;
-            for (int r = 0; r < kNumRowFields; ++r) { x.g[r][0] = x.g[r][1]; x.g[r][1] = x.g[r][2]; }
-            x.rU.nn = ld(a7.ubrtr, cn); x.rV.nn = ld(a7.vbrtr, cn); x.rHV.nn = ld(a7.hhv, cn); x.rMU.nn = ld(a6.mu, cn);
-            x.rHU.nn = ld(a7.hhu, cn); x.rHQ.nn = ld(a6.hq, cn); x.rSTT.nn = ld(a6.str_t, cn); x.rSSH.nn = ld(a7.ssh, cn);
-            x.rVORT.c = ld(a4.vort, c); x.rHH.c = ld(a7.hhh, c); x.rSTS.c = ld(a6.str_s, c);
-            x.bits_c = ld(t.bits, c);
-            for (int id = OCN_DX; id < OCN_NUM_R4; ++id) x.g[id - OCN_DX][2] = row_met(id, n + 1);
-            x.hhun_.v = ld(a7.hhun, c); x.hhup_.v = ld(a7.hhup, c); x.hhvn_.v = ld(a7.hhvn, c);
-            x.hhvp_.v = ld(a7.hhvp, c); x.ubrtrp_.v = ld(a7.ubrtrp, c); x.vbrtrp_.v = ld(a7.vbrtrp, c);
-            x.rhsx_.v = ld(a7.RHSx, c); x.rhsy_.v = ld(a7.RHSy, c);
+            x.met.shift(q.g);
+            x.rU.nn = q.nn[0]; x.rV.nn = q.nn[1]; x.rHV.nn = q.nn[2]; x.rMU.nn = q.nn[3];
+            x.rHU.nn = q.nn[4]; x.rHQ.nn = q.nn[5]; x.rSTT.nn = q.nn[6]; x.rSSH.nn = q.nn[7];
+            x.rVORT.c = q.c[0]; x.rHH.c = q.c[1]; x.rSTS.c = q.c[2]; x.bits_c = q.bits;
+            x.hhun_.v = q.h[0]; x.hhup_.v = q.h[1]; x.hhvn_.v = q.h[2]; x.hhvp_.v = q.h[3];
+            x.ubrtrp_.v = q.h[4]; x.vbrtrp_.v = q.h[5]; x.rhsx_.v = q.h[6]; x.rhsy_.v = q.h[7];
 
             double rxa, rya, rxd, ryd;
             if (k.do_adv) uv_trans_math(x, rxa, rya);
@@ -264,21 +363,228 @@ struct MarchFusedB {
             else { rxd = ld(a7.RHSx_dif, c); ryd = ld(a7.RHSy_dif, c); }
             double un, vn;
             sw_update_uv_math(x, rxa, rxd, rya, ryd, un, vn);
-            if (out) {
+            if (L.out) {
                 if (x.bits_c & (1u << OCN_LCU)) {
-                    if (k.do_adv && k.full) st(a4.RHSx, c, rxa);
-                    if (k.do_dif && k.full) st(a6.RHSx, c, rxd);
+                    if (k.do_adv && k.full) st(k.a4.RHSx, c, rxa);
+                    if (k.do_dif && k.full) st(k.a6.RHSx, c, rxd);
                     st(a7.ubrtrn, c, un);
                 }
                 if (x.bits_c & (1u << OCN_LCV)) {
-                    if (k.do_adv && k.full) st(a4.RHSy, c, rya);
-                    if (k.do_dif && k.full) st(a6.RHSy, c, ryd);
+                    if (k.do_adv && k.full) st(k.a4.RHSy, c, rya);
+                    if (k.do_dif && k.full) st(k.a6.RHSy, c, ryd);
                     st(a7.vbrtrn, c, vn);
                 }
             }
             x.rU.rotate(); x.rV.rotate(); x.rHV.rotate(); x.rMU.rotate();
             x.rHU.rotate(); x.rHQ.rotate(); x.rSTT.rotate(); x.rSSH.rotate();
         }
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{make_fused_b(&b, t, sw, tau, full, reuse), t};
+        const SwUpdateUv<true> &a7 = f.k.a7;
+        View x;
+        x.tau = tau;
+        const Pt s = a7.I(L.m, nb - 1), c = a7.I(L.m, nb);   // rows kept from before the first row
+        x.rU.s = ld(a7.ubrtr, s); x.rU.c = ld(a7.ubrtr, c);
+        x.rV.s = ld(a7.vbrtr, s); x.rV.c = ld(a7.vbrtr, c);
+        x.rHV.s = ld(a7.hhv, s); x.rHV.c = ld(a7.hhv, c);
+        x.rMU.s = ld(f.k.a6.mu, s); x.rMU.c = ld(f.k.a6.mu, c);
+        x.rHU.c = ld(a7.hhu, c); x.rHQ.c = ld(f.k.a6.hq, c); x.rSTT.c = ld(f.k.a6.str_t, c); x.rSSH.c = ld(a7.ssh, c);
+        x.rVORT.c = ld(f.k.a4.vort, s); x.rHH.c = ld(a7.hhh, s); x.rSTS.c = ld(f.k.a6.str_s, s);
+        x.bits_c = ld(t.bits, s);
+        x.met.preload(t.rows, t.nrows, s.r, c.r);
+        march_rows(f, x, L, nb, ne);
+    }
+};
+
+// The view of fused A's stages (sw_stencils.h sw_update_ssh_math, hh_update_math,
+// uv_trans_vort_math, stress_components_math) over the march registers.  Arrays read at m-1 or
+// m+1 keep edge values (aligned layout).
+struct MarchViewA {
+    RowsD<false, true, true> rU, rUP, rHR, rSH;        // ubrtr, ubrtrp, h_r, ssh
+    RowsD<true, false, true> rV, rVP;                  // vbrtr, vbrtrp
+    RowsD<true, false> rHV;                            // hhv
+    RowsD<false, false, true> rHU;                     // hhu
+    Here sshp_;
+    BitRows<false, true, true> bits;
+    MetRows met;
+    double tau;
+    __device__ __forceinline__ double tau2() const { return tau; }
+    OCN_MV(u, rU) OCN_MV(ubrtr, rU) OCN_MV(v, rV) OCN_MV(vbrtr, rV) OCN_MV(up, rUP) OCN_MV(vp, rVP)
+    OCN_MV(hhu, rHU) OCN_MV(hhv, rHV) OCN_MV(sshp, sshp_) OCN_MV(h_r, rHR) OCN_MV(sh, rSH)
+    OCN_MG_ALL
+    __device__ __forceinline__ float lu(int dx, int dy) const { return bits.mask(OCN_LU, dx, dy); }
+};
+
+// fused A (sw_stencils.h FusedA) as a register march (aligned layout); HH = a2 hh_update is part
+// of the launch (range [start-1, end]^2, a1/a3/a5 on [start, end]^2) or not (reuse steps,
+// [start, end]^2)
+template <bool HH> struct MarchFusedA {
+    static constexpr bool kAligned = true;
+    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau;
+    using View = MarchViewA;
+    struct Fn {
+        FusedA<true> k; const Tab<true> &t;
+        // row n: ubrtr, ubrtrp, mask bytes, h_r, ssh at n+1; vbrtr, hhv, vbrtrp, hhu, sshp at n;
+        // edge values of the arrays read at m+-1; metric row n+1
+        struct Batch { double nn[4], c[5], enn[4], ec[3]; unsigned bits, ebits; float g[kNumRowFields]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
+        {
+            const SwUpdateSsh<true> &a1 = k.a1;
+            for (int i = 0; i < 4; ++i) q.enn[i] = 0.0;
+            for (int i = 0; i < 3; ++i) q.ec[i] = 0.0;
+            q.ebits = 0;
+            const Pt c = a1.I(L.m, n), cn = a1.I(L.m, n + 1);
+            q.nn[0] = ld(a1.ubrtr, cn); q.nn[1] = ld(k.a5.u, cn); q.bits = ld(t.bits, cn);
+            if (HH) { q.nn[2] = ld(k.a2.h_r, cn); q.nn[3] = ld(k.a2.sh, cn); }
+            q.c[0] = ld(a1.vbrtr, c); q.c[1] = ld(a1.hhv, c); q.c[2] = ld(k.a5.v, c);
+            q.c[3] = ld(a1.hhu, c); q.c[4] = ld(a1.sshp, c);
+            if (L.edge) {
+                const Pt e = a1.I(L.me, n), en = a1.I(L.me, n + 1);
+                q.enn[0] = ld(a1.ubrtr, en); q.enn[1] = ld(k.a5.u, en); q.ebits = ld(t.bits, en);
+                if (HH) { q.enn[2] = ld(k.a2.h_r, en); q.enn[3] = ld(k.a2.sh, en); }
+                q.ec[0] = ld(a1.vbrtr, e); q.ec[1] = ld(k.a5.v, e); q.ec[2] = ld(a1.hhu, e);
+            }
+            MetRows::load(q.g, t.rows, t.nrows, cn.r);
+        }
+        __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.a1.I(L.m, n);
+            x.rV.s = x.rV.c; x.rV.es = x.rV.ec; x.rHV.s = x.rHV.c; x.rVP.s = x.rVP.c; x.rVP.es = x.rVP.ec;
+            x.met.shift(q.g);
+            x.rU.nn = q.nn[0]; x.rUP.nn = q.nn[1]; x.bits.nn = q.bits;
+            x.rU.enn = q.enn[0]; x.rUP.enn = q.enn[1]; x.bits.enn = q.ebits;
+            if (HH) { x.rHR.nn = q.nn[2]; x.rSH.nn = q.nn[3]; x.rHR.enn = q.enn[2]; x.rSH.enn = q.enn[3]; }
+            x.rV.c = q.c[0]; x.rHV.c = q.c[1]; x.rVP.c = q.c[2]; x.rHU.c = q.c[3]; x.sshp_.v = q.c[4];
+            x.rV.ec = q.ec[0]; x.rVP.ec = q.ec[1]; x.rHU.ec = q.ec[2];
+            const unsigned bc = x.bits.c;
+            if (n >= k.sy) {   // wave-uniform
+                const bool in = L.out && L.m >= k.sx;
+                const double r = sw_update_ssh_math(x);
+                if (in && (bc & (1u << OCN_LU))) st(k.a1.sshn, c, r);
+                if (k.do_vort) {
+                    const double v = uv_trans_vort_math(x);
+                    if (in && (bc & (1u << OCN_LUU))) st(k.a3.vort, c, v);
+                }
+                if (k.do_stress) {
+                    double vt, vs;
+                    stress_components_math(x, vt, vs);
+                    if (in && (bc & (1u << OCN_LU))) st(k.a5.str_t, c, vt);
+                    if (in && (bc & (1u << OCN_LUU))) st(k.a5.str_s, c, vs);
+                }
+            }
+            if (HH) {
+                double xu, xv, xh;
+                hh_update_math(x, x.rHR.c + x.rSH.c, xu, xv, xh);
+                if (L.out) {
+                    if (bc & (1u << OCN_LLU)) st(k.a2.hun, c, xu);
+                    if (bc & (1u << OCN_LLV)) st(k.a2.hvn, c, xv);
+                    if (bc & (1u << OCN_LUH)) st(k.a2.hhn, c, xh);
+                }
+            }
+            x.rU.rotate(); x.rUP.rotate(); x.bits.rotate();
+            if (HH) { x.rHR.rotate(); x.rSH.rotate(); }
+        }
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{make_fused_a(&b, t, sw, tau, !HH), t};
+        const SwUpdateSsh<true> &a1 = f.k.a1;
+        View x{};
+        x.tau = tau;
+        const Pt s = a1.I(L.m, nb - 1), c = a1.I(L.m, nb);
+        x.rU.c = ld(a1.ubrtr, c); x.rUP.c = ld(f.k.a5.u, c); x.bits.c = ld(t.bits, c);
+        if (HH) { x.rHR.c = ld(f.k.a2.h_r, c); x.rSH.c = ld(f.k.a2.sh, c); }
+        x.rV.c = ld(a1.vbrtr, s); x.rHV.c = ld(a1.hhv, s); x.rVP.c = ld(f.k.a5.v, s);
+        if (L.edge) {
+            const Pt es = a1.I(L.me, nb - 1), ec = a1.I(L.me, nb);
+            x.rU.ec = ld(a1.ubrtr, ec); x.rUP.ec = ld(f.k.a5.u, ec); x.bits.ec = ld(t.bits, ec);
+            if (HH) { x.rHR.ec = ld(f.k.a2.h_r, ec); x.rSH.ec = ld(f.k.a2.sh, ec); }
+            x.rV.ec = ld(a1.vbrtr, es); x.rVP.ec = ld(f.k.a5.v, es);
+        }
+        x.met.preload(t.rows, t.nrows, s.r, c.r);
+        march_rows(f, x, L, nb, ne);
+    }
+};
+
+// The view of hh_init (sw_stencils.h hh_init_math) over the march registers.
+struct MarchViewH {
+    RowsD<false, true, true> rHR, rSH, rSHP;           // h_r, ssh, sshp
+    BitRows<false, true, true> bits;
+    MetRows met;
+    OCN_MV(h_r, rHR) OCN_MV(sh, rSH) OCN_MV(shp, rSHP)
+    OCN_MG_ALL
+    __device__ __forceinline__ float lu(int dx, int dy) const { return bits.mask(OCN_LU, dx, dy); }
+};
+
+// fused C2 = a10 hh_init (sw_stencils.h HhInit) as a register march (aligned layout) over any
+// part of the whole bnd range: row n+1 is clamped to bnd_y2 (its values are used only where
+// n <= end, where it is in range)
+struct MarchHhInit {
+    static constexpr bool kAligned = true;
+    ocn_block b; Tab<true> t; int ffs; bool full;
+    using View = MarchViewH;
+    struct Fn {
+        HhInit<true> k; const Tab<true> &t; int ylast;
+        // row n: h_r, ssh, sshp, mask bytes (+ edge values) and metrics at row n+1
+        struct Batch { double nn[3], enn[3]; unsigned bits, ebits; float g[kNumRowFields]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
+        {
+            const int r = min(n + 1, ylast);
+            const Pt cn = k.I(L.m, r);
+            q.enn[0] = q.enn[1] = q.enn[2] = 0.0;
+            q.ebits = 0;
+            q.nn[0] = ld(k.h_r, cn); q.nn[1] = ld(k.sh, cn); q.nn[2] = ld(k.shp, cn); q.bits = ld(t.bits, cn);
+            if (L.edge) {
+                const Pt en = k.I(L.me, r);
+                q.enn[0] = ld(k.h_r, en); q.enn[1] = ld(k.sh, en); q.enn[2] = ld(k.shp, en); q.ebits = ld(t.bits, en);
+            }
+            MetRows::load(q.g, t.rows, t.nrows, cn.r);
+        }
+        __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n);
+            const double f = k.f;
+            x.met.shift(q.g);
+            x.rHR.nn = q.nn[0]; x.rSH.nn = q.nn[1]; x.rSHP.nn = q.nn[2]; x.bits.nn = q.bits;
+            x.rHR.enn = q.enn[0]; x.rSH.enn = q.enn[1]; x.rSHP.enn = q.enn[2]; x.bits.enn = q.ebits;
+            const double r00 = x.rHR.c;
+            if (L.out) {
+                st(k.hq, c, r00 + x.rSH.c * f);
+                if (k.full) { st(k.hqp, c, r00 + x.rSHP.c * f); st(k.hqn, c, r00); }
+            }
+            if (n >= k.j0 && n <= k.j1) {   // wave-uniform
+                HhInitOut o;
+                hh_init_math(x, f, k.full, o);
+                if (L.out && L.m >= k.i0 && L.m <= k.i1) {
+                    const unsigned bc = x.bits.c;
+                    const bool bu = bc & (1u << OCN_LLU), bv = bc & (1u << OCN_LLV), bh = bc & (1u << OCN_LUH);
+                    if (bu) { st(k.hu, c, o.u[0]); st(k.hup, c, o.u[1]); }
+                    if (bv) { st(k.hv, c, o.v[0]); st(k.hvp, c, o.v[1]); }
+                    if (bh) { st(k.hh, c, o.h[0]); st(k.hhp, c, o.h[1]); }
+                    if (k.full) {
+                        if (bu) st(k.hun, c, o.u[2]);
+                        if (bv) st(k.hvn, c, o.v[2]);
+                        if (bh) st(k.hhn, c, o.h[2]);
+                    }
+                }
+            }
+            x.rHR.rotate(); x.rSH.rotate(); x.rSHP.rotate(); x.bits.rotate();
+        }
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{make_hh_init(&b, t, ffs, full), t, b.bnd_y2};
+        View x{};
+        const Pt c = f.k.I(L.m, nb);
+        x.rHR.c = ld(f.k.h_r, c); x.rSH.c = ld(f.k.sh, c); x.rSHP.c = ld(f.k.shp, c); x.bits.c = ld(t.bits, c);
+        if (L.edge) {
+            const Pt e = f.k.I(L.me, nb);
+            x.rHR.ec = ld(f.k.h_r, e); x.rSH.ec = ld(f.k.sh, e); x.rSHP.ec = ld(f.k.shp, e); x.bits.ec = ld(t.bits, e);
+        }
+        x.met.preload(t.rows, t.nrows, c.r, c.r);
+        march_rows(f, x, L, nb, ne);
     }
 };
 
@@ -330,22 +636,35 @@ static int launch_fused(const Range &r, const Range &inner, int part, const ocn_
                        s);
 }
 
+// With the compact tables and OCN_OPT_MARCH, the ALL and INNER parts of fused A, fused B and
+// hh_init run as register marches; the FRAME part (thin strips) stays one thread per point.
+static bool use_march(const Compact *cp, int part) { return cp && cp->march && part != OCN_PART_FRAME; }
+static Range march_range(const Range &all, const ocn_block *b, int part)
+{
+    return part == OCN_PART_INNER ? range_clip(all, inner_interior_shrunk(b)) : all;
+}
+
 int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool reuse, hipStream_t s)
 {
-    return launch_fused<KFusedA>(range_fused_a(b, sw, reuse), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s,
-                                 sw, tau, reuse);
+    const Range all = range_fused_a(b, sw, reuse);
+    if (use_march(cp, part)) {
+        RC_K(check_block(b));
+        const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
+        if (sw.full_free_surface > 0 && !reuse)
+            return launch_march(b, march_range(all, b, part), MarchFusedA<true>{*b, t, sw, tau}, s);
+        return launch_march(b, march_range(all, b, part), MarchFusedA<false>{*b, t, sw, tau}, s);
+    }
+    return launch_fused<KFusedA>(all, inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s, sw, tau, reuse);
 }
 
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s)
 {
-    if (cp && cp->march && part != OCN_PART_FRAME) {
+    if (use_march(cp, part)) {
         RC_K(check_block(b));
-        const Range r = part == OCN_PART_INNER ? range_clip(range_interior(b), inner_interior_shrunk(b))
-                                               : range_interior(b);
         const MarchFusedB k{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0), sw, tau, full, reuse};
-        return launch_march(r.m0, r.m1, r.n0, r.n1, k, s);
+        return launch_march(b, march_range(range_interior(b), b, part), k, s);
     }
     return launch_fused<KFusedB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s, sw, tau,
                                  full, reuse);
@@ -360,6 +679,12 @@ int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compac
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, bool full, hipStream_t s)
 {
+    if (use_march(cp, part)) {
+        RC_K(check_block(b));
+        const MarchHhInit k{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0),
+                            (int)sw.full_free_surface, full};
+        return launch_march(b, march_range(range_bnd(b), b, part), k, s);
+    }
     return launch_fused<KHhInit>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s,
                                  (int)sw.full_free_surface, full);
 }

@@ -105,51 +105,116 @@ OCN_HD OCN_INLINE uint32_t fbits(float f)
     return u;
 }
 
+// ------------------------------------------------------------------ views
+// The stage arithmetic is written against a "view" x: x.u(dx, dy) is u(m+dx, n+dy) of the
+// reference loop, x.dyh(dx, dy) the real(4) metric there, x.lu(dx, dy) the mask value,
+// x.quot(a, b, id, dy) = a / b for b = D(metric id at row n+dy), x.qtau(a) = a / tau,
+// x.tau2() = tau.  The pointer views below load every operand from its block array (the stage
+// kernels, the k_range fused kernels and the host harness); the register marches of
+// sw_kernels.hip supply the same values from registers.  Same expressions, same evaluation
+// order, same results.
+#define OCN_VIEW_LD(name) \
+    OCN_HD OCN_INLINE auto name(int dx, int dy) const { return ld(k.name, k.I.at(c, dx, dy)); }
+#define OCN_VIEW_LD_AS(name, field) \
+    OCN_HD OCN_INLINE auto name(int dx, int dy) const { return ld(k.field, k.I.at(c, dx, dy)); }
+#define OCN_VIEW_PTR_COMMON(K)                                                                         \
+    const K &k; Pt c;                                                                                  \
+    OCN_HD OCN_INLINE double quot(double a, double b, int, int) const { return a / b; }
+
 // ------------------------------------------------------------------ a1 sw_update_ssh
-// vel_ssh.f90:69-106
+// vel_ssh.f90:69-106; returns sshn at this point
+template <class X> OCN_HD OCN_INLINE double sw_update_ssh_math(const X &x)
+{
+    const double t1 = x.ubrtr(0, 0) * x.hhu(0, 0) * D(x.dyh(0, 0));
+    const double t2 = x.ubrtr(-1, 0) * x.hhu(-1, 0) * D(x.dyh(-1, 0));
+    const double t3 = x.vbrtr(0, 0) * x.hhv(0, 0) * D(x.dxh(0, 0));
+    const double t4 = x.vbrtr(0, -1) * x.hhv(0, -1) * D(x.dxh(0, -1));
+    const float area = x.dx(0, 0) * x.dy(0, 0);
+    const double div = (t1 - t2 + t3 - t4) / D(area);
+    return x.sshp(0, 0) + 2.0 * x.tau2() * (-div);
+}
+
 template <bool C> struct SwUpdateSsh {
     Geo I; double tau;
     Msk<C> lu; Met<C> dx, dy, dxh, dyh;
     const double *__restrict__ hhu, *__restrict__ hhv;
     double *__restrict__ sshn;
     const double *__restrict__ sshp, *__restrict__ ubrtr, *__restrict__ vbrtr;
+    struct View {
+        OCN_VIEW_PTR_COMMON(SwUpdateSsh)
+        OCN_HD OCN_INLINE double tau2() const { return k.tau; }
+        OCN_VIEW_LD(ubrtr) OCN_VIEW_LD(vbrtr) OCN_VIEW_LD(hhu) OCN_VIEW_LD(hhv) OCN_VIEW_LD(sshp)
+        OCN_VIEW_LD(dx) OCN_VIEW_LD(dy) OCN_VIEW_LD(dxh) OCN_VIEW_LD(dyh)
+    };
     OCN_HD void operator()(int m, int n) const
     {
-        const Pt c = I(m, n), w = I.w(c), s = I.s(c);
-        const double t1 = ld(ubrtr, c) * ld(hhu, c) * D(ld(dyh, c));
-        const double t2 = ld(ubrtr, w) * ld(hhu, w) * D(ld(dyh, w));
-        const double t3 = ld(vbrtr, c) * ld(hhv, c) * D(ld(dxh, c));
-        const double t4 = ld(vbrtr, s) * ld(hhv, s) * D(ld(dxh, s));
-        const float area = ld(dx, c) * ld(dy, c);
-        const double div = (t1 - t2 + t3 - t4) / D(area);
-        const double r = ld(sshp, c) + 2.0 * tau * (-div);
+        const Pt c = I(m, n);
+        const double r = sw_update_ssh_math(View{*this, c});
         if (ld(lu, c) > 0.5f) st(sshn, c, r);
     }
 };
 
 // ------------------------------------------------------------------ T->U/V/H interpolation
 // kernel/shallow_water/depth.f90:56-97 for one level given its values at the four corners
-// (m,n), (m+1,n), (m,n+1), (m+1,n+1).
+// (m,n), (m+1,n), (m,n+1), (m+1,n+1); per-corner weights dx*dy*lu (products evaluated per
+// use, as the reference does)
+template <class X> OCN_HD OCN_INLINE double interp_wt(const X &x, double h, int i, int j)
+{
+    return h * D(x.dx(i, j)) * D(x.dy(i, j)) * D(x.lu(i, j));
+}
+template <class X> OCN_HD OCN_INLINE double interp_u(const X &x, double h00, double h10)
+{
+    const double slu = D(x.lu(0, 0) + x.lu(1, 0));
+    return (interp_wt(x, h00, 0, 0) + interp_wt(x, h10, 1, 0)) / slu / D(x.dxt(0, 0)) / D(x.dyh(0, 0));
+}
+template <class X> OCN_HD OCN_INLINE double interp_v(const X &x, double h00, double h01)
+{
+    const double slu = D(x.lu(0, 0) + x.lu(0, 1));
+    return (interp_wt(x, h00, 0, 0) + interp_wt(x, h01, 0, 1)) / slu / D(x.dxh(0, 0)) / D(x.dyt(0, 0));
+}
+template <class X> OCN_HD OCN_INLINE double interp_h(const X &x, double h00, double h10, double h01, double h11)
+{
+    const double slu = D(x.lu(0, 0) + x.lu(1, 0) + x.lu(0, 1) + x.lu(1, 1));
+    return (interp_wt(x, h00, 0, 0) + interp_wt(x, h10, 1, 0) + interp_wt(x, h01, 0, 1) + interp_wt(x, h11, 1, 1))
+           / slu / D(x.dxb(0, 0)) / D(x.dyb(0, 0));
+}
+
+// a2 hh_update's interpolation (depth.f90:134-160): q = h_r + sh at each corner, q00 given
+template <class X> OCN_HD OCN_INLINE void hh_update_math(const X &x, double q00, double &xu, double &xv, double &xh)
+{
+    const double q10 = x.h_r(1, 0) + x.sh(1, 0), q01 = x.h_r(0, 1) + x.sh(0, 1), q11 = x.h_r(1, 1) + x.sh(1, 1);
+    xu = interp_u(x, q00, q10);
+    xv = interp_v(x, q00, q01);
+    xh = interp_h(x, q00, q10, q01, q11);
+}
+
+// a10 hh_init's interpolation (depth.f90:52-97) of the levels hq = h_r + sh*f (index 0),
+// hqp = h_r + shp*f (1) and, when `full`, hqn = h_r (2)
+struct HhInitOut { double u[3], v[3], h[3]; };
+template <class X> OCN_HD OCN_INLINE void hh_init_math(const X &x, double f, bool full, HhInitOut &o)
+{
+    const double r00 = x.h_r(0, 0), r10 = x.h_r(1, 0), r01 = x.h_r(0, 1), r11 = x.h_r(1, 1);
+    const double a00 = r00 + x.sh(0, 0) * f, a10 = r10 + x.sh(1, 0) * f, a01 = r01 + x.sh(0, 1) * f,
+                 a11 = r11 + x.sh(1, 1) * f;
+    const double b00 = r00 + x.shp(0, 0) * f, b10 = r10 + x.shp(1, 0) * f, b01 = r01 + x.shp(0, 1) * f,
+                 b11 = r11 + x.shp(1, 1) * f;
+    o.u[0] = interp_u(x, a00, a10); o.u[1] = interp_u(x, b00, b10);
+    o.v[0] = interp_v(x, a00, a01); o.v[1] = interp_v(x, b00, b01);
+    o.h[0] = interp_h(x, a00, a10, a01, a11); o.h[1] = interp_h(x, b00, b10, b01, b11);
+    if (full) {
+        o.u[2] = interp_u(x, r00, r10); o.v[2] = interp_v(x, r00, r01); o.h[2] = interp_h(x, r00, r10, r01, r11);
+    }
+}
+
 template <bool C> struct Interp {
     Msk<C> lu; Met<C> dx, dy, dxt, dyt, dxh, dyh, dxb, dyb;
-    // per-corner weights dx*dy*lu (products evaluated per use, as the reference does)
-    OCN_HD OCN_INLINE double wt(double h, Pt i) const { return h * D(ld(dx, i)) * D(ld(dy, i)) * D(ld(lu, i)); }
-    OCN_HD OCN_INLINE double u(double h00, double h10, Pt c, Pt e) const
-    {
-        const double slu = D(ld(lu, c) + ld(lu, e));
-        return (wt(h00, c) + wt(h10, e)) / slu / D(ld(dxt, c)) / D(ld(dyh, c));
-    }
-    OCN_HD OCN_INLINE double v(double h00, double h01, Pt c, Pt nn) const
-    {
-        const double slu = D(ld(lu, c) + ld(lu, nn));
-        return (wt(h00, c) + wt(h01, nn)) / slu / D(ld(dxh, c)) / D(ld(dyt, c));
-    }
-    OCN_HD OCN_INLINE double h(double h00, double h10, double h01, double h11, Pt c, Pt e, Pt nn, Pt ne) const
-    {
-        const double slu = D(ld(lu, c) + ld(lu, e) + ld(lu, nn) + ld(lu, ne));
-        return (wt(h00, c) + wt(h10, e) + wt(h01, nn) + wt(h11, ne)) / slu / D(ld(dxb, c)) / D(ld(dyb, c));
-    }
 };
+// pointer-view accessors of the Interp operands (member W of the functor)
+#define OCN_VIEW_W(name) \
+    OCN_HD OCN_INLINE auto name(int dx, int dy) const { return ld(k.W.name, k.I.at(c, dx, dy)); }
+#define OCN_VIEW_INTERP                                                                             \
+    OCN_VIEW_W(lu) OCN_VIEW_W(dx) OCN_VIEW_W(dy) OCN_VIEW_W(dxt) OCN_VIEW_W(dyt) OCN_VIEW_W(dxh)    \
+    OCN_VIEW_W(dyh) OCN_VIEW_W(dxb) OCN_VIEW_W(dyb)
 
 // ------------------------------------------------------------------ a2 hh_update
 // depth.f90:101-162.  Thread grid = whole bnd range (hqn = h_r + sh, :129); the
@@ -160,14 +225,15 @@ template <bool C> struct HhUpdate {
     Msk<C> llu, llv, luh;
     double *__restrict__ hqn, *__restrict__ hun, *__restrict__ hvn, *__restrict__ hhn;
     const double *__restrict__ sh, *__restrict__ h_r;
-    // the [start-1, end]^2 interpolation part (depth.f90:134-160); q = h_r + sh at each corner
+    struct View {
+        const HhUpdate &k; Pt c;
+        OCN_VIEW_INTERP OCN_VIEW_LD(sh) OCN_VIEW_LD(h_r)
+    };
+    // the [start-1, end]^2 interpolation part (depth.f90:134-160); q00 = h_r + sh here
     OCN_HD OCN_INLINE void interp(Pt c, double q00) const
     {
-        const Pt e = I.e(c), nn = I.n(c), ne = I.e(nn);
-        const double q10 = ld(h_r, e) + ld(sh, e), q01 = ld(h_r, nn) + ld(sh, nn), q11 = ld(h_r, ne) + ld(sh, ne);
-        const double xu = W.u(q00, q10, c, e);
-        const double xv = W.v(q00, q01, c, nn);
-        const double xh = W.h(q00, q10, q01, q11, c, e, nn, ne);
+        double xu, xv, xh;
+        hh_update_math(View{*this, c}, q00, xu, xv, xh);
         if (ld(llu, c) > 0.5f) st(hun, c, xu);
         if (ld(llv, c) > 0.5f) st(hvn, c, xv);
         if (ld(luh, c) > 0.5f) st(hhn, c, xh);
@@ -201,64 +267,57 @@ template <bool C> struct HhInit {
     double *__restrict__ hv, *__restrict__ hvp, *__restrict__ hvn;
     double *__restrict__ hh, *__restrict__ hhp, *__restrict__ hhn;
     const double *__restrict__ sh, *__restrict__ shp, *__restrict__ h_r;
+    struct View {
+        const HhInit &k; Pt c;
+        OCN_VIEW_INTERP OCN_VIEW_LD(sh) OCN_VIEW_LD(shp) OCN_VIEW_LD(h_r)
+    };
     OCN_HD void operator()(int m, int n) const
     {
         const Pt c = I(m, n);
         const double r00 = ld(h_r, c);
-        const double a00 = r00 + ld(sh, c) * f, b00 = r00 + ld(shp, c) * f;
-        st(hq, c, a00);
-        if (full) { st(hqp, c, b00); st(hqn, c, r00); }
+        st(hq, c, r00 + ld(sh, c) * f);
+        if (full) { st(hqp, c, r00 + ld(shp, c) * f); st(hqn, c, r00); }
         if (m < i0 || m > i1 || n < j0 || n > j1) return;
-        const Pt e = I.e(c), nn = I.n(c), ne = I.e(nn);
-        const double r10 = ld(h_r, e), r01 = ld(h_r, nn), r11 = ld(h_r, ne);
-        const double a10 = r10 + ld(sh, e) * f, a01 = r01 + ld(sh, nn) * f, a11 = r11 + ld(sh, ne) * f;
-        const double b10 = r10 + ld(shp, e) * f, b01 = r01 + ld(shp, nn) * f, b11 = r11 + ld(shp, ne) * f;
-        const double u0 = W.u(a00, a10, c, e), u1 = W.u(b00, b10, c, e);
-        const double v0 = W.v(a00, a01, c, nn), v1 = W.v(b00, b01, c, nn);
-        const double h0 = W.h(a00, a10, a01, a11, c, e, nn, ne), h1 = W.h(b00, b10, b01, b11, c, e, nn, ne);
+        HhInitOut o;
+        hh_init_math(View{*this, c}, f, full, o);
         const bool bu = ld(llu, c) > 0.5f, bv = ld(llv, c) > 0.5f, bh = ld(luh, c) > 0.5f;
-        if (bu) { st(hu, c, u0); st(hup, c, u1); }
-        if (bv) { st(hv, c, v0); st(hvp, c, v1); }
-        if (bh) { st(hh, c, h0); st(hhp, c, h1); }
+        if (bu) { st(hu, c, o.u[0]); st(hup, c, o.u[1]); }
+        if (bv) { st(hv, c, o.v[0]); st(hvp, c, o.v[1]); }
+        if (bh) { st(hh, c, o.h[0]); st(hhp, c, o.h[1]); }
         if (full) {
-            const double u2 = W.u(r00, r10, c, e), v2 = W.v(r00, r01, c, nn), h2 = W.h(r00, r10, r01, r11, c, e, nn, ne);
-            if (bu) st(hun, c, u2);
-            if (bv) st(hvn, c, v2);
-            if (bh) st(hhn, c, h2);
+            if (bu) st(hun, c, o.u[2]);
+            if (bv) st(hvn, c, o.v[2]);
+            if (bh) st(hhn, c, o.h[2]);
         }
     }
 };
 
 // ------------------------------------------------------------------ a3 uv_trans_vort
 // vel_ssh.f90:247-281
+template <class X> OCN_HD OCN_INLINE double uv_trans_vort_math(const X &x)
+{
+    const double a = x.v(1, 0) * D(x.dyt(1, 0)) - x.v(0, 0) * D(x.dyt(0, 0));
+    const double b = x.u(0, 1) * D(x.dxt(0, 1)) - x.u(0, 0) * D(x.dxt(0, 0));
+    const double d = (x.v(1, 0) - x.v(0, 0)) * D(x.dyb(0, 0)) - (x.u(0, 1) - x.u(0, 0)) * D(x.dxb(0, 0));
+    return a - b - d;
+}
+
 template <bool C> struct UvTransVort {
     Geo I;
     Msk<C> luu; Met<C> dxt, dyt, dxb, dyb;
     const double *__restrict__ u, *__restrict__ v;
     double *__restrict__ vort;
+    struct View {
+        OCN_VIEW_PTR_COMMON(UvTransVort)
+        OCN_VIEW_LD(u) OCN_VIEW_LD(v) OCN_VIEW_LD(dxt) OCN_VIEW_LD(dyt) OCN_VIEW_LD(dxb) OCN_VIEW_LD(dyb)
+    };
     OCN_HD void operator()(int m, int n) const
     {
-        const Pt c = I(m, n), e = I.e(c), nn = I.n(c);
-        const double a = ld(v, e) * D(ld(dyt, e)) - ld(v, c) * D(ld(dyt, c));
-        const double b = ld(u, nn) * D(ld(dxt, nn)) - ld(u, c) * D(ld(dxt, c));
-        const double d = (ld(v, e) - ld(v, c)) * D(ld(dyb, c)) - (ld(u, nn) - ld(u, c)) * D(ld(dxb, c));
-        const double r = a - b - d;
+        const Pt c = I(m, n);
+        const double r = uv_trans_vort_math(View{*this, c});
         if (ld(luu, c) > 0.5f) st(vort, c, r);
     }
 };
-
-// ------------------------------------------------------------------ views
-// The arithmetic of the stages fused into launch B (a4, a6, a7) is written against a "view"
-// x: x.u(dx, dy) is u(m+dx, n+dy) of the reference loop, x.dyh(dx, dy) the real(4) metric
-// there, x.quot(a, b, id, dy) = a / b for b = D(metric id at row n+dy), x.qtau(a) = a / tau.
-// The pointer views below load every operand from its block array (the stage kernels, the
-// k_range fused kernel and the host harness); the register march of sw_kernels.hip supplies
-// the same values from registers.  Same expressions, same evaluation order, same results.
-#define OCN_VIEW_LD(name) \
-    OCN_HD OCN_INLINE auto name(int dx, int dy) const { return ld(k.name, k.I.at(c, dx, dy)); }
-#define OCN_VIEW_PTR_COMMON(K)                                                                         \
-    const K &k; Pt c;                                                                                  \
-    OCN_HD OCN_INLINE double quot(double a, double b, int, int) const { return a / b; }
 
 // ------------------------------------------------------------------ a4 uv_trans
 // vel_ssh.f90:283-373
@@ -314,22 +373,36 @@ template <bool C> struct UvTrans {
 
 // ------------------------------------------------------------------ a5 stress_components
 // mixing.f90:14-58
+// The reference kernel's u, v are the previous time level (the PSy layer passes ubrtrp /
+// vbrtrp, sw_interface.f90:110-142); the view names them up / vp.
+template <class X> OCN_HD OCN_INLINE void stress_components_math(const X &x, double &vt, double &vs)
+{
+    const float r1 = x.dy(0, 0) / x.dx(0, 0);
+    const float r2 = x.dx(0, 0) / x.dy(0, 0);
+    vt = D(r1) * (x.up(0, 0) / D(x.dyh(0, 0)) - x.up(-1, 0) / D(x.dyh(-1, 0)))
+         - D(r2) * (x.vp(0, 0) / D(x.dxh(0, 0)) - x.vp(0, -1) / D(x.dxh(0, -1)));
+    const float q1 = x.dxb(0, 0) / x.dyb(0, 0);
+    const float q2 = x.dyb(0, 0) / x.dxb(0, 0);
+    vs = D(q1) * (x.up(0, 1) / D(x.dxt(0, 1)) - x.up(0, 0) / D(x.dxt(0, 0)))
+         + D(q2) * (x.vp(1, 0) / D(x.dyt(1, 0)) - x.vp(0, 0) / D(x.dyt(0, 0)));
+}
+
 template <bool C> struct StressComponents {
     Geo I;
     Msk<C> lu, luu; Met<C> dx, dy, dxt, dyt, dxh, dyh, dxb, dyb;
     const double *__restrict__ u, *__restrict__ v;
     double *__restrict__ str_t, *__restrict__ str_s;
+    struct View {
+        OCN_VIEW_PTR_COMMON(StressComponents)
+        OCN_VIEW_LD_AS(up, u) OCN_VIEW_LD_AS(vp, v)
+        OCN_VIEW_LD(dx) OCN_VIEW_LD(dy) OCN_VIEW_LD(dxt) OCN_VIEW_LD(dyt) OCN_VIEW_LD(dxh) OCN_VIEW_LD(dyh)
+        OCN_VIEW_LD(dxb) OCN_VIEW_LD(dyb)
+    };
     OCN_HD void operator()(int m, int n) const
     {
-        const Pt c = I(m, n), w = I.w(c), s = I.s(c), e = I.e(c), nn = I.n(c);
-        const float r1 = ld(dy, c) / ld(dx, c);
-        const float r2 = ld(dx, c) / ld(dy, c);
-        const double vt = D(r1) * (ld(u, c) / D(ld(dyh, c)) - ld(u, w) / D(ld(dyh, w)))
-                          - D(r2) * (ld(v, c) / D(ld(dxh, c)) - ld(v, s) / D(ld(dxh, s)));
-        const float q1 = ld(dxb, c) / ld(dyb, c);
-        const float q2 = ld(dyb, c) / ld(dxb, c);
-        const double vs = D(q1) * (ld(u, nn) / D(ld(dxt, nn)) - ld(u, c) / D(ld(dxt, c)))
-                          + D(q2) * (ld(v, e) / D(ld(dyt, e)) - ld(v, c) / D(ld(dyt, c)));
+        const Pt c = I(m, n);
+        double vt, vs;
+        stress_components_math(View{*this, c}, vt, vs);
         if (ld(lu, c) > 0.5f) st(str_t, c, vt);
         if (ld(luu, c) > 0.5f) st(str_s, c, vs);
     }
