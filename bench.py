@@ -35,23 +35,30 @@ B_ALG = sum(STAGE_BYTES.values())
 # ocn_ctx_step call of K steps runs its first step plain, steps 2..K-1 as "reuse" steps (fused A
 # skips hh_update, fused B reads hhu/hhv for hhu_n/hhv_n) and its last step "full" (fused B and
 # hh_init store the values only the host reads).  K = 1: one plain + full step.
+# Role-flip steps (every step but the last of a single-block call, OCN_OPT_FLIP): fused B also
+# reads sshn, sshp and writes sshp, ubrtrp, vbrtrp (+40 B); fused C1 only touches the halo ring
+# (~0 B per interior cell).
 FUSED_BYTES = {
     "fused_a": {"first": (129, 180), "mid": (89, 128), "last": (129, 180)},
     "fused_b": {"first": (169, 220), "mid": (153, 204), "last": (201, 252)},
     "fused_c1": {"first": (121, 132), "mid": (121, 132), "last": (121, 132)},
     "hh_init": {"first": (81, 128), "mid": (81, 128), "last": (121, 168)},
 }
+FLIP_BYTES = {"fused_b": {"first": 209, "mid": 193}, "fused_c1": {"first": 0, "mid": 0}}
 
 
-def fused_bytes(compact: bool, steps: int):
+def fused_bytes(compact: bool, steps: int, flip: bool = False):
     """Mean bytes per interior cell per launch over one ocn_ctx_step call of `steps` steps."""
     i = 0 if compact else 1
     out = {}
     for k, kinds in FUSED_BYTES.items():
+        per = {kind: v[i] for kind, v in kinds.items()}
+        if flip and k in FLIP_BYTES:
+            per.update(FLIP_BYTES[k])
         if steps == 1:
-            v = kinds["last"][i]
+            v = per["last"]
         else:
-            v = (kinds["first"][i] + (steps - 2) * kinds["mid"][i] + kinds["last"][i]) / steps
+            v = (per["first"] + (steps - 2) * per["mid"] + per["last"]) / steps
         out[k] = v
     return out
 
@@ -134,6 +141,7 @@ def main():
     ap.add_argument("--stages", action="store_true", help="run the 11 reference stages instead of the fused step")
     ap.add_argument("--no-compact", action="store_true", help="fused step on the 2-D real(4) arrays")
     ap.add_argument("--no-march", action="store_true", help="one thread per point in every launch (no register march)")
+    ap.add_argument("--no-flip", action="store_true", help="standard steps only (no role-flip steps)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -166,6 +174,7 @@ def main():
     model.set_fused(not args.stages)
     model.set_compact(not args.no_compact)
     model.set_march(not args.no_march)
+    model.set_flip(not args.no_flip)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -186,6 +195,7 @@ def main():
     dt = time.perf_counter() - t0
     times = model.stage_times()
     compact = model.compact_active
+    flip = model.flip_active
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -196,7 +206,7 @@ def main():
     local_cells = model.interior_cells
     out = None
     if rank == 0:
-        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps)
+        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip)
         b_path = sum(kbytes.values())
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
@@ -219,6 +229,7 @@ def main():
                           "step": "reference stages" if args.stages else "fused groups",
                           "static_fields": "compact" if compact else "2-D arrays",
                           "march": bool(compact and not args.stages and not args.no_march),
+                          "role_flip_steps": flip,
                           "parallelism": f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else "1 block"},
                "roofline": roof,
                "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),

@@ -289,13 +289,21 @@ int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
  *  real(4) pointer with ocn_ctx_field disables this until it is set to 1 again, which also
  *  rebuilds the tables from the fields at the next ocn_ctx_step.
  *  OCN_OPT_MARCH (default 1): with the compact tables, the stencil launches that have a
- *  register-march form (fused B) run as one (same results bit for bit); 0 = one thread per point.
+ *  register-march form (fused A, fused B, hh_init) run as one (same results bit for bit);
+ *  0 = one thread per point.
+ *  OCN_OPT_FLIP (default 1): one block per process without halo exchanges, compact tables and
+ *  march, no tracers: every step of an ocn_ctx_step call but the last replaces sw_next_step's
+ *  copies (ssh := sshn, ubrtr := ubrtrn, vbrtr := vbrtrn) by swapping the two buffers of each
+ *  pair inside the library, and runs its time filters inside fused B (same results bit for bit;
+ *  the pointers of ocn_ctx_field are the same after the call).  Needs the pairs to agree outside
+ *  their write sets, which holds from ocn_ctx_init_state on and is checked on the device
+ *  whenever those fields were uploaded or handed out; otherwise the standard step runs.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
- * the compact tables. */
+ * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps. */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
-       OCN_OPT_MARCH = 6 };
+       OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers). */

@@ -171,7 +171,7 @@ struct ocn_ctx {
     std::map<std::vector<int>, HaloPlan> plans;
     bool initialized = false;
     bool use_graph = false;
-    struct Graph { hipGraphExec_t exec; double tau; bool check, first, last, compact; };
+    struct Graph { hipGraphExec_t exec; double tau; bool check, first, last, compact, flip; int role; };
     std::vector<Graph> graphs;         // one captured step per (tau, check, last step, compact)
     std::vector<void *> allocs;
     // per-stage HIP-event timing (OCN_OPT_STAGE_TIMING): pending (stage, start, stop) records
@@ -188,6 +188,14 @@ struct ocn_ctx {
     bool compact_req = true, compact = false, static_dirty = true;
     bool march = true;   // OCN_OPT_MARCH
     mutable bool r4_escaped = false;
+    // role-flip steps (one_step_fused): role = 1 while the ssh/sshn, ubrtr/ubrtrn, vbrtr/vbrtrn
+    // buffers of every block are swapped (only inside an ocn_ctx_step call); coherent = the pairs
+    // agree outside their write sets (sw_stencils.h Coherence), coherent_known = that was checked
+    // after the state last changed outside ocn_ctx_step; r8_escaped = raw pointers of a pair were
+    // handed out (check at every call); flip = OCN_OPT_FLIP
+    bool flip = true, coherent = false, flip_used = false;
+    mutable bool coherent_known = false, r8_escaped = false;
+    int role = 0;
     int32_t *d_flags = nullptr;
 };
 
@@ -736,7 +744,51 @@ static int join_sync(ocn_ctx *c)
 
 // block b's launch arguments: geometry, field table, compact tables (or nullptr)
 #define FT(b) &(b).g, (b).ptr.data(), (int)(b).ptr.size(), cp(b, t)
-static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool last)
+// The buffer pairs whose roles a role-flip step swaps (a8's copies ssh := sshn etc.)
+static const int kFlipPairs[3][2] = {{OCN_SSH, OCN_SSHN}, {OCN_UBRTR, OCN_UBRTRN}, {OCN_VBRTR, OCN_VBRTRN}};
+static void swap_roles(ocn_ctx *c)
+{
+    for (LBlock &b : c->blocks)
+        for (const auto &pr : kFlipPairs) std::swap(b.ptr[field_slot(pr[0])], b.ptr[field_slot(pr[1])]);
+    c->role ^= 1;
+}
+static bool is_flip_field(int id)
+{
+    for (const auto &pr : kFlipPairs)
+        if (id == pr[0] || id == pr[1]) return true;
+    return false;
+}
+
+// Whether the pairs agree outside their write sets (sw_stencils.h Coherence); synchronises.
+static int check_coherence(ocn_ctx *c)
+{
+    HIPCHK(hipMemsetAsync(c->d_flags, 0, sizeof(int32_t), c->stream));
+    for (const LBlock &b : c->blocks) RC(launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream));
+    int32_t flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->coherent = flags == 0;
+    c->coherent_known = !c->r8_escaped;
+    return OCN_OK;
+}
+
+// Role-flip steps: the step's a8 copies (ssh := sshn, ubrtr := ubrtrn, vbrtr := vbrtrn on the
+// interior and the ring, under the masks) become a swap of the two buffers of each pair, and
+// a8's time filters and check_ssh_err move into fused B (sw_kernels.hip MarchFusedB<true>), so
+// the step is A | B+a8 | a8+a9 on the ring | swap | hh_init -- one full pass (C1) fewer.  Exact
+// when the pairs are coherent (sw_stencils.h Coherence): inside the write sets the reference
+// leaves both buffers of a pair equal to the new value, and the buffer that becomes "sshn" /
+// "ubrtrn" / "vbrtrn" after the swap holds the old value there instead -- which no kernel
+// reads before a1 / a7 of the next step rewrite it.  The last step of every call is a standard
+// step; it leaves both buffers of each pair equal everywhere, so the swap is undone at the end
+// of the call by swapping the pointers back, with no copy.  Used for one block per process
+// without halo exchanges, compact tables + march, no tracers.
+static bool flip_eligible(ocn_ctx *c)
+{
+    return c->flip && c->fused && c->compact && c->march && c->sw.use_tracers <= 0 && !has_exchange(c);
+}
+
+static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool last, bool flip)
 {
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
@@ -753,6 +805,26 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool l
     // on the first step of a call (the host may have changed ssh since) nor on the last one.
     const bool reuse = sw.full_free_surface == 1 && !first && !last;
     const std::vector<int> &sync_a = reuse ? c->sync_a_reuse : c->sync_a;
+    if (flip) {
+        if (last || has_exchange(c)) return set_error(OCN_ERR_STATE, "role-flip step on a last step or with halos");
+        RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
+        for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
+        RC(timer_end(c, rec));
+        RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, reuse, s, nbad, true));
+        RC(timer_end(c, rec));
+        RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));   // a8 + a9 on the ring (no interior points)
+        for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_FRAME, sw, nullptr, s));
+        RC(timer_end(c, rec));
+        swap_roles(c);
+        if (ffs) {
+            RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
+            for (const LBlock &b : c->blocks) RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, full_c2, s));
+            RC(timer_end(c, rec));
+        }
+        return OCN_OK;
+    }
     if (!(c->overlap && has_exchange(c))) {
         RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
         for (const LBlock &b : c->blocks)
@@ -1161,6 +1233,7 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
         return nullptr;
     }
     if (is_r4(id)) c->r4_escaped = true;   // may be written behind our back: no compact tables
+    if (is_flip_field(id)) { c->r8_escaped = true; c->coherent_known = false; }
     return c->blocks[k].ptr[field_slot(id)];
 }
 
@@ -1189,6 +1262,7 @@ int ocn_ctx_init_state(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
+    c->coherent_known = false;
     return init_state(c);
 }
 
@@ -1196,6 +1270,7 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
 {
     if (!c || !has_r8(c, field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
     HIPCHK(hipSetDevice(c->dec.device));
+    c->coherent_known = false;
     return run_sync(c, {field_id});
 }
 
@@ -1204,6 +1279,7 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
     if (stage_id < 0 || stage_id >= OCN_NUM_STAGES) return set_error(OCN_ERR_ARG, "bad stage id");
+    c->coherent_known = false;
     return envoke(c, stage_id, tau);
 }
 
@@ -1214,24 +1290,28 @@ static void drop_graphs(ocn_ctx *c)
 }
 
 // one model step (model.f90:146-160): expl_shallow_water, then expl_tracer
-static int run_step(ocn_ctx *c, double tau, bool check, bool first, bool last)
+static int run_step(ocn_ctx *c, double tau, bool check, bool first, bool last, bool flip)
 {
-    RC(c->fused ? one_step_fused(c, tau, check, first, last) : one_step(c, tau, check));
+    RC(c->fused ? one_step_fused(c, tau, check, first, last, flip) : one_step(c, tau, check));
     return expl_tracer(c, tau, c->fused && c->compact);
 }
 
-// one step as a replayed hipGraph, captured once per (tau, check, first, last, compact)
-static int graph_step(ocn_ctx *c, double tau, bool check, bool first, bool last)
+// one step as a replayed hipGraph, captured once per (tau, check, first, last, compact, flip,
+// role); a role-flip step swaps the host's pointer roles as the captured launches did
+static int graph_step(ocn_ctx *c, double tau, bool check, bool first, bool last, bool flip)
 {
     for (const auto &g : c->graphs)
-        if (g.tau == tau && g.check == check && g.first == first && g.last == last && g.compact == c->compact) {
+        if (g.tau == tau && g.check == check && g.first == first && g.last == last && g.compact == c->compact &&
+            g.flip == flip && g.role == c->role) {
             HIPCHK(hipGraphLaunch(g.exec, c->stream));
+            if (flip) swap_roles(c);
             return OCN_OK;
         }
-    if (c->graphs.size() >= 8) drop_graphs(c);
+    if (c->graphs.size() >= 16) drop_graphs(c);
+    const int role = c->role;
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = run_step(c, tau, check, first, last);
+    int rc = run_step(c, tau, check, first, last, flip);
     hipError_t e = hipStreamEndCapture(c->stream, &graph);
     if (rc) return rc;
     HIPCHK(e);
@@ -1239,7 +1319,7 @@ static int graph_step(ocn_ctx *c, double tau, bool check, bool first, bool last)
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     HIPCHK(e);
-    c->graphs.push_back(ocn_ctx::Graph{exec, tau, check, first, last, c->compact});
+    c->graphs.push_back(ocn_ctx::Graph{exec, tau, check, first, last, c->compact, flip, role});
     HIPCHK(hipGraphLaunch(exec, c->stream));
     return OCN_OK;
 }
@@ -1261,13 +1341,20 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
     if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
     if (c->fused) RC(prepare_static(c));
     const bool graph_ok = c->use_graph && !c->comm && !c->stage_timing;   // RCCL / events stay outside graphs
-    for (int s = 1; s <= nsteps; ++s) {
+    bool flip_call = nsteps >= 2 && flip_eligible(c);
+    if (flip_call && !c->coherent_known) RC(check_coherence(c));
+    flip_call = flip_call && c->coherent;
+    c->flip_used = flip_call;
+    int rc = OCN_OK;
+    for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
         const bool check = check_every > 0 && (s % check_every == 0);
         const bool first = s == 1, last = s == nsteps;
-        if (graph_ok) RC(graph_step(c, tau, check, first, last));
-        else RC(run_step(c, tau, check, first, last));
+        const bool flip = flip_call && !last;
+        rc = graph_ok ? graph_step(c, tau, check, first, last, flip) : run_step(c, tau, check, first, last, flip);
     }
-    return OCN_OK;
+    // the last (standard) step left both buffers of each pair equal: undo the swap by pointers
+    if (c->role) swap_roles(c);
+    return rc;
 }
 
 int ocn_ctx_synchronize(ocn_ctx *c)
@@ -1318,6 +1405,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
         return set_error(OCN_ERR_ARG, "upload: bad argument");
     HIPCHK(hipStreamSynchronize(c->stream));
     if (is_r4(id)) c->static_dirty = true;
+    if (is_flip_field(id)) c->coherent_known = false;
     return upload_field(c, c->blocks[k], id, host, false);
 }
 
@@ -1336,6 +1424,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         c->overlap = value != 0;
         return OCN_OK;
     case OCN_OPT_MARCH: c->march = value != 0; return OCN_OK;
+    case OCN_OPT_FLIP: c->flip = value != 0; return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -1355,6 +1444,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_OVERLAP: *value = c->overlap; return OCN_OK;
     case OCN_OPT_COMPACT: *value = c->fused && c->compact; return OCN_OK;
     case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
+    case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -58,8 +58,11 @@ struct Compact {
 enum { OCN_PART_ALL = 0, OCN_PART_FRAME = 1, OCN_PART_INNER = 2 };
 int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool reuse, hipStream_t s);
+// flip: the role-flip form (sw_kernels.hip MarchFusedB<true>: + a8's filters and check_ssh_err
+// into flip_nbad on the interior; needs cp->march)
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                   const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s);
+                   const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s,
+                   int32_t *flip_nbad = nullptr, bool flip = false);
 int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, int32_t *nbad, hipStream_t s);
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
@@ -67,6 +70,9 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compac
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);
+// ORs 1 into *flags (device int) if a buffer pair of the role-flip step differs outside the
+// pair's write set (sw_stencils.h Coherence).
+int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int32_t *flags, hipStream_t s);
 // Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
 // they cannot be used into *flags (device int).
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s);

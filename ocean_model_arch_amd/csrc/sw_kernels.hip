@@ -321,16 +321,21 @@ struct MarchViewB {
     }
 };
 
-// fused B (sw_stencils.h FusedB) as a register march (offset layout); compact static fields only
-struct MarchFusedB {
+// fused B (sw_stencils.h FusedB) as a register march (offset layout); compact static fields only.
+// C1F: the "role-flip" form of the step (ocn_ctx.hip one_step_fused): the launch also runs a8
+// sw_next_step's time filters on the interior (sshp, ubrtrp, vbrtrp updated in place -- each is
+// read only at its own point) and check_ssh_err on the new ssh (= sshn on sea points); a8's
+// copies ssh := sshn, ubrtr := ubrtrn, vbrtr := vbrtrn are not made -- the host swaps the roles
+// of the two buffers of each pair instead, so nothing this launch reads at a neighbour is written.
+template <bool C1F> struct MarchFusedB {
     static constexpr bool kAligned = false;
-    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; bool full, reuse;
+    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; bool full, reuse; int32_t *nbad;
     using View = MarchViewB;
     struct Fn {
-        FusedB<true> k; const Tab<true> &t;
+        FusedB<true> k; const Tab<true> &t; SwNextStep<true> a8; int *nbad;
         // row n: ubrtr, vbrtr, hhv, mu, hhu, hhq, str_t, ssh at n+1; vort, hhh, str_s, mask bytes
         // and the pointwise operands at n; metric row n+1
-        struct Batch { double nn[8], c[3], h[8]; unsigned bits; float g[kNumRowFields]; };
+        struct Batch { double nn[8], c[3], h[8], p[2]; unsigned bits; float g[kNumRowFields]; };
         __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
         {
             const SwUpdateUv<true> &a7 = k.a7;
@@ -342,6 +347,7 @@ struct MarchFusedB {
             q.bits = ld(t.bits, c);
             q.h[0] = ld(a7.hhun, c); q.h[1] = ld(a7.hhup, c); q.h[2] = ld(a7.hhvn, c); q.h[3] = ld(a7.hhvp, c);
             q.h[4] = ld(a7.ubrtrp, c); q.h[5] = ld(a7.vbrtrp, c); q.h[6] = ld(a7.RHSx, c); q.h[7] = ld(a7.RHSy, c);
+            if (C1F) { q.p[0] = ld(a8.sshn, c); q.p[1] = ld(a8.sshp, c); }
             MetRows::load(q.g, t.rows, t.nrows, cn.r);
         }
         __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
@@ -375,13 +381,25 @@ struct MarchFusedB {
                     st(a7.vbrtrn, c, vn);
                 }
             }
+            if (C1F) {   // a8 on this interior point (SwNextStep::step without the copies)
+                const double ts = a8.ts, xn = q.p[0];
+                const double fx = asselin(x.rSSH.c, xn, q.p[1], ts);
+                const double fa = asselin(x.rU.c, un, x.ubrtrp_.v, ts), fb = asselin(x.rV.c, vn, x.vbrtrp_.v, ts);
+                if (L.out) {
+                    const bool bl = x.bits_c & (1u << OCN_LU);
+                    if (bl) st(a8.sshp, c, fx);
+                    if (x.bits_c & (1u << OCN_LCU)) st(a8.up, c, fa);
+                    if (x.bits_c & (1u << OCN_LCV)) st(a8.vp, c, fb);
+                    if (nbad && bl && !(xn < 10000.0 && xn > -10000.0)) OCN_ATOMIC_INC(nbad);
+                }
+            }
             x.rU.rotate(); x.rV.rotate(); x.rHV.rotate(); x.rMU.rotate();
             x.rHU.rotate(); x.rHQ.rotate(); x.rSTT.rotate(); x.rSSH.rotate();
         }
     };
     __device__ void march(const Lane &L, int nb, int ne) const
     {
-        const Fn f{make_fused_b(&b, t, sw, tau, full, reuse), t};
+        const Fn f{make_fused_b(&b, t, sw, tau, full, reuse), t, make_sw_next_step(&b, t, sw.time_smooth), (int *)nbad};
         const SwUpdateUv<true> &a7 = f.k.a7;
         View x;
         x.tau = tau;
@@ -659,13 +677,17 @@ int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact
 }
 
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                   const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s)
+                   const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s, int32_t *flip_nbad,
+                   bool flip)
 {
     if (use_march(cp, part)) {
         RC_K(check_block(b));
-        const MarchFusedB k{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0), sw, tau, full, reuse};
-        return launch_march(b, march_range(range_interior(b), b, part), k, s);
+        const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
+        const Range r = march_range(range_interior(b), b, part);
+        if (flip) return launch_march(b, r, MarchFusedB<true>{*b, t, sw, tau, full, reuse, flip_nbad}, s);
+        return launch_march(b, r, MarchFusedB<false>{*b, t, sw, tau, full, reuse, nullptr}, s);
     }
+    if (flip) return set_error(OCN_ERR_ARG, "the role-flip step needs the compact tables and the march");
     return launch_fused<KFusedB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s, sw, tau,
                                  full, reuse);
 }
@@ -704,6 +726,13 @@ int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact 
         return launch_fused<KTracerNextStep>(rr, rr, OCN_PART_ALL, b, ptr, nptr, cp, k, s, ts);
     default: return set_error(OCN_ERR_ARG, "bad tracer stage id");
     }
+}
+
+int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int32_t *flags, hipStream_t s)
+{
+    RC_K(check_block(b));
+    const Range r = range_bnd(b);
+    return launch_range(r.m0, r.m1, r.n0, r.n1, make_coherence(b, ptr, bits, (int *)flags), s);
 }
 
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s)

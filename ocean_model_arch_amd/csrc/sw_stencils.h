@@ -524,7 +524,10 @@ template <bool C> struct SwUpdateUv {
 };
 
 // ------------------------------------------------------------------ a8 sw_next_step
-// vel_ssh.f90:197-245 (interior + halo ring)
+// vel_ssh.f90:197-245 (interior + halo ring).  asselin = the time filter of one field
+// (vel_ssh.f90:230, 234, 238), in the reference's evaluation order.
+OCN_HD OCN_INLINE double asselin(double x, double xn, double xp, double ts) { return x + ts * (xn - 2.0 * x + xp) / 2.0; }
+
 template <bool C> struct SwNextStep {
     Geo I; double ts;
     Msk<C> lu, lcu, lcv;
@@ -537,9 +540,7 @@ template <bool C> struct SwNextStep {
         const double x = ld(ssh, i), xn = ld(sshn, i), xp = ld(sshp, i);
         const double a = ld(u, i), an = ld(un, i), ap = ld(up, i);
         const double b = ld(v, i), bn = ld(vn, i), bp = ld(vp, i);
-        const double fx = x + ts * (xn - 2.0 * x + xp) / 2.0;
-        const double fa = a + ts * (an - 2.0 * a + ap) / 2.0;
-        const double fb = b + ts * (bn - 2.0 * b + bp) / 2.0;
+        const double fx = asselin(x, xn, xp, ts), fa = asselin(a, an, ap, ts), fb = asselin(b, bn, bp, ts);
         const bool bl = ld(lu, i) > 0.5f;
         if (bl) { st(sshp, i, fx); st(ssh, i, xn); }
         if (ld(lcu, i) > 0.5f) { st(up, i, fa); st(u, i, an); }
@@ -764,6 +765,37 @@ struct Prepare {
     }
 };
 
+// ------------------------------------------------------------------ role-flip coherence
+// The role-flip step (ocn_ctx.hip one_step_fused) replaces a8's copies ssh := sshn,
+// ubrtr := ubrtrn, vbrtr := vbrtrn by swapping the two buffers of each pair.  That is exact when
+// the two buffers of a pair agree bit for bit at every point outside the pair's write set
+// (interior points with lu / lcu / lcv; a1 and a7 write there, and a8 makes the pair equal there
+// and on the ring): nothing else ever writes those points, so the agreement then holds for good.
+// This functor (thread grid = bnd range, compact mask bytes) ORs 1 into *flags where it fails.
+struct Coherence {
+    Geo I; int ms, me, ns, ne;
+    const uint8_t *__restrict__ bits;
+    const double *a[3], *b[3];
+    int *flags;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const Pt q = I(m, n);
+        const bool inside = m >= ms && m <= me && n >= ns && n <= ne;
+        const unsigned mb = ld(bits, q);
+        const unsigned mask_bit[3] = {1u << OCN_LU, 1u << OCN_LCU, 1u << OCN_LCV};
+        bool bad = false;
+        for (int k = 0; k < 3; ++k) {
+            if (inside && (mb & mask_bit[k])) continue;
+            uint64_t x, y;
+            const double va = ld(a[k], q), vb = ld(b[k], q);
+            __builtin_memcpy(&x, &va, 8);
+            __builtin_memcpy(&y, &vb, 8);
+            bad |= x != y;
+        }
+        if (bad) OCN_ATOMIC_OR(flags, 1);
+    }
+};
+
 // ------------------------------------------------------------------ functor makers
 // Built from a block's field table (`ptr`, indexed by ocn_field_slot) -- used by the fused
 // launches and by the host harness, so both run exactly the same functors over the same ranges.
@@ -829,6 +861,17 @@ inline OCN_HD void frame_point(const Rects &q, int t, int &m, int &n)
 inline Range inner_interior_shrunk(const ocn_block *b)
 {
     return {b->nx_start + 1, b->nx_end - 1, b->ny_start + 1, b->ny_end - 1};
+}
+
+inline Coherence make_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int *flags)
+{
+    Coherence k{geo(b), b->nx_start, b->nx_end, b->ny_start, b->ny_end, bits, {}, {}, flags};
+    const int pa[3] = {OCN_SSH, OCN_UBRTR, OCN_VBRTR}, pb[3] = {OCN_SSHN, OCN_UBRTRN, OCN_VBRTRN};
+    for (int i = 0; i < 3; ++i) {
+        k.a[i] = (const double *)ptr[ocn_field_slot(pa[i])];
+        k.b[i] = (const double *)ptr[ocn_field_slot(pb[i])];
+    }
+    return k;
 }
 
 inline Prepare make_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int *flags)

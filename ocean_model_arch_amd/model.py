@@ -145,10 +145,22 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MARCH, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_flip(self, on: bool = True):
+        """Role-flip steps (default; one block per process, no halo exchange, compact + march, no
+        tracers): sw_next_step's copies become buffer swaps inside the library and its filters run
+        inside fused B; same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FLIP, int(on)), "ocn_ctx_set_option")
+        return self
+
     def option(self, key: int) -> int:
         v = C.c_int64(0)
         check(lib().ocn_ctx_get_option(self.ctx, key, C.byref(v)), "ocn_ctx_get_option")
         return v.value
+
+    @property
+    def flip_active(self) -> bool:
+        """Whether the last step() used role-flip steps."""
+        return bool(self.option(_lib.OPT_FLIP))
 
     @property
     def compact_active(self) -> bool:

@@ -111,7 +111,7 @@ def test_tracer_kernels_match_reference(amd, geom):
     assert not failures, f"{geom}: differs from the reference: {failures}"
 
 
-def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True, march=True):
+def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True, march=True, flip=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"])
@@ -122,6 +122,7 @@ def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True, 
     m.set_compact(compact)
     m.set_overlap(overlap)
     m.set_march(march)
+    m.set_flip(flip)
     if graph:
         m.set_graph(True)
     return m
@@ -144,18 +145,19 @@ def compare_case(m, case, name):
     return bad
 
 
-@pytest.mark.parametrize("mode", ["compact", "pointwise", "fused", "stages", "serial"])
+@pytest.mark.parametrize("mode", ["compact", "noflip", "pointwise", "fused", "stages", "serial"])
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
-    """compact = the 4-launch step reading the compact static fields, fused B as a register
-    march, halo exchanges overlapped with inner launches when there are several blocks (the
-    default); pointwise = compact with every launch one thread per point; fused = the 4-launch
-    step on the 2-D real(4) arrays; serial = compact without the overlap; stages = the
-    reference's 11 envoke stages."""
+    """compact = the default: the fused step reading the compact static fields, fused A / B /
+    hh_init as register marches, role-flip steps on single-block runs without tracers, halo
+    exchanges overlapped with inner launches when there are several blocks; noflip = compact
+    with standard steps only; pointwise = compact with every launch one thread per point; fused =
+    the 4-launch step on the 2-D real(4) arrays; serial = compact without the overlap; stages =
+    the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    compact = mode in ("compact", "serial", "pointwise")
+    compact = mode in ("compact", "noflip", "serial", "pointwise")
     m = build_model(amd, case, fused=mode != "stages", compact=compact, overlap=mode != "serial",
-                    march=mode != "pointwise")
+                    march=mode != "pointwise", flip=mode != "noflip")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     assert m.compact_active == compact
     bad = compare_case(m, case, name)
@@ -164,10 +166,11 @@ def test_end_to_end_matches_reference(amd, name, mode):
 
 
 @pytest.mark.parametrize("graph", [False, True], ids=["stream", "graph"])
-def test_split_step_calls_match_reference(amd, graph):
+@pytest.mark.parametrize("name", ["box70x54_b3x2_s20", "box70x54_b1x1_s20"])
+def test_split_step_calls_match_reference(amd, graph, name):
     """The run split over several ocn_ctx_step calls (each call's last step writes hh_init's
-    time-invariant levels): same final state as one call and as the reference."""
-    name = "box70x54_b3x2_s20"
+    time-invariant levels; on one block the role-flip steps' swaps are undone at each call's
+    end): same final state as one call and as the reference."""
     case = cases.load_e2e(name)
     m = build_model(amd, case, graph=graph).init()
     for n in (7, 1, 12):
@@ -211,6 +214,34 @@ def test_compact_fallback_is_exact(amd, what):
                 bad.append(f"({b.bm},{b.bn}):{nm}")
     m.close()
     assert not bad, bad
+
+
+def test_flip_falls_back_when_pairs_disagree(amd):
+    """Role-flip steps need ssh/sshn, ubrtr/ubrtrn, vbrtr/vbrtrn to agree outside their write
+    sets (sw_stencils.h Coherence).  A state where sshn differs from ssh on a land point and
+    ubrtrn from ubrtr on the halo must be detected on the device and run with standard steps:
+    same result bit for bit as a run with OCN_OPT_FLIP off.  A coherent upload keeps flip on and
+    still matches."""
+    n, steps = 96, 6
+    out = {}
+    for flip in (True, False):
+        for kind in ("incoherent", "coherent"):
+            m = amd.OceanModel(amd.box_config(n)).set_flip(flip).init()
+            s, u = m.download(0, "sshn"), m.download(0, "ubrtrn")
+            if kind == "incoherent":
+                s[0, 0] += 0.25         # bnd corner: outside every write set
+                u[1, 5] = 1.0e-3        # halo column
+            m.upload(0, "sshn", s)
+            m.upload(0, "ubrtrn", u)
+            m.step(steps).synchronize()
+            out[(flip, kind)] = {nm: m.download(0, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn",
+                                                                   "ubrtrp", "vbrtr", "vbrtrn", "vbrtrp", "hhu",
+                                                                   "hhv", "hhh", "hhq", "vort", "str_t", "str_s")}
+            m.close()
+    for kind in ("incoherent", "coherent"):
+        bad = [nm for nm, a in out[(True, kind)].items() if not bits_equal(a, out[(False, kind)][nm])]
+        assert not bad, f"{kind}: flip vs standard steps differ in {bad}"
+    assert out[(True, "incoherent")]["sshn"][0, 0] != out[(True, "incoherent")]["ssh"][0, 0]
 
 
 @pytest.mark.parametrize("name", ["box70x54_b3x2_s20", "bs_b1x1_s60"])
@@ -310,13 +341,15 @@ def test_full_size_decomposition_invariance(amd):
     b.close()
 
 
-def test_blowup_is_reported(amd):
-    """check_ssh_err_kernel (vel_ssh.f90:40-67): |ssh| >= 1e4 on a sea point must fail the step."""
+@pytest.mark.parametrize("nsteps", [1, 3])
+def test_blowup_is_reported(amd, nsteps):
+    """check_ssh_err_kernel (vel_ssh.f90:40-67): |ssh| >= 1e4 on a sea point must fail the step
+    (nsteps = 3: the check inside the role-flip steps' fused B)."""
     m = amd.OceanModel(amd.box_config(64)).init()
     s = m.download(0, "ssh")
     s[10, 10] = 2.0e4
     for nm in ("ssh", "sshn", "sshp"):
         m.upload(0, nm, s)
     with pytest.raises(amd.OcnError):
-        m.step(1, check_every=1).synchronize()
+        m.step(nsteps, check_every=1).synchronize()
     m.close()
