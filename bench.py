@@ -30,37 +30,55 @@ STAGE_BYTES = {"sw_update_ssh": 68, "hh_update": 96, "uv_trans_vort": 44, "uv_tr
                "stress_components": 72, "uv_diff2": 96, "sw_update_uv": 200, "sw_next_step": 132,
                "hh_shift": 176, "hh_init": 168}
 B_ALG = sum(STAGE_BYTES.values())
-# Distinct arrays read + written once per interior cell by each fused launch, for
-# the bench's sw.par (all three flags on), as (compact static fields, 2-D real(4) arrays).  An
-# ocn_ctx_step call of K steps runs its first step plain, steps 2..K-1 as "reuse" steps (fused A
-# skips hh_update, fused B reads hhu/hhv for hhu_n/hhv_n) and its last step "full" (fused B and
-# hh_init store the values only the host reads).  K = 1: one plain + full step.
-# Role-flip steps (every step but the last of a single-block call, OCN_OPT_FLIP): fused B also
-# reads sshn, sshp and writes sshp, ubrtrp, vbrtrp (+40 B); fused C1 only touches the halo ring
-# (~0 B per interior cell).
-FUSED_BYTES = {
-    "fused_a": {"first": (129, 180), "mid": (89, 128), "last": (129, 180)},
-    "fused_b": {"first": (169, 220), "mid": (153, 204), "last": (201, 252)},
-    "fused_c1": {"first": (121, 132), "mid": (121, 132), "last": (121, 132)},
-    "hh_init": {"first": (81, 128), "mid": (81, 128), "last": (121, 168)},
+# Distinct arrays read + written once per interior cell by each launch kind, for
+# the bench's sw.par (all three flags on), with the compact static fields (index 0) or the 2-D
+# real(4) arrays (index 1).  "reuse" = a step that is neither the first nor the last of its
+# ocn_ctx_step call (fused A skips hh_update, fused B reads hhu/hhv for hhu_n/hhv_n); "full" =
+# the last step (fused B and hh_init also store what only the host reads).
+LAUNCH_BYTES = {
+    "a": (129, 180), "a_reuse": (89, 128),
+    "b": (169, 220), "b_reuse": (153, 204), "b_full": (201, 252),
+    "b_flip": (209, 260), "b_flip_reuse": (193, 244),     # + a8's filters: sshn, sshp in; sshp, ubrtrp, vbrtrp out
+    "c1": (121, 132), "c1_ring": (0, 0),                   # role-flip steps: a8 + a9 on the halo ring only
+    "c2": (81, 128), "c2_full": (121, 168),
+    "ca": (145, 145), "ca_hh": (169, 169),                  # hh_init + next step's A (+ a2's stores)
 }
-FLIP_BYTES = {"fused_b": {"first": 209, "mid": 193}, "fused_c1": {"first": 0, "mid": 0}}
+
+
+def call_launches(steps: int, flip: bool):
+    """The launches of one ocn_ctx_step call of `steps` steps, as (timer, launch kind) pairs --
+    ocn_ctx.hip ocn_ctx_step / one_step_fused for one block (role-flip calls fuse each step's
+    hh_init with the next step's A when full_free_surface = 1, as in sw.par)."""
+    out = []
+    for s in range(1, steps + 1):
+        first, last = s == 1, s == steps
+        reuse = not first and not last
+        flip_step = flip and not last and steps >= 2
+        if not (flip and steps >= 2 and not first):
+            out.append(("fused_a", "a_reuse" if reuse else "a"))
+        if flip_step:
+            out += [("fused_b", "b_flip_reuse" if reuse else "b_flip"), ("fused_c1", "c1_ring"),
+                    ("fused_ca", "ca" if s + 1 < steps else "ca_hh")]
+        else:
+            out += [("fused_b", "b_full" if last else "b_reuse" if reuse else "b"), ("fused_c1", "c1"),
+                    ("hh_init", "c2_full" if last else "c2")]
+    return out
 
 
 def fused_bytes(compact: bool, steps: int, flip: bool = False):
-    """Mean bytes per interior cell per launch over one ocn_ctx_step call of `steps` steps."""
+    """Mean bytes per interior cell per launch of each timer over one ocn_ctx_step call."""
     i = 0 if compact else 1
-    out = {}
-    for k, kinds in FUSED_BYTES.items():
-        per = {kind: v[i] for kind, v in kinds.items()}
-        if flip and k in FLIP_BYTES:
-            per.update(FLIP_BYTES[k])
-        if steps == 1:
-            v = per["last"]
-        else:
-            v = (per["first"] + (steps - 2) * per["mid"] + per["last"]) / steps
-        out[k] = v
-    return out
+    tot, cnt = {}, {}
+    for timer, kind in call_launches(steps, flip):
+        tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
+        cnt[timer] = cnt.get(timer, 0) + 1
+    return {t: tot[t] / cnt[t] for t in tot}
+
+
+def step_bytes(compact: bool, steps: int, flip: bool = False):
+    """Bytes per interior cell per step moved by one ocn_ctx_step call of `steps` steps."""
+    i = 0 if compact else 1
+    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip)) / steps
 
 
 def dims_create(n: int):
@@ -207,7 +225,7 @@ def main():
     out = None
     if rank == 0:
         kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip)
-        b_path = sum(kbytes.values())
+        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:

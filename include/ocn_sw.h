@@ -306,9 +306,9 @@ enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
- * three tracer stages (summed over tracers). */
+ * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A. */
 enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_TIMER_TRACER,
-       OCN_NUM_TIMERS = OCN_TIMER_TRACER + OCN_NUM_TSTAGES };
+       OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_NUM_TIMERS };
 
 /* Per-timer device time (ms, summed) and launch counts since the last call, from the HIP
  * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_TIMERS entries.  Synchronises. */

@@ -154,6 +154,22 @@ struct HaloPlan {
     int n_pack = 0, n_unpack = 0;
 };
 
+namespace ocn {
+// What one step of an ocn_ctx_step call runs: check = check_ssh_err; first / last step of the
+// call; flip = role-flip step; a_done = its fused A already ran (fused into the previous step's
+// hh_init launch); next_a = fuse the next step's fused A into this step's hh_init (MarchCA),
+// next_reuse = the next step is a reuse step.
+struct StepKind {
+    bool check, first, last, flip, a_done, next_a, next_reuse;
+    bool operator==(const StepKind &o) const
+    {
+        return check == o.check && first == o.first && last == o.last && flip == o.flip && a_done == o.a_done &&
+               next_a == o.next_a && next_reuse == o.next_reuse;
+    }
+};
+
+}  // namespace ocn
+
 struct ocn_ctx {
     ocn_basin basin;
     ocn_sw_params sw;
@@ -171,7 +187,7 @@ struct ocn_ctx {
     std::map<std::vector<int>, HaloPlan> plans;
     bool initialized = false;
     bool use_graph = false;
-    struct Graph { hipGraphExec_t exec; double tau; bool check, first, last, compact, flip; int role; };
+    struct Graph { hipGraphExec_t exec; double tau; ocn::StepKind kind; bool compact; int role; };
     std::vector<Graph> graphs;         // one captured step per (tau, check, last step, compact)
     std::vector<void *> allocs;
     // per-stage HIP-event timing (OCN_OPT_STAGE_TIMING): pending (stage, start, stop) records
@@ -788,8 +804,9 @@ static bool flip_eligible(ocn_ctx *c)
     return c->flip && c->fused && c->compact && c->march && c->sw.use_tracers <= 0 && !has_exchange(c);
 }
 
-static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool last, bool flip)
+static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
+    const bool check = k.check, first = k.first, last = k.last, flip = k.flip;
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
     auto cp = [c](const LBlock &b, Compact &t) -> const Compact * {
@@ -807,9 +824,11 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool l
     const std::vector<int> &sync_a = reuse ? c->sync_a_reuse : c->sync_a;
     if (flip) {
         if (last || has_exchange(c)) return set_error(OCN_ERR_STATE, "role-flip step on a last step or with halos");
-        RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-        for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
-        RC(timer_end(c, rec));
+        if (!k.a_done) {
+            RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
+            for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
+            RC(timer_end(c, rec));
+        }
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
         for (const LBlock &b : c->blocks)
             RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, reuse, s, nbad, true));
@@ -818,18 +837,27 @@ static int one_step_fused(ocn_ctx *c, double tau, bool check, bool first, bool l
         for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_FRAME, sw, nullptr, s));
         RC(timer_end(c, rec));
         swap_roles(c);
-        if (ffs) {
+        if (k.next_a) {   // hh_init + the next step's fused A (full_free_surface = 1)
+            RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
+            for (const LBlock &b : c->blocks)
+                RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.next_reuse, s));
+            RC(timer_end(c, rec));
+        } else if (ffs) {
             RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
             for (const LBlock &b : c->blocks) RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, full_c2, s));
             RC(timer_end(c, rec));
         }
         return OCN_OK;
     }
+    if (k.a_done && (c->overlap && has_exchange(c)))
+        return set_error(OCN_ERR_STATE, "fused A merged into the previous step with halos");
     if (!(c->overlap && has_exchange(c))) {
-        RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
-        RC(timer_end(c, rec));
+        if (!k.a_done) {
+            RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
+            for (const LBlock &b : c->blocks)
+                RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
+            RC(timer_end(c, rec));
+        }
         RC(run_sync(c, sync_a));
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
         for (const LBlock &b : c->blocks)
@@ -1290,28 +1318,27 @@ static void drop_graphs(ocn_ctx *c)
 }
 
 // one model step (model.f90:146-160): expl_shallow_water, then expl_tracer
-static int run_step(ocn_ctx *c, double tau, bool check, bool first, bool last, bool flip)
+static int run_step(ocn_ctx *c, double tau, const StepKind &k)
 {
-    RC(c->fused ? one_step_fused(c, tau, check, first, last, flip) : one_step(c, tau, check));
+    RC(c->fused ? one_step_fused(c, tau, k) : one_step(c, tau, k.check));
     return expl_tracer(c, tau, c->fused && c->compact);
 }
 
-// one step as a replayed hipGraph, captured once per (tau, check, first, last, compact, flip,
-// role); a role-flip step swaps the host's pointer roles as the captured launches did
-static int graph_step(ocn_ctx *c, double tau, bool check, bool first, bool last, bool flip)
+// one step as a replayed hipGraph, captured once per (tau, step kind, compact, role); a
+// role-flip step swaps the host's pointer roles as the captured launches did
+static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
 {
     for (const auto &g : c->graphs)
-        if (g.tau == tau && g.check == check && g.first == first && g.last == last && g.compact == c->compact &&
-            g.flip == flip && g.role == c->role) {
+        if (g.tau == tau && g.kind == k && g.compact == c->compact && g.role == c->role) {
             HIPCHK(hipGraphLaunch(g.exec, c->stream));
-            if (flip) swap_roles(c);
+            if (k.flip) swap_roles(c);
             return OCN_OK;
         }
     if (c->graphs.size() >= 16) drop_graphs(c);
     const int role = c->role;
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = run_step(c, tau, check, first, last, flip);
+    int rc = run_step(c, tau, k);
     hipError_t e = hipStreamEndCapture(c->stream, &graph);
     if (rc) return rc;
     HIPCHK(e);
@@ -1319,7 +1346,7 @@ static int graph_step(ocn_ctx *c, double tau, bool check, bool first, bool last,
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     HIPCHK(e);
-    c->graphs.push_back(ocn_ctx::Graph{exec, tau, check, first, last, c->compact, flip, role});
+    c->graphs.push_back(ocn_ctx::Graph{exec, tau, k, c->compact, role});
     HIPCHK(hipGraphLaunch(exec, c->stream));
     return OCN_OK;
 }
@@ -1345,12 +1372,19 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
     if (flip_call && !c->coherent_known) RC(check_coherence(c));
     flip_call = flip_call && c->coherent;
     c->flip_used = flip_call;
+    // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A
+    const bool ca = flip_call && c->sw.full_free_surface == 1;
     int rc = OCN_OK;
     for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
-        const bool check = check_every > 0 && (s % check_every == 0);
-        const bool first = s == 1, last = s == nsteps;
-        const bool flip = flip_call && !last;
-        rc = graph_ok ? graph_step(c, tau, check, first, last, flip) : run_step(c, tau, check, first, last, flip);
+        StepKind k;
+        k.check = check_every > 0 && (s % check_every == 0);
+        k.first = s == 1;
+        k.last = s == nsteps;
+        k.flip = flip_call && !k.last;
+        k.a_done = ca && !k.first;
+        k.next_a = ca && k.flip;
+        k.next_reuse = k.next_a && s + 1 < nsteps;
+        rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
     }
     // the last (standard) step left both buffers of each pair equal: undo the swap by pointers
     if (c->role) swap_roles(c);

@@ -606,6 +606,169 @@ struct MarchHhInit {
     }
 };
 
+// ------------------------------------------------------------------ fused CA = hh_init + next A
+// Role-flip calls (ocn_ctx.hip one_step_fused): step k's a10 hh_init and step k+1's fused A in
+// one aligned march over the bnd range.  A's a1 reads hhu at (m-1, n), (m, n) and hhv at
+// (m, n-1), (m, n): exactly the hu / hv that hh_init computes here (level 0), so they come from
+// registers: hv of row n-1 is carried from the previous row (a "warm" first row computes it
+// for the tile's first row), hu at m-1 is the next lane's value, and the edge lane 0 evaluates
+// interp_u one column to the left itself (same operands, same arithmetic as the neighbouring
+// wave's lane 63: the same bits).  Where llu / llv is 0 hh_init stores nothing and a1 reads the
+// array's (never written) value from memory.  HH: the next step is not a reuse step, so A's a2
+// hh_update stores hun / hvn / hhn -- bit for bit hh_init's level-0 values (the reuse identity,
+// full_free_surface = 1), under the same masks on the same range.  Nothing this launch writes
+// is read at a neighbour, so there are no races.
+struct MarchViewCA {
+    RowsD<false, true, true> rHR, rSH, rSHP, rU, rUP;  // h_r, ssh, sshp, ubrtr, ubrtrp
+    RowsD<true, false, true> rV, rVP;                  // vbrtr, vbrtrp
+    RowsD<false, false, true> rHU;                     // hhu: c = this column, ec = column m-1 (lane 0)
+    RowsD<true, false> rHV;                            // hhv: rows n-1, n
+    BitRows<false, true, true> bits;
+    MetRows met;
+    double tau;
+    __device__ __forceinline__ double tau2() const { return tau; }
+    OCN_MV(h_r, rHR) OCN_MV(sh, rSH) OCN_MV(shp, rSHP) OCN_MV(sshp, rSHP) OCN_MV(u, rU) OCN_MV(ubrtr, rU)
+    OCN_MV(up, rUP) OCN_MV(v, rV) OCN_MV(vbrtr, rV) OCN_MV(vp, rVP) OCN_MV(hhu, rHU) OCN_MV(hhv, rHV)
+    OCN_MG_ALL
+    __device__ __forceinline__ float lu(int dx, int dy) const { return bits.mask(OCN_LU, dx, dy); }
+};
+// the interpolation operands one column to the left (interp_u at m-1)
+struct LeftView {
+    const MarchViewCA &x;
+    __device__ __forceinline__ float lu(int dx, int dy) const { return x.lu(dx - 1, dy); }
+    __device__ __forceinline__ float dx(int i, int dy) const { return x.dx(i - 1, dy); }
+    __device__ __forceinline__ float dy(int i, int dy) const { return x.dy(i - 1, dy); }
+    __device__ __forceinline__ float dxt(int i, int dy) const { return x.dxt(i - 1, dy); }
+    __device__ __forceinline__ float dyh(int i, int dy) const { return x.dyh(i - 1, dy); }
+};
+
+template <bool HH> struct MarchCA {
+    static constexpr bool kAligned = true;
+    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau;
+    struct Fn {
+        HhInit<true> c2; FusedA<true> a; const Tab<true> &t; int ylast;
+        // row n: h_r, ssh, sshp, mask bytes, ubrtr, ubrtrp at n+1 (clamped to bnd_y2); vbrtr,
+        // vbrtrp at n; their edge values; metric row n+1
+        struct Batch { double nn[5], c[2], enn[5], ec[2]; unsigned bits, ebits; float g[kNumRowFields]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
+        {
+            const int r = min(n + 1, ylast), r0 = max(n, (int)c2.I.by1);
+            const Pt cn = c2.I(L.m, r), c = c2.I(L.m, r0);
+            q.nn[0] = ld(c2.h_r, cn); q.nn[1] = ld(c2.sh, cn); q.nn[2] = ld(c2.shp, cn);
+            q.nn[3] = ld(a.a1.ubrtr, cn); q.nn[4] = ld(a.a5.u, cn); q.bits = ld(t.bits, cn);
+            q.c[0] = ld(a.a1.vbrtr, c); q.c[1] = ld(a.a5.v, c);
+            for (int i = 0; i < 5; ++i) q.enn[i] = 0.0;
+            q.ec[0] = q.ec[1] = 0.0;
+            q.ebits = 0;
+            if (L.edge) {
+                const Pt en = c2.I(L.me, r), e = c2.I(L.me, r0);
+                q.enn[0] = ld(c2.h_r, en); q.enn[1] = ld(c2.sh, en); q.enn[2] = ld(c2.shp, en);
+                q.enn[3] = ld(a.a1.ubrtr, en); q.enn[4] = ld(a.a5.u, en); q.ebits = ld(t.bits, en);
+                q.ec[0] = ld(a.a1.vbrtr, e); q.ec[1] = ld(a.a5.v, e);
+            }
+            MetRows::load(q.g, t.rows, t.nrows, cn.r);
+        }
+        // warm = the row before the tile's first row: only hv (for a1's hhv(m, n-1)) is computed
+        __device__ __forceinline__ void row(MarchViewCA &x, const Batch &q, const Lane &L, int n, bool warm) const
+        {
+            const Pt c = c2.I(L.m, max(n, (int)c2.I.by1));
+            const double f = c2.f;
+            x.rV.s = x.rV.c; x.rV.es = x.rV.ec; x.rVP.s = x.rVP.c; x.rVP.es = x.rVP.ec; x.rHV.s = x.rHV.c;
+            x.met.shift(q.g);
+            x.rHR.nn = q.nn[0]; x.rSH.nn = q.nn[1]; x.rSHP.nn = q.nn[2]; x.rU.nn = q.nn[3]; x.rUP.nn = q.nn[4];
+            x.rHR.enn = q.enn[0]; x.rSH.enn = q.enn[1]; x.rSHP.enn = q.enn[2]; x.rU.enn = q.enn[3];
+            x.rUP.enn = q.enn[4];
+            x.bits.nn = q.bits; x.bits.enn = q.ebits;
+            x.rV.c = q.c[0]; x.rVP.c = q.c[1]; x.rV.ec = q.ec[0]; x.rVP.ec = q.ec[1];
+            const unsigned bc = x.bits.c;
+            const bool llu = bc & (1u << OCN_LLU), llv = bc & (1u << OCN_LLV), luh = bc & (1u << OCN_LUH);
+            const bool in_rows = n >= c2.j0 && n <= c2.j1;   // wave-uniform
+            if (warm) {
+                if (in_rows) {
+                    const double a00 = x.rHR.c + x.rSH.c * f, a01 = x.rHR.nn + x.rSH.nn * f;
+                    const double v0 = interp_v(x, a00, a01);
+                    x.rHV.c = llv ? v0 : ld(c2.hv, c);
+                }
+                goto rotate;
+            }
+            {
+                const double r00 = x.rHR.c;
+                if (L.out) st(c2.hq, c, r00 + x.rSH.c * f);
+                if (in_rows) {
+                    HhInitOut o;
+                    hh_init_math(x, f, false, o);
+                    const bool inr = L.out && L.m >= c2.i0 && L.m <= c2.i1;
+                    if (inr) {
+                        if (llu) { st(c2.hu, c, o.u[0]); st(c2.hup, c, o.u[1]); }
+                        if (llv) { st(c2.hv, c, o.v[0]); st(c2.hvp, c, o.v[1]); }
+                        if (luh) { st(c2.hh, c, o.h[0]); st(c2.hhp, c, o.h[1]); }
+                        if (HH) {
+                            if (llu) st(a.a2.hun, c, o.u[0]);
+                            if (llv) st(a.a2.hvn, c, o.v[0]);
+                            if (luh) st(a.a2.hhn, c, o.h[0]);
+                        }
+                    }
+                    // a1's hhu / hhv: the values memory holds after this launch
+                    x.rHU.c = llu ? o.u[0] : ld(c2.hu, c);
+                    x.rHV.c = llv ? o.v[0] : ld(c2.hv, c);
+                    {   // hu at m-1 (used by lane 0 only)
+                        const LeftView lv{x};
+                        const double aw = x.h_r(-1, 0) + x.sh(-1, 0) * f, a00 = r00 + x.rSH.c * f;
+                        const double uw = interp_u(lv, aw, a00);
+                        const bool lluw = x.bits.at(-1, 0) & (1u << OCN_LLU);
+                        x.rHU.ec = lluw ? uw : ld(c2.hu, c2.I(L.me, max(n, (int)c2.I.by1)));
+                    }
+                }
+                if (n >= a.sy && n <= b_ye) {   // A's a1 / a3 / a5 on [start, end]^2 (wave-uniform rows)
+                    const bool in = L.out && L.m >= a.sx && L.m <= b_xe;
+                    const double rs = sw_update_ssh_math(x);
+                    if (in && (bc & (1u << OCN_LU))) st(a.a1.sshn, c, rs);
+                    if (a.do_vort) {
+                        const double v = uv_trans_vort_math(x);
+                        if (in && (bc & (1u << OCN_LUU))) st(a.a3.vort, c, v);
+                    }
+                    if (a.do_stress) {
+                        double vt, vs;
+                        stress_components_math(x, vt, vs);
+                        if (in && (bc & (1u << OCN_LU))) st(a.a5.str_t, c, vt);
+                        if (in && (bc & (1u << OCN_LUU))) st(a.a5.str_s, c, vs);
+                    }
+                }
+            }
+        rotate:
+            x.rHR.rotate(); x.rSH.rotate(); x.rSHP.rotate(); x.rU.rotate(); x.rUP.rotate(); x.bits.rotate();
+        }
+        int b_xe, b_ye;
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{make_hh_init(&b, t, (int)sw.full_free_surface, false), make_fused_a(&b, t, sw, tau, !HH), t,
+                   b.bnd_y2, b.nx_end, b.ny_end};
+        MarchViewCA x{};
+        x.tau = tau;
+        // the warm row nb-1 (when it exists) precedes the tile's rows
+        const int n0 = max(nb - 1, b.bnd_y1);
+        const Pt c = f.c2.I(L.m, n0);
+        x.rHR.c = ld(f.c2.h_r, c); x.rSH.c = ld(f.c2.sh, c); x.rSHP.c = ld(f.c2.shp, c);
+        x.rU.c = ld(f.a.a1.ubrtr, c); x.rUP.c = ld(f.a.a5.u, c); x.bits.c = ld(t.bits, c);
+        if (L.edge) {
+            const Pt e = f.c2.I(L.me, n0);
+            x.rHR.ec = ld(f.c2.h_r, e); x.rSH.ec = ld(f.c2.sh, e); x.rSHP.ec = ld(f.c2.shp, e);
+            x.rU.ec = ld(f.a.a1.ubrtr, e); x.rUP.ec = ld(f.a.a5.u, e); x.bits.ec = ld(t.bits, e);
+        }
+        x.met.preload(t.rows, t.nrows, c.r, c.r);
+        typename Fn::Batch cur, nxt;
+        f.load(cur, L, n0);
+        for (int n = n0; n <= ne; ++n) {
+            f.row(x, cur, L, n, n < nb);
+            if (n < ne) {
+                f.load(nxt, L, n + 1);
+                cur = nxt;
+            }
+        }
+    }
+};
+
 #define CHECK(...)                                                \
     do {                                                          \
         int _rc = check_block(b);                                 \
@@ -709,6 +872,17 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compac
     }
     return launch_fused<KHhInit>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s,
                                  (int)sw.full_free_surface, full);
+}
+
+int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                    double tau_next, bool next_reuse, hipStream_t s)
+{
+    if (!cp || !cp->march || sw.full_free_surface != 1)
+        return set_error(OCN_ERR_ARG, "fused hh_init + A needs the compact tables, the march and full_free_surface = 1");
+    RC_K(check_block(b));
+    const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
+    if (next_reuse) return launch_march(b, range_bnd(b), MarchCA<false>{*b, t, sw, tau_next}, s);
+    return launch_march(b, range_bnd(b), MarchCA<true>{*b, t, sw, tau_next}, s);
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy

@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 STAGE = {"KFusedA": "fused_a", "KFusedB": "fused_b", "MarchFusedB": "fused_b", "KFusedC1": "fused_c1",
-         "KHhInit": "hh_init", "MarchHhInit": "hh_init", "MarchFusedA": "fused_a"}
+         "KHhInit": "hh_init", "MarchHhInit": "hh_init", "MarchFusedA": "fused_a", "MarchCA": "fused_ca"}
 
 
 def means(root):
