@@ -39,13 +39,14 @@ LAUNCH_BYTES = {
     "a": (129, 180), "a_reuse": (89, 128),
     "b": (169, 220), "b_reuse": (153, 204), "b_full": (201, 252),
     "b_flip": (209, 260), "b_flip_reuse": (193, 244),     # + a8's filters: sshn, sshp in; sshp, ubrtrp, vbrtrp out
+    "b_flip_rc": (177, 177),                               # hhq, hhu_p, hhv_p formed from h_r, ssh, sshp
     "c1": (121, 132), "c1_ring": (0, 0),                   # role-flip steps: a8 + a9 on the halo ring only
     "c2": (81, 128), "c2_full": (121, 168),
-    "ca": (145, 145), "ca_hh": (169, 169),                  # hh_init + next step's A (+ a2's stores)
-}
+    "ca": (113, 113), "ca_store": (137, 137), "ca_hh": (161, 161),   # hh_init + next step's A (no hhh_p;
+}   # "ca": next step recomputes -- no interior hhq, hhu_p, hhv_p; "ca_hh": + a2's stores)
 
 
-def call_launches(steps: int, flip: bool):
+def call_launches(steps: int, flip: bool, rc: bool = True):
     """The launches of one ocn_ctx_step call of `steps` steps, as (timer, launch kind) pairs --
     ocn_ctx.hip ocn_ctx_step / one_step_fused for one block (role-flip calls fuse each step's
     hh_init with the next step's A when full_free_surface = 1, as in sw.par)."""
@@ -56,29 +57,29 @@ def call_launches(steps: int, flip: bool):
         flip_step = flip and not last and steps >= 2
         if not (flip and steps >= 2 and not first):
             out.append(("fused_a", "a_reuse" if reuse else "a"))
-        if flip_step:
-            out += [("fused_b", "b_flip_reuse" if reuse else "b_flip"), ("fused_c1", "c1_ring"),
-                    ("fused_ca", "ca" if s + 1 < steps else "ca_hh")]
+        if flip_step:   # ring launch skipped when no halo-ring point has a8 / a9 work (the box)
+            out += [("fused_b", "b_flip" if first else "b_flip_rc" if rc else "b_flip_reuse"),
+                    ("fused_ca", "ca_hh" if s + 1 >= steps else "ca" if rc else "ca_store")]
         else:
             out += [("fused_b", "b_full" if last else "b_reuse" if reuse else "b"), ("fused_c1", "c1"),
                     ("hh_init", "c2_full" if last else "c2")]
     return out
 
 
-def fused_bytes(compact: bool, steps: int, flip: bool = False):
+def fused_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True):
     """Mean bytes per interior cell per launch of each timer over one ocn_ctx_step call."""
     i = 0 if compact else 1
     tot, cnt = {}, {}
-    for timer, kind in call_launches(steps, flip):
+    for timer, kind in call_launches(steps, flip, rc):
         tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
         cnt[timer] = cnt.get(timer, 0) + 1
     return {t: tot[t] / cnt[t] for t in tot}
 
 
-def step_bytes(compact: bool, steps: int, flip: bool = False):
+def step_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True):
     """Bytes per interior cell per step moved by one ocn_ctx_step call of `steps` steps."""
     i = 0 if compact else 1
-    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip)) / steps
+    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc)) / steps
 
 
 def dims_create(n: int):
@@ -160,6 +161,7 @@ def main():
     ap.add_argument("--no-compact", action="store_true", help="fused step on the 2-D real(4) arrays")
     ap.add_argument("--no-march", action="store_true", help="one thread per point in every launch (no register march)")
     ap.add_argument("--no-flip", action="store_true", help="standard steps only (no role-flip steps)")
+    ap.add_argument("--no-recompute", action="store_true", help="role-flip calls without the recompute steps")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -193,6 +195,7 @@ def main():
     model.set_compact(not args.no_compact)
     model.set_march(not args.no_march)
     model.set_flip(not args.no_flip)
+    model.set_recompute(not args.no_recompute)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -224,8 +227,9 @@ def main():
     local_cells = model.interior_cells
     out = None
     if rank == 0:
-        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip)
-        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip)
+        rc = not args.no_recompute
+        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc)
+        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:

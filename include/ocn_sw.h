@@ -298,12 +298,15 @@ int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
  *  the pointers of ocn_ctx_field are the same after the call).  Needs the pairs to agree outside
  *  their write sets, which holds from ocn_ctx_init_state on and is checked on the device
  *  whenever those fields were uploaded or handed out; otherwise the standard step runs.
+ *  OCN_OPT_RECOMPUTE (default 1): in such calls (full_free_surface = 1, no a8 / a9 work on the
+ *  halo ring), steps 2..K-1 form hhq, hhu_p, hhv_p inside fused B instead of storing and
+ *  re-reading them (same results bit for bit).
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps. */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
-       OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7 };
+       OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A. */

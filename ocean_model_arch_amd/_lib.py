@@ -74,6 +74,7 @@ OPT_FUSED = 4
 OPT_COMPACT = 5
 OPT_MARCH = 6
 OPT_FLIP = 7
+OPT_RECOMPUTE = 8
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",

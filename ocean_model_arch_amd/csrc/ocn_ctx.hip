@@ -141,6 +141,7 @@ struct LBlock {
     std::vector<void *> ptr;           // field table, indexed by field_slot(id)
     uint8_t *bits = nullptr;           // compact static fields (sw_stencils.h): mask bytes
     float *rows = nullptr;             // and metric row tables
+    void *sshp_alt = nullptr;          // second sshp buffer of the recompute steps (one_step_fused)
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
@@ -158,13 +159,15 @@ namespace ocn {
 // What one step of an ocn_ctx_step call runs: check = check_ssh_err; first / last step of the
 // call; flip = role-flip step; a_done = its fused A already ran (fused into the previous step's
 // hh_init launch); next_a = fuse the next step's fused A into this step's hh_init (MarchCA),
-// next_reuse = the next step is a reuse step.
+// next_reuse = the next step is a reuse step; rc = recompute steps (fused B forms hhq, hhu_p,
+// hhv_p itself and writes sshp's filter into the second sshp buffer), rc_next = the next step is
+// one (this step's hh_init + A launch then does not store hhq on the interior, hhu_p, hhv_p).
 struct StepKind {
-    bool check, first, last, flip, a_done, next_a, next_reuse;
+    bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next;
     bool operator==(const StepKind &o) const
     {
         return check == o.check && first == o.first && last == o.last && flip == o.flip && a_done == o.a_done &&
-               next_a == o.next_a && next_reuse == o.next_reuse;
+               next_a == o.next_a && next_reuse == o.next_reuse && rc == o.rc && rc_next == o.rc_next;
     }
 };
 
@@ -210,6 +213,8 @@ struct ocn_ctx {
     // after the state last changed outside ocn_ctx_step; r8_escaped = raw pointers of a pair were
     // handed out (check at every call); flip = OCN_OPT_FLIP
     bool flip = true, coherent = false, flip_used = false;
+    bool ring_sea = true;   // some halo-ring point has a mask set (Prepare); else no ring launch
+    bool recompute = true;  // OCN_OPT_RECOMPUTE: recompute steps in role-flip calls
     mutable bool coherent_known = false, r8_escaped = false;
     int role = 0;
     int32_t *d_flags = nullptr;
@@ -359,6 +364,10 @@ static int allocate(ocn_ctx *c)
         c->allocs.push_back(b.bits);
         HIPCHK(hipMalloc(&b.rows, nrow * sizeof(float)));
         c->allocs.push_back(b.rows);
+        void *alt = nullptr;   // laid out as the slab's r8 fields (rows 256-B aligned at nx_start)
+        HIPCHK(hipMalloc(&alt, n * 8 + 512));
+        c->allocs.push_back(alt);
+        b.sshp_alt = (char *)alt + 256 - 16;
     }
     HIPCHK(hipMalloc(&c->d_nbad, 256));
     c->allocs.push_back(c->d_nbad);
@@ -720,7 +729,8 @@ static int prepare_static(ocn_ctx *c)
     int32_t flags = 0;
     HIPCHK(hipMemcpyAsync(&flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    c->compact = flags == 0;
+    c->ring_sea = (flags & kCompactRingSea) != 0;
+    c->compact = (flags & ~kCompactRingSea) == 0;
     c->static_dirty = false;
     return OCN_OK;
 }
@@ -768,6 +778,13 @@ static void swap_roles(ocn_ctx *c)
         for (const auto &pr : kFlipPairs) std::swap(b.ptr[field_slot(pr[0])], b.ptr[field_slot(pr[1])]);
     c->role ^= 1;
 }
+// recompute steps: sshp and its second buffer trade places (role bit 2)
+static void swap_sshp(ocn_ctx *c)
+{
+    for (LBlock &b : c->blocks) std::swap(b.ptr[field_slot(OCN_SSHP)], b.sshp_alt);
+    c->role ^= 2;
+}
+static size_t field_bytes(const LBlock &b) { return (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1) * 8; }
 static bool is_flip_field(int id)
 {
     for (const auto &pr : kFlipPairs)
@@ -831,16 +848,21 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         }
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
         for (const LBlock &b : c->blocks)
-            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, reuse, s, nbad, true));
+            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, reuse, s, nbad, true, k.rc,
+                              (double *)b.sshp_alt));
         RC(timer_end(c, rec));
-        RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));   // a8 + a9 on the ring (no interior points)
-        for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_FRAME, sw, nullptr, s));
-        RC(timer_end(c, rec));
+        if (k.rc) swap_sshp(c);
+        if (c->ring_sea) {   // a8 + a9 on the ring (no interior points); nothing to do on an all-land ring
+            RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
+            for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_FRAME, sw, nullptr, s));
+            RC(timer_end(c, rec));
+        }
         swap_roles(c);
         if (k.next_a) {   // hh_init + the next step's fused A (full_free_surface = 1)
             RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
             for (const LBlock &b : c->blocks)
-                RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.next_reuse, s));
+                RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.next_reuse,
+                                   k.next_reuse && k.rc_next, s));
             RC(timer_end(c, rec));
         } else if (ffs) {
             RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
@@ -1331,6 +1353,7 @@ static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
     for (const auto &g : c->graphs)
         if (g.tau == tau && g.kind == k && g.compact == c->compact && g.role == c->role) {
             HIPCHK(hipGraphLaunch(g.exec, c->stream));
+            if (k.rc) swap_sshp(c);
             if (k.flip) swap_roles(c);
             return OCN_OK;
         }
@@ -1372,8 +1395,15 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
     if (flip_call && !c->coherent_known) RC(check_coherence(c));
     flip_call = flip_call && c->coherent;
     c->flip_used = flip_call;
-    // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A
+    // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A;
+    // their reuse steps recompute hhq / hhu_p / hhv_p in fused B when no a8 / a9 work lies on the
+    // halo ring (so sshp's two buffers only differ where fused B writes)
     const bool ca = flip_call && c->sw.full_free_surface == 1;
+    const bool rc_call = ca && !c->ring_sea && c->recompute;
+    if (rc_call)   // the second sshp buffer starts as a copy: the two agree outside fused B's write set
+        for (const LBlock &b : c->blocks)
+            HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
+                                  c->stream));
     int rc = OCN_OK;
     for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
         StepKind k;
@@ -1384,10 +1414,19 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
         k.a_done = ca && !k.first;
         k.next_a = ca && k.flip;
         k.next_reuse = k.next_a && s + 1 < nsteps;
+        k.rc = rc_call && k.flip && !k.first;
+        k.rc_next = rc_call && s + 1 < nsteps;
         rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
     }
-    // the last (standard) step left both buffers of each pair equal: undo the swap by pointers
-    if (c->role) swap_roles(c);
+    // the last (standard) step left both buffers of each pair equal: undo the swap by pointers;
+    // sshp's buffers are not equal: the current one is copied into the field's own buffer
+    if (c->role & 1) swap_roles(c);
+    if (c->role & 2) {
+        for (LBlock &b : c->blocks)
+            HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
+                                  c->stream));
+        swap_sshp(c);
+    }
     return rc;
 }
 
@@ -1459,6 +1498,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         return OCN_OK;
     case OCN_OPT_MARCH: c->march = value != 0; return OCN_OK;
     case OCN_OPT_FLIP: c->flip = value != 0; return OCN_OK;
+    case OCN_OPT_RECOMPUTE: c->recompute = value != 0; return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -1479,6 +1519,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_COMPACT: *value = c->fused && c->compact; return OCN_OK;
     case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
+    case OCN_OPT_RECOMPUTE: *value = c->recompute; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -59,24 +59,28 @@ enum { OCN_PART_ALL = 0, OCN_PART_FRAME = 1, OCN_PART_INNER = 2 };
 int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool reuse, hipStream_t s);
 // flip: the role-flip form (sw_kernels.hip MarchFusedB<true>: + a8's filters and check_ssh_err
-// into flip_nbad on the interior; needs cp->march)
+// into flip_nbad on the interior; needs cp->march); rc: hhq / hhu_p / hhv_p recomputed from
+// h_r, ssh, sshp (after a MarchCA<false>, which does not store them)
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s,
-                   int32_t *flip_nbad = nullptr, bool flip = false);
+                   int32_t *flip_nbad = nullptr, bool flip = false, bool rc = false, double *sshp_out = nullptr);
 int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, int32_t *nbad, hipStream_t s);
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, bool full, hipStream_t s);
 // Role-flip calls: step k's hh_init (non-final) and step k+1's fused A in one launch
-// (sw_kernels.hip MarchCA); next_reuse = step k+1 is a reuse step (else A's a2 stores too).
+// (sw_kernels.hip MarchCA); next_reuse = step k+1 is a reuse step (else A's a2 stores too);
+// skip_rc = step k+1 is a recompute step (hhq on the interior, hhu_p, hhv_p not stored).
 int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
-                    double tau_next, bool next_reuse, hipStream_t s);
+                    double tau_next, bool next_reuse, bool skip_rc, hipStream_t s);
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);
 // ORs 1 into *flags (device int) if a buffer pair of the role-flip step differs outside the
 // pair's write set (sw_stencils.h Coherence).
 int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int32_t *flags, hipStream_t s);
+// Prepare's flag bit reporting mask bits on the halo ring (sw_stencils.h OCN_COMPACT_RING_SEA)
+constexpr int kCompactRingSea = 4;
 // Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
 // they cannot be used into *flags (device int).
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s);

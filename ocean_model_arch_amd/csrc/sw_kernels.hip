@@ -298,27 +298,36 @@ __device__ __forceinline__ void march_rows(const F &k, V &x, const Lane &L, int 
 // The view of fused B's three stages (sw_stencils.h uv_trans_math / uv_diff2_math /
 // sw_update_uv_math) over the march registers.  Accessor names follow the stage functors; an
 // array named twice there (u = ubrtr, hu = hhu, hh = hhh) is one register set here.
-struct MarchViewB {
+// RC ("recompute"): hhq = h_r + ssh * ffs is formed from h_r and ssh (hh_init's whole-array
+// formula) instead of being read; hhu_p / hhv_p are set by the march from sshp (see MarchFusedB).
+template <bool RC> struct MarchViewB {
     RowsD<true, true> rU, rV, rHV, rMU;                // ubrtr, vbrtr, hhv, mu
-    RowsD<false, true> rHU, rHQ, rSTT, rSSH;           // hhu, hhq, str_t, ssh
+    RowsD<false, true> rHU, rHQ, rSTT, rSSH, rHR, rSHP; // hhu, hhq (or h_r, sshp when RC), str_t, ssh
     RowsD<true, false> rVORT, rHH, rSTS;               // vort, hhh, str_s
     Here hhun_, hhup_, hhvn_, hhvp_, ubrtrp_, vbrtrp_, rhsx_, rhsy_;
-    unsigned bits_s, bits_c;                           // mask bytes at (m, n-1), (m, n)
+    BitRows<true, true> bits;                          // mask bytes (row n+1 only when RC)
     MetRows met;                                       // metric rows n-1, n, n+1 (compact tables)
-    double tau;
+    double tau, f;
     __device__ __forceinline__ double quot(double a, double b, int, int) const { return a / b; }
     __device__ __forceinline__ double qtau(double a) const { return a / tau; }
     OCN_MV(u, rU) OCN_MV(ubrtr, rU) OCN_MV(v, rV) OCN_MV(vbrtr, rV) OCN_MV(hu, rHU) OCN_MV(hhu, rHU)
-    OCN_MV(hv, rHV) OCN_MV(hhv, rHV) OCN_MV(hh, rHH) OCN_MV(hhh, rHH) OCN_MV(mu, rMU) OCN_MV(hq, rHQ)
+    OCN_MV(hv, rHV) OCN_MV(hhv, rHV) OCN_MV(hh, rHH) OCN_MV(hhh, rHH) OCN_MV(mu, rMU)
     OCN_MV(vort, rVORT) OCN_MV(str_t, rSTT) OCN_MV(str_s, rSTS) OCN_MV(ssh, rSSH)
     OCN_MV(hhun, hhun_) OCN_MV(hhup, hhup_) OCN_MV(hhvn, hhvn_) OCN_MV(hhvp, hhvp_) OCN_MV(ubrtrp, ubrtrp_)
     OCN_MV(vbrtrp, vbrtrp_) OCN_MV(RHSx, rhsx_) OCN_MV(RHSy, rhsy_)
+    OCN_MV(h_r, rHR) OCN_MV(shp, rSHP)
     OCN_MG_ALL OCN_MG(rlh_s, OCN_RLH_S) OCN_MG(rdis, OCN_R_DISS)
+    __device__ __forceinline__ double hq(int dx, int dy) const
+    {
+        if constexpr (RC) return rHR.at(dx, dy) + rSSH.at(dx, dy) * f;   // depth.f90:48 hq = h_r + sh*ffs
+        else return rHQ.at(dx, dy);
+    }
     __device__ __forceinline__ float luu(int dx, int dy) const
     {
         if (dx != 0 || dy < -1 || dy > 0) ocn_march_bad_access();
-        return ((dy < 0 ? bits_s : bits_c) & (1u << OCN_LUU)) ? 1.0f : 0.0f;
+        return (bits.at(0, dy) & (1u << OCN_LUU)) ? 1.0f : 0.0f;
     }
+    __device__ __forceinline__ float lu(int dx, int dy) const { return bits.at(dx, dy) & (1u << OCN_LU) ? 1.0f : 0.0f; }
 };
 
 // fused B (sw_stencils.h FusedB) as a register march (offset layout); compact static fields only.
@@ -327,40 +336,63 @@ struct MarchViewB {
 // read only at its own point) and check_ssh_err on the new ssh (= sshn on sea points); a8's
 // copies ssh := sshn, ubrtr := ubrtrn, vbrtr := vbrtrn are not made -- the host swaps the roles
 // of the two buffers of each pair instead, so nothing this launch reads at a neighbour is written.
-template <bool C1F> struct MarchFusedB {
+// RC (role-flip reuse steps after a MarchCA<false>, which did not store hhq, hhu_p, hhv_p on
+// the interior): hhq is formed from h_r + ssh * ffs, and hhu_p / hhv_p are hh_init's level-1
+// interpolations of h_r + sshp * ffs (sw_stencils.h interp_u / interp_v, the same operands and
+// arithmetic as the hh_init that would have stored them; sshp has not changed since) where
+// llu / llv is set, and the array's never-written value elsewhere.  sshp is read at m+1 / n+1
+// here, so a8's new sshp goes to the second sshp buffer (sshp_out), which the host swaps in.
+template <bool C1F, bool RC = false> struct MarchFusedB {
     static constexpr bool kAligned = false;
-    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; bool full, reuse; int32_t *nbad;
-    using View = MarchViewB;
+    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; bool full, reuse; int32_t *nbad; double *sshp_out;
+    using View = MarchViewB<RC>;
     struct Fn {
-        FusedB<true> k; const Tab<true> &t; SwNextStep<true> a8; int *nbad;
-        // row n: ubrtr, vbrtr, hhv, mu, hhu, hhq, str_t, ssh at n+1; vort, hhh, str_s, mask bytes
-        // and the pointwise operands at n; metric row n+1
-        struct Batch { double nn[8], c[3], h[8], p[2]; unsigned bits; float g[kNumRowFields]; };
+        FusedB<true> k; const Tab<true> &t; SwNextStep<true> a8; HhInit<true> c2; int *nbad; double *sshp_out;
+        // row n: ubrtr, vbrtr, hhv, mu, hhu, hhq (RC: h_r and sshp), str_t, ssh at n+1; vort, hhh,
+        // str_s, mask bytes (RC: at n+1) and the pointwise operands at n; metric row n+1
+        struct Batch { double nn[9], c[3], h[8], p[2]; unsigned bits; float g[kNumRowFields]; };
         __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
         {
             const SwUpdateUv<true> &a7 = k.a7;
             const Pt c = a7.I(L.m, n), cn = a7.I(L.m, n + 1);
             q.nn[0] = ld(a7.ubrtr, cn); q.nn[1] = ld(a7.vbrtr, cn); q.nn[2] = ld(a7.hhv, cn);
-            q.nn[3] = ld(k.a6.mu, cn); q.nn[4] = ld(a7.hhu, cn); q.nn[5] = ld(k.a6.hq, cn);
+            q.nn[3] = ld(k.a6.mu, cn); q.nn[4] = ld(a7.hhu, cn);
+            if (RC) { q.nn[5] = ld(c2.h_r, cn); q.nn[8] = ld(a8.sshp, cn); }
+            else q.nn[5] = ld(k.a6.hq, cn);
             q.nn[6] = ld(k.a6.str_t, cn); q.nn[7] = ld(a7.ssh, cn);
             q.c[0] = ld(k.a4.vort, c); q.c[1] = ld(a7.hhh, c); q.c[2] = ld(k.a6.str_s, c);
-            q.bits = ld(t.bits, c);
-            q.h[0] = ld(a7.hhun, c); q.h[1] = ld(a7.hhup, c); q.h[2] = ld(a7.hhvn, c); q.h[3] = ld(a7.hhvp, c);
+            q.bits = ld(t.bits, RC ? cn : c);
+            if (!(RC && k.a7.hhun == k.a7.hhu)) { q.h[0] = ld(a7.hhun, c); q.h[2] = ld(a7.hhvn, c); }
+            if (!RC) { q.h[1] = ld(a7.hhup, c); q.h[3] = ld(a7.hhvp, c); }
             q.h[4] = ld(a7.ubrtrp, c); q.h[5] = ld(a7.vbrtrp, c); q.h[6] = ld(a7.RHSx, c); q.h[7] = ld(a7.RHSy, c);
-            if (C1F) { q.p[0] = ld(a8.sshn, c); q.p[1] = ld(a8.sshp, c); }
+            if (C1F) { q.p[0] = ld(a8.sshn, c); if (!RC) q.p[1] = ld(a8.sshp, c); }
             MetRows::load(q.g, t.rows, t.nrows, cn.r);
         }
         __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
         {
             const SwUpdateUv<true> &a7 = k.a7;
             const Pt c = a7.I(L.m, n);
-            x.rVORT.s = x.rVORT.c; x.rHH.s = x.rHH.c; x.rSTS.s = x.rSTS.c; x.bits_s = x.bits_c;
+            x.rVORT.s = x.rVORT.c; x.rHH.s = x.rHH.c; x.rSTS.s = x.rSTS.c;
             x.met.shift(q.g);
             x.rU.nn = q.nn[0]; x.rV.nn = q.nn[1]; x.rHV.nn = q.nn[2]; x.rMU.nn = q.nn[3];
-            x.rHU.nn = q.nn[4]; x.rHQ.nn = q.nn[5]; x.rSTT.nn = q.nn[6]; x.rSSH.nn = q.nn[7];
-            x.rVORT.c = q.c[0]; x.rHH.c = q.c[1]; x.rSTS.c = q.c[2]; x.bits_c = q.bits;
-            x.hhun_.v = q.h[0]; x.hhup_.v = q.h[1]; x.hhvn_.v = q.h[2]; x.hhvp_.v = q.h[3];
+            x.rHU.nn = q.nn[4]; x.rSTT.nn = q.nn[6]; x.rSSH.nn = q.nn[7];
+            if (RC) { x.rHR.nn = q.nn[5]; x.rSHP.nn = q.nn[8]; x.bits.nn = q.bits; }
+            else { x.rHQ.nn = q.nn[5]; x.bits.s = x.bits.c; x.bits.c = q.bits; }
+            x.rVORT.c = q.c[0]; x.rHH.c = q.c[1]; x.rSTS.c = q.c[2];
+            if (RC && k.a7.hhun == k.a7.hhu) { x.hhun_.v = x.rHU.c; x.hhvn_.v = x.rHV.c; }   // reuse: the same arrays
+            else { x.hhun_.v = q.h[0]; x.hhvn_.v = q.h[2]; }
             x.ubrtrp_.v = q.h[4]; x.vbrtrp_.v = q.h[5]; x.rhsx_.v = q.h[6]; x.rhsy_.v = q.h[7];
+            const unsigned bc = x.bits.c;
+            if (RC) {   // hh_init's level 1 (depth.f90:76-97 with hqp = h_r + sshp*ffs)
+                const double f = x.f;
+                const double b00 = x.rHR.c + x.rSHP.c * f;
+                const double b10 = x.h_r(1, 0) + x.shp(1, 0) * f, b01 = x.rHR.nn + x.rSHP.nn * f;
+                const double up = interp_u(x, b00, b10), vp = interp_v(x, b00, b01);
+                x.hhup_.v = (bc & (1u << OCN_LLU)) ? up : ld(c2.hup, c);
+                x.hhvp_.v = (bc & (1u << OCN_LLV)) ? vp : ld(c2.hvp, c);
+            } else {
+                x.hhup_.v = q.h[1]; x.hhvp_.v = q.h[3];
+            }
 
             double rxa, rya, rxd, ryd;
             if (k.do_adv) uv_trans_math(x, rxa, rya);
@@ -370,12 +402,12 @@ template <bool C1F> struct MarchFusedB {
             double un, vn;
             sw_update_uv_math(x, rxa, rxd, rya, ryd, un, vn);
             if (L.out) {
-                if (x.bits_c & (1u << OCN_LCU)) {
+                if (bc & (1u << OCN_LCU)) {
                     if (k.do_adv && k.full) st(k.a4.RHSx, c, rxa);
                     if (k.do_dif && k.full) st(k.a6.RHSx, c, rxd);
                     st(a7.ubrtrn, c, un);
                 }
-                if (x.bits_c & (1u << OCN_LCV)) {
+                if (bc & (1u << OCN_LCV)) {
                     if (k.do_adv && k.full) st(k.a4.RHSy, c, rya);
                     if (k.do_dif && k.full) st(k.a6.RHSy, c, ryd);
                     st(a7.vbrtrn, c, vn);
@@ -383,34 +415,44 @@ template <bool C1F> struct MarchFusedB {
             }
             if (C1F) {   // a8 on this interior point (SwNextStep::step without the copies)
                 const double ts = a8.ts, xn = q.p[0];
-                const double fx = asselin(x.rSSH.c, xn, q.p[1], ts);
+                const double fx = asselin(x.rSSH.c, xn, RC ? x.rSHP.c : q.p[1], ts);
                 const double fa = asselin(x.rU.c, un, x.ubrtrp_.v, ts), fb = asselin(x.rV.c, vn, x.vbrtrp_.v, ts);
                 if (L.out) {
-                    const bool bl = x.bits_c & (1u << OCN_LU);
-                    if (bl) st(a8.sshp, c, fx);
-                    if (x.bits_c & (1u << OCN_LCU)) st(a8.up, c, fa);
-                    if (x.bits_c & (1u << OCN_LCV)) st(a8.vp, c, fb);
+                    const bool bl = bc & (1u << OCN_LU);
+                    if (bl) st(RC ? sshp_out : a8.sshp, c, fx);   // RC: sshp is read at neighbours here
+                    if (bc & (1u << OCN_LCU)) st(a8.up, c, fa);
+                    if (bc & (1u << OCN_LCV)) st(a8.vp, c, fb);
                     if (nbad && bl && !(xn < 10000.0 && xn > -10000.0)) OCN_ATOMIC_INC(nbad);
                 }
             }
             x.rU.rotate(); x.rV.rotate(); x.rHV.rotate(); x.rMU.rotate();
-            x.rHU.rotate(); x.rHQ.rotate(); x.rSTT.rotate(); x.rSSH.rotate();
+            x.rHU.rotate(); x.rSTT.rotate(); x.rSSH.rotate();
+            if (RC) { x.rHR.rotate(); x.rSHP.rotate(); x.bits.rotate(); }
+            else x.rHQ.rotate();
         }
     };
     __device__ void march(const Lane &L, int nb, int ne) const
     {
-        const Fn f{make_fused_b(&b, t, sw, tau, full, reuse), t, make_sw_next_step(&b, t, sw.time_smooth), (int *)nbad};
+        const Fn f{make_fused_b(&b, t, sw, tau, full, reuse), t, make_sw_next_step(&b, t, sw.time_smooth),
+                   make_hh_init(&b, t, (int)sw.full_free_surface, false), (int *)nbad, sshp_out};
         const SwUpdateUv<true> &a7 = f.k.a7;
-        View x;
+        View x{};
         x.tau = tau;
+        x.f = (double)sw.full_free_surface;
         const Pt s = a7.I(L.m, nb - 1), c = a7.I(L.m, nb);   // rows kept from before the first row
         x.rU.s = ld(a7.ubrtr, s); x.rU.c = ld(a7.ubrtr, c);
         x.rV.s = ld(a7.vbrtr, s); x.rV.c = ld(a7.vbrtr, c);
         x.rHV.s = ld(a7.hhv, s); x.rHV.c = ld(a7.hhv, c);
         x.rMU.s = ld(f.k.a6.mu, s); x.rMU.c = ld(f.k.a6.mu, c);
-        x.rHU.c = ld(a7.hhu, c); x.rHQ.c = ld(f.k.a6.hq, c); x.rSTT.c = ld(f.k.a6.str_t, c); x.rSSH.c = ld(a7.ssh, c);
+        x.rHU.c = ld(a7.hhu, c); x.rSTT.c = ld(f.k.a6.str_t, c); x.rSSH.c = ld(a7.ssh, c);
+        if (RC) {
+            x.rHR.c = ld(f.c2.h_r, c); x.rSHP.c = ld(f.a8.sshp, c);
+            x.bits.s = ld(t.bits, s); x.bits.c = ld(t.bits, c);
+        } else {
+            x.rHQ.c = ld(f.k.a6.hq, c);
+            x.bits.c = ld(t.bits, s);
+        }
         x.rVORT.c = ld(f.k.a4.vort, s); x.rHH.c = ld(a7.hhh, s); x.rSTS.c = ld(f.k.a6.str_s, s);
-        x.bits_c = ld(t.bits, s);
         x.met.preload(t.rows, t.nrows, s.r, c.r);
         march_rows(f, x, L, nb, ne);
     }
@@ -617,7 +659,12 @@ struct MarchHhInit {
 // array's (never written) value from memory.  HH: the next step is not a reuse step, so A's a2
 // hh_update stores hun / hvn / hhn -- bit for bit hh_init's level-0 values (the reuse identity,
 // full_free_surface = 1), under the same masks on the same range.  Nothing this launch writes
-// is read at a neighbour, so there are no races.
+// is read at a neighbour, so there are no races.  hh_init's hhh_p is not stored: on single-block
+// runs its only reader is a9 on the outer ring e+1 (fused C1), outside hh_init's range, and the
+// last step of the call (a standard step) stores it.  SKIP (the next step is a recompute step):
+// hhq on the interior, hhu_p and hhv_p are not stored either -- their only reader, the next
+// step's fused B, recomputes them (MarchFusedB RC); hhq stays stored on the halo rows / columns
+// (a9 on the ring reads it there).
 struct MarchViewCA {
     RowsD<false, true, true> rHR, rSH, rSHP, rU, rUP;  // h_r, ssh, sshp, ubrtr, ubrtrp
     RowsD<true, false, true> rV, rVP;                  // vbrtr, vbrtrp
@@ -642,7 +689,7 @@ struct LeftView {
     __device__ __forceinline__ float dyh(int i, int dy) const { return x.dyh(i - 1, dy); }
 };
 
-template <bool HH> struct MarchCA {
+template <bool HH, bool SKIP> struct MarchCA {
     static constexpr bool kAligned = true;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau;
     struct Fn {
@@ -693,15 +740,17 @@ template <bool HH> struct MarchCA {
             }
             {
                 const double r00 = x.rHR.c;
-                if (L.out) st(c2.hq, c, r00 + x.rSH.c * f);
+                // !HH: the next step's fused B forms hhq itself on the interior (MarchFusedB RC)
+                const bool interior = L.m >= a.sx && L.m <= b_xe && n >= a.sy && n <= b_ye;
+                if (L.out && (!SKIP || !interior)) st(c2.hq, c, r00 + x.rSH.c * f);
                 if (in_rows) {
                     HhInitOut o;
                     hh_init_math(x, f, false, o);
                     const bool inr = L.out && L.m >= c2.i0 && L.m <= c2.i1;
                     if (inr) {
-                        if (llu) { st(c2.hu, c, o.u[0]); st(c2.hup, c, o.u[1]); }
-                        if (llv) { st(c2.hv, c, o.v[0]); st(c2.hvp, c, o.v[1]); }
-                        if (luh) { st(c2.hh, c, o.h[0]); st(c2.hhp, c, o.h[1]); }
+                        if (llu) { st(c2.hu, c, o.u[0]); if (!SKIP) st(c2.hup, c, o.u[1]); }
+                        if (llv) { st(c2.hv, c, o.v[0]); if (!SKIP) st(c2.hvp, c, o.v[1]); }
+                        if (luh) st(c2.hh, c, o.h[0]);   // hhh_p: see below
                         if (HH) {
                             if (llu) st(a.a2.hun, c, o.u[0]);
                             if (llv) st(a.a2.hvn, c, o.v[0]);
@@ -841,14 +890,18 @@ int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact
 
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s, int32_t *flip_nbad,
-                   bool flip)
+                   bool flip, bool rc, double *sshp_out)
 {
+    if (rc && (!flip || !reuse || sw.full_free_surface != 1 || !sshp_out))
+        return set_error(OCN_ERR_ARG, "recomputed depths only on role-flip reuse steps with full_free_surface = 1");
     if (use_march(cp, part)) {
         RC_K(check_block(b));
         const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
         const Range r = march_range(range_interior(b), b, part);
-        if (flip) return launch_march(b, r, MarchFusedB<true>{*b, t, sw, tau, full, reuse, flip_nbad}, s);
-        return launch_march(b, r, MarchFusedB<false>{*b, t, sw, tau, full, reuse, nullptr}, s);
+        if (flip && rc)
+            return launch_march(b, r, MarchFusedB<true, true>{*b, t, sw, tau, full, reuse, flip_nbad, sshp_out}, s);
+        if (flip) return launch_march(b, r, MarchFusedB<true>{*b, t, sw, tau, full, reuse, flip_nbad, nullptr}, s);
+        return launch_march(b, r, MarchFusedB<false>{*b, t, sw, tau, full, reuse, nullptr, nullptr}, s);
     }
     if (flip) return set_error(OCN_ERR_ARG, "the role-flip step needs the compact tables and the march");
     return launch_fused<KFusedB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s, sw, tau,
@@ -875,14 +928,16 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compac
 }
 
 int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
-                    double tau_next, bool next_reuse, hipStream_t s)
+                    double tau_next, bool next_reuse, bool skip_rc, hipStream_t s)
 {
-    if (!cp || !cp->march || sw.full_free_surface != 1)
+    if (!cp || !cp->march || sw.full_free_surface != 1 || (skip_rc && !next_reuse))
         return set_error(OCN_ERR_ARG, "fused hh_init + A needs the compact tables, the march and full_free_surface = 1");
     RC_K(check_block(b));
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
-    if (next_reuse) return launch_march(b, range_bnd(b), MarchCA<false>{*b, t, sw, tau_next}, s);
-    return launch_march(b, range_bnd(b), MarchCA<true>{*b, t, sw, tau_next}, s);
+    const Range r = range_bnd(b);
+    if (skip_rc) return launch_march(b, r, MarchCA<false, true>{*b, t, sw, tau_next}, s);
+    if (next_reuse) return launch_march(b, r, MarchCA<false, false>{*b, t, sw, tau_next}, s);
+    return launch_march(b, r, MarchCA<true, false>{*b, t, sw, tau_next}, s);
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy

@@ -731,12 +731,15 @@ template <bool C> struct FusedC1 {
 // metric ids OCN_DX..OCN_R_DISS, rows[(id - OCN_DX) * nrows + (n - bnd_y1)].
 constexpr int kNumMasks = OCN_DX;                         // OCN_LU..OCN_LLV
 constexpr int kNumRowFields = OCN_NUM_R4 - OCN_DX;        // OCN_DX..OCN_R_DISS
-enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2 };
+enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2,
+       OCN_COMPACT_RING_SEA = 4 };   // not a failure: a8 / a9 write somewhere on the halo ring
 
 // Thread grid = whole bnd range.  Mask bytes everywhere; row values from column nx_start-1
 // for the rows [ny_start-1, ny_end+1] the stencils read; every point of [nx_start-1,
 // nx_end+1] on those rows must carry the same bit pattern, and every mask value must be
 // exactly 0.0f or 1.0f -- otherwise `flags` records why and the caller keeps the 2-D path.
+// OCN_COMPACT_RING_SEA also reports whether a8 (halo ring) or a9 (outer ring e+1, as fused C1
+// runs it) has a point to write: if not, the role-flip steps skip their ring launch.
 struct Prepare {
     Geo I; int ms, me, ns, ne;
     const float *__restrict__ r4[OCN_NUM_R4];
@@ -754,6 +757,12 @@ struct Prepare {
         st(bits, q, (uint8_t)b);
         if (bad) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_MASK_NOT_BINARY);
         if (m < ms || m > me || n < ns || n > ne) return;
+        // a8 on the ring writes under lu / lcu / lcv; a9 (fused C1) on the outer ring e+1 under
+        // lu / llu / llv / luh
+        const unsigned a8m = (1u << OCN_LU) | (1u << OCN_LCU) | (1u << OCN_LCV);
+        const unsigned a9m = (1u << OCN_LU) | (1u << OCN_LLU) | (1u << OCN_LLV) | (1u << OCN_LUH);
+        if (((m == ms || m == me || n == ns || n == ne) && (b & a8m)) || ((m == me || n == ne) && (b & a9m)))
+            OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_RING_SEA);
         const Pt q0 = I(ms, n);
         bool vary = false;
         for (int k = 0; k < kNumRowFields; ++k) {

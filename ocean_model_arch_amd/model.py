@@ -152,6 +152,12 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FLIP, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_recompute(self, on: bool = True):
+        """Recompute steps inside role-flip calls (default): fused B forms hhq, hhu_p, hhv_p itself
+        instead of re-reading them; same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_RECOMPUTE, int(on)), "ocn_ctx_set_option")
+        return self
+
     def option(self, key: int) -> int:
         v = C.c_int64(0)
         check(lib().ocn_ctx_get_option(self.ctx, key, C.byref(v)), "ocn_ctx_get_option")

@@ -111,7 +111,8 @@ def test_tracer_kernels_match_reference(amd, geom):
     assert not failures, f"{geom}: differs from the reference: {failures}"
 
 
-def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True, march=True, flip=True):
+def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True, march=True, flip=True,
+                recompute=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"])
@@ -123,6 +124,7 @@ def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True, 
     m.set_overlap(overlap)
     m.set_march(march)
     m.set_flip(flip)
+    m.set_recompute(recompute)
     if graph:
         m.set_graph(True)
     return m
@@ -145,19 +147,20 @@ def compare_case(m, case, name):
     return bad
 
 
-@pytest.mark.parametrize("mode", ["compact", "noflip", "pointwise", "fused", "stages", "serial"])
+@pytest.mark.parametrize("mode", ["compact", "norecompute", "noflip", "pointwise", "fused", "stages", "serial"])
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
     hh_init as register marches, role-flip steps on single-block runs without tracers, halo
-    exchanges overlapped with inner launches when there are several blocks; noflip = compact
-    with standard steps only; pointwise = compact with every launch one thread per point; fused =
+    exchanges overlapped with inner launches when there are several blocks (and, in role-flip
+    calls, hh_init fused with the next step's A and fused B recomputing hhq / hhu_p / hhv_p);
+    norecompute = compact without the recompute steps; noflip = compact with standard steps only; pointwise = compact with every launch one thread per point; fused =
     the 4-launch step on the 2-D real(4) arrays; serial = compact without the overlap; stages =
     the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    compact = mode in ("compact", "noflip", "serial", "pointwise")
+    compact = mode in ("compact", "norecompute", "noflip", "serial", "pointwise")
     m = build_model(amd, case, fused=mode != "stages", compact=compact, overlap=mode != "serial",
-                    march=mode != "pointwise", flip=mode != "noflip")
+                    march=mode != "pointwise", flip=mode != "noflip", recompute=mode != "norecompute")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     assert m.compact_active == compact
     bad = compare_case(m, case, name)

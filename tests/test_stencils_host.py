@@ -236,7 +236,7 @@ def test_host_step_matches_reference(hst, name, mode):
     tabs = None
     if mode in ("compact", "overlap_early", "overlap_late"):
         tabs = compact_tables(hst, om)
-        assert all(t[2] == 0 for t in tabs), [t[2] for t in tabs]
+        assert all(t[2] & 3 == 0 for t in tabs), [t[2] for t in tabs]   # 4 = sea on the halo ring: fine
     for s in range(case["steps"]):
         host_step(hst, om, mode, nbad, last=s == case["steps"] - 1, tabs=tabs, first=s == 0)
     assert nbad.value == 0
@@ -260,8 +260,18 @@ def test_compact_tables_detect_inexact_fields(hst, what, flag):
             om.f[k]["dyh"][3, 4] = np.nextafter(om.f[k]["dyh"][3, 4], np.float32(2e9))
         elif what == "mask":
             om.f[k]["llv"][5, 5] = 0.5
-    flags = [t[2] for t in compact_tables(hst, om)]
-    assert flags == [flag] * len(om.blocks)
+    tabs = compact_tables(hst, om)
+    assert [t[2] & 3 for t in tabs] == [flag] * len(om.blocks)
+    # OCN_COMPACT_RING_SEA: the blocks' shared edge puts sea points on each block's halo ring
+    assert all(t[2] & 4 for t in tabs)
+
+
+def test_ring_sea_flag_on_closed_box(hst):
+    """One block of the closed box: the halo ring is the land frame, so the role-flip steps may
+    skip a8 / a9 on the ring (Prepare leaves OCN_COMPACT_RING_SEA clear); the Black Sea basin's
+    single block too, when no sea touches its ring."""
+    om = O.OracleModel(O.BasinConfig(nx=40, ny=36), O.SWConfig(), 1, 1).init()
+    assert compact_tables(hst, om)[0][2] == 0
 
 
 def test_compact_row_window_is_what_the_stencils_read(hst):
@@ -270,7 +280,7 @@ def test_compact_row_window_is_what_the_stencils_read(hst):
     om = O.OracleModel(O.BasinConfig(nx=40, ny=36), O.SWConfig(), 1, 1).init()
     om.f[0]["dx"][0, :] *= np.float32(3.0)          # column bnd_x1 = nx_start - 2
     tabs = compact_tables(hst, om)
-    assert tabs[0][2] == 0
+    assert tabs[0][2] & 3 == 0
     ref = O.OracleModel(O.BasinConfig(nx=40, ny=36), O.SWConfig(), 1, 1).init()
     ref.f[0]["dx"][0, :] *= np.float32(3.0)
     nbad = C.c_int32(0)
