@@ -20,12 +20,17 @@ STAGE = {"KFusedA": "fused_a", "KFusedB": "fused_b", "MarchFusedB": "fused_b", "
          "KHhInit": "hh_init", "MarchHhInit": "hh_init", "MarchFusedA": "fused_a", "MarchCA": "fused_ca"}
 
 
-def means(root):
+def values(root):
+    """{kernel name: {counter: [bytes per dispatch]}}"""
     vals = defaultdict(lambda: defaultdict(list))
-    for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recursive=True):
+    for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
             vals[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]) * 1024.0)
-    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in vals.items()}
+    return vals
+
+
+def means(root):
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in values(root).items()}
 
 
 def main():
@@ -37,15 +42,26 @@ def main():
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py; read scale {scale:.4f} "
                      f"calibrated on stenbench k_bench<0,0> ({exact_read:.0f} B read exactly)",
            "fetch_scale": scale, "kernels": {}}
-    for k, d in means(pmc).items():
+    # every dispatch of every template instance of a stage's kernel (e.g. MarchFusedB<true, true>
+    # and <false, false>), averaged per dispatch like bench.py's per-launch timing
+    agg = defaultdict(lambda: {"FETCH_SIZE": [], "WRITE_SIZE": [], "names": set()})
+    for k, d in values(pmc).items():
         m = re.search(r"ocn::(\w+)", k.replace("k_range<ocn::", "").replace("k_march<ocn::", ""))
         name = m.group(1) if m else k
         stage = STAGE.get(name)
-        if not stage or "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+        if not stage:
             continue
-        rd, wr = d["FETCH_SIZE"] * scale, d["WRITE_SIZE"]
-        out["kernels"][stage] = {"kernel": name, "cells": cells, "compact": compact, "fetch_bytes": round(rd),
-                                 "write_bytes": round(wr), "hbm_bytes_per_launch": round(rd + wr)}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            agg[stage][c] += d.get(c, [])
+        agg[stage]["names"].add(name)
+    for stage, d in agg.items():
+        if not d["FETCH_SIZE"] or not d["WRITE_SIZE"]:
+            continue
+        rd = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * scale
+        wr = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
+        out["kernels"][stage] = {"kernel": "/".join(sorted(d["names"])), "dispatches": len(d["WRITE_SIZE"]),
+                                 "cells": cells, "compact": compact, "fetch_bytes": round(rd), "write_bytes": round(wr),
+                                 "hbm_bytes_per_launch": round(rd + wr)}
     print(json.dumps(out, indent=1))
 
 
