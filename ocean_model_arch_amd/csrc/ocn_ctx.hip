@@ -359,7 +359,8 @@ static int allocate(ocn_ctx *c)
     }
     for (LBlock &b : c->blocks) {
         const size_t n = (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1);
-        const size_t nrow = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1) * (OCN_NUM_R4 - OCN_DX);   // metric row tables
+        const size_t nrow = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1) * (OCN_NUM_R4 - OCN_DX + 4);   // metric row tables
+                                                                                                // + 4 ratios (sw_stencils.h kRowTable)
         HIPCHK(hipMalloc(&b.bits, n));
         c->allocs.push_back(b.bits);
         HIPCHK(hipMalloc(&b.rows, nrow * sizeof(float)));

@@ -175,7 +175,7 @@ struct Here {
 
 // per-row metrics of the compact tables (wave-uniform) for rows n-1, n, n+1
 struct MetRows {
-    float g[kNumRowFields][3];
+    float g[kRowTable][3];
     __device__ __forceinline__ float at(int id, int dy) const
     {
         if (dy < -1 || dy > 1) ocn_march_bad_access();
@@ -184,19 +184,19 @@ struct MetRows {
     // rows n-1 <- n <- n+1 = next (one value per metric field)
     __device__ __forceinline__ void shift(const float *next)
     {
-        for (int k = 0; k < kNumRowFields; ++k) { g[k][0] = g[k][1]; g[k][1] = g[k][2]; g[k][2] = next[k]; }
+        for (int k = 0; k < kRowTable; ++k) { g[k][0] = g[k][1]; g[k][1] = g[k][2]; g[k][2] = next[k]; }
     }
     // rows n-1 and n before the first row of a march (table rows[(id - OCN_DX) * nrows + r])
     __device__ __forceinline__ void preload(const float *rows, unsigned nrows, unsigned r_prev, unsigned r_cur)
     {
-        for (int k = 0; k < kNumRowFields; ++k) {
+        for (int k = 0; k < kRowTable; ++k) {
             g[k][1] = ld(rows, (unsigned)k * nrows + r_prev);
             g[k][2] = ld(rows, (unsigned)k * nrows + r_cur);
         }
     }
     __device__ __forceinline__ static void load(float *q, const float *rows, unsigned nrows, unsigned r)
     {
-        for (int k = 0; k < kNumRowFields; ++k) q[k] = ld(rows, (unsigned)k * nrows + r);
+        for (int k = 0; k < kRowTable; ++k) q[k] = ld(rows, (unsigned)k * nrows + r);
     }
 };
 #define OCN_MV(name, reg) \
@@ -205,7 +205,8 @@ struct MetRows {
     __device__ __forceinline__ float name(int, int dy) const { return met.at(id, dy); }
 #define OCN_MG_ALL                                                                                         \
     OCN_MG(dx, OCN_DX) OCN_MG(dy, OCN_DY) OCN_MG(dxt, OCN_DXT) OCN_MG(dyt, OCN_DYT) OCN_MG(dxh, OCN_DXH)     \
-    OCN_MG(dyh, OCN_DYH) OCN_MG(dxb, OCN_DXB) OCN_MG(dyb, OCN_DYB)
+    OCN_MG(dyh, OCN_DYH) OCN_MG(dxb, OCN_DXB) OCN_MG(dyb, OCN_DYB)                                           \
+    __device__ __forceinline__ float sratio(int k) const { return met.at(OCN_DX + kNumRowFields + k, 0); }
 
 // One lane of a march: its loaded column m, its edge column me (aligned layout: lane 0 m-1,
 // lane 63 m+1, both clamped into the block array), whether it is an edge lane, whether it
@@ -350,7 +351,7 @@ template <bool C1F, bool RC = false> struct MarchFusedB {
         FusedB<true> k; const Tab<true> &t; SwNextStep<true> a8; HhInit<true> c2; int *nbad; double *sshp_out;
         // row n: ubrtr, vbrtr, hhv, mu, hhu, hhq (RC: h_r and sshp), str_t, ssh at n+1; vort, hhh,
         // str_s, mask bytes (RC: at n+1) and the pointwise operands at n; metric row n+1
-        struct Batch { double nn[9], c[3], h[8], p[2]; unsigned bits; float g[kNumRowFields]; };
+        struct Batch { double nn[9], c[3], h[8], p[2]; unsigned bits; float g[kRowTable]; };
         __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
         {
             const SwUpdateUv<true> &a7 = k.a7;
@@ -488,7 +489,7 @@ template <bool HH> struct MarchFusedA {
         FusedA<true> k; const Tab<true> &t;
         // row n: ubrtr, ubrtrp, mask bytes, h_r, ssh at n+1; vbrtr, hhv, vbrtrp, hhu, sshp at n;
         // edge values of the arrays read at m+-1; metric row n+1
-        struct Batch { double nn[4], c[5], enn[4], ec[3]; unsigned bits, ebits; float g[kNumRowFields]; };
+        struct Batch { double nn[4], c[5], enn[4], ec[3]; unsigned bits, ebits; float g[kRowTable]; };
         __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
         {
             const SwUpdateSsh<true> &a1 = k.a1;
@@ -588,7 +589,7 @@ struct MarchHhInit {
     struct Fn {
         HhInit<true> k; const Tab<true> &t; int ylast;
         // row n: h_r, ssh, sshp, mask bytes (+ edge values) and metrics at row n+1
-        struct Batch { double nn[3], enn[3]; unsigned bits, ebits; float g[kNumRowFields]; };
+        struct Batch { double nn[3], enn[3]; unsigned bits, ebits; float g[kRowTable]; };
         __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
         {
             const int r = min(n + 1, ylast);
@@ -696,7 +697,7 @@ template <bool HH, bool SKIP> struct MarchCA {
         HhInit<true> c2; FusedA<true> a; const Tab<true> &t; int ylast;
         // row n: h_r, ssh, sshp, mask bytes, ubrtr, ubrtrp at n+1 (clamped to bnd_y2); vbrtr,
         // vbrtrp at n; their edge values; metric row n+1
-        struct Batch { double nn[5], c[2], enn[5], ec[2]; unsigned bits, ebits; float g[kNumRowFields]; };
+        struct Batch { double nn[5], c[2], enn[5], ec[2]; unsigned bits, ebits; float g[kRowTable]; };
         __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
         {
             const int r = min(n + 1, ylast), r0 = max(n, (int)c2.I.by1);

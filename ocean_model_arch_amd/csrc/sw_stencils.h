@@ -158,6 +158,19 @@ template <bool C> struct SwUpdateSsh {
 // kernel/shallow_water/depth.f90:56-97 for one level given its values at the four corners
 // (m,n), (m+1,n), (m,n+1), (m+1,n+1); per-corner weights dx*dy*lu (products evaluated per
 // use, as the reference does)
+// a / s for s a sum of 0/1 masks (0..4): x / 2^k and x * 2^-k are the same correctly rounded
+// value, so when every lane of the wave has s = 1, 2 or 4 (the sea interior) the quotient is a
+// multiply; otherwise (3, or 0 on land) the IEEE division.  Bitwise the same either way.
+#ifndef OCN_WAVE_ALL
+#define OCN_WAVE_ALL(p) __all(p)
+#endif
+OCN_HD OCN_INLINE double div_mask_sum(double a, double s)
+{
+    const double r = s == 4.0 ? 0.25 : s == 2.0 ? 0.5 : 1.0;
+    if (OCN_WAVE_ALL(s == 1.0 || s == 2.0 || s == 4.0)) return a * r;
+    return a / s;
+}
+
 template <class X> OCN_HD OCN_INLINE double interp_wt(const X &x, double h, int i, int j)
 {
     return h * D(x.dx(i, j)) * D(x.dy(i, j)) * D(x.lu(i, j));
@@ -165,18 +178,18 @@ template <class X> OCN_HD OCN_INLINE double interp_wt(const X &x, double h, int 
 template <class X> OCN_HD OCN_INLINE double interp_u(const X &x, double h00, double h10)
 {
     const double slu = D(x.lu(0, 0) + x.lu(1, 0));
-    return (interp_wt(x, h00, 0, 0) + interp_wt(x, h10, 1, 0)) / slu / D(x.dxt(0, 0)) / D(x.dyh(0, 0));
+    return div_mask_sum(interp_wt(x, h00, 0, 0) + interp_wt(x, h10, 1, 0), slu) / D(x.dxt(0, 0)) / D(x.dyh(0, 0));
 }
 template <class X> OCN_HD OCN_INLINE double interp_v(const X &x, double h00, double h01)
 {
     const double slu = D(x.lu(0, 0) + x.lu(0, 1));
-    return (interp_wt(x, h00, 0, 0) + interp_wt(x, h01, 0, 1)) / slu / D(x.dxh(0, 0)) / D(x.dyt(0, 0));
+    return div_mask_sum(interp_wt(x, h00, 0, 0) + interp_wt(x, h01, 0, 1), slu) / D(x.dxh(0, 0)) / D(x.dyt(0, 0));
 }
 template <class X> OCN_HD OCN_INLINE double interp_h(const X &x, double h00, double h10, double h01, double h11)
 {
     const double slu = D(x.lu(0, 0) + x.lu(1, 0) + x.lu(0, 1) + x.lu(1, 1));
-    return (interp_wt(x, h00, 0, 0) + interp_wt(x, h10, 1, 0) + interp_wt(x, h01, 0, 1) + interp_wt(x, h11, 1, 1))
-           / slu / D(x.dxb(0, 0)) / D(x.dyb(0, 0));
+    return div_mask_sum(interp_wt(x, h00, 0, 0) + interp_wt(x, h10, 1, 0) + interp_wt(x, h01, 0, 1)
+                            + interp_wt(x, h11, 1, 1), slu) / D(x.dxb(0, 0)) / D(x.dyb(0, 0));
 }
 
 // a2 hh_update's interpolation (depth.f90:134-160): q = h_r + sh at each corner, q00 given
@@ -375,14 +388,17 @@ template <bool C> struct UvTrans {
 // mixing.f90:14-58
 // The reference kernel's u, v are the previous time level (the PSy layer passes ubrtrp /
 // vbrtrp, sw_interface.f90:110-142); the view names them up / vp.
+// The four real(4) metric ratios (dy/dx, dx/dy, dxb/dyb, dyb/dxb at the point) come from
+// x.sratio(k): divided per point by the pointer views, read from the compact row tables (where
+// Prepare divided the same row values) by the march views.
 template <class X> OCN_HD OCN_INLINE void stress_components_math(const X &x, double &vt, double &vs)
 {
-    const float r1 = x.dy(0, 0) / x.dx(0, 0);
-    const float r2 = x.dx(0, 0) / x.dy(0, 0);
+    const float r1 = x.sratio(0);
+    const float r2 = x.sratio(1);
     vt = D(r1) * (x.up(0, 0) / D(x.dyh(0, 0)) - x.up(-1, 0) / D(x.dyh(-1, 0)))
          - D(r2) * (x.vp(0, 0) / D(x.dxh(0, 0)) - x.vp(0, -1) / D(x.dxh(0, -1)));
-    const float q1 = x.dxb(0, 0) / x.dyb(0, 0);
-    const float q2 = x.dyb(0, 0) / x.dxb(0, 0);
+    const float q1 = x.sratio(2);
+    const float q2 = x.sratio(3);
     vs = D(q1) * (x.up(0, 1) / D(x.dxt(0, 1)) - x.up(0, 0) / D(x.dxt(0, 0)))
          + D(q2) * (x.vp(1, 0) / D(x.dyt(1, 0)) - x.vp(0, 0) / D(x.dyt(0, 0)));
 }
@@ -394,6 +410,11 @@ template <bool C> struct StressComponents {
     double *__restrict__ str_t, *__restrict__ str_s;
     struct View {
         OCN_VIEW_PTR_COMMON(StressComponents)
+        OCN_HD OCN_INLINE float sratio(int k) const   // mixing.f90:33-34, 43-44
+        {
+            return k == 0 ? ld(this->k.dy, c) / ld(this->k.dx, c) : k == 1 ? ld(this->k.dx, c) / ld(this->k.dy, c)
+                 : k == 2 ? ld(this->k.dxb, c) / ld(this->k.dyb, c) : ld(this->k.dyb, c) / ld(this->k.dxb, c);
+        }
         OCN_VIEW_LD_AS(up, u) OCN_VIEW_LD_AS(vp, v)
         OCN_VIEW_LD(dx) OCN_VIEW_LD(dy) OCN_VIEW_LD(dxt) OCN_VIEW_LD(dyt) OCN_VIEW_LD(dxh) OCN_VIEW_LD(dyh)
         OCN_VIEW_LD(dxb) OCN_VIEW_LD(dyb)
@@ -731,6 +752,9 @@ template <bool C> struct FusedC1 {
 // metric ids OCN_DX..OCN_R_DISS, rows[(id - OCN_DX) * nrows + (n - bnd_y1)].
 constexpr int kNumMasks = OCN_DX;                         // OCN_LU..OCN_LLV
 constexpr int kNumRowFields = OCN_NUM_R4 - OCN_DX;        // OCN_DX..OCN_R_DISS
+// then four per-row ratios for stress_components: dy/dx, dx/dy, dxb/dyb, dyb/dxb (real(4))
+constexpr int kNumRowRatios = 4;
+constexpr int kRowTable = kNumRowFields + kNumRowRatios;
 enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2,
        OCN_COMPACT_RING_SEA = 4 };   // not a failure: a8 / a9 write somewhere on the halo ring
 
@@ -769,6 +793,11 @@ struct Prepare {
             const float v = ld(r4[OCN_DX + k], q);
             vary |= fbits(v) != fbits(ld(r4[OCN_DX + k], q0));
             if (m == ms) st(rows, (unsigned)k * nrows + q.r, v);
+        }
+        if (m == ms) {   // the same real(4) divisions as stress_components_math on these row values
+            const float dx = ld(r4[OCN_DX], q), dy = ld(r4[OCN_DY], q), dxb = ld(r4[OCN_DXB], q), dyb = ld(r4[OCN_DYB], q);
+            const float rat[kNumRowRatios] = {dy / dx, dx / dy, dxb / dyb, dyb / dxb};
+            for (int k = 0; k < kNumRowRatios; ++k) st(rows, (unsigned)(kNumRowFields + k) * nrows + q.r, rat[k]);
         }
         if (vary) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_METRIC_NOT_ROW_CONSTANT);
     }

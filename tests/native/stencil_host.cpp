@@ -15,6 +15,7 @@
 #define OCN_ATOMIC_INC(p) (++*(p))
 #define OCN_ATOMIC_OR(p, v) (*(p) |= (v))
 #define OCN_HOST_BOUNDS_CHECK 1
+#define OCN_WAVE_ALL(p) (p)
 #include "../../ocean_model_arch_amd/csrc/sw_stencils.h"
 
 static long g_oob = 0;

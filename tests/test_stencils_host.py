@@ -119,7 +119,7 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a.ravel(order="F")).tobytes()).hexdigest()
 
 
-N_ROW_FIELDS = len(R4) - 7          # dx .. r_diss
+N_ROW_FIELDS = len(R4) - 7 + 4      # dx .. r_diss, then the 4 stress_components ratios (sw_stencils.h kRowTable)
 
 
 def compact_tables(hst, om):
