@@ -42,14 +42,15 @@ LAUNCH_BYTES = {
     "b_flip_rc": (177, 177),                               # hhq, hhu_p, hhv_p formed from h_r, ssh, sshp
     "c1": (121, 132), "c1_ring": (0, 0),                   # role-flip steps: a8 + a9 on the halo ring only
     "c2": (81, 128), "c2_full": (121, 168),
-    "ca": (113, 113), "ca_store": (137, 137), "ca_hh": (161, 161),   # hh_init + next step's A (no hhh_p;
-}   # "ca": next step recomputes -- no interior hhq, hhu_p, hhv_p; "ca_hh": + a2's stores)
+    "ca": (113, 113), "ca_store": (137, 137), "ca_hh": (169, 169),   # hh_init + next step's A (no hhh_p;
+}   # "ca": next step recomputes -- no interior hhq, hhu_p, hhv_p; "ca_hh": + a2's stores and hhh_p)
 
 
-def call_launches(steps: int, flip: bool, rc: bool = True):
+def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False):
     """The launches of one ocn_ctx_step call of `steps` steps, as (timer, launch kind) pairs --
     ocn_ctx.hip ocn_ctx_step / one_step_fused for one block (role-flip calls fuse each step's
-    hh_init with the next step's A when full_free_surface = 1, as in sw.par)."""
+    hh_init with the next step's A when full_free_surface = 1, as in sw.par; ring = the ring
+    launch runs, i.e. a8 / a9 have work on the halo ring: blocks with neighbours)."""
     out = []
     for s in range(1, steps + 1):
         first, last = s == 1, s == steps
@@ -58,28 +59,30 @@ def call_launches(steps: int, flip: bool, rc: bool = True):
         if not (flip and steps >= 2 and not first):
             out.append(("fused_a", "a_reuse" if reuse else "a"))
         if flip_step:   # ring launch skipped when no halo-ring point has a8 / a9 work (the box)
-            out += [("fused_b", "b_flip" if first else "b_flip_rc" if rc else "b_flip_reuse"),
-                    ("fused_ca", "ca_hh" if s + 1 >= steps else "ca" if rc else "ca_store")]
+            out.append(("fused_b", "b_flip" if first else "b_flip_rc" if rc else "b_flip_reuse"))
+            if ring:
+                out.append(("fused_c1", "c1_ring"))
+            out += [("fused_ca", "ca_hh" if s + 1 >= steps else "ca" if rc else "ca_store")]
         else:
             out += [("fused_b", "b_full" if last else "b_reuse" if reuse else "b"), ("fused_c1", "c1"),
                     ("hh_init", "c2_full" if last else "c2")]
     return out
 
 
-def fused_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True):
+def fused_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False):
     """Mean bytes per interior cell per launch of each timer over one ocn_ctx_step call."""
     i = 0 if compact else 1
     tot, cnt = {}, {}
-    for timer, kind in call_launches(steps, flip, rc):
+    for timer, kind in call_launches(steps, flip, rc, ring):
         tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
         cnt[timer] = cnt.get(timer, 0) + 1
     return {t: tot[t] / cnt[t] for t in tot}
 
 
-def step_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True):
+def step_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False):
     """Bytes per interior cell per step moved by one ocn_ctx_step call of `steps` steps."""
     i = 0 if compact else 1
-    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc)) / steps
+    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc, ring)) / steps
 
 
 def dims_create(n: int):
@@ -162,6 +165,9 @@ def main():
     ap.add_argument("--no-march", action="store_true", help="one thread per point in every launch (no register march)")
     ap.add_argument("--no-flip", action="store_true", help="standard steps only (no role-flip steps)")
     ap.add_argument("--no-recompute", action="store_true", help="role-flip calls without the recompute steps")
+    ap.add_argument("--blocks", default=None,
+                    help="block grid BXxBY (default: one block per GPU); with one GPU, several blocks on it "
+                         "exercise the halo-exchange path without RCCL")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -176,6 +182,10 @@ def main():
 
     torch.cuda.set_device(local_rank)
     bx, by = dims_create(world)
+    if args.blocks:
+        bx, by = (int(v) for v in args.blocks.lower().split("x"))
+        if world > 1 and bx * by != world:
+            raise SystemExit("--blocks with several GPUs must give one block per GPU")
     n = args.n
     nxbox, nybox = (n, n) if args.scaling == "strong" else (n * bx, n * by)
     basin = amd.BasinConfig(nx=nxbox + 4, ny=nybox + 4)
@@ -217,6 +227,7 @@ def main():
     times = model.stage_times()
     compact = model.compact_active
     flip = model.flip_active
+    rc = model.recompute_active
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -227,9 +238,9 @@ def main():
     local_cells = model.interior_cells
     out = None
     if rank == 0:
-        rc = not args.no_recompute
-        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc)
-        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc)
+        ring = bx * by > 1
+        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc, ring)
+        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:
@@ -246,13 +257,15 @@ def main():
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
                "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
                "data": "synthetic (Gaussian SSH hump in a closed flat-bottom box, SURVEY.md 8d)",
-               "config": {"workload": f"{nxbox}x{nybox} box, {bx}x{by} blocks (1 per GPU), sw.par defaults, tau=1s",
+               "config": {"workload": f"{nxbox}x{nybox} box, {bx}x{by} blocks ({bx * by // world} per GPU), sw.par defaults, "
+                                      f"tau=1s",
                           "box": [nxbox, nybox], "blocks": [bx, by], "graph": bool(args.graph),
                           "step": "reference stages" if args.stages else "fused groups",
                           "static_fields": "compact" if compact else "2-D arrays",
                           "march": bool(compact and not args.stages and not args.no_march),
-                          "role_flip_steps": flip,
-                          "parallelism": f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else "1 block"},
+                          "role_flip_steps": flip, "recompute_steps": rc,
+                          "parallelism": (f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else
+                                          "1 block" if bx * by == 1 else f"{bx}x{by} blocks, local halo copies")},
                "roofline": roof,
                "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),
                "step_alg_gbs_per_gpu": round(step_gbs, 1),

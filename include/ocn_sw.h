@@ -291,18 +291,21 @@ int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
  *  OCN_OPT_MARCH (default 1): with the compact tables, the stencil launches that have a
  *  register-march form (fused A, fused B, hh_init) run as one (same results bit for bit);
  *  0 = one thread per point.
- *  OCN_OPT_FLIP (default 1): one block per process without halo exchanges, compact tables and
- *  march, no tracers: every step of an ocn_ctx_step call but the last replaces sw_next_step's
- *  copies (ssh := sshn, ubrtr := ubrtrn, vbrtr := vbrtrn) by swapping the two buffers of each
- *  pair inside the library, and runs its time filters inside fused B (same results bit for bit;
- *  the pointers of ocn_ctx_field are the same after the call).  Needs the pairs to agree outside
- *  their write sets, which holds from ocn_ctx_init_state on and is checked on the device
- *  whenever those fields were uploaded or handed out; otherwise the standard step runs.
+ *  OCN_OPT_FLIP (default 1): with compact tables and march, no tracers: every step of an
+ *  ocn_ctx_step call but the last replaces sw_next_step's copies (ssh := sshn, ubrtr := ubrtrn,
+ *  vbrtr := vbrtrn) by swapping the two buffers of each pair inside the library, and runs its
+ *  time filters inside fused B (same results bit for bit; the pointers of ocn_ctx_field are the
+ *  same after the call).  Needs the pairs to agree outside their write sets and, with halo
+ *  exchanges, the halo ring of ssh, ubrtr, vbrtr, hhu, hhv, hhq_rest to hold the neighbours'
+ *  values; both hold from ocn_ctx_init_state on and are checked on the device whenever fields
+ *  were uploaded or handed out (with an RCCL communicator: at every call, all ranks deciding
+ *  together); otherwise the standard step runs.
  *  OCN_OPT_RECOMPUTE (default 1): in such calls (full_free_surface = 1, no a8 / a9 work on the
- *  halo ring), steps 2..K-1 form hhq, hhu_p, hhv_p inside fused B instead of storing and
- *  re-reading them (same results bit for bit).
+ *  halo ring, so one block without halo exchanges), steps 2..K-1 form hhq, hhu_p, hhv_p inside
+ *  fused B instead of storing and re-reading them (same results bit for bit).
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
- * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps. */
+ * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
+ * whether it used recompute steps. */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,

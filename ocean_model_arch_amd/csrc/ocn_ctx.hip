@@ -68,6 +68,23 @@ __global__ __launch_bounds__(256) void k_segments(const Seg *__restrict__ segs, 
     for (int i = threadIdx.x; i < g.count; i += blockDim.x) g.dst[(long)i * g.dst_stride] = g.src[(long)i * g.src_stride];
 }
 
+// The same runs compared instead of copied: ORs 1 into *flags where dst differs from src (bits).
+__global__ __launch_bounds__(256) void k_segments_cmp(const Seg *__restrict__ segs, int nseg, int32_t *flags)
+{
+    const int s = blockIdx.x;
+    if (s >= nseg) return;
+    const Seg g = segs[s];
+    bool bad = false;
+    for (int i = threadIdx.x; i < g.count; i += blockDim.x) {
+        const double a = g.dst[(long)i * g.dst_stride], b = g.src[(long)i * g.src_stride];
+        unsigned long long x, y;
+        __builtin_memcpy(&x, &a, 8);
+        __builtin_memcpy(&y, &b, 8);
+        bad |= x != y;
+    }
+    if (bad) atomicOr(flags, 1);
+}
+
 __global__ void k_fill_r8(double *p, long n, double v)
 {
     long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -201,7 +218,7 @@ struct ocn_ctx {
     double stage_ms[OCN_NUM_TIMERS] = {0};
     int64_t stage_n[OCN_NUM_TIMERS] = {0};
     bool fused = true;
-    std::vector<int> sync_a, sync_a_reuse, sync_b;
+    std::vector<int> sync_a, sync_a_reuse, sync_b, sync_ca, sync_ca_reuse;
     // compact static fields: requested (OCN_OPT_COMPACT), in use, stale (real(4) fields
     // changed since they were built), or unusable because raw real(4) pointers were handed out
     bool compact_req = true, compact = false, static_dirty = true;
@@ -212,7 +229,7 @@ struct ocn_ctx {
     // agree outside their write sets (sw_stencils.h Coherence), coherent_known = that was checked
     // after the state last changed outside ocn_ctx_step; r8_escaped = raw pointers of a pair were
     // handed out (check at every call); flip = OCN_OPT_FLIP
-    bool flip = true, coherent = false, flip_used = false;
+    bool flip = true, coherent = false, flip_used = false, rc_used = false;
     bool ring_sea = true;   // some halo-ring point has a mask set (Prepare); else no ring launch
     bool recompute = true;  // OCN_OPT_RECOMPUTE: recompute steps in role-flip calls
     mutable bool coherent_known = false, r8_escaped = false;
@@ -497,13 +514,17 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
     return OCN_OK;
 }
 
+// Plans hold raw field pointers, so a plan is kept per role of the role-flip pairs (the key is
+// the field list followed by -1 - (role & 1)).
 static int get_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan *&out)
 {
-    auto it = c->plans.find(fields);
+    std::vector<int> key = fields;
+    key.push_back(-1 - (c->role & 1));
+    auto it = c->plans.find(key);
     if (it == c->plans.end()) {
         HaloPlan p;
         RC(build_plan(c, fields, p));
-        it = c->plans.emplace(fields, p).first;
+        it = c->plans.emplace(key, p).first;
     }
     out = &it->second;
     return OCN_OK;
@@ -515,7 +536,9 @@ static int nccl_rc(ncclResult_t r, const char *what)
     return set_error(OCN_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stream = nullptr)
+// cmp != nullptr: compare the halos with what the exchange would deliver instead of writing them
+// (ORs 1 into *cmp where they differ); same messages, so every rank must take part.
+static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stream = nullptr, int32_t *cmp = nullptr)
 {
     HaloPlan *p;
     RC(get_plan(c, fields, p));
@@ -530,6 +553,13 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
             RC(nccl_rc(ncclSend(peer.send, (size_t)peer.count, ncclDouble, peer.rank, c->comm, stream), "ncclSend"));
         }
         RC(nccl_rc(ncclGroupEnd(), "ncclGroupEnd"));
+    }
+    if (cmp) {
+        if (p->n_local) hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_local), dim3(256), 0, stream, p->d_local, p->n_local, cmp);
+        RC(check_launch());
+        if (p->n_unpack)
+            hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_unpack), dim3(256), 0, stream, p->d_unpack, p->n_unpack, cmp);
+        return check_launch();
     }
     if (p->n_local) {
         hipLaunchKernelGGL(k_segments, dim3(p->n_local), dim3(256), 0, stream, p->d_local, p->n_local);
@@ -551,6 +581,9 @@ static const std::vector<int> kSyncUvTrans = {OCN_HHU_P, OCN_HHV_P, OCN_HHH_P};
 static const std::vector<int> kSyncStress = {OCN_STR_T, OCN_STR_S};
 static const std::vector<int> kSyncUv = {OCN_VBRTRN, OCN_UBRTRN};
 static const std::vector<int> kSyncHhInit = {OCN_HHU, OCN_HHV, OCN_HHH};
+// role-flip steps with halo exchanges: halo values that must equal the neighbours' (ocn_ctx.hip
+// check_coherence)
+static const std::vector<int> kHaloCheck = {OCN_SSH, OCN_UBRTR, OCN_VBRTR, OCN_HHU, OCN_HHV, OCN_HHQ_REST};
 
 static int stage_kernel(ocn_ctx *c, const LBlock &b, int stage, double tau)
 {
@@ -628,6 +661,8 @@ static const std::vector<int> *stage_sync(int stage)
     }
 }
 
+static void swap_roles(ocn_ctx *c);
+
 // every plan a step can use, built before any graph capture (no hipMalloc while capturing)
 static int prebuild_plans(ocn_ctx *c)
 {
@@ -655,8 +690,22 @@ static int prebuild_plans(ocn_ctx *c)
         }
     }
     for (const std::vector<int> *l : {&kSyncSsh, &kSyncHhUpdate, &kSyncVort, &kSyncUvTrans, &kSyncStress, &kSyncUv,
-                                      &kSyncHhInit})
+                                      &kSyncHhInit, &kHaloCheck})
         RC(get_plan(c, *l, p));
+    // role-flip steps: after hh_init + the next step's A, one exchange of both launches' fields
+    c->sync_ca = kSyncHhInit;
+    c->sync_ca.insert(c->sync_ca.end(), c->sync_a.begin(), c->sync_a.end());
+    c->sync_ca_reuse = kSyncHhInit;
+    c->sync_ca_reuse.insert(c->sync_ca_reuse.end(), c->sync_a_reuse.begin(), c->sync_a_reuse.end());
+    RC(get_plan(c, c->sync_ca, p));
+    RC(get_plan(c, c->sync_ca_reuse, p));
+    // the same plans with the pairs' buffers swapped (role 1)
+    if (c->role == 0) {
+        swap_roles(c);
+        const int rc = prebuild_plans(c);
+        swap_roles(c);
+        RC(rc);
+    }
     return OCN_OK;
 }
 
@@ -793,16 +842,29 @@ static bool is_flip_field(int id)
     return false;
 }
 
-// Whether the pairs agree outside their write sets (sw_stencils.h Coherence); synchronises.
-static int check_coherence(ocn_ctx *c)
+// Whether role-flip steps are exact for the current state (synchronises):
+//  - the pairs agree outside their write sets (sw_stencils.h Coherence);
+//  - with halo exchanges, the halo ring of ssh / ubrtr / vbrtr, hhu / hhv and hhq_rest holds the
+//    neighbours' values (what an exchange would deliver; compared, not written).  After a swap
+//    the new ssh holds the exchanged sshn on the whole ring, where a8 copies only under lu (so the
+//    land points of the ring must already agree), and the fused hh_init + A launch takes hh_init's
+//    own ring values where the standard step takes the exchanged ones.
+// Every rank must run the same kind of step (the exchanges differ), so with RCCL the verdicts
+// are max-reduced over the ranks; eligible = false: this rank cannot run role-flip steps at all.
+static int check_coherence(ocn_ctx *c, bool eligible = true)
 {
-    HIPCHK(hipMemsetAsync(c->d_flags, 0, sizeof(int32_t), c->stream));
-    for (const LBlock &b : c->blocks) RC(launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_flags, eligible ? 0 : 1, sizeof(int32_t), c->stream));
+    if (eligible)
+        for (const LBlock &b : c->blocks) RC(launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream));
+    const bool exch = has_exchange(c);
+    if (exch) RC(run_sync(c, kHaloCheck, c->stream, c->d_flags));
+    if (c->comm)
+        RC(nccl_rc(ncclAllReduce(c->d_flags, c->d_flags, 1, ncclInt32, ncclMax, c->comm, c->stream), "ncclAllReduce"));
     int32_t flags = 0;
     HIPCHK(hipMemcpyAsync(&flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->coherent = flags == 0;
-    c->coherent_known = !c->r8_escaped;
+    c->coherent_known = !c->r8_escaped && !c->comm;
     return OCN_OK;
 }
 
@@ -815,11 +877,14 @@ static int check_coherence(ocn_ctx *c)
 // "ubrtrn" / "vbrtrn" after the swap holds the old value there instead -- which no kernel
 // reads before a1 / a7 of the next step rewrite it.  The last step of every call is a standard
 // step; it leaves both buffers of each pair equal everywhere, so the swap is undone at the end
-// of the call by swapping the pointers back, with no copy.  Used for one block per process
-// without halo exchanges, compact tables + march, no tracers.
+// of the call by swapping the pointers back, with no copy.  Used with the compact tables + march
+// and no tracers.  With halo exchanges the swapped buffers are exchanged through plans built for
+// the swapped roles (get_plan), the ring launch (a8 + a9 on the halo ring) runs after sync B, and
+// each hh_init's sync and the next step's sync A are one exchange (sync_ca); the exchanges do
+// not overlap computation in these steps.
 static bool flip_eligible(ocn_ctx *c)
 {
-    return c->flip && c->fused && c->compact && c->march && c->sw.use_tracers <= 0 && !has_exchange(c);
+    return c->flip && c->fused && c->compact && c->march && c->sw.use_tracers <= 0;
 }
 
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
@@ -841,17 +906,20 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
     const bool reuse = sw.full_free_surface == 1 && !first && !last;
     const std::vector<int> &sync_a = reuse ? c->sync_a_reuse : c->sync_a;
     if (flip) {
-        if (last || has_exchange(c)) return set_error(OCN_ERR_STATE, "role-flip step on a last step or with halos");
+        if (last) return set_error(OCN_ERR_STATE, "role-flip step on a last step");
+        if (k.rc && has_exchange(c)) return set_error(OCN_ERR_STATE, "recompute step with halo exchanges");
         if (!k.a_done) {
             RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
             for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
             RC(timer_end(c, rec));
+            RC(run_sync(c, sync_a));
         }
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
         for (const LBlock &b : c->blocks)
             RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, reuse, s, nbad, true, k.rc,
                               (double *)b.sshp_alt));
         RC(timer_end(c, rec));
+        RC(run_sync(c, c->sync_b));   // the current roles' ubrtrn / vbrtrn (+ hhu_p / hhv_p / hhh_p)
         if (k.rc) swap_sshp(c);
         if (c->ring_sea) {   // a8 + a9 on the ring (no interior points); nothing to do on an all-land ring
             RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
@@ -865,23 +933,25 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
                 RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.next_reuse,
                                    k.next_reuse && k.rc_next, s));
             RC(timer_end(c, rec));
+            // hh_init's sync and the next step's sync A in one exchange: A's a1 took hhu / hhv on
+            // the low halo ring from hh_init's registers, the values this exchange delivers there
+            RC(run_sync(c, k.next_reuse ? c->sync_ca_reuse : c->sync_ca));
         } else if (ffs) {
             RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
             for (const LBlock &b : c->blocks) RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, full_c2, s));
             RC(timer_end(c, rec));
+            RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
         }
         return OCN_OK;
     }
-    if (k.a_done && (c->overlap && has_exchange(c)))
-        return set_error(OCN_ERR_STATE, "fused A merged into the previous step with halos");
     if (!(c->overlap && has_exchange(c))) {
-        if (!k.a_done) {
+        if (!k.a_done) {   // else fused A and its sync ran with the previous step's hh_init
             RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
             for (const LBlock &b : c->blocks)
                 RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
             RC(timer_end(c, rec));
+            RC(run_sync(c, sync_a));
         }
-        RC(run_sync(c, sync_a));
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
         for (const LBlock &b : c->blocks)
             RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, last, reuse, s));
@@ -899,17 +969,19 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         }
         return OCN_OK;
     }
-    RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-    for (const LBlock &b : c->blocks)
-        RC(launch_fused_a(FT(b), OCN_PART_FRAME, sw, tau, reuse, s));
-    RC(fork_sync(c, sync_a));
-    for (const LBlock &b : c->blocks)
-        RC(launch_fused_a(FT(b), OCN_PART_INNER, sw, tau, reuse, s));
-    RC(timer_end(c, rec));
+    if (!k.a_done) {   // else fused A and its sync ran with the previous step's hh_init
+        RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fused_a(FT(b), OCN_PART_FRAME, sw, tau, reuse, s));
+        RC(fork_sync(c, sync_a));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fused_a(FT(b), OCN_PART_INNER, sw, tau, reuse, s));
+        RC(timer_end(c, rec));
+    }
     RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
     for (const LBlock &b : c->blocks)
         RC(launch_fused_b(FT(b), OCN_PART_INNER, sw, tau, last, reuse, s));
-    RC(join_sync(c));
+    if (!k.a_done) RC(join_sync(c));
     for (const LBlock &b : c->blocks)
         RC(launch_fused_b(FT(b), OCN_PART_FRAME, sw, tau, last, reuse, s));
     RC(fork_sync(c, c->sync_b));
@@ -1392,15 +1464,18 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
     if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
     if (c->fused) RC(prepare_static(c));
     const bool graph_ok = c->use_graph && !c->comm && !c->stage_timing;   // RCCL / events stay outside graphs
-    bool flip_call = nsteps >= 2 && flip_eligible(c);
-    if (flip_call && !c->coherent_known) RC(check_coherence(c));
-    flip_call = flip_call && c->coherent;
+    // with RCCL every rank takes part in the decision (check_coherence reduces the verdicts)
+    const bool eligible = flip_eligible(c);
+    bool flip_call = nsteps >= 2 && (eligible || (c->comm && c->flip));
+    if (flip_call && !c->coherent_known) RC(check_coherence(c, eligible));
+    flip_call = flip_call && eligible && c->coherent;
     c->flip_used = flip_call;
     // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A;
     // their reuse steps recompute hhq / hhu_p / hhv_p in fused B when no a8 / a9 work lies on the
     // halo ring (so sshp's two buffers only differ where fused B writes)
     const bool ca = flip_call && c->sw.full_free_surface == 1;
-    const bool rc_call = ca && !c->ring_sea && c->recompute;
+    const bool rc_call = ca && !c->ring_sea && c->recompute && !has_exchange(c);
+    c->rc_used = rc_call && nsteps >= 3;
     if (rc_call)   // the second sshp buffer starts as a copy: the two agree outside fused B's write set
         for (const LBlock &b : c->blocks)
             HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
@@ -1520,7 +1595,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_COMPACT: *value = c->fused && c->compact; return OCN_OK;
     case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
-    case OCN_OPT_RECOMPUTE: *value = c->recompute; return OCN_OK;
+    case OCN_OPT_RECOMPUTE: *value = c->recompute && c->rc_used; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -660,9 +660,11 @@ struct MarchHhInit {
 // array's (never written) value from memory.  HH: the next step is not a reuse step, so A's a2
 // hh_update stores hun / hvn / hhn -- bit for bit hh_init's level-0 values (the reuse identity,
 // full_free_surface = 1), under the same masks on the same range.  Nothing this launch writes
-// is read at a neighbour, so there are no races.  hh_init's hhh_p is not stored: on single-block
-// runs its only reader is a9 on the outer ring e+1 (fused C1), outside hh_init's range, and the
-// last step of the call (a standard step) stores it.  SKIP (the next step is a recompute step):
+// is read at a neighbour, so there are no races.  hh_init's hhh_p is stored only before the last
+// step (HH): its only reader is a9 on the outer ring e+1 (the ring launch), outside hh_init's
+// range, which gets it from a neighbour's interior through sync B with halo exchanges; what a9
+// derives from the older values is hhh_p on that ring alone (read by a9 only, and exchanged over
+// before each use), and the last, standard step works from the current ones.  SKIP (the next step is a recompute step):
 // hhq on the interior, hhu_p and hhv_p are not stored either -- their only reader, the next
 // step's fused B, recomputes them (MarchFusedB RC); hhq stays stored on the halo rows / columns
 // (a9 on the ring reads it there).
@@ -751,7 +753,7 @@ template <bool HH, bool SKIP> struct MarchCA {
                     if (inr) {
                         if (llu) { st(c2.hu, c, o.u[0]); if (!SKIP) st(c2.hup, c, o.u[1]); }
                         if (llv) { st(c2.hv, c, o.v[0]); if (!SKIP) st(c2.hvp, c, o.v[1]); }
-                        if (luh) st(c2.hh, c, o.h[0]);   // hhh_p: see below
+                        if (luh) { st(c2.hh, c, o.h[0]); if (HH) st(c2.hhp, c, o.h[1]); }   // hhh_p: see below
                         if (HH) {
                             if (llu) st(a.a2.hun, c, o.u[0]);
                             if (llv) st(a.a2.hvn, c, o.v[0]);

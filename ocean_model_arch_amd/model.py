@@ -146,9 +146,9 @@ class OceanModel:
         return self
 
     def set_flip(self, on: bool = True):
-        """Role-flip steps (default; one block per process, no halo exchange, compact + march, no
-        tracers): sw_next_step's copies become buffer swaps inside the library and its filters run
-        inside fused B; same results bit for bit."""
+        """Role-flip steps (default; compact + march, no tracers): sw_next_step's copies become
+        buffer swaps inside the library and its filters run inside fused B; same results bit for
+        bit."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FLIP, int(on)), "ocn_ctx_set_option")
         return self
 
@@ -167,6 +167,11 @@ class OceanModel:
     def flip_active(self) -> bool:
         """Whether the last step() used role-flip steps."""
         return bool(self.option(_lib.OPT_FLIP))
+
+    @property
+    def recompute_active(self) -> bool:
+        """Whether the last step() used recompute steps."""
+        return bool(self.option(_lib.OPT_RECOMPUTE))
 
     @property
     def compact_active(self) -> bool:

@@ -151,9 +151,9 @@ def compare_case(m, case, name):
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
-    hh_init as register marches, role-flip steps on single-block runs without tracers, halo
-    exchanges overlapped with inner launches when there are several blocks (and, in role-flip
-    calls, hh_init fused with the next step's A and fused B recomputing hhq / hhu_p / hhv_p);
+    hh_init as register marches, role-flip steps without tracers (hh_init fused with the next
+    step's A; on one block fused B also recomputes hhq / hhu_p / hhv_p), halo exchanges overlapped
+    with inner launches in the standard steps when there are several blocks;
     norecompute = compact without the recompute steps; noflip = compact with standard steps only; pointwise = compact with every launch one thread per point; fused =
     the 4-launch step on the 2-D real(4) arrays; serial = compact without the overlap; stages =
     the reference's 11 envoke stages."""
@@ -164,8 +164,11 @@ def test_end_to_end_matches_reference(amd, name, mode):
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     assert m.compact_active == compact
     bad = compare_case(m, case, name)
+    flip_used = m.flip_active
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
+    if mode in ("compact", "norecompute", "serial") and case["sw"].get("use_tracers", 0) <= 0:
+        assert flip_used, f"{name}: role-flip steps not used"
 
 
 @pytest.mark.parametrize("graph", [False, True], ids=["stream", "graph"])
@@ -245,6 +248,51 @@ def test_flip_falls_back_when_pairs_disagree(amd):
         bad = [nm for nm, a in out[(True, kind)].items() if not bits_equal(a, out[(False, kind)][nm])]
         assert not bad, f"{kind}: flip vs standard steps differ in {bad}"
     assert out[(True, "incoherent")]["sshn"][0, 0] != out[(True, "incoherent")]["ssh"][0, 0]
+
+
+@pytest.mark.parametrize("kind", ["sea", "land"])
+def test_flip_falls_back_when_halo_disagrees(amd, kind):
+    """With halo exchanges, role-flip steps also need the halo ring of ssh (and ubrtr, vbrtr,
+    hhu, hhv, hhq_rest) to hold the neighbours' values (ocn_ctx.hip check_coherence).  A state
+    whose ssh and sshn differ there (kind = sea: a sea point of the ring between two blocks, which
+    the exchange and a8 overwrite; land: a land point of that ring, where the standard step keeps
+    ssh and the swapped one would not) must run with
+    standard steps, bit for bit as with OCN_OPT_FLIP off; the unmodified state uses them."""
+    n, steps = 96, 6
+    par = amd.ParallelConfig(2, 1)
+    probe = amd.OceanModel(amd.box_config(n), par=par)
+    xe = [x for x in probe.blocks if x.bm == 1][0].nx_end
+    probe.close()
+    mask = np.zeros((n + 4, n + 4), dtype=np.int32)   # the closed box with a 2-cell land frame ...
+    mask[:2, :] = mask[-2:, :] = mask[:, :2] = mask[:, -2:] = 1
+    mask[xe, n // 2 - 3:n // 2 + 3] = 1               # ... and an island on the column right of block 1
+    out, used = {}, {}
+    for flip in (True, False):
+        for mod in (True, False):
+            m = amd.OceanModel(amd.box_config(n, mask=mask), par=par).set_flip(flip).init()
+            b = [x for x in m.blocks if x.bm == 1][0]
+            if mod:   # the halo column right of block (1, 1) (its neighbour's first interior column):
+                # ssh and sshn changed alike, so the pairs still agree on the block itself
+                i = b.nx_end + 1 - b.bnd_x1
+                lu = m.download(b.k, "lu")[i, b.ny_start - b.bnd_y1:b.ny_end - b.bnd_y1 + 1]
+                rows = np.flatnonzero(lu == (1.0 if kind == "sea" else 0.0))
+                assert rows.size, kind
+                j = b.ny_start - b.bnd_y1 + int(rows[rows.size // 2])
+                for nm in ("ssh", "sshn"):
+                    a = m.download(b.k, nm)
+                    a[i, j] += 0.125
+                    m.upload(b.k, nm, a)
+            m.step(steps).synchronize()
+            used[(flip, mod)] = m.flip_active
+            out[(flip, mod)] = [{nm: m.download(x.k, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn",
+                                                                     "vbrtr", "vbrtrn", "hhu", "hhv", "hhh")}
+                                for x in m.blocks]
+            m.close()
+    for mod in (True, False):
+        bad = [(k, nm) for k, d in enumerate(out[(True, mod)]) for nm, a in d.items()
+               if not bits_equal(a, out[(False, mod)][k][nm])]
+        assert not bad, f"modified={mod}: flip vs standard steps differ in {bad}"
+    assert used[(True, False)] and not used[(True, True)]
 
 
 @pytest.mark.parametrize("name", ["box70x54_b3x2_s20", "bs_b1x1_s60"])
