@@ -165,6 +165,8 @@ def main():
     ap.add_argument("--no-march", action="store_true", help="one thread per point in every launch (no register march)")
     ap.add_argument("--no-flip", action="store_true", help="standard steps only (no role-flip steps)")
     ap.add_argument("--no-recompute", action="store_true", help="role-flip calls without the recompute steps")
+    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
+                    help="halo exchanges beside inner launches: 0 never, 1 standard steps, 2 role-flip steps too")
     ap.add_argument("--blocks", default=None,
                     help="block grid BXxBY (default: one block per GPU); with one GPU, several blocks on it "
                          "exercise the halo-exchange path without RCCL")
@@ -206,6 +208,7 @@ def main():
     model.set_march(not args.no_march)
     model.set_flip(not args.no_flip)
     model.set_recompute(not args.no_recompute)
+    model.set_overlap(args.overlap)
     if args.graph:
         model.set_graph(True)
     model.init()

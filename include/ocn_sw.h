@@ -280,6 +280,9 @@ int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
 
 /* Execution options.
  *  OCN_OPT_GRAPH: replay each step as one hipGraph (single-process runs).
+ *  OCN_OPT_OVERLAP (default 1): with halo exchanges, run each exchange on a second stream beside
+ *  the launches' inner parts (points that neither read halos nor feed the exchange): 1 = in the
+ *  standard steps, 2 = in the role-flip steps too, 0 = never (same results bit for bit).
  *  OCN_OPT_STAGE_TIMING: bracket every launch group with HIP events on the context stream.
  *  OCN_OPT_FUSED (default 1): ocn_ctx_step runs the step as 4 fused launch groups and 3 halo
  *  syncs (same results and final state bit for bit); 0 = the 11 envoke stages of the reference.

@@ -60,29 +60,32 @@ struct Seg {
     int count;
 };
 
-__global__ __launch_bounds__(256) void k_segments(const Seg *__restrict__ segs, int nseg)
+// Grid: x = segment, y = 64-element chunk of it -- one element per thread and one wave per
+// workgroup, so every load of a strip is in flight at once, spread over many CUs (column strips
+// touch one cache line per element; a loop per workgroup would pay one memory round trip per
+// pass).
+constexpr int kSegChunk = 64;
+__global__ __launch_bounds__(kSegChunk) void k_segments(const Seg *__restrict__ segs, int nseg)
 {
     const int s = blockIdx.x;
-    if (s >= nseg) return;
+    const int i = (int)(blockIdx.y * kSegChunk + threadIdx.x);
+    if (s >= nseg || i >= segs[s].count) return;
     const Seg g = segs[s];
-    for (int i = threadIdx.x; i < g.count; i += blockDim.x) g.dst[(long)i * g.dst_stride] = g.src[(long)i * g.src_stride];
+    g.dst[(long)i * g.dst_stride] = g.src[(long)i * g.src_stride];
 }
 
 // The same runs compared instead of copied: ORs 1 into *flags where dst differs from src (bits).
-__global__ __launch_bounds__(256) void k_segments_cmp(const Seg *__restrict__ segs, int nseg, int32_t *flags)
+__global__ __launch_bounds__(kSegChunk) void k_segments_cmp(const Seg *__restrict__ segs, int nseg, int32_t *flags)
 {
     const int s = blockIdx.x;
-    if (s >= nseg) return;
+    const int i = (int)(blockIdx.y * kSegChunk + threadIdx.x);
+    if (s >= nseg || i >= segs[s].count) return;
     const Seg g = segs[s];
-    bool bad = false;
-    for (int i = threadIdx.x; i < g.count; i += blockDim.x) {
-        const double a = g.dst[(long)i * g.dst_stride], b = g.src[(long)i * g.src_stride];
-        unsigned long long x, y;
-        __builtin_memcpy(&x, &a, 8);
-        __builtin_memcpy(&y, &b, 8);
-        bad |= x != y;
-    }
-    if (bad) atomicOr(flags, 1);
+    const double a = g.dst[(long)i * g.dst_stride], b = g.src[(long)i * g.src_stride];
+    unsigned long long x, y;
+    __builtin_memcpy(&x, &a, 8);
+    __builtin_memcpy(&y, &b, 8);
+    if (x != y) atomicOr(flags, 1);
 }
 
 __global__ void k_fill_r8(double *p, long n, double v)
@@ -170,6 +173,7 @@ struct HaloPlan {
     std::vector<Peer> peers;
     Seg *d_pack = nullptr, *d_unpack = nullptr;
     int n_pack = 0, n_unpack = 0;
+    int ch_local = 1, ch_pack = 1, ch_unpack = 1;   // kSegChunk-element chunks of the longest segment
 };
 
 namespace ocn {
@@ -201,7 +205,7 @@ struct ocn_ctx {
     hipStream_t stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchanges overlapped with interior compute
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    bool overlap = true;
+    int overlap = 1;             // OCN_OPT_OVERLAP: 0 none, 1 standard steps, 2 + role-flip steps
     int32_t *d_nbad = nullptr;
     ncclComm_t comm = nullptr;
     std::map<std::vector<int>, HaloPlan> plans;
@@ -230,6 +234,8 @@ struct ocn_ctx {
     // after the state last changed outside ocn_ctx_step; r8_escaped = raw pointers of a pair were
     // handed out (check at every call); flip = OCN_OPT_FLIP
     bool flip = true, coherent = false, flip_used = false, rc_used = false;
+    bool capturing = false;      // a step is being captured into a hipGraph
+    bool sync_pending = false;   // an exchange on comm_stream not yet joined (fork_sync)
     bool ring_sea = true;   // some halo-ring point has a mask set (Prepare); else no ring launch
     bool recompute = true;  // OCN_OPT_RECOMPUTE: recompute steps in role-flip calls
     mutable bool coherent_known = false, r8_escaped = false;
@@ -500,17 +506,19 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
             pack.push_back(Seg{sb.f<double>(e.field) + soff, peers.at(e.peer).send + e.buf_off, sstr, 1, scnt});
         }
     }
-    auto upload = [&](const std::vector<Seg> &v, Seg *&d, int &n) -> int {
+    auto upload = [&](const std::vector<Seg> &v, Seg *&d, int &n, int &ch) -> int {
         n = (int)v.size();
+        ch = 1;
+        for (const Seg &g : v) ch = std::max(ch, (g.count + kSegChunk - 1) / kSegChunk);
         if (!n) return OCN_OK;
         HIPCHK(hipMalloc(&d, sizeof(Seg) * v.size()));
         c->allocs.push_back(d);
         HIPCHK(hipMemcpy(d, v.data(), sizeof(Seg) * v.size(), hipMemcpyHostToDevice));
         return OCN_OK;
     };
-    RC(upload(local, plan.d_local, plan.n_local));
-    RC(upload(pack, plan.d_pack, plan.n_pack));
-    RC(upload(unpack, plan.d_unpack, plan.n_unpack));
+    RC(upload(local, plan.d_local, plan.n_local, plan.ch_local));
+    RC(upload(pack, plan.d_pack, plan.n_pack, plan.ch_pack));
+    RC(upload(unpack, plan.d_unpack, plan.n_unpack, plan.ch_unpack));
     return OCN_OK;
 }
 
@@ -545,7 +553,7 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
     if (!stream) stream = c->stream;
     if (!p->peers.empty()) {
         if (!c->comm) return set_error(OCN_ERR_COMM, "remote neighbours but no RCCL communicator attached");
-        hipLaunchKernelGGL(k_segments, dim3(p->n_pack), dim3(256), 0, stream, p->d_pack, p->n_pack);
+        hipLaunchKernelGGL(k_segments, dim3(p->n_pack, p->ch_pack), dim3(kSegChunk), 0, stream, p->d_pack, p->n_pack);
         RC(check_launch());
         RC(nccl_rc(ncclGroupStart(), "ncclGroupStart"));
         for (auto &peer : p->peers) {
@@ -555,18 +563,22 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
         RC(nccl_rc(ncclGroupEnd(), "ncclGroupEnd"));
     }
     if (cmp) {
-        if (p->n_local) hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_local), dim3(256), 0, stream, p->d_local, p->n_local, cmp);
+        if (p->n_local)
+            hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_local, p->ch_local), dim3(kSegChunk), 0, stream, p->d_local,
+                               p->n_local, cmp);
         RC(check_launch());
         if (p->n_unpack)
-            hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_unpack), dim3(256), 0, stream, p->d_unpack, p->n_unpack, cmp);
+            hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_unpack, p->ch_unpack), dim3(kSegChunk), 0, stream, p->d_unpack,
+                               p->n_unpack, cmp);
         return check_launch();
     }
     if (p->n_local) {
-        hipLaunchKernelGGL(k_segments, dim3(p->n_local), dim3(256), 0, stream, p->d_local, p->n_local);
+        hipLaunchKernelGGL(k_segments, dim3(p->n_local, p->ch_local), dim3(kSegChunk), 0, stream, p->d_local, p->n_local);
         RC(check_launch());
     }
     if (p->n_unpack) {
-        hipLaunchKernelGGL(k_segments, dim3(p->n_unpack), dim3(256), 0, stream, p->d_unpack, p->n_unpack);
+        hipLaunchKernelGGL(k_segments, dim3(p->n_unpack, p->ch_unpack), dim3(kSegChunk), 0, stream, p->d_unpack,
+                           p->n_unpack);
         RC(check_launch());
     }
     return OCN_OK;
@@ -804,17 +816,22 @@ static bool has_exchange(ocn_ctx *c)
     return p->n_local > 0 || !p->peers.empty();
 }
 
+// An exchange forked onto the comm stream stays pending until join_sync (a no-op without one);
+// a role-flip step may leave its last exchange pending for the next step's inner launch.
 static int fork_sync(ocn_ctx *c, const std::vector<int> &fields)
 {
     HIPCHK(hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
     RC(run_sync(c, fields, c->comm_stream));
     HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
+    c->sync_pending = true;
     return OCN_OK;
 }
 static int join_sync(ocn_ctx *c)
 {
+    if (!c->sync_pending) return OCN_OK;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    c->sync_pending = false;
     return OCN_OK;
 }
 
@@ -908,43 +925,84 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
     if (flip) {
         if (last) return set_error(OCN_ERR_STATE, "role-flip step on a last step");
         if (k.rc && has_exchange(c)) return set_error(OCN_ERR_STATE, "recompute step with halo exchanges");
+        // With halo exchanges and OCN_OPT_OVERLAP = 2 (not while capturing a graph: the last
+        // exchange stays pending into the next step), each exchange runs on the comm stream beside
+        // the inner part (launch_march_part) of the next launch:
+        //   [A.frame | fork: sync A || A.inner] B.inner | join | B.frame | fork: sync B || swap,
+        //   CA.inner | join | ring launch (the roles before the swap) | CA.frame | fork: sync CA
+        //   || the next step's B.inner ...
+        // Off by default: the frame bands cost about as much as a local exchange (measured on one
+        // GPU with 2x2 / 4x2 blocks: 1.61 vs 1.47, 1.89 vs 1.69 ms per step).
+        const bool ov = c->overlap >= 2 && has_exchange(c) && !c->capturing;
         if (!k.a_done) {
             RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-            for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
+            if (ov) {
+                for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_FRAME, sw, tau, reuse, s));
+                RC(fork_sync(c, sync_a));
+                for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_INNER, sw, tau, reuse, s));
+            } else {
+                for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
+            }
             RC(timer_end(c, rec));
-            RC(run_sync(c, sync_a));
+            if (!ov) RC(run_sync(c, sync_a));
         }
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, reuse, s, nbad, true, k.rc,
-                              (double *)b.sshp_alt));
+        for (int part : ov ? std::initializer_list<int>{OCN_PART_INNER, OCN_PART_FRAME}
+                           : std::initializer_list<int>{OCN_PART_ALL}) {
+            if (part == OCN_PART_FRAME) RC(join_sync(c));
+            for (const LBlock &b : c->blocks)
+                RC(launch_fused_b(FT(b), part, sw, tau, false, reuse, s, nbad, true, k.rc, (double *)b.sshp_alt));
+        }
         RC(timer_end(c, rec));
-        RC(run_sync(c, c->sync_b));   // the current roles' ubrtrn / vbrtrn (+ hhu_p / hhv_p / hhh_p)
+        // the current roles' ubrtrn / vbrtrn (+ hhu_p / hhv_p / hhh_p)
+        if (ov) RC(fork_sync(c, c->sync_b));
+        else RC(run_sync(c, c->sync_b));
         if (k.rc) swap_sshp(c);
-        if (c->ring_sea) {   // a8 + a9 on the ring (no interior points); nothing to do on an all-land ring
-            RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
-            for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_FRAME, sw, nullptr, s));
+        std::vector<std::vector<void *>> pre;   // the ring launch's field tables (roles before the swap)
+        for (const LBlock &b : c->blocks) pre.push_back(b.ptr);
+        swap_roles(c);
+        // hh_init + the next step's fused A (full_free_surface = 1), else hh_init alone
+        auto hh_init = [&](int part) -> int {
+            for (const LBlock &b : c->blocks) {
+                if (k.next_a)
+                    RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), part, sw, tau, k.next_reuse,
+                                       k.next_reuse && k.rc_next, s));
+                else
+                    RC(launch_fused_c2(FT(b), part, sw, full_c2, s));
+            }
+            return OCN_OK;
+        };
+        const int hh_timer = k.next_a ? OCN_TIMER_FUSED_CA : OCN_STAGE_HH_INIT;
+        const bool hh = k.next_a || ffs;
+        if (ov && hh) {
+            RC(timer_begin(c, hh_timer, rec));
+            RC(hh_init(OCN_PART_INNER));
             RC(timer_end(c, rec));
         }
-        swap_roles(c);
-        if (k.next_a) {   // hh_init + the next step's fused A (full_free_surface = 1)
-            RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
-            for (const LBlock &b : c->blocks)
-                RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.next_reuse,
-                                   k.next_reuse && k.rc_next, s));
+        RC(join_sync(c));
+        if (c->ring_sea) {   // a8 + a9 on the ring (no interior points); nothing to do on an all-land ring
+            RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
+            for (size_t i = 0; i < c->blocks.size(); ++i) {
+                const LBlock &b = c->blocks[i];
+                RC(launch_fused_c1(&b.g, pre[i].data(), (int)pre[i].size(), cp(b, t), OCN_PART_FRAME, sw, nullptr, s));
+            }
             RC(timer_end(c, rec));
-            // hh_init's sync and the next step's sync A in one exchange: A's a1 took hhu / hhv on
-            // the low halo ring from hh_init's registers, the values this exchange delivers there
-            RC(run_sync(c, k.next_reuse ? c->sync_ca_reuse : c->sync_ca));
-        } else if (ffs) {
-            RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-            for (const LBlock &b : c->blocks) RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, full_c2, s));
+        }
+        if (hh) {
+            RC(timer_begin(c, hh_timer, rec));
+            RC(hh_init(ov ? OCN_PART_FRAME : OCN_PART_ALL));
             RC(timer_end(c, rec));
-            RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
+            // with CA, hh_init's sync and the next step's sync A in one exchange: A's a1 took
+            // hhu / hhv on the low halo ring from hh_init's registers, the values it delivers there
+            const std::vector<int> &l = !k.next_a ? *stage_sync(OCN_STAGE_HH_INIT)
+                                        : k.next_reuse ? c->sync_ca_reuse : c->sync_ca;
+            if (ov) RC(fork_sync(c, l));
+            else RC(run_sync(c, l));
         }
         return OCN_OK;
     }
     if (!(c->overlap && has_exchange(c))) {
+        RC(join_sync(c));
         if (!k.a_done) {   // else fused A and its sync ran with the previous step's hh_init
             RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
             for (const LBlock &b : c->blocks)
@@ -981,7 +1039,7 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
     RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
     for (const LBlock &b : c->blocks)
         RC(launch_fused_b(FT(b), OCN_PART_INNER, sw, tau, last, reuse, s));
-    if (!k.a_done) RC(join_sync(c));
+    RC(join_sync(c));   // sync A, or the previous role-flip step's last exchange
     for (const LBlock &b : c->blocks)
         RC(launch_fused_b(FT(b), OCN_PART_FRAME, sw, tau, last, reuse, s));
     RC(fork_sync(c, c->sync_b));
@@ -1434,7 +1492,9 @@ static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
     const int role = c->role;
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    c->capturing = true;
     int rc = run_step(c, tau, k);
+    c->capturing = false;
     hipError_t e = hipStreamEndCapture(c->stream, &graph);
     if (rc) return rc;
     HIPCHK(e);
@@ -1480,6 +1540,7 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
         for (const LBlock &b : c->blocks)
             HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
                                   c->stream));
+    RC(join_sync(c));
     int rc = OCN_OK;
     for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
         StepKind k;
@@ -1494,6 +1555,7 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
         k.rc_next = rc_call && s + 1 < nsteps;
         rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
     }
+    if (const int rj = join_sync(c); rc == OCN_OK) rc = rj;   // nothing stays in flight past the call
     // the last (standard) step left both buffers of each pair equal: undo the swap by pointers;
     // sshp's buffers are not equal: the current one is copied into the field's own buffer
     if (c->role & 1) swap_roles(c);
@@ -1569,8 +1631,8 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         c->fused = value != 0;
         return OCN_OK;
     case OCN_OPT_OVERLAP:
-        if (c->overlap != (value != 0)) drop_graphs(c);
-        c->overlap = value != 0;
+        if (c->overlap != value) drop_graphs(c);
+        c->overlap = value < 0 ? 0 : value > 2 ? 2 : (int)value;
         return OCN_OK;
     case OCN_OPT_MARCH: c->march = value != 0; return OCN_OK;
     case OCN_OPT_FLIP: c->flip = value != 0; return OCN_OK;

@@ -71,8 +71,8 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compac
 // Role-flip calls: step k's hh_init (non-final) and step k+1's fused A in one launch
 // (sw_kernels.hip MarchCA); next_reuse = step k+1 is a reuse step (else A's a2 stores too);
 // skip_rc = step k+1 is a recompute step (hhq on the interior, hhu_p, hhv_p not stored).
-int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
-                    double tau_next, bool next_reuse, bool skip_rc, hipStream_t s);
+int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                    const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s);
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);

@@ -65,11 +65,16 @@ static int launch_range(int m0, int m1, int n0, int n1, const Body &body, hipStr
     return check_launch();
 }
 
-// the frame part of a split range (sw_stencils.h frame_rects): one thread per point
+// the frame part of a split range (sw_stencils.h frame_rects): one thread per point, one wave
+// per workgroup.  The frame's columns touch one cache line per point and array, so the loads a
+// CU can have in flight bound these launches: small workgroups spread them over more CUs.
+#ifndef OCN_FRAME_WG
+#define OCN_FRAME_WG 64
+#endif
 template <typename Body>
-__global__ __launch_bounds__(256) void k_frame(Rects q, int total, Body body)
+__global__ __launch_bounds__(OCN_FRAME_WG) void k_frame(Rects q, int total, Body body)
 {
-    const int t = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int t = (int)(blockIdx.x * OCN_FRAME_WG + threadIdx.x);
     if (t >= total) return;
     int m, n;
     frame_point(q, t, m, n);
@@ -88,7 +93,8 @@ static int launch_part(const Range &r, const Range &inner, int part, const Body 
         const Rects q = frame_rects(r, inner);
         const int total = q.total();
         if (total == 0) return OCN_OK;
-        hipLaunchKernelGGL(k_frame<Body>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, q, total, body);
+        hipLaunchKernelGGL(k_frame<Body>, dim3((unsigned)((total + OCN_FRAME_WG - 1) / OCN_FRAME_WG)), dim3(OCN_FRAME_WG),
+                           0, s, q, total, body);
         return check_launch();
     }
     return launch_range(r.m0, r.m1, r.n0, r.n1, body, s);
@@ -218,43 +224,50 @@ struct Lane { int m, me; bool edge, out; };
 #ifndef OCN_MARCH_LB
 #define OCN_MARCH_LB 1   // minimum waves per SIMD asked of the register allocator
 #endif
+// A march launch covers up to 4 rectangles (one, or the frame bands of a split range): each
+// has its own wave origin w0, tile columns ntx, tile count, column clamps, rows per tile, and
+// workgroup shape (vert: the 4 waves take 4 row tiles of one wave column -- narrow bands).
+struct MarchRect { int m0, m1, n0, n1, w0, ntx, tiles, mlo, mhi, rows, vert; };
+struct MarchGrid { int nr, ntiles; MarchRect r[4]; };
+
 template <class Body>
-__global__ __launch_bounds__(256, OCN_MARCH_LB) void k_march(int m0, int m1, int n0, int n1, int w0, int ntx,
-                                                             int ntiles, int mlo, int mhi, Body body)
+__global__ __launch_bounds__(256, OCN_MARCH_LB) void k_march(MarchGrid g, Body body)
 {
     int tile = (int)blockIdx.x;
 #if OCN_XCD_REMAP
-    const int per = (ntiles + 7) / 8;
+    const int per = (g.ntiles + 7) / 8;
     tile = (tile % 8) * per + tile / 8;
-    if (tile >= ntiles) return;
+    if (tile >= g.ntiles) return;
 #endif
-    const int tx = tile % ntx, ty = tile / ntx;
+    int k = 0;   // workgroup-uniform
+    while (k + 1 < g.nr && tile >= g.r[k].tiles) { tile -= g.r[k].tiles; ++k; }
+    const MarchRect R = g.r[k];
+    const int tx = tile % R.ntx, ty = tile / R.ntx;
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     constexpr int cols = Body::kAligned ? 64 : kMarchCols;
-    const int mw = w0 + (tx * 4 + wave) * cols;   // first output column of this wave
-    if (mw > m1) return;                          // wave-uniform
+    const int mw = R.w0 + (R.vert ? tx : tx * 4 + wave) * cols;   // first output column of this wave
+    const int nb = R.n0 + (R.vert ? ty * 4 + wave : ty) * R.rows, ne = min(R.n1, nb + R.rows - 1);
+    if (mw > R.m1 || nb > R.n1) return;                            // wave-uniform
     Lane L;
     if (Body::kAligned) {
         const int m = mw + lane;
-        L.out = m >= m0 && m <= m1;
-        L.m = min(max(m, mlo), mhi);
-        L.me = min(max(lane == 0 ? m - 1 : m + 1, mlo), mhi);
+        L.out = m >= R.m0 && m <= R.m1;
+        L.m = min(max(m, R.mlo), R.mhi);
+        L.me = min(max(lane == 0 ? m - 1 : m + 1, R.mlo), R.mhi);
         L.edge = lane == 0 || lane == 63;
     } else {
         const int m = mw - 1 + lane;
-        L.out = lane >= 1 && lane <= kMarchCols && m <= m1;
-        L.m = L.me = min(max(m, mlo), mhi);
+        L.out = lane >= 1 && lane <= kMarchCols && m <= R.m1;
+        L.m = L.me = min(max(m, R.mlo), R.mhi);
         L.edge = false;
     }
-    const int nb = n0 + ty * OCN_MARCH_ROWS, ne = min(n1, nb + OCN_MARCH_ROWS - 1);
     body.march(L, nb, ne);
 }
 
 template <typename Body>
-static int launch_march(const ocn_block *b, const Range &r, const Body &body, hipStream_t s)
+static MarchRect march_rect(const ocn_block *b, const Range &r, int rows = OCN_MARCH_ROWS, bool vert = false)
 {
-    if (range_empty(r)) return OCN_OK;
     int w0 = r.m0, cols = kMarchCols, mlo = max(r.m0 - 1, b->bnd_x1), mhi = min(r.m1 + 1, b->bnd_x2);
     if (Body::kAligned) {   // waves start at nx_start + 64 j (256-B aligned rows, ocn_ctx.hip allocate)
         const int d = r.m0 - b->nx_start;
@@ -263,13 +276,62 @@ static int launch_march(const ocn_block *b, const Range &r, const Body &body, hi
         mlo = b->bnd_x1;
         mhi = b->bnd_x2;
     }
-    const int wg_cols = 4 * cols;
-    const int ntx = (r.m1 - w0 + wg_cols) / wg_cols, nty = (r.n1 - r.n0 + OCN_MARCH_ROWS) / OCN_MARCH_ROWS;
-    const int ntiles = ntx * nty;
-    const int nblocks = OCN_XCD_REMAP ? 8 * ((ntiles + 7) / 8) : ntiles;
-    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, r.m0, r.m1, r.n0, r.n1, w0, ntx,
-                       ntiles, mlo, mhi, body);
+    const int wg_cols = (vert ? 1 : 4) * cols, wg_rows = (vert ? 4 : 1) * rows;
+    const int ntx = (r.m1 - w0 + wg_cols) / wg_cols, nty = (r.n1 - r.n0 + wg_rows) / wg_rows;
+    return MarchRect{r.m0, r.m1, r.n0, r.n1, w0, ntx, ntx * nty, mlo, mhi, rows, vert ? 1 : 0};
+}
+
+// rows = rows per tile (0: OCN_MARCH_ROWS); vert: see MarchRect
+template <typename Body>
+static int launch_march_rects(const ocn_block *b, const Range *rs, int nr, const Body &body, hipStream_t s,
+                              int rows = 0, bool vert = false)
+{
+    MarchGrid g{};
+    for (int i = 0; i < nr; ++i)
+        if (!range_empty(rs[i])) {
+            g.r[g.nr] = march_rect<Body>(b, rs[i], rows > 0 ? rows : OCN_MARCH_ROWS, vert && i >= 2);
+            g.ntiles += g.r[g.nr].tiles;
+            ++g.nr;
+        }
+    if (!g.nr) return OCN_OK;
+    const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
+    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, body);
     return check_launch();
+}
+
+template <typename Body>
+static int launch_march(const ocn_block *b, const Range &r, const Body &body, hipStream_t s)
+{
+    return launch_march_rects(b, &r, 1, body, s);
+}
+
+// Halo-overlap split of a march launch's range: the inner part keeps 64 columns and 8 rows
+// (a wave's width, a tile's height) away from the interior's edges, the frame is the rest as up
+// to 4 bands, marched in one launch with short tiles (OCN_FRAME_ROWS rows; the left / right
+// bands one wave wide with 4 row tiles per workgroup) -- a frame launch has too few waves to
+// hide a long march's latency.  Inner points read no halo value and produce nothing a
+// neighbour receives (the stencils reach +-1), so the inner part may run while an exchange is
+// in flight.
+#ifndef OCN_FRAME_ROWS
+#define OCN_FRAME_ROWS 2
+#endif
+static Range march_inner(const ocn_block *b)
+{
+    return {b->nx_start + 64, b->nx_end - 64, b->ny_start + OCN_MARCH_ROWS, b->ny_end - OCN_MARCH_ROWS};
+}
+template <typename Body>
+static int launch_march_part(const ocn_block *b, const Range &all, int part, const Body &body, hipStream_t s)
+{
+    if (part == OCN_PART_INNER) return launch_march(b, range_clip(all, march_inner(b)), body, s);
+    if (part == OCN_PART_FRAME) {
+        const Range in = range_clip(all, march_inner(b));
+        if (range_empty(in)) return launch_march(b, all, body, s);
+        const Rects q = frame_rects(all, in);
+        Range rs[4];
+        for (int i = 0; i < 4; ++i) rs[i] = {q.m0[i], q.m0[i] + q.w[i] - 1, q.n0[i], q.n0[i] + q.h[i] - 1};
+        return launch_march_rects(b, rs, 4, body, s, OCN_FRAME_ROWS, true);
+    }
+    return launch_march(b, all, body, s);
 }
 
 // Software pipelining of the marches (OCN_MARCH_PF = 1): the loads a row needs ("batch" of
@@ -869,24 +931,21 @@ static int launch_fused(const Range &r, const Range &inner, int part, const ocn_
                        s);
 }
 
-// With the compact tables and OCN_OPT_MARCH, the ALL and INNER parts of fused A, fused B and
-// hh_init run as register marches; the FRAME part (thin strips) stays one thread per point.
-static bool use_march(const Compact *cp, int part) { return cp && cp->march && part != OCN_PART_FRAME; }
-static Range march_range(const Range &all, const ocn_block *b, int part)
-{
-    return part == OCN_PART_INNER ? range_clip(all, inner_interior_shrunk(b)) : all;
-}
+// With the compact tables and OCN_OPT_MARCH, fused A, fused B and hh_init run as register
+// marches, their halo-overlap parts split as launch_march_part does (bands of a wave's width);
+// otherwise one thread per point, split as sw_stencils.h frame_rects does (thin strips).
+static bool use_march(const Compact *cp) { return cp && cp->march; }
 
 int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool reuse, hipStream_t s)
 {
     const Range all = range_fused_a(b, sw, reuse);
-    if (use_march(cp, part)) {
+    if (use_march(cp)) {
         RC_K(check_block(b));
         const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
         if (sw.full_free_surface > 0 && !reuse)
-            return launch_march(b, march_range(all, b, part), MarchFusedA<true>{*b, t, sw, tau}, s);
-        return launch_march(b, march_range(all, b, part), MarchFusedA<false>{*b, t, sw, tau}, s);
+            return launch_march_part(b, all, part, MarchFusedA<true>{*b, t, sw, tau}, s);
+        return launch_march_part(b, all, part, MarchFusedA<false>{*b, t, sw, tau}, s);
     }
     return launch_fused<KFusedA>(all, inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s, sw, tau, reuse);
 }
@@ -897,14 +956,16 @@ int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact
 {
     if (rc && (!flip || !reuse || sw.full_free_surface != 1 || !sshp_out))
         return set_error(OCN_ERR_ARG, "recomputed depths only on role-flip reuse steps with full_free_surface = 1");
-    if (use_march(cp, part)) {
+    if (use_march(cp)) {
         RC_K(check_block(b));
         const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
-        const Range r = march_range(range_interior(b), b, part);
+        const Range r = range_interior(b);
         if (flip && rc)
-            return launch_march(b, r, MarchFusedB<true, true>{*b, t, sw, tau, full, reuse, flip_nbad, sshp_out}, s);
-        if (flip) return launch_march(b, r, MarchFusedB<true>{*b, t, sw, tau, full, reuse, flip_nbad, nullptr}, s);
-        return launch_march(b, r, MarchFusedB<false>{*b, t, sw, tau, full, reuse, nullptr, nullptr}, s);
+            return launch_march_part(b, r, part, MarchFusedB<true, true>{*b, t, sw, tau, full, reuse, flip_nbad, sshp_out},
+                                     s);
+        if (flip)
+            return launch_march_part(b, r, part, MarchFusedB<true>{*b, t, sw, tau, full, reuse, flip_nbad, nullptr}, s);
+        return launch_march_part(b, r, part, MarchFusedB<false>{*b, t, sw, tau, full, reuse, nullptr, nullptr}, s);
     }
     if (flip) return set_error(OCN_ERR_ARG, "the role-flip step needs the compact tables and the march");
     return launch_fused<KFusedB>(range_interior(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s, sw, tau,
@@ -920,27 +981,27 @@ int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compac
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, bool full, hipStream_t s)
 {
-    if (use_march(cp, part)) {
+    if (use_march(cp)) {
         RC_K(check_block(b));
         const MarchHhInit k{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0),
                             (int)sw.full_free_surface, full};
-        return launch_march(b, march_range(range_bnd(b), b, part), k, s);
+        return launch_march_part(b, range_bnd(b), part, k, s);
     }
     return launch_fused<KHhInit>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s,
                                  (int)sw.full_free_surface, full);
 }
 
-int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
-                    double tau_next, bool next_reuse, bool skip_rc, hipStream_t s)
+int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
+                    const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || (skip_rc && !next_reuse))
         return set_error(OCN_ERR_ARG, "fused hh_init + A needs the compact tables, the march and full_free_surface = 1");
     RC_K(check_block(b));
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
     const Range r = range_bnd(b);
-    if (skip_rc) return launch_march(b, r, MarchCA<false, true>{*b, t, sw, tau_next}, s);
-    if (next_reuse) return launch_march(b, r, MarchCA<false, false>{*b, t, sw, tau_next}, s);
-    return launch_march(b, r, MarchCA<true, false>{*b, t, sw, tau_next}, s);
+    if (skip_rc) return launch_march_part(b, r, part, MarchCA<false, true>{*b, t, sw, tau_next}, s);
+    if (next_reuse) return launch_march_part(b, r, part, MarchCA<false, false>{*b, t, sw, tau_next}, s);
+    return launch_march_part(b, r, part, MarchCA<true, false>{*b, t, sw, tau_next}, s);
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy

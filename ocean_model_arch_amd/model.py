@@ -128,8 +128,9 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FUSED, int(on)), "ocn_ctx_set_option")
         return self
 
-    def set_overlap(self, on: bool = True):
-        """Overlap halo exchanges (comm stream) with the interior part of the fused launches (default)."""
+    def set_overlap(self, on: int = 1):
+        """Overlap halo exchanges (comm stream) with the inner part of the fused launches: 1 = in
+        the standard steps (default), 2 = in the role-flip steps too, 0 = never."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_OVERLAP, int(on)), "ocn_ctx_set_option")
         return self
 

@@ -111,7 +111,7 @@ def test_tracer_kernels_match_reference(amd, geom):
     assert not failures, f"{geom}: differs from the reference: {failures}"
 
 
-def build_model(amd, case, graph=False, fused=True, compact=True, overlap=True, march=True, flip=True,
+def build_model(amd, case, graph=False, fused=True, compact=True, overlap=1, march=True, flip=True,
                 recompute=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
@@ -147,19 +147,23 @@ def compare_case(m, case, name):
     return bad
 
 
-@pytest.mark.parametrize("mode", ["compact", "norecompute", "noflip", "pointwise", "fused", "stages", "serial"])
+@pytest.mark.parametrize("mode", ["compact", "norecompute", "noflip", "pointwise", "fused", "stages", "serial",
+                                  "overlap2"])
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
     hh_init as register marches, role-flip steps without tracers (hh_init fused with the next
     step's A; on one block fused B also recomputes hhq / hhu_p / hhv_p), halo exchanges overlapped
     with inner launches in the standard steps when there are several blocks;
-    norecompute = compact without the recompute steps; noflip = compact with standard steps only; pointwise = compact with every launch one thread per point; fused =
+    norecompute = compact without the recompute steps; noflip = compact with standard steps only;
+    pointwise = compact with every launch one thread per point; overlap2 = compact with the
+    role-flip steps' exchanges overlapped too (OCN_OPT_OVERLAP = 2); fused =
     the 4-launch step on the 2-D real(4) arrays; serial = compact without the overlap; stages =
     the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    compact = mode in ("compact", "norecompute", "noflip", "serial", "pointwise")
-    m = build_model(amd, case, fused=mode != "stages", compact=compact, overlap=mode != "serial",
+    compact = mode in ("compact", "norecompute", "noflip", "serial", "pointwise", "overlap2")
+    m = build_model(amd, case, fused=mode != "stages", compact=compact,
+                    overlap=2 if mode == "overlap2" else int(mode != "serial"),
                     march=mode != "pointwise", flip=mode != "noflip", recompute=mode != "norecompute")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     assert m.compact_active == compact
@@ -167,7 +171,7 @@ def test_end_to_end_matches_reference(amd, name, mode):
     flip_used = m.flip_active
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
-    if mode in ("compact", "norecompute", "serial") and case["sw"].get("use_tracers", 0) <= 0:
+    if mode in ("compact", "norecompute", "serial", "overlap2") and case["sw"].get("use_tracers", 0) <= 0:
         assert flip_used, f"{name}: role-flip steps not used"
 
 
@@ -346,11 +350,16 @@ def _oracle_state(n, bxy, steps):
     return om
 
 
-@pytest.mark.parametrize("n,bxy,steps,fused", [(256, (1, 1), 10, True), (1024, (1, 1), 3, True),
-                                                (300, (3, 2), 8, True), (300, (3, 2), 8, False)])
-def test_larger_boxes_match_oracle(amd, n, bxy, steps, fused):
+@pytest.mark.parametrize("n,bxy,steps,fused,overlap", [(256, (1, 1), 10, True, 1), (1024, (1, 1), 3, True, 1),
+                                                        (300, (3, 2), 8, True, 1), (300, (3, 2), 8, False, 1),
+                                                        (1024, (2, 2), 4, True, 1), (1024, (2, 2), 4, True, 2),
+                                                        (520, (3, 2), 6, True, 2), (520, (3, 2), 6, True, 0)])
+def test_larger_boxes_match_oracle(amd, n, bxy, steps, fused, overlap):
+    """Against the oracle on boxes whose blocks are wide enough for the halo-overlap split of the
+    march launches (inner part 64 columns / 8 rows inside the interior, frame bands around it)."""
     om = _oracle_state(n, bxy, steps)
     m = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(*bxy)).set_fused(fused)
+    m.set_overlap(overlap)
     m.init().step(steps).synchronize()
     bad = []
     for b in m.blocks:
