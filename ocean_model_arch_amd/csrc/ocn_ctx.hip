@@ -924,7 +924,6 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
     const std::vector<int> &sync_a = reuse ? c->sync_a_reuse : c->sync_a;
     if (flip) {
         if (last) return set_error(OCN_ERR_STATE, "role-flip step on a last step");
-        if (k.rc && has_exchange(c)) return set_error(OCN_ERR_STATE, "recompute step with halo exchanges");
         // With halo exchanges and OCN_OPT_OVERLAP = 2 (not while capturing a graph: the last
         // exchange stays pending into the next step), each exchange runs on the comm stream beside
         // the inner part (launch_march_part) of the next launch:
@@ -984,7 +983,10 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
             RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
             for (size_t i = 0; i < c->blocks.size(); ++i) {
                 const LBlock &b = c->blocks[i];
-                RC(launch_fused_c1(&b.g, pre[i].data(), (int)pre[i].size(), cp(b, t), OCN_PART_FRAME, sw, nullptr, s));
+                // recompute steps: B filtered sshp into the other buffer, now the current one; a8
+                // on the ring reads the previous one (sshp_alt after the swap) and completes it
+                RC(launch_fused_c1(&b.g, pre[i].data(), (int)pre[i].size(), cp(b, t), OCN_PART_FRAME, sw, nullptr, s,
+                                   k.rc ? (const double *)b.sshp_alt : nullptr));
             }
             RC(timer_end(c, rec));
         }
@@ -1531,12 +1533,12 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
     flip_call = flip_call && eligible && c->coherent;
     c->flip_used = flip_call;
     // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A;
-    // their reuse steps recompute hhq / hhu_p / hhv_p in fused B when no a8 / a9 work lies on the
-    // halo ring (so sshp's two buffers only differ where fused B writes)
+    // their reuse steps recompute hhq / hhu_p / hhv_p in fused B, which then filters sshp into
+    // the second buffer (the ring launch completes it on the halo ring)
     const bool ca = flip_call && c->sw.full_free_surface == 1;
-    const bool rc_call = ca && !c->ring_sea && c->recompute && !has_exchange(c);
+    const bool rc_call = ca && c->recompute;
     c->rc_used = rc_call && nsteps >= 3;
-    if (rc_call)   // the second sshp buffer starts as a copy: the two agree outside fused B's write set
+    if (rc_call)   // the second sshp buffer starts as a copy: the two agree outside a8's write set
         for (const LBlock &b : c->blocks)
             HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
                                   c->stream));

@@ -64,8 +64,9 @@ int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s,
                    int32_t *flip_nbad = nullptr, bool flip = false, bool rc = false, double *sshp_out = nullptr);
+// sshp_in: a8 reads sshp there and writes the table's sshp (recompute steps), nullptr = in place
 int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s);
+                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s, const double *sshp_in = nullptr);
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, bool full, hipStream_t s);
 // Role-flip calls: step k's hh_init (non-final) and step k+1's fused A in one launch

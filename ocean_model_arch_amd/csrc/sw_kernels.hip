@@ -973,9 +973,9 @@ int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact
 }
 
 int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s)
+                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s, const double *sshp_in)
 {
-    return launch_fused<KFusedC1>(range_ring(b), range_interior(b), part, b, ptr, nptr, cp, 0, s, sw, nbad);
+    return launch_fused<KFusedC1>(range_ring(b), range_interior(b), part, b, ptr, nptr, cp, 0, s, sw, nbad, sshp_in);
 }
 
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,

@@ -552,13 +552,16 @@ OCN_HD OCN_INLINE double asselin(double x, double xn, double xp, double ts) { re
 template <bool C> struct SwNextStep {
     Geo I; double ts;
     Msk<C> lu, lcu, lcv;
-    double *__restrict__ ssh, *__restrict__ sshn, *__restrict__ sshp;
+    double *__restrict__ ssh, *__restrict__ sshn, *sshp;
     double *__restrict__ u, *__restrict__ un, *__restrict__ up;
     double *__restrict__ v, *__restrict__ vn, *__restrict__ vp;
+    // where sshp is read from when it is filtered into another buffer (ocn_ctx.hip recompute
+    // steps with a8 work on the halo ring); nullptr = in place
+    const double *sshp_in = nullptr;
     // returns the ssh value after the update (for check_ssh_err)
     OCN_HD OCN_INLINE double step(Pt i) const
     {
-        const double x = ld(ssh, i), xn = ld(sshn, i), xp = ld(sshp, i);
+        const double x = ld(ssh, i), xn = ld(sshn, i), xp = ld(sshp_in ? sshp_in : sshp, i);
         const double a = ld(u, i), an = ld(un, i), ap = ld(up, i);
         const double b = ld(v, i), bn = ld(vn, i), bp = ld(vp, i);
         const double fx = asselin(x, xn, xp, ts), fa = asselin(a, an, ap, ts), fb = asselin(b, bn, bp, ts);
@@ -1069,10 +1072,14 @@ OCN_HD inline FusedB<C> make_fused_b(const ocn_block *b, const Tab<C> &t, const 
     if (reuse) { k.a7.hhun = k.a7.hhu; k.a7.hhvn = k.a7.hhv; }
     return k;
 }
-template <bool C> OCN_HD inline FusedC1<C> make_fused_c1(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, int32_t *nbad)
+template <bool C>
+OCN_HD inline FusedC1<C> make_fused_c1(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, int32_t *nbad,
+                                       const double *sshp_in = nullptr)
 {
-    return FusedC1<C>{b->nx_start, b->nx_end, b->ny_start, b->ny_end, sw.full_free_surface > 0, (int *)nbad,
-                      make_sw_next_step(b, t, sw.time_smooth), make_hh_shift(b, t, sw.time_smooth)};
+    FusedC1<C> k{b->nx_start, b->nx_end, b->ny_start, b->ny_end, sw.full_free_surface > 0, (int *)nbad,
+                 make_sw_next_step(b, t, sw.time_smooth), make_hh_shift(b, t, sw.time_smooth)};
+    k.a8.sshp_in = sshp_in;
+    return k;
 }
 
 // ------------------------------------------------------------------ launch functors
@@ -1089,7 +1096,8 @@ template <bool C> struct KFusedB {
 };
 template <bool C> struct KFusedC1 {
     ocn_block b; Tab<C> t; ocn_sw_params sw; int32_t *nbad;
-    OCN_HD void operator()(int m, int n) const { make_fused_c1(&b, t, sw, nbad)(m, n); }
+    const double *sshp_in = nullptr;   // see SwNextStep
+    OCN_HD void operator()(int m, int n) const { make_fused_c1(&b, t, sw, nbad, sshp_in)(m, n); }
 };
 template <bool C> struct KHhInit {
     ocn_block b; Tab<C> t; int ffs; bool full;

@@ -153,7 +153,7 @@ def compare_case(m, case, name):
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
     hh_init as register marches, role-flip steps without tracers (hh_init fused with the next
-    step's A; on one block fused B also recomputes hhq / hhu_p / hhv_p), halo exchanges overlapped
+    step's A, fused B recomputing hhq / hhu_p / hhv_p), halo exchanges overlapped
     with inner launches in the standard steps when there are several blocks;
     norecompute = compact without the recompute steps; noflip = compact with standard steps only;
     pointwise = compact with every launch one thread per point; overlap2 = compact with the
