@@ -199,6 +199,14 @@ module ocn_sw_c
             integer(c_int), value :: k, id
             type(c_ptr), value :: host
         end function
+        ! output.f90 copy_from_real8 + io.f90 write_data2D_real4: interior record as real(4), undef on land
+        integer(c_int) function ocn_ctx_output_r4(ctx, k, id, undef, host) bind(C, name='ocn_ctx_output_r4')
+            import :: c_int, c_ptr, c_float
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: k, id
+            real(c_float), value :: undef
+            type(c_ptr), value :: host
+        end function
         type(c_ptr) function ocn_last_error() bind(C, name='ocn_last_error')
             import :: c_ptr
         end function

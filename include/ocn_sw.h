@@ -277,6 +277,11 @@ int ocn_ctx_synchronize(ocn_ctx *ctx);
  * leading dim bnd_x2-bnd_x1+1, 4 or 8 bytes per element by field kind). Synchronous. */
 int ocn_ctx_download(ocn_ctx *ctx, int k, int field_id, void *host);
 int ocn_ctx_upload(ocn_ctx *ctx, int k, int field_id, const void *host);
+/* Output record of one field of local block k (control/output.f90:32-174 bufwp4%copy_from_real8
+ * + tools/io.f90:276-386 write_data2D_real4): the interior nx_start..nx_end x ny_start..ny_end,
+ * Fortran order, as real(4) (round to nearest from real(8)), with `undef` where |lu| < 0.5.
+ * Converted on the device; host receives (nx_end-nx_start+1)*(ny_end-ny_start+1) floats. Synchronous. */
+int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *host);
 
 /* Execution options.
  *  OCN_OPT_GRAPH: replay each step as one hipGraph (single-process runs).

@@ -84,7 +84,7 @@ KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "oc
 CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
                "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm",
                "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
-               "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version"]
+               "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version"]
 ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
 
 
@@ -181,6 +181,7 @@ def lib() -> C.CDLL:
     L.ocn_ctx_step.argtypes = [C.c_void_p, C.c_double, C.c_int32, C.c_int32]
     L.ocn_ctx_download.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
     L.ocn_ctx_upload.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    L.ocn_ctx_output_r4.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_void_p]
     L.ocn_ctx_set_option.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
     L.ocn_ctx_get_option.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]
     L.ocn_ctx_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]

@@ -94,6 +94,17 @@ __global__ void k_fill_r8(double *p, long n, double v)
     if (i < n) p[i] = v;
 }
 
+// One output record of a field (output.f90:101-106 copy_from_real8 + io.f90:343-349): real(4) of
+// the interior value, undef where |lu| < 0.5; dst is the packed interior, Fortran order.
+template <typename T>
+__global__ void k_output_r4(const T *src, const float *lu, long pitch, int w, int h, float undef, float *dst)
+{
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x), j = (int)blockIdx.y;
+    if (i >= w || j >= h) return;
+    const long s = (long)j * pitch + i;
+    dst[(long)j * w + i] = fabsf(lu[s]) < 0.5f ? undef : (float)src[s];
+}
+
 // ------------------------------------------------------------------ geometry helpers
 // decomposition.f90:94-290, directions macros/kernel_macros.fi:4-12
 struct Rect { int x0, x1, y0, y1; };
@@ -1610,6 +1621,32 @@ int ocn_ctx_download(ocn_ctx *c, int k, int id, void *host)
     HIPCHK(hipMemcpy2D(host, w * es, b.ptr[field_slot(id)], (size_t)b.g.pitch * es, w * es, rows,
                        hipMemcpyDeviceToHost));
     return OCN_OK;
+}
+
+int ocn_ctx_output_r4(ocn_ctx *c, int k, int id, float undef, float *host)
+{
+    if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
+        return set_error(OCN_ERR_ARG, "output_r4: bad argument");
+    const LBlock &b = c->blocks[k];
+    const int w = b.g.nx_end - b.g.nx_start + 1, h = b.g.ny_end - b.g.ny_start + 1;
+    if (w <= 0 || h <= 0) return OCN_OK;
+    const long off = (long)(b.g.ny_start - b.g.bnd_y1) * b.g.pitch + (b.g.nx_start - b.g.bnd_x1);
+    float *d = nullptr;
+    HIPCHK(hipMallocAsync((void **)&d, (size_t)w * h * sizeof(float), c->stream));
+    const float *lu = b.f<float>(OCN_LU) + off;
+    const dim3 grid((unsigned)((w + 255) / 256), (unsigned)h);
+    if (is_r4(id))
+        hipLaunchKernelGGL(k_output_r4<float>, grid, dim3(256), 0, c->stream, b.f<float>(id) + off, lu,
+                           (long)b.g.pitch, w, h, undef, d);
+    else
+        hipLaunchKernelGGL(k_output_r4<double>, grid, dim3(256), 0, c->stream, b.f<double>(id) + off, lu,
+                           (long)b.g.pitch, w, h, undef, d);
+    int rc = check_launch();
+    if (rc == OCN_OK && hipMemcpyAsync(host, d, (size_t)w * h * sizeof(float), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        rc = set_error(OCN_ERR_HIP, "output_r4: copy");
+    (void)hipFreeAsync(d, c->stream);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return rc;
 }
 
 int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)

@@ -216,6 +216,15 @@ class OceanModel:
         check(lib().ocn_ctx_download(self.ctx, k, FIELD_ID[name], a.ctypes.data_as(C.c_void_p)), "download")
         return a
 
+    def output_r4(self, k: int, name: str, undef: float) -> np.ndarray:
+        """Output record of field `name` on block k's interior: real(4), undef on land
+        (output.f90 copy_from_real8 + io.f90:343-349), converted on the device."""
+        b = self.blocks[k]
+        a = np.zeros((b.nx_end - b.nx_start + 1, b.ny_end - b.ny_start + 1), dtype=np.float32, order="F")
+        check(lib().ocn_ctx_output_r4(self.ctx, k, FIELD_ID[name], C.c_float(undef), a.ctypes.data_as(C.c_void_p)),
+              "output_r4")
+        return a
+
     def upload(self, k: int, name: str, a: np.ndarray):
         b = self.blocks[k]
         dt = np.float64 if is_r8_name(name) else np.float32
