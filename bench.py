@@ -151,6 +151,19 @@ def load_traffic(stage: str, cells: int, compact: bool):
         return None
 
 
+def launch_ranks(n: int) -> int:
+    """torch.distributed.run with n processes on this node (127.0.0.1 rendezvous), each running
+    this script with the same arguments; returns its exit status.  The parent stays GPU-free."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -172,6 +185,10 @@ def main():
                          "exercise the halo-exchange path without RCCL")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # started directly (`python bench.py --gpus N`): launch the N ranks, one process per GPU,
+        # before this process touches torch or HIP; rank 0 prints the JSON line
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -284,6 +301,10 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     if out is not None:
+        if world > 1 and parity is not True:
+            # the N-rank path disagrees with the single-process block grid: no number
+            print(json.dumps({"error": "multi_gpu_parity_512 failed", "multi_gpu_parity_512": parity}), flush=True)
+            sys.exit(3)
         print(json.dumps(out), flush=True)
 
 

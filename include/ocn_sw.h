@@ -256,6 +256,13 @@ void *ocn_ctx_stream(const ocn_ctx *ctx);
 /* RCCL: unique id (128 bytes) made on rank 0, broadcast by the host, then attached. */
 int ocn_comm_unique_id(void *out_id, int32_t nbytes);
 int ocn_ctx_attach_comm(ocn_ctx *ctx, const void *unique_id, int32_t nbytes);
+/* Test transport: the n ranks of one decomposition as n contexts of ONE process on one device
+ * (ctxs[i] = rank i of nranks = n), each then driven by its own host thread.  Replaces only the
+ * RCCL calls (the per-peer ncclRecv/ncclSend of an exchange become device copies between the
+ * contexts' message buffers behind event handshakes; the role-flip vote's ncclAllReduce a device
+ * max over the contexts); every other part of the multi-rank path is the production one.  Call
+ * before ocn_ctx_init_state; the contexts may be destroyed in any order. */
+int ocn_ctx_attach_loopback(ocn_ctx *const *ctxs, int32_t n);
 
 /* Initial state: init_grid_data + init_ocean_data (control/init_data.f90:29-125). */
 int ocn_ctx_init_state(ocn_ctx *ctx);

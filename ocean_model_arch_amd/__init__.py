@@ -6,7 +6,7 @@ libocn_sw.so (C ABI: include/ocn_sw.h), hosts in Python (this package) and Fortr
 """
 from ._lib import OcnError, OcnLibraryError, build, lib  # noqa: F401
 from .config import BasinConfig, ParallelConfig, SWConfig, box_config, read_mask  # noqa: F401
-from .model import OceanModel, make_unique_id  # noqa: F401
+from .model import OceanModel, make_unique_id, run_ranks  # noqa: F401
 
 __all__ = ["OceanModel", "BasinConfig", "SWConfig", "ParallelConfig", "box_config", "read_mask",
-           "make_unique_id", "build", "lib", "OcnError", "OcnLibraryError"]
+           "make_unique_id", "run_ranks", "build", "lib", "OcnError", "OcnLibraryError"]

@@ -82,7 +82,7 @@ KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "oc
                   "ocn_hh_shift", "ocn_hh_init", "ocn_check_ssh_err", "ocn_tran_diff_fluxes",
                   "ocn_tran_diff_tracer", "ocn_tracer_next_step"]
 CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
-               "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm",
+               "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm", "ocn_ctx_attach_loopback",
                "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
                "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version"]
 ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
@@ -178,6 +178,7 @@ def lib() -> C.CDLL:
     L.ocn_ctx_block_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(OcnBlockInfo)]
     L.ocn_ctx_sync.argtypes = [C.c_void_p, C.c_int]
     L.ocn_ctx_stage.argtypes = [C.c_void_p, C.c_int, C.c_double]
+    L.ocn_ctx_tracer_stage.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double]
     L.ocn_ctx_step.argtypes = [C.c_void_p, C.c_double, C.c_int32, C.c_int32]
     L.ocn_ctx_download.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
     L.ocn_ctx_upload.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
@@ -187,6 +188,7 @@ def lib() -> C.CDLL:
     L.ocn_ctx_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ocn_ctx_attach_comm.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     L.ocn_comm_unique_id.argtypes = [C.c_void_p, C.c_int32]
+    L.ocn_ctx_attach_loopback.argtypes = [C.POINTER(C.c_void_p), C.c_int32]
     L.ocn_decompose.argtypes = [C.POINTER(OcnBasin), C.POINTER(OcnDecomp), C.c_void_p, C.POINTER(OcnBlockInfo),
                                 C.c_int32, C.POINTER(C.c_int32)]
     L.ocn_halo_schedule.argtypes = [C.POINTER(OcnBasin), C.POINTER(OcnDecomp), C.c_void_p, C.POINTER(C.c_int32),

@@ -15,9 +15,12 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -176,6 +179,34 @@ struct LBlock {
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
+// Loopback transport (ocn_ctx_attach_loopback): the N ranks of a decomposition as N contexts of
+// ONE process on one device, each driven by its own host thread.  It replaces exactly two RCCL
+// calls and nothing else -- the ncclRecv / ncclSend pair of an exchange (run_sync) and the
+// ncclAllReduce of the role-flip vote (check_coherence) -- so the remote branch of the halo plans
+// (device pack / unpack, per-peer messages, per-role plans, sync_ca, overlap forks) runs as in
+// production.  An exchange is two host rendezvous with the peers:
+//   A: each rank has enqueued its pack and recorded lb_ev_a, and publishes its plan; then every
+//      rank copies each peer's send buffer (for it) into its own receive buffer, on its stream,
+//      after the peer's lb_ev_a, and records lb_ev_b;
+//   B: every rank's stream waits for its peers' lb_ev_b, so no send buffer is repacked before the
+//      peer's copy out of it has run (the completion guarantee of ncclGroupEnd).
+// The counters make the rendezvous of the k-th exchange of every rank meet (all ranks run the
+// same sequence of exchanges, as with RCCL); a peer cannot pass phase A of exchange k+1 before
+// this rank passed phase B of exchange k, so a published plan / recorded event is never replaced
+// before it was consumed.
+struct HaloPlan;
+struct Loopback {
+    int n = 0;
+    std::vector<ocn_ctx *> ctx;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint64_t> cnt[4];              // per rank: exchange A/B, reduce A/B phases passed
+    std::vector<const HaloPlan *> plan;        // plan of the rank's current exchange (phase A)
+    std::vector<int32_t *> vote;               // the rank's flag word (reduce phase A)
+    bool failed = false;
+    int refs = 0;
+};
+
 struct HaloPlan {
     Seg *d_local = nullptr;           // intra-process copies
     int n_local = 0;
@@ -219,11 +250,15 @@ struct ocn_ctx {
     int overlap = 1;             // OCN_OPT_OVERLAP: 0 none, 1 standard steps, 2 + role-flip steps
     int32_t *d_nbad = nullptr;
     ncclComm_t comm = nullptr;
+    Loopback *lb = nullptr;            // test transport between contexts of one process (ocn_ctx_attach_loopback)
+    hipEvent_t lb_ev_a = nullptr, lb_ev_b = nullptr;
     std::map<std::vector<int>, HaloPlan> plans;
     bool initialized = false;
     bool use_graph = false;
-    struct Graph { hipGraphExec_t exec; double tau; ocn::StepKind kind; bool compact; int role; };
-    std::vector<Graph> graphs;         // one captured step per (tau, check, last step, compact)
+    // the launches a captured step replays depend on everything in its key (march and ring_sea
+    // select launch forms and the ring launch; options that change them also drop the cache)
+    struct Graph { hipGraphExec_t exec; double tau; ocn::StepKind kind; bool compact, march, ring_sea; int role; };
+    std::vector<Graph> graphs;         // one captured step per key
     std::vector<void *> allocs;
     // per-stage HIP-event timing (OCN_OPT_STAGE_TIMING): pending (stage, start, stop) records
     bool stage_timing = false;
@@ -555,6 +590,120 @@ static int nccl_rc(ncclResult_t r, const char *what)
     return set_error(OCN_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
+static bool has_comm(const ocn_ctx *c) { return c->comm || c->lb; }
+
+// a rank of a loopback group that fails releases its peers' waits at once
+static int lb_fail_on_error(ocn_ctx *c, int rc)
+{
+    if (rc && c->lb) {
+        std::lock_guard<std::mutex> g(c->lb->mu);
+        c->lb->failed = true;
+        c->lb->cv.notify_all();
+    }
+    return rc;
+}
+
+// One loopback rendezvous: this rank passes phase `ph`, then waits until every rank in `peers`
+// has passed it as often (bounded wait: a rank that failed or never comes ends it with an error).
+static int lb_meet(ocn_ctx *c, int ph, const std::vector<int> &peers)
+{
+    Loopback &L = *c->lb;
+    const int r = c->dec.rank;
+    std::unique_lock<std::mutex> g(L.mu);
+    const uint64_t mine = ++L.cnt[ph][r];
+    L.cv.notify_all();
+    bool lost = false;   // a peer still needed failed or was destroyed
+    const bool ok = L.cv.wait_for(g, std::chrono::seconds(120), [&] {
+        bool all = true;
+        for (int p : peers)
+            if (L.cnt[ph][p] < mine) {
+                all = false;
+                lost = lost || L.failed || !L.ctx[p];
+            }
+        return all || lost;
+    });
+    if (!ok || lost) {
+        L.failed = true;
+        L.cv.notify_all();
+        return set_error(OCN_ERR_COMM, "loopback transport: a peer rank did not reach the exchange");
+    }
+    return OCN_OK;
+}
+
+// The ncclRecv / ncclSend pairs of one exchange over the loopback transport (see Loopback).
+static int lb_exchange(ocn_ctx *c, const HaloPlan *p, hipStream_t stream)
+{
+    Loopback &L = *c->lb;
+    const int r = c->dec.rank;
+    std::vector<int> peers;
+    for (const auto &q : p->peers) peers.push_back(q.rank);
+    HIPCHK(hipEventRecord(c->lb_ev_a, stream));
+    {
+        std::lock_guard<std::mutex> g(L.mu);
+        L.plan[r] = p;
+    }
+    RC(lb_meet(c, 0, peers));
+    for (const auto &q : p->peers) {
+        const ocn_ctx *pc = L.ctx[q.rank];
+        const HaloPlan *pp;
+        {
+            std::lock_guard<std::mutex> g(L.mu);
+            pp = L.plan[q.rank];
+        }
+        const HaloPlan::Peer *src = nullptr;
+        for (const auto &e : pp->peers)
+            if (e.rank == r) src = &e;
+        if (!src || src->count != q.count) return set_error(OCN_ERR_STATE, "loopback transport: message sizes disagree");
+        HIPCHK(hipStreamWaitEvent(stream, pc->lb_ev_a, 0));
+        HIPCHK(hipMemcpyAsync(q.recv, src->send, sizeof(double) * (size_t)q.count, hipMemcpyDeviceToDevice, stream));
+    }
+    HIPCHK(hipEventRecord(c->lb_ev_b, stream));
+    RC(lb_meet(c, 1, peers));
+    for (const auto &q : p->peers) HIPCHK(hipStreamWaitEvent(stream, L.ctx[q.rank]->lb_ev_b, 0));
+    return OCN_OK;
+}
+
+// max over the ranks of one device int32 (the role-flip vote): ncclAllReduce, or over the
+// loopback transport every rank reads every rank's word (after its lb_ev_a) into d_red and copies
+// it back after all ranks have read (lb_ev_b).
+struct VotePtrs { const int32_t *p[64]; int n; };
+__global__ void k_vote_max(VotePtrs v, int32_t *out)
+{
+    if (threadIdx.x != 0) return;
+    int32_t m = v.p[0][0];
+    for (int i = 1; i < v.n; ++i) m = max(m, v.p[i][0]);
+    *out = m;
+}
+static int allreduce_max(ocn_ctx *c, int32_t *word, hipStream_t s)
+{
+    if (c->comm) return nccl_rc(ncclAllReduce(word, word, 1, ncclInt32, ncclMax, c->comm, s), "ncclAllReduce");
+    if (!c->lb) return OCN_OK;
+    Loopback &L = *c->lb;
+    std::vector<int> all(L.n);
+    for (int i = 0; i < L.n; ++i) all[i] = i;
+    HIPCHK(hipEventRecord(c->lb_ev_a, s));
+    {
+        std::lock_guard<std::mutex> g(L.mu);
+        L.vote[c->dec.rank] = word;
+    }
+    RC(lb_meet(c, 2, all));
+    VotePtrs v{};
+    v.n = L.n;
+    for (int i = 0; i < L.n; ++i) {
+        std::lock_guard<std::mutex> g(L.mu);
+        v.p[i] = L.vote[i];
+        HIPCHK(hipStreamWaitEvent(s, L.ctx[i]->lb_ev_a, 0));
+    }
+    int32_t *red = c->d_nbad + 48;
+    hipLaunchKernelGGL(k_vote_max, dim3(1), dim3(64), 0, s, v, red);
+    RC(check_launch());
+    HIPCHK(hipEventRecord(c->lb_ev_b, s));
+    RC(lb_meet(c, 3, all));
+    for (int i = 0; i < L.n; ++i) HIPCHK(hipStreamWaitEvent(s, L.ctx[i]->lb_ev_b, 0));
+    HIPCHK(hipMemcpyAsync(word, red, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return OCN_OK;
+}
+
 // cmp != nullptr: compare the halos with what the exchange would deliver instead of writing them
 // (ORs 1 into *cmp where they differ); same messages, so every rank must take part.
 static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stream = nullptr, int32_t *cmp = nullptr)
@@ -563,15 +712,19 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
     RC(get_plan(c, fields, p));
     if (!stream) stream = c->stream;
     if (!p->peers.empty()) {
-        if (!c->comm) return set_error(OCN_ERR_COMM, "remote neighbours but no RCCL communicator attached");
+        if (!has_comm(c)) return set_error(OCN_ERR_COMM, "remote neighbours but no RCCL communicator attached");
         hipLaunchKernelGGL(k_segments, dim3(p->n_pack, p->ch_pack), dim3(kSegChunk), 0, stream, p->d_pack, p->n_pack);
         RC(check_launch());
-        RC(nccl_rc(ncclGroupStart(), "ncclGroupStart"));
-        for (auto &peer : p->peers) {
-            RC(nccl_rc(ncclRecv(peer.recv, (size_t)peer.count, ncclDouble, peer.rank, c->comm, stream), "ncclRecv"));
-            RC(nccl_rc(ncclSend(peer.send, (size_t)peer.count, ncclDouble, peer.rank, c->comm, stream), "ncclSend"));
+        if (c->lb) {
+            RC(lb_exchange(c, p, stream));
+        } else {
+            RC(nccl_rc(ncclGroupStart(), "ncclGroupStart"));
+            for (auto &peer : p->peers) {
+                RC(nccl_rc(ncclRecv(peer.recv, (size_t)peer.count, ncclDouble, peer.rank, c->comm, stream), "ncclRecv"));
+                RC(nccl_rc(ncclSend(peer.send, (size_t)peer.count, ncclDouble, peer.rank, c->comm, stream), "ncclSend"));
+            }
+            RC(nccl_rc(ncclGroupEnd(), "ncclGroupEnd"));
         }
-        RC(nccl_rc(ncclGroupEnd(), "ncclGroupEnd"));
     }
     if (cmp) {
         if (p->n_local)
@@ -886,13 +1039,12 @@ static int check_coherence(ocn_ctx *c, bool eligible = true)
         for (const LBlock &b : c->blocks) RC(launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream));
     const bool exch = has_exchange(c);
     if (exch) RC(run_sync(c, kHaloCheck, c->stream, c->d_flags));
-    if (c->comm)
-        RC(nccl_rc(ncclAllReduce(c->d_flags, c->d_flags, 1, ncclInt32, ncclMax, c->comm, c->stream), "ncclAllReduce"));
+    RC(allreduce_max(c, c->d_flags, c->stream));
     int32_t flags = 0;
     HIPCHK(hipMemcpyAsync(&flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->coherent = flags == 0;
-    c->coherent_known = !c->r8_escaped && !c->comm;
+    c->coherent_known = !c->r8_escaped && !has_comm(c);
     return OCN_OK;
 }
 
@@ -1398,6 +1550,19 @@ int ocn_ctx_destroy(ocn_ctx *c)
     for (auto &r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->lb) {
+        Loopback *L = c->lb;
+        bool last;
+        {
+            std::lock_guard<std::mutex> g(L->mu);
+            L->ctx[c->dec.rank] = nullptr;   // a rank still waiting for this one fails (lb_meet)
+            last = --L->refs == 0;
+            L->cv.notify_all();
+        }
+        if (last) delete L;
+    }
+    if (c->lb_ev_a) (void)hipEventDestroy(c->lb_ev_a);
+    if (c->lb_ev_b) (void)hipEventDestroy(c->lb_ev_b);
     for (void *p : c->allocs) (void)hipFree(p);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
@@ -1452,12 +1617,41 @@ int ocn_ctx_attach_comm(ocn_ctx *c, const void *unique_id, int32_t nbytes)
     return OCN_OK;
 }
 
+int ocn_ctx_attach_loopback(ocn_ctx *const *ctxs, int32_t n)
+{
+    if (!ctxs || n < 2 || n > 64) return set_error(OCN_ERR_ARG, "loopback: 2..64 contexts");
+    for (int i = 0; i < n; ++i) {
+        const ocn_ctx *c = ctxs[i];
+        if (!c || c->dec.nranks != n || c->dec.rank != i || c->dec.device != ctxs[0]->dec.device)
+            return set_error(OCN_ERR_ARG, "loopback: context i must be rank i of nranks = n, all on one device");
+        if (c->comm || c->lb || c->initialized)
+            return set_error(OCN_ERR_STATE, "loopback: attach before ocn_ctx_init_state, once, without RCCL");
+    }
+    Loopback *L = new Loopback();
+    L->n = n;
+    L->ctx.assign(ctxs, ctxs + n);
+    for (auto &v : L->cnt) v.assign((size_t)n, 0);
+    L->plan.assign((size_t)n, nullptr);
+    L->vote.assign((size_t)n, nullptr);
+    L->refs = n;
+    int rc = OCN_OK;
+    for (int i = 0; i < n && !rc; ++i) {
+        ocn_ctx *c = ctxs[i];
+        rc = check_hip(hipSetDevice(c->dec.device), "hipSetDevice");
+        if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->lb_ev_a, hipEventDisableTiming), "hipEventCreate");
+        if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->lb_ev_b, hipEventDisableTiming), "hipEventCreate");
+    }
+    if (rc) { delete L; return rc; }
+    for (int i = 0; i < n; ++i) ctxs[i]->lb = L;
+    return OCN_OK;
+}
+
 int ocn_ctx_init_state(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
     c->coherent_known = false;
-    return init_state(c);
+    return lb_fail_on_error(c, init_state(c));
 }
 
 int ocn_ctx_sync(ocn_ctx *c, int field_id)
@@ -1495,7 +1689,8 @@ static int run_step(ocn_ctx *c, double tau, const StepKind &k)
 static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
 {
     for (const auto &g : c->graphs)
-        if (g.tau == tau && g.kind == k && g.compact == c->compact && g.role == c->role) {
+        if (g.tau == tau && g.kind == k && g.compact == c->compact && g.march == c->march && g.ring_sea == c->ring_sea &&
+            g.role == c->role) {
             HIPCHK(hipGraphLaunch(g.exec, c->stream));
             if (k.rc) swap_sshp(c);
             if (k.flip) swap_roles(c);
@@ -1515,7 +1710,7 @@ static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     HIPCHK(e);
-    c->graphs.push_back(ocn_ctx::Graph{exec, tau, k, c->compact, role});
+    c->graphs.push_back(ocn_ctx::Graph{exec, tau, k, c->compact, c->march, c->ring_sea, role});
     HIPCHK(hipGraphLaunch(exec, c->stream));
     return OCN_OK;
 }
@@ -1530,16 +1725,15 @@ int ocn_ctx_tracer_stage(ocn_ctx *c, int stage_id, int tracer, double tau)
     return tracer_stage(c, stage_id, tracer, tau, false);
 }
 
-int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
+static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
 {
-    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
     if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
     if (c->fused) RC(prepare_static(c));
-    const bool graph_ok = c->use_graph && !c->comm && !c->stage_timing;   // RCCL / events stay outside graphs
+    const bool graph_ok = c->use_graph && !has_comm(c) && !c->stage_timing;   // RCCL / events stay outside graphs
     // with RCCL every rank takes part in the decision (check_coherence reduces the verdicts)
     const bool eligible = flip_eligible(c);
-    bool flip_call = nsteps >= 2 && (eligible || (c->comm && c->flip));
+    bool flip_call = nsteps >= 2 && (eligible || (has_comm(c) && c->flip));
     if (flip_call && !c->coherent_known) RC(check_coherence(c, eligible));
     flip_call = flip_call && eligible && c->coherent;
     c->flip_used = flip_call;
@@ -1579,6 +1773,12 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
         swap_sshp(c);
     }
     return rc;
+}
+
+int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return lb_fail_on_error(c, step_impl(c, tau, nsteps, check_every));
 }
 
 int ocn_ctx_synchronize(ocn_ctx *c)
@@ -1673,7 +1873,10 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         if (c->overlap != value) drop_graphs(c);
         c->overlap = value < 0 ? 0 : value > 2 ? 2 : (int)value;
         return OCN_OK;
-    case OCN_OPT_MARCH: c->march = value != 0; return OCN_OK;
+    case OCN_OPT_MARCH:
+        if (c->march != (value != 0)) drop_graphs(c);
+        c->march = value != 0;
+        return OCN_OK;
     case OCN_OPT_FLIP: c->flip = value != 0; return OCN_OK;
     case OCN_OPT_RECOMPUTE: c->recompute = value != 0; return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step

@@ -104,6 +104,14 @@ class OceanModel:
         buf = C.create_string_buffer(bytes(unique_id), len(unique_id))
         check(lib().ocn_ctx_attach_comm(self.ctx, buf, len(unique_id)), "ocn_ctx_attach_comm")
 
+    @staticmethod
+    def attach_loopback(models):
+        """Test transport (ocn_ctx_attach_loopback): models[i] = rank i of len(models) ranks, all
+        on one device, each to be driven from its own thread (run_ranks); only the RCCL calls
+        are replaced."""
+        arr = (C.c_void_p * len(models))(*[m.ctx.value for m in models])
+        check(lib().ocn_ctx_attach_loopback(arr, len(models)), "ocn_ctx_attach_loopback")
+
     def init(self):
         check(lib().ocn_ctx_init_state(self.ctx), "ocn_ctx_init_state")
         return self
@@ -241,6 +249,30 @@ class OceanModel:
     def interior_cells(self) -> int:
         """(nx-4)(ny-4) share of this process: the cell-updates/s unit of SURVEY.md 8(d)."""
         return sum(b.cells for b in self.blocks)
+
+
+def run_ranks(models, fn):
+    """Drive loopback-attached ranks: fn(model) on one host thread per model (the library calls
+    release the GIL), like one process per rank.  Returns the results in rank order; re-raises
+    the first rank's exception."""
+    import threading
+    out, err = [None] * len(models), [None] * len(models)
+
+    def body(i):
+        try:
+            out[i] = fn(models[i])
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            err[i] = e
+
+    th = [threading.Thread(target=body, args=(i,)) for i in range(len(models))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in err:
+        if e is not None:
+            raise e
+    return out
 
 
 def make_unique_id() -> bytes:

@@ -92,9 +92,25 @@ def ctl_file_write(fname: str, undef, nx, ny, nz, nt, xtype, x0, hx, ytype, y0, 
 
 
 # ---------------------------------------------------------------- data records
+def _rank_barrier(model, barrier):
+    """The ordering io.f90 gets from its collective mpi_file_open / write_all: with several
+    processes, rank 0's undef fill must precede every rank's block writes.  Defaults to
+    torch.distributed.barrier when a process group is up; refuses to run unordered."""
+    if barrier is not None or model.nranks <= 1:
+        return barrier
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.barrier
+    except ImportError:
+        pass
+    raise ValueError("write_data with nranks > 1 needs a barrier (no torch.distributed process group is initialised)")
+
+
 def write_data(model, path: str, fname: str, nrec: int, name: str, barrier=None):
     """io.f90:276-386 write_data2D_real4 of field `name` (real(8) fields are converted like
     bufwp4%copy_from_real8) into record nrec (1-based) of path/fname."""
+    barrier = _rank_barrier(model, barrier)
     nx, ny = model.basin.nx, model.basin.ny
     nxb, nxe, nyb, nye = 3, nx - 2, 3, ny - 2           # mmm, mm, nnn, nn (basinpar)
     gw = nxe - nxb + 1

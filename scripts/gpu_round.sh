@@ -6,7 +6,7 @@ OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 ok() { case $1 in 0|1|2|5) return 0 ;; *) echo "[$2] rc=$1 fault/abort/timeout -> stop"; exit $1 ;; esac; }
 if [ "${TESTS:-1}" = "1" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?; echo "[pytest] rc=$rc"; tail -4 "$OUT/pytest_gpu.log"; ok $rc pytest
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?; echo "[pytest] rc=$rc"; tail -4 "$OUT/pytest_gpu.log"; ok $rc pytest
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?; echo "[smoke] rc=$rc"; tail -1 "$OUT/smoke.log"; ok $rc smoke
 fi
 if [ "${BENCH:-1}" = "1" ]; then

@@ -9,6 +9,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 E2E_CASES = ["box40x32_b2x2_s5", "box70x54_b1x1_s20", "box70x54_b3x2_s20",
              "box48x40_flags000_s10", "box48x40_cart_s10", "bs_b1x1_s60", "bs_b4x2_s60"]
 TRACER_E2E_CASES = ["box40x32_tr2_s5", "box70x54_b3x2_tr_s20", "bs_b4x2_tr_s60"]
+# the shipped run length (ocean_run.par: 604 steps), Black Sea, 1 block / 4x2 blocks + 1 tracer
+LONG_CASES = ["bs_b1x1_s604", "bs_b4x2_tr_s604"]
+# step 0: init_grid_data + init_ocean_data only (the initial state)
+INIT_CASES = ["box70x54_b1x1_s0", "box48x40_cart_s0", "bs_b4x2_tr_s0"]
+# BASELINE.json configs at full size (SHA-256 digests of every field of every block only):
+# C2 1024^2 1 block, C3 2048^2 2x2 blocks, the bench workload 4096^2 1 block, C4 4096^2 4x2 blocks
+FULLSIZE_CASES = ["box1024_b1x1_s10", "box2048_b2x2_s4", "box4096_b1x1_s6", "box4096_b4x2_s4"]
 KERNEL_GEOMS = ["b66x50", "b1x1", "b130x7"]
 KERNEL_NAMES = ["sw_update_ssh", "sw_update_uv", "sw_next_step", "uv_trans_vort", "uv_trans",
                 "uv_diff2", "stress_components", "hh_init", "hh_update", "hh_shift"]

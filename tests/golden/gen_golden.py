@@ -263,12 +263,53 @@ CASES = {
     "box40x32_tr2_s5": (dict(BOX, nx=40, ny=32), dict(SW_DEFAULT, tr=1, trn=2), (2, 1), 5, True),
     "box70x54_b3x2_tr_s20": (dict(BOX, nx=70, ny=54), dict(SW_DEFAULT, tr=1, trn=1), (3, 2), 20, False),
     "bs_b4x2_tr_s60": (BS, dict(SW_DEFAULT, tr=1, trn=1), (4, 2), 60, False),
+    # the shipped run length (ocean_run.par: 0.007 days = 604 steps), SURVEY.md 8(c) tolerance
+    "bs_b1x1_s604": (BS, SW_DEFAULT, (1, 1), 604, False),
+    "bs_b4x2_tr_s604": (BS, dict(SW_DEFAULT, tr=1, trn=1), (4, 2), 604, False),
+    # step 0 (init_grid_data + init_ocean_data only): pins the device-side initial state
+    "box70x54_b1x1_s0": (dict(BOX, nx=70, ny=54), SW_DEFAULT, (1, 1), 0, True),
+    "box48x40_cart_s0": (dict(BOX, nx=48, ny=40, curve=0), dict(SW_DEFAULT, ts="0.25d0"), (1, 1), 0, True),
+    "bs_b4x2_tr_s0": (BS, dict(SW_DEFAULT, tr=1, trn=1), (4, 2), 0, False),
+    # BASELINE.json configs at full size: SHA-256 digests only ("sha"), streamed from the dump
+    "box1024_b1x1_s10": (dict(BOX, nx=1028, ny=1028), SW_DEFAULT, (1, 1), 10, "sha"),      # C2
+    "box2048_b2x2_s4": (dict(BOX, nx=2052, ny=2052), SW_DEFAULT, (2, 2), 4, "sha"),        # C3
+    "box4096_b1x1_s6": (dict(BOX, nx=4100, ny=4100), SW_DEFAULT, (1, 1), 6, "sha"),        # the bench workload
+    "box4096_b4x2_s4": (dict(BOX, nx=4100, ny=4100), SW_DEFAULT, (4, 2), 4, "sha"),        # C4
 }
 PROGNOSTIC = ["ssh", "sshp", "ubrtr", "ubrtrp", "vbrtr", "vbrtrp", "ff1_1", "ff1p_1"]
 
 
 def digest(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a.ravel(order="F")).tobytes()).hexdigest()
+
+
+def digest_dump(path):
+    """read_dump's layout, but every field only as its SHA-256 (memory-mapped, for the
+    multi-GB dumps of the full-size boxes): each field record is already the Fortran-ordered
+    array, so its bytes are what digest() hashes."""
+    from tests.golden.refdump import R4_FIELDS as r4, R8_FIELDS as r8
+    raw = np.memmap(path, dtype=np.uint8, mode="r")
+    pos = 0
+
+    def take(nbytes):
+        nonlocal pos
+        a = raw[pos:pos + nbytes]
+        pos += nbytes
+        return a
+
+    bcount, ntr = (int(v) for v in take(8).view("<i4"))
+    out = []
+    for _ in range(bcount):
+        bm, bn, nxs, nxe, nys, nye, bx1, bx2, by1, by2 = (int(v) for v in take(40).view("<i4"))
+        n = (bx2 - bx1 + 1) * (by2 - by1 + 1)
+        names = [(nm, 4) for nm in r4] + [(nm, 8) for nm in r8]
+        if ntr > 0:
+            names += [(nm, 8) for nm in ["flux_x", "flux_y"] +
+                      [f"{p}_{t}" for t in range(1, ntr + 1) for p in ("ff1", "ff1p", "ff1n")]]
+        f = {nm: hashlib.sha256(memoryview(take(n * es))).hexdigest() for nm, es in names}
+        out.append((dict(bm=bm, bn=bn, nxs=nxs, nxe=nxe, nys=nys, nye=nye, bx1=bx1, bx2=bx2, by1=by1, by2=by2), f))
+    assert pos == raw.size, (pos, raw.size)
+    return out
 
 
 def gen_e2e(name, basin, sw, bxy, steps, full):
@@ -280,7 +321,10 @@ def gen_e2e(name, basin, sw, bxy, steps, full):
         env = dict(os.environ, OMP_NUM_THREADS="1")
         subprocess.check_call([REFDRV, str(steps), "dump.bin"], cwd=d, env=env,
                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-        blocks = read_dump(os.path.join(d, "dump.bin"))
+        if full == "sha":
+            blocks = digest_dump(os.path.join(d, "dump.bin"))
+        else:
+            blocks = read_dump(os.path.join(d, "dump.bin"))
     finally:
         shutil.rmtree(d)
     out = {"meta/basin": np.array(repr({k: v for k, v in basin.items() if k != "mask"} |
@@ -295,8 +339,8 @@ def gen_e2e(name, basin, sw, bxy, steps, full):
         out[f"b{key}/info"] = np.array([info[k] for k in ("nxs", "nxe", "nys", "nye", "bx1", "bx2", "by1", "by2")],
                                        np.int32)
         for nm, a in f.items():
-            out[f"b{key}/sha/{nm}"] = np.array(digest(a))
-            if full or nm in PROGNOSTIC:
+            out[f"b{key}/sha/{nm}"] = np.array(a if isinstance(a, str) else digest(a))
+            if full is True or (full is False and nm in PROGNOSTIC):
                 out[f"b{key}/{nm}"] = a
     path = os.path.join(HERE, f"e2e_{name}.npz")
     np.savez_compressed(path, **out)

@@ -1,0 +1,220 @@
+"""GPU parity of the multi-rank path (one block per rank, halos between ranks) and of the
+BASELINE.json configurations at full size, against the reference.
+
+The ranks run as contexts of this one process on the one GPU, joined by the library's loopback
+transport (ocn_ctx_attach_loopback), each driven by its own host thread.  The loopback replaces
+only the two RCCL calls (ncclRecv/ncclSend of an exchange, the ncclAllReduce of the role-flip
+vote); the device pack / unpack of every message, the per-peer plans per buffer role, the
+merged hh_init + A exchange and the overlap forks are the production code that an 8-GPU run
+over RCCL executes.  Reference behaviour replaced: core/kernel_interface.f90:174-184
+(_GPU_MULTI_: block k on device k-1) and shared/mpp/syncborder_block2D_gen_all.fi:100-129.
+
+Tolerance: none (bitwise SHA-256 of every field of every block vs the unmodified reference run).
+"""
+import numpy as np
+import pytest
+
+from tests.golden import cases
+from tests.test_gpu_parity import bits_equal, build_model, compare_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def amd():
+    import ocean_model_arch_amd as amd
+    amd.lib()
+    return amd
+
+
+def run_ranks_case(amd, case, nranks, steps=None, calls=None, **opts):
+    """The fixture's block grid over `nranks` loopback ranks; returns the models (caller closes)."""
+    models = [build_model(amd, case, rank=r, nranks=nranks, **opts) for r in range(nranks)]
+    amd.OceanModel.attach_loopback(models)
+    calls = calls or [steps if steps is not None else case["steps"]]
+
+    def body(m):
+        m.init()
+        for n in calls:
+            m.step(n, tau=1.0, check_every=1)
+        m.synchronize()
+        return m.flip_active
+
+    flips = amd.run_ranks(models, body)
+    return models, flips
+
+
+def check_ranks(models, case, name):
+    bad, nblocks = [], 0
+    for m in models:
+        bad += compare_case(m, case, name, whole=False)
+        nblocks += len(m.blocks)
+    assert nblocks == len(cases.e2e_blocks(case["z"])), name
+    return bad
+
+
+MODES = {   # name -> build_model options
+    "default": {},                            # role-flip steps; exchanges overlapped per OCN_OPT_OVERLAP default
+    "overlap0": dict(overlap=0),
+    "overlap1": dict(overlap=1),
+    "overlap2": dict(overlap=2),
+    "noflip": dict(flip=False),
+    "noflip_overlap0": dict(flip=False, overlap=0),
+    "norecompute": dict(recompute=False),
+    "stages": dict(fused=False),
+}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("name,nranks", [("box70x54_b3x2_s20", 6), ("bs_b4x2_s60", 8), ("bs_b4x2_tr_s60", 8),
+                                         ("box40x32_b2x2_s5", 4)])
+def test_ranks_match_reference(amd, name, nranks, mode):
+    case = cases.load_e2e(name)
+    models, flips = run_ranks_case(amd, case, nranks, **MODES[mode])
+    try:
+        bad = check_ranks(models, case, name)
+    finally:
+        for m in models:
+            m.close()
+    assert not bad, f"{name} over {nranks} ranks ({mode}): fields differ from the reference: {bad}"
+    assert len(set(flips)) == 1, "ranks ran different kinds of steps"
+    if mode in ("default", "overlap0", "overlap1", "overlap2", "norecompute") and \
+            case["sw"].get("use_tracers", 0) <= 0:
+        assert flips[0], f"{name}: role-flip steps not used over ranks"
+
+
+def test_ranks_split_calls_match_reference(amd):
+    """Several ocn_ctx_step calls per rank (each call votes again over the ranks)."""
+    case = cases.load_e2e("box70x54_b3x2_s20")
+    models, _ = run_ranks_case(amd, case, 6, calls=[7, 1, 12])
+    try:
+        bad = check_ranks(models, case, "split")
+    finally:
+        for m in models:
+            m.close()
+    assert not bad, bad
+
+
+def test_ranks_604_steps_tracer_match_reference(amd):
+    """Config 5 at the shipped run length: Black Sea + 1 tracer, 4x2 blocks, one per rank."""
+    case = cases.load_e2e("bs_b4x2_tr_s604")
+    models, _ = run_ranks_case(amd, case, 8)
+    try:
+        bad = check_ranks(models, case, "bs_b4x2_tr_s604")
+    finally:
+        for m in models:
+            m.close()
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("kind", ["sea", "land"])
+def test_ranks_flip_falls_back_when_halo_disagrees(amd, kind):
+    """test_gpu_parity.test_flip_falls_back_when_halo_disagrees with the island on a RANK
+    boundary: rank 0's check finds the disagreement, the vote (the loopback's ncclAllReduce)
+    makes both ranks run standard steps, bit for bit as with OCN_OPT_FLIP off."""
+    n, steps = 96, 6
+    par = amd.ParallelConfig(2, 1)
+    probe = amd.OceanModel(amd.box_config(n), par=par)
+    xe = [x for x in probe.blocks if x.bm == 1][0].nx_end
+    probe.close()
+    mask = np.zeros((n + 4, n + 4), dtype=np.int32)
+    mask[:2, :] = mask[-2:, :] = mask[:, :2] = mask[:, -2:] = 1
+    mask[xe, n // 2 - 3:n // 2 + 3] = 1
+    out, used = {}, {}
+    for flip in (True, False):
+        for mod in (True, False):
+            models = [amd.OceanModel(amd.box_config(n, mask=mask), par=par, rank=r, nranks=2).set_flip(flip)
+                      for r in range(2)]
+            amd.OceanModel.attach_loopback(models)
+            amd.run_ranks(models, lambda m: m.init())
+            m0 = models[0]
+            b = m0.blocks[0]
+            assert b.bm == 1
+            if mod:
+                i = b.nx_end + 1 - b.bnd_x1
+                lu = m0.download(b.k, "lu")[i, b.ny_start - b.bnd_y1:b.ny_end - b.bnd_y1 + 1]
+                rows = np.flatnonzero(lu == (1.0 if kind == "sea" else 0.0))
+                assert rows.size, kind
+                j = b.ny_start - b.bnd_y1 + int(rows[rows.size // 2])
+                for nm in ("ssh", "sshn"):
+                    a = m0.download(b.k, nm)
+                    a[i, j] += 0.125
+                    m0.upload(b.k, nm, a)
+            flips = amd.run_ranks(models, lambda m: m.step(steps).synchronize().flip_active)
+            assert len(set(flips)) == 1
+            used[(flip, mod)] = flips[0]
+            out[(flip, mod)] = [{nm: m.download(x.k, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn",
+                                                                     "vbrtr", "vbrtrn", "hhu", "hhv", "hhh")}
+                                for m in models for x in m.blocks]
+            for m in models:
+                m.close()
+    for mod in (True, False):
+        bad = [(k, nm) for k, d in enumerate(out[(True, mod)]) for nm, a in d.items()
+               if not bits_equal(a, out[(False, mod)][k][nm])]
+        assert not bad, f"modified={mod}: flip vs standard steps differ in {bad}"
+    assert used[(True, False)] and not used[(True, True)]
+
+
+# ---------------------------------------------------------------- BASELINE.json configs, full size
+def _full(amd, name, **opts):
+    case = cases.load_e2e(name)
+    m = build_model(amd, case, **opts)
+    return case, m
+
+
+@pytest.mark.parametrize("variant", ["bench", "graph", "noflip"])
+def test_bench_workload_matches_reference(amd, variant):
+    """The bench's exact workload and options (bench.py: 4096^2 box, 1 block, stage-timing events
+    on, one call whose steps are first / recompute / CA / last) vs the reference's 6-step run."""
+    case, m = _full(amd, "box4096_b1x1_s6", graph=variant == "graph", flip=variant != "noflip")
+    try:
+        m.init()
+        if variant == "bench":
+            m.set_stage_timing(True)
+        m.step(case["steps"], tau=1.0, check_every=1).synchronize()
+        if variant == "bench":
+            assert m.flip_active and m.recompute_active
+        bad = compare_case(m, case, "box4096")
+    finally:
+        m.close()
+    assert not bad, f"4096^2 ({variant}): fields differ from the reference: {bad}"
+
+
+@pytest.mark.parametrize("name", ["box1024_b1x1_s10", "box2048_b2x2_s4", "box4096_b4x2_s4"])
+def test_fullsize_blocks_match_reference(amd, name):
+    """C2 (1024^2), C3 (2048^2 as 2x2 blocks) and C4 (4096^2 as 4x2 blocks) in one process:
+    every block on the GPU, local halo copies."""
+    case, m = _full(amd, name)
+    try:
+        m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
+        bad = compare_case(m, case, name)
+    finally:
+        m.close()
+    assert not bad, f"{name}: fields differ from the reference: {bad}"
+
+
+@pytest.mark.parametrize("name,nranks", [("box2048_b2x2_s4", 4), ("box4096_b4x2_s4", 8)])
+def test_fullsize_ranks_match_reference(amd, name, nranks):
+    """C3 and C4 as BASELINE.json runs them: one block per rank, halos between ranks."""
+    case = cases.load_e2e(name)
+    models, flips = run_ranks_case(amd, case, nranks)
+    try:
+        bad = check_ranks(models, case, name)
+    finally:
+        for m in models:
+            m.close()
+    assert not bad, f"{name} over {nranks} ranks: fields differ from the reference: {bad}"
+    assert all(flips)
+
+
+@pytest.mark.parametrize("name", cases.INIT_CASES)
+def test_initial_state_matches_reference(amd, name):
+    """ocn_ctx_init_state (init_grid_data + init_ocean_data) vs the reference's step-0 state."""
+    case = cases.load_e2e(name)
+    m = build_model(amd, case)
+    try:
+        m.init().synchronize()
+        bad = compare_case(m, case, name)
+    finally:
+        m.close()
+    assert not bad, f"{name}: initial fields differ from the reference: {bad}"

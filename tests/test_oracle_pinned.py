@@ -92,7 +92,8 @@ def build_oracle_model(case):
     return O.OracleModel(basin, sw, *case["bxy"])
 
 
-@pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES)
+@pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES + cases.INIT_CASES
+                         + cases.FULLSIZE_CASES)
 def test_oracle_end_to_end_matches_reference(name):
     case = cases.load_e2e(name)
     z = case["z"]
@@ -109,6 +110,7 @@ def test_oracle_end_to_end_matches_reference(name):
                 continue
             assert _sha(a) == str(z[key]), f"{name}: block ({blk.bm},{blk.bn}) field {nm} differs"
             checked.add(nm)
+    assert len(checked) >= 49, f"{name}: only {len(checked)} fields checked"
     if case["sw"].get("use_tracers", 0) > 0:
         assert {"flux_x", "flux_y", "ff1_1", "ff1p_1", "ff1n_1"} <= checked
 
