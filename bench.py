@@ -43,14 +43,27 @@ LAUNCH_BYTES = {
     "c1": (121, 132), "c1_ring": (0, 0),                   # role-flip steps: a8 + a9 on the halo ring only
     "c2": (81, 128), "c2_full": (121, 168),
     "ca": (113, 113), "ca_store": (137, 137), "ca_hh": (169, 169),   # hh_init + next step's A (no hhh_p;
-}   # "ca": next step recomputes -- no interior hhq, hhu_p, hhv_p; "ca_hh": + a2's stores and hhh_p)
+    # "ca": next step recomputes -- no interior hhq, hhu_p, hhv_p; "ca_hh": + a2's stores and hhh_p)
+    # one-pass step: ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp, h_r, mu, RHSx, RHSy + mask byte in;
+    # sshn, ubrtrn, vbrtrn and the filtered sshp, ubrtrp, vbrtrp out
+    "onepass": (129, 129),
+    "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
+}
 
 
-def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False):
+def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, one: bool = False):
     """The launches of one ocn_ctx_step call of `steps` steps, as (timer, launch kind) pairs --
     ocn_ctx.hip ocn_ctx_step / one_step_fused for one block (role-flip calls fuse each step's
     hh_init with the next step's A when full_free_surface = 1, as in sw.par; ring = the ring
-    launch runs, i.e. a8 / a9 have work on the halo ring: blocks with neighbours)."""
+    launch runs, i.e. a8 / a9 have work on the halo ring: blocks with neighbours; one = one-pass
+    steps 2..K-1)."""
+    if one and flip and steps >= 3:
+        out = [("fused_a", "a"), ("fused_b", "b_flip")]
+        out += [("onepass", "onepass")] * (steps - 2) + [("fused_ca", "ca_hh")]
+        out += [("fused_b", "b_full"), ("fused_c1", "c1"), ("hh_init", "c2_full")]
+        if (steps - 2) % 2:
+            out.append(("copy", "copy3"))
+        return out
     out = []
     for s in range(1, steps + 1):
         first, last = s == 1, s == steps
@@ -69,20 +82,22 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False):
     return out
 
 
-def fused_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False):
+def fused_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False,
+                one: bool = False):
     """Mean bytes per interior cell per launch of each timer over one ocn_ctx_step call."""
     i = 0 if compact else 1
     tot, cnt = {}, {}
-    for timer, kind in call_launches(steps, flip, rc, ring):
+    for timer, kind in call_launches(steps, flip, rc, ring, one):
         tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
         cnt[timer] = cnt.get(timer, 0) + 1
     return {t: tot[t] / cnt[t] for t in tot}
 
 
-def step_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False):
+def step_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False,
+               one: bool = False):
     """Bytes per interior cell per step moved by one ocn_ctx_step call of `steps` steps."""
     i = 0 if compact else 1
-    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc, ring)) / steps
+    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc, ring, one)) / steps
 
 
 def dims_create(n: int):
@@ -178,6 +193,7 @@ def main():
     ap.add_argument("--no-march", action="store_true", help="one thread per point in every launch (no register march)")
     ap.add_argument("--no-flip", action="store_true", help="standard steps only (no role-flip steps)")
     ap.add_argument("--no-recompute", action="store_true", help="role-flip calls without the recompute steps")
+    ap.add_argument("--no-onepass", action="store_true", help="role-flip calls without the one-pass steps")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
                     help="halo exchanges beside inner launches: 0 never, 1 standard steps, 2 role-flip steps too")
     ap.add_argument("--blocks", default=None,
@@ -225,6 +241,7 @@ def main():
     model.set_march(not args.no_march)
     model.set_flip(not args.no_flip)
     model.set_recompute(not args.no_recompute)
+    model.set_onepass(not args.no_onepass)
     model.set_overlap(args.overlap)
     if args.graph:
         model.set_graph(True)
@@ -248,6 +265,7 @@ def main():
     compact = model.compact_active
     flip = model.flip_active
     rc = model.recompute_active
+    one = model.onepass_active
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -259,8 +277,8 @@ def main():
     out = None
     if rank == 0:
         ring = bx * by > 1
-        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc, ring)
-        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring)
+        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc, ring, one)
+        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring, one)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:
@@ -283,7 +301,7 @@ def main():
                           "step": "reference stages" if args.stages else "fused groups",
                           "static_fields": "compact" if compact else "2-D arrays",
                           "march": bool(compact and not args.stages and not args.no_march),
-                          "role_flip_steps": flip, "recompute_steps": rc,
+                          "role_flip_steps": flip, "recompute_steps": rc, "onepass_steps": one,
                           "parallelism": (f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else
                                           "1 block" if bx * by == 1 else f"{bx}x{by} blocks, local halo copies")},
                "roofline": roof,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define OCN_ABI_VERSION 2
+#define OCN_ABI_VERSION 3
 
 enum {
     OCN_OK = 0,
@@ -318,18 +318,23 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_RECOMPUTE (default 1): in such calls (full_free_surface = 1, no a8 / a9 work on the
  *  halo ring, so one block without halo exchanges), steps 2..K-1 form hhq, hhu_p, hhv_p inside
  *  fused B instead of storing and re-reading them (same results bit for bit).
+ *  OCN_OPT_ONEPASS (default 1): in such calls of K >= 3 steps on ONE block without a8 / a9 work on
+ *  the halo ring and with trans_terms and ksw_lat on, steps 2..K-1 run as one launch each: the
+ *  state is read once and the next state written once, hh_init's depths, vort and the stresses
+ *  formed in registers (same results bit for bit; takes precedence over OCN_OPT_RECOMPUTE).
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
- * whether it used recompute steps. */
+ * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps. */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
-       OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8 };
+       OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
- * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A. */
+ * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,
+ * then the one-pass steps. */
 enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_TIMER_TRACER,
-       OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_NUM_TIMERS };
+       OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_TIMER_ONEPASS, OCN_NUM_TIMERS };
 
 /* Per-timer device time (ms, summed) and launch counts since the last call, from the HIP
  * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_TIMERS entries.  Synchronises. */

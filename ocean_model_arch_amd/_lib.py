@@ -66,7 +66,7 @@ STAGES = ["sw_update_ssh", "hh_update", "uv_trans_vort", "uv_trans", "stress_com
 STAGE_ID = {n: i for i, n in enumerate(STAGES)}
 TSTAGES = ["tran_diff_fluxes", "tran_diff_tracer", "tracer_next_step"]
 TSTAGE_ID = {n: i for i, n in enumerate(TSTAGES)}
-TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES + ["fused_ca"]    # OCN_NUM_TIMERS slots
+TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES + ["fused_ca", "onepass"]    # OCN_NUM_TIMERS slots
 OPT_GRAPH = 1
 OPT_OVERLAP = 2
 OPT_STAGE_TIMING = 3
@@ -75,6 +75,7 @@ OPT_COMPACT = 5
 OPT_MARCH = 6
 OPT_FLIP = 7
 OPT_RECOMPUTE = 8
+OPT_ONEPASS = 9
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",

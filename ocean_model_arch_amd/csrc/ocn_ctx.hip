@@ -176,6 +176,7 @@ struct LBlock {
     uint8_t *bits = nullptr;           // compact static fields (sw_stencils.h): mask bytes
     float *rows = nullptr;             // and metric row tables
     void *sshp_alt = nullptr;          // second sshp buffer of the recompute steps (one_step_fused)
+    void *up_alt = nullptr, *vp_alt = nullptr;   // second ubrtrp / vbrtrp buffers of the one-pass steps
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
@@ -225,12 +226,15 @@ namespace ocn {
 // next_reuse = the next step is a reuse step; rc = recompute steps (fused B forms hhq, hhu_p,
 // hhv_p itself and writes sshp's filter into the second sshp buffer), rc_next = the next step is
 // one (this step's hh_init + A launch then does not store hhq on the interior, hhu_p, hhv_p).
+// one = one-pass step (sw_kernels.hip MarchStep), next_one = the next step is one (this step
+// then runs no hh_init: the one-pass step forms hh_init's values itself).
 struct StepKind {
-    bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next;
+    bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next, one, next_one;
     bool operator==(const StepKind &o) const
     {
         return check == o.check && first == o.first && last == o.last && flip == o.flip && a_done == o.a_done &&
-               next_a == o.next_a && next_reuse == o.next_reuse && rc == o.rc && rc_next == o.rc_next;
+               next_a == o.next_a && next_reuse == o.next_reuse && rc == o.rc && rc_next == o.rc_next &&
+               one == o.one && next_one == o.next_one;
     }
 };
 
@@ -284,6 +288,11 @@ struct ocn_ctx {
     bool sync_pending = false;   // an exchange on comm_stream not yet joined (fork_sync)
     bool ring_sea = true;   // some halo-ring point has a mask set (Prepare); else no ring launch
     bool recompute = true;  // OCN_OPT_RECOMPUTE: recompute steps in role-flip calls
+    bool onepass = true;    // OCN_OPT_ONEPASS: one-pass steps in single-block role-flip calls
+    bool one_used = false;
+    // the one-pass steps' second sshp / ubrtrp / vbrtrp buffers agree with the fields outside a8's
+    // write set (else they are copied at the start of the next such call)
+    mutable bool alt_ok = false;
     mutable bool coherent_known = false, r8_escaped = false;
     int role = 0;
     int32_t *d_flags = nullptr;
@@ -434,10 +443,12 @@ static int allocate(ocn_ctx *c)
         c->allocs.push_back(b.bits);
         HIPCHK(hipMalloc(&b.rows, nrow * sizeof(float)));
         c->allocs.push_back(b.rows);
-        void *alt = nullptr;   // laid out as the slab's r8 fields (rows 256-B aligned at nx_start)
-        HIPCHK(hipMalloc(&alt, n * 8 + 512));
-        c->allocs.push_back(alt);
-        b.sshp_alt = (char *)alt + 256 - 16;
+        for (void **dst : {&b.sshp_alt, &b.up_alt, &b.vp_alt}) {
+            void *alt = nullptr;   // laid out as the slab's r8 fields (rows 256-B aligned at nx_start)
+            HIPCHK(hipMalloc(&alt, n * 8 + 512));
+            c->allocs.push_back(alt);
+            *dst = (char *)alt + 256 - 16;
+        }
     }
     HIPCHK(hipMalloc(&c->d_nbad, 256));
     c->allocs.push_back(c->d_nbad);
@@ -1015,7 +1026,18 @@ static void swap_sshp(ocn_ctx *c)
     for (LBlock &b : c->blocks) std::swap(b.ptr[field_slot(OCN_SSHP)], b.sshp_alt);
     c->role ^= 2;
 }
+// one-pass steps: sshp, ubrtrp, vbrtrp and their second buffers trade places (role bit 4)
+static void swap_alt3(ocn_ctx *c)
+{
+    for (LBlock &b : c->blocks) {
+        std::swap(b.ptr[field_slot(OCN_SSHP)], b.sshp_alt);
+        std::swap(b.ptr[field_slot(OCN_UBRTRP)], b.up_alt);
+        std::swap(b.ptr[field_slot(OCN_VBRTRP)], b.vp_alt);
+    }
+    c->role ^= 4;
+}
 static size_t field_bytes(const LBlock &b) { return (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1) * 8; }
+static bool is_alt_field(int id) { return id == OCN_SSHP || id == OCN_UBRTRP || id == OCN_VBRTRP; }
 static bool is_flip_field(int id)
 {
     for (const auto &pr : kFlipPairs)
@@ -1087,6 +1109,23 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
     const std::vector<int> &sync_a = reuse ? c->sync_a_reuse : c->sync_a;
     if (flip) {
         if (last) return set_error(OCN_ERR_STATE, "role-flip step on a last step");
+        if (k.one) {   // the whole step in one launch (single block: no exchange, no ring launch)
+            RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+            for (const LBlock &b : c->blocks)
+                RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad,
+                                  (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s));
+            RC(timer_end(c, rec));
+            swap_alt3(c);
+            swap_roles(c);
+            if (k.next_a) {   // the next step is the last, standard one: hh_init + its fused A
+                RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
+                for (const LBlock &b : c->blocks)
+                    RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_ALL, sw, tau,
+                                       k.next_reuse, false, s));
+                RC(timer_end(c, rec));
+            }
+            return OCN_OK;
+        }
         // With halo exchanges and OCN_OPT_OVERLAP = 2 (not while capturing a graph: the last
         // exchange stays pending into the next step), each exchange runs on the comm stream beside
         // the inner part (launch_march_part) of the next launch:
@@ -1135,7 +1174,7 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
             return OCN_OK;
         };
         const int hh_timer = k.next_a ? OCN_TIMER_FUSED_CA : OCN_STAGE_HH_INIT;
-        const bool hh = k.next_a || ffs;
+        const bool hh = !k.next_one && (k.next_a || ffs);   // a one-pass step forms hh_init's values itself
         if (ov && hh) {
             RC(timer_begin(c, hh_timer, rec));
             RC(hh_init(OCN_PART_INNER));
@@ -1593,6 +1632,7 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
     }
     if (is_r4(id)) c->r4_escaped = true;   // may be written behind our back: no compact tables
     if (is_flip_field(id)) { c->r8_escaped = true; c->coherent_known = false; }
+    if (is_alt_field(id)) c->alt_ok = false;
     return c->blocks[k].ptr[field_slot(id)];
 }
 
@@ -1651,6 +1691,7 @@ int ocn_ctx_init_state(ocn_ctx *c)
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
     c->coherent_known = false;
+    c->alt_ok = false;
     return lb_fail_on_error(c, init_state(c));
 }
 
@@ -1668,6 +1709,7 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     HIPCHK(hipSetDevice(c->dec.device));
     if (stage_id < 0 || stage_id >= OCN_NUM_STAGES) return set_error(OCN_ERR_ARG, "bad stage id");
     c->coherent_known = false;
+    c->alt_ok = false;
     return envoke(c, stage_id, tau);
 }
 
@@ -1693,6 +1735,7 @@ static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
             g.role == c->role) {
             HIPCHK(hipGraphLaunch(g.exec, c->stream));
             if (k.rc) swap_sshp(c);
+            if (k.one) swap_alt3(c);
             if (k.flip) swap_roles(c);
             return OCN_OK;
         }
@@ -1741,7 +1784,23 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     // their reuse steps recompute hhq / hhu_p / hhv_p in fused B, which then filters sshp into
     // the second buffer (the ring launch completes it on the halo ring)
     const bool ca = flip_call && c->sw.full_free_surface == 1;
-    const bool rc_call = ca && c->recompute;
+    // one-pass steps 2..K-1 (single block, no a8 / a9 work on the halo ring, all SW terms on)
+    const bool one_call = ca && c->onepass && nsteps >= 3 && c->blocks.size() == 1 && !has_exchange(c) &&
+                          !has_comm(c) && !c->ring_sea && c->sw.trans_terms > 0 && c->sw.ksw_lat > 0;
+    c->one_used = one_call;
+    const bool rc_call = ca && c->recompute && !one_call;
+    if (rc_call) c->alt_ok = false;
+    if (one_call && !c->alt_ok) {   // the second buffers start as copies (they agree outside a8's write set)
+        for (const LBlock &b : c->blocks) {
+            HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
+                                  c->stream));
+            HIPCHK(hipMemcpyAsync(b.up_alt, b.ptr[field_slot(OCN_UBRTRP)], field_bytes(b), hipMemcpyDeviceToDevice,
+                                  c->stream));
+            HIPCHK(hipMemcpyAsync(b.vp_alt, b.ptr[field_slot(OCN_VBRTRP)], field_bytes(b), hipMemcpyDeviceToDevice,
+                                  c->stream));
+        }
+        c->alt_ok = true;
+    }
     c->rc_used = rc_call && nsteps >= 3;
     if (rc_call)   // the second sshp buffer starts as a copy: the two agree outside a8's write set
         for (const LBlock &b : c->blocks)
@@ -1755,8 +1814,10 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         k.first = s == 1;
         k.last = s == nsteps;
         k.flip = flip_call && !k.last;
+        k.one = one_call && s >= 2 && s <= nsteps - 1;
+        k.next_one = one_call && s + 1 >= 2 && s + 1 <= nsteps - 1;
         k.a_done = ca && !k.first;
-        k.next_a = ca && k.flip;
+        k.next_a = ca && k.flip && !k.next_one;
         k.next_reuse = k.next_a && s + 1 < nsteps;
         k.rc = rc_call && k.flip && !k.first;
         k.rc_next = rc_call && s + 1 < nsteps;
@@ -1771,6 +1832,14 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
             HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
                                   c->stream));
         swap_sshp(c);
+    }
+    if (c->role & 4) {   // one-pass steps: the current sshp / ubrtrp / vbrtrp back into the fields' buffers
+        for (LBlock &b : c->blocks)
+            for (const auto &pr : {std::make_pair(&b.sshp_alt, OCN_SSHP), std::make_pair(&b.up_alt, OCN_UBRTRP),
+                                   std::make_pair(&b.vp_alt, OCN_VBRTRP)})
+                HIPCHK(hipMemcpyAsync(*pr.first, b.ptr[field_slot(pr.second)], field_bytes(b), hipMemcpyDeviceToDevice,
+                                      c->stream));
+        swap_alt3(c);
     }
     return rc;
 }
@@ -1856,6 +1925,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     HIPCHK(hipStreamSynchronize(c->stream));
     if (is_r4(id)) c->static_dirty = true;
     if (is_flip_field(id)) c->coherent_known = false;
+    if (is_alt_field(id)) c->alt_ok = false;
     return upload_field(c, c->blocks[k], id, host, false);
 }
 
@@ -1879,6 +1949,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         return OCN_OK;
     case OCN_OPT_FLIP: c->flip = value != 0; return OCN_OK;
     case OCN_OPT_RECOMPUTE: c->recompute = value != 0; return OCN_OK;
+    case OCN_OPT_ONEPASS: c->onepass = value != 0; return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -1900,6 +1971,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
     case OCN_OPT_RECOMPUTE: *value = c->recompute && c->rc_used; return OCN_OK;
+    case OCN_OPT_ONEPASS: *value = c->onepass && c->one_used; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

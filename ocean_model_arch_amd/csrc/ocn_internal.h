@@ -74,6 +74,11 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compac
 // skip_rc = step k+1 is a recompute step (hhq on the interior, hhu_p, hhv_p not stored).
 int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s);
+// One-pass role-flip step (sw_kernels.hip MarchStep): a1 + fused B + a8's filters + check_ssh_err
+// with hh_init's depths, vort and the stresses formed in registers from the state; single block,
+// no a8 / a9 work on the halo ring; a8's filtered sshp / ubrtrp / vbrtrp go to the given buffers.
+int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                   double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s);
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);

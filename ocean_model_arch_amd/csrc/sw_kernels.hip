@@ -121,7 +121,6 @@ static int launch_part(const Range &r, const Range &inner, int part, const Body 
 //     edge loads, fewer registers; fused B, which stores two arrays).
 // Four waves of a workgroup sit side by side; XCD-banded tile order as k_range.  Whole waves
 // stay active through the loop (the lane shifts need every lane).
-constexpr int kMarchCols = 62;   // output columns of an offset-layout wave
 #ifndef OCN_MARCH_ROWS
 #define OCN_MARCH_ROWS 8
 #endif
@@ -245,7 +244,7 @@ __global__ __launch_bounds__(256, OCN_MARCH_LB) void k_march(MarchGrid g, Body b
     const int tx = tile % R.ntx, ty = tile / R.ntx;
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    constexpr int cols = Body::kAligned ? 64 : kMarchCols;
+    constexpr int cols = Body::kAligned ? 64 : 64 - 2 * Body::kHalo;
     const int mw = R.w0 + (R.vert ? tx : tx * 4 + wave) * cols;   // first output column of this wave
     const int nb = R.n0 + (R.vert ? ty * 4 + wave : ty) * R.rows, ne = min(R.n1, nb + R.rows - 1);
     if (mw > R.m1 || nb > R.n1) return;                            // wave-uniform
@@ -256,9 +255,9 @@ __global__ __launch_bounds__(256, OCN_MARCH_LB) void k_march(MarchGrid g, Body b
         L.m = min(max(m, R.mlo), R.mhi);
         L.me = min(max(lane == 0 ? m - 1 : m + 1, R.mlo), R.mhi);
         L.edge = lane == 0 || lane == 63;
-    } else {
-        const int m = mw - 1 + lane;
-        L.out = lane >= 1 && lane <= kMarchCols && m <= R.m1;
+    } else {   // kHalo lanes on each side only load (the m -/+ kHalo neighbour columns)
+        const int m = mw - Body::kHalo + lane;
+        L.out = lane >= Body::kHalo && lane < 64 - Body::kHalo && m <= R.m1;
         L.m = L.me = min(max(m, R.mlo), R.mhi);
         L.edge = false;
     }
@@ -268,7 +267,8 @@ __global__ __launch_bounds__(256, OCN_MARCH_LB) void k_march(MarchGrid g, Body b
 template <typename Body>
 static MarchRect march_rect(const ocn_block *b, const Range &r, int rows = OCN_MARCH_ROWS, bool vert = false)
 {
-    int w0 = r.m0, cols = kMarchCols, mlo = max(r.m0 - 1, b->bnd_x1), mhi = min(r.m1 + 1, b->bnd_x2);
+    int w0 = r.m0, cols = 64 - 2 * Body::kHalo, mlo = max(r.m0 - Body::kHalo, b->bnd_x1),
+        mhi = min(r.m1 + Body::kHalo, b->bnd_x2);
     if (Body::kAligned) {   // waves start at nx_start + 64 j (256-B aligned rows, ocn_ctx.hip allocate)
         const int d = r.m0 - b->nx_start;
         w0 = b->nx_start + 64 * (d >= 0 ? d / 64 : -((63 - d) / 64));
@@ -407,6 +407,7 @@ template <bool RC> struct MarchViewB {
 // here, so a8's new sshp goes to the second sshp buffer (sshp_out), which the host swaps in.
 template <bool C1F, bool RC = false> struct MarchFusedB {
     static constexpr bool kAligned = false;
+    static constexpr int kHalo = 1;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; bool full, reuse; int32_t *nbad; double *sshp_out;
     using View = MarchViewB<RC>;
     struct Fn {
@@ -545,6 +546,7 @@ struct MarchViewA {
 // [start, end]^2)
 template <bool HH> struct MarchFusedA {
     static constexpr bool kAligned = true;
+    static constexpr int kHalo = 0;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau;
     using View = MarchViewA;
     struct Fn {
@@ -646,6 +648,7 @@ struct MarchViewH {
 // n <= end, where it is in range)
 struct MarchHhInit {
     static constexpr bool kAligned = true;
+    static constexpr int kHalo = 0;
     ocn_block b; Tab<true> t; int ffs; bool full;
     using View = MarchViewH;
     struct Fn {
@@ -756,6 +759,7 @@ struct LeftView {
 
 template <bool HH, bool SKIP> struct MarchCA {
     static constexpr bool kAligned = true;
+    static constexpr int kHalo = 0;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau;
     struct Fn {
         HhInit<true> c2; FusedA<true> a; const Tab<true> &t; int ylast;
@@ -883,6 +887,216 @@ template <bool HH, bool SKIP> struct MarchCA {
     }
 };
 
+// ------------------------------------------------------------------ one-pass step
+// A whole role-flip step in one register march (ocn_ctx.hip one_step_fused, "one-pass" steps of
+// a single-block call): the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp; h_r, mu, RHSx, RHSy)
+// is read once and the next state written once -- 10 + 6 arrays, against fused B + CA's 22 + 12.
+// Per wave row n (the march goes down the rows), two lagged computations:
+//   D(n+1): what the reference's previous hh_init and this step's fused A store and fused B reads
+//     back: hh_init's level-0 hu / hv / hh (interp of h_r + ssh * ffs) and level-1 hu / hv (of
+//     h_r + sshp * ffs) on [start-1, end]^2 under llu / llv / luh, a3's vort (interior, luu), a5's
+//     str_t (interior, lu) and str_s (interior, luu); hq = h_r + ssh * ffs (whole array).  Where
+//     the reference stores nothing (mask 0, or outside the stage's range) the array's value in
+//     memory is what it reads, so that is loaded there (those points are never written during
+//     the call: one block, no a8 / a9 work on the halo ring).
+//   S(n): a1 sw_update_ssh (-> sshn), fused B (a4 + a6 + a7 -> ubrtrn, vbrtrn) and a8's time
+//     filters (-> the second sshp / ubrtrp / vbrtrp buffers: the current ones are read at
+//     neighbours here) + check_ssh_err, reading D at rows n-1, n, n+1.
+// The reference's values are reproduced bit for bit: the same operands (hun = hu, hvn = hv: the
+// reuse identity, full_free_surface = 1) and the same arithmetic (sw_stencils.h *_math).
+// Lane layout: D needs the state at m +- 1 and S needs D at m +- 1, so a wave loads 64 columns
+// and produces 60 (kHalo = 2; output runs start on 32-B boundaries).  Rows n-1 .. n+2 of every
+// array and of the metric table stay in registers; the loads of the next row are issued before
+// the current row is computed.
+struct StepRegs {
+    template <class T> struct Win {   // rows n-1, n, n+1, n+2 at this lane's column
+        T r[4];
+        __device__ __forceinline__ T at(int dx, int dy) const
+        {
+            if (dy < -1 || dy > 2) ocn_march_bad_access();
+            return lane_shift(r[dy + 1], r[dy + 1], dx);
+        }
+        __device__ __forceinline__ void rotate() { r[0] = r[1]; r[1] = r[2]; r[2] = r[3]; }
+    };
+    // state
+    Win<double> u, v, up, vp, ssh, shp, hr, mu;
+    Win<unsigned> bits;
+    double rhsx, rhsy;
+    // D rows (computed one row ahead)
+    Win<double> hu, hv, hh, hu1, hv1, vort, stt, sts;
+    float g[kRowTable][4];            // metric rows n-1 .. n+2 (wave-uniform)
+    double tau, f;
+    __device__ __forceinline__ float met(int id, int dy) const { return g[id - OCN_DX][dy + 1]; }
+    __device__ __forceinline__ void rotate()
+    {
+        u.rotate(); v.rotate(); up.rotate(); vp.rotate(); ssh.rotate(); shp.rotate(); hr.rotate(); mu.rotate();
+        bits.rotate();
+        hu.rotate(); hv.rotate(); hh.rotate(); hu1.rotate(); hv1.rotate(); vort.rotate(); stt.rotate(); sts.rotate();
+        for (int k = 0; k < kRowTable; ++k) { g[k][0] = g[k][1]; g[k][1] = g[k][2]; g[k][2] = g[k][3]; }
+    }
+};
+
+// The stage views over StepRegs: OFF = 0 for S (row n), 1 for D (row n+1).
+#define OCN_SV(name, w) \
+    __device__ __forceinline__ double name(int dx, int dy) const { return x.w.at(dx, dy + OFF); }
+#define OCN_SG(name, id) \
+    __device__ __forceinline__ float name(int, int dy) const { return x.met(id, dy + OFF); }
+template <int OFF> struct StepView {
+    const StepRegs &x;
+    __device__ __forceinline__ double quot(double a, double b, int, int) const { return a / b; }
+    __device__ __forceinline__ double qtau(double a) const { return a / x.tau; }
+    __device__ __forceinline__ double tau2() const { return x.tau; }
+    __device__ __forceinline__ float mk(int id, int dx, int dy) const
+    {
+        return (x.bits.at(dx, dy + OFF) >> id) & 1u ? 1.0f : 0.0f;
+    }
+    __device__ __forceinline__ float lu(int dx, int dy) const { return mk(OCN_LU, dx, dy); }
+    __device__ __forceinline__ float luu(int dx, int dy) const { return mk(OCN_LUU, dx, dy); }
+    OCN_SV(u, u) OCN_SV(ubrtr, u) OCN_SV(v, v) OCN_SV(vbrtr, v) OCN_SV(up, up) OCN_SV(vp, vp)
+    OCN_SV(ubrtrp, up) OCN_SV(vbrtrp, vp) OCN_SV(ssh, ssh) OCN_SV(sh, ssh) OCN_SV(shp, shp) OCN_SV(sshp, shp)
+    OCN_SV(h_r, hr) OCN_SV(mu, mu)
+    OCN_SV(hu, hu) OCN_SV(hhu, hu) OCN_SV(hhun, hu) OCN_SV(hv, hv) OCN_SV(hhv, hv) OCN_SV(hhvn, hv)
+    OCN_SV(hh, hh) OCN_SV(hhh, hh) OCN_SV(hhup, hu1) OCN_SV(hhvp, hv1)
+    OCN_SV(vort, vort) OCN_SV(str_t, stt) OCN_SV(str_s, sts)
+    __device__ __forceinline__ double hq(int dx, int dy) const   // depth.f90:48 hq = h_r + sh*ffs
+    {
+        return x.hr.at(dx, dy + OFF) + x.ssh.at(dx, dy + OFF) * x.f;
+    }
+    __device__ __forceinline__ double RHSx(int dx, int dy) const
+    {
+        if (dx || dy) ocn_march_bad_access();
+        return x.rhsx;
+    }
+    __device__ __forceinline__ double RHSy(int dx, int dy) const
+    {
+        if (dx || dy) ocn_march_bad_access();
+        return x.rhsy;
+    }
+    OCN_SG(dx, OCN_DX) OCN_SG(dy, OCN_DY) OCN_SG(dxt, OCN_DXT) OCN_SG(dyt, OCN_DYT) OCN_SG(dxh, OCN_DXH)
+    OCN_SG(dyh, OCN_DYH) OCN_SG(dxb, OCN_DXB) OCN_SG(dyb, OCN_DYB) OCN_SG(rlh_s, OCN_RLH_S) OCN_SG(rdis, OCN_R_DISS)
+    __device__ __forceinline__ float sratio(int k) const { return x.met(OCN_DX + kNumRowFields + k, OFF); }
+};
+#undef OCN_SV
+#undef OCN_SG
+
+struct MarchStep {
+    static constexpr bool kAligned = false;
+    static constexpr int kHalo = 2;
+    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; int32_t *nbad;
+    double *sshp_out, *up_out, *vp_out;   // a8's filtered sshp / ubrtrp / vbrtrp (the second buffers)
+
+    // one row's loads for iteration n (rows of the state the march adds)
+    struct Batch { double u, v, up, vp, ssh, shp, hr, mu, rhsx, rhsy; unsigned bits; float g[kRowTable]; };
+    __device__ __forceinline__ void load(Batch &q, int m, int n) const
+    {
+        const Geo I = geo(&b);
+        const Pt c = I(m, n), c1 = I(m, n + 1), c2 = I(m, n + 2);
+        q.u = ld(t.f(OCN_UBRTR), c2); q.up = ld(t.f(OCN_UBRTRP), c2);
+        q.ssh = ld(t.f(OCN_SSH), c2); q.shp = ld(t.f(OCN_SSHP), c2); q.hr = ld(t.f(OCN_HHQ_REST), c2);
+        q.bits = ld(t.bits, c2);
+        q.v = ld(t.f(OCN_VBRTR), c1); q.vp = ld(t.f(OCN_VBRTRP), c1); q.mu = ld(t.f(OCN_MU), c1);
+        q.rhsx = ld(t.f(OCN_RHSX), c); q.rhsy = ld(t.f(OCN_RHSY), c);
+        MetRows::load(q.g, t.rows, t.nrows, c2.r);
+    }
+    __device__ __forceinline__ static void take(StepRegs &x, const Batch &q)
+    {
+        x.u.r[3] = q.u; x.up.r[3] = q.up; x.ssh.r[3] = q.ssh; x.shp.r[3] = q.shp; x.hr.r[3] = q.hr;
+        x.bits.r[3] = q.bits;
+        x.v.r[2] = q.v; x.vp.r[2] = q.vp; x.mu.r[2] = q.mu;
+        x.rhsx = q.rhsx; x.rhsy = q.rhsy;
+        for (int k = 0; k < kRowTable; ++k) x.g[k][3] = q.g[k];
+    }
+
+    // D at row r = n + 1 of this lane (column m): the values the reference's arrays hold there
+    __device__ __forceinline__ void derive(StepRegs &x, int m, int r) const
+    {
+        const StepView<1> d{x};
+        const Geo I = geo(&b);
+        const Pt c = I(m, r);
+        const double f = x.f;
+        const double a00 = d.h_r(0, 0) + d.sh(0, 0) * f, a10 = d.h_r(1, 0) + d.sh(1, 0) * f,
+                     a01 = d.h_r(0, 1) + d.sh(0, 1) * f, a11 = d.h_r(1, 1) + d.sh(1, 1) * f;
+        const double b00 = d.h_r(0, 0) + d.shp(0, 0) * f, b10 = d.h_r(1, 0) + d.shp(1, 0) * f,
+                     b01 = d.h_r(0, 1) + d.shp(0, 1) * f;
+        const double u0 = interp_u(d, a00, a10), v0 = interp_v(d, a00, a01), h0 = interp_h(d, a00, a10, a01, a11);
+        const double u1 = interp_u(d, b00, b10), v1 = interp_v(d, b00, b01);
+        const double vo = uv_trans_vort_math(d);
+        double st, ss;
+        stress_components_math(d, st, ss);
+        const unsigned bc = x.bits.r[2];
+        const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && r >= b.ny_start - 1 && r <= b.ny_end;
+        const bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
+        const bool llu = hh_rng && (bc & (1u << OCN_LLU)), llv = hh_rng && (bc & (1u << OCN_LLV)),
+                   luh = hh_rng && (bc & (1u << OCN_LUH));
+        x.hu.r[2] = llu ? u0 : ld(t.f(OCN_HHU), c);
+        x.hu1.r[2] = llu ? u1 : ld(t.f(OCN_HHU_P), c);
+        x.hv.r[2] = llv ? v0 : ld(t.f(OCN_HHV), c);
+        x.hv1.r[2] = llv ? v1 : ld(t.f(OCN_HHV_P), c);
+        x.hh.r[2] = luh ? h0 : ld(t.f(OCN_HHH), c);
+        x.vort.r[2] = in && (bc & (1u << OCN_LUU)) ? vo : ld(t.f(OCN_VORT), c);
+        x.stt.r[2] = in && (bc & (1u << OCN_LU)) ? st : ld(t.f(OCN_STR_T), c);
+        x.sts.r[2] = in && (bc & (1u << OCN_LUU)) ? ss : ld(t.f(OCN_STR_S), c);
+    }
+
+    // S at row n: a1, fused B, a8's filters, check_ssh_err
+    __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n) const
+    {
+        const StepView<0> s{x};
+        const Geo I = geo(&b);
+        const Pt c = I(L.m, n);
+        const double sshn = sw_update_ssh_math(s);
+        double rxa, rya, rxd, ryd, un, vn;
+        uv_trans_math(s, rxa, rya);
+        uv_diff2_math(s, rxd, ryd);
+        sw_update_uv_math(s, rxa, rxd, rya, ryd, un, vn);
+        const double ts = sw.time_smooth;
+        const double fx = asselin(x.ssh.r[1], sshn, x.shp.r[1], ts);
+        const double fa = asselin(x.u.r[1], un, x.up.r[1], ts), fb = asselin(x.v.r[1], vn, x.vp.r[1], ts);
+        if (!L.out) return;
+        const unsigned bc = x.bits.r[1];
+        if (bc & (1u << OCN_LU)) {
+            st(t.f(OCN_SSHN), c, sshn);
+            st(sshp_out, c, fx);
+            if (nbad && !(sshn < 10000.0 && sshn > -10000.0)) OCN_ATOMIC_INC(nbad);
+        }
+        if (bc & (1u << OCN_LCU)) { st(t.f(OCN_UBRTRN), c, un); st(up_out, c, fa); }
+        if (bc & (1u << OCN_LCV)) { st(t.f(OCN_VBRTRN), c, vn); st(vp_out, c, fb); }
+    }
+
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Geo I = geo(&b);
+        StepRegs x{};
+        x.tau = tau;
+        x.f = (double)sw.full_free_surface;
+        // iteration n computes D(n+1) and, from n = nb on, S(n); two warm iterations give D(nb-1)
+        // and D(nb).  Before iteration n0 = nb - 2 the rows it does not load itself: up, ssh, sshp,
+        // h_r, bits at n0+1; vp at n0; metric rows n0, n0+1.
+        const int n0 = nb - 2;
+        {
+            const Pt c = I(L.m, n0), c1 = I(L.m, n0 + 1);
+            x.up.r[2] = ld(t.f(OCN_UBRTRP), c1); x.ssh.r[2] = ld(t.f(OCN_SSH), c1);
+            x.shp.r[2] = ld(t.f(OCN_SSHP), c1); x.hr.r[2] = ld(t.f(OCN_HHQ_REST), c1);
+            x.bits.r[2] = ld(t.bits, c1); x.u.r[2] = ld(t.f(OCN_UBRTR), c1);
+            x.vp.r[1] = ld(t.f(OCN_VBRTRP), c);
+            for (int k = 0; k < kRowTable; ++k) {
+                x.g[k][1] = ld(t.rows, (unsigned)k * t.nrows + c.r);
+                x.g[k][2] = ld(t.rows, (unsigned)k * t.nrows + c1.r);
+            }
+        }
+        Batch cur, nxt;
+        load(cur, L.m, n0);
+        for (int n = n0; n <= ne; ++n) {
+            take(x, cur);
+            if (n < ne) load(nxt, L.m, n + 1);   // in flight while this row is computed
+            derive(x, L.m, n + 1);
+            if (n >= nb) step(x, L, n);      // wave-uniform
+            x.rotate();
+            cur = nxt;
+        }
+    }
+};
+
 #define CHECK(...)                                                \
     do {                                                          \
         int _rc = check_block(b);                                 \
@@ -1002,6 +1216,22 @@ int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compac
     if (skip_rc) return launch_march_part(b, r, part, MarchCA<false, true>{*b, t, sw, tau_next}, s);
     if (next_reuse) return launch_march_part(b, r, part, MarchCA<false, false>{*b, t, sw, tau_next}, s);
     return launch_march_part(b, r, part, MarchCA<true, false>{*b, t, sw, tau_next}, s);
+}
+
+#ifndef OCN_STEP_ROWS
+#define OCN_STEP_ROWS 16   // rows per wave tile of the one-pass step (2 warm rows per tile)
+#endif
+int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                   double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s)
+{
+    if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
+        !up_out || !vp_out)
+        return set_error(OCN_ERR_ARG, "one-pass step: compact tables, march, full_free_surface = 1, trans_terms and "
+                                      "ksw_lat on, three second buffers");
+    RC_K(check_block(b));
+    const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
+    const Range r = range_interior(b);
+    return launch_march_rects(b, &r, 1, MarchStep{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s, OCN_STEP_ROWS);
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy

@@ -167,6 +167,13 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_RECOMPUTE, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_onepass(self, on: bool = True):
+        """One-pass steps in single-block role-flip calls (default): each middle step of a call is
+        one launch that reads the state once and writes the next state once; same results bit
+        for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_ONEPASS, int(on)), "ocn_ctx_set_option")
+        return self
+
     def option(self, key: int) -> int:
         v = C.c_int64(0)
         check(lib().ocn_ctx_get_option(self.ctx, key, C.byref(v)), "ocn_ctx_get_option")
@@ -181,6 +188,11 @@ class OceanModel:
     def recompute_active(self) -> bool:
         """Whether the last step() used recompute steps."""
         return bool(self.option(_lib.OPT_RECOMPUTE))
+
+    @property
+    def onepass_active(self) -> bool:
+        """Whether the last step() used one-pass steps."""
+        return bool(self.option(_lib.OPT_ONEPASS))
 
     @property
     def compact_active(self) -> bool:

@@ -162,17 +162,21 @@ def _full(amd, name, **opts):
     return case, m
 
 
-@pytest.mark.parametrize("variant", ["bench", "graph", "noflip"])
+@pytest.mark.parametrize("variant", ["bench", "graph", "noflip", "noonepass"])
 def test_bench_workload_matches_reference(amd, variant):
     """The bench's exact workload and options (bench.py: 4096^2 box, 1 block, stage-timing events
-    on, one call whose steps are first / recompute / CA / last) vs the reference's 6-step run."""
-    case, m = _full(amd, "box4096_b1x1_s6", graph=variant == "graph", flip=variant != "noflip")
+    on, one call whose steps are first / one-pass x 4 / CA + last) vs the reference's 6-step run;
+    noonepass: the recompute steps instead."""
+    case, m = _full(amd, "box4096_b1x1_s6", graph=variant == "graph", flip=variant != "noflip",
+                    onepass=variant != "noonepass")
     try:
         m.init()
         if variant == "bench":
             m.set_stage_timing(True)
         m.step(case["steps"], tau=1.0, check_every=1).synchronize()
         if variant == "bench":
+            assert m.flip_active and m.onepass_active
+        if variant == "noonepass":
             assert m.flip_active and m.recompute_active
         bad = compare_case(m, case, "box4096")
     finally:

@@ -112,7 +112,7 @@ def test_tracer_kernels_match_reference(amd, geom):
 
 
 def build_model(amd, case, graph=False, fused=True, compact=True, overlap=1, march=True, flip=True,
-                recompute=True, rank=0, nranks=1):
+                recompute=True, rank=0, nranks=1, onepass=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"])
@@ -125,6 +125,7 @@ def build_model(amd, case, graph=False, fused=True, compact=True, overlap=1, mar
     m.set_march(march)
     m.set_flip(flip)
     m.set_recompute(recompute)
+    m.set_onepass(onepass)
     if graph:
         m.set_graph(True)
     return m
@@ -150,8 +151,8 @@ def compare_case(m, case, name, whole=True):
     return bad
 
 
-@pytest.mark.parametrize("mode", ["compact", "norecompute", "noflip", "pointwise", "fused", "stages", "serial",
-                                  "overlap2"])
+@pytest.mark.parametrize("mode", ["compact", "noonepass", "norecompute", "noflip", "pointwise", "fused", "stages",
+                                  "serial", "overlap2"])
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
@@ -164,18 +165,22 @@ def test_end_to_end_matches_reference(amd, name, mode):
     the 4-launch step on the 2-D real(4) arrays; serial = compact without the overlap; stages =
     the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    compact = mode in ("compact", "norecompute", "noflip", "serial", "pointwise", "overlap2")
+    compact = mode in ("compact", "noonepass", "norecompute", "noflip", "serial", "pointwise", "overlap2")
     m = build_model(amd, case, fused=mode != "stages", compact=compact,
                     overlap=2 if mode == "overlap2" else int(mode != "serial"),
-                    march=mode != "pointwise", flip=mode != "noflip", recompute=mode != "norecompute")
+                    march=mode != "pointwise", flip=mode != "noflip", recompute=mode != "norecompute",
+                    onepass=mode != "noonepass")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     assert m.compact_active == compact
     bad = compare_case(m, case, name)
-    flip_used = m.flip_active
+    flip_used, one_used = m.flip_active, m.onepass_active
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
-    if mode in ("compact", "norecompute", "serial", "overlap2") and case["sw"].get("use_tracers", 0) <= 0:
+    if mode in ("compact", "noonepass", "norecompute", "serial", "overlap2") and case["sw"].get("use_tracers", 0) <= 0:
         assert flip_used, f"{name}: role-flip steps not used"
+    if mode == "compact" and name.startswith("box") and "_b1x1_" in name and case["sw"]["trans_terms"] > 0 \
+            and case["sw"]["ksw_lat"] > 0:
+        assert one_used, f"{name}: one-pass steps not used"
 
 
 @pytest.mark.parametrize("graph", [False, True], ids=["stream", "graph"])
