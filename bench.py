@@ -109,18 +109,46 @@ def dims_create(n: int):
     return n, 1
 
 
-def cpu_baseline(seconds_hint: float = 10.0):
-    """Time the oracle (C restatement, one core) on a bounded sample: 2048^2 box, 6 steps."""
+def cpu_cores() -> int:
+    """Host cores this process may use (the GPU box exports OMP_NUM_THREADS = its CPU share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, min(n, 64))
+
+
+def cpu_baseline(n_full: int = 4096):
+    """The CPU path on this node's host cores: the C restatement of the reference
+    (oracle/, bitwise the reference's results) timed on bounded samples of the bench workload --
+      1 core : a 2048^2 box (a quarter of the workload), 1 block, 6 timed steps;
+      C cores: the 4096^2 box decomposed into C blocks (MPI_Dims_create(C) grid), one block per
+               core -- the reference's OpenMP-over-blocks mode (kernel_interface.f90:84-88) --
+               6 timed steps.
+    Each leg runs 1 untimed warm-up step first.  `value` is the C-core rate."""
     from oracle import oracle as O
-    n, steps = 2048, 16
-    om = O.OracleModel(O.BasinConfig(nx=n + 4, ny=n + 4), O.SWConfig(), 1, 1).init()
-    om.run(1)
-    t0 = time.perf_counter()
-    om.run(steps)
-    dt = time.perf_counter() - t0
-    return {"value": n * n * steps / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/sw_oracle.c (gcc -O2 -ffp-contract=off), {n}x{n} box, 1 block, {steps} timed steps "
-                      f"after 1 warm-up step, {dt:.1f} s"}
+    cores = cpu_cores()
+
+    def leg(n, bxy, threads, steps):
+        om = O.OracleModel(O.BasinConfig(nx=n + 4, ny=n + 4), O.SWConfig(), *bxy, threads=threads).init()
+        om.run(1)
+        t0 = time.perf_counter()
+        om.run(steps)
+        dt = time.perf_counter() - t0
+        if om.pool is not None:
+            om.pool.shutdown()
+        return n * n * steps / dt, dt
+
+    v1, t1 = leg(2048, (1, 1), 1, 6)
+    bxy = dims_create(cores)
+    vc, tc = leg(n_full, bxy, cores, 6)
+    return {"value": vc, "unit": "cell-updates/s", "cores": cores, "kind": "port",
+            "1core": {"value": v1, "sample": f"2048x2048 box, 1 block, 6 timed steps, {t1:.1f} s"},
+            "allcores": {"value": vc, "cores": cores,
+                         "sample": f"{n_full}x{n_full} box, {bxy[0]}x{bxy[1]} blocks on {cores} threads, 6 timed steps, "
+                                   f"{tc:.1f} s"},
+            "sample": "oracle/sw_oracle.c (gcc -O2 -ffp-contract=off, bitwise the reference) on this node's host cores; "
+                      "value = the all-cores leg"}
 
 
 def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for):

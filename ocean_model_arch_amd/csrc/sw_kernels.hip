@@ -21,6 +21,9 @@
 // per array.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+#include <type_traits>
+
 #include "ocn_internal.h"
 #include "sw_stencils.h"
 
@@ -229,8 +232,12 @@ struct Lane { int m, me; bool edge, out; };
 struct MarchRect { int m0, m1, n0, n1, w0, ntx, tiles, mlo, mhi, rows, vert; };
 struct MarchGrid { int nr, ntiles; MarchRect r[4]; };
 
+// waves per SIMD a march body asks of the register allocator (Body::kWaves, else OCN_MARCH_LB)
+template <class B, class = void> struct WavesOf { static constexpr int v = OCN_MARCH_LB; };
+template <class B> struct WavesOf<B, std::void_t<decltype(B::kWaves)>> { static constexpr int v = B::kWaves; };
+
 template <class Body>
-__global__ __launch_bounds__(256, OCN_MARCH_LB) void k_march(MarchGrid g, Body body)
+__global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Body body)
 {
     int tile = (int)blockIdx.x;
 #if OCN_XCD_REMAP
@@ -888,6 +895,12 @@ template <bool HH, bool SKIP> struct MarchCA {
 };
 
 // ------------------------------------------------------------------ one-pass step
+#ifndef OCN_STEP_ROWS
+#define OCN_STEP_ROWS 32   // rows per wave tile of the one-pass step (2 warm rows per tile)
+#endif
+#ifndef OCN_STEP_WAVES
+#define OCN_STEP_WAVES 2   // waves per SIMD asked of the register allocator
+#endif
 // A whole role-flip step in one register march (ocn_ctx.hip one_step_fused, "one-pass" steps of
 // a single-block call): the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp; h_r, mu, RHSx, RHSy)
 // is read once and the next state written once -- 10 + 6 arrays, against fused B + CA's 22 + 12.
@@ -925,7 +938,8 @@ struct StepRegs {
     // D rows (computed one row ahead)
     Win<double> hu, hv, hh, hu1, hv1, vort, stt, sts;
     float g[kRowTable][4];            // metric rows n-1 .. n+2 (wave-uniform)
-    double tau, f;
+    double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
+    double tau, inv_tau, f;
     __device__ __forceinline__ float met(int id, int dy) const { return g[id - OCN_DX][dy + 1]; }
     __device__ __forceinline__ void rotate()
     {
@@ -941,10 +955,13 @@ struct StepRegs {
     __device__ __forceinline__ double name(int dx, int dy) const { return x.w.at(dx, dy + OFF); }
 #define OCN_SG(name, id) \
     __device__ __forceinline__ float name(int, int dy) const { return x.met(id, dy + OFF); }
-template <int OFF> struct StepView {
+// P2: tau is a power of two, so a / tau is a * (1 / tau) bit for bit (the same real value
+// rounded once: both are exact scalings by 2^k unless the result is subnormal, and then both
+// round the same real number)
+template <int OFF, bool P2> struct StepView {
     const StepRegs &x;
     __device__ __forceinline__ double quot(double a, double b, int, int) const { return a / b; }
-    __device__ __forceinline__ double qtau(double a) const { return a / x.tau; }
+    __device__ __forceinline__ double qtau(double a) const { return P2 ? a * x.inv_tau : a / x.tau; }
     __device__ __forceinline__ double tau2() const { return x.tau; }
     __device__ __forceinline__ float mk(int id, int dx, int dy) const
     {
@@ -979,9 +996,10 @@ template <int OFF> struct StepView {
 #undef OCN_SV
 #undef OCN_SG
 
-struct MarchStep {
+template <bool P2> struct MarchStep {
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
+    static constexpr int kWaves = OCN_STEP_WAVES;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; int32_t *nbad;
     double *sshp_out, *up_out, *vp_out;   // a8's filtered sshp / ubrtrp / vbrtrp (the second buffers)
 
@@ -1010,7 +1028,7 @@ struct MarchStep {
     // D at row r = n + 1 of this lane (column m): the values the reference's arrays hold there
     __device__ __forceinline__ void derive(StepRegs &x, int m, int r) const
     {
-        const StepView<1> d{x};
+        const StepView<1, P2> d{x};
         const Geo I = geo(&b);
         const Pt c = I(m, r);
         const double f = x.f;
@@ -1021,8 +1039,16 @@ struct MarchStep {
         const double u0 = interp_u(d, a00, a10), v0 = interp_v(d, a00, a01), h0 = interp_h(d, a00, a10, a01, a11);
         const double u1 = interp_u(d, b00, b10), v1 = interp_v(d, b00, b01);
         const double vo = uv_trans_vort_math(d);
-        double st, ss;
-        stress_components_math(d, st, ss);
+        // a5 (mixing.f90:33-44, sw_stencils.h stress_components_math) with its quotients shared:
+        // up/dyh at m-1 is the left lane's up/dyh (dyh is constant along the row), vp/dxh at n-1
+        // is the previous row's, up/dxt at n+1 the next row's (formed here, kept for the next
+        // row), vp/dyt at m+1 the right lane's -- the same operands, so the same values
+        const double qa = d.up(0, 0) / D(d.dyh(0, 0)), qb = d.vp(0, 0) / D(d.dxh(0, 0));
+        const double qc1 = d.up(0, 1) / D(d.dxt(0, 1)), qe = d.vp(0, 0) / D(d.dyt(0, 0));
+        const double st = D(d.sratio(0)) * (qa - lane_shift(qa, qa, -1)) - D(d.sratio(1)) * (qb - x.qb);
+        const double ss = D(d.sratio(2)) * (qc1 - x.qc) + D(d.sratio(3)) * (lane_shift(qe, qe, 1) - qe);
+        x.qb = qb;
+        x.qc = qc1;
         const unsigned bc = x.bits.r[2];
         const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && r >= b.ny_start - 1 && r <= b.ny_end;
         const bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
@@ -1041,7 +1067,7 @@ struct MarchStep {
     // S at row n: a1, fused B, a8's filters, check_ssh_err
     __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n) const
     {
-        const StepView<0> s{x};
+        const StepView<0, P2> s{x};
         const Geo I = geo(&b);
         const Pt c = I(L.m, n);
         const double sshn = sw_update_ssh_math(s);
@@ -1068,6 +1094,7 @@ struct MarchStep {
         const Geo I = geo(&b);
         StepRegs x{};
         x.tau = tau;
+        x.inv_tau = 1.0 / tau;
         x.f = (double)sw.full_free_surface;
         // iteration n computes D(n+1) and, from n = nb on, S(n); two warm iterations give D(nb-1)
         // and D(nb).  Before iteration n0 = nb - 2 the rows it does not load itself: up, ssh, sshp,
@@ -1083,6 +1110,9 @@ struct MarchStep {
                 x.g[k][1] = ld(t.rows, (unsigned)k * t.nrows + c.r);
                 x.g[k][2] = ld(t.rows, (unsigned)k * t.nrows + c1.r);
             }
+            // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
+            x.qb = x.vp.r[1] / D(x.g[OCN_DXH - OCN_DX][1]);
+            x.qc = x.up.r[2] / D(x.g[OCN_DXT - OCN_DX][2]);
         }
         Batch cur, nxt;
         load(cur, L.m, n0);
@@ -1218,9 +1248,6 @@ int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compac
     return launch_march_part(b, r, part, MarchCA<true, false>{*b, t, sw, tau_next}, s);
 }
 
-#ifndef OCN_STEP_ROWS
-#define OCN_STEP_ROWS 16   // rows per wave tile of the one-pass step (2 warm rows per tile)
-#endif
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s)
 {
@@ -1231,7 +1258,12 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
     RC_K(check_block(b));
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
     const Range r = range_interior(b);
-    return launch_march_rects(b, &r, 1, MarchStep{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s, OCN_STEP_ROWS);
+    int ex;
+    if (std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020)   // tau = 2^k
+        return launch_march_rects(b, &r, 1, MarchStep<true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s,
+                                  OCN_STEP_ROWS);
+    return launch_march_rects(b, &r, 1, MarchStep<false>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s,
+                              OCN_STEP_ROWS);
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy

@@ -174,8 +174,15 @@ def _p(a: np.ndarray):
 class OracleModel:
     """Per-block field storage (ocean_type/grid_type restated) + the SW algorithm layer."""
 
-    def __init__(self, basin: BasinConfig, sw: SWConfig = SWConfig(), bnx: int = 1, bny: int = 1):
+    def __init__(self, basin: BasinConfig, sw: SWConfig = SWConfig(), bnx: int = 1, bny: int = 1, threads: int = 1):
+        """threads > 1: the kernel calls of a stage run over the blocks on that many host threads
+        (the reference's OpenMP mode, core/kernel_interface.f90:84-88 `!$omp do schedule(static,1)`
+        over blocks; the C kernels release the GIL); halo copies stay serial."""
         self.basin, self.sw = basin, sw
+        self.pool = None
+        if threads > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            self.pool = ThreadPoolExecutor(max_workers=threads)
         self.mask = basin.global_mask()
         self.blocks = decompose(basin.nx, basin.ny, bnx, bny, self.mask)
         self.f: list[dict[str, np.ndarray]] = []
@@ -267,10 +274,15 @@ class OracleModel:
     # ---------------------------------------------------------------- stages (a1..a10)
     def _each(self, fn, *names, scalars=(), tau=None):
         """fn(bounds, scalars..., arrays...) per block; the names "TAU" / "ONE" pass tau / 1.0d0 by value."""
-        for k, b in enumerate(self.blocks):
-            f = self.f[k]
+        def one(k):
+            b, f = self.blocks[k], self.f[k]
             fn(*b.args, *scalars, *[C.c_double(tau) if n == "TAU" else C.c_double(1.0) if n == "ONE" else _p(f[n])
                                     for n in names])
+        if self.pool is None:
+            for k in range(len(self.blocks)):
+                one(k)
+        else:
+            list(self.pool.map(one, range(len(self.blocks))))
 
     def stage_sw_update_ssh(self, tau):
         self._each(self.L.orc_sw_update_ssh, "lu", "dx", "dy", "dxh", "dyh", "hhu", "hhv",

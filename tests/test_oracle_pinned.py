@@ -120,3 +120,21 @@ def test_uniform_decomposition_sizes():
     assert O.uniform_sizes(285, 4) == [71, 71, 71, 72]
     assert O.uniform_sizes(159, 2) == [79, 80]
     assert sum(O.uniform_sizes(1024, 8)) == 1024
+
+
+def test_oracle_threads_over_blocks_match_reference():
+    """The all-cores CPU baseline's mode (threads over blocks, kernel_interface.f90:84-88) gives the
+    reference's results bit for bit."""
+    name = "box70x54_b3x2_s20"
+    case = cases.load_e2e(name)
+    b = case["basin"]
+    basin = O.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"],
+                          rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"])
+    m = O.OracleModel(basin, O.SWConfig(**case["sw"]), *case["bxy"], threads=3).init().run(case["steps"])
+    m.pool.shutdown()
+    z = case["z"]
+    for k, blk in enumerate(m.blocks):
+        for nm, a in m.f[k].items():
+            key = f"b{blk.bm}_{blk.bn}/sha/{nm}"
+            if key in z.files:
+                assert _sha(a) == str(z[key]), f"block ({blk.bm},{blk.bn}) field {nm} differs"
