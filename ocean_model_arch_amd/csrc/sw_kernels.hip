@@ -921,13 +921,27 @@ template <bool HH, bool SKIP> struct MarchCA {
 // and produces 60 (kHalo = 2; output runs start on 32-B boundaries).  Rows n-1 .. n+2 of every
 // array and of the metric table stay in registers; the loads of the next row are issued before
 // the current row is computed.
+// x of lane + dx (dx in {-1, 0, 1}); 0 in the lane without a source (bound_ctrl): the one-pass
+// march reads such values only in its halo lanes, so no old value needs to be kept
+__device__ __forceinline__ int dpp_shz(int x, int dx)
+{
+    if (dx > 0) return __builtin_amdgcn_mov_dpp(x, 0x130, 0xf, 0xf, true);   // wave_shl:1
+    return __builtin_amdgcn_mov_dpp(x, 0x138, 0xf, 0xf, true);               // wave_shr:1
+}
+__device__ __forceinline__ double shz(double x, int dx)
+{
+    if (dx == 0) return x;
+    return __hiloint2double(dpp_shz(__double2hiint(x), dx), dpp_shz(__double2loint(x), dx));
+}
+__device__ __forceinline__ unsigned shz(unsigned x, int dx) { return dx == 0 ? x : (unsigned)dpp_shz((int)x, dx); }
+
 struct StepRegs {
     template <class T> struct Win {   // rows n-1, n, n+1, n+2 at this lane's column
         T r[4];
         __device__ __forceinline__ T at(int dx, int dy) const
         {
             if (dy < -1 || dy > 2) ocn_march_bad_access();
-            return lane_shift(r[dy + 1], r[dy + 1], dx);
+            return shz(r[dy + 1], dx);
         }
         __device__ __forceinline__ void rotate() { r[0] = r[1]; r[1] = r[2]; r[2] = r[3]; }
     };
@@ -937,64 +951,30 @@ struct StepRegs {
     double rhsx, rhsy;
     // D rows (computed one row ahead)
     Win<double> hu, hv, hh, hu1, hv1, vort, stt, sts;
+    // products shared between lanes / rows (each the reference's own sub-expression, see derive)
+    Win<double> w0, w1;               // interp weights ((h * dx) * dy) * lu of levels 0 / 1 (rows n+1, n+2)
+    Win<double> pu, pv, vh, t3, cx, rr, dt, dxq;
     float g[kRowTable][4];            // metric rows n-1 .. n+2 (wave-uniform)
     double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
     double tau, inv_tau, f;
     __device__ __forceinline__ float met(int id, int dy) const { return g[id - OCN_DX][dy + 1]; }
+    __device__ __forceinline__ float mk(int id, int dx, int dy) const
+    {
+        return (bits.at(dx, dy) >> id) & 1u ? 1.0f : 0.0f;
+    }
     __device__ __forceinline__ void rotate()
     {
         u.rotate(); v.rotate(); up.rotate(); vp.rotate(); ssh.rotate(); shp.rotate(); hr.rotate(); mu.rotate();
         bits.rotate();
         hu.rotate(); hv.rotate(); hh.rotate(); hu1.rotate(); hv1.rotate(); vort.rotate(); stt.rotate(); sts.rotate();
+        w0.rotate(); w1.rotate(); pu.rotate(); pv.rotate(); vh.rotate(); t3.rotate(); cx.rotate(); rr.rotate();
+        dt.rotate(); dxq.rotate();
         for (int k = 0; k < kRowTable; ++k) { g[k][0] = g[k][1]; g[k][1] = g[k][2]; g[k][2] = g[k][3]; }
     }
 };
 
-// The stage views over StepRegs: OFF = 0 for S (row n), 1 for D (row n+1).
-#define OCN_SV(name, w) \
-    __device__ __forceinline__ double name(int dx, int dy) const { return x.w.at(dx, dy + OFF); }
-#define OCN_SG(name, id) \
-    __device__ __forceinline__ float name(int, int dy) const { return x.met(id, dy + OFF); }
-// P2: tau is a power of two, so a / tau is a * (1 / tau) bit for bit (the same real value
-// rounded once: both are exact scalings by 2^k unless the result is subnormal, and then both
-// round the same real number)
-template <int OFF, bool P2> struct StepView {
-    const StepRegs &x;
-    __device__ __forceinline__ double quot(double a, double b, int, int) const { return a / b; }
-    __device__ __forceinline__ double qtau(double a) const { return P2 ? a * x.inv_tau : a / x.tau; }
-    __device__ __forceinline__ double tau2() const { return x.tau; }
-    __device__ __forceinline__ float mk(int id, int dx, int dy) const
-    {
-        return (x.bits.at(dx, dy + OFF) >> id) & 1u ? 1.0f : 0.0f;
-    }
-    __device__ __forceinline__ float lu(int dx, int dy) const { return mk(OCN_LU, dx, dy); }
-    __device__ __forceinline__ float luu(int dx, int dy) const { return mk(OCN_LUU, dx, dy); }
-    OCN_SV(u, u) OCN_SV(ubrtr, u) OCN_SV(v, v) OCN_SV(vbrtr, v) OCN_SV(up, up) OCN_SV(vp, vp)
-    OCN_SV(ubrtrp, up) OCN_SV(vbrtrp, vp) OCN_SV(ssh, ssh) OCN_SV(sh, ssh) OCN_SV(shp, shp) OCN_SV(sshp, shp)
-    OCN_SV(h_r, hr) OCN_SV(mu, mu)
-    OCN_SV(hu, hu) OCN_SV(hhu, hu) OCN_SV(hhun, hu) OCN_SV(hv, hv) OCN_SV(hhv, hv) OCN_SV(hhvn, hv)
-    OCN_SV(hh, hh) OCN_SV(hhh, hh) OCN_SV(hhup, hu1) OCN_SV(hhvp, hv1)
-    OCN_SV(vort, vort) OCN_SV(str_t, stt) OCN_SV(str_s, sts)
-    __device__ __forceinline__ double hq(int dx, int dy) const   // depth.f90:48 hq = h_r + sh*ffs
-    {
-        return x.hr.at(dx, dy + OFF) + x.ssh.at(dx, dy + OFF) * x.f;
-    }
-    __device__ __forceinline__ double RHSx(int dx, int dy) const
-    {
-        if (dx || dy) ocn_march_bad_access();
-        return x.rhsx;
-    }
-    __device__ __forceinline__ double RHSy(int dx, int dy) const
-    {
-        if (dx || dy) ocn_march_bad_access();
-        return x.rhsy;
-    }
-    OCN_SG(dx, OCN_DX) OCN_SG(dy, OCN_DY) OCN_SG(dxt, OCN_DXT) OCN_SG(dyt, OCN_DYT) OCN_SG(dxh, OCN_DXH)
-    OCN_SG(dyh, OCN_DYH) OCN_SG(dxb, OCN_DXB) OCN_SG(dyb, OCN_DYB) OCN_SG(rlh_s, OCN_RLH_S) OCN_SG(rdis, OCN_R_DISS)
-    __device__ __forceinline__ float sratio(int k) const { return x.met(OCN_DX + kNumRowFields + k, OFF); }
-};
-#undef OCN_SV
-#undef OCN_SG
+// metric id `id` of row n + dy as a double
+#define OCN_MD(id, dy) D(x.met((id), (dy)))
 
 template <bool P2> struct MarchStep {
     static constexpr bool kAligned = false;
@@ -1002,6 +982,10 @@ template <bool P2> struct MarchStep {
     static constexpr int kWaves = OCN_STEP_WAVES;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; int32_t *nbad;
     double *sshp_out, *up_out, *vp_out;   // a8's filtered sshp / ubrtrp / vbrtrp (the second buffers)
+
+    // a / tau (sw_update_uv_math qtau).  P2: tau is a power of two, so a / tau is a * (1 / tau) bit
+    // for bit (both round the same real value once; exact scalings unless subnormal)
+    __device__ __forceinline__ double qtau(const StepRegs &x, double a) const { return P2 ? a * x.inv_tau : a / x.tau; }
 
     // one row's loads for iteration n (rows of the state the march adds)
     struct Batch { double u, v, up, vp, ssh, shp, hr, mu, rhsx, rhsy; unsigned bits; float g[kRowTable]; };
@@ -1025,28 +1009,54 @@ template <bool P2> struct MarchStep {
         for (int k = 0; k < kRowTable; ++k) x.g[k][3] = q.g[k];
     }
 
-    // D at row r = n + 1 of this lane (column m): the values the reference's arrays hold there
+    // hh_init's interpolation weights of row n + dy (slot dy + 1): interp_wt(h) = h * dx * dy * lu
+    // (sw_stencils.h) with h = h_r + sh * ffs (level 0) or h_r + shp * ffs (level 1).  The weight
+    // of corner (m+1, n) / (m, n+1) of a point is its right / upper neighbour's own weight: dx and
+    // dy are constant along a row, so the operands are the same.
+    __device__ __forceinline__ static void weights(StepRegs &x, int dy)
+    {
+        const int k = dy + 1;
+        const double gx = OCN_MD(OCN_DX, dy), gy = OCN_MD(OCN_DY, dy);
+        const double l = D(x.mk(OCN_LU, 0, dy));
+        x.w0.r[k] = (x.hr.r[k] + x.ssh.r[k] * x.f) * gx * gy * l;
+        x.w1.r[k] = (x.hr.r[k] + x.shp.r[k] * x.f) * gx * gy * l;
+    }
+
+    // D at row r = n + 1 of this lane (column m): the values the reference's arrays hold there,
+    // plus the shared products of that row
     __device__ __forceinline__ void derive(StepRegs &x, int m, int r) const
     {
-        const StepView<1, P2> d{x};
         const Geo I = geo(&b);
         const Pt c = I(m, r);
-        const double f = x.f;
-        const double a00 = d.h_r(0, 0) + d.sh(0, 0) * f, a10 = d.h_r(1, 0) + d.sh(1, 0) * f,
-                     a01 = d.h_r(0, 1) + d.sh(0, 1) * f, a11 = d.h_r(1, 1) + d.sh(1, 1) * f;
-        const double b00 = d.h_r(0, 0) + d.shp(0, 0) * f, b10 = d.h_r(1, 0) + d.shp(1, 0) * f,
-                     b01 = d.h_r(0, 1) + d.shp(0, 1) * f;
-        const double u0 = interp_u(d, a00, a10), v0 = interp_v(d, a00, a01), h0 = interp_h(d, a00, a10, a01, a11);
-        const double u1 = interp_u(d, b00, b10), v1 = interp_v(d, b00, b01);
-        const double vo = uv_trans_vort_math(d);
+        weights(x, 2);   // row n+2 (rows n+1's were formed one iteration ago)
+        // hh_init levels 0 and 1 (depth.f90:52-97, sw_stencils.h interp_u / interp_v / interp_h)
+        const float l00 = x.mk(OCN_LU, 0, 1), l10 = x.mk(OCN_LU, 1, 1), l01 = x.mk(OCN_LU, 0, 2),
+                    l11 = x.mk(OCN_LU, 1, 2);
+        const double su = D(l00 + l10), sv = D(l00 + l01), sh4 = D(l00 + l10 + l01 + l11);
+        const double dxt = OCN_MD(OCN_DXT, 1), dyt = OCN_MD(OCN_DYT, 1), dxh = OCN_MD(OCN_DXH, 1),
+                     dyh = OCN_MD(OCN_DYH, 1), dxb = OCN_MD(OCN_DXB, 1), dyb = OCN_MD(OCN_DYB, 1);
+        const double w00 = x.w0.r[2], w10 = shz(w00, 1), w01 = x.w0.r[3], w11 = shz(w01, 1);
+        const double p00 = x.w1.r[2], p10 = shz(p00, 1), p01 = x.w1.r[3];
+        const double s0 = w00 + w10;
+        const double u0 = div_mask_sum(s0, su) / dxt / dyh;
+        const double v0 = div_mask_sum(w00 + w01, sv) / dxh / dyt;
+        const double h0 = div_mask_sum(s0 + w01 + w11, sh4) / dxb / dyb;
+        const double u1 = div_mask_sum(p00 + p10, su) / dxt / dyh;
+        const double v1 = div_mask_sum(p00 + p01, sv) / dxh / dyt;
+        // a3 uv_trans_vort (vel_ssh.f90:247-281, sw_stencils.h uv_trans_vort_math)
+        const double u_0 = x.u.r[2], u_1 = x.u.r[3], v_0 = x.v.r[2], v_r = shz(v_0, 1);
+        const double vort = (v_r * dyt - v_0 * dyt) - (u_1 * OCN_MD(OCN_DXT, 2) - u_0 * dxt)
+                            - ((v_r - v_0) * dyb - (u_1 - u_0) * dxb);
         // a5 (mixing.f90:33-44, sw_stencils.h stress_components_math) with its quotients shared:
         // up/dyh at m-1 is the left lane's up/dyh (dyh is constant along the row), vp/dxh at n-1
         // is the previous row's, up/dxt at n+1 the next row's (formed here, kept for the next
         // row), vp/dyt at m+1 the right lane's -- the same operands, so the same values
-        const double qa = d.up(0, 0) / D(d.dyh(0, 0)), qb = d.vp(0, 0) / D(d.dxh(0, 0));
-        const double qc1 = d.up(0, 1) / D(d.dxt(0, 1)), qe = d.vp(0, 0) / D(d.dyt(0, 0));
-        const double st = D(d.sratio(0)) * (qa - lane_shift(qa, qa, -1)) - D(d.sratio(1)) * (qb - x.qb);
-        const double ss = D(d.sratio(2)) * (qc1 - x.qc) + D(d.sratio(3)) * (lane_shift(qe, qe, 1) - qe);
+        const double qa = x.up.r[2] / dyh, qb = x.vp.r[2] / dxh;
+        const double qc1 = x.up.r[3] / OCN_MD(OCN_DXT, 2), qe = x.vp.r[2] / dyt;
+        const double st = D(x.met(OCN_DX + kNumRowFields + 0, 1)) * (qa - shz(qa, -1))
+                          - D(x.met(OCN_DX + kNumRowFields + 1, 1)) * (qb - x.qb);
+        const double ss = D(x.met(OCN_DX + kNumRowFields + 2, 1)) * (qc1 - x.qc)
+                          + D(x.met(OCN_DX + kNumRowFields + 3, 1)) * (shz(qe, 1) - qe);
         x.qb = qb;
         x.qc = qc1;
         const unsigned bc = x.bits.r[2];
@@ -1054,30 +1064,111 @@ template <bool P2> struct MarchStep {
         const bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
         const bool llu = hh_rng && (bc & (1u << OCN_LLU)), llv = hh_rng && (bc & (1u << OCN_LLV)),
                    luh = hh_rng && (bc & (1u << OCN_LUH));
-        x.hu.r[2] = llu ? u0 : ld(t.f(OCN_HHU), c);
+        const double hu = llu ? u0 : ld(t.f(OCN_HHU), c);
+        const double hv = llv ? v0 : ld(t.f(OCN_HHV), c);
+        const double hh = luh ? h0 : ld(t.f(OCN_HHH), c);
+        const double vt = in && (bc & (1u << OCN_LUU)) ? vort : ld(t.f(OCN_VORT), c);
+        const double stt = in && (bc & (1u << OCN_LU)) ? st : ld(t.f(OCN_STR_T), c);
+        x.hu.r[2] = hu; x.hv.r[2] = hv; x.hh.r[2] = hh; x.vort.r[2] = vt; x.stt.r[2] = stt;
         x.hu1.r[2] = llu ? u1 : ld(t.f(OCN_HHU_P), c);
-        x.hv.r[2] = llv ? v0 : ld(t.f(OCN_HHV), c);
         x.hv1.r[2] = llv ? v1 : ld(t.f(OCN_HHV_P), c);
-        x.hh.r[2] = luh ? h0 : ld(t.f(OCN_HHH), c);
-        x.vort.r[2] = in && (bc & (1u << OCN_LUU)) ? vo : ld(t.f(OCN_VORT), c);
-        x.stt.r[2] = in && (bc & (1u << OCN_LU)) ? st : ld(t.f(OCN_STR_T), c);
         x.sts.r[2] = in && (bc & (1u << OCN_LUU)) ? ss : ld(t.f(OCN_STR_S), c);
+        // shared products of row r (S reads them at m +- 1 and at rows n-1 .. n+1); each is the
+        // reference's sub-expression with the same operands in the same order
+        x.pu.r[2] = u_0 * dyh * hu;                                  // uv_trans: u * dyh * hu
+        x.pv.r[2] = v_0 * dxh * hv;                                  // uv_trans: v * dxh * hv
+        x.vh.r[2] = vt * hh;                                         // uv_trans: vort * hh
+        x.t3.r[2] = v_0 * hv * dxh;                                  // sw_update_ssh: vbrtr * hhv * dxh
+        const double rr = D(x.met(OCN_RLH_S, 1)) * hh * dxb * dyb;   // sw_update_uv: rlh_s * hhh * dxb * dyb
+        x.rr.r[2] = rr;
+        x.cx.r[2] = rr * (v_r + v_0);                                //   ... * (vbrtr(1,0) + vbrtr)
+        const double hq = x.hr.r[2] + x.ssh.r[2] * x.f;              // depth.f90:48 hq = h_r + sh*ffs
+        const float gy = x.met(OCN_DY, 1), gx = x.met(OCN_DX, 1);
+        x.dt.r[2] = D(gy * gy) * x.mu.r[2] * hq * stt;               // uv_diff2: dy**2 * mu * hq * str_t
+        x.dxq.r[2] = D(gx * gx) * x.mu.r[2] * hq * stt;              // uv_diff2: dx**2 * mu * hq * str_t
     }
 
-    // S at row n: a1, fused B, a8's filters, check_ssh_err
+    // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
+    // uv_trans_math, uv_diff2_math, sw_update_uv_math written out over the shared products)
     __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n) const
     {
-        const StepView<0, P2> s{x};
         const Geo I = geo(&b);
         const Pt c = I(L.m, n);
-        const double sshn = sw_update_ssh_math(s);
-        double rxa, rya, rxd, ryd, un, vn;
-        uv_trans_math(s, rxa, rya);
-        uv_diff2_math(s, rxd, ryd);
-        sw_update_uv_math(s, rxa, rxd, rya, ryd, un, vn);
+        const double u = x.u.r[1], v = x.v.r[1], hu = x.hu.r[1], hv = x.hv.r[1], hh = x.hh.r[1];
+        const double dxt = OCN_MD(OCN_DXT, 0), dyt = OCN_MD(OCN_DYT, 0), dxh = OCN_MD(OCN_DXH, 0),
+                     dyh = OCN_MD(OCN_DYH, 0);
+        // a1 sw_update_ssh (vel_ssh.f90:69-106)
+        const double t1 = u * hu * dyh;
+        const float area = x.met(OCN_DX, 0) * x.met(OCN_DY, 0);
+        const double sshn = x.shp.r[1] + 2.0 * x.tau * (-((t1 - shz(t1, -1) + x.t3.r[1] - x.t3.r[0]) / D(area)));
+        // a4 uv_trans (vel_ssh.f90:283-373)
+        const double u_r = shz(u, 1), u_l = shz(u, -1), u_n = x.u.r[2], u_s = x.u.r[0];
+        const double v_r = shz(v, 1), v_l = shz(v, -1), v_n = x.v.r[2], v_s = x.v.r[0];
+        const double pu = x.pu.r[1], pun = x.pu.r[2], pv = x.pv.r[1], pvn = x.pv.r[2], pvs = x.pv.r[0];
+        const double luu = D(x.mk(OCN_LUU, 0, 0)), luus = D(x.mk(OCN_LUU, 0, -1));
+        double rxa, rya;
+        {
+            const double fx_p = (pu + shz(pu, 1)) / 2.0 * (u + u_r) / 2.0;
+            const double fx_m = (pu + shz(pu, -1)) / 2.0 * (u + u_l) / 2.0;
+            const double fy_p = (pv + shz(pv, 1)) / 2.0 * (u_n + u) / 2.0 * luu;
+            const double fy_m = (pvs + shz(pvs, 1)) / 2.0 * (u_s + u) / 2.0 * luus;
+            rxa = -(fx_p - fx_m + fy_p - fy_m) + (x.vh.r[1] * (v_r + v) + x.vh.r[0] * (shz(v_s, 1) + v_s)) / 4.0;
+        }
+        {
+            const double fy_p = (pv + pvn) / 2.0 * (v + v_n) / 2.0;
+            const double fy_m = (pv + pvs) / 2.0 * (v + v_s) / 2.0;
+            const double sn = pu + pun;
+            const double fx_p = sn / 2.0 * (v_r + v) / 2.0;
+            const double fx_m = shz(sn, -1) / 2.0 * (v_l + v) / 2.0;
+            const double q = x.vh.r[1] * (u_n + u);
+            rya = -(fx_p - fx_m + fy_p - fy_m) - (q + shz(q, -1)) / 4.0;
+        }
+        // a6 uv_diff2 (vel_ssh.f90:375-452)
+        double rxd, ryd;
+        {
+            const double mu = x.mu.r[1], mu_r = shz(mu, 1), mu_l = shz(mu, -1), mu_n = x.mu.r[2], mu_s = x.mu.r[0];
+            const double muh_p = (mu + mu_r + mu_n + shz(mu_n, 1)) / 4.0;
+            const double muh_m = (mu + mu_r + mu_s + shz(mu_s, 1)) / 4.0;
+            const double muh_m2 = (mu + mu_l + mu_n + shz(mu_n, -1)) / 4.0;
+            const float gxb = x.met(OCN_DXB, 0), gxbm = x.met(OCN_DXB, -1), gyb = x.met(OCN_DYB, 0);
+            const float dxb2 = gxb * gxb, dxb2m = gxbm * gxbm, dyb2 = gyb * gyb;
+            const double sts = x.sts.r[1];
+            const double dtc = x.dt.r[1];
+            rxd = (shz(dtc, 1) - dtc) / dyh
+                  + (D(dxb2) * muh_p * hh * sts - D(dxb2m) * muh_m * x.hh.r[0] * x.sts.r[0]) / dxt;
+            ryd = -(x.dxq.r[2] - x.dxq.r[1]) / dxh
+                  + (D(dyb2) * muh_p * hh * sts - D(dyb2) * muh_m2 * shz(hh, -1) * shz(sts, -1)) / dyt;
+        }
+        // a7 sw_update_uv (vel_ssh.f90:108-195); hun = hu, hvn = hv (the reuse identity)
+        double un, vn;
+        {
+            const double g = D(OCN_FREE_FALL_ACC);
+            const double ssh = x.ssh.r[1];
+            const float rdis = x.met(OCN_R_DISS, 0), rdisn = x.met(OCN_R_DISS, 1);
+            {
+                const double bp = qtau(x, hu * dxt * dyh / 2.0);
+                const double bp0 = qtau(x, x.hu1.r[1] * dxt * dyh / 2.0);
+                const double slx = -(g * (shz(ssh, 1) - ssh) * dyh * hu);
+                const float rd = rdis + rdis;
+                const double fric = D(rd) / 2.0 * x.up.r[1] * dxt * dyh * hu;
+                const double grx = x.rhsx + slx + rxd + rxa - fric + (x.cx.r[1] + x.cx.r[0]) / 4.0;
+                un = (x.up.r[1] * bp0 + grx) / (bp);
+            }
+            {
+                const double bp = qtau(x, hv * dyt * dxh / 2.0);
+                const double bp0 = qtau(x, x.hv1.r[1] * dyt * dxh / 2.0);
+                const double sly = -(g * (x.ssh.r[2] - ssh) * dxh * hv);
+                const float rd = rdis + rdisn;
+                const double fric = D(rd) / 2.0 * x.vp.r[1] * dxh * dyt * hv;
+                const double c1 = x.rr.r[1] * (u_n + u);
+                const double gry = x.rhsy + sly + ryd + rya - fric - (c1 + shz(c1, -1)) / 4.0;
+                vn = (x.vp.r[1] * bp0 + gry) / (bp);
+            }
+        }
+        // a8 sw_next_step's filters (vel_ssh.f90:197-245) + check_ssh_err (vel_ssh.f90:40-67)
         const double ts = sw.time_smooth;
         const double fx = asselin(x.ssh.r[1], sshn, x.shp.r[1], ts);
-        const double fa = asselin(x.u.r[1], un, x.up.r[1], ts), fb = asselin(x.v.r[1], vn, x.vp.r[1], ts);
+        const double fa = asselin(u, un, x.up.r[1], ts), fb = asselin(v, vn, x.vp.r[1], ts);
         if (!L.out) return;
         const unsigned bc = x.bits.r[1];
         if (bc & (1u << OCN_LU)) {
@@ -1098,7 +1189,7 @@ template <bool P2> struct MarchStep {
         x.f = (double)sw.full_free_surface;
         // iteration n computes D(n+1) and, from n = nb on, S(n); two warm iterations give D(nb-1)
         // and D(nb).  Before iteration n0 = nb - 2 the rows it does not load itself: up, ssh, sshp,
-        // h_r, bits at n0+1; vp at n0; metric rows n0, n0+1.
+        // h_r, bits at n0+1; vp at n0; metric rows n0, n0+1; the weights of row n0+1.
         const int n0 = nb - 2;
         {
             const Pt c = I(L.m, n0), c1 = I(L.m, n0 + 1);
@@ -1113,19 +1204,20 @@ template <bool P2> struct MarchStep {
             // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
             x.qb = x.vp.r[1] / D(x.g[OCN_DXH - OCN_DX][1]);
             x.qc = x.up.r[2] / D(x.g[OCN_DXT - OCN_DX][2]);
+            weights(x, 1);
         }
-        Batch cur, nxt;
-        load(cur, L.m, n0);
+        Batch q;
+        load(q, L.m, n0);
         for (int n = n0; n <= ne; ++n) {
-            take(x, cur);
-            if (n < ne) load(nxt, L.m, n + 1);   // in flight while this row is computed
+            take(x, q);
+            if (n < ne) load(q, L.m, n + 1);   // in flight while this row is computed
             derive(x, L.m, n + 1);
             if (n >= nb) step(x, L, n);      // wave-uniform
             x.rotate();
-            cur = nxt;
         }
     }
 };
+#undef OCN_MD
 
 #define CHECK(...)                                                \
     do {                                                          \
