@@ -202,9 +202,15 @@ struct MetRows {
             g[k][2] = ld(rows, (unsigned)k * nrows + r_cur);
         }
     }
+    // The row tables are read-only while any step kernel runs: read them through the constant
+    // address space, so the wave-uniform loads are scalar (s_load, lgkmcnt) and never wait
+    // behind the vector loads of the rows in flight.
     __device__ __forceinline__ static void load(float *q, const float *rows, unsigned nrows, unsigned r)
     {
-        for (int k = 0; k < kRowTable; ++k) q[k] = ld(rows, (unsigned)k * nrows + r);
+        typedef const __attribute__((address_space(4))) float cfloat;
+        const cfloat *t = (const cfloat *)rows;
+        r = __builtin_amdgcn_readfirstlane(r);
+        for (int k = 0; k < kRowTable; ++k) q[k] = t[(unsigned)k * nrows + r];
     }
 };
 #define OCN_MV(name, reg) \
@@ -899,7 +905,7 @@ template <bool HH, bool SKIP> struct MarchCA {
 #define OCN_STEP_ROWS 32   // rows per wave tile of the one-pass step (2 warm rows per tile)
 #endif
 #ifndef OCN_STEP_WAVES
-#define OCN_STEP_WAVES 2   // waves per SIMD asked of the register allocator
+#define OCN_STEP_WAVES 1   // waves per SIMD asked of the register allocator (2 spills)
 #endif
 // A whole role-flip step in one register march (ocn_ctx.hip one_step_fused, "one-pass" steps of
 // a single-block call): the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp; h_r, mu, RHSx, RHSy)
@@ -1022,12 +1028,37 @@ template <bool P2> struct MarchStep {
         x.w1.r[k] = (x.hr.r[k] + x.shp.r[k] * x.f) * gx * gy * l;
     }
 
+    // Where D takes the value in memory (mask 0 or outside the stage's range): those loads, issued
+    // (exec-masked) one iteration ahead, for row r = n + 2 (its mask byte arrives with that row),
+    // so that nothing in an iteration waits for the loads the iteration itself issues
+    struct Fallback {
+        bool llu, llv, luh, vt, st, ss;   // the computed value is used
+        double hu, hv, hh, hu1, hv1, vort, stt, sts;
+    };
+    __device__ __forceinline__ void fallback(const StepRegs &x, Fallback &f, int m, int r, int slot) const
+    {
+        const Pt c = geo(&b)(m, r);
+        const unsigned bc = x.bits.r[slot];
+        const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && r >= b.ny_start - 1 && r <= b.ny_end;
+        const bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
+        f.llu = hh_rng && (bc & (1u << OCN_LLU));
+        f.llv = hh_rng && (bc & (1u << OCN_LLV));
+        f.luh = hh_rng && (bc & (1u << OCN_LUH));
+        f.vt = in && (bc & (1u << OCN_LUU));
+        f.st = in && (bc & (1u << OCN_LU));
+        f.ss = f.vt;
+        f.hu = f.hv = f.hh = f.hu1 = f.hv1 = f.vort = f.stt = f.sts = 0.0;
+        if (!f.llu) { f.hu = ld(t.f(OCN_HHU), c); f.hu1 = ld(t.f(OCN_HHU_P), c); }
+        if (!f.llv) { f.hv = ld(t.f(OCN_HHV), c); f.hv1 = ld(t.f(OCN_HHV_P), c); }
+        if (!f.luh) f.hh = ld(t.f(OCN_HHH), c);
+        if (!f.vt) { f.vort = ld(t.f(OCN_VORT), c); f.sts = ld(t.f(OCN_STR_S), c); }
+        if (!f.st) f.stt = ld(t.f(OCN_STR_T), c);
+    }
+
     // D at row r = n + 1 of this lane (column m): the values the reference's arrays hold there,
     // plus the shared products of that row
-    __device__ __forceinline__ void derive(StepRegs &x, int m, int r) const
+    __device__ __forceinline__ void derive(StepRegs &x, const Fallback &fb) const
     {
-        const Geo I = geo(&b);
-        const Pt c = I(m, r);
         weights(x, 2);   // row n+2 (rows n+1's were formed one iteration ago)
         // hh_init levels 0 and 1 (depth.f90:52-97, sw_stencils.h interp_u / interp_v / interp_h)
         const float l00 = x.mk(OCN_LU, 0, 1), l10 = x.mk(OCN_LU, 1, 1), l01 = x.mk(OCN_LU, 0, 2),
@@ -1059,20 +1090,15 @@ template <bool P2> struct MarchStep {
                           + D(x.met(OCN_DX + kNumRowFields + 3, 1)) * (shz(qe, 1) - qe);
         x.qb = qb;
         x.qc = qc1;
-        const unsigned bc = x.bits.r[2];
-        const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && r >= b.ny_start - 1 && r <= b.ny_end;
-        const bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
-        const bool llu = hh_rng && (bc & (1u << OCN_LLU)), llv = hh_rng && (bc & (1u << OCN_LLV)),
-                   luh = hh_rng && (bc & (1u << OCN_LUH));
-        const double hu = llu ? u0 : ld(t.f(OCN_HHU), c);
-        const double hv = llv ? v0 : ld(t.f(OCN_HHV), c);
-        const double hh = luh ? h0 : ld(t.f(OCN_HHH), c);
-        const double vt = in && (bc & (1u << OCN_LUU)) ? vort : ld(t.f(OCN_VORT), c);
-        const double stt = in && (bc & (1u << OCN_LU)) ? st : ld(t.f(OCN_STR_T), c);
+        const double hu = fb.llu ? u0 : fb.hu;
+        const double hv = fb.llv ? v0 : fb.hv;
+        const double hh = fb.luh ? h0 : fb.hh;
+        const double vt = fb.vt ? vort : fb.vort;
+        const double stt = fb.st ? st : fb.stt;
         x.hu.r[2] = hu; x.hv.r[2] = hv; x.hh.r[2] = hh; x.vort.r[2] = vt; x.stt.r[2] = stt;
-        x.hu1.r[2] = llu ? u1 : ld(t.f(OCN_HHU_P), c);
-        x.hv1.r[2] = llv ? v1 : ld(t.f(OCN_HHV_P), c);
-        x.sts.r[2] = in && (bc & (1u << OCN_LUU)) ? ss : ld(t.f(OCN_STR_S), c);
+        x.hu1.r[2] = fb.llu ? u1 : fb.hu1;
+        x.hv1.r[2] = fb.llv ? v1 : fb.hv1;
+        x.sts.r[2] = fb.ss ? ss : fb.sts;
         // shared products of row r (S reads them at m +- 1 and at rows n-1 .. n+1); each is the
         // reference's sub-expression with the same operands in the same order
         x.pu.r[2] = u_0 * dyh * hu;                                  // uv_trans: u * dyh * hu
@@ -1206,14 +1232,18 @@ template <bool P2> struct MarchStep {
             x.qc = x.up.r[2] / D(x.g[OCN_DXT - OCN_DX][2]);
             weights(x, 1);
         }
+        Fallback fb, fbn;
+        fallback(x, fb, L.m, n0 + 1, 2);
         Batch q;
         load(q, L.m, n0);
         for (int n = n0; n <= ne; ++n) {
             take(x, q);
-            if (n < ne) load(q, L.m, n + 1);   // in flight while this row is computed
-            derive(x, L.m, n + 1);
+            if (n < ne) fallback(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
+            if (n < ne) load(q, L.m, n + 1);              // in flight while this row is computed
+            derive(x, fb);
             if (n >= nb) step(x, L, n);      // wave-uniform
             x.rotate();
+            fb = fbn;
         }
     }
 };
