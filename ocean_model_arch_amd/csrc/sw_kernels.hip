@@ -905,7 +905,7 @@ template <bool HH, bool SKIP> struct MarchCA {
 #define OCN_STEP_ROWS 32   // rows per wave tile of the one-pass step (2 warm rows per tile)
 #endif
 #ifndef OCN_STEP_WAVES
-#define OCN_STEP_WAVES 1   // waves per SIMD asked of the register allocator (2 spills)
+#define OCN_STEP_WAVES 2   // waves per SIMD asked of the register allocator
 #endif
 // A whole role-flip step in one register march (ocn_ctx.hip one_step_fused, "one-pass" steps of
 // a single-block call): the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp; h_r, mu, RHSx, RHSy)
