@@ -960,10 +960,16 @@ struct StepRegs {
     // products shared between lanes / rows (each the reference's own sub-expression, see derive)
     Win<double> w0, w1;               // interp weights ((h * dx) * dy) * lu of levels 0 / 1 (rows n+1, n+2)
     Win<double> pu, pv, vh, t3, cx, rr, dt, dxq;
-    float g[kRowTable][4];            // metric rows n-1 .. n+2 (wave-uniform)
+    // metric rows: read where used, as wave-uniform scalar loads from the (read-only) row table
+    // through the constant address space -- no table of 4 rows x 14 values held in SGPRs
+    const __attribute__((address_space(4))) float *rows;
+    unsigned nrows, rn;               // table stride, row index of n (n - bnd_y1)
     double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
     double tau, inv_tau, f;
-    __device__ __forceinline__ float met(int id, int dy) const { return g[id - OCN_DX][dy + 1]; }
+    __device__ __forceinline__ float met(int id, int dy) const
+    {
+        return rows[(unsigned)(id - OCN_DX) * nrows + __builtin_amdgcn_readfirstlane(rn + dy)];
+    }
     __device__ __forceinline__ float mk(int id, int dx, int dy) const
     {
         return (bits.at(dx, dy) >> id) & 1u ? 1.0f : 0.0f;
@@ -975,7 +981,7 @@ struct StepRegs {
         hu.rotate(); hv.rotate(); hh.rotate(); hu1.rotate(); hv1.rotate(); vort.rotate(); stt.rotate(); sts.rotate();
         w0.rotate(); w1.rotate(); pu.rotate(); pv.rotate(); vh.rotate(); t3.rotate(); cx.rotate(); rr.rotate();
         dt.rotate(); dxq.rotate();
-        for (int k = 0; k < kRowTable; ++k) { g[k][0] = g[k][1]; g[k][1] = g[k][2]; g[k][2] = g[k][3]; }
+        ++rn;
     }
 };
 
@@ -994,7 +1000,7 @@ template <bool P2> struct MarchStep {
     __device__ __forceinline__ double qtau(const StepRegs &x, double a) const { return P2 ? a * x.inv_tau : a / x.tau; }
 
     // one row's loads for iteration n (rows of the state the march adds)
-    struct Batch { double u, v, up, vp, ssh, shp, hr, mu, rhsx, rhsy; unsigned bits; float g[kRowTable]; };
+    struct Batch { double u, v, up, vp, ssh, shp, hr, mu, rhsx, rhsy; unsigned bits; };
     __device__ __forceinline__ void load(Batch &q, int m, int n) const
     {
         const Geo I = geo(&b);
@@ -1004,7 +1010,6 @@ template <bool P2> struct MarchStep {
         q.bits = ld(t.bits, c2);
         q.v = ld(t.f(OCN_VBRTR), c1); q.vp = ld(t.f(OCN_VBRTRP), c1); q.mu = ld(t.f(OCN_MU), c1);
         q.rhsx = ld(t.f(OCN_RHSX), c); q.rhsy = ld(t.f(OCN_RHSY), c);
-        MetRows::load(q.g, t.rows, t.nrows, c2.r);
     }
     __device__ __forceinline__ static void take(StepRegs &x, const Batch &q)
     {
@@ -1012,7 +1017,6 @@ template <bool P2> struct MarchStep {
         x.bits.r[3] = q.bits;
         x.v.r[2] = q.v; x.vp.r[2] = q.vp; x.mu.r[2] = q.mu;
         x.rhsx = q.rhsx; x.rhsy = q.rhsy;
-        for (int k = 0; k < kRowTable; ++k) x.g[k][3] = q.g[k];
     }
 
     // hh_init's interpolation weights of row n + dy (slot dy + 1): interp_wt(h) = h * dx * dy * lu
@@ -1210,6 +1214,9 @@ template <bool P2> struct MarchStep {
     {
         const Geo I = geo(&b);
         StepRegs x{};
+        x.rows = (const __attribute__((address_space(4))) float *)t.rows;
+        x.nrows = t.nrows;
+        x.rn = (unsigned)(nb - 2 - b.bnd_y1);   // row n0
         x.tau = tau;
         x.inv_tau = 1.0 / tau;
         x.f = (double)sw.full_free_surface;
@@ -1223,13 +1230,9 @@ template <bool P2> struct MarchStep {
             x.shp.r[2] = ld(t.f(OCN_SSHP), c1); x.hr.r[2] = ld(t.f(OCN_HHQ_REST), c1);
             x.bits.r[2] = ld(t.bits, c1); x.u.r[2] = ld(t.f(OCN_UBRTR), c1);
             x.vp.r[1] = ld(t.f(OCN_VBRTRP), c);
-            for (int k = 0; k < kRowTable; ++k) {
-                x.g[k][1] = ld(t.rows, (unsigned)k * t.nrows + c.r);
-                x.g[k][2] = ld(t.rows, (unsigned)k * t.nrows + c1.r);
-            }
             // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
-            x.qb = x.vp.r[1] / D(x.g[OCN_DXH - OCN_DX][1]);
-            x.qc = x.up.r[2] / D(x.g[OCN_DXT - OCN_DX][2]);
+            x.qb = x.vp.r[1] / D(x.met(OCN_DXH, 0));
+            x.qc = x.up.r[2] / D(x.met(OCN_DXT, 1));
             weights(x, 1);
         }
         Fallback fb, fbn;
