@@ -1373,6 +1373,23 @@ int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compac
     return launch_march_part(b, r, part, MarchCA<true, false>{*b, t, sw, tau_next}, s);
 }
 
+// The one-pass step's grid: OCN_STEP_VERT = the 4 waves of a workgroup take 4 consecutive row
+// tiles of one 60-column wave column (the rows a wave warms up with are its upper neighbour's,
+// in the same CU's L1); else 4 wave columns side by side.
+#ifndef OCN_STEP_VERT
+#define OCN_STEP_VERT 1
+#endif
+template <class Body> static int launch_step(const ocn_block *b, const Range &r, const Body &body, hipStream_t s)
+{
+    MarchGrid g{};
+    g.r[0] = march_rect<Body>(b, r, OCN_STEP_ROWS, OCN_STEP_VERT != 0);
+    g.nr = 1;
+    g.ntiles = g.r[0].tiles;
+    const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
+    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, body);
+    return check_launch();
+}
+
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s)
 {
@@ -1385,10 +1402,8 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
     const Range r = range_interior(b);
     int ex;
     if (std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020)   // tau = 2^k
-        return launch_march_rects(b, &r, 1, MarchStep<true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s,
-                                  OCN_STEP_ROWS);
-    return launch_march_rects(b, &r, 1, MarchStep<false>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s,
-                              OCN_STEP_ROWS);
+        return launch_step(b, r, MarchStep<true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
+    return launch_step(b, r, MarchStep<false>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy
