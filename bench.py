@@ -181,13 +181,17 @@ def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for):
     return bool(ok)
 
 
-def load_traffic(stage: str, cells: int, compact: bool):
-    """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary (profiles/), or None."""
+def load_traffic(amd, stage: str, cells: int, compact: bool, box, blocks):
+    """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, scripts/pmc_traffic.py), or None unless that summary was taken on
+    this exact library build (ocn_build_id) and workload (box, block grid, cells per block)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
         rec = d["kernels"][stage]
-        if int(rec["cells"]) != cells or bool(rec.get("compact")) != compact:
+        if (d.get("build_id") != amd.build_id() or list(d.get("box", [])) != list(box) or
+                list(d.get("blocks", [])) != list(blocks) or int(rec["cells"]) != cells or
+                bool(rec.get("compact")) != compact):
             return None
         return float(rec["hbm_bytes_per_launch"])
     except Exception:
@@ -213,6 +217,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=4096, help="box interior size (N x N)")
+    ap.add_argument("--basin", choices=["box", "bs", "bs_tr"], default="box",
+                    help="box: the synthetic N x N box; bs / bs_tr: the reference's Black Sea basin (data/BS mask "
+                         "and parameters, as stored in tests/golden), without / with the tracer (configs 1 and 5)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--graph", action="store_true", help="replay steps as hipGraphs (single process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -222,8 +229,9 @@ def main():
     ap.add_argument("--no-flip", action="store_true", help="standard steps only (no role-flip steps)")
     ap.add_argument("--no-recompute", action="store_true", help="role-flip calls without the recompute steps")
     ap.add_argument("--no-onepass", action="store_true", help="role-flip calls without the one-pass steps")
-    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
-                    help="halo exchanges beside inner launches: 0 never, 1 standard steps, 2 role-flip steps too")
+    ap.add_argument("--overlap", type=int, default=-1, choices=[-1, 0, 1, 2],
+                    help="halo exchanges beside inner launches: 0 never, 1 standard steps, 2 role-flip steps too, "
+                         "-1 the library default (2 with RCCL peers, else 1)")
     ap.add_argument("--blocks", default=None,
                     help="block grid BXxBY (default: one block per GPU); with one GPU, several blocks on it "
                          "exercise the halo-exchange path without RCCL")
@@ -250,9 +258,20 @@ def main():
         if world > 1 and bx * by != world:
             raise SystemExit("--blocks with several GPUs must give one block per GPU")
     n = args.n
-    nxbox, nybox = (n, n) if args.scaling == "strong" else (n * bx, n * by)
-    basin = amd.BasinConfig(nx=nxbox + 4, ny=nybox + 4)
-    model = amd.OceanModel(basin, amd.SWConfig(), amd.ParallelConfig(bx, by), rank=rank, nranks=world,
+    if args.basin == "box":
+        nxbox, nybox = (n, n) if args.scaling == "strong" else (n * bx, n * by)
+        basin, sw = amd.BasinConfig(nx=nxbox + 4, ny=nybox + 4), amd.SWConfig()
+        workload = f"{nxbox}x{nybox} box"
+    else:
+        # the Black Sea basin: mask bits and basin / sw.par parameters exactly as the reference's
+        # run uses them (input data of the golden fixture; nothing of the reference runs here)
+        from tests.golden import cases
+        case = cases.load_e2e("bs_b1x1_s60" if args.basin == "bs" else "bs_b4x2_tr_s60")
+        basin = amd.BasinConfig(**case["basin"], mask=case["mask"])
+        sw = amd.SWConfig(**case["sw"])
+        nxbox, nybox = case["basin"]["nx"] - 4, case["basin"]["ny"] - 4
+        workload = f"Black Sea basin {nxbox}x{nybox}" + (" + tracer" if args.basin == "bs_tr" else "")
+    model = amd.OceanModel(basin, sw, amd.ParallelConfig(bx, by), rank=rank, nranks=world,
                            device=local_rank)
     parity = None
     if world > 1:
@@ -294,6 +313,7 @@ def main():
     flip = model.flip_active
     rc = model.recompute_active
     one = model.onepass_active
+    model_overlap = model.overlap_level
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -309,29 +329,33 @@ def main():
         b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring, one)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
-        if stage_ms:
-            dom = max(stage_ms, key=lambda s: stage_ms[s])
+        if stage_ms:   # the dominant kernel: the most device time over the timed steps
+            dom = max(stage_ms, key=lambda s: times[s][0])
             alg = kbytes[dom] * local_cells
             achieved = alg / (stage_ms[dom] * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": load_traffic(dom, local_cells, compact),
+                    "traffic": load_traffic(amd, dom, local_cells, compact, [nxbox, nybox], [bx, by]),
                     "alg_bytes_per_launch": int(alg), "launch_ms": round(stage_ms[dom], 4)}
         step_gbs = B_ALG * cells * args.steps / dt / 1e9 / world
         moved = b_path * cells * args.steps / dt / 1e9 / world
         out = {"metric": METRIC, "value": value, "unit": "cell-updates/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
                "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
-               "data": "synthetic (Gaussian SSH hump in a closed flat-bottom box, SURVEY.md 8d)",
-               "config": {"workload": f"{nxbox}x{nybox} box, {bx}x{by} blocks ({bx * by // world} per GPU), sw.par defaults, "
-                                      f"tau=1s",
+               "data": ("synthetic (Gaussian SSH hump in a closed flat-bottom box, SURVEY.md 8d)" if args.basin == "box"
+                        else "the reference's data/BS mask and basin parameters, its Gaussian initial state"),
+               "config": {"workload": f"{workload}, {bx}x{by} blocks ({bx * by // world} per GPU), "
+                                      f"{'sw.par defaults' if args.basin == 'box' else 'BS sw.par'}, tau=1s",
+                          "basin": args.basin,
                           "box": [nxbox, nybox], "blocks": [bx, by], "graph": bool(args.graph),
                           "step": "reference stages" if args.stages else "fused groups",
                           "static_fields": "compact" if compact else "2-D arrays",
                           "march": bool(compact and not args.stages and not args.no_march),
                           "role_flip_steps": flip, "recompute_steps": rc, "onepass_steps": one,
+                          "overlap": model_overlap,
                           "parallelism": (f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else
                                           "1 block" if bx * by == 1 else f"{bx}x{by} blocks, local halo copies")},
+               "build_id": amd.build_id(),
                "roofline": roof,
                "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),
                "step_alg_gbs_per_gpu": round(step_gbs, 1),

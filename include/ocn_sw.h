@@ -292,9 +292,11 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
 
 /* Execution options.
  *  OCN_OPT_GRAPH: replay each step as one hipGraph (single-process runs).
- *  OCN_OPT_OVERLAP (default 1): with halo exchanges, run each exchange on a second stream beside
- *  the launches' inner parts (points that neither read halos nor feed the exchange): 1 = in the
- *  standard steps, 2 = in the role-flip steps too, 0 = never (same results bit for bit).
+ *  OCN_OPT_OVERLAP (default -1 = auto): with halo exchanges, run each exchange on a second stream
+ *  beside the launches' inner parts (points that neither read halos nor feed the exchange): 1 = in
+ *  the standard steps, 2 = in the role-flip steps too, 0 = never (same results bit for bit); auto
+ *  is 2 when the context exchanges with other ranks (RCCL or loopback attached, nranks > 1), else
+ *  1.  ocn_ctx_get_option returns the level in effect.
  *  OCN_OPT_STAGE_TIMING: bracket every launch group with HIP events on the context stream.
  *  OCN_OPT_FUSED (default 1): ocn_ctx_step runs the step as 4 fused launch groups and 3 halo
  *  syncs (same results and final state bit for bit); 0 = the 11 envoke stages of the reference.
@@ -342,6 +344,9 @@ int ocn_ctx_stage_times(ocn_ctx *ctx, double *ms, int64_t *counts);
 
 const char *ocn_last_error(void);
 int ocn_abi_version(void);
+/* Build id: a hash of the library's sources and compile flags (Makefile), e.g. to tie a
+ * profile taken on one build to the library that is loaded. */
+const char *ocn_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -85,7 +85,8 @@ KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "oc
 CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
                "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm", "ocn_ctx_attach_loopback",
                "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
-               "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version"]
+               "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version",
+               "ocn_build_id"]
 ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
 
 
@@ -168,6 +169,7 @@ def lib() -> C.CDLL:
     for name in ALL_SYMBOLS:
         getattr(L, name)
     L.ocn_last_error.restype = C.c_char_p
+    L.ocn_build_id.restype = C.c_char_p
     L.ocn_ctx_field.restype = C.c_void_p
     L.ocn_ctx_field.argtypes = [C.c_void_p, C.c_int, C.c_int]
     L.ocn_ctx_stream.restype = C.c_void_p
@@ -196,6 +198,11 @@ def lib() -> C.CDLL:
                                     C.c_int32, C.POINTER(OcnHaloMsg), C.c_int32, C.POINTER(C.c_int32)]
     _lib = L
     return L
+
+
+def build_id() -> str:
+    """ocn_build_id(): hash of the loaded library's sources and compile flags."""
+    return lib().ocn_build_id().decode()
 
 
 def check(rc: int, what: str = ""):

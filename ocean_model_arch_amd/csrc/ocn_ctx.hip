@@ -251,7 +251,7 @@ struct ocn_ctx {
     hipStream_t stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchanges overlapped with interior compute
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int overlap = 1;             // OCN_OPT_OVERLAP: 0 none, 1 standard steps, 2 + role-flip steps
+    int overlap = -1;            // OCN_OPT_OVERLAP: 0 none, 1 standard steps, 2 + role-flip steps, -1 auto
     int32_t *d_nbad = nullptr;
     ncclComm_t comm = nullptr;
     Loopback *lb = nullptr;            // test transport between contexts of one process (ocn_ctx_attach_loopback)
@@ -602,6 +602,14 @@ static int nccl_rc(ncclResult_t r, const char *what)
 }
 
 static bool has_comm(const ocn_ctx *c) { return c->comm || c->lb; }
+// OCN_OPT_OVERLAP in effect: by default (-1) the role-flip steps' exchanges overlap their inner
+// launches (2) when exchanges go to other ranks (RCCL: latency, not copy bandwidth), and run
+// between the launches (1) when every exchange is a local device copy -- there the frame bands
+// cost as much as the copies they hide
+static int overlap_level(const ocn_ctx *c)
+{
+    return c->overlap >= 0 ? c->overlap : has_comm(c) && c->dec.nranks > 1 ? 2 : 1;
+}
 
 // a rank of a loopback group that fails releases its peers' waits at once
 static int lb_fail_on_error(ocn_ctx *c, int rc)
@@ -1132,9 +1140,9 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         //   [A.frame | fork: sync A || A.inner] B.inner | join | B.frame | fork: sync B || swap,
         //   CA.inner | join | ring launch (the roles before the swap) | CA.frame | fork: sync CA
         //   || the next step's B.inner ...
-        // Off by default: the frame bands cost about as much as a local exchange (measured on one
-        // GPU with 2x2 / 4x2 blocks: 1.61 vs 1.47, 1.89 vs 1.69 ms per step).
-        const bool ov = c->overlap >= 2 && has_exchange(c) && !c->capturing;
+        // The default (overlap_level) with remote peers; off with only local copies, whose cost
+        // the frame bands match (one GPU, 2x2 / 4x2 blocks: 1.61 vs 1.47, 1.89 vs 1.69 ms per step).
+        const bool ov = overlap_level(c) >= 2 && has_exchange(c) && !c->capturing;
         if (!k.a_done) {
             RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
             if (ov) {
@@ -1205,7 +1213,7 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         }
         return OCN_OK;
     }
-    if (!(c->overlap && has_exchange(c))) {
+    if (!(overlap_level(c) && has_exchange(c))) {
         RC(join_sync(c));
         if (!k.a_done) {   // else fused A and its sync ran with the previous step's hh_init
             RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
@@ -1495,6 +1503,10 @@ extern "C" {
 
 const char *ocn_last_error(void) { return g_last_error.c_str(); }
 int ocn_abi_version(void) { return OCN_ABI_VERSION; }
+#ifndef OCN_BUILD_ID
+#define OCN_BUILD_ID "unknown"
+#endif
+const char *ocn_build_id(void) { return OCN_BUILD_ID; }
 
 int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_decomp *dec, const int32_t *mask,
                    ocn_ctx **out)
@@ -1941,7 +1953,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         return OCN_OK;
     case OCN_OPT_OVERLAP:
         if (c->overlap != value) drop_graphs(c);
-        c->overlap = value < 0 ? 0 : value > 2 ? 2 : (int)value;
+        c->overlap = value < 0 ? -1 : value > 2 ? 2 : (int)value;
         return OCN_OK;
     case OCN_OPT_MARCH:
         if (c->march != (value != 0)) drop_graphs(c);
@@ -1966,7 +1978,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_GRAPH: *value = c->use_graph; return OCN_OK;
     case OCN_OPT_STAGE_TIMING: *value = c->stage_timing; return OCN_OK;
     case OCN_OPT_FUSED: *value = c->fused; return OCN_OK;
-    case OCN_OPT_OVERLAP: *value = c->overlap; return OCN_OK;
+    case OCN_OPT_OVERLAP: *value = overlap_level(c); return OCN_OK;
     case OCN_OPT_COMPACT: *value = c->fused && c->compact; return OCN_OK;
     case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;

@@ -294,7 +294,25 @@ static MarchRect march_rect(const ocn_block *b, const Range &r, int rows = OCN_M
     return MarchRect{r.m0, r.m1, r.n0, r.n1, w0, ntx, ntx * nty, mlo, mhi, rows, vert ? 1 : 0};
 }
 
-// rows = rows per tile (0: OCN_MARCH_ROWS); vert: see MarchRect
+// Rows per wave tile for a range: `rows`, halved (not below OCN_MIN_ROWS) while the launch has
+// fewer waves than fill the chip (256 CUs x 4 SIMDs x 2 waves).  A march wave's rows are a
+// dependent chain of loads, so on small blocks (the Black Sea basin's 285 x 159, a 1024^2 box)
+// a launch of few long tiles is latency-bound; shorter tiles trade warm-up rows for waves.
+#ifndef OCN_FILL_WAVES
+#define OCN_FILL_WAVES 2048
+#endif
+#ifndef OCN_MIN_ROWS
+#define OCN_MIN_ROWS 2
+#endif
+template <typename Body> static int fit_rows(const Range &r, int rows)
+{
+    const int cols = Body::kAligned ? 64 : 64 - 2 * Body::kHalo;
+    const long wx = (r.m1 - r.m0 + cols) / cols + (Body::kAligned ? 1 : 0);
+    while (rows > OCN_MIN_ROWS && wx * ((r.n1 - r.n0 + rows) / rows) < OCN_FILL_WAVES) rows /= 2;
+    return rows < OCN_MIN_ROWS ? OCN_MIN_ROWS : rows;
+}
+
+// rows = rows per tile (0: OCN_MARCH_ROWS, fitted to the range); vert: see MarchRect
 template <typename Body>
 static int launch_march_rects(const ocn_block *b, const Range *rs, int nr, const Body &body, hipStream_t s,
                               int rows = 0, bool vert = false)
@@ -302,7 +320,8 @@ static int launch_march_rects(const ocn_block *b, const Range *rs, int nr, const
     MarchGrid g{};
     for (int i = 0; i < nr; ++i)
         if (!range_empty(rs[i])) {
-            g.r[g.nr] = march_rect<Body>(b, rs[i], rows > 0 ? rows : OCN_MARCH_ROWS, vert && i >= 2);
+            g.r[g.nr] = march_rect<Body>(b, rs[i], rows > 0 ? rows : fit_rows<Body>(rs[i], OCN_MARCH_ROWS),
+                                         vert && i >= 2);
             g.ntiles += g.r[g.nr].tiles;
             ++g.nr;
         }
@@ -1382,7 +1401,7 @@ int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compac
 template <class Body> static int launch_step(const ocn_block *b, const Range &r, const Body &body, hipStream_t s)
 {
     MarchGrid g{};
-    g.r[0] = march_rect<Body>(b, r, OCN_STEP_ROWS, OCN_STEP_VERT != 0);
+    g.r[0] = march_rect<Body>(b, r, fit_rows<Body>(r, OCN_STEP_ROWS), OCN_STEP_VERT != 0);
     g.nr = 1;
     g.ntiles = g.r[0].tiles;
     const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;

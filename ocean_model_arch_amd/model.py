@@ -116,6 +116,13 @@ class OceanModel:
         check(lib().ocn_ctx_init_state(self.ctx), "ocn_ctx_init_state")
         return self
 
+    @property
+    def overlap_level(self) -> int:
+        """OCN_OPT_OVERLAP in effect (auto resolved)."""
+        v = C.c_int64()
+        check(lib().ocn_ctx_get_option(self.ctx, _lib.OPT_OVERLAP, C.byref(v)), "ocn_ctx_get_option")
+        return int(v.value)
+
     def set_graph(self, on: bool = True):
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_GRAPH, int(on)), "ocn_ctx_set_option")
         return self
@@ -136,9 +143,10 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FUSED, int(on)), "ocn_ctx_set_option")
         return self
 
-    def set_overlap(self, on: int = 1):
+    def set_overlap(self, on: int = -1):
         """Overlap halo exchanges (comm stream) with the inner part of the fused launches: 1 = in
-        the standard steps (default), 2 = in the role-flip steps too, 0 = never."""
+        the standard steps, 2 = in the role-flip steps too, 0 = never, -1 = auto (the default:
+        2 with other ranks attached, else 1)."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_OVERLAP, int(on)), "ocn_ctx_set_option")
         return self
 

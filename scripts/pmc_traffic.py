@@ -1,13 +1,20 @@
 """HBM bytes per launch of the fused-step kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 over bench.py (scripts/pmc.sh), written as the JSON bench.py reads for roofline.traffic.
 
-    python scripts/pmc_traffic.py <pmc dir> <stenbench pmc dir> <cells> [--compact] > profiles/pmc_traffic.json
+    python scripts/pmc_traffic.py <pmc dir> <stenbench pmc dir> <cells> --box NXxNY --blocks BXxBY [--compact]
+        > profiles/pmc_traffic.json
+
+The JSON is stamped with the library's ocn_build_id() (run this on the tree that was profiled) and
+the workload (box, block grid, cells per block); bench.py reports roofline.traffic only when all
+of them match the run it is timing.
 
 FETCH_SIZE on gfx950 under-counts wide streaming reads (MI355X_MICROARCH.md 'HBM': half the
 bytes at 16 B/lane); our kernels read 8 B/lane.  The read scale is therefore calibrated on the
 stencil microbenchmark's pointwise kernel k_bench<0,0> (scripts/stenbench.hip), whose reads are
-exactly 20 arrays x 4094^2 x 8 B in the same 64 x 4-thread, 8-B-per-lane pattern.  WRITE_SIZE
-reads exactly for streaming stores.  Counter values are KiB."""
+exactly 20 arrays x 4094^2 x 8 B in the same 64 x 4-thread, 8-B-per-lane pattern; the write
+scale on the same kernel's 2 x 4094^2 x 8 B of stores (the guide calls WRITE_SIZE exact for
+16-B-per-lane stores only).  Counter values are KiB."""
+import argparse
 import csv
 import glob
 import json
@@ -17,7 +24,7 @@ import sys
 from collections import defaultdict
 
 STAGE = {"KFusedA": "fused_a", "KFusedB": "fused_b", "MarchFusedB": "fused_b", "KFusedC1": "fused_c1",
-         "KHhInit": "hh_init", "MarchHhInit": "hh_init", "MarchFusedA": "fused_a", "MarchCA": "fused_ca"}
+         "KHhInit": "hh_init", "MarchHhInit": "hh_init", "MarchFusedA": "fused_a", "MarchCA": "fused_ca", "MarchStep": "onepass"}
 
 
 def values(root):
@@ -34,14 +41,27 @@ def means(root):
 
 
 def main():
-    pmc, sten, cells = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    compact = "--compact" in sys.argv
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pmc")
+    ap.add_argument("sten")
+    ap.add_argument("cells", type=int)
+    ap.add_argument("--box", required=True)
+    ap.add_argument("--blocks", required=True)
+    ap.add_argument("--compact", action="store_true")
+    a = ap.parse_args()
+    pmc, sten, cells, compact = a.pmc, a.sten, a.cells, a.compact
     cal = [v for k, v in means(sten).items() if "k_bench<0, 0>" in k][0]
-    exact_read = 20 * 4094 * 4094 * 8.0
+    exact_read, exact_write = 20 * 4094 * 4094 * 8.0, 2 * 4094 * 4094 * 8.0
     scale = exact_read / cal["FETCH_SIZE"]
+    wscale = exact_write / cal["WRITE_SIZE"]
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from ocean_model_arch_amd._lib import build_id
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py; read scale {scale:.4f} "
-                     f"calibrated on stenbench k_bench<0,0> ({exact_read:.0f} B read exactly)",
-           "fetch_scale": scale, "kernels": {}}
+                     f"calibrated on stenbench k_bench<0,0> ({exact_read:.0f} B read exactly), write scale "
+                     f"{wscale:.4f} ({exact_write:.0f} B written)",
+           "build_id": build_id(), "box": [int(v) for v in a.box.lower().split("x")],
+           "blocks": [int(v) for v in a.blocks.lower().split("x")],
+           "fetch_scale": scale, "write_scale": wscale, "kernels": {}}
     # every dispatch of every template instance of a stage's kernel (e.g. MarchFusedB<true, true>
     # and <false, false>), averaged per dispatch like bench.py's per-launch timing
     agg = defaultdict(lambda: {"FETCH_SIZE": [], "WRITE_SIZE": [], "names": set()})
@@ -58,7 +78,7 @@ def main():
         if not d["FETCH_SIZE"] or not d["WRITE_SIZE"]:
             continue
         rd = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * scale
-        wr = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
+        wr = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * wscale
         out["kernels"][stage] = {"kernel": "/".join(sorted(d["names"])), "dispatches": len(d["WRITE_SIZE"]),
                                  "cells": cells, "compact": compact, "fetch_bytes": round(rd), "write_bytes": round(wr),
                                  "hbm_bytes_per_launch": round(rd + wr)}

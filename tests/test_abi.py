@@ -82,12 +82,14 @@ def test_field_ids_match_header():
     assert _lib.FIELD_ID["flux_x"] == 64 and _lib.FIELD_ID["flux_y"] == 65
     assert [_lib.FIELD_ID[n] for n in ("ff1_1", "ff1p_1", "ff1n_1", "ff1_2")] == [66, 67, 68, 69]
     assert _lib.FIELD_ID.name(71) == "ff1n_2"
-    assert len(_lib.TIMERS) == 11 + 3 + 3 + 1
+    assert len(_lib.TIMERS) == 11 + 3 + 3 + 2   # + fused_ca, onepass
 
 
 def test_abi_version_and_loud_failure_without_device(lib):
     import ocean_model_arch_amd as amd
-    assert lib.ocn_abi_version() == 2
+    assert lib.ocn_abi_version() == 3
+    bid = amd.build_id()
+    assert len(bid) == 16 and int(bid, 16) >= 0, bid   # Makefile: sha256 of sources + flags
     try:
         import torch
         has_gpu = torch.cuda.is_available()

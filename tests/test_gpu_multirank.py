@@ -73,10 +73,13 @@ def test_ranks_match_reference(amd, name, nranks, mode):
     models, flips = run_ranks_case(amd, case, nranks, **MODES[mode])
     try:
         bad = check_ranks(models, case, name)
+        levels = {m.overlap_level for m in models}
     finally:
         for m in models:
             m.close()
     assert not bad, f"{name} over {nranks} ranks ({mode}): fields differ from the reference: {bad}"
+    if mode == "default":   # OCN_OPT_OVERLAP auto: remote peers -> role-flip exchanges overlapped
+        assert levels == {2}, levels
     assert len(set(flips)) == 1, "ranks ran different kinds of steps"
     if mode in ("default", "overlap0", "overlap1", "overlap2", "norecompute") and \
             case["sw"].get("use_tracers", 0) <= 0:

@@ -111,7 +111,7 @@ def test_tracer_kernels_match_reference(amd, geom):
     assert not failures, f"{geom}: differs from the reference: {failures}"
 
 
-def build_model(amd, case, graph=False, fused=True, compact=True, overlap=1, march=True, flip=True,
+def build_model(amd, case, graph=False, fused=True, compact=True, overlap=None, march=True, flip=True,
                 recompute=True, rank=0, nranks=1, onepass=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
@@ -121,7 +121,8 @@ def build_model(amd, case, graph=False, fused=True, compact=True, overlap=1, mar
     m = amd.OceanModel(basin, sw, par, rank=rank, nranks=nranks)
     m.set_fused(fused)
     m.set_compact(compact)
-    m.set_overlap(overlap)
+    if overlap is not None:
+        m.set_overlap(overlap)
     m.set_march(march)
     m.set_flip(flip)
     m.set_recompute(recompute)
