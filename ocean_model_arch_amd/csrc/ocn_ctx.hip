@@ -1303,7 +1303,10 @@ static int expl_tracer(ocn_ctx *c, double tau, bool compact)
     return OCN_OK;
 }
 
-// ------------------------------------------------------------------ host-side initial state
+// ------------------------------------------------------------------ initial state
+// init_grid_data + init_ocean_data (control/init_data.f90:29-125) with every 2-D field formed on
+// the device (init_kernels.hip); the host supplies the basin mask and the grid's O(nx + ny)
+// trigonometric row / column factors from its libm, as the reference computes them.
 static const float kPi = 3.1415926f;              // constants.f90:14
 static const double kDPi = 3.14159265358979;      // constants.f90:17
 static const double kLatExtr = 89.99999;          // constants.f90:20
@@ -1312,97 +1315,33 @@ static const float kEarthAngVel = 7.2921159e-5f;  // constants.f90:22
 static double dsind(double x) { return std::sin((x / 180.0) * kDPi); }   // core/math_tools.f90
 static double dcosd(double x) { return std::cos((x / 180.0) * kDPi); }
 
-struct HostBlock {
-    const ocn_block &g;
-    long ld;
-    std::vector<std::vector<float>> r4;
-    explicit HostBlock(const ocn_block &b) : g(b), ld(b.bnd_x2 - b.bnd_x1 + 1)
-    {
-        r4.assign(OCN_NUM_R4, std::vector<float>((size_t)ld * (b.bnd_y2 - b.bnd_y1 + 1), 0.0f));
-    }
-    long I(int m, int n) const { return (long)(m - g.bnd_x1) + (long)(n - g.bnd_y1) * ld; }
-    float &a(int id, int m, int n) { return r4[id][I(m, n)]; }
+// One block's grid tables in one device allocation (freed by the caller after the launch ran):
+// grid_base_init's coordinates xt / xu (columns) and yt / yv (rows) (grid_kernels.f90:94-202),
+// then grid_geo_init's factors of them (grid_parameters.f90:80-181).
+struct GridTables {
+    std::vector<float> cos_t, cos_v;                   // (float) dcosd(lat_mod(yt)), of yv, per row
+    std::vector<double> sin_v, cosy_v, cos_xu;         // dsind(yv), dcosd(yv) per row; dcosd(xu) per column
 };
-
-// grid_kernels.f90:18-92 (lu_init, lu_lv_init), :94-202 (grid_base_init, uniform steps),
-// grid_geo_init_kernel + grid_parameters.f90 (carthesian / spherical metric scaling, Coriolis)
-static void host_grid(const ocn_ctx *c, HostBlock &h)
+static void grid_tables(const ocn_ctx *c, const ocn_block &g, GridTables &t)
 {
-    const ocn_block &g = h.g;
-    const int nx = c->basin.nx;
-    for (int n = g.bnd_y1; n <= g.bnd_y2; ++n)
-        for (int m = g.bnd_x1; m <= g.bnd_x2; ++m)
-            if (c->mask[(size_t)(m - 1) + (size_t)(n - 1) * nx] == 0) h.a(OCN_LU, m, n) = 1.0f;
-    for (int n = g.bnd_y1; n <= g.bnd_y2 - 1; ++n)
-        for (int m = g.bnd_x1; m <= g.bnd_x2 - 1; ++m) {
-            const float a = h.a(OCN_LU, m, n), b = h.a(OCN_LU, m + 1, n), cc = h.a(OCN_LU, m, n + 1),
-                        d = h.a(OCN_LU, m + 1, n + 1);
-            if (a + b + cc + d > 0.5f) h.a(OCN_LUH, m, n) = 1.0f;
-            if (a * b * cc * d > 0.5f) h.a(OCN_LUU, m, n) = 1.0f;
-            if (a + b > 0.5f) h.a(OCN_LLU, m, n) = 1.0f;
-            if (a + cc > 0.5f) h.a(OCN_LLV, m, n) = 1.0f;
-            if (a * b > 0.5f) h.a(OCN_LCU, m, n) = 1.0f;
-            if (a * cc > 0.5f) h.a(OCN_LCV, m, n) = 1.0f;
-        }
     const ocn_basin &bs = c->basin;
-    const int mmm = 3, nnn = 3;
-    std::vector<double> xt(h.ld), xu(h.ld), yt(g.bnd_y2 - g.bnd_y1 + 1), yv(g.bnd_y2 - g.bnd_y1 + 1);
+    const int w = g.bnd_x2 - g.bnd_x1 + 1, h = g.bnd_y2 - g.bnd_y1 + 1, mmm = 3, nnn = 3;
+    std::vector<double> xt(w), xu(w, 0.0), yt(h), yv(h, 0.0);
     for (int m = g.bnd_x1; m <= g.bnd_x2; ++m) xt[m - g.bnd_x1] = bs.rlon + (double)(m - mmm) * bs.dxst;
     for (int n = g.bnd_y1; n <= g.bnd_y2; ++n) yt[n - g.bnd_y1] = bs.rlat + (double)(n - nnn) * bs.dyst;
-    for (int m = g.bnd_x1; m <= g.bnd_x2 - 1; ++m) xu[m - g.bnd_x1] = (xt[m - g.bnd_x1] + xt[m + 1 - g.bnd_x1]) / 2.0;
-    for (int n = g.bnd_y1; n <= g.bnd_y2 - 1; ++n) yv[n - g.bnd_y1] = (yt[n - g.bnd_y1] + yt[n + 1 - g.bnd_y1]) / 2.0;
-    const float pip180 = kPi / 180.0f;
-    const float sx = (float)bs.dxst * pip180 * kRadEarth;
-    const float sy = (float)bs.dyst * pip180 * kRadEarth;
-    for (int n = g.ny_start - 1; n <= g.ny_end + 1; ++n)
-        for (int m = g.nx_start - 1; m <= g.nx_end + 1; ++m) {
-            for (int id : {OCN_DXT, OCN_DXB, OCN_DX, OCN_DXH}) h.a(id, m, n) = sx;
-            for (int id : {OCN_DYT, OCN_DYB, OCN_DY, OCN_DYH}) h.a(id, m, n) = sy;
-        }
-    std::vector<float> rlh_c(h.r4[OCN_RLH_S].size(), -2.0f * kEarthAngVel);
-    std::fill(h.r4[OCN_RLH_S].begin(), h.r4[OCN_RLH_S].end(), 2.0f * kEarthAngVel);
-    struct Pass { const std::vector<double> *x, *y; int mx, my; bool cor; };
-    const Pass passes[4] = {{&xt, &yt, OCN_DX, OCN_DY, false}, {&xu, &yt, OCN_DXT, OCN_DYH, false},
-                            {&xt, &yv, OCN_DXH, OCN_DYT, false}, {&xu, &yv, OCN_DXB, OCN_DYB, true}};
-    const double sinlat_extr = dsind(kLatExtr);
-    for (const Pass &p : passes)
-        for (int n = g.ny_start - 1; n <= g.ny_end + 1; ++n) {
-            const double y = (*p.y)[n - g.bnd_y1];
-            for (int m = g.nx_start - 1; m <= g.nx_end + 1; ++m) {
-                float &mx = h.a(p.mx, m, n), &my = h.a(p.my, m, n);
-                float &cs = h.a(OCN_RLH_S, m, n);
-                float &cc = rlh_c[h.I(m, n)];
-                if (bs.curve_grid == 0) {
-                    mx = mx * 1.0f; my = my * 1.0f;
-                    if (p.cor) { cs = cs / std::sqrt(2.0f); cc = cc / std::sqrt(2.0f); }
-                } else {
-                    const double lat_mod = std::max(std::min(y, kLatExtr), -kLatExtr);
-                    const double x = (*p.x)[m - g.bnd_x1];
-                    double sin_lat = dsind(y) * dcosd(bs.rotation_on_lat) + dcosd(x) * dcosd(y) * dsind(bs.rotation_on_lat);
-                    sin_lat = std::min(std::max(sin_lat, -sinlat_extr), sinlat_extr);
-                    const double cos_lat = std::sqrt(1.0 - sin_lat * sin_lat);
-                    mx = mx * (float)dcosd(lat_mod);
-                    my = my * 1.0f;
-                    if (p.cor) { cs = cs * (float)sin_lat; cc = cc * (float)cos_lat; }
-                }
-            }
-        }
-}
-
-// vel_ssh.f90:15-38 gaussian_elimination_kernel, (nx0, ny0) = (nx/2, ny/2); sigma = 1 for ssh,
-// 0.5 for tracers (init_data.f90:48, 83)
-static void host_gaussian(const ocn_ctx *c, HostBlock &h, std::vector<double> &ssh, double sigma = 1.0)
-{
-    const ocn_block &g = h.g;
-    const int nx0 = c->basin.nx / 2, ny0 = c->basin.ny / 2;
-    for (int n = g.ny_start; n <= g.ny_end; ++n)
-        for (int m = g.nx_start; m <= g.nx_end; ++m)
-            if (h.a(OCN_LU, m, n) > 0.5f) {
-                const double dx = (double)(m - nx0) / ((double)nx0 * 0.25);
-                const double dy = (double)(n - ny0) / ((double)ny0 * 0.25);
-                ssh[h.I(m, n)] = (1.0 / (std::sqrt(2.0 * kDPi) * sigma)) *
-                                 std::exp(-((dx * dx + dy * dy) / (2.0 * sigma * sigma)));
-            }
+    for (int i = 0; i + 1 < w; ++i) xu[i] = (xt[i] + xt[i + 1]) / 2.0;
+    for (int i = 0; i + 1 < h; ++i) yv[i] = (yt[i] + yt[i + 1]) / 2.0;
+    auto lat_mod = [](double y) { return std::max(std::min(y, kLatExtr), -kLatExtr); };
+    t.cos_t.assign(h, 0.0f); t.cos_v.assign(h, 0.0f); t.sin_v.assign(h, 0.0); t.cosy_v.assign(h, 0.0);
+    t.cos_xu.assign(w, 0.0);
+    for (int n = g.ny_start - 1; n <= g.ny_end + 1; ++n) {   // the metric range's rows and columns
+        const int r = n - g.bnd_y1;
+        t.cos_t[r] = (float)dcosd(lat_mod(yt[r]));
+        t.cos_v[r] = (float)dcosd(lat_mod(yv[r]));
+        t.sin_v[r] = dsind(yv[r]);
+        t.cosy_v[r] = dcosd(yv[r]);
+    }
+    for (int m = g.nx_start - 1; m <= g.nx_end + 1; ++m) t.cos_xu[m - g.bnd_x1] = dcosd(xu[m - g.bnd_x1]);
 }
 
 static int upload_field(ocn_ctx *c, const LBlock &b, int id, const void *host, bool async)
@@ -1421,16 +1360,52 @@ static int upload_field(ocn_ctx *c, const LBlock &b, int id, const void *host, b
 static int init_state(ocn_ctx *c)
 {
     HIPCHK(hipStreamSynchronize(c->stream));
-    for (const LBlock &b : c->blocks) {
-        HostBlock h(b.g);
-        host_grid(c, h);
-        for (int id = 0; id < OCN_NUM_R4; ++id) RC(upload_field(c, b, id, h.r4[id].data(), false));
+    const ocn_basin &bs = c->basin;
+    const size_t nxy = (size_t)bs.nx * bs.ny;
+    // device scratch of this call: the basin mask, then per block its grid tables
+    std::vector<GridTables> tabs(c->blocks.size());
+    size_t bytes = nxy * sizeof(int32_t);
+    std::vector<size_t> at(c->blocks.size());
+    for (size_t i = 0; i < c->blocks.size(); ++i) {
+        grid_tables(c, c->blocks[i].g, tabs[i]);
+        at[i] = (bytes + 255) / 256 * 256;
+        bytes = at[i] + tabs[i].cos_t.size() * 2 * 4 + 256 + (tabs[i].sin_v.size() * 2 + tabs[i].cos_xu.size()) * 8;
+    }
+    char *scratch = nullptr;
+    HIPCHK(hipMalloc(&scratch, bytes));
+    struct Free { char *p; ~Free() { if (p) (void)hipFree(p); } } free_scratch{scratch};
+    HIPCHK(hipMemcpy(scratch, c->mask.data(), nxy * sizeof(int32_t), hipMemcpyHostToDevice));
+    const float pip180 = kPi / 180.0f;
+    for (size_t i = 0; i < c->blocks.size(); ++i) {
+        const LBlock &b = c->blocks[i];
+        const GridTables &t = tabs[i];
+        const size_t h = t.cos_t.size(), w = t.cos_xu.size();
+        char *p = scratch + at[i];
+        GridInit q{};
+        q.g = b.g;
+        q.mask = (const int32_t *)scratch;
+        q.nx = bs.nx;
+        for (int id = 0; id < OCN_NUM_R4; ++id) q.r4[id] = b.f<float>(id);
+        q.cos_t = (const float *)p; q.cos_v = q.cos_t + h;
+        p += (h * 2 * 4 + 255) / 256 * 256;
+        q.sin_v = (const double *)p; q.cosy_v = q.sin_v + h; q.cos_xu = q.cosy_v + h;
+        HIPCHK(hipMemcpy((void *)q.cos_t, t.cos_t.data(), h * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy((void *)q.cos_v, t.cos_v.data(), h * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy((void *)q.sin_v, t.sin_v.data(), h * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy((void *)q.cosy_v, t.cosy_v.data(), h * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy((void *)q.cos_xu, t.cos_xu.data(), w * 8, hipMemcpyHostToDevice));
+        q.cos_rot = dcosd(bs.rotation_on_lat);
+        q.sin_rot = dsind(bs.rotation_on_lat);
+        q.sin_extr = dsind(kLatExtr);
+        q.sx = (float)bs.dxst * pip180 * kRadEarth;
+        q.sy = (float)bs.dyst * pip180 * kRadEarth;
+        q.cor = 2.0f * kEarthAngVel;
+        q.sqrt2 = std::sqrt(2.0f);
+        q.curve = bs.curve_grid != 0;
+        RC(launch_init_grid(q, c->stream));
         c->static_dirty = true;
-        std::vector<double> r8(h.r4[0].size(), 100.0);      // init_data.f90:112-114 hhq_rest = 100 m
-        RC(upload_field(c, b, OCN_HHQ_REST, r8.data(), false));
-        std::fill(r8.begin(), r8.end(), 0.0);
-        host_gaussian(c, h, r8);
-        RC(upload_field(c, b, OCN_SSH, r8.data(), false));
+        RC(launch_fill_field(b.g, b.f<double>(OCN_HHQ_REST), 100.0, c->stream));   // init_data.f90:112-114
+        RC(launch_gaussian(b.g, b.f<double>(OCN_SSH), b.f<float>(OCN_LU), bs.nx / 2, bs.ny / 2, 1.0, c->stream));
     }
     RC(run_sync(c, {OCN_SSH}));                               // envoke_gaussian_elimination's sync
     for (const LBlock &b : c->blocks) {                       // sshn = ssh, sshp = ssh (whole arrays)
@@ -1451,13 +1426,9 @@ static int init_state(ocn_ctx *c)
     }
     if (c->sw.use_tracers > 0) {                              // init_data.f90:80-90
         for (int k = 1; k <= c->sw.tracer_num; ++k) {
-            for (const LBlock &b : c->blocks) {
-                HostBlock h(b.g);
-                host_grid(c, h);
-                std::vector<double> r8(h.r4[0].size(), 0.0);
-                host_gaussian(c, h, r8, 0.5);
-                RC(upload_field(c, b, OCN_FF1(k), r8.data(), false));
-            }
+            for (const LBlock &b : c->blocks)
+                RC(launch_gaussian(b.g, b.f<double>(OCN_FF1(k)), b.f<float>(OCN_LU), bs.nx / 2, bs.ny / 2, 0.5,
+                                   c->stream));
             RC(run_sync(c, {OCN_FF1(k)}));
             for (const LBlock &b : c->blocks) {
                 const size_t bytes = (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1) * 8;

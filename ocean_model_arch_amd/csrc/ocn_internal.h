@@ -74,6 +74,25 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compac
 // skip_rc = step k+1 is a recompute step (hhq on the interior, hhu_p, hhv_p not stored).
 int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s);
+// Initial state on the device (init_kernels.hip; ocn_ctx.hip init_state).  GridInit: one block's
+// real(4) static fields from the basin mask (device copy, nx x ny int32, 1-based (m, n) at
+// (m-1) + (n-1) nx) and the grid's row / column factors from the host's libm.
+struct GridInit {
+    ocn_block g;
+    const int32_t *mask;
+    int nx;
+    float *r4[OCN_NUM_R4];
+    const float *cos_t, *cos_v;                    // per row (n - bnd_y1): (float) dcosd(lat_mod(yt / yv))
+    const double *sin_v, *cosy_v, *cos_xu;         // dsind(yv), dcosd(yv) per row; dcosd(xu) per column
+    double cos_rot, sin_rot, sin_extr;             // dcosd / dsind(rotation_on_lat), dsind(lat_extr)
+    float sx, sy, cor, sqrt2;                      // base steps (m), 2 * EarthAngVel, sqrt(2.0)
+    int curve;
+};
+int launch_init_grid(const GridInit &q, hipStream_t s);
+// gaussian_elimination_kernel (vel_ssh.f90:15-38) into p (zero outside the sea interior)
+int launch_gaussian(const ocn_block &g, double *p, const float *lu, int nx0, int ny0, double sigma, hipStream_t s);
+// v at every point of the block array (not the row padding)
+int launch_fill_field(const ocn_block &g, double *p, double v, hipStream_t s);
 // One-pass role-flip step (sw_kernels.hip MarchStep): a1 + fused B + a8's filters + check_ssh_err
 // with hh_init's depths, vort and the stresses formed in registers from the state; single block,
 // no a8 / a9 work on the halo ring; a8's filtered sshp / ubrtrp / vbrtrp go to the given buffers.
