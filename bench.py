@@ -48,15 +48,33 @@ LAUNCH_BYTES = {
     # sshn, ubrtrn, vbrtrn and the filtered sshp, ubrtrp, vbrtrp out
     "onepass": (129, 129),
     "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
+    # tracer runs: CA also stores hh_init's hhq_p (read by tran_diff_tracer); per tracer and step:
+    # tran_diff_fluxes (lcu, lcv, hhu, hhv, ff, ffp, ubrtr, vbrtr, mu in; flux_x, flux_y out),
+    # tran_diff_tracer (lu, hhq_n, hhq_p, flux_x, flux_y, ffp in; ffn out), tracer_next_step (lu,
+    # ffn, ffp, ff in; ffp, ff out)
+    "hqp": (8, 8),
+    "tr_fluxes": (73, 97), "tr_tracer": (57, 69), "tr_next": (41, 44),
 }
 
 
-def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, one: bool = False):
+def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
+                  tracers: int = 0, full_c2: bool = False):
     """The launches of one ocn_ctx_step call of `steps` steps, as (timer, launch kind) pairs --
     ocn_ctx.hip ocn_ctx_step / one_step_fused for one block (role-flip calls fuse each step's
     hh_init with the next step's A when full_free_surface = 1, as in sw.par; ring = the ring
     launch runs, i.e. a8 / a9 have work on the halo ring: blocks with neighbours; one = one-pass
-    steps 2..K-1)."""
+    steps 2..K-1; tracers = expl_tracer's three launches per tracer after every step, and
+    hh_init's hhq_p stored by every CA / hh_init)."""
+    if tracers:
+        out = []
+        for timer, kind in call_launches(steps, flip, rc, ring, False, full_c2=True):
+            out.append((timer, kind))
+            if timer == "fused_ca":
+                out.append((timer, "hqp"))
+            if timer in ("fused_ca", "hh_init"):   # the step's last SW launch: then its tracers
+                out += [("tran_diff_fluxes", "tr_fluxes"), ("tran_diff_tracer", "tr_tracer"),
+                        ("tracer_next_step", "tr_next")] * tracers
+        return out
     if one and flip and steps >= 3:
         out = [("fused_a", "a"), ("fused_b", "b_flip")]
         out += [("onepass", "onepass")] * (steps - 2) + [("fused_ca", "ca_hh")]
@@ -78,26 +96,26 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
             out += [("fused_ca", "ca_hh" if s + 1 >= steps else "ca" if rc else "ca_store")]
         else:
             out += [("fused_b", "b_full" if last else "b_reuse" if reuse else "b"), ("fused_c1", "c1"),
-                    ("hh_init", "c2_full" if last else "c2")]
+                    ("hh_init", "c2_full" if last or full_c2 else "c2")]
     return out
 
 
 def fused_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False,
-                one: bool = False):
+                one: bool = False, tracers: int = 0):
     """Mean bytes per interior cell per launch of each timer over one ocn_ctx_step call."""
     i = 0 if compact else 1
     tot, cnt = {}, {}
-    for timer, kind in call_launches(steps, flip, rc, ring, one):
+    for timer, kind in call_launches(steps, flip, rc, ring, one, tracers):
         tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
-        cnt[timer] = cnt.get(timer, 0) + 1
+        cnt[timer] = cnt.get(timer, 0) + (kind != "hqp")   # "hqp": bytes of the launch before it
     return {t: tot[t] / cnt[t] for t in tot}
 
 
 def step_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False,
-               one: bool = False):
+               one: bool = False, tracers: int = 0):
     """Bytes per interior cell per step moved by one ocn_ctx_step call of `steps` steps."""
     i = 0 if compact else 1
-    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc, ring, one)) / steps
+    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc, ring, one, tracers)) / steps
 
 
 def dims_create(n: int):
@@ -325,8 +343,9 @@ def main():
     out = None
     if rank == 0:
         ring = bx * by > 1
-        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc, ring, one)
-        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring, one)
+        ntr = sw.tracer_num if sw.use_tracers > 0 else 0
+        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc, ring, one, ntr)
+        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring, one, ntr)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:   # the dominant kernel: the most device time over the timed steps

@@ -1087,14 +1087,15 @@ static int check_coherence(ocn_ctx *c, bool eligible = true)
 // "ubrtrn" / "vbrtrn" after the swap holds the old value there instead -- which no kernel
 // reads before a1 / a7 of the next step rewrite it.  The last step of every call is a standard
 // step; it leaves both buffers of each pair equal everywhere, so the swap is undone at the end
-// of the call by swapping the pointers back, with no copy.  Used with the compact tables + march
-// and no tracers.  With halo exchanges the swapped buffers are exchanged through plans built for
-// the swapped roles (get_plan), the ring launch (a8 + a9 on the halo ring) runs after sync B, and
+// of the call by swapping the pointers back, with no copy.  Used with the compact tables + march,
+// tracer runs included (CA then also stores hh_init's hhq_p, which expl_tracer reads after every
+// step).  With halo exchanges the swapped buffers are exchanged through plans built for the
+// swapped roles (get_plan), the ring launch (a8 + a9 on the halo ring) runs after sync B, and
 // each hh_init's sync and the next step's sync A are one exchange (sync_ca); the exchanges do
 // not overlap computation in these steps.
 static bool flip_eligible(ocn_ctx *c)
 {
-    return c->flip && c->fused && c->compact && c->march && c->sw.use_tracers <= 0;
+    return c->flip && c->fused && c->compact && c->march;
 }
 
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
@@ -1298,6 +1299,7 @@ static int tracer_stage(ocn_ctx *c, int stage, int k, double tau, bool compact)
 static int expl_tracer(ocn_ctx *c, double tau, bool compact)
 {
     if (c->sw.use_tracers <= 0) return OCN_OK;
+    RC(join_sync(c));   // an exchange a role-flip step left in flight (hh_init's hhu / hhv halos)
     for (int k = 1; k <= c->sw.tracer_num; ++k)
         for (int stage = 0; stage < OCN_NUM_TSTAGES; ++stage) RC(tracer_stage(c, stage, k, tau, compact));
     return OCN_OK;
@@ -1768,8 +1770,10 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     // the second buffer (the ring launch completes it on the halo ring)
     const bool ca = flip_call && c->sw.full_free_surface == 1;
     // one-pass steps 2..K-1 (single block, no a8 / a9 work on the halo ring, all SW terms on)
+    // (no tracers: expl_tracer reads hh_init's hhu / hhv / hhq_p, which a one-pass step keeps in registers)
     const bool one_call = ca && c->onepass && nsteps >= 3 && c->blocks.size() == 1 && !has_exchange(c) &&
-                          !has_comm(c) && !c->ring_sea && c->sw.trans_terms > 0 && c->sw.ksw_lat > 0;
+                          !has_comm(c) && !c->ring_sea && c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 &&
+                          c->sw.use_tracers <= 0;
     c->one_used = one_call;
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;

@@ -844,6 +844,10 @@ template <bool HH, bool SKIP> struct MarchCA {
                 // !HH: the next step's fused B forms hhq itself on the interior (MarchFusedB RC)
                 const bool interior = L.m >= a.sx && L.m <= b_xe && n >= a.sy && n <= b_ye;
                 if (L.out && (!SKIP || !interior)) st(c2.hq, c, r00 + x.rSH.c * f);
+                // tracer runs: expl_tracer reads hh_init's whole-array hqp = h_r + shp * ffs after
+                // every step (tran_diff_tracer's hhq_p; its hhq_n = h_r is never changed by the
+                // fused step: fused A does not store hh_update's hqn)
+                if (L.out && tracers) st(c2.hqp, c, r00 + x.rSHP.c * f);
                 if (in_rows) {
                     HhInitOut o;
                     hh_init_math(x, f, false, o);
@@ -889,11 +893,12 @@ template <bool HH, bool SKIP> struct MarchCA {
             x.rHR.rotate(); x.rSH.rotate(); x.rSHP.rotate(); x.rU.rotate(); x.rUP.rotate(); x.bits.rotate();
         }
         int b_xe, b_ye;
+        bool tracers;
     };
     __device__ void march(const Lane &L, int nb, int ne) const
     {
         const Fn f{make_hh_init(&b, t, (int)sw.full_free_surface, false), make_fused_a(&b, t, sw, tau, !HH), t,
-                   b.bnd_y2, b.nx_end, b.ny_end};
+                   b.bnd_y2, b.nx_end, b.ny_end, sw.use_tracers > 0};
         MarchViewCA x{};
         x.tau = tau;
         // the warm row nb-1 (when it exists) precedes the tile's rows

@@ -81,8 +81,7 @@ def test_ranks_match_reference(amd, name, nranks, mode):
     if mode == "default":   # OCN_OPT_OVERLAP auto: remote peers -> role-flip exchanges overlapped
         assert levels == {2}, levels
     assert len(set(flips)) == 1, "ranks ran different kinds of steps"
-    if mode in ("default", "overlap0", "overlap1", "overlap2", "norecompute") and \
-            case["sw"].get("use_tracers", 0) <= 0:
+    if mode in ("default", "overlap0", "overlap1", "overlap2", "norecompute"):   # tracer runs included
         assert flips[0], f"{name}: role-flip steps not used over ranks"
 
 

@@ -157,7 +157,7 @@ def compare_case(m, case, name, whole=True):
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
-    hh_init as register marches, role-flip steps without tracers (hh_init fused with the next
+    hh_init as register marches, role-flip steps, tracer runs included (hh_init fused with the next
     step's A, fused B recomputing hhq / hhu_p / hhv_p), halo exchanges overlapped
     with inner launches in the standard steps when there are several blocks;
     norecompute = compact without the recompute steps; noflip = compact with standard steps only;
@@ -177,7 +177,7 @@ def test_end_to_end_matches_reference(amd, name, mode):
     flip_used, one_used = m.flip_active, m.onepass_active
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
-    if mode in ("compact", "noonepass", "norecompute", "serial", "overlap2") and case["sw"].get("use_tracers", 0) <= 0:
+    if mode in ("compact", "noonepass", "norecompute", "serial", "overlap2"):   # tracer runs included
         assert flip_used, f"{name}: role-flip steps not used"
     if mode == "compact" and name.startswith("box") and "_b1x1_" in name and case["sw"]["trans_terms"] > 0 \
             and case["sw"]["ksw_lat"] > 0:
