@@ -287,6 +287,7 @@ struct ocn_ctx {
     bool capturing = false;      // a step is being captured into a hipGraph
     bool sync_pending = false;   // an exchange on comm_stream not yet joined (fork_sync)
     bool ring_sea = true;   // some halo-ring point has a mask set (Prepare); else no ring launch
+    bool udiv_ok = true;    // every row divisor of the one-pass step in [2^-60, 2^60] (Prepare)
     bool recompute = true;  // OCN_OPT_RECOMPUTE: recompute steps in role-flip calls
     bool onepass = true;    // OCN_OPT_ONEPASS: one-pass steps in single-block role-flip calls
     bool one_used = false;
@@ -419,16 +420,29 @@ static int allocate(ocn_ctx *c)
         const long r8b = ((n * 8 + 16 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW;
         const long r4b = ((n * 4 + 8 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW;
         const int nr8 = num_r8(c);
-        const size_t total = (size_t)nr8 * r8b + (size_t)OCN_NUM_R4 * r4b + 256;
+        // + the three second buffers of the role-flip / one-pass steps
+        const size_t total = (size_t)(nr8 + 3) * r8b + (size_t)OCN_NUM_R4 * r4b + 256;
         HIPCHK(hipMalloc(&b.slab, total));
         c->allocs.push_back(b.slab);
         HIPCHK(hipMemsetAsync(b.slab, 0, total, c->stream));
         char *base = (char *)b.slab;
         size_t off = 0;
         b.ptr.assign((size_t)(OCN_NUM_R4 + nr8), nullptr);
-        for (int id = OCN_SSH; id < OCN_SSH + nr8; ++id) {
-            b.ptr[field_slot(id)] = base + off + 256 - 16;
+        // r8 order in the slab: first the one-pass step's fields and the second buffers, so that
+        // its kernel reaches all of them by 32-bit offsets from one base (sw_kernels.hip
+        // MarchStep), then the other SW fields, then the tracers'
+        std::vector<int> order = {OCN_SSH, OCN_SSHN, OCN_SSHP, OCN_UBRTR, OCN_UBRTRN, OCN_UBRTRP, OCN_VBRTR,
+                                  OCN_VBRTRN, OCN_VBRTRP, -1, -2, -3, OCN_HHU, OCN_HHU_P, OCN_HHV, OCN_HHV_P, OCN_HHH,
+                                  OCN_HHQ_REST, OCN_VORT, OCN_STR_T, OCN_STR_S, OCN_MU, OCN_RHSX, OCN_RHSY};
+        for (int id = OCN_SSH; id < OCN_SSH + nr8; ++id)
+            if (std::find(order.begin(), order.end(), id) == order.end()) order.push_back(id);
+        for (int id : order) {
+            char *p = base + off + 256 - 16;
             off += r8b;
+            if (id == -1) b.sshp_alt = p;
+            else if (id == -2) b.up_alt = p;
+            else if (id == -3) b.vp_alt = p;
+            else b.ptr[field_slot(id)] = p;
         }
         for (int id = 0; id < OCN_NUM_R4; ++id) {
             b.ptr[field_slot(id)] = base + off + 256 - 8;
@@ -437,18 +451,12 @@ static int allocate(ocn_ctx *c)
     }
     for (LBlock &b : c->blocks) {
         const size_t n = (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1);
-        const size_t nrow = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1) * (OCN_NUM_R4 - OCN_DX + 4);   // metric row tables
-                                                                                                // + 4 ratios (sw_stencils.h kRowTable)
+        // metric row tables + ratios + reciprocals (sw_stencils.h kRowTable, recip_offset)
+        const size_t nrow = row_table_size((unsigned)(b.g.bnd_y2 - b.g.bnd_y1 + 1));
         HIPCHK(hipMalloc(&b.bits, n));
         c->allocs.push_back(b.bits);
         HIPCHK(hipMalloc(&b.rows, nrow * sizeof(float)));
         c->allocs.push_back(b.rows);
-        for (void **dst : {&b.sshp_alt, &b.up_alt, &b.vp_alt}) {
-            void *alt = nullptr;   // laid out as the slab's r8 fields (rows 256-B aligned at nx_start)
-            HIPCHK(hipMalloc(&alt, n * 8 + 512));
-            c->allocs.push_back(alt);
-            *dst = (char *)alt + 256 - 16;
-        }
     }
     HIPCHK(hipMalloc(&c->d_nbad, 256));
     c->allocs.push_back(c->d_nbad);
@@ -975,7 +983,8 @@ static int prepare_static(ocn_ctx *c)
     HIPCHK(hipMemcpyAsync(&flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->ring_sea = (flags & kCompactRingSea) != 0;
-    c->compact = (flags & ~kCompactRingSea) == 0;
+    c->udiv_ok = (flags & kCompactDivisorRange) == 0;
+    c->compact = (flags & ~(kCompactRingSea | kCompactDivisorRange)) == 0;
     c->static_dirty = false;
     return OCN_OK;
 }
@@ -1773,7 +1782,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     // (no tracers: expl_tracer reads hh_init's hhu / hhv / hhq_p, which a one-pass step keeps in registers)
     const bool one_call = ca && c->onepass && nsteps >= 3 && c->blocks.size() == 1 && !has_exchange(c) &&
                           !has_comm(c) && !c->ring_sea && c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 &&
-                          c->sw.use_tracers <= 0;
+                          c->sw.use_tracers <= 0 && c->udiv_ok;
     c->one_used = one_call;
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;

@@ -74,6 +74,10 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compac
 // skip_rc = step k+1 is a recompute step (hhq on the interior, hhu_p, hhv_p not stored).
 int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s);
+// floats of a block's compact row table for nrows rows: metric rows, ratios, reciprocals
+// (sw_stencils.h kRowTable, recip_offset)
+size_t row_table_size(unsigned nrows);
+
 // Initial state on the device (init_kernels.hip; ocn_ctx.hip init_state).  GridInit: one block's
 // real(4) static fields from the basin mask (device copy, nx x ny int32, 1-based (m, n) at
 // (m-1) + (n-1) nx) and the grid's row / column factors from the host's libm.
@@ -106,6 +110,7 @@ int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact 
 int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int32_t *flags, hipStream_t s);
 // Prepare's flag bit reporting mask bits on the halo ring (sw_stencils.h OCN_COMPACT_RING_SEA)
 constexpr int kCompactRingSea = 4;
+constexpr int kCompactDivisorRange = 8;   // sw_stencils.h OCN_COMPACT_DIVISOR_RANGE
 // Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
 // they cannot be used into *flags (device int).
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s);

@@ -965,6 +965,25 @@ __device__ __forceinline__ double shz(double x, int dx)
 }
 __device__ __forceinline__ unsigned shz(unsigned x, int dx) { return dx == 0 ? x : (unsigned)dpp_shz((int)x, dx); }
 
+// x / d, correctly rounded, for a wave-uniform divisor d with rd = RN(1 / d) (the row table's
+// reciprocals): q = RN(x rd) is within one ulp of x / d, the residual x - q d is exact in an fma,
+// and RN(q + (x - q d) rd) is the correctly rounded quotient (Markstein's theorem) when nothing
+// underflows: for |d| in [2^-60, 2^60] (launch_prepare flags other divisors, and the one-pass step
+// is then not used) and x = 0 or 2^-900 <= |x| < 2^900 the quotient and the residual are normal.
+// 3 VALU operations instead of the div_scale / rcp / fma / fixup sequence of an IEEE fp64 division
+// (11, one of them quarter rate).  The caller checks the dividend's range (exp_check): a row where
+// any dividend is outside it is computed again with IEEE divisions.  Checked bit for bit against
+// IEEE division on 2e8 random operands (tests/test_udiv.py).
+__device__ __forceinline__ double udiv(double x, double d, double rd)
+{
+    const double q = x * rd;
+    const double e = __builtin_fma(-q, d, x);
+    return __builtin_fma(e, rd, q);
+}
+// the smallest frexp exponent of the dividends of a row (0 for x = 0)
+__device__ __forceinline__ void exp_check(int &acc, double x) { acc = min(acc, __builtin_amdgcn_frexp_exp(x)); }
+constexpr int kUdivMinExp = -899;   // frexp exponent >= -899  <=>  |x| >= 2^-900
+
 struct StepRegs {
     template <class T> struct Win {   // rows n-1, n, n+1, n+2 at this lane's column
         T r[4];
@@ -987,12 +1006,18 @@ struct StepRegs {
     // metric rows: read where used, as wave-uniform scalar loads from the (read-only) row table
     // through the constant address space -- no table of 4 rows x 14 values held in SGPRs
     const __attribute__((address_space(4))) float *rows;
+    const __attribute__((address_space(4))) double *rcp;   // the rows' reciprocals (sw_stencils.h recip_offset)
     unsigned nrows, rn;               // table stride, row index of n (n - bnd_y1)
     double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
     double tau, inv_tau, f;
     __device__ __forceinline__ float met(int id, int dy) const
     {
         return rows[(unsigned)(id - OCN_DX) * nrows + __builtin_amdgcn_readfirstlane(rn + dy)];
+    }
+    // 1 / (double)g of row n + dy for the divisor OCN_RC_* k (wave-uniform scalar load)
+    __device__ __forceinline__ double rc(int k, int dy) const
+    {
+        return rcp[(unsigned)k * nrows + __builtin_amdgcn_readfirstlane(rn + dy)];
     }
     __device__ __forceinline__ float mk(int id, int dx, int dy) const
     {
@@ -1018,6 +1043,7 @@ template <bool P2> struct MarchStep {
     static constexpr int kWaves = OCN_STEP_WAVES;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; int32_t *nbad;
     double *sshp_out, *up_out, *vp_out;   // a8's filtered sshp / ubrtrp / vbrtrp (the second buffers)
+
 
     // a / tau (sw_update_uv_math qtau).  P2: tau is a power of two, so a / tau is a * (1 / tau) bit
     // for bit (both round the same real value once; exact scalings unless subnormal)
@@ -1085,7 +1111,15 @@ template <bool P2> struct MarchStep {
 
     // D at row r = n + 1 of this lane (column m): the values the reference's arrays hold there,
     // plus the shared products of that row
-    __device__ __forceinline__ void derive(StepRegs &x, const Fallback &fb) const
+    // E: IEEE divisions (the exact re-run of a row some dividend of which is out of udiv's range)
+    template <bool E> __device__ __forceinline__ static double dv(double a, double d, double rd)
+    {
+        if constexpr (E) return a / d;
+        else return udiv(a, d, rd);
+    }
+    template <bool E>
+    __device__ __forceinline__ void derive(StepRegs &x, const Fallback &fb, int &acc, double &qb_next,
+                                           double &qc_next) const
     {
         weights(x, 2);   // row n+2 (rows n+1's were formed one iteration ago)
         // hh_init levels 0 and 1 (depth.f90:52-97, sw_stencils.h interp_u / interp_v / interp_h)
@@ -1097,11 +1131,20 @@ template <bool P2> struct MarchStep {
         const double w00 = x.w0.r[2], w10 = shz(w00, 1), w01 = x.w0.r[3], w11 = shz(w01, 1);
         const double p00 = x.w1.r[2], p10 = shz(p00, 1), p01 = x.w1.r[3];
         const double s0 = w00 + w10;
-        const double u0 = div_mask_sum(s0, su) / dxt / dyh;
-        const double v0 = div_mask_sum(w00 + w01, sv) / dxh / dyt;
-        const double h0 = div_mask_sum(s0 + w01 + w11, sh4) / dxb / dyb;
-        const double u1 = div_mask_sum(p00 + p10, su) / dxt / dyh;
-        const double v1 = div_mask_sum(p00 + p01, sv) / dxh / dyt;
+        const double rxt = x.rc(OCN_RC_DXT, 1), ryh = x.rc(OCN_RC_DYH, 1), rxh = x.rc(OCN_RC_DXH, 1),
+                     ryt = x.rc(OCN_RC_DYT, 1);
+        const double a_u0 = div_mask_sum(s0, su), a_v0 = div_mask_sum(w00 + w01, sv),
+                     a_h0 = div_mask_sum(s0 + w01 + w11, sh4), a_u1 = div_mask_sum(p00 + p10, su),
+                     a_v1 = div_mask_sum(p00 + p01, sv);
+        if (!E) {   // (a / g1) / g2: a's range bounds a / g1's (|g1| <= 2^60)
+            exp_check(acc, a_u0); exp_check(acc, a_v0); exp_check(acc, a_h0); exp_check(acc, a_u1);
+            exp_check(acc, a_v1); exp_check(acc, x.up.r[2]); exp_check(acc, x.vp.r[2]); exp_check(acc, x.up.r[3]);
+        }
+        const double u0 = dv<E>(dv<E>(a_u0, dxt, rxt), dyh, ryh);
+        const double v0 = dv<E>(dv<E>(a_v0, dxh, rxh), dyt, ryt);
+        const double h0 = dv<E>(dv<E>(a_h0, dxb, x.rc(OCN_RC_DXB, 1)), dyb, x.rc(OCN_RC_DYB, 1));
+        const double u1 = dv<E>(dv<E>(a_u1, dxt, rxt), dyh, ryh);
+        const double v1 = dv<E>(dv<E>(a_v1, dxh, rxh), dyt, ryt);
         // a3 uv_trans_vort (vel_ssh.f90:247-281, sw_stencils.h uv_trans_vort_math)
         const double u_0 = x.u.r[2], u_1 = x.u.r[3], v_0 = x.v.r[2], v_r = shz(v_0, 1);
         const double vort = (v_r * dyt - v_0 * dyt) - (u_1 * OCN_MD(OCN_DXT, 2) - u_0 * dxt)
@@ -1110,14 +1153,14 @@ template <bool P2> struct MarchStep {
         // up/dyh at m-1 is the left lane's up/dyh (dyh is constant along the row), vp/dxh at n-1
         // is the previous row's, up/dxt at n+1 the next row's (formed here, kept for the next
         // row), vp/dyt at m+1 the right lane's -- the same operands, so the same values
-        const double qa = x.up.r[2] / dyh, qb = x.vp.r[2] / dxh;
-        const double qc1 = x.up.r[3] / OCN_MD(OCN_DXT, 2), qe = x.vp.r[2] / dyt;
+        const double qa = dv<E>(x.up.r[2], dyh, ryh), qb = dv<E>(x.vp.r[2], dxh, rxh);
+        const double qc1 = dv<E>(x.up.r[3], OCN_MD(OCN_DXT, 2), x.rc(OCN_RC_DXT, 2)), qe = dv<E>(x.vp.r[2], dyt, ryt);
         const double st = D(x.met(OCN_DX + kNumRowFields + 0, 1)) * (qa - shz(qa, -1))
                           - D(x.met(OCN_DX + kNumRowFields + 1, 1)) * (qb - x.qb);
         const double ss = D(x.met(OCN_DX + kNumRowFields + 2, 1)) * (qc1 - x.qc)
                           + D(x.met(OCN_DX + kNumRowFields + 3, 1)) * (shz(qe, 1) - qe);
-        x.qb = qb;
-        x.qc = qc1;
+        qb_next = qb;
+        qc_next = qc1;
         const double hu = fb.llu ? u0 : fb.hu;
         const double hv = fb.llv ? v0 : fb.hv;
         const double hh = fb.luh ? h0 : fb.hh;
@@ -1144,7 +1187,7 @@ template <bool P2> struct MarchStep {
 
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
     // uv_trans_math, uv_diff2_math, sw_update_uv_math written out over the shared products)
-    __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n) const
+    template <bool E> __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n, int &acc) const
     {
         const Geo I = geo(&b);
         const Pt c = I(L.m, n);
@@ -1154,7 +1197,9 @@ template <bool P2> struct MarchStep {
         // a1 sw_update_ssh (vel_ssh.f90:69-106)
         const double t1 = u * hu * dyh;
         const float area = x.met(OCN_DX, 0) * x.met(OCN_DY, 0);
-        const double sshn = x.shp.r[1] + 2.0 * x.tau * (-((t1 - shz(t1, -1) + x.t3.r[1] - x.t3.r[0]) / D(area)));
+        const double a_ssh = t1 - shz(t1, -1) + x.t3.r[1] - x.t3.r[0];
+        if (!E) exp_check(acc, a_ssh);
+        const double sshn = x.shp.r[1] + 2.0 * x.tau * (-dv<E>(a_ssh, D(area), x.rc(OCN_RC_AREA, 0)));
         // a4 uv_trans (vel_ssh.f90:283-373)
         const double u_r = shz(u, 1), u_l = shz(u, -1), u_n = x.u.r[2], u_s = x.u.r[0];
         const double v_r = shz(v, 1), v_l = shz(v, -1), v_n = x.v.r[2], v_s = x.v.r[0];
@@ -1188,10 +1233,12 @@ template <bool P2> struct MarchStep {
             const float dxb2 = gxb * gxb, dxb2m = gxbm * gxbm, dyb2 = gyb * gyb;
             const double sts = x.sts.r[1];
             const double dtc = x.dt.r[1];
-            rxd = (shz(dtc, 1) - dtc) / dyh
-                  + (D(dxb2) * muh_p * hh * sts - D(dxb2m) * muh_m * x.hh.r[0] * x.sts.r[0]) / dxt;
-            ryd = -(x.dxq.r[2] - x.dxq.r[1]) / dxh
-                  + (D(dyb2) * muh_p * hh * sts - D(dyb2) * muh_m2 * shz(hh, -1) * shz(sts, -1)) / dyt;
+            const double a1 = shz(dtc, 1) - dtc, a2 = D(dxb2) * muh_p * hh * sts - D(dxb2m) * muh_m * x.hh.r[0] * x.sts.r[0];
+            const double a3 = x.dxq.r[2] - x.dxq.r[1],
+                         a4 = D(dyb2) * muh_p * hh * sts - D(dyb2) * muh_m2 * shz(hh, -1) * shz(sts, -1);
+            if (!E) { exp_check(acc, a1); exp_check(acc, a2); exp_check(acc, a3); exp_check(acc, a4); }
+            rxd = dv<E>(a1, dyh, x.rc(OCN_RC_DYH, 0)) + dv<E>(a2, dxt, x.rc(OCN_RC_DXT, 0));
+            ryd = -dv<E>(a3, dxh, x.rc(OCN_RC_DXH, 0)) + dv<E>(a4, dyt, x.rc(OCN_RC_DYT, 0));
         }
         // a7 sw_update_uv (vel_ssh.f90:108-195); hun = hu, hvn = hv (the reuse identity)
         double un, vn;
@@ -1239,6 +1286,7 @@ template <bool P2> struct MarchStep {
         const Geo I = geo(&b);
         StepRegs x{};
         x.rows = (const __attribute__((address_space(4))) float *)t.rows;
+        x.rcp = (const __attribute__((address_space(4))) double *)(t.rows + recip_offset(t.nrows));
         x.nrows = t.nrows;
         x.rn = (unsigned)(nb - 2 - b.bnd_y1);   // row n0
         x.tau = tau;
@@ -1267,8 +1315,19 @@ template <bool P2> struct MarchStep {
             take(x, q);
             if (n < ne) fallback(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
             if (n < ne) load(q, L.m, n + 1);              // in flight while this row is computed
-            derive(x, fb);
-            if (n >= nb) step(x, L, n);      // wave-uniform
+            {   // D(n+1) with udiv; again with IEEE divisions if a dividend is out of its range
+                int acc = 0;
+                double qb, qc;
+                derive<false>(x, fb, acc, qb, qc);
+                if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) derive<true>(x, fb, acc, qb, qc);
+                x.qb = qb;
+                x.qc = qc;
+            }
+            if (n >= nb) {   // wave-uniform
+                int acc = 0;
+                step<false>(x, L, n, acc);
+                if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) step<true>(x, L, n, acc);
+            }
             x.rotate();
             fb = fbn;
         }
@@ -1453,6 +1512,8 @@ int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, 
     const Range r = range_bnd(b);
     return launch_range(r.m0, r.m1, r.n0, r.n1, make_coherence(b, ptr, bits, (int *)flags), s);
 }
+
+size_t row_table_size(unsigned nrows) { return row_table_floats(nrows); }
 
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s)
 {

@@ -758,8 +758,16 @@ constexpr int kNumRowFields = OCN_NUM_R4 - OCN_DX;        // OCN_DX..OCN_R_DISS
 // then four per-row ratios for stress_components: dy/dx, dx/dy, dxb/dyb, dyb/dxb (real(4))
 constexpr int kNumRowRatios = 4;
 constexpr int kRowTable = kNumRowFields + kNumRowRatios;
+// then, as doubles from float offset recip_offset(nrows) on, per row the correctly rounded
+// reciprocals 1 / (double)g of the divisors the one-pass step divides by (its uniform-divisor
+// division, sw_kernels.hip udiv): dxt, dyh, dxh, dyt, dxb, dyb, and the cell area dx*dy (real(4)
+// product, as sw_update_ssh forms it)
+enum { OCN_RC_DXT = 0, OCN_RC_DYH, OCN_RC_DXH, OCN_RC_DYT, OCN_RC_DXB, OCN_RC_DYB, OCN_RC_AREA, kNumRecips };
+OCN_HD inline unsigned recip_offset(unsigned nrows) { return ((unsigned)kRowTable * nrows + 1u) & ~1u; }
+inline size_t row_table_floats(unsigned nrows) { return recip_offset(nrows) + 2u * (unsigned)kNumRecips * nrows; }
 enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2,
-       OCN_COMPACT_RING_SEA = 4 };   // not a failure: a8 / a9 write somewhere on the halo ring
+       OCN_COMPACT_RING_SEA = 4,     // not a failure: a8 / a9 write somewhere on the halo ring
+       OCN_COMPACT_DIVISOR_RANGE = 8 };   // not a failure: a divisor outside [2^-60, 2^60] (no udiv)
 
 // Thread grid = whole bnd range.  Mask bytes everywhere; row values from column nx_start-1
 // for the rows [ny_start-1, ny_end+1] the stencils read; every point of [nx_start-1,
@@ -801,6 +809,17 @@ struct Prepare {
             const float dx = ld(r4[OCN_DX], q), dy = ld(r4[OCN_DY], q), dxb = ld(r4[OCN_DXB], q), dyb = ld(r4[OCN_DYB], q);
             const float rat[kNumRowRatios] = {dy / dx, dx / dy, dxb / dyb, dyb / dxb};
             for (int k = 0; k < kNumRowRatios; ++k) st(rows, (unsigned)(kNumRowFields + k) * nrows + q.r, rat[k]);
+            const float area = dx * dy;
+            const float g[kNumRecips] = {ld(r4[OCN_DXT], q), ld(r4[OCN_DYH], q), ld(r4[OCN_DXH], q), ld(r4[OCN_DYT], q),
+                                         dxb, dyb, area};
+            double *rc = (double *)(rows + recip_offset(nrows));
+            bool range = true;
+            for (int k = 0; k < kNumRecips; ++k) {
+                st(rc, (unsigned)k * nrows + q.r, 1.0 / (double)g[k]);
+                const float a = g[k] < 0.0f ? -g[k] : g[k];
+                range &= a >= 0x1p-60f && a <= 0x1p60f;   // false for NaN
+            }
+            if (!range) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_DIVISOR_RANGE);
         }
         if (vary) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_METRIC_NOT_ROW_CONSTANT);
     }

@@ -130,7 +130,8 @@ def compact_tables(hst, om):
         blk_ = Block(*b.args, b.bx2 - b.bx1 + 1)
         shape = om.f[k]["lu"].shape
         bits = np.zeros(shape[0] * shape[1], dtype=np.uint8)
-        rows = np.full(N_ROW_FIELDS * shape[1], np.nan, dtype=np.float32)
+        # + the one-pass step's per-row reciprocals (sw_stencils.h recip_offset / row_table_floats)
+        rows = np.full(((N_ROW_FIELDS * shape[1] + 1) & ~1) + 2 * 7 * shape[1], np.nan, dtype=np.float32)
         flags = hst.hst_prepare(C.byref(blk_), table(om.f[k]), bits.ctypes.data, rows.ctypes.data)
         out.append((bits, rows, flags))
     return out
