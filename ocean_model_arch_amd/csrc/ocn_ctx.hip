@@ -1107,6 +1107,104 @@ static bool flip_eligible(ocn_ctx *c)
     return c->flip && c->fused && c->compact && c->march;
 }
 
+// The part of block b's interior the one-pass step covers when halos are exchanged: the interior
+// less w points on each side that has a neighbour block (E, W, N, S; diagonal neighbours only
+// feed the state at the halo corners, which the stencils read as the reference does).
+static Range onepass_inner(const LBlock &b, int w)
+{
+    Range r{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
+    if (b.nbr_rank[1] >= 0) r.m0 += w;   // kDirDm / kDirDn: d = 2 W, 1 E, 4 S, 3 N
+    if (b.nbr_rank[0] >= 0) r.m1 -= w;
+    if (b.nbr_rank[3] >= 0) r.n0 += w;
+    if (b.nbr_rank[2] >= 0) r.n1 -= w;
+    return r;
+}
+
+// A one-pass step with halo exchanges (several blocks or ranks), or with a8 / a9 work on the
+// halo ring.  The one-pass march needs D (hh_init's depths, vort, stresses) at the points next to
+// the ones it updates, formed from the state one point further out; at a halo the reference holds
+// D as exchanged from the neighbour, which would need the neighbour's state TWO points out -- the
+// reference never exchanges that.  So the points one away from an exchanged side take the
+// role-flip path (D stored by CA, exchanged, read back by B) and the rest the one-pass march:
+//   CA frame (hh_init of the previous step + this step's A, on the bands two points deep along
+//   the exchanged sides and their halos) | sync CA || one-pass on the inner part | join |
+//   B on the one-point bands | sync B | swap | ring launch (a8 + a9 on the halo ring)
+// All of a8's filtered sshp / ubrtrp / vbrtrp go to the second buffers (the inner part reads the
+// current ones at neighbours); the ring launch reads the current ones and writes the new ones on
+// the ring after the swap, as the recompute steps do with sshp.
+static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
+{
+    const ocn_sw_params &sw = c->sw;
+    ocn_ctx::Rec rec;
+    Compact t;
+    auto cp = [c](const LBlock &b, Compact &tt) -> const Compact * {
+        tt = Compact{b.bits, b.rows, c->march};
+        return &tt;
+    };
+    int32_t *nbad = k.check ? c->d_nbad : nullptr;
+    hipStream_t s = c->stream;
+    const bool xch = has_exchange(c);
+    const bool ov = xch && overlap_level(c) >= 2 && !c->capturing;
+    // the previous step's hh_init and this step's A on the frames (bnd range outside inner_ca)
+    RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
+    for (const LBlock &b : c->blocks) {
+        Range in = onepass_inner(b, 2);
+        if (b.nbr_rank[1] < 0) in.m0 = b.g.bnd_x1;   // no frame on the sides without a neighbour
+        if (b.nbr_rank[0] < 0) in.m1 = b.g.bnd_x2;
+        if (b.nbr_rank[3] < 0) in.n0 = b.g.bnd_y1;
+        if (b.nbr_rank[2] < 0) in.n1 = b.g.bnd_y2;
+        RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_FRAME, sw, tau, true, false, s,
+                           &in));
+    }
+    RC(timer_end(c, rec));
+    if (xch) {
+        if (ov) RC(fork_sync(c, c->sync_ca_reuse));
+        else RC(run_sync(c, c->sync_ca_reuse));
+    }
+    RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+    for (const LBlock &b : c->blocks) {
+        const Range in = onepass_inner(b, 1);
+        RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
+                          (double *)b.up_alt, (double *)b.vp_alt, s, &in));
+    }
+    RC(timer_end(c, rec));
+    RC(join_sync(c));
+    if (xch) {   // B on the one-point bands along the exchanged sides
+        RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
+        for (const LBlock &b : c->blocks) {
+            const Range in = onepass_inner(b, 1);
+            const Range all{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
+            if (in.m0 == all.m0 && in.m1 == all.m1 && in.n0 == all.n0 && in.n1 == all.n1) continue;
+            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, true, s, nbad, true, false, (double *)b.sshp_alt,
+                              (double *)b.up_alt, (double *)b.vp_alt, &in));
+        }
+        RC(timer_end(c, rec));
+        RC(run_sync(c, c->sync_b));
+    }
+    swap_alt3(c);
+    std::vector<std::vector<void *>> pre;   // the ring launch's field tables (pair roles before the swap)
+    for (const LBlock &b : c->blocks) pre.push_back(b.ptr);
+    swap_roles(c);
+    if (c->ring_sea) {   // a8 + a9 on the ring: the previous sshp / ubrtrp / vbrtrp in, the new ones out
+        RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
+        for (size_t i = 0; i < c->blocks.size(); ++i) {
+            const LBlock &b = c->blocks[i];
+            RC(launch_fused_c1(&b.g, pre[i].data(), (int)pre[i].size(), cp(b, t), OCN_PART_FRAME, sw, nullptr, s,
+                               (const double *)b.sshp_alt, (const double *)b.up_alt, (const double *)b.vp_alt));
+        }
+        RC(timer_end(c, rec));
+    }
+    if (k.next_a) {   // the next step is the last, standard one: hh_init + its fused A, then their sync
+        RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_ALL, sw, tau, k.next_reuse,
+                               false, s));
+        RC(timer_end(c, rec));
+        if (xch) RC(run_sync(c, k.next_reuse ? c->sync_ca_reuse : c->sync_ca));
+    }
+    return OCN_OK;
+}
+
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
     const bool check = k.check, first = k.first, last = k.last, flip = k.flip;
@@ -1127,6 +1225,7 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
     const std::vector<int> &sync_a = reuse ? c->sync_a_reuse : c->sync_a;
     if (flip) {
         if (last) return set_error(OCN_ERR_STATE, "role-flip step on a last step");
+        if (k.one && (has_exchange(c) || c->ring_sea)) return one_step_hybrid(c, tau, k);
         if (k.one) {   // the whole step in one launch (single block: no exchange, no ring launch)
             RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
             for (const LBlock &b : c->blocks)
@@ -1780,8 +1879,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     const bool ca = flip_call && c->sw.full_free_surface == 1;
     // one-pass steps 2..K-1 (single block, no a8 / a9 work on the halo ring, all SW terms on)
     // (no tracers: expl_tracer reads hh_init's hhu / hhv / hhq_p, which a one-pass step keeps in registers)
-    const bool one_call = ca && c->onepass && nsteps >= 3 && c->blocks.size() == 1 && !has_exchange(c) &&
-                          !has_comm(c) && !c->ring_sea && c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 &&
+    const bool one_call = ca && c->onepass && nsteps >= 3 && c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 &&
                           c->sw.use_tracers <= 0 && c->udiv_ok;
     c->one_used = one_call;
     const bool rc_call = ca && c->recompute && !one_call;

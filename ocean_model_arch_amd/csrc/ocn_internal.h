@@ -44,6 +44,11 @@ inline int field_slot(int id) { return is_r4(id) ? id : OCN_NUM_R4 + (id - OCN_S
 constexpr int kNumSlots = OCN_NUM_R4 + OCN_NUM_R8;   // without tracer fields
 constexpr int kMaxTracers = 64;
 
+#ifndef OCN_RANGE_DEFINED   // also in sw_stencils.h
+#define OCN_RANGE_DEFINED
+struct Range { int m0, m1, n0, n1; };   // [m0, m1] x [n0, n1], 1-based global indices
+#endif
+
 // A block's compact static fields (sw_stencils.h): mask bytes (pitch x rows) and metric rows;
 // march: run the stencil launches that have one as register marches (sw_kernels.hip k_march).
 struct Compact {
@@ -61,19 +66,25 @@ int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact
 // flip: the role-flip form (sw_kernels.hip MarchFusedB<true>: + a8's filters and check_ssh_err
 // into flip_nbad on the interior; needs cp->march); rc: hhq / hhu_p / hhv_p recomputed from
 // h_r, ssh, sshp (after a MarchCA<false>, which does not store them)
+// up_out / vp_out / inner (one-pass calls with halo exchanges): the role-flip B on the interior
+// outside *inner, a8's filtered sshp / ubrtrp / vbrtrp into sshp_out / up_out / vp_out
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s,
-                   int32_t *flip_nbad = nullptr, bool flip = false, bool rc = false, double *sshp_out = nullptr);
+                   int32_t *flip_nbad = nullptr, bool flip = false, bool rc = false, double *sshp_out = nullptr,
+                   double *up_out = nullptr, double *vp_out = nullptr, const Range *inner = nullptr);
 // sshp_in: a8 reads sshp there and writes the table's sshp (recompute steps), nullptr = in place
 int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s, const double *sshp_in = nullptr);
+                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s, const double *sshp_in = nullptr,
+                    const double *up_in = nullptr, const double *vp_in = nullptr);
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                     const ocn_sw_params &sw, bool full, hipStream_t s);
 // Role-flip calls: step k's hh_init (non-final) and step k+1's fused A in one launch
 // (sw_kernels.hip MarchCA); next_reuse = step k+1 is a reuse step (else A's a2 stores too);
 // skip_rc = step k+1 is a recompute step (hhq on the interior, hhu_p, hhv_p not stored).
+// inner: only the bnd range outside *inner (the frame of a one-pass step with halo exchanges)
 int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s);
+                    const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s,
+                    const Range *inner = nullptr);
 // floats of a block's compact row table for nrows rows: metric rows, ratios, reciprocals
 // (sw_stencils.h kRowTable, recip_offset)
 size_t row_table_size(unsigned nrows);
@@ -100,8 +111,11 @@ int launch_fill_field(const ocn_block &g, double *p, double v, hipStream_t s);
 // One-pass role-flip step (sw_kernels.hip MarchStep): a1 + fused B + a8's filters + check_ssh_err
 // with hh_init's depths, vort and the stresses formed in registers from the state; single block,
 // no a8 / a9 work on the halo ring; a8's filtered sshp / ubrtrp / vbrtrp go to the given buffers.
+// range: the points it computes (default: the interior) -- with halo exchanges, the part of the
+// interior whose stencils stay off the halos the exchanges fill
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
-                   double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s);
+                   double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
+                   const Range *range = nullptr);
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);

@@ -351,18 +351,22 @@ static Range march_inner(const ocn_block *b)
 {
     return {b->nx_start + 64, b->nx_end - 64, b->ny_start + OCN_MARCH_ROWS, b->ny_end - OCN_MARCH_ROWS};
 }
+// the points of `all` outside `inner`, as up to 4 bands in one launch
+template <typename Body>
+static int launch_march_frame(const ocn_block *b, const Range &all, const Range &inner, const Body &body, hipStream_t s)
+{
+    const Range in = range_clip(all, inner);
+    if (range_empty(in)) return launch_march(b, all, body, s);
+    const Rects q = frame_rects(all, in);
+    Range rs[4];
+    for (int i = 0; i < 4; ++i) rs[i] = {q.m0[i], q.m0[i] + q.w[i] - 1, q.n0[i], q.n0[i] + q.h[i] - 1};
+    return launch_march_rects(b, rs, 4, body, s, OCN_FRAME_ROWS, true);
+}
 template <typename Body>
 static int launch_march_part(const ocn_block *b, const Range &all, int part, const Body &body, hipStream_t s)
 {
     if (part == OCN_PART_INNER) return launch_march(b, range_clip(all, march_inner(b)), body, s);
-    if (part == OCN_PART_FRAME) {
-        const Range in = range_clip(all, march_inner(b));
-        if (range_empty(in)) return launch_march(b, all, body, s);
-        const Rects q = frame_rects(all, in);
-        Range rs[4];
-        for (int i = 0; i < 4; ++i) rs[i] = {q.m0[i], q.m0[i] + q.w[i] - 1, q.n0[i], q.n0[i] + q.h[i] - 1};
-        return launch_march_rects(b, rs, 4, body, s, OCN_FRAME_ROWS, true);
-    }
+    if (part == OCN_PART_FRAME) return launch_march_frame(b, all, march_inner(b), body, s);
     return launch_march(b, all, body, s);
 }
 
@@ -437,13 +441,18 @@ template <bool RC> struct MarchViewB {
 // arithmetic as the hh_init that would have stored them; sshp has not changed since) where
 // llu / llv is set, and the array's never-written value elsewhere.  sshp is read at m+1 / n+1
 // here, so a8's new sshp goes to the second sshp buffer (sshp_out), which the host swaps in.
-template <bool C1F, bool RC = false> struct MarchFusedB {
+// ALT (one-pass calls with halo exchanges, the frame around the one-pass step's inner part): a8's
+// filtered sshp / ubrtrp / vbrtrp all go to the second buffers (sshp_out, up_out, vp_out), as the
+// one-pass step writes them, since it reads the current ones at neighbours.
+template <bool C1F, bool RC = false, bool ALT = false> struct MarchFusedB {
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 1;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; bool full, reuse; int32_t *nbad; double *sshp_out;
+    double *up_out = nullptr, *vp_out = nullptr;
     using View = MarchViewB<RC>;
     struct Fn {
         FusedB<true> k; const Tab<true> &t; SwNextStep<true> a8; HhInit<true> c2; int *nbad; double *sshp_out;
+        double *up_out, *vp_out;
         // row n: ubrtr, vbrtr, hhv, mu, hhu, hhq (RC: h_r and sshp), str_t, ssh at n+1; vort, hhh,
         // str_s, mask bytes (RC: at n+1) and the pointwise operands at n; metric row n+1
         struct Batch { double nn[9], c[3], h[8], p[2]; unsigned bits; float g[kRowTable]; };
@@ -515,9 +524,9 @@ template <bool C1F, bool RC = false> struct MarchFusedB {
                 const double fa = asselin(x.rU.c, un, x.ubrtrp_.v, ts), fb = asselin(x.rV.c, vn, x.vbrtrp_.v, ts);
                 if (L.out) {
                     const bool bl = bc & (1u << OCN_LU);
-                    if (bl) st(RC ? sshp_out : a8.sshp, c, fx);   // RC: sshp is read at neighbours here
-                    if (bc & (1u << OCN_LCU)) st(a8.up, c, fa);
-                    if (bc & (1u << OCN_LCV)) st(a8.vp, c, fb);
+                    if (bl) st(RC || ALT ? sshp_out : a8.sshp, c, fx);   // RC: sshp is read at neighbours here
+                    if (bc & (1u << OCN_LCU)) st(ALT ? up_out : a8.up, c, fa);
+                    if (bc & (1u << OCN_LCV)) st(ALT ? vp_out : a8.vp, c, fb);
                     if (nbad && bl && !(xn < 10000.0 && xn > -10000.0)) OCN_ATOMIC_INC(nbad);
                 }
             }
@@ -530,7 +539,7 @@ template <bool C1F, bool RC = false> struct MarchFusedB {
     __device__ void march(const Lane &L, int nb, int ne) const
     {
         const Fn f{make_fused_b(&b, t, sw, tau, full, reuse), t, make_sw_next_step(&b, t, sw.time_smooth),
-                   make_hh_init(&b, t, (int)sw.full_free_surface, false), (int *)nbad, sshp_out};
+                   make_hh_init(&b, t, (int)sw.full_free_surface, false), (int *)nbad, sshp_out, up_out, vp_out};
         const SwUpdateUv<true> &a7 = f.k.a7;
         View x{};
         x.tau = tau;
@@ -973,7 +982,7 @@ __device__ __forceinline__ unsigned shz(unsigned x, int dx) { return dx == 0 ? x
 // 3 VALU operations instead of the div_scale / rcp / fma / fixup sequence of an IEEE fp64 division
 // (11, one of them quarter rate).  The caller checks the dividend's range (exp_check): a row where
 // any dividend is outside it is computed again with IEEE divisions.  Checked bit for bit against
-// IEEE division on 2e8 random operands (tests/test_udiv.py).
+// IEEE division on random operands over that domain (tests/test_udiv.py).
 __device__ __forceinline__ double udiv(double x, double d, double rd)
 {
     const double q = x * rd;
@@ -1404,10 +1413,21 @@ int launch_fused_a(const ocn_block *b, void *const *ptr, int nptr, const Compact
 
 int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
                    const ocn_sw_params &sw, double tau, bool full, bool reuse, hipStream_t s, int32_t *flip_nbad,
-                   bool flip, bool rc, double *sshp_out)
+                   bool flip, bool rc, double *sshp_out, double *up_out, double *vp_out, const Range *inner)
 {
     if (rc && (!flip || !reuse || sw.full_free_surface != 1 || !sshp_out))
         return set_error(OCN_ERR_ARG, "recomputed depths only on role-flip reuse steps with full_free_surface = 1");
+    if (up_out || vp_out || inner) {   // the frame of a one-pass step with halo exchanges
+        if (!flip || rc || !sshp_out || !up_out || !vp_out || !inner || !use_march(cp))
+            return set_error(OCN_ERR_ARG, "fused B into the second buffers: role-flip, no recompute, three buffers, "
+                                          "a frame, the march");
+        RC_K(check_block(b));
+        const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
+        MarchFusedB<true, false, true> k{*b, t, sw, tau, full, reuse, flip_nbad, sshp_out};
+        k.up_out = up_out;
+        k.vp_out = vp_out;
+        return launch_march_frame(b, range_interior(b), *inner, k, s);
+    }
     if (use_march(cp)) {
         RC_K(check_block(b));
         const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
@@ -1425,9 +1445,11 @@ int launch_fused_b(const ocn_block *b, void *const *ptr, int nptr, const Compact
 }
 
 int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s, const double *sshp_in)
+                    const ocn_sw_params &sw, int32_t *nbad, hipStream_t s, const double *sshp_in,
+                    const double *up_in, const double *vp_in)
 {
-    return launch_fused<KFusedC1>(range_ring(b), range_interior(b), part, b, ptr, nptr, cp, 0, s, sw, nbad, sshp_in);
+    return launch_fused<KFusedC1>(range_ring(b), range_interior(b), part, b, ptr, nptr, cp, 0, s, sw, nbad, sshp_in,
+                                  up_in, vp_in);
 }
 
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
@@ -1444,13 +1466,18 @@ int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compac
 }
 
 int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s)
+                    const ocn_sw_params &sw, double tau_next, bool next_reuse, bool skip_rc, hipStream_t s,
+                    const Range *inner)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || (skip_rc && !next_reuse))
         return set_error(OCN_ERR_ARG, "fused hh_init + A needs the compact tables, the march and full_free_surface = 1");
     RC_K(check_block(b));
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
     const Range r = range_bnd(b);
+    if (inner) {   // the frame of a one-pass step with halo exchanges: the bnd range outside *inner
+        if (skip_rc || !next_reuse) return set_error(OCN_ERR_ARG, "fused CA frame: reuse steps only");
+        return launch_march_frame(b, r, *inner, MarchCA<false, false>{*b, t, sw, tau_next}, s);
+    }
     if (skip_rc) return launch_march_part(b, r, part, MarchCA<false, true>{*b, t, sw, tau_next}, s);
     if (next_reuse) return launch_march_part(b, r, part, MarchCA<false, false>{*b, t, sw, tau_next}, s);
     return launch_march_part(b, r, part, MarchCA<true, false>{*b, t, sw, tau_next}, s);
@@ -1474,7 +1501,8 @@ template <class Body> static int launch_step(const ocn_block *b, const Range &r,
 }
 
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
-                   double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s)
+                   double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
+                   const Range *range)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
@@ -1482,7 +1510,8 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
                                       "ksw_lat on, three second buffers");
     RC_K(check_block(b));
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
-    const Range r = range_interior(b);
+    const Range r = range ? range_clip(range_interior(b), *range) : range_interior(b);
+    if (range_empty(r)) return OCN_OK;
     int ex;
     if (std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020)   // tau = 2^k
         return launch_step(b, r, MarchStep<true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);

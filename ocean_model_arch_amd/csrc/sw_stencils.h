@@ -555,15 +555,15 @@ template <bool C> struct SwNextStep {
     double *__restrict__ ssh, *__restrict__ sshn, *sshp;
     double *__restrict__ u, *__restrict__ un, *__restrict__ up;
     double *__restrict__ v, *__restrict__ vn, *__restrict__ vp;
-    // where sshp is read from when it is filtered into another buffer (ocn_ctx.hip recompute
-    // steps with a8 work on the halo ring); nullptr = in place
-    const double *sshp_in = nullptr;
+    // where sshp / ubrtrp / vbrtrp are read from when they are filtered into other buffers
+    // (ocn_ctx.hip recompute and one-pass steps with a8 work on the halo ring); nullptr = in place
+    const double *sshp_in = nullptr, *up_in = nullptr, *vp_in = nullptr;
     // returns the ssh value after the update (for check_ssh_err)
     OCN_HD OCN_INLINE double step(Pt i) const
     {
         const double x = ld(ssh, i), xn = ld(sshn, i), xp = ld(sshp_in ? sshp_in : sshp, i);
-        const double a = ld(u, i), an = ld(un, i), ap = ld(up, i);
-        const double b = ld(v, i), bn = ld(vn, i), bp = ld(vp, i);
+        const double a = ld(u, i), an = ld(un, i), ap = ld(up_in ? up_in : up, i);
+        const double b = ld(v, i), bn = ld(vn, i), bp = ld(vp_in ? vp_in : vp, i);
         const double fx = asselin(x, xn, xp, ts), fa = asselin(a, an, ap, ts), fb = asselin(b, bn, bp, ts);
         const bool bl = ld(lu, i) > 0.5f;
         if (bl) { st(sshp, i, fx); st(ssh, i, xn); }
@@ -863,7 +863,10 @@ inline int ocn_field_slot(int id) { return id < OCN_NUM_R4 ? id : OCN_NUM_R4 + (
 OCN_HD inline Geo geo(const ocn_block *b) { return Geo{b->bnd_x1, b->bnd_y1, (unsigned)b->pitch}; }
 OCN_HD inline unsigned block_rows(const ocn_block *b) { return (unsigned)(b->bnd_y2 - b->bnd_y1 + 1); }
 
-struct Range { int m0, m1, n0, n1; };
+#ifndef OCN_RANGE_DEFINED   // also in ocn_internal.h
+#define OCN_RANGE_DEFINED
+struct Range { int m0, m1, n0, n1; };   // [m0, m1] x [n0, n1], 1-based global indices
+#endif
 inline Range range_interior(const ocn_block *b) { return {b->nx_start, b->nx_end, b->ny_start, b->ny_end}; }
 inline Range range_ring(const ocn_block *b)
 {
@@ -1093,11 +1096,14 @@ OCN_HD inline FusedB<C> make_fused_b(const ocn_block *b, const Tab<C> &t, const 
 }
 template <bool C>
 OCN_HD inline FusedC1<C> make_fused_c1(const ocn_block *b, const Tab<C> &t, const ocn_sw_params &sw, int32_t *nbad,
-                                       const double *sshp_in = nullptr)
+                                       const double *sshp_in = nullptr, const double *up_in = nullptr,
+                                       const double *vp_in = nullptr)
 {
     FusedC1<C> k{b->nx_start, b->nx_end, b->ny_start, b->ny_end, sw.full_free_surface > 0, (int *)nbad,
                  make_sw_next_step(b, t, sw.time_smooth), make_hh_shift(b, t, sw.time_smooth)};
     k.a8.sshp_in = sshp_in;
+    k.a8.up_in = up_in;
+    k.a8.vp_in = vp_in;
     return k;
 }
 
@@ -1115,8 +1121,8 @@ template <bool C> struct KFusedB {
 };
 template <bool C> struct KFusedC1 {
     ocn_block b; Tab<C> t; ocn_sw_params sw; int32_t *nbad;
-    const double *sshp_in = nullptr;   // see SwNextStep
-    OCN_HD void operator()(int m, int n) const { make_fused_c1(&b, t, sw, nbad, sshp_in)(m, n); }
+    const double *sshp_in = nullptr, *up_in = nullptr, *vp_in = nullptr;   // see SwNextStep
+    OCN_HD void operator()(int m, int n) const { make_fused_c1(&b, t, sw, nbad, sshp_in, up_in, vp_in)(m, n); }
 };
 template <bool C> struct KHhInit {
     ocn_block b; Tab<C> t; int ffs; bool full;
