@@ -294,6 +294,11 @@ struct ocn_ctx {
     // the one-pass steps' second sshp / ubrtrp / vbrtrp buffers agree with the fields outside a8's
     // write set (else they are copied at the start of the next such call)
     mutable bool alt_ok = false;
+    // hh_init's stored depths were formed from the current state (the last step of the previous
+    // call or init_state ran it and nothing has changed the state since): the first step of a
+    // call may then be a one-pass step too, as a reuse step.  Never again once an r8 field's
+    // device pointer was handed out (it may be written behind our back).
+    mutable bool hh_consistent = false, r8_handed = false;
     mutable bool coherent_known = false, r8_escaped = false;
     int role = 0;
     int32_t *d_flags = nullptr;
@@ -1726,6 +1731,7 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
     if (is_r4(id)) c->r4_escaped = true;   // may be written behind our back: no compact tables
     if (is_flip_field(id)) { c->r8_escaped = true; c->coherent_known = false; }
     if (is_alt_field(id)) c->alt_ok = false;
+    if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; }
     return c->blocks[k].ptr[field_slot(id)];
 }
 
@@ -1785,7 +1791,9 @@ int ocn_ctx_init_state(ocn_ctx *c)
     HIPCHK(hipSetDevice(c->dec.device));
     c->coherent_known = false;
     c->alt_ok = false;
-    return lb_fail_on_error(c, init_state(c));
+    const int rc = lb_fail_on_error(c, init_state(c));
+    c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // init_data.f90:60-63 ran hh_init last
+    return rc;
 }
 
 int ocn_ctx_sync(ocn_ctx *c, int field_id)
@@ -1793,6 +1801,7 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
     if (!c || !has_r8(c, field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
     HIPCHK(hipSetDevice(c->dec.device));
     c->coherent_known = false;
+    c->hh_consistent = false;
     return run_sync(c, {field_id});
 }
 
@@ -1803,6 +1812,7 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     if (stage_id < 0 || stage_id >= OCN_NUM_STAGES) return set_error(OCN_ERR_ARG, "bad stage id");
     c->coherent_known = false;
     c->alt_ok = false;
+    c->hh_consistent = false;
     return envoke(c, stage_id, tau);
 }
 
@@ -1879,8 +1889,11 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     const bool ca = flip_call && c->sw.full_free_surface == 1;
     // one-pass steps 2..K-1 (single block, no a8 / a9 work on the halo ring, all SW terms on)
     // (no tracers: expl_tracer reads hh_init's hhu / hhv / hhq_p, which a one-pass step keeps in registers)
-    const bool one_call = ca && c->onepass && nsteps >= 3 && c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 &&
-                          c->sw.use_tracers <= 0 && c->udiv_ok;
+    // (the first step too when hh_init's stored depths match the state: hh_consistent)
+    const bool first_one = c->hh_consistent;
+    const bool one_call = ca && c->onepass && (nsteps >= 3 || (nsteps >= 2 && first_one)) &&
+                          c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 && c->sw.use_tracers <= 0 && c->udiv_ok;
+    c->hh_consistent = false;   // until this call's last step has run
     c->one_used = one_call;
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;
@@ -1908,8 +1921,8 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         k.first = s == 1;
         k.last = s == nsteps;
         k.flip = flip_call && !k.last;
-        k.one = one_call && s >= 2 && s <= nsteps - 1;
-        k.next_one = one_call && s + 1 >= 2 && s + 1 <= nsteps - 1;
+        k.one = one_call && (s >= 2 || first_one) && s <= nsteps - 1;
+        k.next_one = one_call && s + 1 <= nsteps - 1;
         k.a_done = ca && !k.first;
         k.next_a = ca && k.flip && !k.next_one;
         k.next_reuse = k.next_a && s + 1 < nsteps;
@@ -1935,6 +1948,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
                                       c->stream));
         swap_alt3(c);
     }
+    c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // the last step ran a full hh_init
     return rc;
 }
 
@@ -2020,6 +2034,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     if (is_r4(id)) c->static_dirty = true;
     if (is_flip_field(id)) c->coherent_known = false;
     if (is_alt_field(id)) c->alt_ok = false;
+    c->hh_consistent = false;
     return upload_field(c, c->blocks[k], id, host, false);
 }
 
