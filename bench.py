@@ -47,6 +47,7 @@ LAUNCH_BYTES = {
     # one-pass step: ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp, h_r, mu, RHSx, RHSy + mask byte in;
     # sshn, ubrtrn, vbrtrn and the filtered sshp, ubrtrp, vbrtrp out
     "onepass": (129, 129),
+    "onepass_last": (185, 185),   # + vort, str_t, str_s and the four RHS terms out
     "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
     # tracer runs: CA also stores hh_init's hhq_p (read by tran_diff_tracer); per tracer and step:
     # tran_diff_fluxes (lcu, lcv, hhu, hhv, ff, ffp, ubrtr, vbrtr, mu in; flux_x, flux_y out),
@@ -76,9 +77,14 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
                         ("tracer_next_step", "tr_next")] * tracers
         return out
     if one and flip and steps >= 2:   # steps 1 .. K-1 (the state is unchanged since the last call / init)
-        out = [("onepass", "onepass")] * (steps - 1) + [("fused_ca", "ca_hh")]
-        out += [("fused_b", "b_full"), ("fused_c1", "c1"), ("hh_init", "c2_full")]
-        if (steps - 1) % 2:
+        out = [("onepass", "onepass")] * (steps - 1)
+        if ring:   # several blocks: CA + the standard last step
+            out += [("fused_ca", "ca_hh"), ("fused_b", "b_full"), ("fused_c1", "c1"), ("hh_init", "c2_full")]
+            swaps = steps - 1
+        else:      # one block: the last step as one march (+ vort, stresses, RHS terms), a8's copies, hh_init
+            out += [("onepass", "onepass_last"), ("copy", "copy3"), ("hh_init", "c2_full")]
+            swaps = steps
+        if swaps % 2:
             out.append(("copy", "copy3"))
         return out
     out = []

@@ -229,12 +229,12 @@ namespace ocn {
 // one = one-pass step (sw_kernels.hip MarchStep), next_one = the next step is one (this step
 // then runs no hh_init: the one-pass step forms hh_init's values itself).
 struct StepKind {
-    bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next, one, next_one;
+    bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next, one, next_one, one_last;
     bool operator==(const StepKind &o) const
     {
         return check == o.check && first == o.first && last == o.last && flip == o.flip && a_done == o.a_done &&
                next_a == o.next_a && next_reuse == o.next_reuse && rc == o.rc && rc_next == o.rc_next &&
-               one == o.one && next_one == o.next_one;
+               one == o.one && next_one == o.next_one && one_last == o.one_last;
     }
 };
 
@@ -1210,8 +1210,43 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
     return OCN_OK;
 }
 
+// The last step of a single-block one-pass call (no exchange, no a8 / a9 work on the halo ring):
+// the one-pass march that also stores vort, the stresses and the RHS terms (sw_kernels.hip
+// MarchStep<.., true>), the role swaps, a8's copies (ssh := sshn, ubrtr := ubrtrn, vbrtr := vbrtrn:
+// both buffers of each pair end equal, as the reference leaves them), then hh_init with every
+// level (a10; a9's results on its range are rewritten by it).  Replaces CA + fused B + C1 +
+// hh_init of the standard last step.
+static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
+{
+    const ocn_sw_params &sw = c->sw;
+    ocn_ctx::Rec rec;
+    Compact t;
+    auto cp = [c](const LBlock &b, Compact &tt) -> const Compact * {
+        tt = Compact{b.bits, b.rows, c->march};
+        return &tt;
+    };
+    hipStream_t s = c->stream;
+    RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+    for (const LBlock &b : c->blocks)
+        RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.check ? c->d_nbad : nullptr,
+                          (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, true));
+    RC(timer_end(c, rec));
+    swap_alt3(c);
+    swap_roles(c);
+    for (const LBlock &b : c->blocks)
+        for (const auto &pr : {std::make_pair(OCN_SSH, OCN_SSHN), std::make_pair(OCN_UBRTR, OCN_UBRTRN),
+                               std::make_pair(OCN_VBRTR, OCN_VBRTRN)})
+            HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr.second)], b.ptr[field_slot(pr.first)], field_bytes(b),
+                                  hipMemcpyDeviceToDevice, s));
+    RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
+    for (const LBlock &b : c->blocks) RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, true, s));
+    RC(timer_end(c, rec));
+    return OCN_OK;
+}
+
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
+    if (k.one_last) return one_step_last(c, tau, k);
     const bool check = k.check, first = k.first, last = k.last, flip = k.flip;
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
@@ -1838,8 +1873,8 @@ static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
             g.role == c->role) {
             HIPCHK(hipGraphLaunch(g.exec, c->stream));
             if (k.rc) swap_sshp(c);
-            if (k.one) swap_alt3(c);
-            if (k.flip) swap_roles(c);
+            if (k.one || k.one_last) swap_alt3(c);
+            if (k.flip || k.one_last) swap_roles(c);
             return OCN_OK;
         }
     if (c->graphs.size() >= 16) drop_graphs(c);
@@ -1894,6 +1929,8 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     const bool one_call = ca && c->onepass && (nsteps >= 3 || (nsteps >= 2 && first_one)) &&
                           c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 && c->sw.use_tracers <= 0 && c->udiv_ok;
     c->hh_consistent = false;   // until this call's last step has run
+    // the last step as one march + hh_init too (single block, no exchange, no ring work)
+    const bool last_one = one_call && c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) && !c->ring_sea;
     c->one_used = one_call;
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;
@@ -1923,8 +1960,9 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         k.flip = flip_call && !k.last;
         k.one = one_call && (s >= 2 || first_one) && s <= nsteps - 1;
         k.next_one = one_call && s + 1 <= nsteps - 1;
+        k.one_last = last_one && k.last;
         k.a_done = ca && !k.first;
-        k.next_a = ca && k.flip && !k.next_one;
+        k.next_a = ca && k.flip && !k.next_one && !(last_one && s + 1 == nsteps);
         k.next_reuse = k.next_a && s + 1 < nsteps;
         k.rc = rc_call && k.flip && !k.first;
         k.rc_next = rc_call && s + 1 < nsteps;

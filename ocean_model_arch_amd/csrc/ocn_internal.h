@@ -115,7 +115,7 @@ int launch_fill_field(const ocn_block &g, double *p, double v, hipStream_t s);
 // interior whose stencils stay off the halos the exchanges fill
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range = nullptr);
+                   const Range *range = nullptr, bool last = false);
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);

@@ -977,17 +977,21 @@ __device__ __forceinline__ unsigned shz(unsigned x, int dx) { return dx == 0 ? x
 // x / d, correctly rounded, for a wave-uniform divisor d with rd = RN(1 / d) (the row table's
 // reciprocals): q = RN(x rd) is within one ulp of x / d, the residual x - q d is exact in an fma,
 // and RN(q + (x - q d) rd) is the correctly rounded quotient (Markstein's theorem) when nothing
-// underflows: for |d| in [2^-60, 2^60] (launch_prepare flags other divisors, and the one-pass step
+// underflows: for d in [2^-60, 2^60] (launch_prepare flags other divisors, and the one-pass step
 // is then not used) and x = 0 or 2^-900 <= |x| < 2^900 the quotient and the residual are normal.
 // 3 VALU operations instead of the div_scale / rcp / fma / fixup sequence of an IEEE fp64 division
 // (11, one of them quarter rate).  The caller checks the dividend's range (exp_check): a row where
 // any dividend is outside it is computed again with IEEE divisions.  Checked bit for bit against
 // IEEE division on random operands over that domain (tests/test_udiv.py).
+// The residual is formed negated, t = RN(q d - x), and added as RN(q - t rd): the same values as
+// RN(q + (x - q d) rd) for x != 0, and the sign of a zero quotient kept (x = -0: q = -0, t = +0,
+// -0 - 0 = -0), which IEEE division gives and the uv_diff2 terms carry (mu = 0: dividends of +-0).
+// d > 0 (the metrics; launch_prepare flags others).
 __device__ __forceinline__ double udiv(double x, double d, double rd)
 {
     const double q = x * rd;
-    const double e = __builtin_fma(-q, d, x);
-    return __builtin_fma(e, rd, q);
+    const double t = __builtin_fma(q, d, -x);
+    return __builtin_fma(-t, rd, q);
 }
 // the smallest frexp exponent of the dividends of a row (0 for x = 0)
 __device__ __forceinline__ void exp_check(int &acc, double x) { acc = min(acc, __builtin_amdgcn_frexp_exp(x)); }
@@ -1046,7 +1050,12 @@ struct StepRegs {
 // metric id `id` of row n + dy as a double
 #define OCN_MD(id, dy) D(x.met((id), (dy)))
 
-template <bool P2> struct MarchStep {
+// LAST: the last step of a call (ocn_ctx.hip one_step_last): it also stores what the reference's
+// last step leaves in the arrays and no later launch rewrites -- a3's vort and a5's stresses (the
+// values D formed, where the reference stores them: the interior under luu / lu / luu) and the
+// RHS terms a4 / a6 keep on the last step (sw_stencils.h FusedB `full`).  hh_init's and hh_update's
+// levels are not stored: the call's final hh_init rewrites them on the same ranges.
+template <bool P2, bool LAST = false> struct MarchStep {
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
     static constexpr int kWaves = OCN_STEP_WAVES;
@@ -1281,6 +1290,12 @@ template <bool P2> struct MarchStep {
         const double fa = asselin(u, un, x.up.r[1], ts), fb = asselin(v, vn, x.vp.r[1], ts);
         if (!L.out) return;
         const unsigned bc = x.bits.r[1];
+        if (LAST) {
+            if (bc & (1u << OCN_LUU)) { st(t.f(OCN_VORT), c, x.vort.r[1]); st(t.f(OCN_STR_S), c, x.sts.r[1]); }
+            if (bc & (1u << OCN_LU)) st(t.f(OCN_STR_T), c, x.stt.r[1]);
+            if (bc & (1u << OCN_LCU)) { st(t.f(OCN_RHSX_ADV), c, rxa); st(t.f(OCN_RHSX_DIF), c, rxd); }
+            if (bc & (1u << OCN_LCV)) { st(t.f(OCN_RHSY_ADV), c, rya); st(t.f(OCN_RHSY_DIF), c, ryd); }
+        }
         if (bc & (1u << OCN_LU)) {
             st(t.f(OCN_SSHN), c, sshn);
             st(sshp_out, c, fx);
@@ -1523,7 +1538,7 @@ template <class Body> static int launch_step(const ocn_block *b, const Range &r,
 
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range)
+                   const Range *range, bool last)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
@@ -1534,8 +1549,13 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
     const Range r = range ? range_clip(range_interior(b), *range) : range_interior(b);
     if (range_empty(r)) return OCN_OK;
     int ex;
-    if (std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020)   // tau = 2^k
-        return launch_step(b, r, MarchStep<true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
+    const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
+    if (last) {
+        if (range) return set_error(OCN_ERR_ARG, "one-pass last step: whole interior only");
+        if (p2) return launch_step(b, r, MarchStep<true, true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
+        return launch_step(b, r, MarchStep<false, true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
+    }
+    if (p2) return launch_step(b, r, MarchStep<true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
     return launch_step(b, r, MarchStep<false>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
 }
 

@@ -767,7 +767,7 @@ OCN_HD inline unsigned recip_offset(unsigned nrows) { return ((unsigned)kRowTabl
 inline size_t row_table_floats(unsigned nrows) { return recip_offset(nrows) + 2u * (unsigned)kNumRecips * nrows; }
 enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2,
        OCN_COMPACT_RING_SEA = 4,     // not a failure: a8 / a9 write somewhere on the halo ring
-       OCN_COMPACT_DIVISOR_RANGE = 8 };   // not a failure: a divisor outside [2^-60, 2^60] (no udiv)
+       OCN_COMPACT_DIVISOR_RANGE = 8 };   // not a failure: a divisor outside [2^-60, 2^60] (no one-pass step)
 
 // Thread grid = whole bnd range.  Mask bytes everywhere; row values from column nx_start-1
 // for the rows [ny_start-1, ny_end+1] the stencils read; every point of [nx_start-1,
@@ -816,8 +816,7 @@ struct Prepare {
             bool range = true;
             for (int k = 0; k < kNumRecips; ++k) {
                 st(rc, (unsigned)k * nrows + q.r, 1.0 / (double)g[k]);
-                const float a = g[k] < 0.0f ? -g[k] : g[k];
-                range &= a >= 0x1p-60f && a <= 0x1p60f;   // false for NaN
+                range &= g[k] >= 0x1p-60f && g[k] <= 0x1p60f;   // positive; false for NaN
             }
             if (!range) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_DIVISOR_RANGE);
         }

@@ -1,7 +1,7 @@
 """The one-pass step's division by a wave-uniform row metric (sw_kernels.hip udiv: Markstein's
-q = RN(x r), e = x - q d (fma), RN(q + e r) (fma) with r = RN(1/d) from the row table) against
-IEEE division, bit for bit, over the domain the kernel uses it on: d a real(4) metric promoted
-to real(8) with |d| in [2^-60, 2^60] (launch_prepare flags other divisors and the step then
+q = RN(x r), t = RN(q d - x) (fma), RN(q - t r) (fma) with r = RN(1/d) from the row table) against
+IEEE division, bit for bit (signed zeros included), over the domain the kernel uses it on: d a
+real(4) metric promoted to real(8) with d in [2^-60, 2^60] (launch_prepare flags other divisors and the step then
 does not run), x = 0 or 2^-900 <= |x| < 2^900 (the kernel re-runs a row with IEEE divisions
 when a dividend is outside).  fma and IEEE division are correctly rounded on the host as on the
 GPU (v_fma_f64), so the host check pins the arithmetic; the GPU tests pin the kernel."""
@@ -16,7 +16,9 @@ HARNESS = r"""
 static uint64_t s = 0x1234567890abcdefull;
 static inline uint64_t rnd() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
 static inline double asd(uint64_t u) { double x; std::memcpy(&x, &u, 8); return x; }
-static inline double udiv(double x, double d, double r) { double q = x * r; double e = std::fma(-q, d, x); return std::fma(e, r, q); }
+// (volatile: keeps g++ from folding -fma(q, d, -x) into fma(-q, d, x), which loses the sign of
+// a zero residual; the device compiler keeps IEEE signed zeros without fast-math flags)
+static double udiv(double x, double d, double r) { double q = x * r; volatile double t = std::fma(q, d, -x); double mt = -t; return std::fma(mt, r, q); }
 int main(int argc, char **argv) {
     const long n = std::atol(argv[1]);
     long bad = 0;
@@ -26,13 +28,13 @@ int main(int argc, char **argv) {
         if ((i & 31) == 1) fb &= ~0x7fffffu;        // powers of two
         float f; std::memcpy(&f, &fb, 4);
         double d = (double)f;
-        if (rnd() & 1) d = -d;
         uint64_t xb = (rnd() & 0x000fffffffffffffull) | ((uint64_t)(1023 - 900 + rnd() % 1800) << 52);
         if ((i & 7) == 0) xb &= ~0x000ffffffffff000ull;
         if ((i & 7) == 1) xb |= 0x000fffffffffff00ull;
         double x = asd(xb);
         if (rnd() & 1) x = -x;
-        if ((i & 1023) == 7) x = 0.0;
+        if ((i & 63) == 7) x = 0.0;
+        if ((i & 63) == 8) x = -0.0;
         const double r = 1.0 / d, a = x / d, b = udiv(x, d, r);
         if (std::memcmp(&a, &b, 8)) { if (bad < 5) std::printf("x=%a d=%a ieee=%a udiv=%a\n", x, d, a, b); ++bad; }
     }
