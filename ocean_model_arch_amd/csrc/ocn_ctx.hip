@@ -1132,8 +1132,9 @@ static Range onepass_inner(const LBlock &b, int w)
 // reference never exchanges that.  So the points one away from an exchanged side take the
 // role-flip path (D stored by CA, exchanged, read back by B) and the rest the one-pass march:
 //   CA frame (hh_init of the previous step + this step's A, on the bands two points deep along
-//   the exchanged sides and their halos) | sync CA || one-pass on the inner part | join |
-//   B on the one-point bands | sync B | swap | ring launch (a8 + a9 on the halo ring)
+//   the exchanged sides and their halos) | sync CA || one-pass on the inner part's first half |
+//   join | B on the one-point bands | sync B || the inner part's second half | join | swap |
+//   ring launch (a8 + a9 on the halo ring); without overlap the exchanges run in place.
 // All of a8's filtered sshp / ubrtrp / vbrtrp go to the second buffers (the inner part reads the
 // current ones at neighbours); the ring launch reads the current ones and writes the new ones on
 // the ring after the swap, as the recompute steps do with sshp.
@@ -1166,13 +1167,30 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
         if (ov) RC(fork_sync(c, c->sync_ca_reuse));
         else RC(run_sync(c, c->sync_ca_reuse));
     }
-    RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
-    for (const LBlock &b : c->blocks) {
-        const Range in = onepass_inner(b, 1);
-        RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
-                          (double *)b.up_alt, (double *)b.vp_alt, s, &in));
-    }
-    RC(timer_end(c, rec));
+    // with overlap, the inner march in two row halves: one beside sync CA, one beside sync B
+    // (it reads neither what those exchanges write nor what B writes)
+    auto inner_part = [&](const LBlock &b, int half) {
+        Range in = onepass_inner(b, 1);
+        if (ov) {
+            const int mid = (in.n0 + in.n1) / 2;
+            if (half == 0) in.n1 = mid;
+            else in.n0 = mid + 1;
+        } else if (half == 1) {
+            in.n1 = in.n0 - 1;   // empty
+        }
+        return in;
+    };
+    auto inner = [&](int half) -> int {
+        RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+        for (const LBlock &b : c->blocks) {
+            const Range in = inner_part(b, half);
+            RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
+                              (double *)b.up_alt, (double *)b.vp_alt, s, &in));
+        }
+        RC(timer_end(c, rec));
+        return OCN_OK;
+    };
+    RC(inner(0));
     RC(join_sync(c));
     if (xch) {   // B on the one-point bands along the exchanged sides
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
@@ -1184,7 +1202,12 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
                               (double *)b.up_alt, (double *)b.vp_alt, &in));
         }
         RC(timer_end(c, rec));
-        RC(run_sync(c, c->sync_b));
+        if (ov) RC(fork_sync(c, c->sync_b));
+        else RC(run_sync(c, c->sync_b));
+    }
+    if (ov) {
+        RC(inner(1));
+        RC(join_sync(c));
     }
     swap_alt3(c);
     std::vector<std::vector<void *>> pre;   // the ring launch's field tables (pair roles before the swap)
