@@ -299,6 +299,9 @@ struct ocn_ctx {
     // call may then be a one-pass step too, as a reuse step.  Never again once an r8 field's
     // device pointer was handed out (it may be written behind our back).
     mutable bool hh_consistent = false, r8_handed = false;
+    // the one-pass step's fallback points hold +0.0 (sw_kernels.hip FallbackCheck; rechecked after
+    // anything may have written the depth / vort / stress arrays from outside the step)
+    mutable bool fb_zero = false, fb_zero_known = false;
     mutable bool coherent_known = false, r8_escaped = false;
     int role = 0;
     int32_t *d_flags = nullptr;
@@ -1185,7 +1188,7 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
         for (const LBlock &b : c->blocks) {
             const Range in = inner_part(b, half);
             RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
-                              (double *)b.up_alt, (double *)b.vp_alt, s, &in));
+                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, false, c->fb_zero));
         }
         RC(timer_end(c, rec));
         return OCN_OK;
@@ -1252,7 +1255,8 @@ static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
     RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
     for (const LBlock &b : c->blocks)
         RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.check ? c->d_nbad : nullptr,
-                          (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, true));
+                          (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, true,
+                          c->fb_zero));
     RC(timer_end(c, rec));
     swap_alt3(c);
     swap_roles(c);
@@ -1293,7 +1297,8 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
             RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
             for (const LBlock &b : c->blocks)
                 RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad,
-                                  (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s));
+                                  (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, false,
+                                  c->fb_zero));
             RC(timer_end(c, rec));
             swap_alt3(c);
             swap_roles(c);
@@ -1789,7 +1794,7 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
     if (is_r4(id)) c->r4_escaped = true;   // may be written behind our back: no compact tables
     if (is_flip_field(id)) { c->r8_escaped = true; c->coherent_known = false; }
     if (is_alt_field(id)) c->alt_ok = false;
-    if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; }
+    if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_zero_known = false; }
     return c->blocks[k].ptr[field_slot(id)];
 }
 
@@ -1849,6 +1854,7 @@ int ocn_ctx_init_state(ocn_ctx *c)
     HIPCHK(hipSetDevice(c->dec.device));
     c->coherent_known = false;
     c->alt_ok = false;
+    c->fb_zero_known = false;
     const int rc = lb_fail_on_error(c, init_state(c));
     c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // init_data.f90:60-63 ran hh_init last
     return rc;
@@ -1860,6 +1866,7 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
     HIPCHK(hipSetDevice(c->dec.device));
     c->coherent_known = false;
     c->hh_consistent = false;
+    c->fb_zero_known = false;
     return run_sync(c, {field_id});
 }
 
@@ -1871,6 +1878,7 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     c->coherent_known = false;
     c->alt_ok = false;
     c->hh_consistent = false;
+    c->fb_zero_known = false;
     return envoke(c, stage_id, tau);
 }
 
@@ -1955,6 +1963,16 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     // the last step as one march + hh_init too (single block, no exchange, no ring work)
     const bool last_one = one_call && c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) && !c->ring_sea;
     c->one_used = one_call;
+    if (one_call && (!c->fb_zero_known || c->r8_handed)) {   // until something may write the D arrays from outside
+        HIPCHK(hipMemsetAsync(c->d_flags, 0, sizeof(int32_t), c->stream));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fallback_check(&b.g, b.ptr.data(), b.bits, onepass_inner(b, 1), c->d_flags, c->stream));
+        int32_t flag = 0;
+        HIPCHK(hipMemcpyAsync(&flag, c->d_flags, sizeof(flag), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->fb_zero = flag == 0;
+        c->fb_zero_known = true;
+    }
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;
     if (one_call && !c->alt_ok) {   // the second buffers start as copies (they agree outside a8's write set)
@@ -2096,6 +2114,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     if (is_flip_field(id)) c->coherent_known = false;
     if (is_alt_field(id)) c->alt_ok = false;
     c->hh_consistent = false;
+    c->fb_zero_known = false;
     return upload_field(c, c->blocks[k], id, host, false);
 }
 

@@ -1055,7 +1055,11 @@ struct StepRegs {
 // values D formed, where the reference stores them: the interior under luu / lu / luu) and the
 // RHS terms a4 / a6 keep on the last step (sw_stencils.h FusedB `full`).  hh_init's and hh_update's
 // levels are not stored: the call's final hh_init rewrites them on the same ranges.
-template <bool P2, bool LAST = false> struct MarchStep {
+// ZF: every point where D takes the array's value (mask 0, outside the stage's range) holds +0.0
+// in those arrays (checked by launch_fallback_check; true from init on, since no stage ever
+// writes those points): the fallback values are the constant 0 -- no loads, and eight array
+// pointers fewer in the kernel's scalar registers.
+template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
     static constexpr int kWaves = OCN_STEP_WAVES;
@@ -1120,6 +1124,7 @@ template <bool P2, bool LAST = false> struct MarchStep {
         f.st = in && (bc & (1u << OCN_LU));
         f.ss = f.vt;
         f.hu = f.hv = f.hh = f.hu1 = f.hv1 = f.vort = f.stt = f.sts = 0.0;
+        if (ZF) return;
         if (!f.llu) { f.hu = ld(t.f(OCN_HHU), c); f.hu1 = ld(t.f(OCN_HHU_P), c); }
         if (!f.llv) { f.hv = ld(t.f(OCN_HHV), c); f.hv1 = ld(t.f(OCN_HHV_P), c); }
         if (!f.luh) f.hh = ld(t.f(OCN_HHH), c);
@@ -1536,9 +1541,43 @@ template <class Body> static int launch_step(const ocn_block *b, const Range &r,
     return check_launch();
 }
 
+// D's fallback points within r +- 1 (the points the one-pass step over r may take D from
+// memory at) all hold +0.0 in the arrays it would read there: OR 1 into *flag otherwise
+struct FallbackCheck {
+    ocn_block b; const uint8_t *bits; const double *hu, *hu1, *hv, *hv1, *hh, *vort, *stt, *sts; int *flag;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const Pt c = geo(&b)(m, n);
+        const unsigned bc = ld(bits, c);
+        const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && n >= b.ny_start - 1 && n <= b.ny_end;
+        const bool in = m >= b.nx_start && m <= b.nx_end && n >= b.ny_start && n <= b.ny_end;
+        auto nz = [&](const double *p) { return fbits64(ld(p, c)) != 0; };
+        bool bad = false;
+        if (!(hh_rng && (bc & (1u << OCN_LLU)))) bad |= nz(hu) || nz(hu1);
+        if (!(hh_rng && (bc & (1u << OCN_LLV)))) bad |= nz(hv) || nz(hv1);
+        if (!(hh_rng && (bc & (1u << OCN_LUH)))) bad |= nz(hh);
+        if (!(in && (bc & (1u << OCN_LUU)))) bad |= nz(vort) || nz(sts);
+        if (!(in && (bc & (1u << OCN_LU)))) bad |= nz(stt);
+        if (bad) OCN_ATOMIC_OR(flag, 1);
+    }
+};
+
+int launch_fallback_check(const ocn_block *b, void *const *ptr, const uint8_t *bits, const Range &r, int32_t *flag,
+                          hipStream_t s)
+{
+    RC_K(check_block(b));
+    auto f = [&](int id) { return (const double *)ptr[ocn_field_slot(id)]; };
+    const FallbackCheck k{*b, bits, f(OCN_HHU), f(OCN_HHU_P), f(OCN_HHV), f(OCN_HHV_P), f(OCN_HHH), f(OCN_VORT),
+                          f(OCN_STR_T), f(OCN_STR_S), (int *)flag};
+    const int m0 = max(r.m0 - 1, b->bnd_x1), m1 = min(r.m1 + 1, b->bnd_x2);
+    const int n0 = max(r.n0 - 1, b->bnd_y1), n1 = min(r.n1 + 1, b->bnd_y2);
+    if (m0 > m1 || n0 > n1) return OCN_OK;
+    return launch_range(m0, m1, n0, n1, k, s);
+}
+
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range, bool last)
+                   const Range *range, bool last, bool zero_fallback)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
@@ -1550,13 +1589,18 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
     if (range_empty(r)) return OCN_OK;
     int ex;
     const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
-    if (last) {
-        if (range) return set_error(OCN_ERR_ARG, "one-pass last step: whole interior only");
-        if (p2) return launch_step(b, r, MarchStep<true, true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
-        return launch_step(b, r, MarchStep<false, true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
+#define OCN_STEP_LAUNCH(P, L, Z) \
+    return launch_step(b, r, MarchStep<P, L, Z>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s)
+    if (last && range) return set_error(OCN_ERR_ARG, "one-pass last step: whole interior only");
+    if (zero_fallback) {
+        if (last) { if (p2) OCN_STEP_LAUNCH(true, true, true); OCN_STEP_LAUNCH(false, true, true); }
+        if (p2) OCN_STEP_LAUNCH(true, false, true);
+        OCN_STEP_LAUNCH(false, false, true);
     }
-    if (p2) return launch_step(b, r, MarchStep<true>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
-    return launch_step(b, r, MarchStep<false>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s);
+    if (last) { if (p2) OCN_STEP_LAUNCH(true, true, false); OCN_STEP_LAUNCH(false, true, false); }
+    if (p2) OCN_STEP_LAUNCH(true, false, false);
+    OCN_STEP_LAUNCH(false, false, false);
+#undef OCN_STEP_LAUNCH
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy

@@ -104,6 +104,12 @@ OCN_HD OCN_INLINE uint32_t fbits(float f)
     __builtin_memcpy(&u, &f, sizeof(u));
     return u;
 }
+OCN_HD OCN_INLINE uint64_t fbits64(double d)
+{
+    uint64_t u;
+    __builtin_memcpy(&u, &d, 8);
+    return u;
+}
 
 // ------------------------------------------------------------------ views
 // The stage arithmetic is written against a "view" x: x.u(dx, dy) is u(m+dx, n+dy) of the

@@ -422,3 +422,33 @@ def test_blowup_is_reported(amd, nsteps):
     with pytest.raises(amd.OcnError):
         m.step(nsteps, check_every=1).synchronize()
     m.close()
+
+
+@pytest.mark.parametrize("blocks", [(1, 1), (2, 2)])
+def test_onepass_with_nonzero_fallback_values(amd, blocks):
+    """The one-pass step where D takes the arrays' values (mask 0, outside a stage's range) when
+    those are not zero (sw_kernels.hip MarchStep ZF = false: loaded, not the constant 0): hhu,
+    hhv, hhh, vort and the stresses set to nonzero values on the land frame and the halo, then
+    the same call with one-pass steps and with the round-1 role-flip path (pinned to the
+    reference by the other tests), bit for bit."""
+    n, steps = 96, 8
+    out = {}
+    for onepass in (True, False):
+        m = amd.OceanModel(amd.box_config(n), par=amd.ParallelConfig(*blocks)).set_onepass(onepass)
+        m.init()
+        for b in m.blocks:
+            lu = m.download(b.k, "lu")
+            for nm, v in (("hhu", 0.25), ("hhv", 0.5), ("hhh", 0.75), ("vort", 1e-3), ("str_t", 2e-3),
+                          ("str_s", 3e-3), ("hhu_p", 0.125), ("hhv_p", 0.375)):
+                a = m.download(b.k, nm)
+                a[lu < 0.5] = v            # land and the land halo
+                m.upload(b.k, nm, a)
+        m.step(steps, tau=1.0, check_every=1).synchronize()
+        assert m.onepass_active == onepass
+        out[onepass] = [{nm: m.download(x.k, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp",
+                                                            "vbrtr", "vbrtrn", "vbrtrp", "hhu", "hhv", "hhh",
+                                                            "vort", "str_t", "str_s", "RHSx_dif", "RHSy_adv")}
+                        for x in m.blocks]
+        m.close()
+    bad = [(k, nm) for k, d in enumerate(out[True]) for nm, a in d.items() if not bits_equal(a, out[False][k][nm])]
+    assert not bad, f"one-pass with nonzero fallback values differs from the role-flip path: {bad}"
