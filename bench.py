@@ -48,6 +48,8 @@ LAUNCH_BYTES = {
     # sshn, ubrtrn, vbrtrn and the filtered sshp, ubrtrp, vbrtrp out
     "onepass": (129, 129),
     "onepass_last": (185, 185),   # + vort, str_t, str_s and the four RHS terms out
+    # the same with the forcing RHSx / RHSy known to be zero (checked once; not read)
+    "onepass_z": (113, 113), "onepass_last_z": (169, 169),
     "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
     # tracer runs: CA also stores hh_init's hhq_p (read by tran_diff_tracer); per tracer and step:
     # tran_diff_fluxes (lcu, lcv, hhu, hhv, ff, ffp, ubrtr, vbrtr, mu in; flux_x, flux_y out),
@@ -59,7 +61,7 @@ LAUNCH_BYTES = {
 
 
 def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
-                  tracers: int = 0, full_c2: bool = False):
+                  tracers: int = 0, full_c2: bool = False, zero: bool = False):
     """The launches of one ocn_ctx_step call of `steps` steps, as (timer, launch kind) pairs --
     ocn_ctx.hip ocn_ctx_step / one_step_fused for one block (role-flip calls fuse each step's
     hh_init with the next step's A when full_free_surface = 1, as in sw.par; ring = the ring
@@ -77,12 +79,13 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
                         ("tracer_next_step", "tr_next")] * tracers
         return out
     if one and flip and steps >= 2:   # steps 1 .. K-1 (the state is unchanged since the last call / init)
-        out = [("onepass", "onepass")] * (steps - 1)
+        z = "_z" if zero else ""
+        out = [("onepass", "onepass" + z)] * (steps - 1)
         if ring:   # several blocks: CA + the standard last step
             out += [("fused_ca", "ca_hh"), ("fused_b", "b_full"), ("fused_c1", "c1"), ("hh_init", "c2_full")]
             swaps = steps - 1
         else:      # one block: the last step as one march (+ vort, stresses, RHS terms), a8's copies, hh_init
-            out += [("onepass", "onepass_last"), ("copy", "copy3"), ("hh_init", "c2_full")]
+            out += [("onepass", "onepass_last" + z), ("copy", "copy3"), ("hh_init", "c2_full")]
             swaps = steps
         if swaps % 2:
             out.append(("copy", "copy3"))
@@ -106,21 +109,22 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
 
 
 def fused_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False,
-                one: bool = False, tracers: int = 0):
+                one: bool = False, tracers: int = 0, zero: bool = False):
     """Mean bytes per interior cell per launch of each timer over one ocn_ctx_step call."""
     i = 0 if compact else 1
     tot, cnt = {}, {}
-    for timer, kind in call_launches(steps, flip, rc, ring, one, tracers):
+    for timer, kind in call_launches(steps, flip, rc, ring, one, tracers, zero=zero):
         tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
         cnt[timer] = cnt.get(timer, 0) + (kind != "hqp")   # "hqp": bytes of the launch before it
     return {t: tot[t] / cnt[t] for t in tot}
 
 
 def step_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False,
-               one: bool = False, tracers: int = 0):
+               one: bool = False, tracers: int = 0, zero: bool = False):
     """Bytes per interior cell per step moved by one ocn_ctx_step call of `steps` steps."""
     i = 0 if compact else 1
-    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc, ring, one, tracers)) / steps
+    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc, ring, one, tracers,
+                                                                   zero=zero)) / steps
 
 
 def dims_create(n: int):
@@ -336,6 +340,7 @@ def main():
     flip = model.flip_active
     rc = model.recompute_active
     one = model.onepass_active
+    one_zero = model.onepass_zero
     model_overlap = model.overlap_level
     if world > 1:
         t = torch.tensor([dt], device="cuda")
@@ -349,8 +354,8 @@ def main():
     if rank == 0:
         ring = bx * by > 1
         ntr = sw.tracer_num if sw.use_tracers > 0 else 0
-        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc, ring, one, ntr)
-        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring, one, ntr)
+        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc, ring, one, ntr, one_zero)
+        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring, one, ntr, one_zero)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:   # the dominant kernel: the most device time over the timed steps
@@ -376,6 +381,7 @@ def main():
                           "static_fields": "compact" if compact else "2-D arrays",
                           "march": bool(compact and not args.stages and not args.no_march),
                           "role_flip_steps": flip, "recompute_steps": rc, "onepass_steps": one,
+                          "onepass_known_zero_forcing": one_zero,
                           "overlap": model_overlap,
                           "parallelism": (f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else
                                           "1 block" if bx * by == 1 else f"{bx}x{by} blocks, local halo copies")},

@@ -320,13 +320,16 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_RECOMPUTE (default 1): in such calls (full_free_surface = 1, no a8 / a9 work on the
  *  halo ring, so one block without halo exchanges), steps 2..K-1 form hhq, hhu_p, hhv_p inside
  *  fused B instead of storing and re-reading them (same results bit for bit).
- *  OCN_OPT_ONEPASS (default 1): in such calls of K >= 3 steps on ONE block without a8 / a9 work on
- *  the halo ring and with trans_terms and ksw_lat on, steps 2..K-1 run as one launch each: the
- *  state is read once and the next state written once, hh_init's depths, vort and the stresses
- *  formed in registers (same results bit for bit; takes precedence over OCN_OPT_RECOMPUTE).
+ *  OCN_OPT_ONEPASS (default 1): in such calls with trans_terms and ksw_lat on and no tracers,
+ *  steps 2..K-1 run as one launch each: the state is read once and the next state written once,
+ *  hh_init's depths, vort and the stresses formed in registers (same results bit for bit; takes
+ *  precedence over OCN_OPT_RECOMPUTE).  Step 1 too when nothing changed the state since the
+ *  last hh_init; on one block without halo exchanges and a8 / a9 work on the halo ring, the last
+ *  step as well; with halo exchanges, the bands along the exchanged sides run the role-flip path.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
- * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps. */
+ * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
+ * the known-zero forcing and fallback values taken as constants, not read). */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,

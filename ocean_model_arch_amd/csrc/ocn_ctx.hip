@@ -2160,7 +2160,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
     case OCN_OPT_RECOMPUTE: *value = c->recompute && c->rc_used; return OCN_OK;
-    case OCN_OPT_ONEPASS: *value = c->onepass && c->one_used; return OCN_OK;
+    case OCN_OPT_ONEPASS: *value = c->onepass && c->one_used ? (c->fb_zero ? 2 : 1) : 0; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -1056,9 +1056,10 @@ struct StepRegs {
 // RHS terms a4 / a6 keep on the last step (sw_stencils.h FusedB `full`).  hh_init's and hh_update's
 // levels are not stored: the call's final hh_init rewrites them on the same ranges.
 // ZF: every point where D takes the array's value (mask 0, outside the stage's range) holds +0.0
-// in those arrays (checked by launch_fallback_check; true from init on, since no stage ever
-// writes those points): the fallback values are the constant 0 -- no loads, and eight array
-// pointers fewer in the kernel's scalar registers.
+// in those arrays, and the external forcing RHSx / RHSy is +0.0 on the interior (checked by
+// launch_fallback_check; true from init on for the fallback points, since no stage ever writes
+// them, and for the forcing until one is uploaded): those values are the constant +0.0 -- no
+// loads (16 B per cell fewer), and ten array pointers fewer in the kernel's scalar registers.
 template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
@@ -1081,7 +1082,8 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         q.ssh = ld(t.f(OCN_SSH), c2); q.shp = ld(t.f(OCN_SSHP), c2); q.hr = ld(t.f(OCN_HHQ_REST), c2);
         q.bits = ld(t.bits, c2);
         q.v = ld(t.f(OCN_VBRTR), c1); q.vp = ld(t.f(OCN_VBRTRP), c1); q.mu = ld(t.f(OCN_MU), c1);
-        q.rhsx = ld(t.f(OCN_RHSX), c); q.rhsy = ld(t.f(OCN_RHSY), c);
+        if (ZF) q.rhsx = q.rhsy = 0.0;
+        else { q.rhsx = ld(t.f(OCN_RHSX), c); q.rhsy = ld(t.f(OCN_RHSY), c); }
     }
     __device__ __forceinline__ static void take(StepRegs &x, const Batch &q)
     {
@@ -1544,7 +1546,8 @@ template <class Body> static int launch_step(const ocn_block *b, const Range &r,
 // D's fallback points within r +- 1 (the points the one-pass step over r may take D from
 // memory at) all hold +0.0 in the arrays it would read there: OR 1 into *flag otherwise
 struct FallbackCheck {
-    ocn_block b; const uint8_t *bits; const double *hu, *hu1, *hv, *hv1, *hh, *vort, *stt, *sts; int *flag;
+    ocn_block b; const uint8_t *bits; const double *hu, *hu1, *hv, *hv1, *hh, *vort, *stt, *sts, *rx, *ry; int *flag;
+    Range r;   // the points the step updates: RHSx / RHSy are read there
     OCN_HD void operator()(int m, int n) const
     {
         const Pt c = geo(&b)(m, n);
@@ -1558,6 +1561,7 @@ struct FallbackCheck {
         if (!(hh_rng && (bc & (1u << OCN_LUH)))) bad |= nz(hh);
         if (!(in && (bc & (1u << OCN_LUU)))) bad |= nz(vort) || nz(sts);
         if (!(in && (bc & (1u << OCN_LU)))) bad |= nz(stt);
+        if (m >= r.m0 && m <= r.m1 && n >= r.n0 && n <= r.n1) bad |= nz(rx) || nz(ry);
         if (bad) OCN_ATOMIC_OR(flag, 1);
     }
 };
@@ -1568,7 +1572,7 @@ int launch_fallback_check(const ocn_block *b, void *const *ptr, const uint8_t *b
     RC_K(check_block(b));
     auto f = [&](int id) { return (const double *)ptr[ocn_field_slot(id)]; };
     const FallbackCheck k{*b, bits, f(OCN_HHU), f(OCN_HHU_P), f(OCN_HHV), f(OCN_HHV_P), f(OCN_HHH), f(OCN_VORT),
-                          f(OCN_STR_T), f(OCN_STR_S), (int *)flag};
+                          f(OCN_STR_T), f(OCN_STR_S), f(OCN_RHSX), f(OCN_RHSY), (int *)flag, r};
     const int m0 = max(r.m0 - 1, b->bnd_x1), m1 = min(r.m1 + 1, b->bnd_x2);
     const int n0 = max(r.n0 - 1, b->bnd_y1), n1 = min(r.n1 + 1, b->bnd_y2);
     if (m0 > m1 || n0 > n1) return OCN_OK;

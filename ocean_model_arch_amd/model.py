@@ -203,6 +203,11 @@ class OceanModel:
         return bool(self.option(_lib.OPT_ONEPASS))
 
     @property
+    def onepass_zero(self) -> bool:
+        """Whether those steps took the forcing and the fallback values as known zeros (not read)."""
+        return self.option(_lib.OPT_ONEPASS) == 2
+
+    @property
     def compact_active(self) -> bool:
         """Whether the last step() read the compact static fields."""
         return bool(self.option(_lib.OPT_COMPACT))

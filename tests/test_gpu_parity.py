@@ -427,8 +427,9 @@ def test_blowup_is_reported(amd, nsteps):
 @pytest.mark.parametrize("blocks", [(1, 1), (2, 2)])
 def test_onepass_with_nonzero_fallback_values(amd, blocks):
     """The one-pass step where D takes the arrays' values (mask 0, outside a stage's range) when
-    those are not zero (sw_kernels.hip MarchStep ZF = false: loaded, not the constant 0): hhu,
-    hhv, hhh, vort and the stresses set to nonzero values on the land frame and the halo, then
+    those are not zero, and with a forcing (sw_kernels.hip MarchStep ZF = false: loaded, not the
+    constant 0): hhu, hhv, hhh, vort and the stresses set to nonzero values on the land frame and
+    the halo, RHSx / RHSy on the sea, then
     the same call with one-pass steps and with the round-1 role-flip path (pinned to the
     reference by the other tests), bit for bit."""
     n, steps = 96, 8
@@ -442,6 +443,10 @@ def test_onepass_with_nonzero_fallback_values(amd, blocks):
                           ("str_s", 3e-3), ("hhu_p", 0.125), ("hhv_p", 0.375)):
                 a = m.download(b.k, nm)
                 a[lu < 0.5] = v            # land and the land halo
+                m.upload(b.k, nm, a)
+            for nm, v in (("RHSx", 2e-7), ("RHSy", -3e-7)):   # a wind forcing on the sea
+                a = m.download(b.k, nm)
+                a[lu > 0.5] = v
                 m.upload(b.k, nm, a)
         m.step(steps, tau=1.0, check_every=1).synchronize()
         assert m.onepass_active == onepass
