@@ -48,8 +48,9 @@ LAUNCH_BYTES = {
     # sshn, ubrtrn, vbrtrn and the filtered sshp, ubrtrp, vbrtrp out
     "onepass": (129, 129),
     "onepass_last": (185, 185),   # + vort, str_t, str_s and the four RHS terms out
-    # the same with the forcing RHSx / RHSy known to be zero (checked once; not read)
-    "onepass_z": (113, 113), "onepass_last_z": (169, 169),
+    # the same with the forcing RHSx / RHSy known to be zero and h_r, mu known to be uniform
+    # (checked once per call chain; taken as kernel constants, not read)
+    "onepass_z": (97, 97), "onepass_last_z": (153, 153),
     "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
     # tracer runs: CA also stores hh_init's hhq_p (read by tran_diff_tracer); per tracer and step:
     # tran_diff_fluxes (lcu, lcv, hhu, hhv, ff, ffp, ubrtr, vbrtr, mu in; flux_x, flux_y out),
@@ -381,7 +382,7 @@ def main():
                           "static_fields": "compact" if compact else "2-D arrays",
                           "march": bool(compact and not args.stages and not args.no_march),
                           "role_flip_steps": flip, "recompute_steps": rc, "onepass_steps": one,
-                          "onepass_known_zero_forcing": one_zero,
+                          "onepass_known_constants": one_zero,
                           "overlap": model_overlap,
                           "parallelism": (f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else
                                           "1 block" if bx * by == 1 else f"{bx}x{by} blocks, local halo copies")},

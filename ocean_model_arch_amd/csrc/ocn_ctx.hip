@@ -177,6 +177,7 @@ struct LBlock {
     float *rows = nullptr;             // and metric row tables
     void *sshp_alt = nullptr;          // second sshp buffer of the recompute steps (one_step_fused)
     void *up_alt = nullptr, *vp_alt = nullptr;   // second ubrtrp / vbrtrp buffers of the one-pass steps
+    double hr0 = 0.0, mu0 = 0.0;       // h_r, mu where the one-pass step reads them (ctx fb_zero)
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
@@ -1188,7 +1189,7 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
         for (const LBlock &b : c->blocks) {
             const Range in = inner_part(b, half);
             RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
-                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, false, c->fb_zero));
+                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, false, c->fb_zero, b.hr0, b.mu0));
         }
         RC(timer_end(c, rec));
         return OCN_OK;
@@ -1256,7 +1257,7 @@ static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
     for (const LBlock &b : c->blocks)
         RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.check ? c->d_nbad : nullptr,
                           (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, true,
-                          c->fb_zero));
+                          c->fb_zero, b.hr0, b.mu0));
     RC(timer_end(c, rec));
     swap_alt3(c);
     swap_roles(c);
@@ -1298,7 +1299,7 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
             for (const LBlock &b : c->blocks)
                 RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad,
                                   (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, false,
-                                  c->fb_zero));
+                                  c->fb_zero, b.hr0, b.mu0));
             RC(timer_end(c, rec));
             swap_alt3(c);
             swap_roles(c);
@@ -1972,6 +1973,12 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         HIPCHK(hipStreamSynchronize(c->stream));
         c->fb_zero = flag == 0;
         c->fb_zero_known = true;
+        for (LBlock &b : c->blocks) {   // the uniform h_r and mu the check compared against
+            const Range in = onepass_inner(b, 1);
+            const size_t at = (size_t)(in.m0 - b.g.bnd_x1) + (size_t)(in.n0 - b.g.bnd_y1) * b.g.pitch;
+            HIPCHK(hipMemcpy(&b.hr0, b.f<double>(OCN_HHQ_REST) + at, 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&b.mu0, b.f<double>(OCN_MU) + at, 8, hipMemcpyDeviceToHost));
+        }
     }
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;

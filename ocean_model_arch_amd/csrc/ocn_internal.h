@@ -115,9 +115,11 @@ int launch_fill_field(const ocn_block &g, double *p, double v, hipStream_t s);
 // interior whose stencils stay off the halos the exchanges fill
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range = nullptr, bool last = false, bool zero_fallback = false);
+                   const Range *range = nullptr, bool last = false, bool zero_fallback = false,
+                   double hr0 = 0.0, double mu0 = 0.0);
 // zero_fallback precondition of launch_onepass over r (sw_kernels.hip FallbackCheck: the fallback
-// points and the forcing hold +0.0): ORs 1 into *flag where it does not hold
+// points and the forcing hold +0.0, h_r and mu are uniform -- hr0 / mu0 are then their values at
+// (r.m0, r.n0)): ORs 1 into *flag where it does not hold
 int launch_fallback_check(const ocn_block *b, void *const *ptr, const uint8_t *bits, const Range &r, int32_t *flag,
                           hipStream_t s);
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.

@@ -1056,16 +1056,19 @@ struct StepRegs {
 // RHS terms a4 / a6 keep on the last step (sw_stencils.h FusedB `full`).  hh_init's and hh_update's
 // levels are not stored: the call's final hh_init rewrites them on the same ranges.
 // ZF: every point where D takes the array's value (mask 0, outside the stage's range) holds +0.0
-// in those arrays, and the external forcing RHSx / RHSy is +0.0 on the interior (checked by
-// launch_fallback_check; true from init on for the fallback points, since no stage ever writes
-// them, and for the forcing until one is uploaded): those values are the constant +0.0 -- no
-// loads (16 B per cell fewer), and ten array pointers fewer in the kernel's scalar registers.
+// in those arrays, the external forcing RHSx / RHSy is +0.0 on the interior, and the rest depth
+// h_r and the viscosity mu hold one value each over the step's reach (checked by
+// launch_fallback_check; true from init on -- no stage ever writes the fallback points, and
+// init_data.f90 sets h_r = 100 m and mu = 0 everywhere -- until a field is uploaded): those are
+// kernel constants -- no loads (32 B per cell fewer), twelve array pointers fewer in the kernel's
+// scalar registers, and the same arithmetic on the same values.
 template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
     static constexpr int kWaves = OCN_STEP_WAVES;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; int32_t *nbad;
     double *sshp_out, *up_out, *vp_out;   // a8's filtered sshp / ubrtrp / vbrtrp (the second buffers)
+    double hr0 = 0.0, mu0 = 0.0;          // ZF: the values h_r and mu hold at every point the step reads
 
 
     // a / tau (sw_update_uv_math qtau).  P2: tau is a power of two, so a / tau is a * (1 / tau) bit
@@ -1079,9 +1082,10 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const Geo I = geo(&b);
         const Pt c = I(m, n), c1 = I(m, n + 1), c2 = I(m, n + 2);
         q.u = ld(t.f(OCN_UBRTR), c2); q.up = ld(t.f(OCN_UBRTRP), c2);
-        q.ssh = ld(t.f(OCN_SSH), c2); q.shp = ld(t.f(OCN_SSHP), c2); q.hr = ld(t.f(OCN_HHQ_REST), c2);
+        q.ssh = ld(t.f(OCN_SSH), c2); q.shp = ld(t.f(OCN_SSHP), c2);
+        q.hr = ZF ? hr0 : ld(t.f(OCN_HHQ_REST), c2);
         q.bits = ld(t.bits, c2);
-        q.v = ld(t.f(OCN_VBRTR), c1); q.vp = ld(t.f(OCN_VBRTRP), c1); q.mu = ld(t.f(OCN_MU), c1);
+        q.v = ld(t.f(OCN_VBRTR), c1); q.vp = ld(t.f(OCN_VBRTRP), c1); q.mu = ZF ? mu0 : ld(t.f(OCN_MU), c1);
         if (ZF) q.rhsx = q.rhsy = 0.0;
         else { q.rhsx = ld(t.f(OCN_RHSX), c); q.rhsy = ld(t.f(OCN_RHSY), c); }
     }
@@ -1330,7 +1334,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         {
             const Pt c = I(L.m, n0), c1 = I(L.m, n0 + 1);
             x.up.r[2] = ld(t.f(OCN_UBRTRP), c1); x.ssh.r[2] = ld(t.f(OCN_SSH), c1);
-            x.shp.r[2] = ld(t.f(OCN_SSHP), c1); x.hr.r[2] = ld(t.f(OCN_HHQ_REST), c1);
+            x.shp.r[2] = ld(t.f(OCN_SSHP), c1); x.hr.r[2] = ZF ? hr0 : ld(t.f(OCN_HHQ_REST), c1);
             x.bits.r[2] = ld(t.bits, c1); x.u.r[2] = ld(t.f(OCN_UBRTR), c1);
             x.vp.r[1] = ld(t.f(OCN_VBRTRP), c);
             // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
@@ -1548,9 +1552,13 @@ template <class Body> static int launch_step(const ocn_block *b, const Range &r,
 struct FallbackCheck {
     ocn_block b; const uint8_t *bits; const double *hu, *hu1, *hv, *hv1, *hh, *vort, *stt, *sts, *rx, *ry; int *flag;
     Range r;   // the points the step updates: RHSx / RHSy are read there
+    const double *hr, *mu;   // uniform over r +- 2 (h_r) / r +- 1 (mu): equal to their values at (r.m0, r.n0)
     OCN_HD void operator()(int m, int n) const
     {
-        const Pt c = geo(&b)(m, n);
+        const Pt c = geo(&b)(m, n), c0 = geo(&b)(r.m0, r.n0);
+        if (fbits64(ld(hr, c)) != fbits64(ld(hr, c0))) OCN_ATOMIC_OR(flag, 1);
+        if (m < r.m0 - 1 || m > r.m1 + 1 || n < r.n0 - 1 || n > r.n1 + 1) return;   // the ring of r +- 2
+        if (fbits64(ld(mu, c)) != fbits64(ld(mu, c0))) OCN_ATOMIC_OR(flag, 1);
         const unsigned bc = ld(bits, c);
         const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && n >= b.ny_start - 1 && n <= b.ny_end;
         const bool in = m >= b.nx_start && m <= b.nx_end && n >= b.ny_start && n <= b.ny_end;
@@ -1572,16 +1580,17 @@ int launch_fallback_check(const ocn_block *b, void *const *ptr, const uint8_t *b
     RC_K(check_block(b));
     auto f = [&](int id) { return (const double *)ptr[ocn_field_slot(id)]; };
     const FallbackCheck k{*b, bits, f(OCN_HHU), f(OCN_HHU_P), f(OCN_HHV), f(OCN_HHV_P), f(OCN_HHH), f(OCN_VORT),
-                          f(OCN_STR_T), f(OCN_STR_S), f(OCN_RHSX), f(OCN_RHSY), (int *)flag, r};
-    const int m0 = max(r.m0 - 1, b->bnd_x1), m1 = min(r.m1 + 1, b->bnd_x2);
-    const int n0 = max(r.n0 - 1, b->bnd_y1), n1 = min(r.n1 + 1, b->bnd_y2);
+                          f(OCN_STR_T), f(OCN_STR_S), f(OCN_RHSX), f(OCN_RHSY), (int *)flag, r, f(OCN_HHQ_REST),
+                          f(OCN_MU)};
+    const int m0 = max(r.m0 - 2, b->bnd_x1), m1 = min(r.m1 + 2, b->bnd_x2);
+    const int n0 = max(r.n0 - 2, b->bnd_y1), n1 = min(r.n1 + 2, b->bnd_y2);
     if (m0 > m1 || n0 > n1) return OCN_OK;
     return launch_range(m0, m1, n0, n1, k, s);
 }
 
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range, bool last, bool zero_fallback)
+                   const Range *range, bool last, bool zero_fallback, double hr0, double mu0)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
@@ -1594,7 +1603,7 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
     int ex;
     const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
 #define OCN_STEP_LAUNCH(P, L, Z) \
-    return launch_step(b, r, MarchStep<P, L, Z>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out}, s)
+    return launch_step(b, r, MarchStep<P, L, Z>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out, hr0, mu0}, s)
     if (last && range) return set_error(OCN_ERR_ARG, "one-pass last step: whole interior only");
     if (zero_fallback) {
         if (last) { if (p2) OCN_STEP_LAUNCH(true, true, true); OCN_STEP_LAUNCH(false, true, true); }

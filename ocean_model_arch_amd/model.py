@@ -204,7 +204,8 @@ class OceanModel:
 
     @property
     def onepass_zero(self) -> bool:
-        """Whether those steps took the forcing and the fallback values as known zeros (not read)."""
+        """Whether those steps took the forcing, the fallback values (known zeros) and h_r, mu (known
+        uniform) as kernel constants instead of reading them."""
         return self.option(_lib.OPT_ONEPASS) == 2
 
     @property
