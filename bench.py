@@ -257,6 +257,8 @@ def main():
     ap.add_argument("--no-flip", action="store_true", help="standard steps only (no role-flip steps)")
     ap.add_argument("--no-recompute", action="store_true", help="role-flip calls without the recompute steps")
     ap.add_argument("--no-onepass", action="store_true", help="role-flip calls without the one-pass steps")
+    ap.add_argument("--no-known-constants", action="store_true",
+                    help="one-pass steps in their general variant only (no known-constant specialization)")
     ap.add_argument("--overlap", type=int, default=-1, choices=[-1, 0, 1, 2],
                     help="halo exchanges beside inner launches: 0 never, 1 standard steps, 2 role-flip steps too, "
                          "-1 the library default (2 with RCCL peers, else 1)")
@@ -317,6 +319,7 @@ def main():
     model.set_flip(not args.no_flip)
     model.set_recompute(not args.no_recompute)
     model.set_onepass(not args.no_onepass)
+    model.set_known_constants(not args.no_known_constants)
     model.set_overlap(args.overlap)
     if args.graph:
         model.set_graph(True)

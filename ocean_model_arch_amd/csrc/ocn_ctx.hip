@@ -291,6 +291,7 @@ struct ocn_ctx {
     bool udiv_ok = true;    // every row divisor of the one-pass step in [2^-60, 2^60] (Prepare)
     bool recompute = true;  // OCN_OPT_RECOMPUTE: recompute steps in role-flip calls
     bool onepass = true;    // OCN_OPT_ONEPASS: one-pass steps in single-block role-flip calls
+    bool known_const = true;   // OCN_OPT_KNOWN_CONSTANTS: the one-pass step's known-constant variant
     bool one_used = false;
     // the one-pass steps' second sshp / ubrtrp / vbrtrp buffers agree with the fields outside a8's
     // write set (else they are copied at the start of the next such call)
@@ -1971,7 +1972,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         int32_t flag = 0;
         HIPCHK(hipMemcpyAsync(&flag, c->d_flags, sizeof(flag), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        c->fb_zero = flag == 0;
+        c->fb_zero = flag == 0 && c->known_const;
         c->fb_zero_known = true;
         for (LBlock &b : c->blocks) {   // the uniform h_r and mu the check compared against
             const Range in = onepass_inner(b, 1);
@@ -2146,6 +2147,10 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     case OCN_OPT_FLIP: c->flip = value != 0; return OCN_OK;
     case OCN_OPT_RECOMPUTE: c->recompute = value != 0; return OCN_OK;
     case OCN_OPT_ONEPASS: c->onepass = value != 0; return OCN_OK;
+    case OCN_OPT_KNOWN_CONSTANTS:
+        c->known_const = value != 0;
+        c->fb_zero_known = false;   // checked again at the next one-pass call
+        return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -2168,6 +2173,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
     case OCN_OPT_RECOMPUTE: *value = c->recompute && c->rc_used; return OCN_OK;
     case OCN_OPT_ONEPASS: *value = c->onepass && c->one_used ? (c->fb_zero ? 2 : 1) : 0; return OCN_OK;
+    case OCN_OPT_KNOWN_CONSTANTS: *value = c->known_const; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -242,6 +242,10 @@ struct MarchGrid { int nr, ntiles; MarchRect r[4]; };
 template <class B, class = void> struct WavesOf { static constexpr int v = OCN_MARCH_LB; };
 template <class B> struct WavesOf<B, std::void_t<decltype(B::kWaves)>> { static constexpr int v = B::kWaves; };
 
+// a body with a workgroup prologue (Body::prologue(R, ty), called by all 4 waves of a workgroup)
+template <class B, class = void> struct HasPrologue { static constexpr bool v = false; };
+template <class B> struct HasPrologue<B, std::void_t<decltype(B::kPrologue)>> { static constexpr bool v = B::kPrologue; };
+
 template <class Body>
 __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Body body)
 {
@@ -260,6 +264,7 @@ __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Bo
     constexpr int cols = Body::kAligned ? 64 : 64 - 2 * Body::kHalo;
     const int mw = R.w0 + (R.vert ? tx : tx * 4 + wave) * cols;   // first output column of this wave
     const int nb = R.n0 + (R.vert ? ty * 4 + wave : ty) * R.rows, ne = min(R.n1, nb + R.rows - 1);
+    if constexpr (HasPrologue<Body>::v) body.prologue(R, ty);     // all 4 waves (a barrier)
     if (mw > R.m1 || nb > R.n1) return;                            // wave-uniform
     Lane L;
     if (Body::kAligned) {
@@ -997,6 +1002,69 @@ __device__ __forceinline__ double udiv(double x, double d, double rd)
 __device__ __forceinline__ void exp_check(int &acc, double x) { acc = min(acc, __builtin_amdgcn_frexp_exp(x)); }
 constexpr int kUdivMinExp = -899;   // frexp exponent >= -899  <=>  |x| >= 2^-900
 
+// The row-uniform operands of the one-pass step, per row r, as the doubles the arithmetic uses
+// (each formed exactly as the step forms it from the real(4) row table: promoted metrics, the
+// real(4) products and sums of metrics, the reciprocals of udiv's divisors).  OCN_STEP_LDS: a
+// workgroup forms them once for its rows into LDS (MarchStep::prologue, a thread per row) and
+// its waves read them there (broadcast ds_read: no scalar loads, conversions or SGPR spills;
+// 0.554 -> 0.480 ms per 4096^2 step); else they are formed from scalar loads of the row table
+// where used.  The general variant keeps the scalar loads: with its loaded h_r, mu, forcing and
+// fallback values, the LDS operands push it into VGPR spills.
+enum RowC { RC_DX, RC_DY, RC_DXT, RC_DYT, RC_DXH, RC_DYH, RC_DXB, RC_DYB, RC_RDXT, RC_RDYH, RC_RDXH, RC_RDYT,
+            RC_RDXB, RC_RDYB, RC_RAT0, RC_RAT1, RC_RAT2, RC_RAT3, RC_RLH, RC_DY2, RC_DX2, RC_AREA, RC_RAREA,
+            RC_DXB2, RC_DYB2, RC_RDSELF, RC_RDNEXT, kRowC };
+#ifndef OCN_STEP_LDS
+#define OCN_STEP_LDS 1
+#endif
+#ifndef OCN_STEP_LDS_GENERAL
+#define OCN_STEP_LDS_GENERAL 0   // also in the general variant (its VGPRs spill: 0.83 vs 0.64 ms at 4096^2)
+#endif
+constexpr int kStepLdsRows = 4 * OCN_STEP_ROWS + 4;   // a workgroup's 4 stacked tiles + 2 rows each side
+
+#if OCN_STEP_LDS
+__shared__ double g_step_rc[kStepLdsRows * kRowC];   // the workgroup's rows [nb - 2, ne + 2]
+__shared__ unsigned g_step_rlo;                       // table row of its first row
+#endif
+
+// row constant k of table row r (rows[(id - OCN_DX) * nrows + r], real(4)); r + 1 for RC_RDNEXT
+__device__ __forceinline__ double row_const(const float *rows, unsigned nrows, unsigned r, int k)
+{
+    auto g = [&](int id) { return rows[(unsigned)(id - OCN_DX) * nrows + r]; };
+    auto rc = [&](int j) { return ((const double *)(rows + recip_offset(nrows)))[(unsigned)j * nrows + r]; };
+    switch (k) {
+    case RC_DX: return D(g(OCN_DX));
+    case RC_DY: return D(g(OCN_DY));
+    case RC_DXT: return D(g(OCN_DXT));
+    case RC_DYT: return D(g(OCN_DYT));
+    case RC_DXH: return D(g(OCN_DXH));
+    case RC_DYH: return D(g(OCN_DYH));
+    case RC_DXB: return D(g(OCN_DXB));
+    case RC_DYB: return D(g(OCN_DYB));
+    case RC_RDXT: return rc(OCN_RC_DXT);
+    case RC_RDYH: return rc(OCN_RC_DYH);
+    case RC_RDXH: return rc(OCN_RC_DXH);
+    case RC_RDYT: return rc(OCN_RC_DYT);
+    case RC_RDXB: return rc(OCN_RC_DXB);
+    case RC_RDYB: return rc(OCN_RC_DYB);
+    case RC_RAT0: case RC_RAT1: case RC_RAT2: case RC_RAT3:
+        return D(rows[(unsigned)(kNumRowFields + k - RC_RAT0) * nrows + r]);
+    case RC_RLH: return D(g(OCN_RLH_S));
+    case RC_DY2: { const float a = g(OCN_DY); return D(a * a); }
+    case RC_DX2: { const float a = g(OCN_DX); return D(a * a); }
+    case RC_AREA: { const float a = g(OCN_DX) * g(OCN_DY); return D(a); }
+    case RC_RAREA: return rc(OCN_RC_AREA);
+    case RC_DXB2: { const float a = g(OCN_DXB); return D(a * a); }
+    case RC_DYB2: { const float a = g(OCN_DYB); return D(a * a); }
+    case RC_RDSELF: { const float a = g(OCN_R_DISS); const float rd = a + a; return D(rd); }
+    case RC_RDNEXT: {
+        const float a = g(OCN_R_DISS), an = rows[(unsigned)(OCN_R_DISS - OCN_DX) * nrows + min(r + 1, nrows - 1)];
+        const float rd = a + an;
+        return D(rd);
+    }
+    default: return 0.0;
+    }
+}
+
 struct StepRegs {
     template <class T> struct Win {   // rows n-1, n, n+1, n+2 at this lane's column
         T r[4];
@@ -1023,6 +1091,49 @@ struct StepRegs {
     unsigned nrows, rn;               // table stride, row index of n (n - bnd_y1)
     double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
     double tau, inv_tau, f;
+    const __attribute__((address_space(3))) double *lds;   // OCN_STEP_LDS: the workgroup's row constants
+    unsigned rlo;                                            // table row of lds row 0
+    // row constant k (RowC) of row n + dy, from LDS or from scalar loads
+    template <bool LDS> __device__ __forceinline__ double cst(int k, int dy) const
+    {
+        if (LDS) return lds[(rn + dy - rlo) * kRowC + k];
+        switch (k) {   // the same values from scalar loads of the row table
+        case RC_RDXT: return rc(OCN_RC_DXT, dy);
+        case RC_RDYH: return rc(OCN_RC_DYH, dy);
+        case RC_RDXH: return rc(OCN_RC_DXH, dy);
+        case RC_RDYT: return rc(OCN_RC_DYT, dy);
+        case RC_RDXB: return rc(OCN_RC_DXB, dy);
+        case RC_RDYB: return rc(OCN_RC_DYB, dy);
+        case RC_RAREA: return rc(OCN_RC_AREA, dy);
+        default: break;
+        }
+        return row_const_s(k, dy);
+    }
+    // (OCN_STEP_LDS 0) row constant k from scalar loads
+    __device__ __forceinline__ double row_const_s(int k, int dy) const
+    {
+        auto g = [&](int id) { return met(id, dy); };
+        switch (k) {
+        case RC_DX: return D(g(OCN_DX));
+        case RC_DY: return D(g(OCN_DY));
+        case RC_DXT: return D(g(OCN_DXT));
+        case RC_DYT: return D(g(OCN_DYT));
+        case RC_DXH: return D(g(OCN_DXH));
+        case RC_DYH: return D(g(OCN_DYH));
+        case RC_DXB: return D(g(OCN_DXB));
+        case RC_DYB: return D(g(OCN_DYB));
+        case RC_RAT0: case RC_RAT1: case RC_RAT2: case RC_RAT3: return D(met(OCN_DX + kNumRowFields + k - RC_RAT0, dy));
+        case RC_RLH: return D(g(OCN_RLH_S));
+        case RC_DY2: { const float a = g(OCN_DY); return D(a * a); }
+        case RC_DX2: { const float a = g(OCN_DX); return D(a * a); }
+        case RC_AREA: { const float a = g(OCN_DX) * g(OCN_DY); return D(a); }
+        case RC_DXB2: { const float a = g(OCN_DXB); return D(a * a); }
+        case RC_DYB2: { const float a = g(OCN_DYB); return D(a * a); }
+        case RC_RDSELF: { const float a = g(OCN_R_DISS); const float rd = a + a; return D(rd); }
+        case RC_RDNEXT: { const float rd = g(OCN_R_DISS) + met(OCN_R_DISS, dy + 1); return D(rd); }
+        default: return 0.0;
+        }
+    }
     __device__ __forceinline__ float met(int id, int dy) const
     {
         return rows[(unsigned)(id - OCN_DX) * nrows + __builtin_amdgcn_readfirstlane(rn + dy)];
@@ -1104,7 +1215,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     __device__ __forceinline__ static void weights(StepRegs &x, int dy)
     {
         const int k = dy + 1;
-        const double gx = OCN_MD(OCN_DX, dy), gy = OCN_MD(OCN_DY, dy);
+        const double gx = x.cst<kLds>(RC_DX, dy), gy = x.cst<kLds>(RC_DY, dy);
         const double l = D(x.mk(OCN_LU, 0, dy));
         x.w0.r[k] = (x.hr.r[k] + x.ssh.r[k] * x.f) * gx * gy * l;
         x.w1.r[k] = (x.hr.r[k] + x.shp.r[k] * x.f) * gx * gy * l;
@@ -1155,13 +1266,13 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const float l00 = x.mk(OCN_LU, 0, 1), l10 = x.mk(OCN_LU, 1, 1), l01 = x.mk(OCN_LU, 0, 2),
                     l11 = x.mk(OCN_LU, 1, 2);
         const double su = D(l00 + l10), sv = D(l00 + l01), sh4 = D(l00 + l10 + l01 + l11);
-        const double dxt = OCN_MD(OCN_DXT, 1), dyt = OCN_MD(OCN_DYT, 1), dxh = OCN_MD(OCN_DXH, 1),
-                     dyh = OCN_MD(OCN_DYH, 1), dxb = OCN_MD(OCN_DXB, 1), dyb = OCN_MD(OCN_DYB, 1);
+        const double dxt = x.cst<kLds>(RC_DXT, 1), dyt = x.cst<kLds>(RC_DYT, 1), dxh = x.cst<kLds>(RC_DXH, 1),
+                     dyh = x.cst<kLds>(RC_DYH, 1), dxb = x.cst<kLds>(RC_DXB, 1), dyb = x.cst<kLds>(RC_DYB, 1);
         const double w00 = x.w0.r[2], w10 = shz(w00, 1), w01 = x.w0.r[3], w11 = shz(w01, 1);
         const double p00 = x.w1.r[2], p10 = shz(p00, 1), p01 = x.w1.r[3];
         const double s0 = w00 + w10;
-        const double rxt = x.rc(OCN_RC_DXT, 1), ryh = x.rc(OCN_RC_DYH, 1), rxh = x.rc(OCN_RC_DXH, 1),
-                     ryt = x.rc(OCN_RC_DYT, 1);
+        const double rxt = x.cst<kLds>(RC_RDXT, 1), ryh = x.cst<kLds>(RC_RDYH, 1), rxh = x.cst<kLds>(RC_RDXH, 1),
+                     ryt = x.cst<kLds>(RC_RDYT, 1);
         const double a_u0 = div_mask_sum(s0, su), a_v0 = div_mask_sum(w00 + w01, sv),
                      a_h0 = div_mask_sum(s0 + w01 + w11, sh4), a_u1 = div_mask_sum(p00 + p10, su),
                      a_v1 = div_mask_sum(p00 + p01, sv);
@@ -1171,23 +1282,21 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         }
         const double u0 = dv<E>(dv<E>(a_u0, dxt, rxt), dyh, ryh);
         const double v0 = dv<E>(dv<E>(a_v0, dxh, rxh), dyt, ryt);
-        const double h0 = dv<E>(dv<E>(a_h0, dxb, x.rc(OCN_RC_DXB, 1)), dyb, x.rc(OCN_RC_DYB, 1));
+        const double h0 = dv<E>(dv<E>(a_h0, dxb, x.cst<kLds>(RC_RDXB, 1)), dyb, x.cst<kLds>(RC_RDYB, 1));
         const double u1 = dv<E>(dv<E>(a_u1, dxt, rxt), dyh, ryh);
         const double v1 = dv<E>(dv<E>(a_v1, dxh, rxh), dyt, ryt);
         // a3 uv_trans_vort (vel_ssh.f90:247-281, sw_stencils.h uv_trans_vort_math)
         const double u_0 = x.u.r[2], u_1 = x.u.r[3], v_0 = x.v.r[2], v_r = shz(v_0, 1);
-        const double vort = (v_r * dyt - v_0 * dyt) - (u_1 * OCN_MD(OCN_DXT, 2) - u_0 * dxt)
+        const double vort = (v_r * dyt - v_0 * dyt) - (u_1 * x.cst<kLds>(RC_DXT, 2) - u_0 * dxt)
                             - ((v_r - v_0) * dyb - (u_1 - u_0) * dxb);
         // a5 (mixing.f90:33-44, sw_stencils.h stress_components_math) with its quotients shared:
         // up/dyh at m-1 is the left lane's up/dyh (dyh is constant along the row), vp/dxh at n-1
         // is the previous row's, up/dxt at n+1 the next row's (formed here, kept for the next
         // row), vp/dyt at m+1 the right lane's -- the same operands, so the same values
         const double qa = dv<E>(x.up.r[2], dyh, ryh), qb = dv<E>(x.vp.r[2], dxh, rxh);
-        const double qc1 = dv<E>(x.up.r[3], OCN_MD(OCN_DXT, 2), x.rc(OCN_RC_DXT, 2)), qe = dv<E>(x.vp.r[2], dyt, ryt);
-        const double st = D(x.met(OCN_DX + kNumRowFields + 0, 1)) * (qa - shz(qa, -1))
-                          - D(x.met(OCN_DX + kNumRowFields + 1, 1)) * (qb - x.qb);
-        const double ss = D(x.met(OCN_DX + kNumRowFields + 2, 1)) * (qc1 - x.qc)
-                          + D(x.met(OCN_DX + kNumRowFields + 3, 1)) * (shz(qe, 1) - qe);
+        const double qc1 = dv<E>(x.up.r[3], x.cst<kLds>(RC_DXT, 2), x.cst<kLds>(RC_RDXT, 2)), qe = dv<E>(x.vp.r[2], dyt, ryt);
+        const double st = x.cst<kLds>(RC_RAT0, 1) * (qa - shz(qa, -1)) - x.cst<kLds>(RC_RAT1, 1) * (qb - x.qb);
+        const double ss = x.cst<kLds>(RC_RAT2, 1) * (qc1 - x.qc) + x.cst<kLds>(RC_RAT3, 1) * (shz(qe, 1) - qe);
         qb_next = qb;
         qc_next = qc1;
         const double hu = fb.llu ? u0 : fb.hu;
@@ -1205,13 +1314,12 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         x.pv.r[2] = v_0 * dxh * hv;                                  // uv_trans: v * dxh * hv
         x.vh.r[2] = vt * hh;                                         // uv_trans: vort * hh
         x.t3.r[2] = v_0 * hv * dxh;                                  // sw_update_ssh: vbrtr * hhv * dxh
-        const double rr = D(x.met(OCN_RLH_S, 1)) * hh * dxb * dyb;   // sw_update_uv: rlh_s * hhh * dxb * dyb
+        const double rr = x.cst<kLds>(RC_RLH, 1) * hh * dxb * dyb;   // sw_update_uv: rlh_s * hhh * dxb * dyb
         x.rr.r[2] = rr;
         x.cx.r[2] = rr * (v_r + v_0);                                //   ... * (vbrtr(1,0) + vbrtr)
         const double hq = x.hr.r[2] + x.ssh.r[2] * x.f;              // depth.f90:48 hq = h_r + sh*ffs
-        const float gy = x.met(OCN_DY, 1), gx = x.met(OCN_DX, 1);
-        x.dt.r[2] = D(gy * gy) * x.mu.r[2] * hq * stt;               // uv_diff2: dy**2 * mu * hq * str_t
-        x.dxq.r[2] = D(gx * gx) * x.mu.r[2] * hq * stt;              // uv_diff2: dx**2 * mu * hq * str_t
+        x.dt.r[2] = x.cst<kLds>(RC_DY2, 1) * x.mu.r[2] * hq * stt;         // uv_diff2: dy**2 * mu * hq * str_t
+        x.dxq.r[2] = x.cst<kLds>(RC_DX2, 1) * x.mu.r[2] * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
     }
 
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
@@ -1221,14 +1329,13 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const Geo I = geo(&b);
         const Pt c = I(L.m, n);
         const double u = x.u.r[1], v = x.v.r[1], hu = x.hu.r[1], hv = x.hv.r[1], hh = x.hh.r[1];
-        const double dxt = OCN_MD(OCN_DXT, 0), dyt = OCN_MD(OCN_DYT, 0), dxh = OCN_MD(OCN_DXH, 0),
-                     dyh = OCN_MD(OCN_DYH, 0);
+        const double dxt = x.cst<kLds>(RC_DXT, 0), dyt = x.cst<kLds>(RC_DYT, 0), dxh = x.cst<kLds>(RC_DXH, 0),
+                     dyh = x.cst<kLds>(RC_DYH, 0);
         // a1 sw_update_ssh (vel_ssh.f90:69-106)
         const double t1 = u * hu * dyh;
-        const float area = x.met(OCN_DX, 0) * x.met(OCN_DY, 0);
         const double a_ssh = t1 - shz(t1, -1) + x.t3.r[1] - x.t3.r[0];
         if (!E) exp_check(acc, a_ssh);
-        const double sshn = x.shp.r[1] + 2.0 * x.tau * (-dv<E>(a_ssh, D(area), x.rc(OCN_RC_AREA, 0)));
+        const double sshn = x.shp.r[1] + 2.0 * x.tau * (-dv<E>(a_ssh, x.cst<kLds>(RC_AREA, 0), x.cst<kLds>(RC_RAREA, 0)));
         // a4 uv_trans (vel_ssh.f90:283-373)
         const double u_r = shz(u, 1), u_l = shz(u, -1), u_n = x.u.r[2], u_s = x.u.r[0];
         const double v_r = shz(v, 1), v_l = shz(v, -1), v_n = x.v.r[2], v_s = x.v.r[0];
@@ -1258,29 +1365,26 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             const double muh_p = (mu + mu_r + mu_n + shz(mu_n, 1)) / 4.0;
             const double muh_m = (mu + mu_r + mu_s + shz(mu_s, 1)) / 4.0;
             const double muh_m2 = (mu + mu_l + mu_n + shz(mu_n, -1)) / 4.0;
-            const float gxb = x.met(OCN_DXB, 0), gxbm = x.met(OCN_DXB, -1), gyb = x.met(OCN_DYB, 0);
-            const float dxb2 = gxb * gxb, dxb2m = gxbm * gxbm, dyb2 = gyb * gyb;
+            const double dxb2 = x.cst<kLds>(RC_DXB2, 0), dxb2m = x.cst<kLds>(RC_DXB2, -1), dyb2 = x.cst<kLds>(RC_DYB2, 0);
             const double sts = x.sts.r[1];
             const double dtc = x.dt.r[1];
-            const double a1 = shz(dtc, 1) - dtc, a2 = D(dxb2) * muh_p * hh * sts - D(dxb2m) * muh_m * x.hh.r[0] * x.sts.r[0];
+            const double a1 = shz(dtc, 1) - dtc, a2 = dxb2 * muh_p * hh * sts - dxb2m * muh_m * x.hh.r[0] * x.sts.r[0];
             const double a3 = x.dxq.r[2] - x.dxq.r[1],
-                         a4 = D(dyb2) * muh_p * hh * sts - D(dyb2) * muh_m2 * shz(hh, -1) * shz(sts, -1);
+                         a4 = dyb2 * muh_p * hh * sts - dyb2 * muh_m2 * shz(hh, -1) * shz(sts, -1);
             if (!E) { exp_check(acc, a1); exp_check(acc, a2); exp_check(acc, a3); exp_check(acc, a4); }
-            rxd = dv<E>(a1, dyh, x.rc(OCN_RC_DYH, 0)) + dv<E>(a2, dxt, x.rc(OCN_RC_DXT, 0));
-            ryd = -dv<E>(a3, dxh, x.rc(OCN_RC_DXH, 0)) + dv<E>(a4, dyt, x.rc(OCN_RC_DYT, 0));
+            rxd = dv<E>(a1, dyh, x.cst<kLds>(RC_RDYH, 0)) + dv<E>(a2, dxt, x.cst<kLds>(RC_RDXT, 0));
+            ryd = -dv<E>(a3, dxh, x.cst<kLds>(RC_RDXH, 0)) + dv<E>(a4, dyt, x.cst<kLds>(RC_RDYT, 0));
         }
         // a7 sw_update_uv (vel_ssh.f90:108-195); hun = hu, hvn = hv (the reuse identity)
         double un, vn;
         {
             const double g = D(OCN_FREE_FALL_ACC);
             const double ssh = x.ssh.r[1];
-            const float rdis = x.met(OCN_R_DISS, 0), rdisn = x.met(OCN_R_DISS, 1);
             {
                 const double bp = qtau(x, hu * dxt * dyh / 2.0);
                 const double bp0 = qtau(x, x.hu1.r[1] * dxt * dyh / 2.0);
                 const double slx = -(g * (shz(ssh, 1) - ssh) * dyh * hu);
-                const float rd = rdis + rdis;
-                const double fric = D(rd) / 2.0 * x.up.r[1] * dxt * dyh * hu;
+                const double fric = x.cst<kLds>(RC_RDSELF, 0) / 2.0 * x.up.r[1] * dxt * dyh * hu;   // (rdis + rdis) / 2
                 const double grx = x.rhsx + slx + rxd + rxa - fric + (x.cx.r[1] + x.cx.r[0]) / 4.0;
                 un = (x.up.r[1] * bp0 + grx) / (bp);
             }
@@ -1288,8 +1392,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
                 const double bp = qtau(x, hv * dyt * dxh / 2.0);
                 const double bp0 = qtau(x, x.hv1.r[1] * dyt * dxh / 2.0);
                 const double sly = -(g * (x.ssh.r[2] - ssh) * dxh * hv);
-                const float rd = rdis + rdisn;
-                const double fric = D(rd) / 2.0 * x.vp.r[1] * dxh * dyt * hv;
+                const double fric = x.cst<kLds>(RC_RDNEXT, 0) / 2.0 * x.vp.r[1] * dxh * dyt * hv;   // (rdis + rdis(n+1)) / 2
                 const double c1 = x.rr.r[1] * (u_n + u);
                 const double gry = x.rhsy + sly + ryd + rya - fric - (c1 + shz(c1, -1)) / 4.0;
                 vn = (x.vp.r[1] * bp0 + gry) / (bp);
@@ -1316,10 +1419,36 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         if (bc & (1u << OCN_LCV)) { st(t.f(OCN_VBRTRN), c, vn); st(vp_out, c, fb); }
     }
 
+    static constexpr bool kLds = OCN_STEP_LDS && (ZF || OCN_STEP_LDS_GENERAL);
+#if OCN_STEP_LDS
+    static constexpr bool kPrologue = kLds;
+    // the row constants of the workgroup's rows into LDS (rows fit: launch_step's tiles have at
+    // most OCN_STEP_ROWS rows)
+    __device__ void prologue(const MarchRect &R, int ty) const
+    {
+        const int h = R.vert ? 4 * R.rows : R.rows, nb = R.n0 + ty * h;
+        if (nb > R.n1) return;   // workgroup-uniform
+        const int ne = min(R.n1, nb + h - 1), lo = nb - 2 - b.bnd_y1, i = (int)threadIdx.x;
+        if (i < ne - nb + 5) {   // a thread per row
+            const unsigned r = (unsigned)min(max(lo + i, 0), (int)t.nrows - 1);
+#pragma unroll
+            for (int k = 0; k < kRowC; ++k) g_step_rc[i * kRowC + k] = row_const(t.rows, t.nrows, r, k);
+        }
+        if (threadIdx.x == 0) g_step_rlo = (unsigned)lo;
+        __syncthreads();
+    }
+#endif
+
     __device__ void march(const Lane &L, int nb, int ne) const
     {
         const Geo I = geo(&b);
         StepRegs x{};
+#if OCN_STEP_LDS
+        if (kLds) {
+            x.lds = (const __attribute__((address_space(3))) double *)g_step_rc;
+            x.rlo = g_step_rlo;
+        }
+#endif
         x.rows = (const __attribute__((address_space(4))) float *)t.rows;
         x.rcp = (const __attribute__((address_space(4))) double *)(t.rows + recip_offset(t.nrows));
         x.nrows = t.nrows;
@@ -1338,8 +1467,8 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             x.bits.r[2] = ld(t.bits, c1); x.u.r[2] = ld(t.f(OCN_UBRTR), c1);
             x.vp.r[1] = ld(t.f(OCN_VBRTRP), c);
             // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
-            x.qb = x.vp.r[1] / D(x.met(OCN_DXH, 0));
-            x.qc = x.up.r[2] / D(x.met(OCN_DXT, 1));
+            x.qb = x.vp.r[1] / x.cst<kLds>(RC_DXH, 0);
+            x.qc = x.up.r[2] / x.cst<kLds>(RC_DXT, 1);
             weights(x, 1);
         }
         Fallback fb, fbn;

@@ -182,6 +182,13 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_ONEPASS, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_known_constants(self, on: bool = True):
+        """The one-pass steps' known-constant variant (default): forcing and D's fallback values
+        zero, h_r and mu uniform, when a check of the arrays finds them so; off: always the
+        general variant (same results bit for bit)."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_KNOWN_CONSTANTS, int(on)), "ocn_ctx_set_option")
+        return self
+
     def option(self, key: int) -> int:
         v = C.c_int64(0)
         check(lib().ocn_ctx_get_option(self.ctx, key, C.byref(v)), "ocn_ctx_get_option")

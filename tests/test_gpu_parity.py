@@ -457,3 +457,23 @@ def test_onepass_with_nonzero_fallback_values(amd, blocks):
         m.close()
     bad = [(k, nm) for k, d in enumerate(out[True]) for nm, a in d.items() if not bits_equal(a, out[False][k][nm])]
     assert not bad, f"one-pass with nonzero fallback values differs from the role-flip path: {bad}"
+
+
+@pytest.mark.gpu
+def test_known_constants_option(amd):
+    """OCN_OPT_KNOWN_CONSTANTS 0: the one-pass steps run their general variant (h_r, mu, the
+    forcing and D's fallback values read from the arrays) -- the same results bit for bit as the
+    known-constant variant the check selects by default."""
+    n, steps = 130, 9
+    out = {}
+    for kc in (True, False):
+        m = amd.OceanModel(amd.box_config(n)).set_known_constants(kc)
+        m.init()
+        m.step(steps, tau=1.0, check_every=1).synchronize()
+        assert m.onepass_active and m.onepass_zero == kc
+        out[kc] = {nm: m.download(0, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp", "vbrtr",
+                                                   "vbrtrn", "vbrtrp", "hhu", "hhv", "hhh", "vort", "str_t",
+                                                   "str_s", "RHSx_dif", "RHSy_adv")}
+        m.close()
+    bad = [nm for nm, a in out[True].items() if not bits_equal(a, out[False][nm])]
+    assert not bad, f"known-constant and general one-pass variants differ: {bad}"
