@@ -1065,6 +1065,17 @@ __device__ __forceinline__ double row_const(const float *rows, unsigned nrows, u
     }
 }
 
+// 1 / c for a sea count c in {0, 1, 2, 4} (+inf for 0): a * rcp_count(c) is a / (double)c bit for
+// bit -- 1, 1/2, 1/4 are exact, so both round the same real value once; for c = 0, a * inf and
+// a / 0 are the same infinity or NaN (0 * inf, 0 / 0); c = 3 takes a division (derive).  The
+// counts are integers from the mask bits: no float sums, compares or conversions, and u / v
+// (c <= 2) need no wave-wide test.
+__device__ __forceinline__ double rcp_count(unsigned c)
+{
+    const unsigned hi = c == 0 ? 0x7ff00000u : 0x3ff00000u - ((c >> 1) << 20);
+    return __builtin_bit_cast(double, (unsigned long long)hi << 32);
+}
+
 struct StepRegs {
     template <class T> struct Win {   // rows n-1, n, n+1, n+2 at this lane's column
         T r[4];
@@ -1143,6 +1154,7 @@ struct StepRegs {
     {
         return rcp[(unsigned)k * nrows + __builtin_amdgcn_readfirstlane(rn + dy)];
     }
+    __device__ __forceinline__ unsigned bit(int id, int dx, int dy) const { return (bits.at(dx, dy) >> id) & 1u; }
     __device__ __forceinline__ float mk(int id, int dx, int dy) const
     {
         return (bits.at(dx, dy) >> id) & 1u ? 1.0f : 0.0f;
@@ -1263,9 +1275,10 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     {
         weights(x, 2);   // row n+2 (rows n+1's were formed one iteration ago)
         // hh_init levels 0 and 1 (depth.f90:52-97, sw_stencils.h interp_u / interp_v / interp_h)
-        const float l00 = x.mk(OCN_LU, 0, 1), l10 = x.mk(OCN_LU, 1, 1), l01 = x.mk(OCN_LU, 0, 2),
-                    l11 = x.mk(OCN_LU, 1, 2);
-        const double su = D(l00 + l10), sv = D(l00 + l01), sh4 = D(l00 + l10 + l01 + l11);
+        // the sea counts of the averages (sw_stencils.h div_mask_sum: a / s, s the sum of lu)
+        const unsigned b00 = x.bit(OCN_LU, 0, 1), b10 = x.bit(OCN_LU, 1, 1), b01 = x.bit(OCN_LU, 0, 2),
+                       b11 = x.bit(OCN_LU, 1, 2);
+        const unsigned cu = b00 + b10, cv = b00 + b01, ch = cu + b01 + b11;
         const double dxt = x.cst<kLds>(RC_DXT, 1), dyt = x.cst<kLds>(RC_DYT, 1), dxh = x.cst<kLds>(RC_DXH, 1),
                      dyh = x.cst<kLds>(RC_DYH, 1), dxb = x.cst<kLds>(RC_DXB, 1), dyb = x.cst<kLds>(RC_DYB, 1);
         const double w00 = x.w0.r[2], w10 = shz(w00, 1), w01 = x.w0.r[3], w11 = shz(w01, 1);
@@ -1273,9 +1286,10 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const double s0 = w00 + w10;
         const double rxt = x.cst<kLds>(RC_RDXT, 1), ryh = x.cst<kLds>(RC_RDYH, 1), rxh = x.cst<kLds>(RC_RDXH, 1),
                      ryt = x.cst<kLds>(RC_RDYT, 1);
-        const double a_u0 = div_mask_sum(s0, su), a_v0 = div_mask_sum(w00 + w01, sv),
-                     a_h0 = div_mask_sum(s0 + w01 + w11, sh4), a_u1 = div_mask_sum(p00 + p10, su),
-                     a_v1 = div_mask_sum(p00 + p01, sv);
+        const double ru = rcp_count(cu), rv = rcp_count(cv);
+        const double a_u0 = s0 * ru, a_v0 = (w00 + w01) * rv, a_u1 = (p00 + p10) * ru, a_v1 = (p00 + p01) * rv;
+        const double a_h0 = __builtin_amdgcn_ballot_w64(ch == 3) ? (s0 + w01 + w11) / D(ch)
+                                                                 : (s0 + w01 + w11) * rcp_count(ch);
         if (!E) {   // (a / g1) / g2: a's range bounds a / g1's (|g1| <= 2^60)
             exp_check(acc, a_u0); exp_check(acc, a_v0); exp_check(acc, a_h0); exp_check(acc, a_u1);
             exp_check(acc, a_v1); exp_check(acc, x.up.r[2]); exp_check(acc, x.vp.r[2]); exp_check(acc, x.up.r[3]);
