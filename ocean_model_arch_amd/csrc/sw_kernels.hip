@@ -1016,6 +1016,9 @@ enum RowC { RC_DX, RC_DY, RC_DXT, RC_DYT, RC_DXH, RC_DYH, RC_DXB, RC_DYB, RC_RDX
 #ifndef OCN_STEP_LDS
 #define OCN_STEP_LDS 1
 #endif
+#ifndef OCN_STEP_PF
+#define OCN_STEP_PF 1   // rows the one-pass step's loads run ahead
+#endif
 #ifndef OCN_STEP_LDS_GENERAL
 #define OCN_STEP_LDS_GENERAL 0   // also in the general variant (its VGPRs spill: 0.83 vs 0.64 ms at 4096^2)
 #endif
@@ -1375,10 +1378,14 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         // a6 uv_diff2 (vel_ssh.f90:375-452)
         double rxd, ryd;
         {
-            const double mu = x.mu.r[1], mu_r = shz(mu, 1), mu_l = shz(mu, -1), mu_n = x.mu.r[2], mu_s = x.mu.r[0];
-            const double muh_p = (mu + mu_r + mu_n + shz(mu_n, 1)) / 4.0;
-            const double muh_m = (mu + mu_r + mu_s + shz(mu_s, 1)) / 4.0;
-            const double muh_m2 = (mu + mu_l + mu_n + shz(mu_n, -1)) / 4.0;
+            // ZF: mu is one value over the step's reach, so its neighbours are that value (the lane
+            // shifts differ only on the edge lanes, which produce no output and whose mu terms no
+            // other lane reads) and the three averages are one loop-invariant value
+            auto sh = [](double a, int d) { return ZF ? a : shz(a, d); };
+            const double mu = x.mu.r[1], mu_r = sh(mu, 1), mu_l = sh(mu, -1), mu_n = x.mu.r[2], mu_s = x.mu.r[0];
+            const double muh_p = (mu + mu_r + mu_n + sh(mu_n, 1)) / 4.0;
+            const double muh_m = (mu + mu_r + mu_s + sh(mu_s, 1)) / 4.0;
+            const double muh_m2 = (mu + mu_l + mu_n + sh(mu_n, -1)) / 4.0;
             const double dxb2 = x.cst<kLds>(RC_DXB2, 0), dxb2m = x.cst<kLds>(RC_DXB2, -1), dyb2 = x.cst<kLds>(RC_DYB2, 0);
             const double sts = x.sts.r[1];
             const double dtc = x.dt.r[1];
@@ -1489,10 +1496,19 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         fallback(x, fb, L.m, n0 + 1, 2);
         Batch q;
         load(q, L.m, n0);
+#if OCN_STEP_PF == 2
+        Batch q2;
+        if (n0 < ne) load(q2, L.m, n0 + 1);
+#endif
         for (int n = n0; n <= ne; ++n) {
             take(x, q);
             if (n < ne) fallback(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
+#if OCN_STEP_PF == 2
+            q = q2;
+            if (n + 1 < ne) load(q2, L.m, n + 2);          // two rows ahead
+#else
             if (n < ne) load(q, L.m, n + 1);              // in flight while this row is computed
+#endif
             {   // D(n+1) with udiv; again with IEEE divisions if a dividend is out of its range
                 int acc = 0;
                 double qb, qc;
