@@ -1016,9 +1016,6 @@ enum RowC { RC_DX, RC_DY, RC_DXT, RC_DYT, RC_DXH, RC_DYH, RC_DXB, RC_DYB, RC_RDX
 #ifndef OCN_STEP_LDS
 #define OCN_STEP_LDS 1
 #endif
-#ifndef OCN_STEP_PF
-#define OCN_STEP_PF 1   // rows the one-pass step's loads run ahead
-#endif
 #ifndef OCN_STEP_LDS_GENERAL
 #define OCN_STEP_LDS_GENERAL 0   // also in the general variant (its VGPRs spill: 0.83 vs 0.64 ms at 4096^2)
 #endif
@@ -1079,15 +1076,25 @@ __device__ __forceinline__ double rcp_count(unsigned c)
     return __builtin_bit_cast(double, (unsigned long long)hi << 32);
 }
 
+#ifndef OCN_STEP_UNROLL
+#define OCN_STEP_UNROLL 1
+#endif
+constexpr int kRing = 5;   // StepRegs::Win: 4 rows, written out for 5 phases (MarchStep::march)
+
 struct StepRegs {
-    template <class T> struct Win {   // rows n-1, n, n+1, n+2 at this lane's column
-        T r[4];
-        __device__ __forceinline__ T at(int dx, int dy) const
+    // rows n-1, n, n+1, n+2 at this lane's column: a ring of kRing slots, row n + k - 1 in slot
+    // (PH + k) % kRing for the iteration's phase PH (n - n0 mod kRing, a template parameter: the
+    // march is unrolled kRing times), so that no register moves rotate the rows
+    template <class T> struct Win {
+        T r[kRing];
+        template <int PH> __device__ __forceinline__ T &s(int k) { return r[(PH + k) % kRing]; }
+        template <int PH> __device__ __forceinline__ T s(int k) const { return r[(PH + k) % kRing]; }
+        template <int PH> __device__ __forceinline__ T at(int dx, int dy) const
         {
             if (dy < -1 || dy > 2) ocn_march_bad_access();
-            return shz(r[dy + 1], dx);
+            return shz(s<PH>(dy + 1), dx);
         }
-        __device__ __forceinline__ void rotate() { r[0] = r[1]; r[1] = r[2]; r[2] = r[3]; }
+        __device__ __forceinline__ void rotate() { r[0] = r[1]; r[1] = r[2]; r[2] = r[3]; }   // (phase 0 only)
     };
     // state
     Win<double> u, v, up, vp, ssh, shp, hr, mu;
@@ -1157,11 +1164,7 @@ struct StepRegs {
     {
         return rcp[(unsigned)k * nrows + __builtin_amdgcn_readfirstlane(rn + dy)];
     }
-    __device__ __forceinline__ unsigned bit(int id, int dx, int dy) const { return (bits.at(dx, dy) >> id) & 1u; }
-    __device__ __forceinline__ float mk(int id, int dx, int dy) const
-    {
-        return (bits.at(dx, dy) >> id) & 1u ? 1.0f : 0.0f;
-    }
+    // the rotating form (every iteration in phase 0): rows n-1 .. n+2 move down one slot
     __device__ __forceinline__ void rotate()
     {
         u.rotate(); v.rotate(); up.rotate(); vp.rotate(); ssh.rotate(); shp.rotate(); hr.rotate(); mu.rotate();
@@ -1169,7 +1172,14 @@ struct StepRegs {
         hu.rotate(); hv.rotate(); hh.rotate(); hu1.rotate(); hv1.rotate(); vort.rotate(); stt.rotate(); sts.rotate();
         w0.rotate(); w1.rotate(); pu.rotate(); pv.rotate(); vh.rotate(); t3.rotate(); cx.rotate(); rr.rotate();
         dt.rotate(); dxq.rotate();
-        ++rn;
+    }
+    template <int PH> __device__ __forceinline__ unsigned bit(int id, int dx, int dy) const
+    {
+        return (bits.at<PH>(dx, dy) >> id) & 1u;
+    }
+    template <int PH> __device__ __forceinline__ float mk(int id, int dx, int dy) const
+    {
+        return (bits.at<PH>(dx, dy) >> id) & 1u ? 1.0f : 0.0f;
     }
 };
 
@@ -1215,11 +1225,11 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         if (ZF) q.rhsx = q.rhsy = 0.0;
         else { q.rhsx = ld(t.f(OCN_RHSX), c); q.rhsy = ld(t.f(OCN_RHSY), c); }
     }
-    __device__ __forceinline__ static void take(StepRegs &x, const Batch &q)
+    template <int PH> __device__ __forceinline__ static void take(StepRegs &x, const Batch &q)
     {
-        x.u.r[3] = q.u; x.up.r[3] = q.up; x.ssh.r[3] = q.ssh; x.shp.r[3] = q.shp; x.hr.r[3] = q.hr;
-        x.bits.r[3] = q.bits;
-        x.v.r[2] = q.v; x.vp.r[2] = q.vp; x.mu.r[2] = q.mu;
+        x.u.s<PH>(3) = q.u; x.up.s<PH>(3) = q.up; x.ssh.s<PH>(3) = q.ssh; x.shp.s<PH>(3) = q.shp; x.hr.s<PH>(3) = q.hr;
+        x.bits.s<PH>(3) = q.bits;
+        x.v.s<PH>(2) = q.v; x.vp.s<PH>(2) = q.vp; x.mu.s<PH>(2) = q.mu;
         x.rhsx = q.rhsx; x.rhsy = q.rhsy;
     }
 
@@ -1227,13 +1237,13 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     // (sw_stencils.h) with h = h_r + sh * ffs (level 0) or h_r + shp * ffs (level 1).  The weight
     // of corner (m+1, n) / (m, n+1) of a point is its right / upper neighbour's own weight: dx and
     // dy are constant along a row, so the operands are the same.
-    __device__ __forceinline__ static void weights(StepRegs &x, int dy)
+    template <int PH> __device__ __forceinline__ static void weights(StepRegs &x, int dy)
     {
         const int k = dy + 1;
         const double gx = x.cst<kLds>(RC_DX, dy), gy = x.cst<kLds>(RC_DY, dy);
-        const double l = D(x.mk(OCN_LU, 0, dy));
-        x.w0.r[k] = (x.hr.r[k] + x.ssh.r[k] * x.f) * gx * gy * l;
-        x.w1.r[k] = (x.hr.r[k] + x.shp.r[k] * x.f) * gx * gy * l;
+        const double l = D(x.mk<PH>(OCN_LU, 0, dy));
+        x.w0.s<PH>(k) = (x.hr.s<PH>(k) + x.ssh.s<PH>(k) * x.f) * gx * gy * l;
+        x.w1.s<PH>(k) = (x.hr.s<PH>(k) + x.shp.s<PH>(k) * x.f) * gx * gy * l;
     }
 
     // Where D takes the value in memory (mask 0 or outside the stage's range): those loads, issued
@@ -1243,10 +1253,10 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         bool llu, llv, luh, vt, st, ss;   // the computed value is used
         double hu, hv, hh, hu1, hv1, vort, stt, sts;
     };
-    __device__ __forceinline__ void fallback(const StepRegs &x, Fallback &f, int m, int r, int slot) const
+    template <int PH> __device__ __forceinline__ void fallback(const StepRegs &x, Fallback &f, int m, int r, int slot) const
     {
         const Pt c = geo(&b)(m, r);
-        const unsigned bc = x.bits.r[slot];
+        const unsigned bc = x.bits.s<PH>(slot);
         const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && r >= b.ny_start - 1 && r <= b.ny_end;
         const bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
         f.llu = hh_rng && (bc & (1u << OCN_LLU));
@@ -1272,20 +1282,20 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         if constexpr (E) return a / d;
         else return udiv(a, d, rd);
     }
-    template <bool E>
+    template <bool E, int PH>
     __device__ __forceinline__ void derive(StepRegs &x, const Fallback &fb, int &acc, double &qb_next,
                                            double &qc_next) const
     {
-        weights(x, 2);   // row n+2 (rows n+1's were formed one iteration ago)
+        weights<PH>(x, 2);   // row n+2 (rows n+1's were formed one iteration ago)
         // hh_init levels 0 and 1 (depth.f90:52-97, sw_stencils.h interp_u / interp_v / interp_h)
         // the sea counts of the averages (sw_stencils.h div_mask_sum: a / s, s the sum of lu)
-        const unsigned b00 = x.bit(OCN_LU, 0, 1), b10 = x.bit(OCN_LU, 1, 1), b01 = x.bit(OCN_LU, 0, 2),
-                       b11 = x.bit(OCN_LU, 1, 2);
+        const unsigned b00 = x.bit<PH>(OCN_LU, 0, 1), b10 = x.bit<PH>(OCN_LU, 1, 1), b01 = x.bit<PH>(OCN_LU, 0, 2),
+                       b11 = x.bit<PH>(OCN_LU, 1, 2);
         const unsigned cu = b00 + b10, cv = b00 + b01, ch = cu + b01 + b11;
         const double dxt = x.cst<kLds>(RC_DXT, 1), dyt = x.cst<kLds>(RC_DYT, 1), dxh = x.cst<kLds>(RC_DXH, 1),
                      dyh = x.cst<kLds>(RC_DYH, 1), dxb = x.cst<kLds>(RC_DXB, 1), dyb = x.cst<kLds>(RC_DYB, 1);
-        const double w00 = x.w0.r[2], w10 = shz(w00, 1), w01 = x.w0.r[3], w11 = shz(w01, 1);
-        const double p00 = x.w1.r[2], p10 = shz(p00, 1), p01 = x.w1.r[3];
+        const double w00 = x.w0.s<PH>(2), w10 = shz(w00, 1), w01 = x.w0.s<PH>(3), w11 = shz(w01, 1);
+        const double p00 = x.w1.s<PH>(2), p10 = shz(p00, 1), p01 = x.w1.s<PH>(3);
         const double s0 = w00 + w10;
         const double rxt = x.cst<kLds>(RC_RDXT, 1), ryh = x.cst<kLds>(RC_RDYH, 1), rxh = x.cst<kLds>(RC_RDXH, 1),
                      ryt = x.cst<kLds>(RC_RDYT, 1);
@@ -1295,7 +1305,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
                                                                  : (s0 + w01 + w11) * rcp_count(ch);
         if (!E) {   // (a / g1) / g2: a's range bounds a / g1's (|g1| <= 2^60)
             exp_check(acc, a_u0); exp_check(acc, a_v0); exp_check(acc, a_h0); exp_check(acc, a_u1);
-            exp_check(acc, a_v1); exp_check(acc, x.up.r[2]); exp_check(acc, x.vp.r[2]); exp_check(acc, x.up.r[3]);
+            exp_check(acc, a_v1); exp_check(acc, x.up.s<PH>(2)); exp_check(acc, x.vp.s<PH>(2)); exp_check(acc, x.up.s<PH>(3));
         }
         const double u0 = dv<E>(dv<E>(a_u0, dxt, rxt), dyh, ryh);
         const double v0 = dv<E>(dv<E>(a_v0, dxh, rxh), dyt, ryt);
@@ -1303,15 +1313,15 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const double u1 = dv<E>(dv<E>(a_u1, dxt, rxt), dyh, ryh);
         const double v1 = dv<E>(dv<E>(a_v1, dxh, rxh), dyt, ryt);
         // a3 uv_trans_vort (vel_ssh.f90:247-281, sw_stencils.h uv_trans_vort_math)
-        const double u_0 = x.u.r[2], u_1 = x.u.r[3], v_0 = x.v.r[2], v_r = shz(v_0, 1);
+        const double u_0 = x.u.s<PH>(2), u_1 = x.u.s<PH>(3), v_0 = x.v.s<PH>(2), v_r = shz(v_0, 1);
         const double vort = (v_r * dyt - v_0 * dyt) - (u_1 * x.cst<kLds>(RC_DXT, 2) - u_0 * dxt)
                             - ((v_r - v_0) * dyb - (u_1 - u_0) * dxb);
         // a5 (mixing.f90:33-44, sw_stencils.h stress_components_math) with its quotients shared:
         // up/dyh at m-1 is the left lane's up/dyh (dyh is constant along the row), vp/dxh at n-1
         // is the previous row's, up/dxt at n+1 the next row's (formed here, kept for the next
         // row), vp/dyt at m+1 the right lane's -- the same operands, so the same values
-        const double qa = dv<E>(x.up.r[2], dyh, ryh), qb = dv<E>(x.vp.r[2], dxh, rxh);
-        const double qc1 = dv<E>(x.up.r[3], x.cst<kLds>(RC_DXT, 2), x.cst<kLds>(RC_RDXT, 2)), qe = dv<E>(x.vp.r[2], dyt, ryt);
+        const double qa = dv<E>(x.up.s<PH>(2), dyh, ryh), qb = dv<E>(x.vp.s<PH>(2), dxh, rxh);
+        const double qc1 = dv<E>(x.up.s<PH>(3), x.cst<kLds>(RC_DXT, 2), x.cst<kLds>(RC_RDXT, 2)), qe = dv<E>(x.vp.s<PH>(2), dyt, ryt);
         const double st = x.cst<kLds>(RC_RAT0, 1) * (qa - shz(qa, -1)) - x.cst<kLds>(RC_RAT1, 1) * (qb - x.qb);
         const double ss = x.cst<kLds>(RC_RAT2, 1) * (qc1 - x.qc) + x.cst<kLds>(RC_RAT3, 1) * (shz(qe, 1) - qe);
         qb_next = qb;
@@ -1321,50 +1331,51 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const double hh = fb.luh ? h0 : fb.hh;
         const double vt = fb.vt ? vort : fb.vort;
         const double stt = fb.st ? st : fb.stt;
-        x.hu.r[2] = hu; x.hv.r[2] = hv; x.hh.r[2] = hh; x.vort.r[2] = vt; x.stt.r[2] = stt;
-        x.hu1.r[2] = fb.llu ? u1 : fb.hu1;
-        x.hv1.r[2] = fb.llv ? v1 : fb.hv1;
-        x.sts.r[2] = fb.ss ? ss : fb.sts;
+        x.hu.s<PH>(2) = hu; x.hv.s<PH>(2) = hv; x.hh.s<PH>(2) = hh; x.vort.s<PH>(2) = vt; x.stt.s<PH>(2) = stt;
+        x.hu1.s<PH>(2) = fb.llu ? u1 : fb.hu1;
+        x.hv1.s<PH>(2) = fb.llv ? v1 : fb.hv1;
+        x.sts.s<PH>(2) = fb.ss ? ss : fb.sts;
         // shared products of row r (S reads them at m +- 1 and at rows n-1 .. n+1); each is the
         // reference's sub-expression with the same operands in the same order
-        x.pu.r[2] = u_0 * dyh * hu;                                  // uv_trans: u * dyh * hu
-        x.pv.r[2] = v_0 * dxh * hv;                                  // uv_trans: v * dxh * hv
-        x.vh.r[2] = vt * hh;                                         // uv_trans: vort * hh
-        x.t3.r[2] = v_0 * hv * dxh;                                  // sw_update_ssh: vbrtr * hhv * dxh
+        x.pu.s<PH>(2) = u_0 * dyh * hu;                                  // uv_trans: u * dyh * hu
+        x.pv.s<PH>(2) = v_0 * dxh * hv;                                  // uv_trans: v * dxh * hv
+        x.vh.s<PH>(2) = vt * hh;                                         // uv_trans: vort * hh
+        x.t3.s<PH>(2) = v_0 * hv * dxh;                                  // sw_update_ssh: vbrtr * hhv * dxh
         const double rr = x.cst<kLds>(RC_RLH, 1) * hh * dxb * dyb;   // sw_update_uv: rlh_s * hhh * dxb * dyb
-        x.rr.r[2] = rr;
-        x.cx.r[2] = rr * (v_r + v_0);                                //   ... * (vbrtr(1,0) + vbrtr)
-        const double hq = x.hr.r[2] + x.ssh.r[2] * x.f;              // depth.f90:48 hq = h_r + sh*ffs
-        x.dt.r[2] = x.cst<kLds>(RC_DY2, 1) * x.mu.r[2] * hq * stt;         // uv_diff2: dy**2 * mu * hq * str_t
-        x.dxq.r[2] = x.cst<kLds>(RC_DX2, 1) * x.mu.r[2] * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
+        x.rr.s<PH>(2) = rr;
+        x.cx.s<PH>(2) = rr * (v_r + v_0);                                //   ... * (vbrtr(1,0) + vbrtr)
+        const double hq = x.hr.s<PH>(2) + x.ssh.s<PH>(2) * x.f;              // depth.f90:48 hq = h_r + sh*ffs
+        x.dt.s<PH>(2) = x.cst<kLds>(RC_DY2, 1) * x.mu.s<PH>(2) * hq * stt;         // uv_diff2: dy**2 * mu * hq * str_t
+        x.dxq.s<PH>(2) = x.cst<kLds>(RC_DX2, 1) * x.mu.s<PH>(2) * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
     }
 
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
     // uv_trans_math, uv_diff2_math, sw_update_uv_math written out over the shared products)
-    template <bool E> __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n, int &acc) const
+    template <bool E, int PH>
+    __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n, int &acc) const
     {
         const Geo I = geo(&b);
         const Pt c = I(L.m, n);
-        const double u = x.u.r[1], v = x.v.r[1], hu = x.hu.r[1], hv = x.hv.r[1], hh = x.hh.r[1];
+        const double u = x.u.s<PH>(1), v = x.v.s<PH>(1), hu = x.hu.s<PH>(1), hv = x.hv.s<PH>(1), hh = x.hh.s<PH>(1);
         const double dxt = x.cst<kLds>(RC_DXT, 0), dyt = x.cst<kLds>(RC_DYT, 0), dxh = x.cst<kLds>(RC_DXH, 0),
                      dyh = x.cst<kLds>(RC_DYH, 0);
         // a1 sw_update_ssh (vel_ssh.f90:69-106)
         const double t1 = u * hu * dyh;
-        const double a_ssh = t1 - shz(t1, -1) + x.t3.r[1] - x.t3.r[0];
+        const double a_ssh = t1 - shz(t1, -1) + x.t3.s<PH>(1) - x.t3.s<PH>(0);
         if (!E) exp_check(acc, a_ssh);
-        const double sshn = x.shp.r[1] + 2.0 * x.tau * (-dv<E>(a_ssh, x.cst<kLds>(RC_AREA, 0), x.cst<kLds>(RC_RAREA, 0)));
+        const double sshn = x.shp.s<PH>(1) + 2.0 * x.tau * (-dv<E>(a_ssh, x.cst<kLds>(RC_AREA, 0), x.cst<kLds>(RC_RAREA, 0)));
         // a4 uv_trans (vel_ssh.f90:283-373)
-        const double u_r = shz(u, 1), u_l = shz(u, -1), u_n = x.u.r[2], u_s = x.u.r[0];
-        const double v_r = shz(v, 1), v_l = shz(v, -1), v_n = x.v.r[2], v_s = x.v.r[0];
-        const double pu = x.pu.r[1], pun = x.pu.r[2], pv = x.pv.r[1], pvn = x.pv.r[2], pvs = x.pv.r[0];
-        const double luu = D(x.mk(OCN_LUU, 0, 0)), luus = D(x.mk(OCN_LUU, 0, -1));
+        const double u_r = shz(u, 1), u_l = shz(u, -1), u_n = x.u.s<PH>(2), u_s = x.u.s<PH>(0);
+        const double v_r = shz(v, 1), v_l = shz(v, -1), v_n = x.v.s<PH>(2), v_s = x.v.s<PH>(0);
+        const double pu = x.pu.s<PH>(1), pun = x.pu.s<PH>(2), pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2), pvs = x.pv.s<PH>(0);
+        const double luu = D(x.mk<PH>(OCN_LUU, 0, 0)), luus = D(x.mk<PH>(OCN_LUU, 0, -1));
         double rxa, rya;
         {
             const double fx_p = (pu + shz(pu, 1)) / 2.0 * (u + u_r) / 2.0;
             const double fx_m = (pu + shz(pu, -1)) / 2.0 * (u + u_l) / 2.0;
             const double fy_p = (pv + shz(pv, 1)) / 2.0 * (u_n + u) / 2.0 * luu;
             const double fy_m = (pvs + shz(pvs, 1)) / 2.0 * (u_s + u) / 2.0 * luus;
-            rxa = -(fx_p - fx_m + fy_p - fy_m) + (x.vh.r[1] * (v_r + v) + x.vh.r[0] * (shz(v_s, 1) + v_s)) / 4.0;
+            rxa = -(fx_p - fx_m + fy_p - fy_m) + (x.vh.s<PH>(1) * (v_r + v) + x.vh.s<PH>(0) * (shz(v_s, 1) + v_s)) / 4.0;
         }
         {
             const double fy_p = (pv + pvn) / 2.0 * (v + v_n) / 2.0;
@@ -1372,7 +1383,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             const double sn = pu + pun;
             const double fx_p = sn / 2.0 * (v_r + v) / 2.0;
             const double fx_m = shz(sn, -1) / 2.0 * (v_l + v) / 2.0;
-            const double q = x.vh.r[1] * (u_n + u);
+            const double q = x.vh.s<PH>(1) * (u_n + u);
             rya = -(fx_p - fx_m + fy_p - fy_m) - (q + shz(q, -1)) / 4.0;
         }
         // a6 uv_diff2 (vel_ssh.f90:375-452)
@@ -1382,15 +1393,15 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             // shifts differ only on the edge lanes, which produce no output and whose mu terms no
             // other lane reads) and the three averages are one loop-invariant value
             auto sh = [](double a, int d) { return ZF ? a : shz(a, d); };
-            const double mu = x.mu.r[1], mu_r = sh(mu, 1), mu_l = sh(mu, -1), mu_n = x.mu.r[2], mu_s = x.mu.r[0];
+            const double mu = x.mu.s<PH>(1), mu_r = sh(mu, 1), mu_l = sh(mu, -1), mu_n = x.mu.s<PH>(2), mu_s = x.mu.s<PH>(0);
             const double muh_p = (mu + mu_r + mu_n + sh(mu_n, 1)) / 4.0;
             const double muh_m = (mu + mu_r + mu_s + sh(mu_s, 1)) / 4.0;
             const double muh_m2 = (mu + mu_l + mu_n + sh(mu_n, -1)) / 4.0;
             const double dxb2 = x.cst<kLds>(RC_DXB2, 0), dxb2m = x.cst<kLds>(RC_DXB2, -1), dyb2 = x.cst<kLds>(RC_DYB2, 0);
-            const double sts = x.sts.r[1];
-            const double dtc = x.dt.r[1];
-            const double a1 = shz(dtc, 1) - dtc, a2 = dxb2 * muh_p * hh * sts - dxb2m * muh_m * x.hh.r[0] * x.sts.r[0];
-            const double a3 = x.dxq.r[2] - x.dxq.r[1],
+            const double sts = x.sts.s<PH>(1);
+            const double dtc = x.dt.s<PH>(1);
+            const double a1 = shz(dtc, 1) - dtc, a2 = dxb2 * muh_p * hh * sts - dxb2m * muh_m * x.hh.s<PH>(0) * x.sts.s<PH>(0);
+            const double a3 = x.dxq.s<PH>(2) - x.dxq.s<PH>(1),
                          a4 = dyb2 * muh_p * hh * sts - dyb2 * muh_m2 * shz(hh, -1) * shz(sts, -1);
             if (!E) { exp_check(acc, a1); exp_check(acc, a2); exp_check(acc, a3); exp_check(acc, a4); }
             rxd = dv<E>(a1, dyh, x.cst<kLds>(RC_RDYH, 0)) + dv<E>(a2, dxt, x.cst<kLds>(RC_RDXT, 0));
@@ -1400,34 +1411,34 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         double un, vn;
         {
             const double g = D(OCN_FREE_FALL_ACC);
-            const double ssh = x.ssh.r[1];
+            const double ssh = x.ssh.s<PH>(1);
             {
                 const double bp = qtau(x, hu * dxt * dyh / 2.0);
-                const double bp0 = qtau(x, x.hu1.r[1] * dxt * dyh / 2.0);
+                const double bp0 = qtau(x, x.hu1.s<PH>(1) * dxt * dyh / 2.0);
                 const double slx = -(g * (shz(ssh, 1) - ssh) * dyh * hu);
-                const double fric = x.cst<kLds>(RC_RDSELF, 0) / 2.0 * x.up.r[1] * dxt * dyh * hu;   // (rdis + rdis) / 2
-                const double grx = x.rhsx + slx + rxd + rxa - fric + (x.cx.r[1] + x.cx.r[0]) / 4.0;
-                un = (x.up.r[1] * bp0 + grx) / (bp);
+                const double fric = x.cst<kLds>(RC_RDSELF, 0) / 2.0 * x.up.s<PH>(1) * dxt * dyh * hu;   // (rdis + rdis) / 2
+                const double grx = x.rhsx + slx + rxd + rxa - fric + (x.cx.s<PH>(1) + x.cx.s<PH>(0)) / 4.0;
+                un = (x.up.s<PH>(1) * bp0 + grx) / (bp);
             }
             {
                 const double bp = qtau(x, hv * dyt * dxh / 2.0);
-                const double bp0 = qtau(x, x.hv1.r[1] * dyt * dxh / 2.0);
-                const double sly = -(g * (x.ssh.r[2] - ssh) * dxh * hv);
-                const double fric = x.cst<kLds>(RC_RDNEXT, 0) / 2.0 * x.vp.r[1] * dxh * dyt * hv;   // (rdis + rdis(n+1)) / 2
-                const double c1 = x.rr.r[1] * (u_n + u);
+                const double bp0 = qtau(x, x.hv1.s<PH>(1) * dyt * dxh / 2.0);
+                const double sly = -(g * (x.ssh.s<PH>(2) - ssh) * dxh * hv);
+                const double fric = x.cst<kLds>(RC_RDNEXT, 0) / 2.0 * x.vp.s<PH>(1) * dxh * dyt * hv;   // (rdis + rdis(n+1)) / 2
+                const double c1 = x.rr.s<PH>(1) * (u_n + u);
                 const double gry = x.rhsy + sly + ryd + rya - fric - (c1 + shz(c1, -1)) / 4.0;
-                vn = (x.vp.r[1] * bp0 + gry) / (bp);
+                vn = (x.vp.s<PH>(1) * bp0 + gry) / (bp);
             }
         }
         // a8 sw_next_step's filters (vel_ssh.f90:197-245) + check_ssh_err (vel_ssh.f90:40-67)
         const double ts = sw.time_smooth;
-        const double fx = asselin(x.ssh.r[1], sshn, x.shp.r[1], ts);
-        const double fa = asselin(u, un, x.up.r[1], ts), fb = asselin(v, vn, x.vp.r[1], ts);
+        const double fx = asselin(x.ssh.s<PH>(1), sshn, x.shp.s<PH>(1), ts);
+        const double fa = asselin(u, un, x.up.s<PH>(1), ts), fb = asselin(v, vn, x.vp.s<PH>(1), ts);
         if (!L.out) return;
-        const unsigned bc = x.bits.r[1];
+        const unsigned bc = x.bits.s<PH>(1);
         if (LAST) {
-            if (bc & (1u << OCN_LUU)) { st(t.f(OCN_VORT), c, x.vort.r[1]); st(t.f(OCN_STR_S), c, x.sts.r[1]); }
-            if (bc & (1u << OCN_LU)) st(t.f(OCN_STR_T), c, x.stt.r[1]);
+            if (bc & (1u << OCN_LUU)) { st(t.f(OCN_VORT), c, x.vort.s<PH>(1)); st(t.f(OCN_STR_S), c, x.sts.s<PH>(1)); }
+            if (bc & (1u << OCN_LU)) st(t.f(OCN_STR_T), c, x.stt.s<PH>(1));
             if (bc & (1u << OCN_LCU)) { st(t.f(OCN_RHSX_ADV), c, rxa); st(t.f(OCN_RHSX_DIF), c, rxd); }
             if (bc & (1u << OCN_LCV)) { st(t.f(OCN_RHSY_ADV), c, rya); st(t.f(OCN_RHSY_DIF), c, ryd); }
         }
@@ -1441,6 +1452,10 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     }
 
     static constexpr bool kLds = OCN_STEP_LDS && (ZF || OCN_STEP_LDS_GENERAL);
+    // the march unrolled over the register ring (StepRegs::Win) -- the known-constant variant; the
+    // general one (loaded h_r, mu, forcing, fallback values) keeps the rotating loop: unrolled,
+    // its scalar and vector registers spill
+    static constexpr bool kUnroll = ZF && OCN_STEP_UNROLL;
 #if OCN_STEP_LDS
     static constexpr bool kPrologue = kLds;
     // the row constants of the workgroup's rows into LDS (rows fit: launch_step's tiles have at
@@ -1483,48 +1498,64 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const int n0 = nb - 2;
         {
             const Pt c = I(L.m, n0), c1 = I(L.m, n0 + 1);
-            x.up.r[2] = ld(t.f(OCN_UBRTRP), c1); x.ssh.r[2] = ld(t.f(OCN_SSH), c1);
-            x.shp.r[2] = ld(t.f(OCN_SSHP), c1); x.hr.r[2] = ZF ? hr0 : ld(t.f(OCN_HHQ_REST), c1);
-            x.bits.r[2] = ld(t.bits, c1); x.u.r[2] = ld(t.f(OCN_UBRTR), c1);
-            x.vp.r[1] = ld(t.f(OCN_VBRTRP), c);
+            x.up.s<0>(2) = ld(t.f(OCN_UBRTRP), c1); x.ssh.s<0>(2) = ld(t.f(OCN_SSH), c1);
+            x.shp.s<0>(2) = ld(t.f(OCN_SSHP), c1); x.hr.s<0>(2) = ZF ? hr0 : ld(t.f(OCN_HHQ_REST), c1);
+            x.bits.s<0>(2) = ld(t.bits, c1); x.u.s<0>(2) = ld(t.f(OCN_UBRTR), c1);
+            x.vp.s<0>(1) = ld(t.f(OCN_VBRTRP), c);
             // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
-            x.qb = x.vp.r[1] / x.cst<kLds>(RC_DXH, 0);
-            x.qc = x.up.r[2] / x.cst<kLds>(RC_DXT, 1);
-            weights(x, 1);
+            x.qb = x.vp.s<0>(1) / x.cst<kLds>(RC_DXH, 0);
+            x.qc = x.up.s<0>(2) / x.cst<kLds>(RC_DXT, 1);
+            weights<0>(x, 1);
         }
-        Fallback fb, fbn;
-        fallback(x, fb, L.m, n0 + 1, 2);
+        Fallback fb;
+        fallback<0>(x, fb, L.m, n0 + 1, 2);
         Batch q;
         load(q, L.m, n0);
-#if OCN_STEP_PF == 2
-        Batch q2;
-        if (n0 < ne) load(q2, L.m, n0 + 1);
-#endif
-        for (int n = n0; n <= ne; ++n) {
-            take(x, q);
-            if (n < ne) fallback(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
-#if OCN_STEP_PF == 2
-            q = q2;
-            if (n + 1 < ne) load(q2, L.m, n + 2);          // two rows ahead
-#else
-            if (n < ne) load(q, L.m, n + 1);              // in flight while this row is computed
-#endif
-            {   // D(n+1) with udiv; again with IEEE divisions if a dividend is out of its range
-                int acc = 0;
-                double qb, qc;
-                derive<false>(x, fb, acc, qb, qc);
-                if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) derive<true>(x, fb, acc, qb, qc);
-                x.qb = qb;
-                x.qc = qc;
+        if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
+            for (int n = n0;; n += kRing) {
+                if (iteration<0>(x, fb, q, L, n, nb, ne)) break;
+                if (iteration<1>(x, fb, q, L, n + 1, nb, ne)) break;
+                if (iteration<2>(x, fb, q, L, n + 2, nb, ne)) break;
+                if (iteration<3>(x, fb, q, L, n + 3, nb, ne)) break;
+                if (iteration<4>(x, fb, q, L, n + 4, nb, ne)) break;
             }
-            if (n >= nb) {   // wave-uniform
-                int acc = 0;
-                step<false>(x, L, n, acc);
-                if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) step<true>(x, L, n, acc);
+        } else {
+            for (int n = n0;; ++n) {
+                if (iteration<0>(x, fb, q, L, n, nb, ne)) break;
+                x.rotate();
             }
-            x.rotate();
-            fb = fbn;
         }
+    }
+
+    // iteration n (phase PH): D(n+1), and S(n) from n = nb on; true after the last (n = ne)
+    template <int PH>
+    __device__ __forceinline__ bool iteration(StepRegs &x, Fallback &fb, Batch &q, const Lane &L0, int n, int nb,
+                                              int ne) const
+    {
+        // the lane's column, opaque to the compiler in every iteration: its addresses are formed
+        // where used, not held per phase across the unrolled loop
+        Lane L = L0;
+        asm volatile("" : "+v"(L.m));
+        take<PH>(x, q);
+        Fallback fbn;
+        if (n < ne) fallback<PH>(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
+        if (n < ne) load(q, L.m, n + 1);                   // in flight while this row is computed
+        {   // D(n+1) with udiv; again with IEEE divisions if a dividend is out of its range
+            int acc = 0;
+            double qb, qc;
+            derive<false, PH>(x, fb, acc, qb, qc);
+            if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) derive<true, PH>(x, fb, acc, qb, qc);
+            x.qb = qb;
+            x.qc = qc;
+        }
+        if (n >= nb) {   // wave-uniform
+            int acc = 0;
+            step<false, PH>(x, L, n, acc);
+            if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) step<true, PH>(x, L, n, acc);
+        }
+        ++x.rn;
+        fb = fbn;
+        return n >= ne;
     }
 };
 #undef OCN_MD
