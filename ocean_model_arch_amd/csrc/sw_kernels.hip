@@ -1352,7 +1352,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
     // uv_trans_math, uv_diff2_math, sw_update_uv_math written out over the shared products)
     template <bool E, int PH>
-    __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n, int &acc) const
+    __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n, int &acc, bool &bad) const
     {
         const Geo I = geo(&b);
         const Pt c = I(L.m, n);
@@ -1445,7 +1445,10 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         if (bc & (1u << OCN_LU)) {
             st(t.f(OCN_SSHN), c, sshn);
             st(sshp_out, c, fx);
-            if (nbad && !(sshn < 10000.0 && sshn > -10000.0)) OCN_ATOMIC_INC(nbad);
+            // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
+            const bool b = !(sshn < 10000.0 && sshn > -10000.0);
+            if (nbad && b != (E && bad)) atomicAdd(nbad, b ? 1 : -1);
+            bad = b;
         }
         if (bc & (1u << OCN_LCU)) { st(t.f(OCN_UBRTRN), c, un); st(up_out, c, fa); }
         if (bc & (1u << OCN_LCV)) { st(t.f(OCN_VBRTRN), c, vn); st(vp_out, c, fb); }
@@ -1550,8 +1553,9 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         }
         if (n >= nb) {   // wave-uniform
             int acc = 0;
-            step<false, PH>(x, L, n, acc);
-            if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) step<true, PH>(x, L, n, acc);
+            bool bad = false;
+            step<false, PH>(x, L, n, acc, bad);
+            if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) step<true, PH>(x, L, n, acc, bad);
         }
         ++x.rn;
         fb = fbn;

@@ -477,3 +477,31 @@ def test_known_constants_option(amd):
         m.close()
     bad = [nm for nm, a in out[True].items() if not bits_equal(a, out[False][nm])]
     assert not bad, f"known-constant and general one-pass variants differ: {bad}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kc", [True, False])
+def test_onepass_rows_rerun_with_ieee_divisions(amd, kc):
+    """Dividends below udiv's range (|x| < 2^-900: velocities of ~1e-290 on 20 rows) make
+    the one-pass step re-run those rows with IEEE divisions (sw_kernels.hip MarchStep::iteration,
+    a wave-uniform branch no other test takes); the results must still be the role-flip path's
+    bit for bit, in both variants (known constants / general)."""
+    n, steps = 130, 6
+    out = {}
+    for onepass in (True, False):
+        m = amd.OceanModel(amd.box_config(n)).set_onepass(onepass).set_known_constants(kc)
+        m.init()
+        rng = np.random.default_rng(7)
+        for nms in (("ubrtr", "ubrtrn"), ("ubrtrp",), ("vbrtr", "vbrtrn"), ("vbrtrp",)):
+            a = m.download(0, nms[0])
+            a[:, 40:60] = 1e-290 * (1.0 + rng.random(a[:, 40:60].shape))   # rows 40..59 (at rest: 0 before)
+            for nm in nms:   # both buffers of a role-flip pair (they agree, as the reference leaves them)
+                m.upload(0, nm, a)
+        m.step(steps, tau=1.0, check_every=1).synchronize()
+        assert m.onepass_active == onepass
+        out[onepass] = {nm: m.download(0, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp", "vbrtr",
+                                                        "vbrtrn", "vbrtrp", "hhu", "hhv", "hhh", "vort", "str_t",
+                                                        "str_s", "RHSx_dif", "RHSy_adv")}
+        m.close()
+    bad = [nm for nm, a in out[True].items() if not bits_equal(a, out[False][nm])]
+    assert not bad, f"one-pass rows re-run with IEEE divisions differ from the role-flip path: {bad}"
