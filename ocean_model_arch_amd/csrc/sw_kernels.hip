@@ -945,6 +945,9 @@ template <bool HH, bool SKIP> struct MarchCA {
 #ifndef OCN_STEP_WAVES
 #define OCN_STEP_WAVES 2   // waves per SIMD asked of the register allocator
 #endif
+#ifndef OCN_STEP_BUFST
+#define OCN_STEP_BUFST 1   // the step's stores as st_on (no exec branches around them)
+#endif
 // A whole role-flip step in one register march (ocn_ctx.hip one_step_fused, "one-pass" steps of
 // a single-block call): the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp; h_r, mu, RHSx, RHSy)
 // is read once and the next state written once -- 10 + 6 arrays, against fused B + CA's 22 + 12.
@@ -978,6 +981,18 @@ __device__ __forceinline__ double shz(double x, int dx)
     return __hiloint2double(dpp_shz(__double2hiint(x), dx), dpp_shz(__double2loint(x), dx));
 }
 __device__ __forceinline__ unsigned shz(unsigned x, int dx) { return dx == 0 ? x : (unsigned)dpp_shz((int)x, dx); }
+
+// A masked store the wave always issues: a lane with !on gets a byte offset past the buffer's
+// range (nbytes = the array's size) and the buffer unit drops its write.  With no exec branch
+// around the stores every path through an iteration issues the same number of vector memory
+// operations, so the wait for the next row's loads (issued before them) is vmcnt(#stores), not
+// vmcnt(0) -- which would also wait for the stores' write acknowledgements.
+typedef unsigned ocn_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_on(double *p, unsigned nbytes, unsigned i, double v, bool on)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)nbytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ocn_u32x2, v), r, on ? i * 8u : 0xfffffff8u, 0, 0);
+}
 
 // x / d, correctly rounded, for a wave-uniform divisor d with rd = RN(1 / d) (the row table's
 // reciprocals): q = RN(x rd) is within one ulp of x / d, the residual x - q d is exact in an fma,
@@ -1349,10 +1364,15 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         x.dxq.s<PH>(2) = x.cst<kLds>(RC_DX2, 1) * x.mu.s<PH>(2) * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
     }
 
+    // a row's outputs and where they are stored (OCN_STEP_BUFST: stored after S's branch)
+    struct Out {
+        bool lu = false, cu = false, cv = false;
+        double sshn = 0.0, fx = 0.0, un = 0.0, fa = 0.0, vn = 0.0, fb = 0.0;
+    };
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
     // uv_trans_math, uv_diff2_math, sw_update_uv_math written out over the shared products)
     template <bool E, int PH>
-    __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n, int &acc, bool &bad) const
+    __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n, int &acc, bool &bad, Out &o) const
     {
         const Geo I = geo(&b);
         const Pt c = I(L.m, n);
@@ -1434,6 +1454,20 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const double ts = sw.time_smooth;
         const double fx = asselin(x.ssh.s<PH>(1), sshn, x.shp.s<PH>(1), ts);
         const double fa = asselin(u, un, x.up.s<PH>(1), ts), fb = asselin(v, vn, x.vp.s<PH>(1), ts);
+#if OCN_STEP_BUFST
+        if (!LAST) {   // the row's stores are issued after the branch (iteration, st_on)
+            const unsigned bc = x.bits.s<PH>(1);
+            o.lu = L.out && (bc & (1u << OCN_LU));
+            o.cu = L.out && (bc & (1u << OCN_LCU));
+            o.cv = L.out && (bc & (1u << OCN_LCV));
+            o.sshn = sshn; o.fx = fx; o.un = un; o.fa = fa; o.vn = vn; o.fb = fb;
+            // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
+            const bool bd = o.lu && !(sshn < 10000.0 && sshn > -10000.0);
+            if (nbad && bd != (E && bad)) atomicAdd(nbad, bd ? 1 : -1);
+            bad = bd;
+            return;
+        }
+#endif
         if (!L.out) return;
         const unsigned bc = x.bits.s<PH>(1);
         if (LAST) {
@@ -1452,6 +1486,19 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         }
         if (bc & (1u << OCN_LCU)) { st(t.f(OCN_UBRTRN), c, un); st(up_out, c, fa); }
         if (bc & (1u << OCN_LCV)) { st(t.f(OCN_VBRTRN), c, vn); st(vp_out, c, fb); }
+    }
+
+    // a row's six stores, issued by every iteration (warm-up rows with every lane dropped) and by
+    // no branch: every path to the next row's use of its loads has issued the same six after them
+    __device__ __forceinline__ void store_out(const Out &o, unsigned c) const
+    {
+        const unsigned nbytes = (unsigned)b.pitch * (unsigned)(b.bnd_y2 - b.bnd_y1 + 1) * 8u;
+        st_on(t.f(OCN_SSHN), nbytes, c, o.sshn, o.lu);
+        st_on(sshp_out, nbytes, c, o.fx, o.lu);
+        st_on(t.f(OCN_UBRTRN), nbytes, c, o.un, o.cu);
+        st_on(up_out, nbytes, c, o.fa, o.cu);
+        st_on(t.f(OCN_VBRTRN), nbytes, c, o.vn, o.cv);
+        st_on(vp_out, nbytes, c, o.fb, o.cv);
     }
 
     static constexpr bool kLds = OCN_STEP_LDS && (ZF || OCN_STEP_LDS_GENERAL);
@@ -1514,6 +1561,9 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         fallback<0>(x, fb, L.m, n0 + 1, 2);
         Batch q;
         load(q, L.m, n0);
+#if OCN_STEP_BUFST
+        if (!LAST) store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
+#endif
         if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
             for (int n = n0;; n += kRing) {
                 if (iteration<0>(x, fb, q, L, n, nb, ne)) break;
@@ -1551,12 +1601,16 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             x.qb = qb;
             x.qc = qc;
         }
+        Out o;
         if (n >= nb) {   // wave-uniform
             int acc = 0;
             bool bad = false;
-            step<false, PH>(x, L, n, acc, bad);
-            if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) step<true, PH>(x, L, n, acc, bad);
+            step<false, PH>(x, L, n, acc, bad, o);
+            if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) step<true, PH>(x, L, n, acc, bad, o);
         }
+#if OCN_STEP_BUFST
+        if (!LAST) store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
+#endif
         ++x.rn;
         fb = fbn;
         return n >= ne;
