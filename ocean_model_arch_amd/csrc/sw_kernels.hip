@@ -1316,7 +1316,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
                      ryt = x.cst<kLds>(RC_RDYT, 1);
         const double ru = rcp_count(cu), rv = rcp_count(cv);
         const double a_u0 = s0 * ru, a_v0 = (w00 + w01) * rv, a_u1 = (p00 + p10) * ru, a_v1 = (p00 + p01) * rv;
-        const double a_h0 = __builtin_amdgcn_ballot_w64(ch == 3) ? (s0 + w01 + w11) / D(ch)
+        const double a_h0 = __builtin_expect(__builtin_amdgcn_ballot_w64(ch == 3) != 0, 0) ? (s0 + w01 + w11) / D(ch)
                                                                  : (s0 + w01 + w11) * rcp_count(ch);
         if (!E) {   // (a / g1) / g2: a's range bounds a / g1's (|g1| <= 2^60)
             exp_check(acc, a_u0); exp_check(acc, a_v0); exp_check(acc, a_h0); exp_check(acc, a_u1);
@@ -1463,7 +1463,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             o.sshn = sshn; o.fx = fx; o.un = un; o.fa = fa; o.vn = vn; o.fb = fb;
             // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
             const bool bd = o.lu && !(sshn < 10000.0 && sshn > -10000.0);
-            if (nbad && bd != (E && bad)) atomicAdd(nbad, bd ? 1 : -1);
+            if (__builtin_expect(nbad && bd != (E && bad), 0)) atomicAdd(nbad, bd ? 1 : -1);
             bad = bd;
             return;
         }
@@ -1597,7 +1597,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             int acc = 0;
             double qb, qc;
             derive<false, PH>(x, fb, acc, qb, qc);
-            if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) derive<true, PH>(x, fb, acc, qb, qc);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) derive<true, PH>(x, fb, acc, qb, qc);
             x.qb = qb;
             x.qc = qc;
         }
@@ -1606,7 +1606,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             int acc = 0;
             bool bad = false;
             step<false, PH>(x, L, n, acc, bad, o);
-            if (__builtin_amdgcn_ballot_w64(acc < kUdivMinExp)) step<true, PH>(x, L, n, acc, bad, o);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) step<true, PH>(x, L, n, acc, bad, o);
         }
 #if OCN_STEP_BUFST
         if (!LAST) store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
