@@ -260,7 +260,8 @@ def main():
     ap.add_argument("--no-known-constants", action="store_true",
                     help="one-pass steps in their general variant only (no known-constant specialization)")
     ap.add_argument("--overlap", type=int, default=-1, choices=[-1, 0, 1, 2],
-                    help="halo exchanges beside inner launches: 0 never, 1 standard steps, 2 role-flip steps too, "
+                    help="halo exchanges beside inner launches: 0 never, 1 standard steps and the one-pass steps' side "
+                         "chain, 2 role-flip steps too, "
                          "-1 the library default (2 with RCCL peers, else 1)")
     ap.add_argument("--blocks", default=None,
                     help="block grid BXxBY (default: one block per GPU); with one GPU, several blocks on it "

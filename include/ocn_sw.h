@@ -294,7 +294,9 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_GRAPH: replay each step as one hipGraph (single-process runs).
  *  OCN_OPT_OVERLAP (default -1 = auto): with halo exchanges, run each exchange on a second stream
  *  beside the launches' inner parts (points that neither read halos nor feed the exchange): 1 = in
- *  the standard steps, 2 = in the role-flip steps too, 0 = never (same results bit for bit); auto
+ *  the standard steps and in the one-pass steps (there the frame launches and both exchanges as one
+ *  chain on the second stream beside the whole inner march), 2 = in the role-flip steps too,
+ *  0 = never (same results bit for bit); auto
  *  is 2 when the context exchanges with other ranks (RCCL or loopback attached, nranks > 1), else
  *  1.  ocn_ctx_get_option returns the level in effect.
  *  OCN_OPT_STAGE_TIMING: bracket every launch group with HIP events on the context stream.

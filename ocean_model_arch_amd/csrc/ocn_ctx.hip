@@ -1137,12 +1137,18 @@ static Range onepass_inner(const LBlock &b, int w)
 // reference never exchanges that.  So the points one away from an exchanged side take the
 // role-flip path (D stored by CA, exchanged, read back by B) and the rest the one-pass march:
 //   CA frame (hh_init of the previous step + this step's A, on the bands two points deep along
-//   the exchanged sides and their halos) | sync CA || one-pass on the inner part's first half |
-//   join | B on the one-point bands | sync B || the inner part's second half | join | swap |
-//   ring launch (a8 + a9 on the halo ring); without overlap the exchanges run in place.
+//   the exchanged sides and their halos) | sync CA | B on the one-point bands | sync B, as a side
+//   chain on the comm stream beside the one-pass march of the inner part on the compute stream |
+//   join | swap | ring launch (a8 + a9 on the halo ring).  With OCN_OPT_OVERLAP 0 (or while
+//   capturing a graph) the same launches run in that order on one stream, the inner march
+//   between sync CA and B.  (The side chain is the overlap of every level >= 1: with local copies
+//   too it hides the latency-bound frame launches -- one GPU, 4x2 blocks of a 4096^2 box: 0.947
+//   -> 0.856 ms per step, 2x2 of 2048^2: 0.334 -> 0.294; the earlier split of the inner march
+//   into two halves beside the two exchanges took 1.065 / 0.398.)
 // All of a8's filtered sshp / ubrtrp / vbrtrp go to the second buffers (the inner part reads the
 // current ones at neighbours); the ring launch reads the current ones and writes the new ones on
 // the ring after the swap, as the recompute steps do with sshp.
+static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k);
 static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
 {
     const ocn_sw_params &sw = c->sw;
@@ -1155,65 +1161,88 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
     int32_t *nbad = k.check ? c->d_nbad : nullptr;
     hipStream_t s = c->stream;
     const bool xch = has_exchange(c);
-    const bool ov = xch && overlap_level(c) >= 2 && !c->capturing;
     // the previous step's hh_init and this step's A on the frames (bnd range outside inner_ca)
-    RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
-    for (const LBlock &b : c->blocks) {
-        Range in = onepass_inner(b, 2);
-        if (b.nbr_rank[1] < 0) in.m0 = b.g.bnd_x1;   // no frame on the sides without a neighbour
-        if (b.nbr_rank[0] < 0) in.m1 = b.g.bnd_x2;
-        if (b.nbr_rank[3] < 0) in.n0 = b.g.bnd_y1;
-        if (b.nbr_rank[2] < 0) in.n1 = b.g.bnd_y2;
-        RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_FRAME, sw, tau, true, false, s,
-                           &in));
-    }
-    RC(timer_end(c, rec));
-    if (xch) {
-        if (ov) RC(fork_sync(c, c->sync_ca_reuse));
-        else RC(run_sync(c, c->sync_ca_reuse));
-    }
-    // with overlap, the inner march in two row halves: one beside sync CA, one beside sync B
-    // (it reads neither what those exchanges write nor what B writes)
-    auto inner_part = [&](const LBlock &b, int half) {
-        Range in = onepass_inner(b, 1);
-        if (ov) {
-            const int mid = (in.n0 + in.n1) / 2;
-            if (half == 0) in.n1 = mid;
-            else in.n0 = mid + 1;
-        } else if (half == 1) {
-            in.n1 = in.n0 - 1;   // empty
-        }
-        return in;
-    };
-    auto inner = [&](int half) -> int {
-        RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+    auto ca_frames = [&](hipStream_t st) -> int {
         for (const LBlock &b : c->blocks) {
-            const Range in = inner_part(b, half);
-            RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
-                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, false, c->fb_zero, b.hr0, b.mu0));
+            Range in = onepass_inner(b, 2);
+            if (b.nbr_rank[1] < 0) in.m0 = b.g.bnd_x1;   // no frame on the sides without a neighbour
+            if (b.nbr_rank[0] < 0) in.m1 = b.g.bnd_x2;
+            if (b.nbr_rank[3] < 0) in.n0 = b.g.bnd_y1;
+            if (b.nbr_rank[2] < 0) in.n1 = b.g.bnd_y2;
+            RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_FRAME, sw, tau, true, false,
+                               st, &in));
         }
-        RC(timer_end(c, rec));
         return OCN_OK;
     };
-    RC(inner(0));
-    RC(join_sync(c));
-    if (xch) {   // B on the one-point bands along the exchanged sides
-        RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
+    // B on the one-point bands along the exchanged sides
+    auto b_bands = [&](hipStream_t st) -> int {
         for (const LBlock &b : c->blocks) {
             const Range in = onepass_inner(b, 1);
             const Range all{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
             if (in.m0 == all.m0 && in.m1 == all.m1 && in.n0 == all.n0 && in.n1 == all.n1) continue;
-            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, true, s, nbad, true, false, (double *)b.sshp_alt,
+            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, true, st, nbad, true, false, (double *)b.sshp_alt,
                               (double *)b.up_alt, (double *)b.vp_alt, &in));
         }
+        return OCN_OK;
+    };
+    if (xch && overlap_level(c) >= 1 && !c->capturing) {
+        // side chain (OCN_OPT_OVERLAP >= 1): CA frames | sync CA | B bands | sync B on the comm stream,
+        // beside the whole inner march on the compute stream -- the two read nothing the other
+        // writes (disjoint points; the inner march forms its D from the state, the bands read
+        // CA's stored D and the exchanged halos), so the frame launches and both exchanges hide
+        // behind it
+        HIPCHK(hipEventRecord(c->ev_fork, s));
+        HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
+        RC(ca_frames(c->comm_stream));
+        RC(run_sync(c, c->sync_ca_reuse, c->comm_stream));
+        RC(b_bands(c->comm_stream));
+        RC(run_sync(c, c->sync_b, c->comm_stream));
+        HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
+        c->sync_pending = true;
+        RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+        for (const LBlock &b : c->blocks) {
+            const Range in = onepass_inner(b, 1);
+            RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
+                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, false, c->fb_zero, b.hr0, b.mu0));
+        }
         RC(timer_end(c, rec));
-        if (ov) RC(fork_sync(c, c->sync_b));
-        else RC(run_sync(c, c->sync_b));
-    }
-    if (ov) {
-        RC(inner(1));
         RC(join_sync(c));
+        return hybrid_tail(c, tau, k);
     }
+    // without overlap (or while capturing a graph): CA frames | sync CA | inner | B bands | sync B
+    RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
+    RC(ca_frames(s));
+    RC(timer_end(c, rec));
+    if (xch) RC(run_sync(c, c->sync_ca_reuse));
+    RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+    for (const LBlock &b : c->blocks) {
+        const Range in = onepass_inner(b, 1);
+        RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
+                          (double *)b.up_alt, (double *)b.vp_alt, s, &in, false, c->fb_zero, b.hr0, b.mu0));
+    }
+    RC(timer_end(c, rec));
+    if (xch) {
+        RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
+        RC(b_bands(s));
+        RC(timer_end(c, rec));
+        RC(run_sync(c, c->sync_b));
+    }
+    return hybrid_tail(c, tau, k);
+}
+
+// the end of a hybrid one-pass step (one_step_hybrid): the role swaps, the ring launch, and the
+// next step's CA + sync before a standard last step
+static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k)
+{
+    const ocn_sw_params &sw = c->sw;
+    ocn_ctx::Rec rec;
+    Compact t;
+    auto cp = [c](const LBlock &b, Compact &tt) -> const Compact * {
+        tt = Compact{b.bits, b.rows, c->march};
+        return &tt;
+    };
+    hipStream_t s = c->stream;
+    const bool xch = has_exchange(c);
     swap_alt3(c);
     std::vector<std::vector<void *>> pre;   // the ring launch's field tables (pair roles before the swap)
     for (const LBlock &b : c->blocks) pre.push_back(b.ptr);

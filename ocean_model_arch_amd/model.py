@@ -145,7 +145,8 @@ class OceanModel:
 
     def set_overlap(self, on: int = -1):
         """Overlap halo exchanges (comm stream) with the inner part of the fused launches: 1 = in
-        the standard steps, 2 = in the role-flip steps too, 0 = never, -1 = auto (the default:
+        the standard steps and (frame launches + exchanges as a side chain beside the inner march)
+        in the one-pass steps, 2 = in the role-flip steps too, 0 = never, -1 = auto (the default:
         2 with other ranks attached, else 1)."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_OVERLAP, int(on)), "ocn_ctx_set_option")
         return self
