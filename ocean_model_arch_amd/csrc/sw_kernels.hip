@@ -1366,8 +1366,9 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
 
     // a row's outputs and where they are stored (OCN_STEP_BUFST: stored after S's branch)
     struct Out {
-        bool lu = false, cu = false, cv = false;
+        bool lu = false, cu = false, cv = false, uu = false;   // uu: luu (LAST's vort / str_s)
         double sshn = 0.0, fx = 0.0, un = 0.0, fa = 0.0, vn = 0.0, fb = 0.0;
+        double vort = 0.0, sts = 0.0, stt = 0.0, rxa = 0.0, rxd = 0.0, rya = 0.0, ryd = 0.0;   // LAST
     };
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
     // uv_trans_math, uv_diff2_math, sw_update_uv_math written out over the shared products)
@@ -1455,12 +1456,17 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const double fx = asselin(x.ssh.s<PH>(1), sshn, x.shp.s<PH>(1), ts);
         const double fa = asselin(u, un, x.up.s<PH>(1), ts), fb = asselin(v, vn, x.vp.s<PH>(1), ts);
 #if OCN_STEP_BUFST
-        if (!LAST) {   // the row's stores are issued after the branch (iteration, st_on)
+        {   // the row's stores are issued after the branch (iteration, st_on)
             const unsigned bc = x.bits.s<PH>(1);
             o.lu = L.out && (bc & (1u << OCN_LU));
             o.cu = L.out && (bc & (1u << OCN_LCU));
             o.cv = L.out && (bc & (1u << OCN_LCV));
             o.sshn = sshn; o.fx = fx; o.un = un; o.fa = fa; o.vn = vn; o.fb = fb;
+            if (LAST) {
+                o.uu = L.out && (bc & (1u << OCN_LUU));
+                o.vort = x.vort.s<PH>(1); o.sts = x.sts.s<PH>(1); o.stt = x.stt.s<PH>(1);
+                o.rxa = rxa; o.rxd = rxd; o.rya = rya; o.ryd = ryd;
+            }
             // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
             const bool bd = o.lu && !(sshn < 10000.0 && sshn > -10000.0);
             if (__builtin_expect(nbad && bd != (E && bad), 0)) atomicAdd(nbad, bd ? 1 : -1);
@@ -1499,6 +1505,15 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         st_on(up_out, nbytes, c, o.fa, o.cu);
         st_on(t.f(OCN_VBRTRN), nbytes, c, o.vn, o.cv);
         st_on(vp_out, nbytes, c, o.fb, o.cv);
+        if (LAST) {   // what the reference's last step leaves (see MarchStep)
+            st_on(t.f(OCN_VORT), nbytes, c, o.vort, o.uu);
+            st_on(t.f(OCN_STR_S), nbytes, c, o.sts, o.uu);
+            st_on(t.f(OCN_STR_T), nbytes, c, o.stt, o.lu);
+            st_on(t.f(OCN_RHSX_ADV), nbytes, c, o.rxa, o.cu);
+            st_on(t.f(OCN_RHSX_DIF), nbytes, c, o.rxd, o.cu);
+            st_on(t.f(OCN_RHSY_ADV), nbytes, c, o.rya, o.cv);
+            st_on(t.f(OCN_RHSY_DIF), nbytes, c, o.ryd, o.cv);
+        }
     }
 
     static constexpr bool kLds = OCN_STEP_LDS && (ZF || OCN_STEP_LDS_GENERAL);
@@ -1562,7 +1577,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         Batch q;
         load(q, L.m, n0);
 #if OCN_STEP_BUFST
-        if (!LAST) store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
+        store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
 #endif
         if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
             for (int n = n0;; n += kRing) {
@@ -1609,7 +1624,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) step<true, PH>(x, L, n, acc, bad, o);
         }
 #if OCN_STEP_BUFST
-        if (!LAST) store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
+        store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
 #endif
         ++x.rn;
         fb = fbn;
