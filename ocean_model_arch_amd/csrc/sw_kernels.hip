@@ -948,6 +948,15 @@ template <bool HH, bool SKIP> struct MarchCA {
 #ifndef OCN_STEP_BUFST
 #define OCN_STEP_BUFST 1   // the step's stores as st_on (no exec branches around them)
 #endif
+#ifndef OCN_STEP_ONEBLOCK
+#define OCN_STEP_ONEBLOCK 1   // D(n+1) and S(n) in one basic block, warm-up rows peeled (MarchStep::iteration)
+#endif
+#ifndef OCN_STEP_JOINT
+#define OCN_STEP_JOINT 0   // 1: one IEEE re-run test after D and S (else D's before S, as without ONEBLOCK)
+#endif
+#ifndef OCN_STEP_SCHEDB
+#define OCN_STEP_SCHEDB -1   // (JOINT) sched_barrier mask between D and S: only LDS reads and SALU cross (-1: none)
+#endif
 // A whole role-flip step in one register march (ocn_ctx.hip one_step_fused, "one-pass" steps of
 // a single-block call): the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp; h_r, mu, RHSx, RHSy)
 // is read once and the next state written once -- 10 + 6 arrays, against fused B + CA's 22 + 12.
@@ -1316,8 +1325,16 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
                      ryt = x.cst<kLds>(RC_RDYT, 1);
         const double ru = rcp_count(cu), rv = rcp_count(cv);
         const double a_u0 = s0 * ru, a_v0 = (w00 + w01) * rv, a_u1 = (p00 + p10) * ru, a_v1 = (p00 + p01) * rv;
+#if OCN_STEP_ONEBLOCK
+        // a / 3 (three sea corners): udiv by 3 (the same correctly rounded quotient: its dividend's
+        // range is checked with the others below), IEEE division in the re-run -- per lane, no branch
+        const double sh = s0 + w01 + w11;
+        const double a_h0 = ch == 3 ? (E ? sh / 3.0 : udiv(sh, 3.0, 1.0 / 3.0)) : sh * rcp_count(ch);
+        if (!E) exp_check(acc, sh);
+#else
         const double a_h0 = __builtin_expect(__builtin_amdgcn_ballot_w64(ch == 3) != 0, 0) ? (s0 + w01 + w11) / D(ch)
                                                                  : (s0 + w01 + w11) * rcp_count(ch);
+#endif
         if (!E) {   // (a / g1) / g2: a's range bounds a / g1's (|g1| <= 2^60)
             exp_check(acc, a_u0); exp_check(acc, a_v0); exp_check(acc, a_h0); exp_check(acc, a_u1);
             exp_check(acc, a_v1); exp_check(acc, x.up.s<PH>(2)); exp_check(acc, x.vp.s<PH>(2)); exp_check(acc, x.up.s<PH>(3));
@@ -1579,6 +1596,28 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
 #if OCN_STEP_BUFST
         store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
 #endif
+#if OCN_STEP_ONEBLOCK
+        // the two warm-up rows (D only), then rows nb .. ne with D and S in one basic block
+        iteration<0, true>(x, fb, q, L, n0, nb, ne);
+        if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
+            iteration<1, true>(x, fb, q, L, n0 + 1, nb, ne);
+            for (int n = nb;; n += kRing) {
+                if (iteration<2>(x, fb, q, L, n, nb, ne)) break;
+                if (iteration<3>(x, fb, q, L, n + 1, nb, ne)) break;
+                if (iteration<4>(x, fb, q, L, n + 2, nb, ne)) break;
+                if (iteration<0>(x, fb, q, L, n + 3, nb, ne)) break;
+                if (iteration<1>(x, fb, q, L, n + 4, nb, ne)) break;
+            }
+        } else {
+            x.rotate();
+            iteration<0, true>(x, fb, q, L, n0 + 1, nb, ne);
+            x.rotate();
+            for (int n = nb;; ++n) {
+                if (iteration<0>(x, fb, q, L, n, nb, ne)) break;
+                x.rotate();
+            }
+        }
+#else
         if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
             for (int n = n0;; n += kRing) {
                 if (iteration<0>(x, fb, q, L, n, nb, ne)) break;
@@ -1593,10 +1632,15 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
                 x.rotate();
             }
         }
+#endif
     }
 
-    // iteration n (phase PH): D(n+1), and S(n) from n = nb on; true after the last (n = ne)
-    template <int PH>
+    // iteration n (phase PH): D(n+1), and S(n) from n = nb on; true after the last (n = ne).
+    // OCN_STEP_ONEBLOCK: WARM = a warm-up row (n < nb: D only); else D(n+1) and S(n) are one basic
+    // block (no branch between them: the scheduler interleaves S's work with D's division chains)
+    // and one wave-uniform test after both re-runs the two with IEEE divisions if any dividend of
+    // either was out of udiv's range (nothing is stored before: store_out follows)
+    template <int PH, bool WARM = false>
     __device__ __forceinline__ bool iteration(StepRegs &x, Fallback &fb, Batch &q, const Lane &L0, int n, int nb,
                                               int ne) const
     {
@@ -1608,6 +1652,35 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         Fallback fbn;
         if (n < ne) fallback<PH>(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
         if (n < ne) load(q, L.m, n + 1);                   // in flight while this row is computed
+        Out o;
+#if OCN_STEP_ONEBLOCK
+        {
+            int acc = 0;
+            double qb, qc;
+            derive<false, PH>(x, fb, acc, qb, qc);
+#if !OCN_STEP_JOINT
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0))
+                derive<true, PH>(x, fb, acc, qb, qc);
+            acc = 0;
+#endif
+            if (WARM) {
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0))
+                    derive<true, PH>(x, fb, acc, qb, qc);
+            } else {
+                bool bad = false;
+#if OCN_STEP_SCHEDB >= 0
+                __builtin_amdgcn_sched_barrier(OCN_STEP_SCHEDB);   // what may move between D and S
+#endif
+                step<false, PH>(x, L, n, acc, bad, o);
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) {
+                    if (OCN_STEP_JOINT) derive<true, PH>(x, fb, acc, qb, qc);
+                    step<true, PH>(x, L, n, acc, bad, o);
+                }
+            }
+            x.qb = qb;
+            x.qc = qc;
+        }
+#else
         {   // D(n+1) with udiv; again with IEEE divisions if a dividend is out of its range
             int acc = 0;
             double qb, qc;
@@ -1616,13 +1689,13 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             x.qb = qb;
             x.qc = qc;
         }
-        Out o;
         if (n >= nb) {   // wave-uniform
             int acc = 0;
             bool bad = false;
             step<false, PH>(x, L, n, acc, bad, o);
             if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) step<true, PH>(x, L, n, acc, bad, o);
         }
+#endif
 #if OCN_STEP_BUFST
         store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
 #endif
