@@ -331,6 +331,9 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_KNOWN_CONSTANTS (default 1): the one-pass steps take the forcing and D's fallback
  *  values as zero and h_r, mu as uniform constants when a check of the arrays (at the first
  *  one-pass call, and after any field is handed in) finds them so; 0: always the general variant.
+ *  OCN_OPT_ONEPASS_LAST (default 1): with halo exchanges or a8 / a9 work on the halo ring, the
+ *  call's last step as a one-pass step too (the inner march storing what the reference's last
+ *  step leaves, then a8's copies and hh_init with every level); 0: a standard last step there.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
  * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
@@ -340,7 +343,7 @@ int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9,
-       OCN_OPT_KNOWN_CONSTANTS = 10 };
+       OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,

@@ -77,6 +77,7 @@ OPT_FLIP = 7
 OPT_RECOMPUTE = 8
 OPT_ONEPASS = 9
 OPT_KNOWN_CONSTANTS = 10
+OPT_ONEPASS_LAST = 11
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",

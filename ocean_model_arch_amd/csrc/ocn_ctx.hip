@@ -292,6 +292,7 @@ struct ocn_ctx {
     bool recompute = true;  // OCN_OPT_RECOMPUTE: recompute steps in role-flip calls
     bool onepass = true;    // OCN_OPT_ONEPASS: one-pass steps in single-block role-flip calls
     bool known_const = true;   // OCN_OPT_KNOWN_CONSTANTS: the one-pass step's known-constant variant
+    bool last_hybrid = true;   // OCN_OPT_ONEPASS_LAST: one-pass last steps with exchanges / ring work too
     bool one_used = false;
     // the one-pass steps' second sshp / ubrtrp / vbrtrp buffers agree with the fields outside a8's
     // write set (else they are copied at the start of the next such call)
@@ -1148,8 +1149,13 @@ static Range onepass_inner(const LBlock &b, int w)
 // All of a8's filtered sshp / ubrtrp / vbrtrp go to the second buffers (the inner part reads the
 // current ones at neighbours); the ring launch reads the current ones and writes the new ones on
 // the ring after the swap, as the recompute steps do with sshp.
-static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k);
-static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
+static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k, bool last);
+// last: the call's last step (StepKind::one_last with exchanges or ring work): the CA frames' A
+// stores hh_update's levels and sync CA exchanges them (the halo values the reference's a2 sync
+// leaves and its a9 on the halo ring reads), the inner march also stores vort, the stresses and
+// the RHS terms (MarchStep<.., true>), B on the bands keeps the RHS terms (fused B `full`), and the
+// tail adds a8's copies and hh_init with every level + its sync
+static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last = false)
 {
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
@@ -1169,7 +1175,7 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
             if (b.nbr_rank[0] < 0) in.m1 = b.g.bnd_x2;
             if (b.nbr_rank[3] < 0) in.n0 = b.g.bnd_y1;
             if (b.nbr_rank[2] < 0) in.n1 = b.g.bnd_y2;
-            RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_FRAME, sw, tau, true, false,
+            RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_FRAME, sw, tau, !last, false,
                                st, &in));
         }
         return OCN_OK;
@@ -1180,7 +1186,7 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
             const Range in = onepass_inner(b, 1);
             const Range all{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
             if (in.m0 == all.m0 && in.m1 == all.m1 && in.n0 == all.n0 && in.n1 == all.n1) continue;
-            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, false, true, st, nbad, true, false, (double *)b.sshp_alt,
+            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, last, true, st, nbad, true, false, (double *)b.sshp_alt,
                               (double *)b.up_alt, (double *)b.vp_alt, &in));
         }
         return OCN_OK;
@@ -1194,7 +1200,7 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
         HIPCHK(hipEventRecord(c->ev_fork, s));
         HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
         RC(ca_frames(c->comm_stream));
-        RC(run_sync(c, c->sync_ca_reuse, c->comm_stream));
+        RC(run_sync(c, last ? c->sync_ca : c->sync_ca_reuse, c->comm_stream));
         RC(b_bands(c->comm_stream));
         RC(run_sync(c, c->sync_b, c->comm_stream));
         HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
@@ -1203,22 +1209,22 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
         for (const LBlock &b : c->blocks) {
             const Range in = onepass_inner(b, 1);
             RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
-                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, false, c->fb_zero, b.hr0, b.mu0));
+                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, c->fb_zero, b.hr0, b.mu0));
         }
         RC(timer_end(c, rec));
         RC(join_sync(c));
-        return hybrid_tail(c, tau, k);
+        return hybrid_tail(c, tau, k, last);
     }
     // without overlap (or while capturing a graph): CA frames | sync CA | inner | B bands | sync B
     RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
     RC(ca_frames(s));
     RC(timer_end(c, rec));
-    if (xch) RC(run_sync(c, c->sync_ca_reuse));
+    if (xch) RC(run_sync(c, last ? c->sync_ca : c->sync_ca_reuse));
     RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
     for (const LBlock &b : c->blocks) {
         const Range in = onepass_inner(b, 1);
         RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
-                          (double *)b.up_alt, (double *)b.vp_alt, s, &in, false, c->fb_zero, b.hr0, b.mu0));
+                          (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, c->fb_zero, b.hr0, b.mu0));
     }
     RC(timer_end(c, rec));
     if (xch) {
@@ -1227,12 +1233,14 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k)
         RC(timer_end(c, rec));
         RC(run_sync(c, c->sync_b));
     }
-    return hybrid_tail(c, tau, k);
+    return hybrid_tail(c, tau, k, last);
 }
 
 // the end of a hybrid one-pass step (one_step_hybrid): the role swaps, the ring launch, and the
-// next step's CA + sync before a standard last step
-static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k)
+// next step's CA + sync before a standard last step -- or, on the call's last step, a8's copies
+// (both buffers of each pair end equal, as one_step_last leaves them) and hh_init with every level
+// (a10; the levels a9 and hh_update leave are rewritten by it on the same ranges) and its sync
+static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k, bool last)
 {
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
@@ -1255,6 +1263,17 @@ static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k)
                                (const double *)b.sshp_alt, (const double *)b.up_alt, (const double *)b.vp_alt));
         }
         RC(timer_end(c, rec));
+    }
+    if (last) {
+        for (const LBlock &b : c->blocks)
+            for (const auto &pr : kFlipPairs)
+                HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr[1])], b.ptr[field_slot(pr[0])], field_bytes(b),
+                                      hipMemcpyDeviceToDevice, s));
+        RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
+        for (const LBlock &b : c->blocks) RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, true, s));
+        RC(timer_end(c, rec));
+        if (xch) RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
+        return OCN_OK;
     }
     if (k.next_a) {   // the next step is the last, standard one: hh_init + its fused A, then their sync
         RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
@@ -1304,7 +1323,7 @@ static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
 
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
-    if (k.one_last) return one_step_last(c, tau, k);
+    if (k.one_last) return has_exchange(c) || c->ring_sea ? one_step_hybrid(c, tau, k, true) : one_step_last(c, tau, k);
     const bool check = k.check, first = k.first, last = k.last, flip = k.flip;
     const ocn_sw_params &sw = c->sw;
     ocn_ctx::Rec rec;
@@ -1992,7 +2011,9 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
                           c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 && c->sw.use_tracers <= 0 && c->udiv_ok;
     c->hh_consistent = false;   // until this call's last step has run
     // the last step as one march + hh_init too (single block, no exchange, no ring work)
-    const bool last_one = one_call && c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) && !c->ring_sea;
+    // (with exchanges or ring work: the hybrid last step, OCN_OPT_ONEPASS_LAST)
+    const bool last_one = one_call && ((c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) && !c->ring_sea) ||
+                                       c->last_hybrid);
     c->one_used = one_call;
     if (one_call && (!c->fb_zero_known || c->r8_handed)) {   // until something may write the D arrays from outside
         HIPCHK(hipMemsetAsync(c->d_flags, 0, sizeof(int32_t), c->stream));
@@ -2176,6 +2197,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     case OCN_OPT_FLIP: c->flip = value != 0; return OCN_OK;
     case OCN_OPT_RECOMPUTE: c->recompute = value != 0; return OCN_OK;
     case OCN_OPT_ONEPASS: c->onepass = value != 0; return OCN_OK;
+    case OCN_OPT_ONEPASS_LAST: c->last_hybrid = value != 0; return OCN_OK;
     case OCN_OPT_KNOWN_CONSTANTS:
         c->known_const = value != 0;
         c->fb_zero_known = false;   // checked again at the next one-pass call
@@ -2203,6 +2225,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_RECOMPUTE: *value = c->recompute && c->rc_used; return OCN_OK;
     case OCN_OPT_ONEPASS: *value = c->onepass && c->one_used ? (c->fb_zero ? 2 : 1) : 0; return OCN_OK;
     case OCN_OPT_KNOWN_CONSTANTS: *value = c->known_const; return OCN_OK;
+    case OCN_OPT_ONEPASS_LAST: *value = c->last_hybrid; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

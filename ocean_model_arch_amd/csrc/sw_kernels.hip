@@ -1837,7 +1837,9 @@ int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compac
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
     const Range r = range_bnd(b);
     if (inner) {   // the frame of a one-pass step with halo exchanges: the bnd range outside *inner
-        if (skip_rc || !next_reuse) return set_error(OCN_ERR_ARG, "fused CA frame: reuse steps only");
+        if (skip_rc) return set_error(OCN_ERR_ARG, "fused CA frame: no recompute steps");
+        if (!next_reuse)   // the call's last step: A stores hh_update's levels (its sync exchanges them)
+            return launch_march_frame(b, r, *inner, MarchCA<true, false>{*b, t, sw, tau_next}, s);
         return launch_march_frame(b, r, *inner, MarchCA<false, false>{*b, t, sw, tau_next}, s);
     }
     if (skip_rc) return launch_march_part(b, r, part, MarchCA<false, true>{*b, t, sw, tau_next}, s);
@@ -1940,7 +1942,6 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
     const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
 #define OCN_STEP_LAUNCH(P, L, Z) \
     return launch_step(b, r, MarchStep<P, L, Z>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out, hr0, mu0}, s)
-    if (last && range) return set_error(OCN_ERR_ARG, "one-pass last step: whole interior only");
     if (zero_fallback) {
         if (last) { if (p2) OCN_STEP_LAUNCH(true, true, true); OCN_STEP_LAUNCH(false, true, true); }
         if (p2) OCN_STEP_LAUNCH(true, false, true);

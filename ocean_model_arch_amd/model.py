@@ -183,6 +183,12 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_ONEPASS, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_onepass_last(self, on: bool = True):
+        """With halo exchanges or ring work, the call's last step as a one-pass step too (default);
+        off: a standard last step there (same results bit for bit)."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_ONEPASS_LAST, int(on)), "ocn_ctx_set_option")
+        return self
+
     def set_known_constants(self, on: bool = True):
         """The one-pass steps' known-constant variant (default): forcing and D's fallback values
         zero, h_r and mu uniform, when a check of the arrays finds them so; off: always the

@@ -61,6 +61,7 @@ MODES = {   # name -> build_model options
     "noflip": dict(flip=False),
     "noflip_overlap0": dict(flip=False, overlap=0),
     "norecompute": dict(recompute=False),
+    "nolast": dict(onepass_last=False),
     "stages": dict(fused=False),
 }
 

@@ -112,7 +112,7 @@ def test_tracer_kernels_match_reference(amd, geom):
 
 
 def build_model(amd, case, graph=False, fused=True, compact=True, overlap=None, march=True, flip=True,
-                recompute=True, rank=0, nranks=1, onepass=True):
+                recompute=True, rank=0, nranks=1, onepass=True, onepass_last=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"])
@@ -127,6 +127,7 @@ def build_model(amd, case, graph=False, fused=True, compact=True, overlap=None, 
     m.set_flip(flip)
     m.set_recompute(recompute)
     m.set_onepass(onepass)
+    m.set_onepass_last(onepass_last)
     if graph:
         m.set_graph(True)
     return m
@@ -152,32 +153,34 @@ def compare_case(m, case, name, whole=True):
     return bad
 
 
-@pytest.mark.parametrize("mode", ["compact", "noonepass", "norecompute", "noflip", "pointwise", "fused", "stages",
-                                  "serial", "overlap2"])
+@pytest.mark.parametrize("mode", ["compact", "noonepass", "nolast", "norecompute", "noflip", "pointwise", "fused",
+                                  "stages", "serial", "overlap2"])
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
     hh_init as register marches, role-flip steps, tracer runs included (hh_init fused with the next
     step's A, fused B recomputing hhq / hhu_p / hhv_p), halo exchanges overlapped
     with inner launches in the standard steps when there are several blocks;
-    norecompute = compact without the recompute steps; noflip = compact with standard steps only;
+    nolast = compact with a standard last step where exchanges or ring work make the one-pass last
+    step a hybrid one; norecompute = compact without the recompute steps; noflip = compact with
+    standard steps only;
     pointwise = compact with every launch one thread per point; overlap2 = compact with the
     role-flip steps' exchanges overlapped too (OCN_OPT_OVERLAP = 2); fused =
     the 4-launch step on the 2-D real(4) arrays; serial = compact without the overlap; stages =
     the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    compact = mode in ("compact", "noonepass", "norecompute", "noflip", "serial", "pointwise", "overlap2")
+    compact = mode in ("compact", "noonepass", "nolast", "norecompute", "noflip", "serial", "pointwise", "overlap2")
     m = build_model(amd, case, fused=mode != "stages", compact=compact,
                     overlap=2 if mode == "overlap2" else int(mode != "serial"),
                     march=mode != "pointwise", flip=mode != "noflip", recompute=mode != "norecompute",
-                    onepass=mode != "noonepass")
+                    onepass=mode != "noonepass", onepass_last=mode != "nolast")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     assert m.compact_active == compact
     bad = compare_case(m, case, name)
     flip_used, one_used = m.flip_active, m.onepass_active
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
-    if mode in ("compact", "noonepass", "norecompute", "serial", "overlap2"):   # tracer runs included
+    if mode in ("compact", "noonepass", "nolast", "norecompute", "serial", "overlap2"):   # tracer runs included
         assert flip_used, f"{name}: role-flip steps not used"
     if mode == "compact" and name.startswith("box") and "_b1x1_" in name and case["sw"]["trans_terms"] > 0 \
             and case["sw"]["ksw_lat"] > 0:
