@@ -1103,7 +1103,12 @@ __device__ __forceinline__ double rcp_count(unsigned c)
 #ifndef OCN_STEP_UNROLL
 #define OCN_STEP_UNROLL 1
 #endif
-constexpr int kRing = 5;   // StepRegs::Win: 4 rows, written out for 5 phases (MarchStep::march)
+#ifndef OCN_STEP_PF2
+#define OCN_STEP_PF2 0   // 1: the known-constant variant issues each row's loads two rows ahead (measured: no gain)
+#endif
+// StepRegs::Win: 4 rows, written out for kRing phases (MarchStep::march); even with OCN_STEP_PF2,
+// so that the batch a phase takes (phase parity) is known in every unrolled phase
+constexpr int kRing = OCN_STEP_PF2 ? 6 : 5;
 
 struct StepRegs {
     // rows n-1, n, n+1, n+2 at this lane's column: a ring of kRing slots, row n + k - 1 in slot
@@ -1538,6 +1543,8 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     // general one (loaded h_r, mu, forcing, fallback values) keeps the rotating loop: unrolled,
     // its scalar and vector registers spill
     static constexpr bool kUnroll = ZF && OCN_STEP_UNROLL;
+    // rows ahead a batch is loaded (MarchStep::march): 2 in the unrolled variant with OCN_STEP_PF2
+    static constexpr int kAhead = OCN_STEP_PF2 && OCN_STEP_ONEBLOCK && OCN_STEP_BUFST && kUnroll ? 2 : 1;
 #if OCN_STEP_LDS
     static constexpr bool kPrologue = kLds;
     // the row constants of the workgroup's rows into LDS (rows fit: launch_step's tiles have at
@@ -1591,6 +1598,26 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         }
         Fallback fb;
         fallback<0>(x, fb, L.m, n0 + 1, 2);
+#if OCN_STEP_ONEBLOCK && OCN_STEP_PF2 && OCN_STEP_BUFST
+        if constexpr (kUnroll) {   // two batches in flight: iteration n takes qs[n - n0 & 1], loaded at n - 2
+            Batch qs[2];
+            load(qs[0], L.m, n0);
+            store_out(Out{}, 0u);   // (every lane dropped: the same operations after each batch's loads as
+            load(qs[1], L.m, n0 + 1);   // in the loop, so its waits stay vmcnt(19))
+            store_out(Out{}, 0u);
+            iteration<0, true>(x, fb, qs[0], L, n0, nb, ne);
+            iteration<1, true>(x, fb, qs[1], L, n0 + 1, nb, ne);
+            for (int n = nb;; n += kRing) {
+                if (iteration<2>(x, fb, qs[0], L, n, nb, ne)) break;
+                if (iteration<3>(x, fb, qs[1], L, n + 1, nb, ne)) break;
+                if (iteration<4>(x, fb, qs[0], L, n + 2, nb, ne)) break;
+                if (iteration<5 % kRing>(x, fb, qs[1], L, n + 3, nb, ne)) break;
+                if (iteration<0>(x, fb, qs[0], L, n + 4, nb, ne)) break;
+                if (iteration<1>(x, fb, qs[1], L, n + 5, nb, ne)) break;
+            }
+            return;
+        }
+#endif
         Batch q;
         load(q, L.m, n0);
 #if OCN_STEP_BUFST
@@ -1651,7 +1678,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         take<PH>(x, q);
         Fallback fbn;
         if (n < ne) fallback<PH>(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
-        if (n < ne) load(q, L.m, n + 1);                   // in flight while this row is computed
+        if (n + kAhead - 1 < ne) load(q, L.m, n + kAhead);   // in flight while this row (and the next) is computed
         Out o;
 #if OCN_STEP_ONEBLOCK
         {
