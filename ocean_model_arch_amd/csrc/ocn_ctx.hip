@@ -603,6 +603,8 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
 static int get_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan *&out)
 {
     std::vector<int> key = fields;
+    // a plan holds the buffers its fields had when it was built: the pair roles (bit 1) matter; no
+    // sync list holds sshp / ubrtrp / vbrtrp, whose buffers roles 2 and 4 swap
     key.push_back(-1 - (c->role & 1));
     auto it = c->plans.find(key);
     if (it == c->plans.end()) {
@@ -1835,6 +1837,7 @@ int ocn_ctx_block_info(const ocn_ctx *c, int k, ocn_block_info *out)
     return OCN_OK;
 }
 
+static int alt_home(ocn_ctx *c);
 void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
 {
     if (!c || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id)) {
@@ -1842,6 +1845,9 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
         return nullptr;
     }
     if (is_r4(id)) c->r4_escaped = true;   // may be written behind our back: no compact tables
+    // a raw r8 pointer names the field's own buffer from now on (step_impl returns the current
+    // values there at the end of every call)
+    if (!is_r4(id) && alt_home(const_cast<ocn_ctx *>(c)) != OCN_OK) return nullptr;
     if (is_flip_field(id)) { c->r8_escaped = true; c->coherent_known = false; }
     if (is_alt_field(id)) c->alt_ok = false;
     if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_zero_known = false; }
@@ -1987,6 +1993,20 @@ int ocn_ctx_tracer_stage(ocn_ctx *c, int stage_id, int tracer, double tau)
     return tracer_stage(c, stage_id, tracer, tau, false);
 }
 
+// the current sshp / ubrtrp / vbrtrp (in the second buffers after one-pass steps: role bit 4)
+// back into the fields' own buffers, stream-ordered
+static int alt_home(ocn_ctx *c)
+{
+    if (!(c->role & 4)) return OCN_OK;
+    for (LBlock &b : c->blocks)
+        for (const auto &pr : {std::make_pair(&b.sshp_alt, OCN_SSHP), std::make_pair(&b.up_alt, OCN_UBRTRP),
+                               std::make_pair(&b.vp_alt, OCN_VBRTRP)})
+            HIPCHK(hipMemcpyAsync(*pr.first, b.ptr[field_slot(pr.second)], field_bytes(b), hipMemcpyDeviceToDevice,
+                                  c->stream));
+    swap_alt3(c);
+    return OCN_OK;
+}
+
 static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
 {
     HIPCHK(hipSetDevice(c->dec.device));
@@ -2077,14 +2097,9 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
                                   c->stream));
         swap_sshp(c);
     }
-    if (c->role & 4) {   // one-pass steps: the current sshp / ubrtrp / vbrtrp back into the fields' buffers
-        for (LBlock &b : c->blocks)
-            for (const auto &pr : {std::make_pair(&b.sshp_alt, OCN_SSHP), std::make_pair(&b.up_alt, OCN_UBRTRP),
-                                   std::make_pair(&b.vp_alt, OCN_VBRTRP)})
-                HIPCHK(hipMemcpyAsync(*pr.first, b.ptr[field_slot(pr.second)], field_bytes(b), hipMemcpyDeviceToDevice,
-                                      c->stream));
-        swap_alt3(c);
-    }
+    // one-pass steps: sshp / ubrtrp / vbrtrp stay in the second buffers (every access goes through
+    // the field table) unless a raw r8 pointer was handed out: then back into the fields' buffers
+    if ((c->role & 4) && c->r8_handed) RC(alt_home(c));
     c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // the last step ran a full hh_init
     return rc;
 }

@@ -508,3 +508,36 @@ def test_onepass_rows_rerun_with_ieee_divisions(amd, kc):
         m.close()
     bad = [nm for nm, a in out[True].items() if not bits_equal(a, out[False][nm])]
     assert not bad, f"one-pass rows re-run with IEEE divisions differ from the role-flip path: {bad}"
+
+
+def test_second_buffers_across_calls(amd):
+    """One-pass calls leave sshp / ubrtrp / vbrtrp in their second buffers between calls (no
+    copies back at a call's end).  A raw pointer handed out afterwards holds the current values,
+    later calls keep returning them there, and the run equals one that never handed one out."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    names = ("sshp", "ubrtrp", "vbrtrp")
+    m = amd.OceanModel(amd.box_config(130)).init()
+    m.step(6, tau=1.0).synchronize()
+    assert m.onepass_active
+    ptr = {nm: m.field_ptr(0, nm) for nm in names}
+    m.synchronize()
+    b = m.blocks[0]
+    w, h = b.shape
+
+    def raw(nm):
+        a = np.zeros((h, b.pitch), dtype=np.float64)
+        assert hip.hipMemcpy(a.ctypes.data_as(C.c_void_p), C.c_void_p(ptr[nm]), C.c_size_t(a.nbytes), 2) == 0
+        return np.asfortranarray(a[:, :w].T)
+
+    for nm in names:
+        assert bits_equal(raw(nm), m.download(0, nm)), nm
+    m.step(5, tau=1.0).synchronize()
+    for nm in names:
+        assert bits_equal(raw(nm), m.download(0, nm)), nm
+    ref = amd.OceanModel(amd.box_config(130)).init()
+    ref.step(6, tau=1.0).step(5, tau=1.0).synchronize()
+    bad = [nm for nm in m.field_names if not bits_equal(m.download(0, nm), ref.download(0, nm))]
+    m.close()
+    ref.close()
+    assert not bad, bad
