@@ -1103,6 +1103,9 @@ __device__ __forceinline__ double rcp_count(unsigned c)
 #ifndef OCN_STEP_UNROLL
 #define OCN_STEP_UNROLL 1
 #endif
+#ifndef OCN_STEP_CARRY
+#define OCN_STEP_CARRY 1   // shifted weights / v kept in the ring (no second shift), sh * ffs as sh
+#endif
 #ifndef OCN_STEP_PF2
 #define OCN_STEP_PF2 0   // 1: the known-constant variant issues each row's loads two rows ahead (measured: no gain)
 #endif
@@ -1134,6 +1137,7 @@ struct StepRegs {
     // products shared between lanes / rows (each the reference's own sub-expression, see derive)
     Win<double> w0, w1;               // interp weights ((h * dx) * dy) * lu of levels 0 / 1 (rows n+1, n+2)
     Win<double> pu, pv, vh, t3, cx, rr, dt, dxq;
+    Win<double> w0r, vr;              // OCN_STEP_CARRY: w0 and v shifted one lane left (their m+1 values)
     // metric rows: read where used, as wave-uniform scalar loads from the (read-only) row table
     // through the constant address space -- no table of 4 rows x 14 values held in SGPRs
     const __attribute__((address_space(4))) float *rows;
@@ -1200,6 +1204,7 @@ struct StepRegs {
         bits.rotate();
         hu.rotate(); hv.rotate(); hh.rotate(); hu1.rotate(); hv1.rotate(); vort.rotate(); stt.rotate(); sts.rotate();
         w0.rotate(); w1.rotate(); pu.rotate(); pv.rotate(); vh.rotate(); t3.rotate(); cx.rotate(); rr.rotate();
+        w0r.rotate(); vr.rotate();
         dt.rotate(); dxq.rotate();
     }
     template <int PH> __device__ __forceinline__ unsigned bit(int id, int dx, int dy) const
@@ -1271,8 +1276,14 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const int k = dy + 1;
         const double gx = x.cst<kLds>(RC_DX, dy), gy = x.cst<kLds>(RC_DY, dy);
         const double l = D(x.mk<PH>(OCN_LU, 0, dy));
+#if OCN_STEP_CARRY   // ffs = 1 (launch_onepass requires it): sh * ffs is sh bit for bit
+        x.w0.s<PH>(k) = (x.hr.s<PH>(k) + x.ssh.s<PH>(k)) * gx * gy * l;
+        x.w1.s<PH>(k) = (x.hr.s<PH>(k) + x.shp.s<PH>(k)) * gx * gy * l;
+        x.w0r.s<PH>(k) = shz(x.w0.s<PH>(k), 1);   // its right lane's weight: the corner (m+1) weight
+#else
         x.w0.s<PH>(k) = (x.hr.s<PH>(k) + x.ssh.s<PH>(k) * x.f) * gx * gy * l;
         x.w1.s<PH>(k) = (x.hr.s<PH>(k) + x.shp.s<PH>(k) * x.f) * gx * gy * l;
+#endif
     }
 
     // Where D takes the value in memory (mask 0 or outside the stage's range): those loads, issued
@@ -1323,7 +1334,11 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const unsigned cu = b00 + b10, cv = b00 + b01, ch = cu + b01 + b11;
         const double dxt = x.cst<kLds>(RC_DXT, 1), dyt = x.cst<kLds>(RC_DYT, 1), dxh = x.cst<kLds>(RC_DXH, 1),
                      dyh = x.cst<kLds>(RC_DYH, 1), dxb = x.cst<kLds>(RC_DXB, 1), dyb = x.cst<kLds>(RC_DYB, 1);
+#if OCN_STEP_CARRY   // the right lane's weights, shifted once per row (weights) and kept in the ring
+        const double w00 = x.w0.s<PH>(2), w10 = x.w0r.s<PH>(2), w01 = x.w0.s<PH>(3), w11 = x.w0r.s<PH>(3);
+#else
         const double w00 = x.w0.s<PH>(2), w10 = shz(w00, 1), w01 = x.w0.s<PH>(3), w11 = shz(w01, 1);
+#endif
         const double p00 = x.w1.s<PH>(2), p10 = shz(p00, 1), p01 = x.w1.s<PH>(3);
         const double s0 = w00 + w10;
         const double rxt = x.cst<kLds>(RC_RDXT, 1), ryh = x.cst<kLds>(RC_RDYH, 1), rxh = x.cst<kLds>(RC_RDXH, 1),
@@ -1351,6 +1366,9 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const double v1 = dv<E>(dv<E>(a_v1, dxh, rxh), dyt, ryt);
         // a3 uv_trans_vort (vel_ssh.f90:247-281, sw_stencils.h uv_trans_vort_math)
         const double u_0 = x.u.s<PH>(2), u_1 = x.u.s<PH>(3), v_0 = x.v.s<PH>(2), v_r = shz(v_0, 1);
+#if OCN_STEP_CARRY
+        x.vr.s<PH>(2) = v_r;   // S reads it at rows n and n-1 (the same shift of the same values)
+#endif
         const double vort = (v_r * dyt - v_0 * dyt) - (u_1 * x.cst<kLds>(RC_DXT, 2) - u_0 * dxt)
                             - ((v_r - v_0) * dyb - (u_1 - u_0) * dxb);
         // a5 (mixing.f90:33-44, sw_stencils.h stress_components_math) with its quotients shared:
@@ -1381,7 +1399,11 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const double rr = x.cst<kLds>(RC_RLH, 1) * hh * dxb * dyb;   // sw_update_uv: rlh_s * hhh * dxb * dyb
         x.rr.s<PH>(2) = rr;
         x.cx.s<PH>(2) = rr * (v_r + v_0);                                //   ... * (vbrtr(1,0) + vbrtr)
+#if OCN_STEP_CARRY
+        const double hq = x.hr.s<PH>(2) + x.ssh.s<PH>(2);                    // depth.f90:48 hq = h_r + sh*ffs (ffs = 1)
+#else
         const double hq = x.hr.s<PH>(2) + x.ssh.s<PH>(2) * x.f;              // depth.f90:48 hq = h_r + sh*ffs
+#endif
         x.dt.s<PH>(2) = x.cst<kLds>(RC_DY2, 1) * x.mu.s<PH>(2) * hq * stt;         // uv_diff2: dy**2 * mu * hq * str_t
         x.dxq.s<PH>(2) = x.cst<kLds>(RC_DX2, 1) * x.mu.s<PH>(2) * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
     }
@@ -1409,7 +1431,11 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         const double sshn = x.shp.s<PH>(1) + 2.0 * x.tau * (-dv<E>(a_ssh, x.cst<kLds>(RC_AREA, 0), x.cst<kLds>(RC_RAREA, 0)));
         // a4 uv_trans (vel_ssh.f90:283-373)
         const double u_r = shz(u, 1), u_l = shz(u, -1), u_n = x.u.s<PH>(2), u_s = x.u.s<PH>(0);
-        const double v_r = shz(v, 1), v_l = shz(v, -1), v_n = x.v.s<PH>(2), v_s = x.v.s<PH>(0);
+#if OCN_STEP_CARRY
+        const double v_r = x.vr.s<PH>(1), v_l = shz(v, -1), v_n = x.v.s<PH>(2), v_s = x.v.s<PH>(0), v_sr = x.vr.s<PH>(0);
+#else
+        const double v_r = shz(v, 1), v_l = shz(v, -1), v_n = x.v.s<PH>(2), v_s = x.v.s<PH>(0), v_sr = shz(v_s, 1);
+#endif
         const double pu = x.pu.s<PH>(1), pun = x.pu.s<PH>(2), pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2), pvs = x.pv.s<PH>(0);
         const double luu = D(x.mk<PH>(OCN_LUU, 0, 0)), luus = D(x.mk<PH>(OCN_LUU, 0, -1));
         double rxa, rya;
@@ -1418,7 +1444,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
             const double fx_m = (pu + shz(pu, -1)) / 2.0 * (u + u_l) / 2.0;
             const double fy_p = (pv + shz(pv, 1)) / 2.0 * (u_n + u) / 2.0 * luu;
             const double fy_m = (pvs + shz(pvs, 1)) / 2.0 * (u_s + u) / 2.0 * luus;
-            rxa = -(fx_p - fx_m + fy_p - fy_m) + (x.vh.s<PH>(1) * (v_r + v) + x.vh.s<PH>(0) * (shz(v_s, 1) + v_s)) / 4.0;
+            rxa = -(fx_p - fx_m + fy_p - fy_m) + (x.vh.s<PH>(1) * (v_r + v) + x.vh.s<PH>(0) * (v_sr + v_s)) / 4.0;
         }
         {
             const double fy_p = (pv + pvn) / 2.0 * (v + v_n) / 2.0;
