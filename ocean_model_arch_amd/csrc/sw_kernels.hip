@@ -1913,14 +1913,15 @@ int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compac
 #ifndef OCN_STEP_SLOTS
 #define OCN_STEP_SLOTS 2048
 #endif
-template <class Body> static int step_rows(const Range &r)
+template <class Body> static int step_rows(const Range &r, bool vert)
 {
-    const long wx = (r.m1 - r.m0 + 60) / 60, h = r.n1 - r.n0 + 1;
+    const long wx = (r.m1 - r.m0 + 60) / 60, h = r.n1 - r.n0 + 1, wgx = (r.m1 - r.m0 + 240) / 240;
     int best = OCN_STEP_ROWS;
     long cost = -1;
     for (int rows = OCN_STEP_ROWS; rows >= 2; --rows) {
-        const long tiles = (h + 4 * rows - 1) / (4 * rows);   // 4 vertically stacked waves per workgroup
-        const long waves = 4 * tiles * wx, rounds = (waves + OCN_STEP_SLOTS - 1) / OCN_STEP_SLOTS;
+        // vert: 4 vertically stacked waves per workgroup; else 4 side by side (240 columns)
+        const long tiles = vert ? (h + 4 * rows - 1) / (4 * rows) : (h + rows - 1) / rows;
+        const long waves = vert ? 4 * tiles * wx : 4 * tiles * wgx, rounds = (waves + OCN_STEP_SLOTS - 1) / OCN_STEP_SLOTS;
         const long c = rounds * (rows + 2);
         if (cost < 0 || c < cost) { cost = c; best = rows; }
     }
@@ -1929,8 +1930,7 @@ template <class Body> static int step_rows(const Range &r)
 template <class Body> static int launch_step(const ocn_block *b, const Range &r, const Body &body, hipStream_t s)
 {
     MarchGrid g{};
-    g.r[0] = march_rect<Body>(b, r, OCN_STEP_VERT ? step_rows<Body>(r) : fit_rows<Body>(r, OCN_STEP_ROWS),
-                              OCN_STEP_VERT != 0);
+    g.r[0] = march_rect<Body>(b, r, step_rows<Body>(r, OCN_STEP_VERT != 0), OCN_STEP_VERT != 0);
     g.nr = 1;
     g.ntiles = g.r[0].tiles;
     const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
