@@ -600,12 +600,15 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
 
 // Plans hold raw field pointers, so a plan is kept per role of the role-flip pairs (the key is
 // the field list followed by -1 - (role & 1)).
+static bool is_alt_field(int id);
 static int get_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan *&out)
 {
     std::vector<int> key = fields;
-    // a plan holds the buffers its fields had when it was built: the pair roles (bit 1) matter; no
-    // sync list holds sshp / ubrtrp / vbrtrp, whose buffers roles 2 and 4 swap
-    key.push_back(-1 - (c->role & 1));
+    // a plan holds the buffers its fields had when it was built: the pair roles (bit 1), and for
+    // sshp / ubrtrp / vbrtrp (a user's ocn_ctx_sync; no step's sync list holds them) the second
+    // buffers' roles (bit 4: they persist between one-pass calls)
+    const bool alt = std::any_of(fields.begin(), fields.end(), [](int id) { return is_alt_field(id); });
+    key.push_back(-1 - (c->role & 1) - (alt ? (c->role & 4) : 0));
     auto it = c->plans.find(key);
     if (it == c->plans.end()) {
         HaloPlan p;

@@ -541,3 +541,38 @@ def test_second_buffers_across_calls(amd):
     m.close()
     ref.close()
     assert not bad, bad
+
+
+def test_user_sync_of_second_buffer_fields(amd):
+    """ocn_ctx_sync of sshp / ubrtrp / vbrtrp between one-pass calls (their values in the second
+    buffers after an odd number of one-pass steps) and after they return home (ocn_ctx_field):
+    the halo plan follows the field's current buffer."""
+    m = amd.OceanModel(amd.box_config(130), par=amd.ParallelConfig(2, 2)).init()
+    nx = ny = 134
+    f = lambda i, j: i * 10000.0 + j   # noqa: E731
+
+    def check_sync(nm):
+        for b in m.blocks:
+            i = np.arange(b.bnd_x1, b.bnd_x2 + 1)[:, None]
+            j = np.arange(b.bnd_y1, b.bnd_y2 + 1)[None, :]
+            inner = (i >= b.nx_start) & (i <= b.nx_end) & (j >= b.ny_start) & (j <= b.ny_end)
+            m.upload(b.k, nm, np.asfortranarray(np.where(inner, f(i, j), -1.0)))
+        m.sync(nm)
+        m.synchronize()
+        for b in m.blocks:
+            i = np.arange(b.bnd_x1, b.bnd_x2 + 1)[:, None]
+            j = np.arange(b.bnd_y1, b.bnd_y2 + 1)[None, :]
+            # the 1-wide halo ring inside the global interior receives the neighbours' values
+            ring = (i >= b.nx_start - 1) & (i <= b.nx_end + 1) & (j >= b.ny_start - 1) & (j <= b.ny_end + 1)
+            glob = ring & (i >= 3) & (i <= nx - 2) & (j >= 3) & (j <= ny - 2)
+            assert bits_equal(m.download(b.k, nm), np.asfortranarray(np.where(glob, f(i, j), -1.0))), (nm, b.k)
+
+    m.step(5, tau=1.0).synchronize()
+    assert m.onepass_active
+    for nm in ("sshp", "ubrtrp", "vbrtrp"):
+        check_sync(nm)
+    m.init().step(5, tau=1.0).synchronize()   # (the patterns are no state to step from)
+    for nm in ("sshp", "ubrtrp", "vbrtrp"):
+        m.field_ptr(0, nm)   # the values return to the fields' own buffers
+        check_sync(nm)
+    m.close()
