@@ -598,8 +598,8 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
     return OCN_OK;
 }
 
-// Plans hold raw field pointers, so a plan is kept per role of the role-flip pairs (the key is
-// the field list followed by -1 - (role & 1)).
+// Plans hold raw field pointers, so a plan is kept per role of the buffers its fields swap
+// between (the key is the field list followed by -1 - the relevant role bits).
 static bool is_alt_field(int id);
 static int get_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan *&out)
 {
