@@ -241,6 +241,9 @@ struct StepKind {
 
 }  // namespace ocn
 
+#ifndef OCN_COMM_PRIO
+#define OCN_COMM_PRIO 1   // the comm stream at the device's highest stream priority
+#endif
 struct ocn_ctx {
     ocn_basin basin;
     ocn_sw_params sw;
@@ -1202,14 +1205,10 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last 
         // writes (disjoint points; the inner march forms its D from the state, the bands read
         // CA's stored D and the exchanged halos), so the frame launches and both exchanges hide
         // behind it
+        // The inner march is enqueued first (the fork event recorded before it): with several
+        // blocks the host's enqueueing of the side chain's ~3 launches per block took longer than
+        // the GPU's previous work, and the compute stream sat idle until it was done
         HIPCHK(hipEventRecord(c->ev_fork, s));
-        HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
-        RC(ca_frames(c->comm_stream));
-        RC(run_sync(c, last ? c->sync_ca : c->sync_ca_reuse, c->comm_stream));
-        RC(b_bands(c->comm_stream));
-        RC(run_sync(c, c->sync_b, c->comm_stream));
-        HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
-        c->sync_pending = true;
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
         for (const LBlock &b : c->blocks) {
             const Range in = onepass_inner(b, 1);
@@ -1217,6 +1216,13 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last 
                               (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, c->fb_zero, b.hr0, b.mu0));
         }
         RC(timer_end(c, rec));
+        HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
+        RC(ca_frames(c->comm_stream));
+        RC(run_sync(c, last ? c->sync_ca : c->sync_ca_reuse, c->comm_stream));
+        RC(b_bands(c->comm_stream));
+        RC(run_sync(c, c->sync_b, c->comm_stream));
+        HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
+        c->sync_pending = true;
         RC(join_sync(c));
         return hybrid_tail(c, tau, k, last);
     }
@@ -1727,7 +1733,15 @@ int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_de
     set_mask(c, mask);
     int rc = check_hip(hipSetDevice(dec->device), "hipSetDevice");
     if (!rc) rc = check_hip(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
-    if (!rc) rc = check_hip(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking), "hipStreamCreate");
+    // the comm stream at the highest priority: the side chains' short frame launches and the
+    // exchanges take wave slots as they free up instead of queueing behind the inner marches
+    if (!rc) {
+        int lo = 0, hi = 0;
+        rc = check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+        if (!rc)
+            rc = check_hip(hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, OCN_COMM_PRIO ? hi : lo),
+                           "hipStreamCreateWithPriority");
+    }
     if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming), "hipEventCreate");
     if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming), "hipEventCreate");
     if (!rc) rc = decompose(c);
