@@ -62,7 +62,7 @@ LAUNCH_BYTES = {
 
 
 def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
-                  tracers: int = 0, full_c2: bool = False, zero: bool = False):
+                  tracers: int = 0, full_c2: bool = False, zero: bool = False, lazy: bool = False):
     """The launches of one ocn_ctx_step call of `steps` steps, as (timer, launch kind) pairs --
     ocn_ctx.hip ocn_ctx_step / one_step_fused for one block (role-flip calls fuse each step's
     hh_init with the next step's A when full_free_surface = 1, as in sw.par; ring = the ring
@@ -79,6 +79,8 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
                 out += [("tran_diff_fluxes", "tr_fluxes"), ("tran_diff_tracer", "tr_tracer"),
                         ("tracer_next_step", "tr_next")] * tracers
         return out
+    if one and lazy:   # an open one-pass sequence (OCN_OPT_LAZY_TAIL): every step one launch, no tail
+        return [("onepass", "onepass" + ("_z" if zero else ""))] * steps
     if one and flip and steps >= 2:   # steps 1 .. K-1 (the state is unchanged since the last call / init)
         z = "_z" if zero else ""
         out = [("onepass", "onepass" + z)] * (steps - 1)
@@ -109,23 +111,40 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
     return out
 
 
-def fused_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False,
-                one: bool = False, tracers: int = 0, zero: bool = False):
-    """Mean bytes per interior cell per launch of each timer over one ocn_ctx_step call."""
+# the tail of an open one-pass sequence, formed by ocn_ctx_complete: the last step run again as the
+# call's last step (+ vort, the stresses, the RHS terms), a8's copies, hh_init with every level
+TAIL_LAUNCHES = [("onepass", "onepass_last"), ("copy", "copy3"), ("hh_init", "c2_full")]
+
+
+def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
+                    tracers: int = 0, zero: bool = False, lazy: bool = False):
+    """The launches of a timed region: ocn_ctx_step calls of calls[i] steps each, then (lazy) the
+    pending tail formed by ocn_ctx_complete."""
+    out = []
+    for n in calls:
+        out += call_launches(n, flip, rc, ring, one, tracers, zero=zero, lazy=lazy)
+    if lazy and one:
+        out += [(t, k + ("_z" if zero and t == "onepass" else "")) for t, k in TAIL_LAUNCHES]
+    return out
+
+
+def fused_bytes(compact: bool, calls, flip: bool = False, rc: bool = True, ring: bool = False,
+                one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False):
+    """Mean bytes per interior cell per launch of each timer over the timed region's calls."""
     i = 0 if compact else 1
     tot, cnt = {}, {}
-    for timer, kind in call_launches(steps, flip, rc, ring, one, tracers, zero=zero):
+    for timer, kind in region_launches(calls, flip, rc, ring, one, tracers, zero, lazy):
         tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
         cnt[timer] = cnt.get(timer, 0) + (kind != "hqp")   # "hqp": bytes of the launch before it
     return {t: tot[t] / cnt[t] for t in tot}
 
 
-def step_bytes(compact: bool, steps: int, flip: bool = False, rc: bool = True, ring: bool = False,
-               one: bool = False, tracers: int = 0, zero: bool = False):
-    """Bytes per interior cell per step moved by one ocn_ctx_step call of `steps` steps."""
+def step_bytes(compact: bool, calls, flip: bool = False, rc: bool = True, ring: bool = False,
+               one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False):
+    """Bytes per interior cell per step moved by the timed region's calls."""
     i = 0 if compact else 1
-    return sum(LAUNCH_BYTES[kind][i] for _, kind in call_launches(steps, flip, rc, ring, one, tracers,
-                                                                   zero=zero)) / steps
+    return sum(LAUNCH_BYTES[kind][i] for _, kind in region_launches(calls, flip, rc, ring, one, tracers, zero,
+                                                                    lazy)) / sum(calls)
 
 
 def dims_create(n: int):
@@ -242,8 +261,13 @@ def launch_ranks(n: int) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100, help="timed steps (SURVEY.md 8d: >= 100)")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed warm-up steps (SURVEY.md 8d: 10)")
+    ap.add_argument("--steps-per-call", type=int, default=0,
+                    help="steps per ocn_ctx_step call in the timed region (1 = the reference's cadence, one "
+                         "expl_shallow_water per time-loop iteration, model.f90:146); 0 = all in one call")
+    ap.add_argument("--no-lazy-tail", action="store_true",
+                    help="every call forms its own tail (OCN_OPT_LAZY_TAIL off)")
     ap.add_argument("--n", type=int, default=4096, help="box interior size (N x N)")
     ap.add_argument("--basin", choices=["box", "bs", "bs_tr"], default="box",
                     help="box: the synthetic N x N box; bs / bs_tr: the reference's Black Sea basin (data/BS mask "
@@ -322,6 +346,7 @@ def main():
     model.set_onepass(not args.no_onepass)
     model.set_known_constants(not args.no_known_constants)
     model.set_overlap(args.overlap)
+    model.set_lazy_tail(not args.no_lazy_tail)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -334,12 +359,21 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    spc = args.steps_per_call if args.steps_per_call > 0 else args.steps
+    calls = [min(spc, args.steps - i) for i in range(0, args.steps, spc)]
     barrier()
+    n_launch0 = amd._lib.launch_count()
     t0 = time.perf_counter()
-    model.step(args.steps, check_every=1)
+    for n_call in calls:
+        model.step(n_call, check_every=1)
+    lazy = model.tail_pending
+    # the timed region ends with every array as the reference leaves it after the last step: a
+    # pending call tail (OCN_OPT_LAZY_TAIL) is formed inside it
+    model.complete()
     model.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    launches = amd._lib.launch_count() - n_launch0
     times = model.stage_times()
     compact = model.compact_active
     flip = model.flip_active
@@ -359,8 +393,8 @@ def main():
     if rank == 0:
         ring = bx * by > 1
         ntr = sw.tracer_num if sw.use_tracers > 0 else 0
-        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, args.steps, flip, rc, ring, one, ntr, one_zero)
-        b_path = B_ALG if args.stages else step_bytes(compact, args.steps, flip, rc, ring, one, ntr, one_zero)
+        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, calls, flip, rc, ring, one, ntr, one_zero, lazy)
+        b_path = B_ALG if args.stages else step_bytes(compact, calls, flip, rc, ring, one, ntr, one_zero, lazy)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:   # the dominant kernel: the most device time over the timed steps
@@ -387,16 +421,23 @@ def main():
                           "march": bool(compact and not args.stages and not args.no_march),
                           "role_flip_steps": flip, "recompute_steps": rc, "onepass_steps": one,
                           "onepass_known_constants": one_zero,
+                          "steps_per_call": spc, "calls": len(calls),
+                          "call_tail": ("pending between calls (OCN_OPT_LAZY_TAIL), formed once by ocn_ctx_complete "
+                                        "inside the timed region") if lazy else "formed by every call",
+                          "kernel_launches_per_step": round(launches / args.steps, 2),
                           "overlap": model_overlap,
                           "parallelism": (f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else
                                           "1 block" if bx * by == 1 else f"{bx}x{by} blocks, local halo copies")},
                "build_id": amd.build_id(),
                "roofline": roof,
-               "step_hbm_frac": round(step_gbs / HBM_PEAK_GBS, 4),
-               "step_alg_gbs_per_gpu": round(step_gbs, 1),
-               "step_bytes_per_cell": {"reference_stages_B_alg": B_ALG,
-                                       "this_path": round(b_path, 1)},
-               "step_moved_frac": round(moved / HBM_PEAK_GBS, 4),
+               # whole-step rates (not the roofline, which is `roofline`: the dominant kernel's bytes
+               # over its own time): the bytes this path moves per step, and -- for comparison with
+               # SURVEY.md 8d only -- the reference's 11-stage B_alg at this step rate
+               "step_moved": {"bytes_per_cell": round(b_path, 1), "GBps_per_gpu": round(moved, 1),
+                              "frac_of_peak": round(moved / HBM_PEAK_GBS, 4)},
+               "reference_B_alg_equivalent": {"bytes_per_cell": B_ALG, "GBps_per_gpu": round(step_gbs, 1),
+                                              "note": "bytes the reference's 11 stages would move at this step "
+                                                      "rate; not moved by this path, not a roofline fraction"},
                "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()}}
         if world > 1:
             out["multi_gpu_parity_512"] = parity

@@ -43,6 +43,11 @@ module ocn_psy
     integer, public :: bcount = 0
     type(ocn_block), allocatable, public :: blk(:)
     type(ocn_sw_params), public :: sw_params
+    ! psy_fused (default): expl_shallow_water is one ocn_ctx_step(ctx, tau, 1) -- the library's fused
+    ! step, expl_tracer included (model.f90:146-160), which continues a one-pass sequence across
+    ! calls (OCN_OPT_LAZY_TAIL); .false.: the reference's 11 envoke stages through the kernel-layer
+    ! entries (per-stage hooks, e.g. to inspect a stage's output).  Same results bit for bit.
+    logical, public :: psy_fused = .true.
 
     public :: psy_init, envoke, expl_shallow_water, expl_tracer, fld
 
@@ -279,6 +284,7 @@ contains
         type(kernel_parameters_type) :: p
         integer :: k
         if (sw_params%use_tracers <= 0) return
+        if (psy_fused) return   ! ran inside expl_shallow_water's ocn_ctx_step
         do k = 1, sw_params%tracer_num
             call p%clear()
             p%tau = tau
@@ -294,6 +300,10 @@ contains
     subroutine expl_shallow_water(tau)
         real(c_double), intent(in) :: tau
         type(kernel_parameters_type) :: p
+        if (psy_fused) then
+            call ocn_check(ocn_ctx_step(ctx, tau, 1_c_int32_t, 1_c_int32_t), 'ocn_ctx_step')
+            return
+        endif
         call p%clear()
         p%tau = tau
         p%time_smooth = sw_params%time_smooth

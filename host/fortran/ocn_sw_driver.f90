@@ -2,11 +2,13 @@
 ! shallow-water step running on the MI355X through libocn_sw.
 !
 ! usage (in a directory holding basin.par, sw.par, parallel.par):
-!     ocn_sw_driver NSTEPS DUMPFILE [native]
+!     ocn_sw_driver NSTEPS DUMPFILE [native|stages]
 ! Reads the positional .par files (first lexeme per line, readpar semantics), builds the model
 ! (decomposition + init_grid_data + init_ocean_data on the device), runs NSTEPS of
-! expl_shallow_water + expl_tracer through the Fortran PSy layer (or, with "native", ocn_ctx_step), and
-! writes every field of every block in the oracle/ref_driver.f90 dump format.
+! expl_shallow_water + expl_tracer through the Fortran PSy layer -- by default its fused form (one
+! ocn_ctx_step per time step), with "stages" the reference's envoke stages, with "native" one
+! ocn_ctx_step call of NSTEPS -- and writes every field of every block in the oracle/ref_driver.f90
+! dump format.
 program ocn_sw_driver
     use iso_c_binding
     use ocn_sw_c
@@ -30,6 +32,7 @@ program ocn_sw_driver
     call get_command_argument(1, arg); read(arg, *) nsteps
     call get_command_argument(2, dumpfile)
     call get_command_argument(3, arg); native = (trim(arg) == 'native')
+    if (trim(arg) == 'stages') psy_fused = .false.
 
     ! basin.par (configs/basinpar.f90:53-77)
     call read_par('basin.par', lines, nlo)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define OCN_ABI_VERSION 3
+#define OCN_ABI_VERSION 4
 
 enum {
     OCN_OK = 0,
@@ -279,6 +279,11 @@ int ocn_ctx_tracer_stage(ocn_ctx *ctx, int stage_id, int tracer, double tau);
 int ocn_ctx_step(ocn_ctx *ctx, double tau, int32_t nsteps, int32_t check_every);
 /* Wait for the context's stream; returns OCN_ERR_BLOWUP if a check found |ssh| >= 1e4. */
 int ocn_ctx_synchronize(ocn_ctx *ctx);
+/* Form a pending call tail now (OCN_OPT_LAZY_TAIL): afterwards every array holds what the
+ * reference leaves after the last step run.  Every entry that reads or writes fields, hands out a
+ * pointer, runs a stage or a sync, or sets an option does this first; a host that reads device
+ * memory by other means calls it itself.  Asynchronous on the context stream. */
+int ocn_ctx_complete(ocn_ctx *ctx);
 
 /* Host <-> device copies of a whole field of local block k (host array: Fortran order,
  * leading dim bnd_x2-bnd_x1+1, 4 or 8 bytes per element by field kind). Synchronous. */
@@ -334,6 +339,14 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_ONEPASS_LAST (default 1): with halo exchanges or a8 / a9 work on the halo ring, the
  *  call's last step as a one-pass step too (the inner march storing what the reference's last
  *  step leaves, then a8's copies and hh_init with every level); 0: a standard last step there.
+ *  OCN_OPT_LAZY_TAIL (default 1): in one process, one block without halo exchanges, no tracers and
+ *  no raw real(8) pointer handed out, a call whose steps are one-pass steps leaves its tail (what
+ *  the reference's last step stores beyond the next state: vort, the stresses, the RHS terms,
+ *  sw_next_step's copies, hh_init with every level) pending: the next ocn_ctx_step continues with
+ *  one-pass steps -- so 1-step calls (the reference's own cadence, model.f90:146) run as fast as
+ *  long ones -- and ocn_ctx_complete, or any entry that looks at the fields, forms it first (the
+ *  last step run again from the previous state, which is still in the library's second buffers:
+ *  the same results bit for bit).  ocn_ctx_get_option returns 2 while a tail is pending.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
  * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
@@ -343,7 +356,7 @@ int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9,
-       OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11 };
+       OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,
@@ -360,6 +373,9 @@ int ocn_abi_version(void);
 /* Build id: a hash of the library's sources and compile flags (Makefile), e.g. to tie a
  * profile taken on one build to the library that is loaded. */
 const char *ocn_build_id(void);
+/* Kernel launches this process has issued through the library so far (every context, copies
+ * between buffers not included): a host takes differences around a region to count launches. */
+int64_t ocn_launch_count(void);
 
 #ifdef __cplusplus
 }

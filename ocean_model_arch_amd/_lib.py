@@ -78,6 +78,7 @@ OPT_RECOMPUTE = 8
 OPT_ONEPASS = 9
 OPT_KNOWN_CONSTANTS = 10
 OPT_ONEPASS_LAST = 11
+OPT_LAZY_TAIL = 12
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",
@@ -87,8 +88,8 @@ KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "oc
 CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
                "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm", "ocn_ctx_attach_loopback",
                "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
-               "ocn_ctx_download", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version",
-               "ocn_build_id"]
+               "ocn_ctx_download", "ocn_ctx_complete", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version",
+               "ocn_build_id", "ocn_launch_count"]
 ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
 
 
@@ -172,13 +173,15 @@ def lib() -> C.CDLL:
         getattr(L, name)
     L.ocn_last_error.restype = C.c_char_p
     L.ocn_build_id.restype = C.c_char_p
+    L.ocn_launch_count.restype = C.c_int64
     L.ocn_ctx_field.restype = C.c_void_p
     L.ocn_ctx_field.argtypes = [C.c_void_p, C.c_int, C.c_int]
     L.ocn_ctx_stream.restype = C.c_void_p
     L.ocn_ctx_stream.argtypes = [C.c_void_p]
     L.ocn_ctx_create.argtypes = [C.POINTER(OcnBasin), C.POINTER(OcnSwParams), C.POINTER(OcnDecomp), C.c_void_p,
                                  C.POINTER(C.c_void_p)]
-    for nm in ("ocn_ctx_destroy", "ocn_ctx_init_state", "ocn_ctx_synchronize", "ocn_ctx_block_count"):
+    for nm in ("ocn_ctx_destroy", "ocn_ctx_init_state", "ocn_ctx_synchronize", "ocn_ctx_block_count",
+               "ocn_ctx_complete"):
         getattr(L, nm).argtypes = [C.c_void_p]
     L.ocn_ctx_block_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(OcnBlockInfo)]
     L.ocn_ctx_sync.argtypes = [C.c_void_p, C.c_int]
@@ -205,6 +208,11 @@ def lib() -> C.CDLL:
 def build_id() -> str:
     """ocn_build_id(): hash of the loaded library's sources and compile flags."""
     return lib().ocn_build_id().decode()
+
+
+def launch_count() -> int:
+    """ocn_launch_count(): kernel launches issued through the library by this process so far."""
+    return int(lib().ocn_launch_count())
 
 
 def check(rc: int, what: str = ""):

@@ -18,6 +18,30 @@
 
 namespace ocn {
 
+// grid_base_init + grid_geo_init at one point of the metric range (grid_kernels.f90:94-202,
+// grid_parameters.f90:80-181): the four passes (t, u, v, b points) each scale their own pair of
+// metrics, the b pass the Coriolis term.  ct / cv: (float) dcosd(lat_mod) of the row's yt / yv;
+// sin_v, cosy_v: dsind / dcosd of its yv; cos_xu: dcosd of the column's xu.  out: OCN_DX .. OCN_R_DISS.
+__device__ __forceinline__ void grid_metrics(const GridInit &q, float ct, float cv, double sin_v, double cosy_v,
+                                             double cos_xu, float *out)
+{
+    if (!q.curve) ct = cv = 1.0f;
+    out[OCN_DX - OCN_DX] = q.sx * ct; out[OCN_DY - OCN_DX] = q.sy * 1.0f;    // t points (xt, yt)
+    out[OCN_DXT - OCN_DX] = q.sx * ct; out[OCN_DYH - OCN_DX] = q.sy * 1.0f;  // u points (xu, yt)
+    out[OCN_DXH - OCN_DX] = q.sx * cv; out[OCN_DYT - OCN_DX] = q.sy * 1.0f;  // v points (xt, yv)
+    out[OCN_DXB - OCN_DX] = q.sx * cv; out[OCN_DYB - OCN_DX] = q.sy * 1.0f;  // b points (xu, yv)
+    float rlh = q.cor;
+    if (q.curve) {
+        double s = sin_v * q.cos_rot + cos_xu * cosy_v * q.sin_rot;
+        s = fmin(fmax(s, -q.sin_extr), q.sin_extr);
+        rlh = rlh * (float)s;
+    } else {
+        rlh = rlh / q.sqrt2;
+    }
+    out[OCN_RLH_S - OCN_DX] = rlh;
+    out[OCN_R_DISS - OCN_DX] = 0.0f;
+}
+
 __global__ __launch_bounds__(256) void k_init_grid(GridInit q)
 {
     const ocn_block &g = q.g;
@@ -44,27 +68,27 @@ __global__ __launch_bounds__(256) void k_init_grid(GridInit q)
     q.r4[OCN_LLV][at] = llv; q.r4[OCN_LCU][at] = lcu; q.r4[OCN_LCV][at] = lcv;
     // grid_base_init + grid_geo_init on [nx_start-1, nx_end+1] x [ny_start-1, ny_end+1]; the four
     // passes (t, u, v, b points) each scale their own pair of metrics, the b pass the Coriolis term
-    float dx = 0.0f, dy = 0.0f, dxt = 0.0f, dyt = 0.0f, dxh = 0.0f, dyh = 0.0f, dxb = 0.0f, dyb = 0.0f;
-    float rlh = q.cor;
+    // grid_base_init + grid_geo_init on [nx_start-1, nx_end+1] x [ny_start-1, ny_end+1] (zero
+    // elsewhere, the Coriolis term 2 * EarthAngVel)
+    float v[OCN_NUM_R4 - OCN_DX] = {0.0f};
+    v[OCN_RLH_S - OCN_DX] = q.cor;
     if (m >= g.nx_start - 1 && m <= g.nx_end + 1 && n >= g.ny_start - 1 && n <= g.ny_end + 1) {
         const int r = n - g.bnd_y1;
-        const float ct = q.curve ? q.cos_t[r] : 1.0f, cv = q.curve ? q.cos_v[r] : 1.0f;   // (float) dcosd(lat_mod)
-        dx = q.sx * ct; dy = q.sy * 1.0f;      // t points (xt, yt)
-        dxt = q.sx * ct; dyh = q.sy * 1.0f;    // u points (xu, yt)
-        dxh = q.sx * cv; dyt = q.sy * 1.0f;    // v points (xt, yv)
-        dxb = q.sx * cv; dyb = q.sy * 1.0f;    // b points (xu, yv)
-        if (q.curve) {
-            double s = q.sin_v[r] * q.cos_rot + q.cos_xu[m - g.bnd_x1] * q.cosy_v[r] * q.sin_rot;
-            s = fmin(fmax(s, -q.sin_extr), q.sin_extr);
-            rlh = rlh * (float)s;
-        } else {
-            rlh = rlh / q.sqrt2;
-        }
+        grid_metrics(q, q.cos_t[r], q.cos_v[r], q.sin_v[r], q.cosy_v[r], q.cos_xu[m - g.bnd_x1], v);
     }
-    q.r4[OCN_DX][at] = dx; q.r4[OCN_DY][at] = dy; q.r4[OCN_DXT][at] = dxt; q.r4[OCN_DYT][at] = dyt;
-    q.r4[OCN_DXH][at] = dxh; q.r4[OCN_DYH][at] = dyh; q.r4[OCN_DXB][at] = dxb; q.r4[OCN_DYB][at] = dyb;
-    q.r4[OCN_RLH_S][at] = rlh;
-    q.r4[OCN_R_DISS][at] = 0.0f;
+    for (int id = OCN_DX; id < OCN_NUM_R4; ++id) q.r4[id][at] = v[id - OCN_DX];
+}
+
+// The metric values of the rows just outside the block's metric range (bnd_y1 and bnd_y2, where
+// the reference leaves 0) as the neighbour block above / below forms them on its interior -- the
+// same global row, the same arithmetic: the one-pass step forms its halo points' depths and
+// stresses there (ocn_ctx.hip one_step_x2).  Column nx_start - 1 (the compact row tables' column).
+__global__ void k_ext_rows(GridInit q)
+{
+    const int i = (int)threadIdx.x;
+    if (i >= 2) return;
+    grid_metrics(q, q.ext_ct[i], q.ext_cv[i], q.ext_sin_v[i], q.ext_cosy_v[i], q.cos_xu[q.g.nx_start - 1 - q.g.bnd_x1],
+                 q.ext + i * (OCN_NUM_R4 - OCN_DX));
 }
 
 // gaussian_elimination_kernel (vel_ssh.f90:15-38): on the interior where lu > 0.5, centre
@@ -103,6 +127,9 @@ static unsigned grid_of(const ocn_block &g)
 int launch_init_grid(const GridInit &q, hipStream_t s)
 {
     hipLaunchKernelGGL(k_init_grid, dim3(grid_of(q.g)), dim3(256), 0, s, q);
+    int rc = check_launch();
+    if (rc || !q.ext) return rc;
+    hipLaunchKernelGGL(k_ext_rows, dim3(1), dim3(64), 0, s, q);
     return check_launch();
 }
 

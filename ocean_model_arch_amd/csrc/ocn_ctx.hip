@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -35,6 +36,9 @@ int set_error(int code, const std::string &msg)
     g_last_error = msg;
     return code;
 }
+
+static std::atomic<long long> g_launches{0};
+void count_launch() { g_launches.fetch_add(1, std::memory_order_relaxed); }
 
 int check_hip(hipError_t e, const char *what)
 {
@@ -111,37 +115,6 @@ __global__ void k_output_r4(const T *src, const float *lu, long pitch, int w, in
 // ------------------------------------------------------------------ geometry helpers
 // decomposition.f90:94-290, directions macros/kernel_macros.fi:4-12
 struct Rect { int x0, x1, y0, y1; };
-static Rect boundary_points(const ocn_block &b, int dir)
-{
-    switch (dir) {
-    case 1: return {b.nx_end, b.nx_end, b.ny_start, b.ny_end};
-    case 2: return {b.nx_start, b.nx_start, b.ny_start, b.ny_end};
-    case 3: return {b.nx_start, b.nx_end, b.ny_end, b.ny_end};
-    case 4: return {b.nx_start, b.nx_end, b.ny_start, b.ny_start};
-    case 5: return {b.nx_end, b.nx_end, b.ny_end, b.ny_end};
-    case 6: return {b.nx_end, b.nx_end, b.ny_start, b.ny_start};
-    case 7: return {b.nx_start, b.nx_start, b.ny_end, b.ny_end};
-    default: return {b.nx_start, b.nx_start, b.ny_start, b.ny_start};
-    }
-}
-static Rect halo_points(const ocn_block &b, int dir)
-{
-    switch (dir) {
-    case 1: return {b.nx_end + 1, b.nx_end + 1, b.ny_start, b.ny_end};
-    case 2: return {b.nx_start - 1, b.nx_start - 1, b.ny_start, b.ny_end};
-    case 3: return {b.nx_start, b.nx_end, b.ny_end + 1, b.ny_end + 1};
-    case 4: return {b.nx_start, b.nx_end, b.ny_start - 1, b.ny_start - 1};
-    case 5: return {b.nx_end + 1, b.nx_end + 1, b.ny_end + 1, b.ny_end + 1};
-    case 6: return {b.nx_end + 1, b.nx_end + 1, b.ny_start - 1, b.ny_start - 1};
-    case 7: return {b.nx_start - 1, b.nx_start - 1, b.ny_end + 1, b.ny_end + 1};
-    default: return {b.nx_start - 1, b.nx_start - 1, b.ny_start - 1, b.ny_start - 1};
-    }
-}
-static int inverse_dir(int d)
-{
-    static const int inv[9] = {0, 2, 1, 4, 3, 8, 7, 6, 5};
-    return inv[d];
-}
 static const int kDirDm[9] = {0, 1, -1, 0, 0, 1, 1, -1, -1};
 static const int kDirDn[9] = {0, 0, 0, 1, -1, 1, -1, 1, -1};
 
@@ -177,7 +150,7 @@ struct LBlock {
     float *rows = nullptr;             // and metric row tables
     void *sshp_alt = nullptr;          // second sshp buffer of the recompute steps (one_step_fused)
     void *up_alt = nullptr, *vp_alt = nullptr;   // second ubrtrp / vbrtrp buffers of the one-pass steps
-    double hr0 = 0.0, mu0 = 0.0;       // h_r, mu where the one-pass step reads them (ctx fb_zero)
+    double *kc = nullptr;              // device: h_r, mu of the one-pass step's known-constant variant
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
@@ -241,6 +214,9 @@ struct StepKind {
 
 }  // namespace ocn
 
+// ocn_ctx::fb_state
+enum { kFbUnchecked = 0, kFbDevice = 1, kFbZero = 2, kFbGeneral = 3 };
+
 #ifndef OCN_COMM_PRIO
 #define OCN_COMM_PRIO 1   // the comm stream at the device's highest stream priority
 #endif
@@ -265,7 +241,7 @@ struct ocn_ctx {
     bool use_graph = false;
     // the launches a captured step replays depend on everything in its key (march and ring_sea
     // select launch forms and the ring launch; options that change them also drop the cache)
-    struct Graph { hipGraphExec_t exec; double tau; ocn::StepKind kind; bool compact, march, ring_sea; int role; };
+    struct Graph { hipGraphExec_t exec; double tau; ocn::StepKind kind; bool compact, march, ring_sea; int role, kc_mode; };
     std::vector<Graph> graphs;         // one captured step per key
     std::vector<void *> allocs;
     // per-stage HIP-event timing (OCN_OPT_STAGE_TIMING): pending (stage, start, stop) records
@@ -305,11 +281,24 @@ struct ocn_ctx {
     // call may then be a one-pass step too, as a reuse step.  Never again once an r8 field's
     // device pointer was handed out (it may be written behind our back).
     mutable bool hh_consistent = false, r8_handed = false;
-    // the one-pass step's fallback points hold +0.0 (sw_kernels.hip FallbackCheck; rechecked after
-    // anything may have written the depth / vort / stress arrays from outside the step)
-    mutable bool fb_zero = false, fb_zero_known = false;
+    // the one-pass step's known-constant precondition (sw_kernels.hip FallbackCheck: fallback points
+    // and forcing +0.0, h_r and mu uniform): kFbUnchecked until a check ran after the arrays last
+    // changed from outside the step; kFbDevice = its verdict is in device memory (d_fbz; both
+    // variants are launched and the device picks, ocn_ctx.hip never waits for it) until a host
+    // sync the caller makes anyway reads it (learn_fb): kFbZero / kFbGeneral
+    mutable int fb_state = 0;
+    int kc_mode = 0;             // OCN_KC_* of the current call's one-pass launches
+    int32_t *d_fbz = nullptr;    // the check's verdict word
+    // lazy call tail (OCN_OPT_LAZY_TAIL): the last step run was a one-pass step; what the reference's
+    // last step leaves beyond the state (vort, stresses, RHS terms, hh_init's levels, a8's copies) is
+    // formed when the host next looks (complete_open: the step redone from the previous state, still
+    // intact in the other buffers, as the call's last step), so 1-step calls run one-pass steps
+    bool lazy = true, open = false;
+    double open_tau = 0.0;
     mutable bool coherent_known = false, r8_escaped = false;
     int role = 0;
+    int steps_run = 0;           // launches statistics of the last call (ocn_ctx_get_option OCN_OPT_LAUNCHES)
+    int64_t launches = 0;
     int32_t *d_flags = nullptr;
 };
 
@@ -442,9 +431,10 @@ static int allocate(ocn_ctx *c)
         char *base = (char *)b.slab;
         size_t off = 0;
         b.ptr.assign((size_t)(OCN_NUM_R4 + nr8), nullptr);
-        // r8 order in the slab: first the one-pass step's fields and the second buffers, so that
-        // its kernel reaches all of them by 32-bit offsets from one base (sw_kernels.hip
-        // MarchStep), then the other SW fields, then the tracers'
+        // r8 order in the slab: the one-pass step's state fields and their second buffers first,
+        // next to each other (the arrays one march streams through share DRAM pages and TLB
+        // entries), then the other SW fields, then the tracers'.  (Kernels address every field
+        // through its own pointer; only byte offsets within one field are 32-bit.)
         std::vector<int> order = {OCN_SSH, OCN_SSHN, OCN_SSHP, OCN_UBRTR, OCN_UBRTRN, OCN_UBRTRP, OCN_VBRTR,
                                   OCN_VBRTRN, OCN_VBRTRP, -1, -2, -3, OCN_HHU, OCN_HHU_P, OCN_HHV, OCN_HHV_P, OCN_HHH,
                                   OCN_HHQ_REST, OCN_VORT, OCN_STR_T, OCN_STR_S, OCN_MU, OCN_RHSX, OCN_RHSY};
@@ -472,10 +462,15 @@ static int allocate(ocn_ctx *c)
         HIPCHK(hipMalloc(&b.rows, nrow * sizeof(float)));
         c->allocs.push_back(b.rows);
     }
-    HIPCHK(hipMalloc(&c->d_nbad, 256));
+    // d_nbad words: 0 check_ssh_err's count, 16 the fallback check's verdict (d_fbz), 32..47 flags and
+    // the vote (d_flags), 48..63 the loopback vote's reduction; then per block h_r, mu (LBlock::kc)
+    const size_t kcb = 16 * c->blocks.size();
+    HIPCHK(hipMalloc(&c->d_nbad, 256 + kcb));
     c->allocs.push_back(c->d_nbad);
-    HIPCHK(hipMemsetAsync(c->d_nbad, 0, 256, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_nbad, 0, 256 + kcb, c->stream));
+    c->d_fbz = c->d_nbad + 16;
     c->d_flags = c->d_nbad + 32;
+    for (size_t i = 0; i < c->blocks.size(); ++i) c->blocks[i].kc = (double *)((char *)c->d_nbad + 256) + 2 * i;
     return OCN_OK;
 }
 
@@ -498,13 +493,38 @@ struct PlanEntry {
     int count;
 };
 
-static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::vector<PlanEntry> &out)
+// Layer j (1 .. depth) of the halo of block `rcv` in direction d and the boundary of its
+// neighbour `src` it receives: layer 1 is the reference's 1-wide exchange (syncborder_block2D_gen_all.fi);
+// layer 2 (depth 2, the one-pass steps' state exchange, one_step_x2) the next row / column out
+// (and depth x depth corner patches).  Corner layers are rows of `depth` points.
+static void halo_layer(const ocn_block &rcv, const ocn_block &src, int d, int j, int depth, Rect &hr, Rect &br)
+{
+    const int dm = kDirDm[d], dn = kDirDn[d];
+    // x: halo columns / source columns of this direction
+    int hx0, hx1, sx0, sx1;
+    if (dm > 0) { hx0 = rcv.nx_end + 1; hx1 = rcv.nx_end + (dn ? depth : 1); sx0 = src.nx_start; sx1 = sx0 + (hx1 - hx0); }
+    else if (dm < 0) { hx1 = rcv.nx_start - 1; hx0 = rcv.nx_start - (dn ? depth : 1); sx1 = src.nx_end; sx0 = sx1 - (hx1 - hx0); }
+    else { hx0 = rcv.nx_start; hx1 = rcv.nx_end; sx0 = src.nx_start; sx1 = src.nx_end; }
+    if (dm && !dn) {   // E / W edge: layer j is one column
+        hx0 = hx1 = dm > 0 ? rcv.nx_end + j : rcv.nx_start - j;
+        sx0 = sx1 = dm > 0 ? src.nx_start + j - 1 : src.nx_end - j + 1;
+    }
+    int hy, sy;
+    if (dn > 0) { hy = rcv.ny_end + j; sy = src.ny_start + j - 1; }
+    else if (dn < 0) { hy = rcv.ny_start - j; sy = src.ny_end - j + 1; }
+    else { hy = -1; sy = -1; }
+    if (dn) { hr = {hx0, hx1, hy, hy}; br = {sx0, sx1, sy, sy}; }
+    else { hr = {hx0, hx1, rcv.ny_start, rcv.ny_end}; br = {sx0, sx1, src.ny_start, src.ny_end}; }
+}
+
+static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::vector<PlanEntry> &out,
+                        int depth = 1)
 {
     out.clear();
     std::map<int, int> k_of_gid;
     for (size_t k = 0; k < c->blocks.size(); ++k) k_of_gid[c->blocks[k].gid] = (int)k;
     std::map<int, long> send_count, recv_count;
-    // receiving side: my halos in gid order, dirs 1..8
+    // receiving side: my halos in gid order, dirs 1..8, layers 1..depth
     for (auto &kv : k_of_gid) {
         const int k = kv.second;
         const LBlock &b = c->blocks[k];
@@ -512,20 +532,22 @@ static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::v
             const int r = b.nbr_rank[d - 1];
             if (r < 0) continue;
             const GBlock &src = c->gblocks[b.nbr_gid[d - 1]];
-            const Rect hr = halo_points(b.g, d);
-            const Rect br = boundary_points(src.g, inverse_dir(d));
-            const int cnt = (hr.x1 - hr.x0 + 1) * (hr.y1 - hr.y0 + 1);
-            for (int id : fields) {
-                if (r == c->dec.rank)
-                    out.push_back(PlanEntry{OCN_HALO_LOCAL, r, k, k_of_gid.at(b.nbr_gid[d - 1]), id, hr, br, 0, cnt});
-                else {
-                    out.push_back(PlanEntry{OCN_HALO_RECV, r, k, -1, id, hr, br, recv_count[r], cnt});
-                    recv_count[r] += cnt;
+            for (int j = 1; j <= depth; ++j) {
+                Rect hr, br;
+                halo_layer(b.g, src.g, d, j, depth, hr, br);
+                const int cnt = (hr.x1 - hr.x0 + 1) * (hr.y1 - hr.y0 + 1);
+                for (int id : fields) {
+                    if (r == c->dec.rank)
+                        out.push_back(PlanEntry{OCN_HALO_LOCAL, r, k, k_of_gid.at(b.nbr_gid[d - 1]), id, hr, br, 0, cnt});
+                    else {
+                        out.push_back(PlanEntry{OCN_HALO_RECV, r, k, -1, id, hr, br, recv_count[r], cnt});
+                        recv_count[r] += cnt;
+                    }
                 }
             }
         }
     }
-    // sending side: remote receivers in gid order, dirs 1..8, whose source block is mine
+    // sending side: remote receivers in gid order, dirs 1..8, layers 1..depth, whose source block is mine
     for (size_t gid = 0; gid < c->gblocks.size(); ++gid) {
         const GBlock &rb = c->gblocks[gid];
         if (rb.rank < 0 || rb.rank == c->dec.rank) continue;
@@ -535,12 +557,14 @@ static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::v
             const int sg = (m - 1) + (n - 1) * c->bnx;
             if (c->gblocks[sg].rank != c->dec.rank) continue;
             const int ks = k_of_gid.at(sg);
-            const Rect br = boundary_points(c->blocks[ks].g, inverse_dir(d));
-            const Rect hr = halo_points(rb.g, d);
-            const int cnt = (br.x1 - br.x0 + 1) * (br.y1 - br.y0 + 1);
-            for (int id : fields) {
-                out.push_back(PlanEntry{OCN_HALO_SEND, rb.rank, -1, ks, id, hr, br, send_count[rb.rank], cnt});
-                send_count[rb.rank] += cnt;
+            for (int j = 1; j <= depth; ++j) {
+                Rect hr, br;
+                halo_layer(rb.g, c->blocks[ks].g, d, j, depth, hr, br);
+                const int cnt = (br.x1 - br.x0 + 1) * (br.y1 - br.y0 + 1);
+                for (int id : fields) {
+                    out.push_back(PlanEntry{OCN_HALO_SEND, rb.rank, -1, ks, id, hr, br, send_count[rb.rank], cnt});
+                    send_count[rb.rank] += cnt;
+                }
             }
         }
     }
@@ -551,10 +575,10 @@ static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::v
     return OCN_OK;
 }
 
-static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan)
+static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan, int depth = 1)
 {
     std::vector<PlanEntry> entries;
-    RC(plan_entries(c, fields, entries));
+    RC(plan_entries(c, fields, entries, depth));
     std::map<int, long> msg;                       // peer -> message length
     for (const PlanEntry &e : entries)
         if (e.kind == OCN_HALO_RECV) msg[e.peer] = std::max(msg[e.peer], e.buf_off + e.count);
@@ -604,18 +628,21 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
 // Plans hold raw field pointers, so a plan is kept per role of the buffers its fields swap
 // between (the key is the field list followed by -1 - the relevant role bits).
 static bool is_alt_field(int id);
-static int get_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan *&out)
+// depth 2: the one-pass steps' 2-deep state exchange (halo_layer); priv: a plan over a private
+// buffer swapped into the field table while it is built and run (one_step_x2's h_r copy)
+static int get_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan *&out, int depth = 1, int priv = 0)
 {
     std::vector<int> key = fields;
     // a plan holds the buffers its fields had when it was built: the pair roles (bit 1), and for
-    // sshp / ubrtrp / vbrtrp (a user's ocn_ctx_sync; no step's sync list holds them) the second
-    // buffers' roles (bit 4: they persist between one-pass calls)
+    // sshp / ubrtrp / vbrtrp the second buffers' roles (bit 4: they persist between one-pass calls)
     const bool alt = std::any_of(fields.begin(), fields.end(), [](int id) { return is_alt_field(id); });
     key.push_back(-1 - (c->role & 1) - (alt ? (c->role & 4) : 0));
+    if (depth != 1 || priv) key.push_back(-100 - depth - 10 * priv);
     auto it = c->plans.find(key);
     if (it == c->plans.end()) {
+        if (c->capturing) return set_error(OCN_ERR_STATE, "halo plan built while a step is captured");
         HaloPlan p;
-        RC(build_plan(c, fields, p));
+        RC(build_plan(c, fields, p, depth));
         it = c->plans.emplace(key, p).first;
     }
     out = &it->second;
@@ -690,39 +717,52 @@ static int lb_exchange(ocn_ctx *c, const HaloPlan *p, hipStream_t stream)
     }
     RC(lb_meet(c, 0, peers));
     for (const auto &q : p->peers) {
-        const ocn_ctx *pc = L.ctx[q.rank];
         const HaloPlan *pp;
-        {
+        hipEvent_t ev;
+        {   // a peer destroyed after the rendezvous has left its slot empty: fail, do not dereference
             std::lock_guard<std::mutex> g(L.mu);
+            if (!L.ctx[q.rank]) return set_error(OCN_ERR_COMM, "loopback transport: a peer rank was destroyed");
             pp = L.plan[q.rank];
+            ev = L.ctx[q.rank]->lb_ev_a;
         }
         const HaloPlan::Peer *src = nullptr;
         for (const auto &e : pp->peers)
             if (e.rank == r) src = &e;
         if (!src || src->count != q.count) return set_error(OCN_ERR_STATE, "loopback transport: message sizes disagree");
-        HIPCHK(hipStreamWaitEvent(stream, pc->lb_ev_a, 0));
+        HIPCHK(hipStreamWaitEvent(stream, ev, 0));
         HIPCHK(hipMemcpyAsync(q.recv, src->send, sizeof(double) * (size_t)q.count, hipMemcpyDeviceToDevice, stream));
     }
     HIPCHK(hipEventRecord(c->lb_ev_b, stream));
     RC(lb_meet(c, 1, peers));
-    for (const auto &q : p->peers) HIPCHK(hipStreamWaitEvent(stream, L.ctx[q.rank]->lb_ev_b, 0));
+    std::vector<hipEvent_t> evs;
+    {
+        std::lock_guard<std::mutex> g(L.mu);
+        for (const auto &q : p->peers) {
+            if (!L.ctx[q.rank]) return set_error(OCN_ERR_COMM, "loopback transport: a peer rank was destroyed");
+            evs.push_back(L.ctx[q.rank]->lb_ev_b);
+        }
+    }
+    for (hipEvent_t e : evs) HIPCHK(hipStreamWaitEvent(stream, e, 0));
     return OCN_OK;
 }
 
 // max over the ranks of one device int32 (the role-flip vote): ncclAllReduce, or over the
 // loopback transport every rank reads every rank's word (after its lb_ev_a) into d_red and copies
 // it back after all ranks have read (lb_ev_b).
-struct VotePtrs { const int32_t *p[64]; int n; };
+struct VotePtrs { const int32_t *p[64]; int n, words; };
 __global__ void k_vote_max(VotePtrs v, int32_t *out)
 {
-    if (threadIdx.x != 0) return;
-    int32_t m = v.p[0][0];
-    for (int i = 1; i < v.n; ++i) m = max(m, v.p[i][0]);
-    *out = m;
+    const int w = (int)threadIdx.x;
+    if (w >= v.words) return;
+    int32_t m = v.p[0][w];
+    for (int i = 1; i < v.n; ++i) m = max(m, v.p[i][w]);
+    out[w] = m;
 }
-static int allreduce_max(ocn_ctx *c, int32_t *word, hipStream_t s)
+constexpr int kVoteWords = 8;   // the role-flip vote (check_coherence): one 0/1 word per condition
+static int allreduce_max(ocn_ctx *c, int32_t *word, hipStream_t s, int words = 1)
 {
-    if (c->comm) return nccl_rc(ncclAllReduce(word, word, 1, ncclInt32, ncclMax, c->comm, s), "ncclAllReduce");
+    if (c->comm)
+        return nccl_rc(ncclAllReduce(word, word, (size_t)words, ncclInt32, ncclMax, c->comm, s), "ncclAllReduce");
     if (!c->lb) return OCN_OK;
     Loopback &L = *c->lb;
     std::vector<int> all(L.n);
@@ -735,27 +775,42 @@ static int allreduce_max(ocn_ctx *c, int32_t *word, hipStream_t s)
     RC(lb_meet(c, 2, all));
     VotePtrs v{};
     v.n = L.n;
-    for (int i = 0; i < L.n; ++i) {
+    v.words = words;
+    std::vector<hipEvent_t> evs;
+    {   // snapshot under the lock: a peer destroyed after the rendezvous fails the vote
         std::lock_guard<std::mutex> g(L.mu);
-        v.p[i] = L.vote[i];
-        HIPCHK(hipStreamWaitEvent(s, L.ctx[i]->lb_ev_a, 0));
+        for (int i = 0; i < L.n; ++i) {
+            if (!L.ctx[i]) return set_error(OCN_ERR_COMM, "loopback transport: a peer rank was destroyed");
+            v.p[i] = L.vote[i];
+            evs.push_back(L.ctx[i]->lb_ev_a);
+        }
     }
+    for (hipEvent_t e : evs) HIPCHK(hipStreamWaitEvent(s, e, 0));
     int32_t *red = c->d_nbad + 48;
     hipLaunchKernelGGL(k_vote_max, dim3(1), dim3(64), 0, s, v, red);
     RC(check_launch());
     HIPCHK(hipEventRecord(c->lb_ev_b, s));
     RC(lb_meet(c, 3, all));
-    for (int i = 0; i < L.n; ++i) HIPCHK(hipStreamWaitEvent(s, L.ctx[i]->lb_ev_b, 0));
-    HIPCHK(hipMemcpyAsync(word, red, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    evs.clear();
+    {
+        std::lock_guard<std::mutex> g(L.mu);
+        for (int i = 0; i < L.n; ++i) {
+            if (!L.ctx[i]) return set_error(OCN_ERR_COMM, "loopback transport: a peer rank was destroyed");
+            evs.push_back(L.ctx[i]->lb_ev_b);
+        }
+    }
+    for (hipEvent_t e : evs) HIPCHK(hipStreamWaitEvent(s, e, 0));
+    HIPCHK(hipMemcpyAsync(word, red, sizeof(int32_t) * (size_t)words, hipMemcpyDeviceToDevice, s));
     return OCN_OK;
 }
 
 // cmp != nullptr: compare the halos with what the exchange would deliver instead of writing them
 // (ORs 1 into *cmp where they differ); same messages, so every rank must take part.
-static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stream = nullptr, int32_t *cmp = nullptr)
+static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stream = nullptr, int32_t *cmp = nullptr,
+                    int depth = 1, int priv = 0)
 {
     HaloPlan *p;
-    RC(get_plan(c, fields, p));
+    RC(get_plan(c, fields, p, depth, priv));
     if (!stream) stream = c->stream;
     if (!p->peers.empty()) {
         if (!has_comm(c)) return set_error(OCN_ERR_COMM, "remote neighbours but no RCCL communicator attached");
@@ -1090,19 +1145,34 @@ static bool is_flip_field(int id)
 //    own ring values where the standard step takes the exchanged ones.
 // Every rank must run the same kind of step (the exchanges differ), so with RCCL the verdicts
 // are max-reduced over the ranks; eligible = false: this rank cannot run role-flip steps at all.
-static int check_coherence(ocn_ctx *c, bool eligible = true)
+// The vote also carries the other per-rank conditions that decide which launches and exchanges a
+// call runs (one 0/1 word each, max-reduced = OR over the ranks): every rank then takes the same
+// one-pass / hybrid decisions, so the exchange sequences of all ranks match.
+enum { kVoteIncoherent = 0, kVoteIneligible, kVoteUdiv, kVoteHhStale, kVoteX2, kVoteUsed };
+static_assert(kVoteUsed <= kVoteWords, "vote words");
+struct VoteIn { bool eligible, udiv_ok, hh_consistent, x2_ok; };
+struct VoteOut { bool udiv_ok, hh_consistent, x2_ok; };
+static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
 {
-    HIPCHK(hipMemsetAsync(c->d_flags, eligible ? 0 : 1, sizeof(int32_t), c->stream));
-    if (eligible)
+    int32_t host[kVoteWords] = {0};
+    host[kVoteIneligible] = !in.eligible;
+    host[kVoteUdiv] = !in.udiv_ok;
+    host[kVoteHhStale] = !in.hh_consistent;
+    host[kVoteX2] = !in.x2_ok;
+    HIPCHK(hipMemcpyAsync(c->d_flags, host, sizeof(host), hipMemcpyHostToDevice, c->stream));
+    if (in.eligible)
         for (const LBlock &b : c->blocks) RC(launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream));
     const bool exch = has_exchange(c);
     if (exch) RC(run_sync(c, kHaloCheck, c->stream, c->d_flags));
-    RC(allreduce_max(c, c->d_flags, c->stream));
-    int32_t flags = 0;
-    HIPCHK(hipMemcpyAsync(&flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+    RC(allreduce_max(c, c->d_flags, c->stream, kVoteUsed));
+    int32_t w[kVoteWords] = {0};
+    HIPCHK(hipMemcpyAsync(w, c->d_flags, sizeof(int32_t) * kVoteUsed, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    c->coherent = flags == 0;
+    c->coherent = w[kVoteIncoherent] == 0 && w[kVoteIneligible] == 0;
     c->coherent_known = !c->r8_escaped && !has_comm(c);
+    out.udiv_ok = w[kVoteUdiv] == 0;
+    out.hh_consistent = w[kVoteHhStale] == 0;
+    out.x2_ok = w[kVoteX2] == 0;
     return OCN_OK;
 }
 
@@ -1125,6 +1195,9 @@ static bool flip_eligible(ocn_ctx *c)
 {
     return c->flip && c->fused && c->compact && c->march;
 }
+
+// block b's one-pass variant for the current call (ctx kc_mode, the device verdict, its constants)
+static OnepassKC kc_of(const ocn_ctx *c, const LBlock &b) { return OnepassKC{c->kc_mode, c->d_fbz, b.kc}; }
 
 // The part of block b's interior the one-pass step covers when halos are exchanged: the interior
 // less w points on each side that has a neighbour block (E, W, N, S; diagonal neighbours only
@@ -1213,7 +1286,7 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last 
         for (const LBlock &b : c->blocks) {
             const Range in = onepass_inner(b, 1);
             RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
-                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, c->fb_zero, b.hr0, b.mu0));
+                              (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, kc_of(c, b)));
         }
         RC(timer_end(c, rec));
         HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
@@ -1235,7 +1308,7 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last 
     for (const LBlock &b : c->blocks) {
         const Range in = onepass_inner(b, 1);
         RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
-                          (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, c->fb_zero, b.hr0, b.mu0));
+                          (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, kc_of(c, b)));
     }
     RC(timer_end(c, rec));
     if (xch) {
@@ -1317,7 +1390,7 @@ static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
     for (const LBlock &b : c->blocks)
         RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.check ? c->d_nbad : nullptr,
                           (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, true,
-                          c->fb_zero, b.hr0, b.mu0));
+                          kc_of(c, b)));
     RC(timer_end(c, rec));
     swap_alt3(c);
     swap_roles(c);
@@ -1359,7 +1432,7 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
             for (const LBlock &b : c->blocks)
                 RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad,
                                   (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, false,
-                                  c->fb_zero, b.hr0, b.mu0));
+                                  kc_of(c, b)));
             RC(timer_end(c, rec));
             swap_alt3(c);
             swap_roles(c);
@@ -1717,6 +1790,7 @@ int ocn_abi_version(void) { return OCN_ABI_VERSION; }
 #define OCN_BUILD_ID "unknown"
 #endif
 const char *ocn_build_id(void) { return OCN_BUILD_ID; }
+int64_t ocn_launch_count(void) { return (int64_t)g_launches.load(std::memory_order_relaxed); }
 
 int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_decomp *dec, const int32_t *mask,
                    ocn_ctx **out)
@@ -1855,19 +1929,22 @@ int ocn_ctx_block_info(const ocn_ctx *c, int k, ocn_block_info *out)
 }
 
 static int alt_home(ocn_ctx *c);
+static int complete_open(ocn_ctx *c);
 void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
 {
     if (!c || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id)) {
         set_error(OCN_ERR_ARG, "bad block index or field id");
         return nullptr;
     }
+    ocn_ctx *w = const_cast<ocn_ctx *>(c);
+    if (complete_open(w) != OCN_OK) return nullptr;   // the arrays hold what the reference leaves
     if (is_r4(id)) c->r4_escaped = true;   // may be written behind our back: no compact tables
     // a raw r8 pointer names the field's own buffer from now on (step_impl returns the current
     // values there at the end of every call)
-    if (!is_r4(id) && alt_home(const_cast<ocn_ctx *>(c)) != OCN_OK) return nullptr;
+    if (!is_r4(id) && alt_home(w) != OCN_OK) return nullptr;
     if (is_flip_field(id)) { c->r8_escaped = true; c->coherent_known = false; }
     if (is_alt_field(id)) c->alt_ok = false;
-    if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_zero_known = false; }
+    if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_state = kFbUnchecked; }
     return c->blocks[k].ptr[field_slot(id)];
 }
 
@@ -1925,9 +2002,10 @@ int ocn_ctx_init_state(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
+    c->open = false;   // a pending call tail is void: every field is formed again
     c->coherent_known = false;
     c->alt_ok = false;
-    c->fb_zero_known = false;
+    c->fb_state = kFbUnchecked;
     const int rc = lb_fail_on_error(c, init_state(c));
     c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // init_data.f90:60-63 ran hh_init last
     return rc;
@@ -1937,9 +2015,18 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
 {
     if (!c || !has_r8(c, field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
     HIPCHK(hipSetDevice(c->dec.device));
+    RC(complete_open(c));
+    HaloPlan *p;
+    RC(get_plan(c, {field_id}, p));
+    // no neighbour block anywhere (one block, no other rank): the exchange writes nothing, so
+    // nothing the step decisions rest on changes -- a PSy-style caller syncing between 1-step
+    // calls pays no re-check (and no host wait) for it
+    if (!p->n_local && p->peers.empty()) return OCN_OK;
     c->coherent_known = false;
     c->hh_consistent = false;
-    c->fb_zero_known = false;
+    c->fb_state = kFbUnchecked;
+    // the current buffer's halos change; the one-pass steps' second buffer must be copied again
+    if (is_alt_field(field_id)) c->alt_ok = false;
     return run_sync(c, {field_id});
 }
 
@@ -1948,10 +2035,11 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
     if (stage_id < 0 || stage_id >= OCN_NUM_STAGES) return set_error(OCN_ERR_ARG, "bad stage id");
+    RC(complete_open(c));
     c->coherent_known = false;
     c->alt_ok = false;
     c->hh_consistent = false;
-    c->fb_zero_known = false;
+    c->fb_state = kFbUnchecked;
     return envoke(c, stage_id, tau);
 }
 
@@ -1968,13 +2056,15 @@ static int run_step(ocn_ctx *c, double tau, const StepKind &k)
     return expl_tracer(c, tau, c->fused && c->compact);
 }
 
-// one step as a replayed hipGraph, captured once per (tau, step kind, compact, role); a
-// role-flip step swaps the host's pointer roles as the captured launches did
+// one step as a replayed hipGraph, captured once per (tau, step kind, compact, role, one-pass
+// variant); a role-flip step swaps the host's pointer roles as the captured launches did.  The
+// known-constant variant's constants and the device check's verdict are read from device memory
+// by the launches, so a replay sees their current values.
 static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
 {
     for (const auto &g : c->graphs)
         if (g.tau == tau && g.kind == k && g.compact == c->compact && g.march == c->march && g.ring_sea == c->ring_sea &&
-            g.role == c->role) {
+            g.role == c->role && g.kc_mode == c->kc_mode) {
             HIPCHK(hipGraphLaunch(g.exec, c->stream));
             if (k.rc) swap_sshp(c);
             if (k.one || k.one_last) swap_alt3(c);
@@ -1995,7 +2085,7 @@ static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     HIPCHK(e);
-    c->graphs.push_back(ocn_ctx::Graph{exec, tau, k, c->compact, c->march, c->ring_sea, role});
+    c->graphs.push_back(ocn_ctx::Graph{exec, tau, k, c->compact, c->march, c->ring_sea, role, c->kc_mode});
     HIPCHK(hipGraphLaunch(exec, c->stream));
     return OCN_OK;
 }
@@ -2007,6 +2097,7 @@ int ocn_ctx_tracer_stage(ocn_ctx *c, int stage_id, int tracer, double tau)
     if (c->sw.use_tracers <= 0 || tracer < 1 || tracer > c->sw.tracer_num)
         return set_error(OCN_ERR_ARG, "no such tracer (use_tracers / tracer_num)");
     if (stage_id < 0 || stage_id >= OCN_NUM_TSTAGES) return set_error(OCN_ERR_ARG, "bad tracer stage id");
+    RC(complete_open(c));
     return tracer_stage(c, stage_id, tracer, tau, false);
 }
 
@@ -2024,50 +2115,143 @@ static int alt_home(ocn_ctx *c)
     return OCN_OK;
 }
 
+// The stream has been synchronised by the caller: read a pending device verdict of the
+// known-constant check, so that later calls launch only the variant it selected.
+static void learn_fb(ocn_ctx *c)
+{
+    if (c->fb_state != kFbDevice) return;
+    int32_t f = 0;
+    if (hipMemcpy(&f, c->d_fbz, sizeof(f), hipMemcpyDeviceToHost) != hipSuccess) return;
+    c->fb_state = f == 0 ? kFbZero : kFbGeneral;
+}
+
+// The one-pass variant of this call (OCN_KC_*): the known-constant one only when its precondition
+// is known to hold; a raw r8 pointer in the caller's hands (r8_handed) may change the arrays at any
+// time, so then always the general one (a check per call would cost a pass over 12 arrays);
+// unchecked: the check runs on the stream and both variants are launched (the device picks) --
+// no host wait inside a step.
+static int prepare_kc(ocn_ctx *c)
+{
+    if (!c->known_const || c->r8_handed) { c->kc_mode = OCN_KC_GENERAL; return OCN_OK; }
+    if (c->fb_state == kFbUnchecked) {
+        HIPCHK(hipMemsetAsync(c->d_fbz, 0, sizeof(int32_t), c->stream));
+        for (const LBlock &b : c->blocks)
+            RC(launch_fallback_check(&b.g, b.ptr.data(), b.bits, onepass_inner(b, 1), c->d_fbz, b.kc, c->stream));
+        c->fb_state = kFbDevice;
+    }
+    c->kc_mode = c->fb_state == kFbZero ? OCN_KC_KNOWN : c->fb_state == kFbGeneral ? OCN_KC_GENERAL : OCN_KC_DEVICE;
+    return OCN_OK;
+}
+
+// The end of a call that leaves no step pending: nothing stays in flight, the pairs' roles return
+// (the last step left both buffers of each pair equal), the recompute steps' sshp comes home
+static int finish_call(ocn_ctx *c, int rc)
+{
+    if (const int rj = join_sync(c); rc == OCN_OK) rc = rj;
+    if (c->role & 1) swap_roles(c);
+    if (c->role & 2) {   // sshp's buffers are not equal: the current one is copied into the field's own buffer
+        for (LBlock &b : c->blocks)
+            HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
+                                  c->stream));
+        swap_sshp(c);
+    }
+    // one-pass steps: sshp / ubrtrp / vbrtrp stay in the second buffers (every access goes through
+    // the field table) unless a raw r8 pointer was handed out: then back into the fields' buffers
+    if ((c->role & 4) && c->r8_handed) RC(alt_home(c));
+    c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // the last step ran a full hh_init
+    return rc;
+}
+
+// Lazy call tail possible: single process (a tail formed on one rank only would unbalance the
+// exchanges), no raw r8 pointers handed out, no tracers (expl_tracer reads hh_init's arrays after
+// every step), and the one-pass step as one launch per block (no exchange, no a8 / a9 work on the
+// halo ring: the redone step must find the previous state intact).
+static bool lazy_allowed(const ocn_ctx *c)
+{
+    return c->lazy && !has_comm(c) && !c->r8_handed && c->sw.use_tracers <= 0 && !c->ring_sea &&
+           !has_exchange(const_cast<ocn_ctx *>(c));
+}
+
+// The pending tail of an open sequence: the last step run (a one-pass step) is run again from the
+// previous state -- untouched in the other buffer of each pair and the other sshp / ubrtrp / vbrtrp
+// buffers -- as the call's last step (one_step_last: the same new state bit for bit, plus vort,
+// the stresses, the RHS terms, a8's copies and hh_init with every level).  Its check_ssh_err
+// count was taken the first time.
+static int complete_open(ocn_ctx *c)
+{
+    if (!c->open) return OCN_OK;
+    c->open = false;
+    HIPCHK(hipSetDevice(c->dec.device));
+    swap_roles(c);
+    swap_alt3(c);
+    StepKind k{};
+    k.last = k.one_last = true;
+    return finish_call(c, one_step_last(c, c->open_tau, k));
+}
+
 static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
 {
     HIPCHK(hipSetDevice(c->dec.device));
     if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
-    if (c->fused) RC(prepare_static(c));
+    if (nsteps < 0) return set_error(OCN_ERR_ARG, "nsteps < 0");
+    if (nsteps == 0) return OCN_OK;
     const bool graph_ok = c->use_graph && !has_comm(c) && !c->stage_timing;   // RCCL / events stay outside graphs
-    // with RCCL every rank takes part in the decision (check_coherence reduces the verdicts)
+    if (c->open) {
+        if (tau == c->open_tau && c->onepass && lazy_allowed(c)) {
+            // the open sequence goes on: every step of this call is a one-pass step (the state and
+            // the constants are what its last step left), and the tail stays pending; a device
+            // verdict the host has read since selects one variant
+            RC(prepare_kc(c));
+            int rc = OCN_OK;
+            for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
+                StepKind k{};
+                k.check = check_every > 0 && (s % check_every == 0);
+                k.flip = k.one = k.next_one = k.a_done = true;
+                rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
+            }
+            if (rc) { c->open = false; return finish_call(c, rc); }
+            return OCN_OK;
+        }
+        RC(complete_open(c));
+    }
+    if (c->fused) RC(prepare_static(c));
+    // with RCCL every rank takes part in the decisions (check_coherence reduces the verdicts)
     const bool eligible = flip_eligible(c);
-    bool flip_call = nsteps >= 2 && (eligible || (has_comm(c) && c->flip));
-    if (flip_call && !c->coherent_known) RC(check_coherence(c, eligible));
-    flip_call = flip_call && eligible && c->coherent;
+    // a lazy call is planned as the first nsteps steps of a call of nsteps + 1 (the last deferred)
+    const bool lazy_cand = eligible && c->onepass && lazy_allowed(c);
+    bool udiv_ok = c->udiv_ok, first_one = c->hh_consistent;
+    int N = lazy_cand ? nsteps + 1 : nsteps;
+    if (N >= 2 && (eligible || (has_comm(c) && c->flip)) && !c->coherent_known) {
+        VoteOut v;
+        RC(check_coherence(c, VoteIn{eligible, c->udiv_ok, c->hh_consistent, true}, v));
+        udiv_ok = v.udiv_ok;
+        first_one = v.hh_consistent;
+    }
+    bool flip_call = false, ca = false, one_call = false;
+    auto decide = [&](int n) {
+        flip_call = n >= 2 && eligible && c->coherent;
+        // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A;
+        // their reuse steps recompute hhq / hhu_p / hhv_p in fused B, which then filters sshp into
+        // the second buffer (the ring launch completes it on the halo ring)
+        ca = flip_call && c->sw.full_free_surface == 1;
+        // one-pass steps 2..K-1 (all SW terms on, no tracers: expl_tracer reads hh_init's hhu / hhv /
+        // hhq_p, which a one-pass step keeps in registers; row divisors in udiv's range) -- the first
+        // step too when hh_init's stored depths match the state (hh_consistent)
+        one_call = ca && c->onepass && (n >= 3 || (n >= 2 && first_one)) && c->sw.trans_terms > 0 &&
+                   c->sw.ksw_lat > 0 && c->sw.use_tracers <= 0 && udiv_ok;
+    };
+    decide(N);
+    // the last step run is a one-pass step: the tail may wait
+    const bool lazy_end = lazy_cand && one_call && (nsteps >= 2 || first_one);
+    if (!lazy_end && N != nsteps) decide(N = nsteps);
     c->flip_used = flip_call;
-    // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A;
-    // their reuse steps recompute hhq / hhu_p / hhv_p in fused B, which then filters sshp into
-    // the second buffer (the ring launch completes it on the halo ring)
-    const bool ca = flip_call && c->sw.full_free_surface == 1;
-    // one-pass steps 2..K-1 (single block, no a8 / a9 work on the halo ring, all SW terms on)
-    // (no tracers: expl_tracer reads hh_init's hhu / hhv / hhq_p, which a one-pass step keeps in registers)
-    // (the first step too when hh_init's stored depths match the state: hh_consistent)
-    const bool first_one = c->hh_consistent;
-    const bool one_call = ca && c->onepass && (nsteps >= 3 || (nsteps >= 2 && first_one)) &&
-                          c->sw.trans_terms > 0 && c->sw.ksw_lat > 0 && c->sw.use_tracers <= 0 && c->udiv_ok;
     c->hh_consistent = false;   // until this call's last step has run
     // the last step as one march + hh_init too (single block, no exchange, no ring work)
     // (with exchanges or ring work: the hybrid last step, OCN_OPT_ONEPASS_LAST)
     const bool last_one = one_call && ((c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) && !c->ring_sea) ||
                                        c->last_hybrid);
     c->one_used = one_call;
-    if (one_call && (!c->fb_zero_known || c->r8_handed)) {   // until something may write the D arrays from outside
-        HIPCHK(hipMemsetAsync(c->d_flags, 0, sizeof(int32_t), c->stream));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fallback_check(&b.g, b.ptr.data(), b.bits, onepass_inner(b, 1), c->d_flags, c->stream));
-        int32_t flag = 0;
-        HIPCHK(hipMemcpyAsync(&flag, c->d_flags, sizeof(flag), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        c->fb_zero = flag == 0 && c->known_const;
-        c->fb_zero_known = true;
-        for (LBlock &b : c->blocks) {   // the uniform h_r and mu the check compared against
-            const Range in = onepass_inner(b, 1);
-            const size_t at = (size_t)(in.m0 - b.g.bnd_x1) + (size_t)(in.n0 - b.g.bnd_y1) * b.g.pitch;
-            HIPCHK(hipMemcpy(&b.hr0, b.f<double>(OCN_HHQ_REST) + at, 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(&b.mu0, b.f<double>(OCN_MU) + at, 8, hipMemcpyDeviceToHost));
-        }
-    }
+    if (one_call) RC(prepare_kc(c));
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;
     if (one_call && !c->alt_ok) {   // the second buffers start as copies (they agree outside a8's write set)
@@ -2081,7 +2265,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         }
         c->alt_ok = true;
     }
-    c->rc_used = rc_call && nsteps >= 3;
+    c->rc_used = rc_call && N >= 3;
     if (rc_call)   // the second sshp buffer starts as a copy: the two agree outside a8's write set
         for (const LBlock &b : c->blocks)
             HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
@@ -2092,33 +2276,24 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         StepKind k;
         k.check = check_every > 0 && (s % check_every == 0);
         k.first = s == 1;
-        k.last = s == nsteps;
+        k.last = s == N;
         k.flip = flip_call && !k.last;
-        k.one = one_call && (s >= 2 || first_one) && s <= nsteps - 1;
-        k.next_one = one_call && s + 1 <= nsteps - 1;
+        k.one = one_call && (s >= 2 || first_one) && s <= N - 1;
+        k.next_one = one_call && s + 1 <= N - 1;
         k.one_last = last_one && k.last;
         k.a_done = ca && !k.first;
-        k.next_a = ca && k.flip && !k.next_one && !(last_one && s + 1 == nsteps);
-        k.next_reuse = k.next_a && s + 1 < nsteps;
+        k.next_a = ca && k.flip && !k.next_one && !(last_one && s + 1 == N);
+        k.next_reuse = k.next_a && s + 1 < N;
         k.rc = rc_call && k.flip && !k.first;
-        k.rc_next = rc_call && s + 1 < nsteps;
+        k.rc_next = rc_call && s + 1 < N;
         rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
     }
-    if (const int rj = join_sync(c); rc == OCN_OK) rc = rj;   // nothing stays in flight past the call
-    // the last (standard) step left both buffers of each pair equal: undo the swap by pointers;
-    // sshp's buffers are not equal: the current one is copied into the field's own buffer
-    if (c->role & 1) swap_roles(c);
-    if (c->role & 2) {
-        for (LBlock &b : c->blocks)
-            HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
-                                  c->stream));
-        swap_sshp(c);
+    if (lazy_end && rc == OCN_OK) {   // the pending tail: complete_open
+        c->open = true;
+        c->open_tau = tau;
+        return OCN_OK;
     }
-    // one-pass steps: sshp / ubrtrp / vbrtrp stay in the second buffers (every access goes through
-    // the field table) unless a raw r8 pointer was handed out: then back into the fields' buffers
-    if ((c->role & 4) && c->r8_handed) RC(alt_home(c));
-    c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // the last step ran a full hh_init
-    return rc;
+    return finish_call(c, rc);
 }
 
 int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
@@ -2127,11 +2302,18 @@ int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
     return lb_fail_on_error(c, step_impl(c, tau, nsteps, check_every));
 }
 
+int ocn_ctx_complete(ocn_ctx *c)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return complete_open(c);
+}
+
 int ocn_ctx_synchronize(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
     HIPCHK(hipStreamSynchronize(c->stream));
+    learn_fb(c);
     int32_t nbad = 0;
     HIPCHK(hipMemcpy(&nbad, c->d_nbad, sizeof(nbad), hipMemcpyDeviceToHost));
     if (nbad) return set_error(OCN_ERR_BLOWUP, "SIGFPRE predict error: |ssh| >= 1e4 on " + std::to_string(nbad) +
@@ -2143,6 +2325,7 @@ int ocn_ctx_stage_times(ocn_ctx *c, double *ms, int64_t *counts)
 {
     if (!c || !ms || !counts) return set_error(OCN_ERR_ARG, "null argument");
     HIPCHK(hipStreamSynchronize(c->stream));
+    learn_fb(c);
     for (auto &r : c->recs) {
         float t = 0.f;
         HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
@@ -2160,10 +2343,13 @@ int ocn_ctx_download(ocn_ctx *c, int k, int id, void *host)
 {
     if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
         return set_error(OCN_ERR_ARG, "download: bad argument");
+    HIPCHK(hipSetDevice(c->dec.device));
+    RC(complete_open(c));
     const LBlock &b = c->blocks[k];
     const size_t es = is_r4(id) ? 4 : 8;
     const size_t w = (size_t)(b.g.bnd_x2 - b.g.bnd_x1 + 1), rows = (size_t)(b.g.bnd_y2 - b.g.bnd_y1 + 1);
     HIPCHK(hipStreamSynchronize(c->stream));
+    learn_fb(c);
     HIPCHK(hipMemcpy2D(host, w * es, b.ptr[field_slot(id)], (size_t)b.g.pitch * es, w * es, rows,
                        hipMemcpyDeviceToHost));
     return OCN_OK;
@@ -2173,6 +2359,8 @@ int ocn_ctx_output_r4(ocn_ctx *c, int k, int id, float undef, float *host)
 {
     if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
         return set_error(OCN_ERR_ARG, "output_r4: bad argument");
+    HIPCHK(hipSetDevice(c->dec.device));
+    RC(complete_open(c));
     const LBlock &b = c->blocks[k];
     const int w = b.g.nx_end - b.g.nx_start + 1, h = b.g.ny_end - b.g.ny_start + 1;
     if (w <= 0 || h <= 0) return OCN_OK;
@@ -2192,6 +2380,7 @@ int ocn_ctx_output_r4(ocn_ctx *c, int k, int id, float undef, float *host)
         rc = set_error(OCN_ERR_HIP, "output_r4: copy");
     (void)hipFreeAsync(d, c->stream);
     HIPCHK(hipStreamSynchronize(c->stream));
+    learn_fb(c);
     return rc;
 }
 
@@ -2199,18 +2388,25 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
 {
     if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
         return set_error(OCN_ERR_ARG, "upload: bad argument");
+    HIPCHK(hipSetDevice(c->dec.device));
+    RC(complete_open(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (is_r4(id)) c->static_dirty = true;
     if (is_flip_field(id)) c->coherent_known = false;
     if (is_alt_field(id)) c->alt_ok = false;
     c->hh_consistent = false;
-    c->fb_zero_known = false;
+    c->fb_state = kFbUnchecked;
     return upload_field(c, c->blocks[k], id, host, false);
 }
 
 int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    // an option may change what the next launches are: a pending call tail is formed first
+    if (key != OCN_OPT_STAGE_TIMING) {
+        HIPCHK(hipSetDevice(c->dec.device));
+        RC(complete_open(c));
+    }
     switch (key) {
     case OCN_OPT_GRAPH: c->use_graph = value != 0; return OCN_OK;
     case OCN_OPT_STAGE_TIMING: c->stage_timing = value != 0; return OCN_OK;
@@ -2231,9 +2427,9 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     case OCN_OPT_ONEPASS: c->onepass = value != 0; return OCN_OK;
     case OCN_OPT_ONEPASS_LAST: c->last_hybrid = value != 0; return OCN_OK;
     case OCN_OPT_KNOWN_CONSTANTS:
-        c->known_const = value != 0;
-        c->fb_zero_known = false;   // checked again at the next one-pass call
+        c->known_const = value != 0;   // (the check's verdict stays valid: it describes the arrays)
         return OCN_OK;
+    case OCN_OPT_LAZY_TAIL: c->lazy = value != 0; return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -2255,9 +2451,16 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
     case OCN_OPT_RECOMPUTE: *value = c->recompute && c->rc_used; return OCN_OK;
-    case OCN_OPT_ONEPASS: *value = c->onepass && c->one_used ? (c->fb_zero ? 2 : 1) : 0; return OCN_OK;
+    case OCN_OPT_ONEPASS: {
+        // 2: the known-constant variant ran (chosen by the host, or by the device check whose verdict
+        // the host has read since)
+        const bool z = c->kc_mode == OCN_KC_KNOWN || (c->kc_mode == OCN_KC_DEVICE && c->fb_state == kFbZero);
+        *value = c->onepass && c->one_used ? (z ? 2 : 1) : 0;
+        return OCN_OK;
+    }
     case OCN_OPT_KNOWN_CONSTANTS: *value = c->known_const; return OCN_OK;
     case OCN_OPT_ONEPASS_LAST: *value = c->last_hybrid; return OCN_OK;
+    case OCN_OPT_LAZY_TAIL: *value = c->open ? 2 : c->lazy; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -102,7 +102,13 @@ struct GridInit {
     double cos_rot, sin_rot, sin_extr;             // dcosd / dsind(rotation_on_lat), dsind(lat_extr)
     float sx, sy, cor, sqrt2;                      // base steps (m), 2 * EarthAngVel, sqrt(2.0)
     int curve;
+    // rows bnd_y1 / bnd_y2 (outside the metric range): their factors and where their metric values
+    // go (2 x (OCN_NUM_R4 - OCN_DX) floats: OCN_DX .. OCN_R_DISS of each; nullptr: not formed)
+    float ext_ct[2], ext_cv[2];
+    double ext_sin_v[2], ext_cosy_v[2];
+    float *ext;
 };
+constexpr int kExtRowFloats = 2 * (OCN_NUM_R4 - OCN_DX);
 int launch_init_grid(const GridInit &q, hipStream_t s);
 // gaussian_elimination_kernel (vel_ssh.f90:15-38) into p (zero outside the sea interior)
 int launch_gaussian(const ocn_block &g, double *p, const float *lu, int nx0, int ny0, double sigma, hipStream_t s);
@@ -112,16 +118,34 @@ int launch_fill_field(const ocn_block &g, double *p, double v, hipStream_t s);
 // with hh_init's depths, vort and the stresses formed in registers from the state; single block,
 // no a8 / a9 work on the halo ring; a8's filtered sshp / ubrtrp / vbrtrp go to the given buffers.
 // range: the points it computes (default: the interior) -- with halo exchanges, the part of the
-// interior whose stencils stay off the halos the exchanges fill
+// interior whose stencils stay off the halos the exchanges fill.
+// kc: which variant -- OCN_KC_GENERAL reads h_r, mu, the forcing and D's fallback values;
+// OCN_KC_KNOWN takes them as +0.0 / the uniform values kc[0], kc[1] (device memory, written by
+// launch_fallback_check); OCN_KC_DEVICE launches both, each running only if the device verdict
+// *flag (launch_fallback_check's) is its own -- no host wait for the check.
+enum { OCN_KC_GENERAL = 0, OCN_KC_KNOWN = 1, OCN_KC_DEVICE = 2 };
+struct OnepassKC { int mode; const int32_t *flag; const double *kc; };
+// own (sw_stencils.h own_class bits, not with last): the halo points neighbour blocks own hold the
+// neighbours' state two points deep -- D there is formed as on their interior (MarchStep X2)
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range = nullptr, bool last = false, bool zero_fallback = false,
-                   double hr0 = 0.0, double mu0 = 0.0);
-// zero_fallback precondition of launch_onepass over r (sw_kernels.hip FallbackCheck: the fallback
-// points and the forcing hold +0.0, h_r and mu are uniform -- hr0 / mu0 are then their values at
-// (r.m0, r.n0)): ORs 1 into *flag where it does not hold
+                   const Range *range, bool last, const OnepassKC &kc, unsigned own = 0);
+// the known-constant precondition of launch_onepass over r (sw_kernels.hip FallbackCheck: the
+// fallback points and the forcing hold +0.0, h_r and mu are uniform): ORs 1 into *flag where it
+// does not hold; writes h_r and mu at (r.m0, r.n0) to kc[0], kc[1]
 int launch_fallback_check(const ocn_block *b, void *const *ptr, const uint8_t *bits, const Range &r, int32_t *flag,
-                          hipStream_t s);
+                          double *kc, hipStream_t s, unsigned own = 0);
+// Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
+// they cannot be used into *flags (device int); own: the halo points neighbour blocks own
+// (sw_stencils.h own_class bits; OCN_COMPACT_EDGE_RING_SEA tests the others)
+int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s,
+                   unsigned own = 0);
+// rows_x = the row table `rows` with rows 0 and nrows - 1 formed from ext (init_kernels.hip k_ext_rows:
+// the metric values of rows bnd_y1 / bnd_y2 as the neighbours form them); ORs
+// OCN_COMPACT_DIVISOR_RANGE into *flags if a divisor there is out of udiv's range
+int launch_rows_ext(const ocn_block *b, const float *rows, float *rows_x, const float *ext, int32_t *flags,
+                    hipStream_t s);
+constexpr int kCompactEdgeRingSea = 16;   // sw_stencils.h OCN_COMPACT_EDGE_RING_SEA
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);
@@ -131,10 +155,15 @@ int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, 
 // Prepare's flag bit reporting mask bits on the halo ring (sw_stencils.h OCN_COMPACT_RING_SEA)
 constexpr int kCompactRingSea = 4;
 constexpr int kCompactDivisorRange = 8;   // sw_stencils.h OCN_COMPACT_DIVISOR_RANGE
-// Builds the compact tables of a block from its real(4) arrays; ORs OCN_COMPACT_* reasons
-// they cannot be used into *flags (device int).
-int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s);
+
 int check_hip(hipError_t e, const char *what);
-inline int check_launch() { return check_hip(hipGetLastError(), "kernel launch"); }
+// every kernel launch of the library is followed by check_launch(): it also counts them
+// (ocn_launch_count, for the launches-per-step figure of bench.py)
+void count_launch();
+inline int check_launch()
+{
+    count_launch();
+    return check_hip(hipGetLastError(), "kernel launch");
+}
 
 }  // namespace ocn

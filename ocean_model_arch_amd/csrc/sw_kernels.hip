@@ -245,10 +245,17 @@ template <class B> struct WavesOf<B, std::void_t<decltype(B::kWaves)>> { static 
 // a body with a workgroup prologue (Body::prologue(R, ty), called by all 4 waves of a workgroup)
 template <class B, class = void> struct HasPrologue { static constexpr bool v = false; };
 template <class B> struct HasPrologue<B, std::void_t<decltype(B::kPrologue)>> { static constexpr bool v = B::kPrologue; };
+// a body whose launch may be void at run time (Body::enabled(), a device-side predicate read by
+// every workgroup before anything else: the one-pass step's two variants, one of which a device
+// check selected -- ocn_ctx.hip launches both and never waits for the verdict)
+template <class B, class = void> struct HasGate { static constexpr bool v = false; };
+template <class B> struct HasGate<B, std::void_t<decltype(B::kGate)>> { static constexpr bool v = B::kGate; };
 
 template <class Body>
 __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Body body)
 {
+    if constexpr (HasGate<Body>::v)
+        if (!body.enabled()) return;   // workgroup-uniform (a value in memory)
     int tile = (int)blockIdx.x;
 #if OCN_XCD_REMAP
     const int per = (g.ntiles + 7) / 8;
@@ -1145,6 +1152,7 @@ struct StepRegs {
     unsigned nrows, rn;               // table stride, row index of n (n - bnd_y1)
     double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
     double tau, inv_tau, f;
+    double hr0, mu0;                   // known-constant variant: the uniform h_r and mu (MarchStep::kc)
     const __attribute__((address_space(3))) double *lds;   // OCN_STEP_LDS: the workgroup's row constants
     unsigned rlo;                                            // table row of lds row 0
     // row constant k (RowC) of row n + dy, from LDS or from scalar loads
@@ -1232,14 +1240,28 @@ struct StepRegs {
 // init_data.f90 sets h_r = 100 m and mu = 0 everywhere -- until a field is uploaded): those are
 // kernel constants -- no loads (32 B per cell fewer), twelve array pointers fewer in the kernel's
 // scalar registers, and the same arithmetic on the same values.
-template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
+// X2: the block's halo points that neighbour blocks own (`own`, sw_stencils.h own_class bits) hold
+// the neighbours' state two points deep (ocn_ctx.hip one_step_x2: one 2-deep exchange per step),
+// so D there is formed here as the neighbour forms it on its interior -- what the reference's
+// exchanges of D deliver -- and the march covers the whole interior.
+template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct MarchStep {
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
     static constexpr int kWaves = OCN_STEP_WAVES;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; int32_t *nbad;
     double *sshp_out, *up_out, *vp_out;   // a8's filtered sshp / ubrtrp / vbrtrp (the second buffers)
-    double hr0 = 0.0, mu0 = 0.0;          // ZF: the values h_r and mu hold at every point the step reads
-
+    // ZF: kc[0], kc[1] = the values h_r and mu hold at every point the step reads (device memory,
+    // written by launch_fallback_check).  gate: 0 = always run; 1 / 2 = run only if the device
+    // check's verdict *fbz is 0 / nonzero (both variants launched, the device picks: no host wait)
+    const double *kc; const int32_t *fbz; int gate;
+    unsigned own;   // X2: own_class bits of the halo points neighbour blocks own
+    static constexpr bool kGate = true;
+    __device__ __forceinline__ bool enabled() const
+    {
+        if (gate == 0) return true;
+        const int f = *(const volatile int32_t *)fbz;
+        return gate == 1 ? f == 0 : f != 0;
+    }
 
     // a / tau (sw_update_uv_math qtau).  P2: tau is a power of two, so a / tau is a * (1 / tau) bit
     // for bit (both round the same real value once; exact scalings unless subnormal)
@@ -1247,15 +1269,15 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
 
     // one row's loads for iteration n (rows of the state the march adds)
     struct Batch { double u, v, up, vp, ssh, shp, hr, mu, rhsx, rhsy; unsigned bits; };
-    __device__ __forceinline__ void load(Batch &q, int m, int n) const
+    __device__ __forceinline__ void load(const StepRegs &x, Batch &q, int m, int n) const
     {
         const Geo I = geo(&b);
         const Pt c = I(m, n), c1 = I(m, n + 1), c2 = I(m, n + 2);
         q.u = ld(t.f(OCN_UBRTR), c2); q.up = ld(t.f(OCN_UBRTRP), c2);
         q.ssh = ld(t.f(OCN_SSH), c2); q.shp = ld(t.f(OCN_SSHP), c2);
-        q.hr = ZF ? hr0 : ld(t.f(OCN_HHQ_REST), c2);
+        q.hr = ZF ? x.hr0 : ld(t.f(OCN_HHQ_REST), c2);
         q.bits = ld(t.bits, c2);
-        q.v = ld(t.f(OCN_VBRTR), c1); q.vp = ld(t.f(OCN_VBRTRP), c1); q.mu = ZF ? mu0 : ld(t.f(OCN_MU), c1);
+        q.v = ld(t.f(OCN_VBRTR), c1); q.vp = ld(t.f(OCN_VBRTRP), c1); q.mu = ZF ? x.mu0 : ld(t.f(OCN_MU), c1);
         if (ZF) q.rhsx = q.rhsy = 0.0;
         else { q.rhsx = ld(t.f(OCN_RHSX), c); q.rhsy = ld(t.f(OCN_RHSY), c); }
     }
@@ -1297,8 +1319,13 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
     {
         const Pt c = geo(&b)(m, r);
         const unsigned bc = x.bits.s<PH>(slot);
-        const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && r >= b.ny_start - 1 && r <= b.ny_end;
-        const bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
+        bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && r >= b.ny_start - 1 && r <= b.ny_end;
+        bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
+        if (X2) {   // a point a neighbour owns is in its interior: in both stages' ranges there
+            const bool owned = (own >> (own_class(m, b.nx_start, b.nx_end) * 3u + own_class(r, b.ny_start, b.ny_end))) & 1u;
+            hh_rng = hh_rng || owned;
+            in = in || owned;
+        }
         f.llu = hh_rng && (bc & (1u << OCN_LLU));
         f.llv = hh_rng && (bc & (1u << OCN_LLV));
         f.luh = hh_rng && (bc & (1u << OCN_LUH));
@@ -1607,6 +1634,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         x.tau = tau;
         x.inv_tau = 1.0 / tau;
         x.f = (double)sw.full_free_surface;
+        if (ZF) { x.hr0 = kc[0]; x.mu0 = kc[1]; }
         // iteration n computes D(n+1) and, from n = nb on, S(n); two warm iterations give D(nb-1)
         // and D(nb).  Before iteration n0 = nb - 2 the rows it does not load itself: up, ssh, sshp,
         // h_r, bits at n0+1; vp at n0; metric rows n0, n0+1; the weights of row n0+1.
@@ -1614,7 +1642,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         {
             const Pt c = I(L.m, n0), c1 = I(L.m, n0 + 1);
             x.up.s<0>(2) = ld(t.f(OCN_UBRTRP), c1); x.ssh.s<0>(2) = ld(t.f(OCN_SSH), c1);
-            x.shp.s<0>(2) = ld(t.f(OCN_SSHP), c1); x.hr.s<0>(2) = ZF ? hr0 : ld(t.f(OCN_HHQ_REST), c1);
+            x.shp.s<0>(2) = ld(t.f(OCN_SSHP), c1); x.hr.s<0>(2) = ZF ? x.hr0 : ld(t.f(OCN_HHQ_REST), c1);
             x.bits.s<0>(2) = ld(t.bits, c1); x.u.s<0>(2) = ld(t.f(OCN_UBRTR), c1);
             x.vp.s<0>(1) = ld(t.f(OCN_VBRTRP), c);
             // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
@@ -1627,9 +1655,9 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
 #if OCN_STEP_ONEBLOCK && OCN_STEP_PF2 && OCN_STEP_BUFST
         if constexpr (kUnroll) {   // two batches in flight: iteration n takes qs[n - n0 & 1], loaded at n - 2
             Batch qs[2];
-            load(qs[0], L.m, n0);
+            load(x, qs[0], L.m, n0);
             store_out(Out{}, 0u);   // (every lane dropped: the same operations after each batch's loads as
-            load(qs[1], L.m, n0 + 1);   // in the loop, so its waits stay vmcnt(19))
+            load(x, qs[1], L.m, n0 + 1);   // in the loop, so its waits stay vmcnt(19))
             store_out(Out{}, 0u);
             iteration<0, true>(x, fb, qs[0], L, n0, nb, ne);
             iteration<1, true>(x, fb, qs[1], L, n0 + 1, nb, ne);
@@ -1645,7 +1673,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         }
 #endif
         Batch q;
-        load(q, L.m, n0);
+        load(x, q, L.m, n0);
 #if OCN_STEP_BUFST
         store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
 #endif
@@ -1704,7 +1732,7 @@ template <bool P2, bool LAST = false, bool ZF = false> struct MarchStep {
         take<PH>(x, q);
         Fallback fbn;
         if (n < ne) fallback<PH>(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
-        if (n + kAhead - 1 < ne) load(q, L.m, n + kAhead);   // in flight while this row (and the next) is computed
+        if (n + kAhead - 1 < ne) load(x, q, L.m, n + kAhead);   // in flight while this row (and the next) is computed
         Out o;
 #if OCN_STEP_ONEBLOCK
         {
@@ -1944,15 +1972,19 @@ struct FallbackCheck {
     ocn_block b; const uint8_t *bits; const double *hu, *hu1, *hv, *hv1, *hh, *vort, *stt, *sts, *rx, *ry; int *flag;
     Range r;   // the points the step updates: RHSx / RHSy are read there
     const double *hr, *mu;   // uniform over r +- 2 (h_r) / r +- 1 (mu): equal to their values at (r.m0, r.n0)
+    double *kc;              // <- h_r, mu at (r.m0, r.n0): the known-constant variant's constants
+    unsigned own;            // MarchStep X2: halo points neighbours own are no fallback points
     OCN_HD void operator()(int m, int n) const
     {
         const Pt c = geo(&b)(m, n), c0 = geo(&b)(r.m0, r.n0);
+        if (m == r.m0 && n == r.n0) { kc[0] = ld(hr, c0); kc[1] = ld(mu, c0); }
         if (fbits64(ld(hr, c)) != fbits64(ld(hr, c0))) OCN_ATOMIC_OR(flag, 1);
         if (m < r.m0 - 1 || m > r.m1 + 1 || n < r.n0 - 1 || n > r.n1 + 1) return;   // the ring of r +- 2
         if (fbits64(ld(mu, c)) != fbits64(ld(mu, c0))) OCN_ATOMIC_OR(flag, 1);
         const unsigned bc = ld(bits, c);
-        const bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && n >= b.ny_start - 1 && n <= b.ny_end;
-        const bool in = m >= b.nx_start && m <= b.nx_end && n >= b.ny_start && n <= b.ny_end;
+        const bool owned = (own >> (own_class(m, b.nx_start, b.nx_end) * 3u + own_class(n, b.ny_start, b.ny_end))) & 1u;
+        const bool hh_rng = owned || (m >= b.nx_start - 1 && m <= b.nx_end && n >= b.ny_start - 1 && n <= b.ny_end);
+        const bool in = owned || (m >= b.nx_start && m <= b.nx_end && n >= b.ny_start && n <= b.ny_end);
         auto nz = [&](const double *p) { return fbits64(ld(p, c)) != 0; };
         bool bad = false;
         if (!(hh_rng && (bc & (1u << OCN_LLU)))) bad |= nz(hu) || nz(hu1);
@@ -1966,13 +1998,13 @@ struct FallbackCheck {
 };
 
 int launch_fallback_check(const ocn_block *b, void *const *ptr, const uint8_t *bits, const Range &r, int32_t *flag,
-                          hipStream_t s)
+                          double *kc, hipStream_t s, unsigned own)
 {
     RC_K(check_block(b));
     auto f = [&](int id) { return (const double *)ptr[ocn_field_slot(id)]; };
     const FallbackCheck k{*b, bits, f(OCN_HHU), f(OCN_HHU_P), f(OCN_HHV), f(OCN_HHV_P), f(OCN_HHH), f(OCN_VORT),
                           f(OCN_STR_T), f(OCN_STR_S), f(OCN_RHSX), f(OCN_RHSY), (int *)flag, r, f(OCN_HHQ_REST),
-                          f(OCN_MU)};
+                          f(OCN_MU), kc, own};
     const int m0 = max(r.m0 - 2, b->bnd_x1), m1 = min(r.m1 + 2, b->bnd_x2);
     const int n0 = max(r.n0 - 2, b->bnd_y1), n1 = min(r.n1 + 2, b->bnd_y2);
     if (m0 > m1 || n0 > n1) return OCN_OK;
@@ -1981,29 +2013,43 @@ int launch_fallback_check(const ocn_block *b, void *const *ptr, const uint8_t *b
 
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range, bool last, bool zero_fallback, double hr0, double mu0)
+                   const Range *range, bool last, const OnepassKC &kc, unsigned own)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
         return set_error(OCN_ERR_ARG, "one-pass step: compact tables, march, full_free_surface = 1, trans_terms and "
                                       "ksw_lat on, three second buffers");
+    if (kc.mode != OCN_KC_GENERAL && (!kc.kc || (kc.mode == OCN_KC_DEVICE && !kc.flag)))
+        return set_error(OCN_ERR_ARG, "one-pass step: known constants without their device words");
+    if (own && last) return set_error(OCN_ERR_ARG, "one-pass step over neighbour-owned halos: not a last step");
     RC_K(check_block(b));
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
     const Range r = range ? range_clip(range_interior(b), *range) : range_interior(b);
     if (range_empty(r)) return OCN_OK;
     int ex;
     const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
-#define OCN_STEP_LAUNCH(P, L, Z) \
-    return launch_step(b, r, MarchStep<P, L, Z>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out, hr0, mu0}, s)
-    if (zero_fallback) {
-        if (last) { if (p2) OCN_STEP_LAUNCH(true, true, true); OCN_STEP_LAUNCH(false, true, true); }
-        if (p2) OCN_STEP_LAUNCH(true, false, true);
-        OCN_STEP_LAUNCH(false, false, true);
+    // OCN_KC_DEVICE: the known-constant variant runs if the device check found its conditions, the
+    // general one otherwise (each launch's workgroups read the verdict and return at once if it
+    // is not theirs)
+    const int gz = kc.mode == OCN_KC_DEVICE ? 1 : 0, gg = kc.mode == OCN_KC_DEVICE ? 2 : 0;
+#define OCN_STEP_LAUNCH(P, L, Z, X, G)                                                                          \
+    RC_K(launch_step(b, r, MarchStep<P, L, Z, X>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out, kc.kc, kc.flag, G, \
+                                                 own}, s))
+#define OCN_STEP_VARIANT(Z, G)                                                                                   \
+    do {                                                                                                         \
+        if (own) { if (p2) OCN_STEP_LAUNCH(true, false, Z, true, G); else OCN_STEP_LAUNCH(false, false, Z, true, G); } \
+        else if (last) { if (p2) OCN_STEP_LAUNCH(true, true, Z, false, G); else OCN_STEP_LAUNCH(false, true, Z, false, G); } \
+        else if (p2) OCN_STEP_LAUNCH(true, false, Z, false, G);                                                    \
+        else OCN_STEP_LAUNCH(false, false, Z, false, G);                                                           \
+    } while (0)
+    if (kc.mode != OCN_KC_GENERAL) {
+        OCN_STEP_VARIANT(true, gz);
+        if (kc.mode == OCN_KC_KNOWN) return OCN_OK;
     }
-    if (last) { if (p2) OCN_STEP_LAUNCH(true, true, false); OCN_STEP_LAUNCH(false, true, false); }
-    if (p2) OCN_STEP_LAUNCH(true, false, false);
-    OCN_STEP_LAUNCH(false, false, false);
+    OCN_STEP_VARIANT(false, gg);
+#undef OCN_STEP_VARIANT
 #undef OCN_STEP_LAUNCH
+    return OCN_OK;
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy
@@ -2032,11 +2078,31 @@ int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, 
 
 size_t row_table_size(unsigned nrows) { return row_table_floats(nrows); }
 
-int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s)
+int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s,
+                   unsigned own)
 {
     RC_K(check_block(b));
     const Range r = range_bnd(b);
-    return launch_range(r.m0, r.m1, r.n0, r.n1, make_prepare(b, ptr, bits, rows, (int *)flags), s);
+    return launch_range(r.m0, r.m1, r.n0, r.n1, make_prepare(b, ptr, bits, rows, (int *)flags, own), s);
+}
+
+__global__ void k_rows_ext(float *rows_x, unsigned nrows, const float *ext, int *flags)
+{
+    const int i = (int)threadIdx.x;
+    if (i >= 2) return;
+    if (!write_table_row(rows_x, nrows, i == 0 ? 0u : nrows - 1u, ext + i * kNumRowFields))
+        atomicOr(flags, (int)OCN_COMPACT_DIVISOR_RANGE);
+}
+
+int launch_rows_ext(const ocn_block *b, const float *rows, float *rows_x, const float *ext, int32_t *flags,
+                    hipStream_t s)
+{
+    RC_K(check_block(b));
+    const unsigned nrows = block_rows(b);
+    if (hipMemcpyAsync(rows_x, rows, row_table_floats(nrows) * sizeof(float), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return set_error(OCN_ERR_HIP, "rows_ext: copy");
+    hipLaunchKernelGGL(k_rows_ext, dim3(1), dim3(64), 0, s, rows_x, nrows, ext, (int *)flags);
+    return check_launch();
 }
 
 }  // namespace ocn

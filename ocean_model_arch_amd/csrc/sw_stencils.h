@@ -773,7 +773,34 @@ OCN_HD inline unsigned recip_offset(unsigned nrows) { return ((unsigned)kRowTabl
 inline size_t row_table_floats(unsigned nrows) { return recip_offset(nrows) + 2u * (unsigned)kNumRecips * nrows; }
 enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2,
        OCN_COMPACT_RING_SEA = 4,     // not a failure: a8 / a9 write somewhere on the halo ring
-       OCN_COMPACT_DIVISOR_RANGE = 8 };   // not a failure: a divisor outside [2^-60, 2^60] (no one-pass step)
+       OCN_COMPACT_DIVISOR_RANGE = 8,     // not a failure: a divisor outside [2^-60, 2^60] (no one-pass step)
+       OCN_COMPACT_EDGE_RING_SEA = 16 };  // not a failure: ... on the ring of a side no neighbour block fills
+
+// Which halo points of a block a neighbour block owns (they are its interior points, filled by the
+// exchanges): bit (cx * 3 + cy) with cx = 0 / 1 / 2 for m < nx_start / inside / m > nx_end and cy
+// likewise for n -- the 8 directions' bits set where that neighbour exists (ocn_ctx.hip own_mask).
+OCN_HD inline unsigned own_class(int v, int lo, int hi) { return v < lo ? 0u : v > hi ? 2u : 1u; }
+
+// One row of the compact row table (rows, nrows: sw_stencils.h kRowTable, recip_offset) from the
+// row's metric values v[OCN_DX .. OCN_R_DISS]: the values, the stress ratios and the reciprocals,
+// formed exactly as Prepare forms them; false if a divisor is outside udiv's range.
+OCN_HD inline bool write_table_row(float *rows, unsigned nrows, unsigned r, const float *v)
+{
+    for (int k = 0; k < kNumRowFields; ++k) rows[(unsigned)k * nrows + r] = v[k];
+    const float dx = v[0], dy = v[OCN_DY - OCN_DX], dxb = v[OCN_DXB - OCN_DX], dyb = v[OCN_DYB - OCN_DX];
+    const float rat[kNumRowRatios] = {dy / dx, dx / dy, dxb / dyb, dyb / dxb};
+    for (int k = 0; k < kNumRowRatios; ++k) rows[(unsigned)(kNumRowFields + k) * nrows + r] = rat[k];
+    const float area = dx * dy;
+    const float g[kNumRecips] = {v[OCN_DXT - OCN_DX], v[OCN_DYH - OCN_DX], v[OCN_DXH - OCN_DX], v[OCN_DYT - OCN_DX],
+                                 dxb, dyb, area};
+    double *rc = (double *)(rows + recip_offset(nrows));
+    bool range = true;
+    for (int k = 0; k < kNumRecips; ++k) {
+        rc[(unsigned)k * nrows + r] = 1.0 / (double)g[k];
+        range &= g[k] >= 0x1p-60f && g[k] <= 0x1p60f;   // positive; false for NaN
+    }
+    return range;
+}
 
 // Thread grid = whole bnd range.  Mask bytes everywhere; row values from column nx_start-1
 // for the rows [ny_start-1, ny_end+1] the stencils read; every point of [nx_start-1,
@@ -785,6 +812,7 @@ struct Prepare {
     Geo I; int ms, me, ns, ne;
     const float *__restrict__ r4[OCN_NUM_R4];
     uint8_t *__restrict__ bits; float *__restrict__ rows; unsigned nrows; int *flags;
+    unsigned own;   // halo points neighbour blocks own (own_class bits): OCN_COMPACT_EDGE_RING_SEA tests the rest
     OCN_HD void operator()(int m, int n) const
     {
         const Pt q = I(m, n);
@@ -802,30 +830,20 @@ struct Prepare {
         // lu / llu / llv / luh
         const unsigned a8m = (1u << OCN_LU) | (1u << OCN_LCU) | (1u << OCN_LCV);
         const unsigned a9m = (1u << OCN_LU) | (1u << OCN_LLU) | (1u << OCN_LLV) | (1u << OCN_LUH);
-        if (((m == ms || m == me || n == ns || n == ne) && (b & a8m)) || ((m == me || n == ne) && (b & a9m)))
+        if (((m == ms || m == me || n == ns || n == ne) && (b & a8m)) || ((m == me || n == ne) && (b & a9m))) {
             OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_RING_SEA);
+            const unsigned cls = own_class(m, ms + 1, me - 1) * 3u + own_class(n, ns + 1, ne - 1);
+            if (!((own >> cls) & 1u)) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_EDGE_RING_SEA);
+        }
         const Pt q0 = I(ms, n);
         bool vary = false;
+        float v[kNumRowFields];
         for (int k = 0; k < kNumRowFields; ++k) {
-            const float v = ld(r4[OCN_DX + k], q);
-            vary |= fbits(v) != fbits(ld(r4[OCN_DX + k], q0));
-            if (m == ms) st(rows, (unsigned)k * nrows + q.r, v);
+            v[k] = ld(r4[OCN_DX + k], q);
+            vary |= fbits(v[k]) != fbits(ld(r4[OCN_DX + k], q0));
         }
-        if (m == ms) {   // the same real(4) divisions as stress_components_math on these row values
-            const float dx = ld(r4[OCN_DX], q), dy = ld(r4[OCN_DY], q), dxb = ld(r4[OCN_DXB], q), dyb = ld(r4[OCN_DYB], q);
-            const float rat[kNumRowRatios] = {dy / dx, dx / dy, dxb / dyb, dyb / dxb};
-            for (int k = 0; k < kNumRowRatios; ++k) st(rows, (unsigned)(kNumRowFields + k) * nrows + q.r, rat[k]);
-            const float area = dx * dy;
-            const float g[kNumRecips] = {ld(r4[OCN_DXT], q), ld(r4[OCN_DYH], q), ld(r4[OCN_DXH], q), ld(r4[OCN_DYT], q),
-                                         dxb, dyb, area};
-            double *rc = (double *)(rows + recip_offset(nrows));
-            bool range = true;
-            for (int k = 0; k < kNumRecips; ++k) {
-                st(rc, (unsigned)k * nrows + q.r, 1.0 / (double)g[k]);
-                range &= g[k] >= 0x1p-60f && g[k] <= 0x1p60f;   // positive; false for NaN
-            }
-            if (!range) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_DIVISOR_RANGE);
-        }
+        // the row values, and the same real(4) divisions as stress_components_math on them
+        if (m == ms && !write_table_row(rows, nrows, q.r, v)) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_DIVISOR_RANGE);
         if (vary) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_METRIC_NOT_ROW_CONSTANT);
     }
 };
@@ -942,10 +960,11 @@ inline Coherence make_coherence(const ocn_block *b, void *const *ptr, const uint
     return k;
 }
 
-inline Prepare make_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int *flags)
+inline Prepare make_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int *flags,
+                            unsigned own = 0)
 {
     Prepare k{geo(b), b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, {}, bits, rows,
-              block_rows(b), flags};
+              block_rows(b), flags, own};
     for (int id = 0; id < OCN_NUM_R4; ++id) k.r4[id] = (const float *)ptr[ocn_field_slot(id)];
     return k;
 }

@@ -196,6 +196,26 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_KNOWN_CONSTANTS, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_lazy_tail(self, on: bool = True):
+        """Lazy call tail (default): in one process, one block without halo exchanges, a call whose
+        steps are one-pass steps leaves what the reference's last step stores beyond the next state
+        pending, so the next step() continues with one-pass steps (1-step calls run as fast as long
+        ones); complete(), or anything that looks at the fields, forms it first (same results bit
+        for bit)."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_LAZY_TAIL, int(on)), "ocn_ctx_set_option")
+        return self
+
+    @property
+    def tail_pending(self) -> bool:
+        """Whether the last step() left its call tail pending (OCN_OPT_LAZY_TAIL)."""
+        return self.option(_lib.OPT_LAZY_TAIL) == 2
+
+    def complete(self):
+        """Form a pending call tail now (ocn_ctx_complete): every array then holds what the
+        reference leaves after the last step run.  Asynchronous."""
+        check(lib().ocn_ctx_complete(self.ctx), "ocn_ctx_complete")
+        return self
+
     def option(self, key: int) -> int:
         v = C.c_int64(0)
         check(lib().ocn_ctx_get_option(self.ctx, key, C.byref(v)), "ocn_ctx_get_option")

@@ -14,7 +14,7 @@ HEADER = os.path.join(REPO, "include", "ocn_sw.h")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(?:int|void\s*\*|const\s+char\s*\*)\s*(ocn_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(?:int|int64_t|void\s*\*|const\s+char\s*\*)\s*(ocn_\w+)\s*\(", src)))
 
 
 @pytest.fixture(scope="module")
@@ -87,7 +87,7 @@ def test_field_ids_match_header():
 
 def test_abi_version_and_loud_failure_without_device(lib):
     import ocean_model_arch_amd as amd
-    assert lib.ocn_abi_version() == 3
+    assert lib.ocn_abi_version() == 4
     bid = amd.build_id()
     assert len(bid) == 16 and int(bid, 16) >= 0, bid   # Makefile: sha256 of sources + flags
     try:

@@ -25,14 +25,29 @@ def test_onepass_call_launches(steps):
 
 def test_step_bytes_orders():
     """Fewer bytes per step the further the fusion goes; the known-constant variant reads less."""
-    std = bench.step_bytes(True, 20, flip=False)
-    flip = bench.step_bytes(True, 20, flip=True)
-    one = bench.step_bytes(True, 20, flip=True, one=True)
-    onez = bench.step_bytes(True, 20, flip=True, one=True, zero=True)
+    std = bench.step_bytes(True, [20], flip=False)
+    flip = bench.step_bytes(True, [20], flip=True)
+    one = bench.step_bytes(True, [20], flip=True, one=True)
+    onez = bench.step_bytes(True, [20], flip=True, one=True, zero=True)
     assert std > flip > one > onez
     assert round(one, 2) == 140.25 and round(onez, 2) == 108.25
-    assert bench.step_bytes(True, 20, flip=True, one=True, tracers=1) == bench.step_bytes(True, 20, flip=True,
-                                                                                           tracers=1)
+    assert bench.step_bytes(True, [20], flip=True, one=True, tracers=1) == bench.step_bytes(True, [20], flip=True,
+                                                                                             tracers=1)
+
+
+def test_lazy_region_launches():
+    """An open one-pass sequence (OCN_OPT_LAZY_TAIL): one launch per step whatever the call length,
+    and the tail once at the end of the region; 100 steps in 1-step calls move what one 100-step
+    call moves plus the one step the tail runs again."""
+    one = bench.region_launches([1] * 100, flip=True, one=True, zero=True, lazy=True)
+    assert [k for _, k in one[:100]] == ["onepass_z"] * 100
+    assert [k for _, k in one[100:]] == ["onepass_last_z", "copy3", "c2_full"]
+    lazy = bench.step_bytes(True, [1] * 100, flip=True, one=True, zero=True, lazy=True)
+    whole = bench.step_bytes(True, [100], flip=True, one=True, zero=True)
+    assert lazy == bench.step_bytes(True, [100], flip=True, one=True, zero=True, lazy=True)
+    assert abs(lazy - whole - 97 / 100) < 1e-9
+    per_call = bench.step_bytes(True, [1] * 100, flip=False)
+    assert per_call > 3 * lazy
 
 
 class _Amd:

@@ -67,13 +67,18 @@ def test_fortran_host_builds():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,mode", [("box70x54_b3x2_s20", "psy"), ("bs_b4x2_s60", "psy"),
+@pytest.mark.parametrize("name,mode", [("box70x54_b3x2_s20", "stages"), ("bs_b4x2_s60", "stages"),
                                        ("box48x40_flags000_s10", "native"), ("bs_b1x1_s60", "native"),
-                                       ("box40x32_tr2_s5", "psy"), ("bs_b4x2_tr_s60", "native")])
+                                       ("box40x32_tr2_s5", "stages"), ("bs_b4x2_tr_s60", "native"),
+                                       ("box70x54_b1x1_s20", "psy"), ("box70x54_b3x2_tr_s20", "psy"),
+                                       ("bs_b1x1_s604", "psy")])
 def test_fortran_host_matches_reference(tmp_path, name, mode):
+    """stages = the reference's envoke stages over the kernel-layer entries; psy = the same PSy
+    time loop (one expl_shallow_water per step, model.f90:146) in its fused form, one
+    ocn_ctx_step(ctx, tau, 1) per step; native = one ocn_ctx_step call for the whole run."""
     case = cases.load_e2e(name)
     write_case(str(tmp_path), case)
-    args = [DRIVER, str(case["steps"]), "dump.bin"] + (["native"] if mode == "native" else [])
+    args = [DRIVER, str(case["steps"]), "dump.bin"] + ([mode] if mode != "psy" else [])
     r = subprocess.run(args, cwd=tmp_path, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     z = case["z"]

@@ -187,20 +187,57 @@ def test_end_to_end_matches_reference(amd, name, mode):
         assert one_used, f"{name}: one-pass steps not used"
 
 
+@pytest.mark.parametrize("calls", ["7,1,12", "1x20"])
 @pytest.mark.parametrize("graph", [False, True], ids=["stream", "graph"])
 @pytest.mark.parametrize("name", ["box70x54_b3x2_s20", "box70x54_b1x1_s20"])
-def test_split_step_calls_match_reference(amd, graph, name):
-    """The run split over several ocn_ctx_step calls (each call's last step writes hh_init's
-    time-invariant levels; on one block the role-flip steps' swaps are undone at each call's
-    end): same final state as one call and as the reference."""
+def test_split_step_calls_match_reference(amd, graph, name, calls):
+    """The run split over several ocn_ctx_step calls -- down to the reference's own cadence of one
+    expl_shallow_water per call (model.f90:146): same final state as one call and as the
+    reference.  One block: every call after the first continues the one-pass sequence and leaves
+    its tail pending (OCN_OPT_LAZY_TAIL), formed when the fields are read."""
     case = cases.load_e2e(name)
     m = build_model(amd, case, graph=graph).init()
-    for n in (7, 1, 12):
+    split = [7, 1, 12] if calls == "7,1,12" else [1] * 20
+    pend = []
+    for n in split:
         m.step(n, tau=1.0, check_every=0)
+        pend.append(m.tail_pending)
     m.synchronize()
     bad = compare_case(m, case, name)
+    pending_after = m.tail_pending
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
+    assert not pending_after   # the downloads formed the tail
+    if "_b1x1_" in name:
+        assert all(pend), pend
+    else:
+        assert not any(pend), pend   # exchanges: every call forms its own tail
+
+
+def test_lazy_tail_interleaved_with_reads(amd):
+    """1-step calls on one block with the fields read (tail formed) after some of them and a
+    field written in between: every read sees the reference's state of that step, and the run
+    ends bitwise equal to the one-call run with the same upload."""
+    case = cases.load_e2e("box70x54_b1x1_s20")
+    a = build_model(amd, case).init()
+    b = build_model(amd, case).init()
+    b.set_lazy_tail(False)
+    for s in range(1, 13):
+        a.step(1, check_every=1)
+        b.step(1, check_every=1)
+        if s in (3, 4, 9):
+            for nm in ("ssh", "vort", "str_t", "hhu", "hhq", "sshp", "ubrtrp"):
+                assert bits_equal(a.download(0, nm), b.download(0, nm)), (s, nm)
+        if s == 6:   # a forcing change between steps (the known-constant check must see it)
+            r = np.zeros(a.blocks[0].shape)
+            r[10:20, 10:20] = 1.0e-7
+            a.upload(0, "RHSx", r)
+            b.upload(0, "RHSx", r)
+    a.synchronize(); b.synchronize()
+    bad = [nm for nm in a.field_names if not bits_equal(a.download(0, nm), b.download(0, nm))]
+    assert a.onepass_active
+    a.close(); b.close()
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("what", ["metric", "mask"])
