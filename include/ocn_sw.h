@@ -264,6 +264,10 @@ int ocn_ctx_attach_comm(ocn_ctx *ctx, const void *unique_id, int32_t nbytes);
  * before ocn_ctx_init_state; the contexts may be destroyed in any order. */
 int ocn_ctx_attach_loopback(ocn_ctx *const *ctxs, int32_t n);
 
+/* Bottom topography (basin.par line 20, control/init_data.f90:111-121): the real(4) file's values,
+ * the (nx-4) x (ny-4) interior points in Fortran order (tools/io.f90:84-176 read_data2D_real4);
+ * h = NULL: none (100 m everywhere).  Used by the next ocn_ctx_init_state. */
+int ocn_ctx_set_topography(ocn_ctx *ctx, const float *h, int64_t count);
 /* Initial state: init_grid_data + init_ocean_data (control/init_data.f90:29-125). */
 int ocn_ctx_init_state(ocn_ctx *ctx);
 
@@ -339,14 +343,23 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_ONEPASS_LAST (default 1): with halo exchanges or a8 / a9 work on the halo ring, the
  *  call's last step as a one-pass step too (the inner march storing what the reference's last
  *  step leaves, then a8's copies and hh_init with every level); 0: a standard last step there.
- *  OCN_OPT_LAZY_TAIL (default 1): in one process, one block without halo exchanges, no tracers and
- *  no raw real(8) pointer handed out, a call whose steps are one-pass steps leaves its tail (what
+ *  OCN_OPT_LAZY_TAIL (default 1): in one process (one block without halo exchanges, or the blocks of
+ *  OCN_OPT_X2 steps), no tracers and no raw real(8) pointer handed out, a call whose steps are one-pass steps leaves its tail (what
  *  the reference's last step stores beyond the next state: vort, the stresses, the RHS terms,
  *  sw_next_step's copies, hh_init with every level) pending: the next ocn_ctx_step continues with
  *  one-pass steps -- so 1-step calls (the reference's own cadence, model.f90:146) run as fast as
  *  long ones -- and ocn_ctx_complete, or any entry that looks at the fields, forms it first (the
  *  last step run again from the previous state, which is still in the library's second buffers:
  *  the same results bit for bit).  ocn_ctx_get_option returns 2 while a tail is pending.
+ *  OCN_OPT_X2 (default 1): with halo exchanges (several blocks or ranks), the one-pass steps
+ *  exchange the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp) two points deep, once per step, and
+ *  form the depths, vort and stresses on the halo themselves, so the march covers the whole
+ *  interior (one exchange per step instead of two, no frame launches); needs the real(4) fields
+ *  from ocn_ctx_init_state, blocks of at least 2 x 2 points, no a8 / a9 work on a halo ring no
+ *  neighbour fills, and OCN_OPT_ONEPASS_LAST; the second halo ring, which the reference never
+ *  writes, is restored before the call's last step (same results bit for bit).  ocn_ctx_get_option:
+ *  whether the last ocn_ctx_step used such steps.  Lazy call tails (OCN_OPT_LAZY_TAIL) apply to them
+ *  too when the context exchanges only with blocks of its own process.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
  * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
@@ -356,7 +369,7 @@ int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9,
-       OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12 };
+       OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,

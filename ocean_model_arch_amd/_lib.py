@@ -79,6 +79,7 @@ OPT_ONEPASS = 9
 OPT_KNOWN_CONSTANTS = 10
 OPT_ONEPASS_LAST = 11
 OPT_LAZY_TAIL = 12
+OPT_X2 = 13
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",
@@ -87,7 +88,7 @@ KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "oc
                   "ocn_tran_diff_tracer", "ocn_tracer_next_step"]
 CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
                "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm", "ocn_ctx_attach_loopback",
-               "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
+               "ocn_ctx_set_topography", "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
                "ocn_ctx_download", "ocn_ctx_complete", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version",
                "ocn_build_id", "ocn_launch_count"]
 ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
@@ -184,6 +185,7 @@ def lib() -> C.CDLL:
                "ocn_ctx_complete"):
         getattr(L, nm).argtypes = [C.c_void_p]
     L.ocn_ctx_block_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(OcnBlockInfo)]
+    L.ocn_ctx_set_topography.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     L.ocn_ctx_sync.argtypes = [C.c_void_p, C.c_int]
     L.ocn_ctx_stage.argtypes = [C.c_void_p, C.c_int, C.c_double]
     L.ocn_ctx_tracer_stage.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double]

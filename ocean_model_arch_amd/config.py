@@ -38,19 +38,25 @@ class BasinConfig:
     rotation_on_lat: float = 0.0
     mask_file_name: str = "none"
     mask: np.ndarray | None = field(default=None, repr=False)   # int32 (nx, ny) Fortran order
+    topography_file_name: str = "none"
+    # bottom topography: float32 (nx-4, ny-4) interior points, Fortran order (None: 100 m everywhere)
+    topography: np.ndarray | None = field(default=None, repr=False)
 
     @classmethod
     def from_par(cls, path: str) -> "BasinConfig":
         c = _lexemes(path)
         cfg = cls(nx=int(c[0]), ny=int(c[1]), dxst=_real(c[5]), dyst=_real(c[6]), rlon=_real(c[7]),
                   rlat=_real(c[8]), curve_grid=int(c[11]), rotation_on_lon=_real(c[12]),
-                  rotation_on_lat=_real(c[13]), mask_file_name=c[18])
+                  rotation_on_lat=_real(c[13]), mask_file_name=c[18],
+                  topography_file_name=c[19] if len(c) > 19 and c[19] else "none")
         if int(c[9]) != 0 or int(c[10]) != 0:
             raise NotImplementedError("non-uniform (levels) grids: only xgr_type = ygr_type = 0 are supported")
         if cfg.curve_grid not in (0, 1):
             raise NotImplementedError("curve_grid = 2 (distorted sphere) is not supported")
         if cfg.mask_file_name != "none":
             cfg.mask = read_mask(cfg.mask_file_name, cfg.nx, cfg.ny)
+        if cfg.topography_file_name != "none":
+            cfg.topography = read_topography(cfg.topography_file_name, cfg.nx, cfg.ny)
         return cfg
 
 
@@ -98,6 +104,15 @@ def read_mask(path: str, nx: int, ny: int) -> np.ndarray:
     for r, ln in enumerate(lines[1:1 + ny]):
         m[:, ny - 1 - r] = [int(ch) for ch in ln[:nx]]
     return m
+
+
+def read_topography(path: str, nx: int, ny: int) -> np.ndarray:
+    """tools/io.f90:84-176 read_data2D_real4 (record 1): a raw real(4) file of the (nx-4) x (ny-4)
+    interior points (nxb = mmm = 3 .. nxe = mm = nx-2), Fortran order, native byte order."""
+    a = np.fromfile(path, dtype=np.float32, count=(nx - 4) * (ny - 4))
+    if a.size != (nx - 4) * (ny - 4):
+        raise ValueError(f"{path}: {a.size} values, (nx-4)*(ny-4) = {(nx - 4) * (ny - 4)} expected")
+    return a.reshape((nx - 4, ny - 4), order="F")
 
 
 def box_config(n: int, **kw) -> BasinConfig:

@@ -95,6 +95,23 @@ __global__ __launch_bounds__(kSegChunk) void k_segments_cmp(const Seg *__restric
     if (x != y) atomicOr(flags, 1);
 }
 
+// init_grid_data's bottom topography (control/init_data.f90:115-120): read_data2D_real4 fills the
+// block's interior from the file (tools/io.f90:130-147; the file holds the (nx-4) x (ny-4) interior,
+// Fortran order) and zeroes every point with |lu| < 0.5 (:158-171), the rest of the zero-initialised
+// array stays 0, then copy_from_real4 promotes it (core/data_types.f90:638-652); the sync follows.
+__global__ void k_topography(ocn_block g, double *h, const float *lu, const float *topo, int nxi)
+{
+    const int w = g.bnd_x2 - g.bnd_x1 + 1, rows = g.bnd_y2 - g.bnd_y1 + 1;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)w * rows) return;
+    const int m = g.bnd_x1 + (int)(i % w), n = g.bnd_y1 + (int)(i / w);
+    const long at = (long)(m - g.bnd_x1) + (long)(n - g.bnd_y1) * g.pitch;
+    float v = 0.0f;
+    if (m >= g.nx_start && m <= g.nx_end && n >= g.ny_start && n <= g.ny_end) v = topo[(long)(m - 3) + (long)(n - 3) * nxi];
+    if (fabsf(lu[at]) < 0.5f) v = 0.0f;
+    h[at] = (double)v;
+}
+
 __global__ void k_fill_r8(double *p, long n, double v)
 {
     long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -151,6 +168,14 @@ struct LBlock {
     void *sshp_alt = nullptr;          // second sshp buffer of the recompute steps (one_step_fused)
     void *up_alt = nullptr, *vp_alt = nullptr;   // second ubrtrp / vbrtrp buffers of the one-pass steps
     double *kc = nullptr;              // device: h_r, mu of the one-pass step's known-constant variant
+    // one_step_x2 (one 2-deep state exchange per one-pass step, the march over the whole interior):
+    unsigned own = 0;                  // halo points neighbour blocks own (sw_stencils.h own_class bits)
+    float *ext = nullptr;              // metric values of rows bnd_y1 / bnd_y2 as the neighbours form them
+    float *rows_x = nullptr;           // the row table with those two rows (launch_rows_ext)
+    double *hr_x = nullptr;            // h_r with its second halo ring from the neighbours
+    double *ring2 = nullptr;           // the state's second halo ring as the reference leaves it (saved)
+    Seg *d_save = nullptr, *d_restore = nullptr;   // its save / restore runs (k_segments)
+    int n_save = 0, n_restore = 0, ch_ring2 = 1;
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
@@ -202,13 +227,18 @@ namespace ocn {
 // one (this step's hh_init + A launch then does not store hhq on the interior, hhu_p, hhv_p).
 // one = one-pass step (sw_kernels.hip MarchStep), next_one = the next step is one (this step
 // then runs no hh_init: the one-pass step forms hh_init's values itself).
+// x2 = the one-pass step as one_step_x2 (2-deep state exchange, whole-interior march); x2_save = the
+// first of a sequence (the reference's second halo ring of the state is saved first); x2_end = a
+// last step after such a sequence (that ring restored and the state's first ring exchanged first).
 struct StepKind {
     bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next, one, next_one, one_last;
+    bool x2, x2_save, x2_end;
     bool operator==(const StepKind &o) const
     {
         return check == o.check && first == o.first && last == o.last && flip == o.flip && a_done == o.a_done &&
                next_a == o.next_a && next_reuse == o.next_reuse && rc == o.rc && rc_next == o.rc_next &&
-               one == o.one && next_one == o.next_one && one_last == o.one_last;
+               one == o.one && next_one == o.next_one && one_last == o.one_last && x2 == o.x2 &&
+               x2_save == o.x2_save && x2_end == o.x2_end;
     }
 };
 
@@ -225,6 +255,7 @@ struct ocn_ctx {
     ocn_sw_params sw;
     ocn_decomp dec;
     std::vector<int32_t> mask;         // global (nx, ny) column-major
+    std::vector<float> topo;           // bottom topography, (nx-4) x (ny-4) interior points (empty: none)
     int bnx = 1, bny = 1;
     std::vector<GBlock> gblocks;       // (bm-1) + (bn-1)*bnx
     std::vector<LBlock> blocks;
@@ -293,8 +324,18 @@ struct ocn_ctx {
     // last step leaves beyond the state (vort, stresses, RHS terms, hh_init's levels, a8's copies) is
     // formed when the host next looks (complete_open: the step redone from the previous state, still
     // intact in the other buffers, as the call's last step), so 1-step calls run one-pass steps
-    bool lazy = true, open = false;
+    bool lazy = true, open = false, open_x2 = false;
     double open_tau = 0.0;
+    // one_step_x2 (OCN_OPT_X2): its static conditions (ext_ok: the real(4) fields are init_state's,
+    // so the ext rows are the neighbours' metric rows; rows_x_ok: their divisors in udiv's range;
+    // edge_ring_sea: a8 / a9 work on a halo ring no neighbour fills), the device checks of the last
+    // check_coherence (x2_dev_ok: the state's first halo ring holds the neighbours' values and its
+    // halo points no exchange fills hold +0.0), whether the h_r copy is current, and whether the
+    // state's second halo ring is saved (a sequence of x2 steps is under way)
+    bool x2 = true, rows_x_ok = false, edge_ring_sea = true, x2_dev_ok = false;
+    mutable bool ext_ok = false, hrx_ok = false;
+    bool ring2_saved = false, x2_used = false;
+    bool fb_x2 = false;          // the known-constant check's verdict is for the x2 range / tables
     mutable bool coherent_known = false, r8_escaped = false;
     int role = 0;
     int steps_run = 0;           // launches statistics of the last call (ocn_ctx_get_option OCN_OPT_LAUNCHES)
@@ -405,6 +446,8 @@ static int decompose(ocn_ctx *c)
                 lb.nbr_k[d - 1] = c->gblocks[ng].k;
                 lb.nbr_gid[d - 1] = c->gblocks[ng].rank >= 0 ? ng : -1;
             }
+            if (lb.nbr_rank[d - 1] >= 0)   // own_class(m) * 3 + own_class(n) of direction d's halo points
+                lb.own |= 1u << ((unsigned)(kDirDm[d] + 1) * 3u + (unsigned)(kDirDn[d] + 1));
         }
         c->blocks.push_back(lb);
     }
@@ -412,6 +455,67 @@ static int decompose(ocn_ctx *c)
 }
 
 // ------------------------------------------------------------------ storage
+// The state arrays of the one-pass step as groups of physical buffers that agree on the second
+// halo ring (the reference never writes it; the pairs are coherent, the second buffers copies):
+// the field's own buffer first.
+static const int kStateIds[6] = {OCN_SSH, OCN_SSHP, OCN_UBRTR, OCN_UBRTRP, OCN_VBRTR, OCN_VBRTRP};
+static void state_group(const LBlock &b, int g, void *out[2])
+{
+    const int id = kStateIds[g];
+    out[0] = b.ptr[field_slot(id)];
+    switch (id) {
+    case OCN_SSH: out[1] = b.ptr[field_slot(OCN_SSHN)]; break;
+    case OCN_UBRTR: out[1] = b.ptr[field_slot(OCN_UBRTRN)]; break;
+    case OCN_VBRTR: out[1] = b.ptr[field_slot(OCN_VBRTRN)]; break;
+    case OCN_SSHP: out[1] = b.sshp_alt; break;
+    case OCN_UBRTRP: out[1] = b.up_alt; break;
+    default: out[1] = b.vp_alt; break;
+    }
+}
+
+// one_step_x2's per-block storage: the ext metric rows, the row table with them, the h_r copy, the
+// save area of the state's second halo ring and the runs that save / restore it (pointers of the
+// physical buffers: role independent)
+static int allocate_x2(ocn_ctx *c, LBlock &b)
+{
+    const int w = b.g.bnd_x2 - b.g.bnd_x1 + 1, h = b.g.bnd_y2 - b.g.bnd_y1 + 1;
+    const size_t nrow = row_table_size((unsigned)h);
+    HIPCHK(hipMalloc(&b.ext, kExtRowFloats * sizeof(float)));
+    c->allocs.push_back(b.ext);
+    HIPCHK(hipMalloc(&b.rows_x, nrow * sizeof(float)));
+    c->allocs.push_back(b.rows_x);
+    HIPCHK(hipMalloc(&b.hr_x, (size_t)b.g.pitch * h * sizeof(double)));
+    c->allocs.push_back(b.hr_x);
+    const long per = 2L * w + 2L * (h - 2);   // rows bnd_y1, bnd_y2; columns bnd_x1, bnd_x2 between them
+    HIPCHK(hipMalloc(&b.ring2, sizeof(double) * (size_t)(6 * per)));
+    c->allocs.push_back(b.ring2);
+    std::vector<Seg> save, restore;
+    const long p = (long)b.g.pitch;
+    for (int g = 0; g < 6; ++g) {
+        void *buf[2];
+        state_group(b, g, buf);
+        double *area = b.ring2 + g * per;
+        // (offset in the array, stride, count, offset in the area)
+        const long runs[4][4] = {{0, 1, w, 0}, {(long)(h - 1) * p, 1, w, w}, {p, p, h - 2, 2L * w},
+                                 {p + w - 1, p, h - 2, 2L * w + h - 2}};
+        for (const auto &r : runs) {
+            if (r[2] <= 0) continue;
+            save.push_back(Seg{(const double *)buf[0] + r[0], area + r[3], r[1], 1, (int)r[2]});
+            for (void *q : buf) restore.push_back(Seg{area + r[3], (double *)q + r[0], 1, r[1], (int)r[2]});
+        }
+    }
+    b.ch_ring2 = (std::max(w, h) + kSegChunk - 1) / kSegChunk;
+    b.n_save = (int)save.size();
+    b.n_restore = (int)restore.size();
+    HIPCHK(hipMalloc(&b.d_save, sizeof(Seg) * save.size()));
+    c->allocs.push_back(b.d_save);
+    HIPCHK(hipMalloc(&b.d_restore, sizeof(Seg) * restore.size()));
+    c->allocs.push_back(b.d_restore);
+    HIPCHK(hipMemcpy(b.d_save, save.data(), sizeof(Seg) * save.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b.d_restore, restore.data(), sizeof(Seg) * restore.size(), hipMemcpyHostToDevice));
+    return OCN_OK;
+}
+
 static int allocate(ocn_ctx *c)
 {
     for (LBlock &b : c->blocks) {
@@ -461,6 +565,7 @@ static int allocate(ocn_ctx *c)
         c->allocs.push_back(b.bits);
         HIPCHK(hipMalloc(&b.rows, nrow * sizeof(float)));
         c->allocs.push_back(b.rows);
+        RC(allocate_x2(c, b));
     }
     // d_nbad words: 0 check_ssh_err's count, 16 the fallback check's verdict (d_fbz), 32..47 flags and
     // the vote (d_flags), 48..63 the loopback vote's reduction; then per block h_r, mu (LBlock::kc)
@@ -1051,14 +1156,19 @@ static int prepare_static(ocn_ctx *c)
 {
     if (!c->compact_req || c->r4_escaped) { c->compact = false; return OCN_OK; }
     if (!c->static_dirty) return OCN_OK;
-    HIPCHK(hipMemsetAsync(c->d_flags, 0, sizeof(int32_t), c->stream));
-    for (const LBlock &b : c->blocks) RC(launch_prepare(&b.g, b.ptr.data(), b.bits, b.rows, c->d_flags, c->stream));
-    int32_t flags = 0;
-    HIPCHK(hipMemcpyAsync(&flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_flags, 0, 2 * sizeof(int32_t), c->stream));
+    for (const LBlock &b : c->blocks)
+        RC(launch_prepare(&b.g, b.ptr.data(), b.bits, b.rows, c->d_flags, c->stream, b.own));
+    if (c->ext_ok)   // one_step_x2's row tables: the ext rows' divisor range into the second word
+        for (const LBlock &b : c->blocks) RC(launch_rows_ext(&b.g, b.rows, b.rows_x, b.ext, c->d_flags + 1, c->stream));
+    int32_t flags[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    c->ring_sea = (flags & kCompactRingSea) != 0;
-    c->udiv_ok = (flags & kCompactDivisorRange) == 0;
-    c->compact = (flags & ~(kCompactRingSea | kCompactDivisorRange)) == 0;
+    c->ring_sea = (flags[0] & kCompactRingSea) != 0;
+    c->edge_ring_sea = (flags[0] & kCompactEdgeRingSea) != 0;
+    c->udiv_ok = (flags[0] & kCompactDivisorRange) == 0;
+    c->rows_x_ok = c->ext_ok && flags[1] == 0;
+    c->compact = (flags[0] & ~(kCompactRingSea | kCompactDivisorRange | kCompactEdgeRingSea)) == 0;
     c->static_dirty = false;
     return OCN_OK;
 }
@@ -1152,6 +1262,62 @@ enum { kVoteIncoherent = 0, kVoteIneligible, kVoteUdiv, kVoteHhStale, kVoteX2, k
 static_assert(kVoteUsed <= kVoteWords, "vote words");
 struct VoteIn { bool eligible, udiv_ok, hh_consistent, x2_ok; };
 struct VoteOut { bool udiv_ok, hh_consistent, x2_ok; };
+
+// one_step_x2's condition on the state's halo points that no exchange fills (the rings 1 and 2 of a
+// side, or corner, without a neighbour block): +0.0 in the six state arrays.  The reference never
+// writes them (no a8 / a9 work on such a ring: ocn_ctx::edge_ring_sea) and init leaves +0.0 there;
+// a neighbour's D formed next to such a point reads the neighbour's own copy of it, which then
+// holds +0.0 as well (every rank checks and the verdicts are reduced).  ORs 1 into *flag otherwise.
+// The same at the points of the outer halo ring (nx_end + 1, ny_end + 1) no neighbour fills for the
+// nine depth arrays of hh_shift's u / v / h triples (a9's own arrays there: hh_init and hh_update
+// stop at nx_end / ny_end): +0.0 makes a9 there an exact no-op (0 + ts (0 - 0 + 0) / 2 = +0), which
+// the x2 steps then skip; the hybrid last step runs it as the reference does.
+struct HaloZero {
+    const double *a[6], *d[9];
+    int w, h, nxs, nxe, nys, nye, bx1, by1;
+    long pitch;
+    unsigned own;
+};
+__global__ void k_halo_zero(HaloZero q, int32_t *flag)
+{
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)q.w * q.h) return;
+    const int m = q.bx1 + (int)(i % q.w), n = q.by1 + (int)(i / q.w);
+    const unsigned cx = m < q.nxs ? 0u : m > q.nxe ? 2u : 1u, cy = n < q.nys ? 0u : n > q.nye ? 2u : 1u;
+    if ((cx == 1u && cy == 1u) || ((q.own >> (cx * 3u + cy)) & 1u)) return;   // interior, or a neighbour's
+    const long at = (i % q.w) + (i / q.w) * q.pitch;
+    auto nz = [&](const double *p) {
+        unsigned long long x;
+        const double v = p[at];
+        __builtin_memcpy(&x, &v, 8);
+        return x != 0ull;
+    };
+    bool bad = false;
+    for (int k = 0; k < 6; ++k) bad |= nz(q.a[k]);
+    const bool outer = (m == q.nxe + 1 && n >= q.nys - 1 && n <= q.nye + 1) ||
+                       (n == q.nye + 1 && m >= q.nxs - 1 && m <= q.nxe + 1);
+    if (outer)
+        for (int k = 0; k < 9; ++k) bad |= nz(q.d[k]);
+    if (bad) atomicOr(flag, 1);
+}
+static int launch_halo_zero(ocn_ctx *c, int32_t *flag)
+{
+    static const int ids[6] = {OCN_SSH, OCN_SSHP, OCN_UBRTR, OCN_UBRTRP, OCN_VBRTR, OCN_VBRTRP};
+    static const int dids[9] = {OCN_HHU, OCN_HHU_P, OCN_HHU_N, OCN_HHV, OCN_HHV_P, OCN_HHV_N, OCN_HHH, OCN_HHH_P, OCN_HHH_N};
+    for (const LBlock &b : c->blocks) {
+        HaloZero q{};
+        for (int k = 0; k < 6; ++k) q.a[k] = b.f<double>(ids[k]);
+        for (int k = 0; k < 9; ++k) q.d[k] = b.f<double>(dids[k]);
+        q.w = b.g.bnd_x2 - b.g.bnd_x1 + 1; q.h = b.g.bnd_y2 - b.g.bnd_y1 + 1;
+        q.nxs = b.g.nx_start; q.nxe = b.g.nx_end; q.nys = b.g.ny_start; q.nye = b.g.ny_end;
+        q.bx1 = b.g.bnd_x1; q.by1 = b.g.bnd_y1; q.pitch = (long)b.g.pitch; q.own = b.own;
+        const long pts = (long)q.w * q.h;
+        hipLaunchKernelGGL(k_halo_zero, dim3((unsigned)((pts + 255) / 256)), dim3(256), 0, c->stream, q, flag);
+        RC(check_launch());
+    }
+    return OCN_OK;
+}
+
 static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
 {
     int32_t host[kVoteWords] = {0};
@@ -1164,6 +1330,10 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
         for (const LBlock &b : c->blocks) RC(launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream));
     const bool exch = has_exchange(c);
     if (exch) RC(run_sync(c, kHaloCheck, c->stream, c->d_flags));
+    if (exch && c->x2) {   // one_step_x2: the rest of the state's first halo ring, and the unexchanged halos
+        RC(run_sync(c, {OCN_SSHP, OCN_UBRTRP, OCN_VBRTRP}, c->stream, c->d_flags + kVoteX2));
+        RC(launch_halo_zero(c, c->d_flags + kVoteX2));
+    }
     RC(allreduce_max(c, c->d_flags, c->stream, kVoteUsed));
     int32_t w[kVoteWords] = {0};
     HIPCHK(hipMemcpyAsync(w, c->d_flags, sizeof(int32_t) * kVoteUsed, hipMemcpyDeviceToHost, c->stream));
@@ -1172,7 +1342,8 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
     c->coherent_known = !c->r8_escaped && !has_comm(c);
     out.udiv_ok = w[kVoteUdiv] == 0;
     out.hh_consistent = w[kVoteHhStale] == 0;
-    out.x2_ok = w[kVoteX2] == 0;
+    out.x2_ok = w[kVoteX2] == 0 && exch && c->x2;
+    c->x2_dev_ok = out.x2_ok;
     return OCN_OK;
 }
 
@@ -1405,8 +1576,146 @@ static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
     return OCN_OK;
 }
 
+// ------------------------------------------------------------------ one-pass steps with one exchange
+// With halo exchanges the reference holds D (hh_init's depths, vort, the stresses) at a halo as the
+// neighbour formed it on its interior, from the neighbour's state one point further out -- two
+// points into our halo.  one_step_x2 exchanges the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp)
+// two points deep once per step, so every block forms D on its halo itself (the same operands, the
+// same arithmetic: sw_kernels.hip MarchStep X2, with the metric rows of the second ring from
+// ext / rows_x and h_r's second ring from the h_r copy hr_x) and the one-pass march covers the whole
+// interior: no CA / B frame launches and one exchange per step instead of two.  The state's first
+// halo ring then holds the neighbours' values as the reference's a8 on the ring leaves it (checked
+// in check_coherence); its second ring, which the reference never writes, is saved when a sequence
+// of such steps starts and restored when it ends (x2_end, before the call's last step).
+static const std::vector<int> kStateX2 = {OCN_SSH, OCN_SSHP, OCN_UBRTR, OCN_UBRTRP, OCN_VBRTR, OCN_VBRTRP};
+
+static int ring2_run(ocn_ctx *c, bool save, hipStream_t s)
+{
+    for (const LBlock &b : c->blocks) {
+        const int n = save ? b.n_save : b.n_restore;
+        if (!n) continue;
+        hipLaunchKernelGGL(k_segments, dim3((unsigned)n, (unsigned)b.ch_ring2), dim3(kSegChunk), 0, s,
+                           save ? b.d_save : b.d_restore, n);
+        RC(check_launch());
+    }
+    return OCN_OK;
+}
+
+// the end of a sequence of x2 steps: the second ring as the reference leaves it, the first ring of
+// the current state exchanged (what the reference's exchanges and a8 on the ring leave there)
+static int x2_end(ocn_ctx *c, hipStream_t s)
+{
+    RC(ring2_run(c, false, s));
+    return run_sync(c, kStateX2, s);
+}
+
+// hr_x = h_r with the neighbours' second ring (the general variant of one_step_x2 reads it there)
+static int refresh_hrx(ocn_ctx *c)
+{
+    for (const LBlock &b : c->blocks)
+        HIPCHK(hipMemcpyAsync(b.hr_x, b.ptr[field_slot(OCN_HHQ_REST)], field_bytes(b), hipMemcpyDeviceToDevice,
+                              c->stream));
+    auto swap_hr = [c] {
+        for (LBlock &b : c->blocks) {
+            void *t = b.ptr[field_slot(OCN_HHQ_REST)];
+            b.ptr[field_slot(OCN_HHQ_REST)] = b.hr_x;
+            b.hr_x = (double *)t;
+        }
+    };
+    swap_hr();
+    const int rc = run_sync(c, {OCN_HHQ_REST}, c->stream, nullptr, 2, 1);
+    swap_hr();
+    RC(rc);
+    c->hrx_ok = true;
+    return OCN_OK;
+}
+
+// every plan one_step_x2 and x2_end use, for the pair / second-buffer roles a call passes through
+// (built before any graph capture)
+static int prebuild_x2(ocn_ctx *c)
+{
+    int rc = OCN_OK;
+    for (int i = 0; i < 4 && rc == OCN_OK; ++i) {
+        if (i & 1) swap_roles(c);
+        if (i & 2) swap_alt3(c);
+        HaloPlan *p;
+        rc = get_plan(c, kStateX2, p, 2);
+        if (rc == OCN_OK) rc = get_plan(c, kStateX2, p, 1);
+        if (i & 2) swap_alt3(c);
+        if (i & 1) swap_roles(c);
+    }
+    return rc;
+}
+
+// The part of the interior an x2 step computes without the exchange: the interior less 2 points
+// on every side a neighbour (diagonals included) fills halos of -- a point's stencil reaches the
+// state 2 points away (D at +-1, formed from the state at +-1).
+static Range x2_inner(const LBlock &b)
+{
+    auto any = [&](int a, int d1, int d2) { return b.nbr_rank[a - 1] >= 0 || b.nbr_rank[d1 - 1] >= 0 || b.nbr_rank[d2 - 1] >= 0; };
+    Range r{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
+    if (any(1, 5, 6)) r.m1 -= 2;   // E, NE, SE
+    if (any(2, 7, 8)) r.m0 += 2;   // W, NW, SW
+    if (any(3, 5, 7)) r.n1 -= 2;   // N, NE, NW
+    if (any(4, 6, 8)) r.n0 += 2;   // S, SE, SW
+    return r;
+}
+
+// One x2 step.  With OCN_OPT_OVERLAP 2 (the default when the context exchanges with other ranks;
+// not while capturing a graph): the inner part (x2_inner) on the compute stream beside the exchange
+// and then the frame bands on the comm stream (which runs at the device's highest priority) -- the
+// exchange's latency hides behind the inner march.  The two parts write disjoint points of the new
+// state (other buffers than the ones read), the exchange writes halos only the frame reads; the join
+// orders the next step after both.  With only local copies (one GPU) the exchange costs less than
+// the extra frame launch: one GPU, 4x2 blocks of 4096^2, 0.482 ms per step in sequence against
+// 0.521 overlapped; 2x2 of 2048^2 0.154 against 0.170.
+static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
+{
+    const ocn_sw_params &sw = c->sw;
+    hipStream_t s = c->stream;
+    ocn_ctx::Rec rec;
+    int32_t *nbad = k.check ? c->d_nbad : nullptr;
+    auto march = [&](const LBlock &b, hipStream_t st, const Range *range, const Range *frame_of) -> int {
+        std::vector<void *> tab = b.ptr;
+        tab[field_slot(OCN_HHQ_REST)] = b.hr_x;
+        const Compact t{b.bits, b.rows_x, c->march};
+        return launch_onepass(&b.g, tab.data(), (int)tab.size(), &t, sw, tau, nbad, (double *)b.sshp_alt,
+                              (double *)b.up_alt, (double *)b.vp_alt, st, range, false, kc_of(c, b), b.own, frame_of);
+    };
+    if (overlap_level(c) >= 2 && !c->capturing) {
+        HIPCHK(hipEventRecord(c->ev_fork, s));
+        RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+        for (const LBlock &b : c->blocks) {
+            const Range in = x2_inner(b);
+            RC(march(b, s, &in, nullptr));
+        }
+        RC(timer_end(c, rec));
+        HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
+        if (k.x2_save) RC(ring2_run(c, true, c->comm_stream));
+        RC(run_sync(c, kStateX2, c->comm_stream, nullptr, 2));   // the state two points deep
+        for (const LBlock &b : c->blocks) {
+            const Range in = x2_inner(b);
+            RC(march(b, c->comm_stream, nullptr, &in));
+        }
+        HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
+        c->sync_pending = true;
+        RC(join_sync(c));
+    } else {
+        if (k.x2_save) RC(ring2_run(c, true, s));
+        RC(run_sync(c, kStateX2, s, nullptr, 2));   // the state two points deep
+        RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
+        for (const LBlock &b : c->blocks) RC(march(b, s, nullptr, nullptr));
+        RC(timer_end(c, rec));
+    }
+    swap_alt3(c);
+    swap_roles(c);
+    return OCN_OK;
+}
+
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
+    if (k.x2) return one_step_x2(c, tau, k);
+    if (k.one_last && k.x2_end) RC(x2_end(c, c->stream));
     if (k.one_last) return has_exchange(c) || c->ring_sea ? one_step_hybrid(c, tau, k, true) : one_step_last(c, tau, k);
     const bool check = k.check, first = k.first, last = k.last, flip = k.flip;
     const ocn_sw_params &sw = c->sw;
@@ -1633,6 +1942,10 @@ static double dcosd(double x) { return std::cos((x / 180.0) * kDPi); }
 struct GridTables {
     std::vector<float> cos_t, cos_v;                   // (float) dcosd(lat_mod(yt)), of yv, per row
     std::vector<double> sin_v, cosy_v, cos_xu;         // dsind(yv), dcosd(yv) per row; dcosd(xu) per column
+    // the same factors of rows bnd_y1 and bnd_y2 (outside the metric range) from the global row
+    // formulas, as the neighbour blocks form them (GridInit ext)
+    float ext_ct[2], ext_cv[2];
+    double ext_sin_v[2], ext_cosy_v[2];
 };
 static void grid_tables(const ocn_ctx *c, const ocn_block &g, GridTables &t)
 {
@@ -1654,6 +1967,15 @@ static void grid_tables(const ocn_ctx *c, const ocn_block &g, GridTables &t)
         t.cosy_v[r] = dcosd(yv[r]);
     }
     for (int m = g.nx_start - 1; m <= g.nx_end + 1; ++m) t.cos_xu[m - g.bnd_x1] = dcosd(xu[m - g.bnd_x1]);
+    for (int i = 0; i < 2; ++i) {   // grid_base_init on the neighbour: yt(n), yv(n) = (yt(n) + yt(n + 1)) / 2
+        const int n = i == 0 ? g.bnd_y1 : g.bnd_y2;
+        const double yt_n = bs.rlat + (double)(n - nnn) * bs.dyst, yt_n1 = bs.rlat + (double)(n + 1 - nnn) * bs.dyst;
+        const double yv_n = (yt_n + yt_n1) / 2.0;
+        t.ext_ct[i] = (float)dcosd(lat_mod(yt_n));
+        t.ext_cv[i] = (float)dcosd(lat_mod(yv_n));
+        t.ext_sin_v[i] = dsind(yv_n);
+        t.ext_cosy_v[i] = dcosd(yv_n);
+    }
 }
 
 static int upload_field(ocn_ctx *c, const LBlock &b, int id, const void *host, bool async)
@@ -1676,7 +1998,8 @@ static int init_state(ocn_ctx *c)
     const size_t nxy = (size_t)bs.nx * bs.ny;
     // device scratch of this call: the basin mask, then per block its grid tables
     std::vector<GridTables> tabs(c->blocks.size());
-    size_t bytes = nxy * sizeof(int32_t);
+    const size_t topo_at = (nxy * sizeof(int32_t) + 255) / 256 * 256;
+    size_t bytes = topo_at + c->topo.size() * sizeof(float);
     std::vector<size_t> at(c->blocks.size());
     for (size_t i = 0; i < c->blocks.size(); ++i) {
         grid_tables(c, c->blocks[i].g, tabs[i]);
@@ -1687,6 +2010,8 @@ static int init_state(ocn_ctx *c)
     HIPCHK(hipMalloc(&scratch, bytes));
     struct Free { char *p; ~Free() { if (p) (void)hipFree(p); } } free_scratch{scratch};
     HIPCHK(hipMemcpy(scratch, c->mask.data(), nxy * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (!c->topo.empty())
+        HIPCHK(hipMemcpy(scratch + topo_at, c->topo.data(), c->topo.size() * sizeof(float), hipMemcpyHostToDevice));
     const float pip180 = kPi / 180.0f;
     for (size_t i = 0; i < c->blocks.size(); ++i) {
         const LBlock &b = c->blocks[i];
@@ -1714,11 +2039,24 @@ static int init_state(ocn_ctx *c)
         q.cor = 2.0f * kEarthAngVel;
         q.sqrt2 = std::sqrt(2.0f);
         q.curve = bs.curve_grid != 0;
+        for (int j = 0; j < 2; ++j) {
+            q.ext_ct[j] = t.ext_ct[j]; q.ext_cv[j] = t.ext_cv[j];
+            q.ext_sin_v[j] = t.ext_sin_v[j]; q.ext_cosy_v[j] = t.ext_cosy_v[j];
+        }
+        q.ext = b.ext;
         RC(launch_init_grid(q, c->stream));
         c->static_dirty = true;
-        RC(launch_fill_field(b.g, b.f<double>(OCN_HHQ_REST), 100.0, c->stream));   // init_data.f90:112-114
+        if (c->topo.empty()) {
+            RC(launch_fill_field(b.g, b.f<double>(OCN_HHQ_REST), 100.0, c->stream));   // init_data.f90:112-114
+        } else {
+            const long pts = (long)(b.g.bnd_x2 - b.g.bnd_x1 + 1) * (b.g.bnd_y2 - b.g.bnd_y1 + 1);
+            hipLaunchKernelGGL(k_topography, dim3((unsigned)((pts + 255) / 256)), dim3(256), 0, c->stream, b.g,
+                               b.f<double>(OCN_HHQ_REST), b.f<float>(OCN_LU), (const float *)(scratch + topo_at), bs.nx - 4);
+            RC(check_launch());
+        }
         RC(launch_gaussian(b.g, b.f<double>(OCN_SSH), b.f<float>(OCN_LU), bs.nx / 2, bs.ny / 2, 1.0, c->stream));
     }
+    if (!c->topo.empty()) RC(run_sync(c, {OCN_HHQ_REST}));   // init_data.f90:119
     RC(run_sync(c, {OCN_SSH}));                               // envoke_gaussian_elimination's sync
     for (const LBlock &b : c->blocks) {                       // sshn = ssh, sshp = ssh (whole arrays)
         const size_t bytes = (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1) * 8;
@@ -1761,6 +2099,8 @@ static int init_state(ocn_ctx *c)
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->initialized = true;
+    c->ext_ok = true;   // the real(4) fields are init_state's: the ext rows are the neighbours' metric rows
+    c->hrx_ok = false;
     return OCN_OK;
 }
 
@@ -1938,13 +2278,14 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
     }
     ocn_ctx *w = const_cast<ocn_ctx *>(c);
     if (complete_open(w) != OCN_OK) return nullptr;   // the arrays hold what the reference leaves
-    if (is_r4(id)) c->r4_escaped = true;   // may be written behind our back: no compact tables
+    if (is_r4(id)) { c->r4_escaped = true; c->ext_ok = false; }   // may be written behind our back: no compact tables
     // a raw r8 pointer names the field's own buffer from now on (step_impl returns the current
     // values there at the end of every call)
     if (!is_r4(id) && alt_home(w) != OCN_OK) return nullptr;
     if (is_flip_field(id)) { c->r8_escaped = true; c->coherent_known = false; }
     if (is_alt_field(id)) c->alt_ok = false;
-    if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_state = kFbUnchecked; }
+    if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_state = kFbUnchecked; c->hrx_ok = false; }
+    if (is_alt_field(id) || id == OCN_HHQ_REST) { c->r8_escaped = true; c->coherent_known = false; }
     return c->blocks[k].ptr[field_slot(id)];
 }
 
@@ -1998,6 +2339,16 @@ int ocn_ctx_attach_loopback(ocn_ctx *const *ctxs, int32_t n)
     return OCN_OK;
 }
 
+int ocn_ctx_set_topography(ocn_ctx *c, const float *h, int64_t count)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    if (!h) { c->topo.clear(); return OCN_OK; }
+    const int64_t n = (int64_t)(c->basin.nx - 4) * (c->basin.ny - 4);
+    if (count != n) return set_error(OCN_ERR_ARG, "topography: (nx-4)*(ny-4) values expected");
+    c->topo.assign(h, h + n);
+    return OCN_OK;
+}
+
 int ocn_ctx_init_state(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
@@ -2025,6 +2376,7 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
     c->coherent_known = false;
     c->hh_consistent = false;
     c->fb_state = kFbUnchecked;
+    if (field_id == OCN_HHQ_REST) c->hrx_ok = false;
     // the current buffer's halos change; the one-pass steps' second buffer must be copied again
     if (is_alt_field(field_id)) c->alt_ok = false;
     return run_sync(c, {field_id});
@@ -2130,14 +2482,24 @@ static void learn_fb(ocn_ctx *c)
 // time, so then always the general one (a check per call would cost a pass over 12 arrays);
 // unchecked: the check runs on the stream and both variants are launched (the device picks) --
 // no host wait inside a step.
-static int prepare_kc(ocn_ctx *c)
+// x2: for one_step_x2 (the whole interior; the halo points neighbours own are no fallback points;
+// h_r with the neighbours' second ring).  A verdict for that range also holds for the hybrid
+// steps' inner range (its points and their +-2 neighbourhood lie inside what it covered, with the
+// same values there), not the other way round.
+static int prepare_kc(ocn_ctx *c, bool x2 = false)
 {
     if (!c->known_const || c->r8_handed) { c->kc_mode = OCN_KC_GENERAL; return OCN_OK; }
+    if (c->fb_state != kFbUnchecked && x2 && !c->fb_x2) c->fb_state = kFbUnchecked;
     if (c->fb_state == kFbUnchecked) {
         HIPCHK(hipMemsetAsync(c->d_fbz, 0, sizeof(int32_t), c->stream));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fallback_check(&b.g, b.ptr.data(), b.bits, onepass_inner(b, 1), c->d_fbz, b.kc, c->stream));
+        for (const LBlock &b : c->blocks) {
+            std::vector<void *> tab = b.ptr;
+            if (x2) tab[field_slot(OCN_HHQ_REST)] = b.hr_x;
+            const Range r = x2 ? Range{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end} : onepass_inner(b, 1);
+            RC(launch_fallback_check(&b.g, tab.data(), b.bits, r, c->d_fbz, b.kc, c->stream, x2 ? b.own : 0u));
+        }
         c->fb_state = kFbDevice;
+        c->fb_x2 = x2;
     }
     c->kc_mode = c->fb_state == kFbZero ? OCN_KC_KNOWN : c->fb_state == kFbGeneral ? OCN_KC_GENERAL : OCN_KC_DEVICE;
     return OCN_OK;
@@ -2166,10 +2528,22 @@ static int finish_call(ocn_ctx *c, int rc)
 // exchanges), no raw r8 pointers handed out, no tracers (expl_tracer reads hh_init's arrays after
 // every step), and the one-pass step as one launch per block (no exchange, no a8 / a9 work on the
 // halo ring: the redone step must find the previous state intact).
-static bool lazy_allowed(const ocn_ctx *c)
+static bool lazy_allowed(const ocn_ctx *c, bool x2)
 {
-    return c->lazy && !has_comm(c) && !c->r8_handed && c->sw.use_tracers <= 0 && !c->ring_sea &&
-           !has_exchange(const_cast<ocn_ctx *>(c));
+    return c->lazy && !has_comm(c) && !c->r8_handed && c->sw.use_tracers <= 0 &&
+           (x2 || (!c->ring_sea && !has_exchange(const_cast<ocn_ctx *>(c))));
+}
+
+// one_step_x2's static conditions on this rank (the device checks come from check_coherence):
+// halo exchanges to do, the compact tables with the ext rows, no a8 / a9 work on a ring no neighbour
+// fills, every block of the grid at least 2 x 2 (its 2-deep strips lie in its interior)
+static bool x2_local(const ocn_ctx *c)
+{
+    if (!c->x2 || !c->compact || !c->rows_x_ok || c->edge_ring_sea || !has_exchange(const_cast<ocn_ctx *>(c)))
+        return false;
+    for (const GBlock &g : c->gblocks)
+        if (g.rank >= 0 && (g.g.nx_end - g.g.nx_start < 1 || g.g.ny_end - g.g.ny_start < 1)) return false;
+    return true;
 }
 
 // The pending tail of an open sequence: the last step run (a one-pass step) is run again from the
@@ -2186,7 +2560,9 @@ static int complete_open(ocn_ctx *c)
     swap_alt3(c);
     StepKind k{};
     k.last = k.one_last = true;
-    return finish_call(c, one_step_last(c, c->open_tau, k));
+    k.x2_end = c->ring2_saved;   // x2 steps: the second ring restored, the first exchanged (x2_end)
+    c->ring2_saved = false;
+    return finish_call(c, one_step_fused(c, c->open_tau, k));
 }
 
 static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
@@ -2197,16 +2573,17 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     if (nsteps == 0) return OCN_OK;
     const bool graph_ok = c->use_graph && !has_comm(c) && !c->stage_timing;   // RCCL / events stay outside graphs
     if (c->open) {
-        if (tau == c->open_tau && c->onepass && lazy_allowed(c)) {
+        if (tau == c->open_tau && c->onepass && lazy_allowed(c, c->open_x2)) {
             // the open sequence goes on: every step of this call is a one-pass step (the state and
             // the constants are what its last step left), and the tail stays pending; a device
             // verdict the host has read since selects one variant
-            RC(prepare_kc(c));
+            RC(prepare_kc(c, c->open_x2));
             int rc = OCN_OK;
             for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
                 StepKind k{};
                 k.check = check_every > 0 && (s % check_every == 0);
                 k.flip = k.one = k.next_one = k.a_done = true;
+                k.x2 = c->open_x2;
                 rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
             }
             if (rc) { c->open = false; return finish_call(c, rc); }
@@ -2217,15 +2594,17 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     if (c->fused) RC(prepare_static(c));
     // with RCCL every rank takes part in the decisions (check_coherence reduces the verdicts)
     const bool eligible = flip_eligible(c);
+    const bool x2_here = x2_local(c);
     // a lazy call is planned as the first nsteps steps of a call of nsteps + 1 (the last deferred)
-    const bool lazy_cand = eligible && c->onepass && lazy_allowed(c);
-    bool udiv_ok = c->udiv_ok, first_one = c->hh_consistent;
+    const bool lazy_cand = eligible && c->onepass && lazy_allowed(c, x2_here);
+    bool udiv_ok = c->udiv_ok, first_one = c->hh_consistent, x2_ok = x2_here && c->x2_dev_ok;
     int N = lazy_cand ? nsteps + 1 : nsteps;
     if (N >= 2 && (eligible || (has_comm(c) && c->flip)) && !c->coherent_known) {
         VoteOut v;
-        RC(check_coherence(c, VoteIn{eligible, c->udiv_ok, c->hh_consistent, true}, v));
+        RC(check_coherence(c, VoteIn{eligible, c->udiv_ok, c->hh_consistent, x2_here}, v));
         udiv_ok = v.udiv_ok;
         first_one = v.hh_consistent;
+        x2_ok = x2_here && v.x2_ok;
     }
     bool flip_call = false, ca = false, one_call = false;
     auto decide = [&](int n) {
@@ -2241,9 +2620,13 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
                    c->sw.ksw_lat > 0 && c->sw.use_tracers <= 0 && udiv_ok;
     };
     decide(N);
-    // the last step run is a one-pass step: the tail may wait
-    const bool lazy_end = lazy_cand && one_call && (nsteps >= 2 || first_one);
+    // one-pass steps with one 2-deep exchange each (one_step_x2) where there are exchanges
+    const bool x2_call = one_call && x2_ok && c->last_hybrid;   // (its sequences end in the hybrid last step)
+    // the last step run is a one-pass step (one launch per block, or an x2 step): the tail may wait
+    const bool lazy_end = lazy_cand && one_call && (nsteps >= 2 || first_one) &&
+                          (x2_call || (!c->ring_sea && !has_exchange(c)));
     if (!lazy_end && N != nsteps) decide(N = nsteps);
+    c->x2_used = x2_call && one_call;
     c->flip_used = flip_call;
     c->hh_consistent = false;   // until this call's last step has run
     // the last step as one march + hh_init too (single block, no exchange, no ring work)
@@ -2251,7 +2634,11 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     const bool last_one = one_call && ((c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) && !c->ring_sea) ||
                                        c->last_hybrid);
     c->one_used = one_call;
-    if (one_call) RC(prepare_kc(c));
+    if (x2_call && one_call) {
+        if (!c->hrx_ok || has_comm(c)) RC(refresh_hrx(c));   // (with RCCL: every rank, every call)
+        RC(prebuild_x2(c));
+    }
+    if (one_call) RC(prepare_kc(c, x2_call));
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;
     if (one_call && !c->alt_ok) {   // the second buffers start as copies (they agree outside a8's write set)
@@ -2286,11 +2673,17 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         k.next_reuse = k.next_a && s + 1 < N;
         k.rc = rc_call && k.flip && !k.first;
         k.rc_next = rc_call && s + 1 < N;
+        k.x2 = x2_call && k.one;
+        k.x2_save = k.x2 && !c->ring2_saved;
+        k.x2_end = k.one_last && c->ring2_saved;
+        if (k.x2_save) c->ring2_saved = true;
+        if (k.x2_end) c->ring2_saved = false;
         rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
     }
     if (lazy_end && rc == OCN_OK) {   // the pending tail: complete_open
         c->open = true;
         c->open_tau = tau;
+        c->open_x2 = x2_call;
         return OCN_OK;
     }
     return finish_call(c, rc);
@@ -2391,9 +2784,11 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     HIPCHK(hipSetDevice(c->dec.device));
     RC(complete_open(c));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (is_r4(id)) c->static_dirty = true;
-    if (is_flip_field(id)) c->coherent_known = false;
+    if (is_r4(id)) { c->static_dirty = true; c->ext_ok = false; }
+    // (the x2 checks also cover sshp / ubrtrp / vbrtrp and h_r: check_coherence)
+    if (is_flip_field(id) || is_alt_field(id) || id == OCN_HHQ_REST) c->coherent_known = false;
     if (is_alt_field(id)) c->alt_ok = false;
+    if (id == OCN_HHQ_REST) c->hrx_ok = false;
     c->hh_consistent = false;
     c->fb_state = kFbUnchecked;
     return upload_field(c, c->blocks[k], id, host, false);
@@ -2430,6 +2825,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         c->known_const = value != 0;   // (the check's verdict stays valid: it describes the arrays)
         return OCN_OK;
     case OCN_OPT_LAZY_TAIL: c->lazy = value != 0; return OCN_OK;
+    case OCN_OPT_X2: c->x2 = value != 0; c->coherent_known = false; return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -2461,6 +2857,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_KNOWN_CONSTANTS: *value = c->known_const; return OCN_OK;
     case OCN_OPT_ONEPASS_LAST: *value = c->last_hybrid; return OCN_OK;
     case OCN_OPT_LAZY_TAIL: *value = c->open ? 2 : c->lazy; return OCN_OK;
+    case OCN_OPT_X2: *value = c->x2 && c->x2_used; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

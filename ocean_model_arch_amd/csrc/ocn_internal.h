@@ -126,10 +126,12 @@ int launch_fill_field(const ocn_block &g, double *p, double v, hipStream_t s);
 enum { OCN_KC_GENERAL = 0, OCN_KC_KNOWN = 1, OCN_KC_DEVICE = 2 };
 struct OnepassKC { int mode; const int32_t *flag; const double *kc; };
 // own (sw_stencils.h own_class bits, not with last): the halo points neighbour blocks own hold the
-// neighbours' state two points deep -- D there is formed as on their interior (MarchStep X2)
+// neighbours' state two points deep -- D there is formed as on their interior (MarchStep X2).
+// frame_of: only the part of the range outside *frame_of, as up to 4 bands in one launch
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range, bool last, const OnepassKC &kc, unsigned own = 0);
+                   const Range *range, bool last, const OnepassKC &kc, unsigned own = 0,
+                   const Range *frame_of = nullptr);
 // the known-constant precondition of launch_onepass over r (sw_kernels.hip FallbackCheck: the
 // fallback points and the forcing hold +0.0, h_r and mu are uniform): ORs 1 into *flag where it
 // does not hold; writes h_r and mu at (r.m0, r.n0) to kc[0], kc[1]

@@ -1966,6 +1966,33 @@ template <class Body> static int launch_step(const ocn_block *b, const Range &r,
     return check_launch();
 }
 
+// The one-pass step over the frame of `all` outside `inner` (up to 4 bands in one launch: the
+// overlapped x2 step's part that waits for the exchange): short tiles, the side bands with 4
+// vertically stacked tiles per workgroup -- a band is a few points wide, so its waves are few
+// and their length is the launch's latency
+#ifndef OCN_FRAME_STEP_ROWS
+#define OCN_FRAME_STEP_ROWS 4
+#endif
+template <class Body>
+static int launch_step_frame(const ocn_block *b, const Range &all, const Range &inner, const Body &body, hipStream_t s)
+{
+    const Range in = range_clip(all, inner);
+    if (range_empty(in)) return launch_step(b, all, body, s);
+    const Rects q = frame_rects(all, in);
+    MarchGrid g{};
+    for (int i = 0; i < 4; ++i) {
+        if (q.w[i] <= 0 || q.h[i] <= 0) continue;
+        const Range r{q.m0[i], q.m0[i] + q.w[i] - 1, q.n0[i], q.n0[i] + q.h[i] - 1};
+        g.r[g.nr] = march_rect<Body>(b, r, OCN_FRAME_STEP_ROWS, i >= 2);
+        g.ntiles += g.r[g.nr].tiles;
+        ++g.nr;
+    }
+    if (!g.nr) return OCN_OK;
+    const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
+    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, body);
+    return check_launch();
+}
+
 // D's fallback points within r +- 1 (the points the one-pass step over r may take D from
 // memory at) all hold +0.0 in the arrays it would read there: OR 1 into *flag otherwise
 struct FallbackCheck {
@@ -2013,7 +2040,7 @@ int launch_fallback_check(const ocn_block *b, void *const *ptr, const uint8_t *b
 
 int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
-                   const Range *range, bool last, const OnepassKC &kc, unsigned own)
+                   const Range *range, bool last, const OnepassKC &kc, unsigned own, const Range *frame_of)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
@@ -2032,9 +2059,11 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
     // general one otherwise (each launch's workgroups read the verdict and return at once if it
     // is not theirs)
     const int gz = kc.mode == OCN_KC_DEVICE ? 1 : 0, gg = kc.mode == OCN_KC_DEVICE ? 2 : 0;
-#define OCN_STEP_LAUNCH(P, L, Z, X, G)                                                                          \
-    RC_K(launch_step(b, r, MarchStep<P, L, Z, X>{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out, kc.kc, kc.flag, G, \
-                                                 own}, s))
+#define OCN_STEP_LAUNCH(P, L, Z, X, G)                                                                           \
+    do {                                                                                                          \
+        const MarchStep<P, L, Z, X> k_{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out, kc.kc, kc.flag, G, own};   \
+        RC_K(frame_of ? launch_step_frame(b, r, *frame_of, k_, s) : launch_step(b, r, k_, s));                   \
+    } while (0)
 #define OCN_STEP_VARIANT(Z, G)                                                                                   \
     do {                                                                                                         \
         if (own) { if (p2) OCN_STEP_LAUNCH(true, false, Z, true, G); else OCN_STEP_LAUNCH(false, false, Z, true, G); } \

@@ -774,7 +774,7 @@ inline size_t row_table_floats(unsigned nrows) { return recip_offset(nrows) + 2u
 enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2,
        OCN_COMPACT_RING_SEA = 4,     // not a failure: a8 / a9 write somewhere on the halo ring
        OCN_COMPACT_DIVISOR_RANGE = 8,     // not a failure: a divisor outside [2^-60, 2^60] (no one-pass step)
-       OCN_COMPACT_EDGE_RING_SEA = 16 };  // not a failure: ... on the ring of a side no neighbour block fills
+       OCN_COMPACT_EDGE_RING_SEA = 16 };  // not a failure: a8 writes on the ring of a side no neighbour fills
 
 // Which halo points of a block a neighbour block owns (they are its interior points, filled by the
 // exchanges): bit (cx * 3 + cy) with cx = 0 / 1 / 2 for m < nx_start / inside / m > nx_end and cy
@@ -830,11 +830,11 @@ struct Prepare {
         // lu / llu / llv / luh
         const unsigned a8m = (1u << OCN_LU) | (1u << OCN_LCU) | (1u << OCN_LCV);
         const unsigned a9m = (1u << OCN_LU) | (1u << OCN_LLU) | (1u << OCN_LLV) | (1u << OCN_LUH);
-        if (((m == ms || m == me || n == ns || n == ne) && (b & a8m)) || ((m == me || n == ne) && (b & a9m))) {
-            OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_RING_SEA);
-            const unsigned cls = own_class(m, ms + 1, me - 1) * 3u + own_class(n, ns + 1, ne - 1);
-            if (!((own >> cls) & 1u)) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_EDGE_RING_SEA);
-        }
+        const bool a8w = (m == ms || m == me || n == ns || n == ne) && (b & a8m);
+        if (a8w || ((m == me || n == ne) && (b & a9m))) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_RING_SEA);
+        // a8 on a ring point no neighbour block fills (a9 there: see ocn_ctx.hip k_halo_zero)
+        const unsigned cls = own_class(m, ms + 1, me - 1) * 3u + own_class(n, ns + 1, ne - 1);
+        if (a8w && !((own >> cls) & 1u)) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_EDGE_RING_SEA);
         const Pt q0 = I(ms, n);
         bool vary = false;
         float v[kNumRowFields];

@@ -78,6 +78,12 @@ class OceanModel:
         h = C.c_void_p()
         check(L.ocn_ctx_create(C.byref(cb), C.byref(cs), C.byref(cd), mptr, C.byref(h)), "ocn_ctx_create")
         self.ctx = h
+        if basin.topography is not None:   # init_data.f90:115-120 (used by init())
+            t = np.asfortranarray(basin.topography, dtype=np.float32)
+            if t.shape != (basin.nx - 4, basin.ny - 4):
+                raise ValueError(f"topography shape {t.shape} != (nx-4, ny-4) = {(basin.nx - 4, basin.ny - 4)}")
+            self._topo = t
+            check(L.ocn_ctx_set_topography(self.ctx, t.ctypes.data_as(C.c_void_p), t.size), "ocn_ctx_set_topography")
         self.blocks: list[BlockInfo] = []
         for k in range(L.ocn_ctx_block_count(self.ctx)):
             bi = _lib.OcnBlockInfo()
@@ -204,6 +210,18 @@ class OceanModel:
         for bit)."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_LAZY_TAIL, int(on)), "ocn_ctx_set_option")
         return self
+
+    def set_x2(self, on: bool = True):
+        """One-pass steps with one 2-deep state exchange each where there are halo exchanges
+        (default): every block forms the depths, vort and stresses on its halo itself and marches its
+        whole interior; same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_X2, int(on)), "ocn_ctx_set_option")
+        return self
+
+    @property
+    def x2_active(self) -> bool:
+        """Whether the last step() used one-pass steps with 2-deep state exchanges."""
+        return bool(self.option(_lib.OPT_X2))
 
     @property
     def tail_pending(self) -> bool:

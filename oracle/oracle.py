@@ -66,6 +66,8 @@ class BasinConfig:
     rotation_on_lon: float = 0.0
     rotation_on_lat: float = 0.0
     mask: np.ndarray | None = None   # int32 (nx, ny) Fortran order; None -> box, io.f90:49-59
+    # bottom topography: float32 (nx-4, ny-4) interior points (basin.par line 20), None -> 100 m
+    topography: np.ndarray | None = None
 
     def global_mask(self) -> np.ndarray:
         if self.mask is not None:
@@ -233,7 +235,16 @@ class OracleModel:
                             _p(xt), _p(yt), _p(xu), _p(yv),
                             *[_p(f[n]) for n in ("dx", "dy", "dxt", "dyt", "dxh", "dyh", "dxb", "dyb")],
                             _p(f["rlh_s"]), _p(f["rlh_c"]))
-            f["hhq_rest"][...] = 100.0
+            if bc.topography is None:
+                f["hhq_rest"][...] = 100.0   # init_data.f90:112-114
+            else:   # init_data.f90:115-120: read_data2D_real4 (io.f90:130-171) on the block interior,
+                t = np.zeros(b.shape, dtype=np.float32, order="F")   # zero where |lu| < 0.5, then real(., wp8)
+                t[b.nxs - b.bx1:b.nxe - b.bx1 + 1, b.nys - b.by1:b.nye - b.by1 + 1] = \
+                    bc.topography[b.nxs - 3:b.nxe - 2, b.nys - 3:b.nye - 2]
+                t[np.abs(f["lu"]) < 0.5] = 0.0
+                f["hhq_rest"][...] = t.astype(np.float64)
+        if bc.topography is not None:
+            self.sync("hhq_rest")
 
     def sync_r4(self, name: str):
         """sync() on an r4 field (same geometry as the r8 one, done in numpy)."""

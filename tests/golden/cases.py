@@ -16,6 +16,10 @@ INIT_CASES = ["box70x54_b1x1_s0", "box48x40_cart_s0", "bs_b4x2_tr_s0"]
 # BASELINE.json configs at full size (SHA-256 digests of every field of every block only):
 # C2 1024^2 1 block, C3 2048^2 2x2 blocks, the bench workload 4096^2 1 block, C4 4096^2 4x2 blocks
 FULLSIZE_CASES = ["box1024_b1x1_s10", "box2048_b2x2_s4", "box4096_b1x1_s6", "box4096_b4x2_s4"]
+# the reference's shipped default run (basin.par 1525 x 1115, 604 steps) on 1 and 2 x 2 blocks
+SHIPPED_CASES = ["box1521x1111_b1x1_s604", "box1521x1111_b2x2_s604"]
+# a non-uniform rest depth read from a basin.par topography file (control/init_data.f90:115-120)
+TOPO_CASES = ["box70x54_topo_b1x1_s20", "box70x54_topo_b3x2_s20", "bs_topo_b4x2_s60"]
 KERNEL_GEOMS = ["b66x50", "b1x1", "b130x7"]
 KERNEL_NAMES = ["sw_update_ssh", "sw_update_uv", "sw_next_step", "uv_trans_vort", "uv_trans",
                 "uv_diff2", "stress_components", "hh_init", "hh_update", "hh_shift"]
@@ -42,8 +46,9 @@ def load_e2e(name):
                time_smooth=_f(sw["ts"]))
     if int(sw.get("tr", 0)) > 0:
         swc.update(use_tracers=int(sw["tr"]), tracer_num=int(sw["trn"]))
+    topo = z["in/topo"] if "in/topo" in z.files else None
     return dict(basin=basin, sw=swc, bxy=tuple(int(v) for v in z["meta/bxy"]), steps=int(z["meta/steps"]),
-                mask=mask, z=z)
+                mask=mask, topography=topo, z=z)
 
 
 def e2e_blocks(z):

@@ -223,7 +223,7 @@ BASIN_TMPL = """{nx} : nx
 90.0d0 : p_pole
 -90.0d0 : q_pole
 {mask} : mask
-none : topography
+{topo} : topography
 """
 SW_TMPL = """{ffs} : full free surface
 {trans} : trans terms
@@ -245,9 +245,20 @@ none : out
 0 : dlb
 """
 
-BOX = dict(dxst="0.00312d0", dyst="0.00225d0", rlon="34.751560d0", rlat="44.801125d0", curve=1, mask="none")
+BOX = dict(dxst="0.00312d0", dyst="0.00225d0", rlon="34.751560d0", rlat="44.801125d0", curve=1, mask="none",
+           topo="none")
 BS = dict(nx=289, ny=163, dxst="0.05d0", dyst="0.04d0", rlon="27.525d0", rlat="40.940d0", curve=1,
-          mask=os.path.join(REF, "data/BS/mask_bs4km.txt"))
+          mask=os.path.join(REF, "data/BS/mask_bs4km.txt"), topo="none")
+
+
+def topography(nx, ny):
+    """A synthetic bottom topography (real(4), the (nx-4) x (ny-4) interior points, Fortran order):
+    depths between 20 and 100 m varying along both axes -- the reference reads it as its
+    basin.par line-20 file (control/init_data.f90:115-120)."""
+    i = np.arange(nx - 4, dtype=np.float64)[:, None] / (nx - 4)
+    j = np.arange(ny - 4, dtype=np.float64)[None, :] / (ny - 4)
+    h = 20.0 + 80.0 * (0.5 + 0.25 * np.sin(2 * np.pi * 1.5 * i + 0.3) + 0.25 * np.cos(2 * np.pi * 2.3 * j))
+    return np.asfortranarray(h.astype(np.float32))
 SW_DEFAULT = dict(ffs=1, trans=1, ksw=1, ts="0.5d0")
 
 # name -> (basin, sw, (bppnx, bppny), steps, keep_full_arrays)
@@ -275,6 +286,15 @@ CASES = {
     "box2048_b2x2_s4": (dict(BOX, nx=2052, ny=2052), SW_DEFAULT, (2, 2), 4, "sha"),        # C3
     "box4096_b1x1_s6": (dict(BOX, nx=4100, ny=4100), SW_DEFAULT, (1, 1), 6, "sha"),        # the bench workload
     "box4096_b4x2_s4": (dict(BOX, nx=4100, ny=4100), SW_DEFAULT, (4, 2), 4, "sha"),        # C4
+    # the reference's shipped default run: basin.par 1525 x 1115, mask and topography none, sw.par,
+    # ocean_run.par's tau = 1 s for 0.007 days = 604 steps (model.f90:135-160); one block as
+    # parallel.par ships it, and 2 x 2 blocks (odd, non-64-aligned block sizes)
+    "box1521x1111_b1x1_s604": (dict(BOX, nx=1525, ny=1115), SW_DEFAULT, (1, 1), 604, "sha"),
+    "box1521x1111_b2x2_s604": (dict(BOX, nx=1525, ny=1115), SW_DEFAULT, (2, 2), 604, "sha"),
+    # a non-uniform rest depth (basin.par line 20 file): the one-pass steps' general variant
+    "box70x54_topo_b1x1_s20": (dict(BOX, nx=70, ny=54, topo="wave"), SW_DEFAULT, (1, 1), 20, True),
+    "box70x54_topo_b3x2_s20": (dict(BOX, nx=70, ny=54, topo="wave"), SW_DEFAULT, (3, 2), 20, False),
+    "bs_topo_b4x2_s60": (dict(BS, topo="wave"), SW_DEFAULT, (4, 2), 60, False),
 }
 PROGNOSTIC = ["ssh", "sshp", "ubrtr", "ubrtrp", "vbrtr", "vbrtrp", "ff1_1", "ff1p_1"]
 
@@ -314,8 +334,13 @@ def digest_dump(path):
 
 def gen_e2e(name, basin, sw, bxy, steps, full):
     d = tempfile.mkdtemp()
+    topo = None
     try:
-        open(os.path.join(d, "basin.par"), "w").write(BASIN_TMPL.format(**basin))
+        if basin.get("topo", "none") != "none":
+            topo = topography(basin["nx"], basin["ny"])
+            topo.ravel(order="F").tofile(os.path.join(d, "topo.dat"))
+        open(os.path.join(d, "basin.par"), "w").write(
+            BASIN_TMPL.format(**dict(basin, topo="topo.dat" if topo is not None else "none")))
         open(os.path.join(d, "sw.par"), "w").write(SW_TMPL.format(**dict(dict(tr=0, trn=1), **sw)))
         open(os.path.join(d, "parallel.par"), "w").write(PAR_TMPL.format(bx=bxy[0], by=bxy[1]))
         env = dict(os.environ, OMP_NUM_THREADS="1")
@@ -327,9 +352,11 @@ def gen_e2e(name, basin, sw, bxy, steps, full):
             blocks = read_dump(os.path.join(d, "dump.bin"))
     finally:
         shutil.rmtree(d)
-    out = {"meta/basin": np.array(repr({k: v for k, v in basin.items() if k != "mask"} |
+    out = {"meta/basin": np.array(repr({k: v for k, v in basin.items() if k not in ("mask", "topo")} |
                                          {"mask": "BS" if basin["mask"] != "none" else "none"})),
            "meta/sw": np.array(repr(sw)), "meta/bxy": np.array(bxy, np.int32), "meta/steps": np.int32(steps)}
+    if topo is not None:
+        out["in/topo"] = topo
     if basin["mask"] != "none":
         from oracle.oracle import read_mask_file
         m = read_mask_file(basin["mask"], basin["nx"], basin["ny"])

@@ -38,10 +38,11 @@ def run_ranks_case(amd, case, nranks, steps=None, calls=None, **opts):
         for n in calls:
             m.step(n, tau=1.0, check_every=1)
         m.synchronize()
-        return m.flip_active
+        return m.flip_active, m.x2_active
 
-    flips = amd.run_ranks(models, body)
-    return models, flips
+    used = amd.run_ranks(models, body)
+    run_ranks_case.x2 = [u[1] for u in used]
+    return models, [u[0] for u in used]
 
 
 def check_ranks(models, case, name):
@@ -62,6 +63,8 @@ MODES = {   # name -> build_model options
     "noflip_overlap0": dict(flip=False, overlap=0),
     "norecompute": dict(recompute=False),
     "nolast": dict(onepass_last=False),
+    "nox2": dict(x2=False),                   # hybrid one-pass steps: CA / B bands, two exchanges per step
+    "nox2_overlap0": dict(x2=False, overlap=0),
     "stages": dict(fused=False),
 }
 
@@ -81,9 +84,14 @@ def test_ranks_match_reference(amd, name, nranks, mode):
     assert not bad, f"{name} over {nranks} ranks ({mode}): fields differ from the reference: {bad}"
     if mode == "default":   # OCN_OPT_OVERLAP auto: remote peers -> role-flip exchanges overlapped
         assert levels == {2}, levels
-    assert len(set(flips)) == 1, "ranks ran different kinds of steps"
-    if mode in ("default", "overlap0", "overlap1", "overlap2", "norecompute"):   # tracer runs included
+    x2 = run_ranks_case.x2
+    assert len(set(flips)) == 1 and len(set(x2)) == 1, "ranks ran different kinds of steps"
+    if mode in ("default", "overlap0", "overlap1", "overlap2", "norecompute", "nox2"):   # tracer runs included
         assert flips[0], f"{name}: role-flip steps not used over ranks"
+    if mode == "default" and "_tr_" not in name and case["steps"] >= 3:
+        assert x2[0], f"{name}: x2 steps not used over ranks"
+    if mode.startswith("nox2") or mode == "nolast":
+        assert not x2[0]
 
 
 def test_ranks_split_calls_match_reference(amd):
@@ -187,20 +195,47 @@ def test_bench_workload_matches_reference(amd, variant):
     assert not bad, f"4096^2 ({variant}): fields differ from the reference: {bad}"
 
 
+@pytest.mark.parametrize("x2", [True, False], ids=["x2", "nox2"])
 @pytest.mark.parametrize("name", ["box1024_b1x1_s10", "box2048_b2x2_s4", "box4096_b4x2_s4"])
-def test_fullsize_blocks_match_reference(amd, name):
+def test_fullsize_blocks_match_reference(amd, name, x2):
     """C2 (1024^2), C3 (2048^2 as 2x2 blocks) and C4 (4096^2 as 4x2 blocks) in one process:
-    every block on the GPU, local halo copies."""
-    case, m = _full(amd, name)
+    every block on the GPU, local halo copies; the one-pass steps of the block grids with one 2-deep
+    state exchange each (x2) or as hybrid steps (nox2)."""
+    if not x2 and "_b1x1_" in name:
+        pytest.skip("one block: no exchange")
+    case, m = _full(amd, name, x2=x2)
     try:
         m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
+        used = m.x2_active
         bad = compare_case(m, case, name)
     finally:
         m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
+    assert used == (x2 and "_b1x1_" not in name)
 
 
-@pytest.mark.parametrize("name,nranks", [("box2048_b2x2_s4", 4), ("box4096_b4x2_s4", 8)])
+@pytest.mark.parametrize("calls", ["one", "per_step"])
+@pytest.mark.parametrize("name", cases.SHIPPED_CASES)
+def test_shipped_default_run_matches_reference(amd, name, calls):
+    """The reference's shipped run (basin.par 1525 x 1115: a non-power-of-two, non-64-aligned box;
+    ocean_run.par: tau = 1 s for 604 steps, model.f90:135-160) on one block and on 2 x 2 blocks
+    (odd block sizes, x2 steps), in one ocn_ctx_step call and in 604 calls of one step (the
+    reference's own cadence), bitwise against the unmodified reference run."""
+    case, m = _full(amd, name)
+    try:
+        m.init()
+        for n in ([case["steps"]] if calls == "one" else [1] * case["steps"]):
+            m.step(n, tau=1.0, check_every=1)
+        m.synchronize()
+        one, x2 = m.onepass_active, m.x2_active
+        bad = compare_case(m, case, name)
+    finally:
+        m.close()
+    assert not bad, f"{name} ({calls}): fields differ from the reference: {bad}"
+    assert one and x2 == ("_b2x2_" in name), (one, x2)
+
+
+@pytest.mark.parametrize("name,nranks", [("box2048_b2x2_s4", 4), ("box4096_b4x2_s4", 8), ("box1521x1111_b2x2_s604", 4)])
 def test_fullsize_ranks_match_reference(amd, name, nranks):
     """C3 and C4 as BASELINE.json runs them: one block per rank, halos between ranks."""
     case = cases.load_e2e(name)
@@ -211,7 +246,7 @@ def test_fullsize_ranks_match_reference(amd, name, nranks):
         for m in models:
             m.close()
     assert not bad, f"{name} over {nranks} ranks: fields differ from the reference: {bad}"
-    assert all(flips)
+    assert all(flips) and all(run_ranks_case.x2)
 
 
 @pytest.mark.parametrize("name", cases.INIT_CASES)

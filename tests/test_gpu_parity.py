@@ -112,10 +112,11 @@ def test_tracer_kernels_match_reference(amd, geom):
 
 
 def build_model(amd, case, graph=False, fused=True, compact=True, overlap=None, march=True, flip=True,
-                recompute=True, rank=0, nranks=1, onepass=True, onepass_last=True):
+                recompute=True, rank=0, nranks=1, onepass=True, onepass_last=True, x2=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
-                            curve_grid=b["curve_grid"], mask=case["mask"])
+                            curve_grid=b["curve_grid"], mask=case["mask"],
+                            topography=case.get("topography"))
     sw = amd.SWConfig(**case["sw"])
     par = amd.ParallelConfig(bppnx=case["bxy"][0], bppny=case["bxy"][1])
     m = amd.OceanModel(basin, sw, par, rank=rank, nranks=nranks)
@@ -128,6 +129,7 @@ def build_model(amd, case, graph=False, fused=True, compact=True, overlap=None, 
     m.set_recompute(recompute)
     m.set_onepass(onepass)
     m.set_onepass_last(onepass_last)
+    m.set_x2(x2)
     if graph:
         m.set_graph(True)
     return m
@@ -153,38 +155,66 @@ def compare_case(m, case, name, whole=True):
     return bad
 
 
-@pytest.mark.parametrize("mode", ["compact", "noonepass", "nolast", "norecompute", "noflip", "pointwise", "fused",
-                                  "stages", "serial", "overlap2"])
-@pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES)
+@pytest.mark.parametrize("mode", ["compact", "nox2", "noonepass", "nolast", "norecompute", "noflip", "pointwise",
+                                  "fused", "stages", "serial", "overlap2"])
+@pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES + cases.TOPO_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
     hh_init as register marches, role-flip steps, tracer runs included (hh_init fused with the next
     step's A, fused B recomputing hhq / hhu_p / hhv_p), halo exchanges overlapped
     with inner launches in the standard steps when there are several blocks;
-    nolast = compact with a standard last step where exchanges or ring work make the one-pass last
-    step a hybrid one; norecompute = compact without the recompute steps; noflip = compact with
+    nox2 = compact with the one-pass steps of several blocks as hybrid steps (role-flip bands along
+    the exchanged sides, two exchanges per step) instead of x2 steps (one 2-deep state exchange,
+    the whole interior marched); nolast = compact with a standard last step where exchanges or ring
+    work make the one-pass last step a hybrid one (so no x2 steps either); norecompute = compact without the recompute steps; noflip = compact with
     standard steps only;
     pointwise = compact with every launch one thread per point; overlap2 = compact with the
     role-flip steps' exchanges overlapped too (OCN_OPT_OVERLAP = 2); fused =
     the 4-launch step on the 2-D real(4) arrays; serial = compact without the overlap; stages =
     the reference's 11 envoke stages."""
     case = cases.load_e2e(name)
-    compact = mode in ("compact", "noonepass", "nolast", "norecompute", "noflip", "serial", "pointwise", "overlap2")
+    compact = mode in ("compact", "nox2", "noonepass", "nolast", "norecompute", "noflip", "serial", "pointwise",
+                       "overlap2")
     m = build_model(amd, case, fused=mode != "stages", compact=compact,
                     overlap=2 if mode == "overlap2" else int(mode != "serial"),
                     march=mode != "pointwise", flip=mode != "noflip", recompute=mode != "norecompute",
-                    onepass=mode != "noonepass", onepass_last=mode != "nolast")
+                    onepass=mode != "noonepass", onepass_last=mode != "nolast", x2=mode != "nox2")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     assert m.compact_active == compact
     bad = compare_case(m, case, name)
-    flip_used, one_used = m.flip_active, m.onepass_active
+    flip_used, one_used, x2_used = m.flip_active, m.onepass_active, m.x2_active
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
-    if mode in ("compact", "noonepass", "nolast", "norecompute", "serial", "overlap2"):   # tracer runs included
+    if mode in ("compact", "nox2", "noonepass", "nolast", "norecompute", "serial", "overlap2"):   # tracer runs included
         assert flip_used, f"{name}: role-flip steps not used"
-    if mode == "compact" and name.startswith("box") and "_b1x1_" in name and case["sw"]["trans_terms"] > 0 \
-            and case["sw"]["ksw_lat"] > 0:
+    full_sw = case["sw"]["trans_terms"] > 0 and case["sw"]["ksw_lat"] > 0 and not case["sw"].get("use_tracers", 0)
+    one_block = tuple(case["bxy"]) == (1, 1)
+    if mode == "compact" and one_block and full_sw:
         assert one_used, f"{name}: one-pass steps not used"
+    if mode == "compact" and not one_block and full_sw and case["steps"] >= 3:
+        assert x2_used, f"{name}: x2 steps not used"
+    if mode in ("nox2", "nolast"):
+        assert not x2_used
+
+
+@pytest.mark.parametrize("name", cases.TOPO_CASES)
+def test_topography_general_variant_matches_reference(amd, name):
+    """A non-uniform rest depth from a basin.par topography file (control/init_data.f90:115-120):
+    the one-pass steps run their general variant (h_r read, not a kernel constant) -- on one block,
+    and with x2 steps (h_r's second halo ring from the neighbours) on several -- bitwise against the
+    reference run that read the same file; also in 1-step calls (lazy tail)."""
+    case = cases.load_e2e(name)
+    for calls in ([case["steps"]], [1] * case["steps"]):
+        m = build_model(amd, case).init()
+        for n in calls:
+            m.step(n, tau=1.0, check_every=1)
+        m.synchronize()
+        one, zero, x2 = m.onepass_active, m.onepass_zero, m.x2_active
+        bad = compare_case(m, case, name)
+        m.close()
+        assert not bad, f"{name} ({len(calls)} calls): fields differ from the reference: {bad}"
+        assert one and not zero, (one, zero)
+        assert x2 == ("_b1x1_" not in name), x2
 
 
 @pytest.mark.parametrize("calls", ["7,1,12", "1x20"])
@@ -208,10 +238,7 @@ def test_split_step_calls_match_reference(amd, graph, name, calls):
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
     assert not pending_after   # the downloads formed the tail
-    if "_b1x1_" in name:
-        assert all(pend), pend
-    else:
-        assert not any(pend), pend   # exchanges: every call forms its own tail
+    assert all(pend), pend     # one block, or x2 steps between the blocks: the tail stays pending
 
 
 def test_lazy_tail_interleaved_with_reads(amd):

@@ -87,13 +87,14 @@ def _sha(a):
 def build_oracle_model(case):
     b = case["basin"]
     basin = O.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"],
-                          rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"])
+                          rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"],
+                            topography=case.get("topography"))
     sw = O.SWConfig(**case["sw"])
     return O.OracleModel(basin, sw, *case["bxy"])
 
 
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES + cases.INIT_CASES
-                         + cases.FULLSIZE_CASES)
+                         + cases.FULLSIZE_CASES + cases.TOPO_CASES)
 def test_oracle_end_to_end_matches_reference(name):
     case = cases.load_e2e(name)
     z = case["z"]
@@ -129,7 +130,8 @@ def test_oracle_threads_over_blocks_match_reference():
     case = cases.load_e2e(name)
     b = case["basin"]
     basin = O.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"],
-                          rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"])
+                          rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"],
+                            topography=case.get("topography"))
     m = O.OracleModel(basin, O.SWConfig(**case["sw"]), *case["bxy"], threads=3).init().run(case["steps"])
     m.pool.shutdown()
     z = case["z"]
@@ -138,3 +140,18 @@ def test_oracle_threads_over_blocks_match_reference():
             key = f"b{blk.bm}_{blk.bn}/sha/{nm}"
             if key in z.files:
                 assert _sha(a) == str(z[key]), f"block ({blk.bm},{blk.bn}) field {nm} differs"
+
+
+@pytest.mark.parametrize("name", ["box70x54_b3x2_s20", "bs_b4x2_s60", "bs_b4x2_tr_s60"])
+def test_noparallel_build_matches_block_build(name):
+    """BASELINE.json's north star names the reference's _MPP_NO_PARALLEL_MODE_ CPU run; the fixtures
+    come from its default _MPP_BLOCK_MODE_ build (one thread).  tests/golden/gen_noparallel.py built
+    the reference once more with that one macro switched (macros/mpp_macros.fi:23) and ran the same
+    multi-block cases: every field of every block has the same digest."""
+    a = cases.load_e2e(name)["z"]
+    b = np.load(cases.HERE + f"/e2e_{name}_noparallel.npz")
+    sha_a = {k for k in a.files if "/sha/" in k}
+    sha_b = {k for k in b.files if "/sha/" in k}
+    assert sha_a == sha_b and len(sha_a) >= 49
+    diff = [k for k in sha_a if str(a[k]) != str(b[k])]
+    assert not diff, diff
