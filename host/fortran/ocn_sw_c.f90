@@ -168,7 +168,18 @@ module ocn_sw_c
             import :: c_ptr
             type(c_ptr), value :: ctx
         end function
+        ! control/init_data.f90:115-120: the basin.par topography file's real(4) interior values
+        integer(c_int) function ocn_ctx_set_topography(ctx, h, count) bind(C, name='ocn_ctx_set_topography')
+            import :: c_int, c_int64_t, c_ptr
+            type(c_ptr), value :: ctx, h
+            integer(c_int64_t), value :: count
+        end function
         integer(c_int) function ocn_ctx_init_state(ctx) bind(C, name='ocn_ctx_init_state')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: ctx
+        end function
+        ! forms a pending call tail (OCN_OPT_LAZY_TAIL) before a host reads device memory itself
+        integer(c_int) function ocn_ctx_complete(ctx) bind(C, name='ocn_ctx_complete')
             import :: c_int, c_ptr
             type(c_ptr), value :: ctx
         end function

@@ -16,7 +16,7 @@ program ocn_sw_driver
     implicit none
 
     integer :: nsteps, step, k, id, u, nx, ny, nlo, ntr
-    character(len=512) :: arg, dumpfile, maskfile
+    character(len=512) :: arg, dumpfile, maskfile, topofile
     character(len=256) :: lines(32)
     type(ocn_basin) :: basin
     type(ocn_sw_params) :: sw
@@ -26,6 +26,7 @@ program ocn_sw_driver
     integer(c_int32_t), allocatable, target :: mask(:, :)
     real(c_float), allocatable, target :: a4(:, :)
     real(c_double), allocatable, target :: a8(:, :)
+    real(c_float), allocatable, target :: topo(:, :)
     logical :: native
     integer, parameter :: r4_order(17) = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16]
 
@@ -42,6 +43,7 @@ program ocn_sw_driver
     read(lines(12), *) basin%curve_grid
     read(lines(13), *) basin%rotation_on_lon; read(lines(14), *) basin%rotation_on_lat
     maskfile = lines(19)
+    topofile = lines(20)
     ! sw.par (configs/sw.f90:34-41)
     call read_par('sw.par', lines, nlo)
     read(lines(1), *) sw%full_free_surface; read(lines(2), *) sw%trans_terms; read(lines(3), *) sw%ksw_lat
@@ -61,6 +63,13 @@ program ocn_sw_driver
         call ocn_check(ocn_ctx_create(basin, sw, dec, c_loc(mask), c), 'ocn_ctx_create')
     endif
     call psy_init(c, sw)
+    if (len_trim(topofile) > 0 .and. trim(topofile) /= 'none') then   ! init_data.f90:115-120
+        allocate(topo(nx - 4, ny - 4))
+        open(newunit=u, file=trim(topofile), access='stream', form='unformatted', status='old', action='read')
+        read(u) topo
+        close(u)
+        call ocn_check(ocn_ctx_set_topography(c, c_loc(topo), int(size(topo), c_int64_t)), 'set_topography')
+    endif
     call ocn_check(ocn_ctx_init_state(c), 'ocn_ctx_init_state')
 
     if (native) then

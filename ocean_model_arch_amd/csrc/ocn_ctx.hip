@@ -2366,13 +2366,13 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
 {
     if (!c || !has_r8(c, field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
     HIPCHK(hipSetDevice(c->dec.device));
-    RC(complete_open(c));
     HaloPlan *p;
     RC(get_plan(c, {field_id}, p));
     // no neighbour block anywhere (one block, no other rank): the exchange writes nothing, so
-    // nothing the step decisions rest on changes -- a PSy-style caller syncing between 1-step
-    // calls pays no re-check (and no host wait) for it
+    // nothing the step decisions rest on changes and a pending call tail may stay pending -- a
+    // PSy-style caller syncing between 1-step calls pays no re-check, host wait or tail for it
     if (!p->n_local && p->peers.empty()) return OCN_OK;
+    RC(complete_open(c));
     c->coherent_known = false;
     c->hh_consistent = false;
     c->fb_state = kFbUnchecked;

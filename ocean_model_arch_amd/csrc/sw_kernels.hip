@@ -1113,6 +1113,9 @@ __device__ __forceinline__ double rcp_count(unsigned c)
 #ifndef OCN_STEP_CARRY
 #define OCN_STEP_CARRY 1   // shifted weights / v kept in the ring (no second shift), sh * ffs as sh
 #endif
+#ifndef OCN_STEP_MZ_FORCE
+#define OCN_STEP_MZ_FORCE 0   // A/B only: the known-constant variant assumes mu = +0 (a measurement of that saving)
+#endif
 #ifndef OCN_STEP_PF2
 #define OCN_STEP_PF2 0   // 1: the known-constant variant issues each row's loads two rows ahead (measured: no gain)
 #endif
@@ -1499,9 +1502,17 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct M
             const double a1 = shz(dtc, 1) - dtc, a2 = dxb2 * muh_p * hh * sts - dxb2m * muh_m * x.hh.s<PH>(0) * x.sts.s<PH>(0);
             const double a3 = x.dxq.s<PH>(2) - x.dxq.s<PH>(1),
                          a4 = dyb2 * muh_p * hh * sts - dyb2 * muh_m2 * shz(hh, -1) * shz(sts, -1);
-            if (!E) { exp_check(acc, a1); exp_check(acc, a2); exp_check(acc, a3); exp_check(acc, a4); }
-            rxd = dv<E>(a1, dyh, x.cst<kLds>(RC_RDYH, 0)) + dv<E>(a2, dxt, x.cst<kLds>(RC_RDXT, 0));
-            ryd = -dv<E>(a3, dxh, x.cst<kLds>(RC_RDXH, 0)) + dv<E>(a4, dyt, x.cst<kLds>(RC_RDYT, 0));
+#if OCN_STEP_MZ_FORCE
+            if (ZF) {   // (A/B measurement only) mu = +0: a1..a4 are +-0 or NaN, a / d = a for the metrics
+                rxd = a1 + a2;
+                ryd = -a3 + a4;
+            } else
+#endif
+            {
+                if (!E) { exp_check(acc, a1); exp_check(acc, a2); exp_check(acc, a3); exp_check(acc, a4); }
+                rxd = dv<E>(a1, dyh, x.cst<kLds>(RC_RDYH, 0)) + dv<E>(a2, dxt, x.cst<kLds>(RC_RDXT, 0));
+                ryd = -dv<E>(a3, dxh, x.cst<kLds>(RC_RDXH, 0)) + dv<E>(a4, dyt, x.cst<kLds>(RC_RDYT, 0));
+            }
         }
         // a7 sw_update_uv (vel_ssh.f90:108-195); hun = hu, hvn = hv (the reuse identity)
         double un, vn;

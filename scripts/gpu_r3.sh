@@ -11,7 +11,7 @@ stop_on_fault() {  # rc name
   case $rc in 0|1|2|5) return 0 ;; *) echo "[$2] fault/abort/timeout -> stop"; exit $rc ;; esac
 }
 if [ -n "${TESTS:-tests -m gpu}" ] && [ "${TESTS:-x}" != "none" ]; then
-  timeout -k 10 ${T_TEST:-600} python -u -m pytest ${TESTS:-tests -m gpu} -q -rf --timeout 120 \
+  timeout -k 10 ${T_TEST:-600} python -u -m pytest ${TESTS:-tests -m gpu} -q -rf --durations=30 --timeout 120 \
       --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
   stop_on_fault $? pytest
   tail -4 "$OUT/pytest_gpu.log"

@@ -36,7 +36,7 @@ BASIN = """{nx} : nx
 90.0 :
 -90.0 :
 {mask} : mask
-none : topography
+{topo} : topography
 """
 
 
@@ -50,7 +50,11 @@ def write_case(d, case):
             f.write("mask written from tests/golden (reference data/BS/mask_bs4km.txt)\n")
             for n in range(b["ny"] - 1, -1, -1):
                 f.write("".join(str(int(v)) for v in m[:, n]) + "\n")
-    open(os.path.join(d, "basin.par"), "w").write(BASIN.format(mask=mask, **b))
+    topo = "none"
+    if case.get("topography") is not None:   # the basin.par line-20 real(4) file (init_data.f90:115-120)
+        topo = os.path.join(d, "topo.dat")
+        np.asarray(case["topography"], dtype=np.float32).ravel(order="F").tofile(topo)
+    open(os.path.join(d, "basin.par"), "w").write(BASIN.format(mask=mask, topo=topo, **b))
     s = case["sw"]
     open(os.path.join(d, "sw.par"), "w").write(
         f"{s['full_free_surface']} : ffs\n{s['trans_terms']} : trans\n{s['ksw_lat']} : ksw\n"
@@ -71,7 +75,8 @@ def test_fortran_host_builds():
                                        ("box48x40_flags000_s10", "native"), ("bs_b1x1_s60", "native"),
                                        ("box40x32_tr2_s5", "stages"), ("bs_b4x2_tr_s60", "native"),
                                        ("box70x54_b1x1_s20", "psy"), ("box70x54_b3x2_tr_s20", "psy"),
-                                       ("bs_b1x1_s604", "psy")])
+                                       ("bs_b1x1_s604", "psy"), ("box70x54_topo_b3x2_s20", "psy"),
+                                       ("bs_topo_b4x2_s60", "stages")])
 def test_fortran_host_matches_reference(tmp_path, name, mode):
     """stages = the reference's envoke stages over the kernel-layer entries; psy = the same PSy
     time loop (one expl_shallow_water per step, model.f90:146) in its fused form, one

@@ -166,6 +166,38 @@ def test_ranks_flip_falls_back_when_halo_disagrees(amd, kind):
     assert used[(True, False)] and not used[(True, True)]
 
 
+def test_ranks_upload_on_one_rank_votes_together(amd):
+    """A field uploaded on one rank only (its hh_init depths then no longer match the state, so that
+    rank alone could not start the call with a one-pass step): the vote (loopback ncclAllReduce)
+    carries that condition too, so every rank runs the same kind of first step and the exchange
+    sequences match -- the run completes, equal bit for bit to the same upload in one process."""
+    n, steps = 96, 6
+    par = amd.ParallelConfig(2, 1)
+    outs = {}
+    for ranks in (2, 1):
+        models = [amd.OceanModel(amd.box_config(n), par=par, rank=r, nranks=ranks) for r in range(ranks)]
+        if ranks > 1:
+            amd.OceanModel.attach_loopback(models)
+            amd.run_ranks(models, lambda m: m.init().step(3).synchronize())
+        else:
+            models[0].init().step(3).synchronize()
+        m0 = [m for m in models if any(b.bm == 1 for b in m.blocks)][0]
+        k = [b.k for b in m0.blocks if b.bm == 1][0]
+        a = m0.download(k, "ssh")
+        a[10:14, 20:24] += 1.0e-3     # sea points of block (1, 1) only
+        m0.upload(k, "ssh", a)
+        if ranks > 1:
+            amd.run_ranks(models, lambda m: m.step(steps).synchronize())
+        else:
+            models[0].step(steps).synchronize()
+        outs[ranks] = {(b.bm, b.bn): {nm: m.download(b.k, nm) for nm in ("ssh", "ubrtr", "vbrtr", "hhu", "sshp")}
+                       for m in models for b in m.blocks}
+        for m in models:
+            m.close()
+    bad = [(key, nm) for key, d in outs[2].items() for nm, a in d.items() if not bits_equal(a, outs[1][key][nm])]
+    assert not bad, bad
+
+
 # ---------------------------------------------------------------- BASELINE.json configs, full size
 def _full(amd, name, **opts):
     case = cases.load_e2e(name)

@@ -546,6 +546,37 @@ def test_known_constants_option(amd):
     assert not bad, f"known-constant and general one-pass variants differ: {bad}"
 
 
+@pytest.mark.parametrize("what", ["forcing", "mu", "h_r"])
+def test_graph_replay_sees_uploads_between_calls(amd, what):
+    """Graph replay (OCN_OPT_GRAPH) with a field uploaded between two step calls that changes the
+    one-pass variant's preconditions (a forcing, a new uniform mu, a new uniform h_r): the replayed
+    steps must see the new values (the known-constant variant reads them from device memory, the
+    device check picks the variant, the captured step's key holds the variant mode) -- bitwise as
+    the same run on the stream."""
+    n = 96
+    out = {}
+    for graph in (True, False):
+        m = amd.OceanModel(amd.box_config(n)).init()
+        m.set_graph(graph)
+        m.step(6, check_every=1).synchronize()
+        b = m.blocks[0]
+        if what == "forcing":
+            a = np.zeros(b.shape)
+            a[20:40, 30:50] = 2.5e-7
+            m.upload(0, "RHSx", a)
+        else:
+            nm = "mu" if what == "mu" else "hhq_rest"
+            m.upload(0, nm, np.full(b.shape, 3.0 if what == "mu" else 80.0))
+        m.step(5, check_every=1)
+        m.step(4, check_every=1).synchronize()
+        out[graph] = {nm: m.download(0, nm) for nm in ("ssh", "sshp", "ubrtr", "ubrtrp", "vbrtr", "vbrtrp", "hhu",
+                                                       "vort", "str_t", "RHSx_dif")}
+        assert m.onepass_active
+        m.close()
+    bad = [nm for nm, a in out[True].items() if not bits_equal(a, out[False][nm])]
+    assert not bad, f"graph replay vs stream after a {what} upload: {bad}"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kc", [True, False])
 def test_onepass_rows_rerun_with_ieee_divisions(amd, kc):
