@@ -287,6 +287,8 @@ def main():
                     help="halo exchanges beside inner launches: 0 never, 1 standard steps and the one-pass steps' side "
                          "chain, 2 role-flip steps too, "
                          "-1 the library default (2 with RCCL peers, else 1)")
+    ap.add_argument("--no-batch", action="store_true",
+                    help="several blocks on a GPU: one launch per block and launch group (no block batching)")
     ap.add_argument("--blocks", default=None,
                     help="block grid BXxBY (default: one block per GPU); with one GPU, several blocks on it "
                          "exercise the halo-exchange path without RCCL")
@@ -347,6 +349,7 @@ def main():
     model.set_known_constants(not args.no_known_constants)
     model.set_overlap(args.overlap)
     model.set_lazy_tail(not args.no_lazy_tail)
+    model.set_batch(not args.no_batch)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -425,6 +428,7 @@ def main():
                           "call_tail": ("pending between calls (OCN_OPT_LAZY_TAIL), formed once by ocn_ctx_complete "
                                         "inside the timed region") if lazy else "formed by every call",
                           "kernel_launches_per_step": round(launches / args.steps, 2),
+                          "block_batching": bool(not args.no_batch and bx * by // world > 1),
                           "overlap": model_overlap,
                           "parallelism": (f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else
                                           "1 block" if bx * by == 1 else f"{bx}x{by} blocks, local halo copies")},

@@ -80,6 +80,7 @@ OPT_KNOWN_CONSTANTS = 10
 OPT_ONEPASS_LAST = 11
 OPT_LAZY_TAIL = 12
 OPT_X2 = 13
+OPT_BATCH = 14
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",

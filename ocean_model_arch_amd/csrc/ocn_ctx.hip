@@ -341,6 +341,8 @@ struct ocn_ctx {
     int steps_run = 0;           // launches statistics of the last call (ocn_ctx_get_option OCN_OPT_LAUNCHES)
     int64_t launches = 0;
     int32_t *d_flags = nullptr;
+    bool batch = true;           // OCN_OPT_BATCH
+    ocn::Batcher batcher;
 };
 
 namespace ocn {
@@ -967,6 +969,26 @@ static const std::vector<int> kSyncHhInit = {OCN_HHU, OCN_HHV, OCN_HHH};
 // check_coherence)
 static const std::vector<int> kHaloCheck = {OCN_SSH, OCN_UBRTR, OCN_VBRTR, OCN_HHU, OCN_HHV, OCN_HHQ_REST};
 
+// f(b) for every block of the context.  With OCN_OPT_BATCH and several blocks the launches f makes
+// on stream s are batched (ocn_internal.h Batcher): each kernel of the loop is launched once for all
+// the blocks (up to kPack of them per launch) instead of once per block.  Only for loops whose
+// launches read and write their own block's arrays, with nothing but batchable launches on s.
+template <class F> static int each_block(ocn_ctx *c, hipStream_t s, F &&f)
+{
+    const bool on = c->batch && c->blocks.size() > 1;
+    if (on) batch_begin(&c->batcher, s);
+    int rc = OCN_OK;
+    for (size_t i = 0; i < c->blocks.size() && rc == OCN_OK; ++i) {
+        if (on) batch_next(&c->batcher);
+        rc = f(c->blocks[i]);
+    }
+    if (on) {
+        const int r2 = batch_end(&c->batcher);
+        if (rc == OCN_OK) rc = r2;
+    }
+    return rc;
+}
+
 static int stage_kernel(ocn_ctx *c, const LBlock &b, int stage, double tau)
 {
     const ocn_block *g = &b.g;
@@ -1118,7 +1140,7 @@ static int envoke(ocn_ctx *c, int stage, double tau)
 {
     ocn_ctx::Rec rec;
     RC(timer_begin(c, stage, rec));
-    for (const LBlock &b : c->blocks) RC(stage_kernel(c, b, stage, tau));
+    RC(each_block(c, c->stream, [&](const LBlock &b) { return stage_kernel(c, b, stage, tau); }));
     RC(timer_end(c, rec));
     const std::vector<int> *sl = stage_sync(stage);
     if (sl) RC(run_sync(c, *sl));
@@ -1157,8 +1179,7 @@ static int prepare_static(ocn_ctx *c)
     if (!c->compact_req || c->r4_escaped) { c->compact = false; return OCN_OK; }
     if (!c->static_dirty) return OCN_OK;
     HIPCHK(hipMemsetAsync(c->d_flags, 0, 2 * sizeof(int32_t), c->stream));
-    for (const LBlock &b : c->blocks)
-        RC(launch_prepare(&b.g, b.ptr.data(), b.bits, b.rows, c->d_flags, c->stream, b.own));
+    RC(each_block(c, c->stream, [&](const LBlock &b) { return launch_prepare(&b.g, b.ptr.data(), b.bits, b.rows, c->d_flags, c->stream, b.own); }));
     if (c->ext_ok)   // one_step_x2's row tables: the ext rows' divisor range into the second word
         for (const LBlock &b : c->blocks) RC(launch_rows_ext(&b.g, b.rows, b.rows_x, b.ext, c->d_flags + 1, c->stream));
     int32_t flags[2] = {0, 0};
@@ -1327,7 +1348,7 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
     host[kVoteX2] = !in.x2_ok;
     HIPCHK(hipMemcpyAsync(c->d_flags, host, sizeof(host), hipMemcpyHostToDevice, c->stream));
     if (in.eligible)
-        for (const LBlock &b : c->blocks) RC(launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream));
+        RC(each_block(c, c->stream, [&](const LBlock &b) { return launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream); }));
     const bool exch = has_exchange(c);
     if (exch) RC(run_sync(c, kHaloCheck, c->stream, c->d_flags));
     if (exch && c->x2) {   // one_step_x2: the rest of the state's first halo ring, and the unexchanged halos
@@ -1421,7 +1442,7 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last 
     const bool xch = has_exchange(c);
     // the previous step's hh_init and this step's A on the frames (bnd range outside inner_ca)
     auto ca_frames = [&](hipStream_t st) -> int {
-        for (const LBlock &b : c->blocks) {
+        RC(each_block(c, st, [&](const LBlock &b) -> int {
             Range in = onepass_inner(b, 2);
             if (b.nbr_rank[1] < 0) in.m0 = b.g.bnd_x1;   // no frame on the sides without a neighbour
             if (b.nbr_rank[0] < 0) in.m1 = b.g.bnd_x2;
@@ -1429,18 +1450,20 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last 
             if (b.nbr_rank[2] < 0) in.n1 = b.g.bnd_y2;
             RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_FRAME, sw, tau, !last, false,
                                st, &in));
-        }
+            return OCN_OK;
+        }));
         return OCN_OK;
     };
     // B on the one-point bands along the exchanged sides
     auto b_bands = [&](hipStream_t st) -> int {
-        for (const LBlock &b : c->blocks) {
+        RC(each_block(c, st, [&](const LBlock &b) -> int {
             const Range in = onepass_inner(b, 1);
             const Range all{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
-            if (in.m0 == all.m0 && in.m1 == all.m1 && in.n0 == all.n0 && in.n1 == all.n1) continue;
+            if (in.m0 == all.m0 && in.m1 == all.m1 && in.n0 == all.n0 && in.n1 == all.n1) return OCN_OK;
             RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, last, true, st, nbad, true, false, (double *)b.sshp_alt,
                               (double *)b.up_alt, (double *)b.vp_alt, &in));
-        }
+            return OCN_OK;
+        }));
         return OCN_OK;
     };
     if (xch && overlap_level(c) >= 1 && !c->capturing) {
@@ -1454,11 +1477,12 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last 
         // the GPU's previous work, and the compute stream sat idle until it was done
         HIPCHK(hipEventRecord(c->ev_fork, s));
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
-        for (const LBlock &b : c->blocks) {
+        RC(each_block(c, s, [&](const LBlock &b) -> int {
             const Range in = onepass_inner(b, 1);
             RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
                               (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, kc_of(c, b)));
-        }
+            return OCN_OK;
+        }));
         RC(timer_end(c, rec));
         HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
         RC(ca_frames(c->comm_stream));
@@ -1476,11 +1500,12 @@ static int one_step_hybrid(ocn_ctx *c, double tau, const StepKind &k, bool last 
     RC(timer_end(c, rec));
     if (xch) RC(run_sync(c, last ? c->sync_ca : c->sync_ca_reuse));
     RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
-    for (const LBlock &b : c->blocks) {
+    RC(each_block(c, s, [&](const LBlock &b) -> int {
         const Range in = onepass_inner(b, 1);
         RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad, (double *)b.sshp_alt,
                           (double *)b.up_alt, (double *)b.vp_alt, s, &in, last, kc_of(c, b)));
-    }
+        return OCN_OK;
+    }));
     RC(timer_end(c, rec));
     if (xch) {
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
@@ -1525,16 +1550,15 @@ static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k, bool last)
                 HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr[1])], b.ptr[field_slot(pr[0])], field_bytes(b),
                                       hipMemcpyDeviceToDevice, s));
         RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-        for (const LBlock &b : c->blocks) RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, true, s));
+        RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_ALL, sw, true, s); }));
         RC(timer_end(c, rec));
         if (xch) RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
         return OCN_OK;
     }
     if (k.next_a) {   // the next step is the last, standard one: hh_init + its fused A, then their sync
         RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_ALL, sw, tau, k.next_reuse,
-                               false, s));
+        RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_ALL, sw, tau, k.next_reuse,
+                               false, s); }));
         RC(timer_end(c, rec));
         if (xch) RC(run_sync(c, k.next_reuse ? c->sync_ca_reuse : c->sync_ca));
     }
@@ -1558,10 +1582,9 @@ static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
     };
     hipStream_t s = c->stream;
     RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
-    for (const LBlock &b : c->blocks)
-        RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.check ? c->d_nbad : nullptr,
+    RC(each_block(c, s, [&](const LBlock &b) { return launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, k.check ? c->d_nbad : nullptr,
                           (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, true,
-                          kc_of(c, b)));
+                          kc_of(c, b)); }));
     RC(timer_end(c, rec));
     swap_alt3(c);
     swap_roles(c);
@@ -1571,7 +1594,7 @@ static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
             HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr.second)], b.ptr[field_slot(pr.first)], field_bytes(b),
                                   hipMemcpyDeviceToDevice, s));
     RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-    for (const LBlock &b : c->blocks) RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, true, s));
+    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_ALL, sw, true, s); }));
     RC(timer_end(c, rec));
     return OCN_OK;
 }
@@ -1685,18 +1708,20 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
     if (overlap_level(c) >= 2 && !c->capturing) {
         HIPCHK(hipEventRecord(c->ev_fork, s));
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
-        for (const LBlock &b : c->blocks) {
+        RC(each_block(c, s, [&](const LBlock &b) -> int {
             const Range in = x2_inner(b);
             RC(march(b, s, &in, nullptr));
-        }
+            return OCN_OK;
+        }));
         RC(timer_end(c, rec));
         HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
         if (k.x2_save) RC(ring2_run(c, true, c->comm_stream));
         RC(run_sync(c, kStateX2, c->comm_stream, nullptr, 2));   // the state two points deep
-        for (const LBlock &b : c->blocks) {
+        RC(each_block(c, c->comm_stream, [&](const LBlock &b) -> int {
             const Range in = x2_inner(b);
             RC(march(b, c->comm_stream, nullptr, &in));
-        }
+            return OCN_OK;
+        }));
         HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
         c->sync_pending = true;
         RC(join_sync(c));
@@ -1704,7 +1729,7 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
         if (k.x2_save) RC(ring2_run(c, true, s));
         RC(run_sync(c, kStateX2, s, nullptr, 2));   // the state two points deep
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
-        for (const LBlock &b : c->blocks) RC(march(b, s, nullptr, nullptr));
+        RC(each_block(c, s, [&](const LBlock &b) { return march(b, s, nullptr, nullptr); }));
         RC(timer_end(c, rec));
     }
     swap_alt3(c);
@@ -1738,18 +1763,16 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         if (k.one && (has_exchange(c) || c->ring_sea)) return one_step_hybrid(c, tau, k);
         if (k.one) {   // the whole step in one launch (single block: no exchange, no ring launch)
             RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
-            for (const LBlock &b : c->blocks)
-                RC(launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad,
+            RC(each_block(c, s, [&](const LBlock &b) { return launch_onepass(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), sw, tau, nbad,
                                   (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, s, nullptr, false,
-                                  kc_of(c, b)));
+                                  kc_of(c, b)); }));
             RC(timer_end(c, rec));
             swap_alt3(c);
             swap_roles(c);
             if (k.next_a) {   // the next step is the last, standard one: hh_init + its fused A
                 RC(timer_begin(c, OCN_TIMER_FUSED_CA, rec));
-                for (const LBlock &b : c->blocks)
-                    RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_ALL, sw, tau,
-                                       k.next_reuse, false, s));
+                RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), OCN_PART_ALL, sw, tau,
+                                       k.next_reuse, false, s); }));
                 RC(timer_end(c, rec));
             }
             return OCN_OK;
@@ -1766,11 +1789,11 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         if (!k.a_done) {
             RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
             if (ov) {
-                for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_FRAME, sw, tau, reuse, s));
+                RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_a(FT(b), OCN_PART_FRAME, sw, tau, reuse, s); }));
                 RC(fork_sync(c, sync_a));
-                for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_INNER, sw, tau, reuse, s));
+                RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_a(FT(b), OCN_PART_INNER, sw, tau, reuse, s); }));
             } else {
-                for (const LBlock &b : c->blocks) RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
+                RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s); }));
             }
             RC(timer_end(c, rec));
             if (!ov) RC(run_sync(c, sync_a));
@@ -1779,8 +1802,7 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         for (int part : ov ? std::initializer_list<int>{OCN_PART_INNER, OCN_PART_FRAME}
                            : std::initializer_list<int>{OCN_PART_ALL}) {
             if (part == OCN_PART_FRAME) RC(join_sync(c));
-            for (const LBlock &b : c->blocks)
-                RC(launch_fused_b(FT(b), part, sw, tau, false, reuse, s, nbad, true, k.rc, (double *)b.sshp_alt));
+            RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_b(FT(b), part, sw, tau, false, reuse, s, nbad, true, k.rc, (double *)b.sshp_alt); }));
         }
         RC(timer_end(c, rec));
         // the current roles' ubrtrn / vbrtrn (+ hhu_p / hhv_p / hhh_p)
@@ -1792,13 +1814,14 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         swap_roles(c);
         // hh_init + the next step's fused A (full_free_surface = 1), else hh_init alone
         auto hh_init = [&](int part) -> int {
-            for (const LBlock &b : c->blocks) {
+            RC(each_block(c, s, [&](const LBlock &b) -> int {
                 if (k.next_a)
                     RC(launch_fused_ca(&b.g, b.ptr.data(), (int)b.ptr.size(), cp(b, t), part, sw, tau, k.next_reuse,
                                        k.next_reuse && k.rc_next, s));
                 else
                     RC(launch_fused_c2(FT(b), part, sw, full_c2, s));
-            }
+                return OCN_OK;
+            }));
             return OCN_OK;
         };
         const int hh_timer = k.next_a ? OCN_TIMER_FUSED_CA : OCN_STAGE_HH_INIT;
@@ -1837,23 +1860,20 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
         RC(join_sync(c));
         if (!k.a_done) {   // else fused A and its sync ran with the previous step's hh_init
             RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-            for (const LBlock &b : c->blocks)
-                RC(launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s));
+            RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_a(FT(b), OCN_PART_ALL, sw, tau, reuse, s); }));
             RC(timer_end(c, rec));
             RC(run_sync(c, sync_a));
         }
         RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, last, reuse, s));
+        RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_b(FT(b), OCN_PART_ALL, sw, tau, last, reuse, s); }));
         RC(timer_end(c, rec));
         RC(run_sync(c, c->sync_b));
         RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
-        for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_ALL, sw, nbad, s));
+        RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c1(FT(b), OCN_PART_ALL, sw, nbad, s); }));
         RC(timer_end(c, rec));
         if (ffs) {
             RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-            for (const LBlock &b : c->blocks)
-                RC(launch_fused_c2(FT(b), OCN_PART_ALL, sw, full_c2, s));
+            RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_ALL, sw, full_c2, s); }));
             RC(timer_end(c, rec));
             RC(run_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
         }
@@ -1861,33 +1881,27 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
     }
     if (!k.a_done) {   // else fused A and its sync ran with the previous step's hh_init
         RC(timer_begin(c, OCN_TIMER_FUSED_A, rec));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fused_a(FT(b), OCN_PART_FRAME, sw, tau, reuse, s));
+        RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_a(FT(b), OCN_PART_FRAME, sw, tau, reuse, s); }));
         RC(fork_sync(c, sync_a));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fused_a(FT(b), OCN_PART_INNER, sw, tau, reuse, s));
+        RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_a(FT(b), OCN_PART_INNER, sw, tau, reuse, s); }));
         RC(timer_end(c, rec));
     }
     RC(timer_begin(c, OCN_TIMER_FUSED_B, rec));
-    for (const LBlock &b : c->blocks)
-        RC(launch_fused_b(FT(b), OCN_PART_INNER, sw, tau, last, reuse, s));
+    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_b(FT(b), OCN_PART_INNER, sw, tau, last, reuse, s); }));
     RC(join_sync(c));   // sync A, or the previous role-flip step's last exchange
-    for (const LBlock &b : c->blocks)
-        RC(launch_fused_b(FT(b), OCN_PART_FRAME, sw, tau, last, reuse, s));
+    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_b(FT(b), OCN_PART_FRAME, sw, tau, last, reuse, s); }));
     RC(fork_sync(c, c->sync_b));
     RC(timer_end(c, rec));
     RC(timer_begin(c, OCN_TIMER_FUSED_C1, rec));
-    for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_INNER, sw, nbad, s));
+    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c1(FT(b), OCN_PART_INNER, sw, nbad, s); }));
     RC(join_sync(c));
-    for (const LBlock &b : c->blocks) RC(launch_fused_c1(FT(b), OCN_PART_FRAME, sw, nbad, s));
+    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c1(FT(b), OCN_PART_FRAME, sw, nbad, s); }));
     RC(timer_end(c, rec));
     if (ffs) {
         RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fused_c2(FT(b), OCN_PART_FRAME, sw, full_c2, s));
+        RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_FRAME, sw, full_c2, s); }));
         RC(fork_sync(c, *stage_sync(OCN_STAGE_HH_INIT)));
-        for (const LBlock &b : c->blocks)
-            RC(launch_fused_c2(FT(b), OCN_PART_INNER, sw, full_c2, s));
+        RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_INNER, sw, full_c2, s); }));
         RC(join_sync(c));
         RC(timer_end(c, rec));
     }
@@ -1904,11 +1918,12 @@ static int tracer_stage(ocn_ctx *c, int stage, int k, double tau, bool compact)
 {
     ocn_ctx::Rec rec;
     RC(timer_begin(c, OCN_TIMER_TRACER + stage, rec));
-    for (const LBlock &b : c->blocks) {
+    RC(each_block(c, c->stream, [&](const LBlock &b) -> int {
         const Compact t{b.bits, b.rows};
         RC(launch_tracer(&b.g, b.ptr.data(), (int)b.ptr.size(), compact ? &t : nullptr, stage, k, tau, c->sw.time_smooth,
                           c->stream));
-    }
+        return OCN_OK;
+    }));
     RC(timer_end(c, rec));
     if (stage == OCN_TSTAGE_TRAN_DIFF_FLUXES) RC(run_sync(c, kSyncFlux));
     if (stage == OCN_TSTAGE_TRAN_DIFF_TRACER) RC(run_sync(c, {OCN_FF1N(k)}));
@@ -2826,6 +2841,10 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         return OCN_OK;
     case OCN_OPT_LAZY_TAIL: c->lazy = value != 0; return OCN_OK;
     case OCN_OPT_X2: c->x2 = value != 0; c->coherent_known = false; return OCN_OK;
+    case OCN_OPT_BATCH:
+        if (c->batch != (value != 0)) drop_graphs(c);
+        c->batch = value != 0;
+        return OCN_OK;
     case OCN_OPT_COMPACT:   // (re)arms the compact tables: rebuilt from the real(4) fields at the next step
         c->compact_req = value != 0;
         c->r4_escaped = false;
@@ -2858,6 +2877,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_ONEPASS_LAST: *value = c->last_hybrid; return OCN_OK;
     case OCN_OPT_LAZY_TAIL: *value = c->open ? 2 : c->lazy; return OCN_OK;
     case OCN_OPT_X2: *value = c->x2 && c->x2_used; return OCN_OK;
+    case OCN_OPT_BATCH: *value = c->batch; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

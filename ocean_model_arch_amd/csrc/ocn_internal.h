@@ -4,6 +4,7 @@
 
 #include <initializer_list>
 #include <string>
+#include <vector>
 
 #include "../../include/ocn_sw.h"
 
@@ -158,13 +159,43 @@ int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, 
 constexpr int kCompactRingSea = 4;
 constexpr int kCompactDivisorRange = 8;   // sw_stencils.h OCN_COMPACT_DIVISOR_RANGE
 
+// Block batching (sw_kernels.hip): while a Batcher is active on this thread, the launches of the
+// march / range / frame kernels are collected per kernel type instead of issued, and batch_end
+// issues each kind for all the blocks that added one together (their tiles in one grid, up to
+// kPack launch bodies by value in the kernel arguments).  A block loop of a stage launches one
+// kernel per block: with several small blocks per device those launches are latency-bound.
+//   batch_begin(bt, s); for each block { batch_next(bt); launches on s } batch_end(bt);
+// Each block's launches keep their order (a block that adds a kind out of the batch's kind order,
+// or one kind twice, flushes the batch first); launches of different blocks may be reordered, so
+// a batched loop must not let one block's launch read what another block's writes.  Any other
+// launch while a batch is open (another kernel, another stream) is an error (check_launch).
+struct BatchEntry {
+    virtual ~BatchEntry() {}
+    virtual int flush(hipStream_t s) = 0;
+    const void *kind = nullptr;   // the kernel type (its host stub's address)
+};
+struct Batcher {
+    bool active = false;
+    hipStream_t s = nullptr;
+    int cur = -1;                        // position of the current block's last entry
+    std::vector<BatchEntry *> entries;   // in first-added order
+    int flush();                         // issue and clear the collected launches
+    ~Batcher();
+};
+extern thread_local Batcher *g_batcher;
+void batch_begin(Batcher *bt, hipStream_t s);
+inline void batch_next(Batcher *bt) { if (bt) bt->cur = -1; }
+int batch_end(Batcher *bt);
+
 int check_hip(hipError_t e, const char *what);
 // every kernel launch of the library is followed by check_launch(): it also counts them
 // (ocn_launch_count, for the launches-per-step figure of bench.py)
 void count_launch();
+int batch_violation();
 inline int check_launch()
 {
     count_launch();
+    if (g_batcher && g_batcher->active) return batch_violation();
     return check_hip(hipGetLastError(), "kernel launch");
 }
 

@@ -21,13 +21,17 @@
 // per array.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
+#include <cstring>
 #include <type_traits>
 
 #include "ocn_internal.h"
 #include "sw_stencils.h"
 
 namespace ocn {
+
+#define RC_KB(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
 
 // ------------------------------------------------------------------ launch scaffolding
 // A workgroup owns a tile of OCN_TW columns x OCN_ROWS rows: OCN_TW lanes across (a multiple
@@ -36,19 +40,13 @@ namespace ocn {
 // id is remapped so that each of the 8 XCDs (workgroups are dealt round-robin, id % 8) works
 // on one contiguous band of tiles: horizontally adjacent tiles then run back to back on the
 // same XCD and their shared +-1 columns / rows are L2 hits instead of refetches.
+// Tiles start at column w0 <= m0 (an aligned column, see launch_range); lanes left of m0 idle.
 template <typename Body>
-__global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range(int m0, int m1, int n0, int n1, int ntx, int ntiles,
-                                                             Body body)
+__device__ __forceinline__ void range_tile(int w0, int m0, int m1, int n0, int n1, int ntx, int tile, const Body &body)
 {
-    int tile = (int)blockIdx.x;
-#if OCN_XCD_REMAP
-    const int per = (ntiles + 7) / 8;
-    tile = (tile % 8) * per + tile / 8;
-    if (tile >= ntiles) return;
-#endif
     const int tx = tile % ntx, ty = tile / ntx;
-    const int m = m0 + tx * OCN_TW + (int)threadIdx.x;
-    if (m > m1) return;
+    const int m = w0 + tx * OCN_TW + (int)threadIdx.x;
+    if (m < m0 || m > m1) return;
     const int nb = n0 + ty * OCN_ROWS;
     const int ne = min(n1, nb + OCN_ROWS - 1);
     // every wave is one thread-row: its row index is wave-uniform (scalar registers)
@@ -57,13 +55,132 @@ __global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range(int m0, int m1, int
 }
 
 template <typename Body>
-static int launch_range(int m0, int m1, int n0, int n1, const Body &body, hipStream_t s)
+__global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range(int w0, int m0, int m1, int n0, int n1, int ntx,
+                                                             int ntiles, Body body)
+{
+    int tile = (int)blockIdx.x;
+#if OCN_XCD_REMAP
+    const int per = (ntiles + 7) / 8;
+    tile = (tile % 8) * per + tile / 8;
+    if (tile >= ntiles) return;
+#endif
+    range_tile(w0, m0, m1, n0, n1, ntx, tile, body);
+}
+
+// ------------------------------------------------------------------ block batching (ocn_internal.h Batcher)
+// The bodies of a batched launch travel by value in its kernel arguments (as a single body does),
+// kPack<Body> of them per launch within a 3.5 KB argument budget: no copies to device memory, and
+// the launches stay capturable into graphs.
+constexpr int kBatchMax = 16;   // ranges / rects per batched launch
+constexpr int kArgBudget = 3584 - kBatchMax * 48 - 64;
+template <class Body> constexpr int kPack = (int)(kArgBudget / sizeof(Body)) < 1 ? 1
+                                            : (int)(kArgBudget / sizeof(Body)) > 8 ? 8 : (int)(kArgBudget / sizeof(Body));
+template <class Body> struct Pack { Body b[kPack<Body>]; };
+// the bodies [b, b + n) as a Pack (bytes: the bodies are trivially copyable launch arguments)
+template <class Body> struct PackBuf {
+    alignas(Pack<Body>) unsigned char raw[sizeof(Pack<Body>)] = {};
+    PackBuf(const Body *b, size_t n) { std::memcpy(raw, (const void *)b, n * sizeof(Body)); }
+    const Pack<Body> &get() const { return *reinterpret_cast<const Pack<Body> *>(raw); }
+};
+struct RangeB { int w0, m0, m1, n0, n1, ntx, tiles, blk; };
+struct RangeGridB { int nr, ntiles; RangeB r[kBatchMax]; };
+template <typename Body>
+__global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range_b(RangeGridB g, Pack<Body> bodies)
+{
+    int tile = (int)blockIdx.x;
+#if OCN_XCD_REMAP
+    const int per = (g.ntiles + 7) / 8;
+    tile = (tile % 8) * per + tile / 8;
+    if (tile >= g.ntiles) return;
+#endif
+    int k = 0;   // workgroup-uniform
+    while (k + 1 < g.nr && tile >= g.r[k].tiles) { tile -= g.r[k].tiles; ++k; }
+    const RangeB R = g.r[k];
+    range_tile(R.w0, R.m0, R.m1, R.n0, R.n1, R.ntx, tile, bodies.b[__builtin_amdgcn_readfirstlane(R.blk)]);
+}
+
+thread_local Batcher *g_batcher = nullptr;
+// a launch on stream s joins the active batch
+static bool batching(hipStream_t s) { return g_batcher && g_batcher->active && g_batcher->s == s; }
+// the entry of kernel `kind` in the active batch for the current block (created on first use; the
+// batch is flushed first if this block's launches would lose their order)
+template <class E> static E *batch_entry(const void *kind, int &rc)
+{
+    Batcher &bt = *g_batcher;
+    int p = -1;
+    for (size_t i = 0; i < bt.entries.size(); ++i)
+        if (bt.entries[i]->kind == kind) p = (int)i;
+    if (p >= 0 && p <= bt.cur) {
+        rc = bt.flush();
+        p = -1;
+    }
+    if (p < 0) {
+        E *e = new E();
+        e->kind = kind;
+        bt.entries.push_back(e);
+        p = (int)bt.entries.size() - 1;
+    }
+    bt.cur = p;
+    return static_cast<E *>(bt.entries[(size_t)p]);
+}
+
+template <typename Body> struct RangeBatch : BatchEntry {
+    std::vector<Body> bodies;
+    std::vector<RangeB> ranges;   // one per body (blk = its index)
+    int flush(hipStream_t s) override
+    {
+        for (size_t i = 0; i < bodies.size(); i += kPack<Body>) {
+            const size_t n = std::min(bodies.size() - i, (size_t)kPack<Body>);
+            if (n == 1) {
+                const RangeB &r = ranges[i];
+                const int nblocks = OCN_XCD_REMAP ? 8 * ((r.tiles + 7) / 8) : r.tiles;
+                hipLaunchKernelGGL(k_range<Body>, dim3((unsigned)nblocks), dim3(OCN_TW, OCN_WY), 0, s, r.w0, r.m0, r.m1,
+                                   r.n0, r.n1, r.ntx, r.tiles, bodies[i]);
+                RC_KB(check_launch());
+                continue;
+            }
+            RangeGridB g{};
+            const PackBuf<Body> pk(&bodies[i], n);
+            for (size_t j = 0; j < n; ++j) {
+                g.r[g.nr] = ranges[i + j];
+                g.r[g.nr].blk = (int)j;
+                g.ntiles += ranges[i + j].tiles;
+                ++g.nr;
+            }
+            const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
+            hipLaunchKernelGGL(k_range_b<Body>, dim3((unsigned)nblocks), dim3(OCN_TW, OCN_WY), 0, s, g, pk.get());
+            RC_KB(check_launch());
+        }
+        return OCN_OK;
+    }
+};
+
+// wa: a column whose row addresses start a 256-B line (the block's nx_start in the library's
+// allocation): the tiles' columns then start on whole lines, so no wave stores a partial line at
+// both of its ends (partial-line stores cost HBM bandwidth).  INT_MIN: tiles from m0.
+#ifndef OCN_RANGE_ALIGN
+#define OCN_RANGE_ALIGN 1
+#endif
+template <typename Body>
+static int launch_range(int m0, int m1, int n0, int n1, const Body &body, hipStream_t s, int wa = INT_MIN)
 {
     if (m1 < m0 || n1 < n0) return OCN_OK;
-    const int ntx = (m1 - m0 + OCN_TW) / OCN_TW, nty = (n1 - n0 + OCN_ROWS) / OCN_ROWS;
+    int w0 = m0;
+    if (OCN_RANGE_ALIGN && wa != INT_MIN) {
+        const int d = m0 - wa;
+        w0 = wa + 64 * (d >= 0 ? d / 64 : -((63 - d) / 64));
+    }
+    const int ntx = (m1 - w0 + OCN_TW) / OCN_TW, nty = (n1 - n0 + OCN_ROWS) / OCN_ROWS;
     const int ntiles = ntx * nty;
+    if (batching(s)) {
+        int rc = OCN_OK;
+        auto *e = batch_entry<RangeBatch<Body>>((const void *)&k_range<Body>, rc);
+        e->ranges.push_back(RangeB{w0, m0, m1, n0, n1, ntx, ntiles, (int)e->bodies.size()});
+        e->bodies.push_back(body);
+        return rc;
+    }
     const int nblocks = OCN_XCD_REMAP ? 8 * ((ntiles + 7) / 8) : ntiles;
-    hipLaunchKernelGGL(k_range<Body>, dim3((unsigned)nblocks), dim3(OCN_TW, OCN_WY), 0, s, m0, m1, n0, n1, ntx,
+    hipLaunchKernelGGL(k_range<Body>, dim3((unsigned)nblocks), dim3(OCN_TW, OCN_WY), 0, s, w0, m0, m1, n0, n1, ntx,
                        ntiles, body);
     return check_launch();
 }
@@ -84,6 +201,49 @@ __global__ __launch_bounds__(OCN_FRAME_WG) void k_frame(Rects q, int total, Body
     body(m, n);
 }
 
+// batched: entry k's points take workgroups [w0[k], w0[k+1])
+struct FrameGridB { int n; int w0[9]; int total[8]; int blk[8]; Rects q[8]; };   // (kPack <= 8)
+template <typename Body>
+__global__ __launch_bounds__(OCN_FRAME_WG) void k_frame_b(FrameGridB g, Pack<Body> bodies)
+{
+    const int w = (int)blockIdx.x;
+    int k = 0;
+    while (k + 1 < g.n && w >= g.w0[k + 1]) ++k;
+    const int t = (w - g.w0[k]) * OCN_FRAME_WG + (int)threadIdx.x;
+    if (t >= g.total[k]) return;
+    int m, n;
+    frame_point(g.q[k], t, m, n);
+    bodies.b[__builtin_amdgcn_readfirstlane(g.blk[k])](m, n);
+}
+
+template <typename Body> struct FrameBatch : BatchEntry {
+    std::vector<Body> bodies;
+    std::vector<Rects> q;
+    std::vector<int> total;
+    int flush(hipStream_t s) override
+    {
+        for (size_t i = 0; i < bodies.size(); i += kPack<Body>) {
+            const size_t n = std::min(bodies.size() - i, (size_t)kPack<Body>);
+            if (n == 1) {
+                hipLaunchKernelGGL(k_frame<Body>, dim3((unsigned)((total[i] + OCN_FRAME_WG - 1) / OCN_FRAME_WG)),
+                                   dim3(OCN_FRAME_WG), 0, s, q[i], total[i], bodies[i]);
+                RC_KB(check_launch());
+                continue;
+            }
+            FrameGridB g{};
+            const PackBuf<Body> pk(&bodies[i], n);
+            for (size_t j = 0; j < n; ++j) {
+                g.q[g.n] = q[i + j]; g.total[g.n] = total[i + j]; g.blk[g.n] = (int)j;
+                g.w0[g.n + 1] = g.w0[g.n] + (total[i + j] + OCN_FRAME_WG - 1) / OCN_FRAME_WG;
+                ++g.n;
+            }
+            hipLaunchKernelGGL(k_frame_b<Body>, dim3((unsigned)g.w0[g.n]), dim3(OCN_FRAME_WG), 0, s, g, pk.get());
+            RC_KB(check_launch());
+        }
+        return OCN_OK;
+    }
+};
+
 // part: OCN_PART_ALL = R, OCN_PART_FRAME = R minus `inner`, OCN_PART_INNER = R clipped to `inner`
 template <typename Body>
 static int launch_part(const Range &r, const Range &inner, int part, const Body &body, hipStream_t s)
@@ -96,6 +256,14 @@ static int launch_part(const Range &r, const Range &inner, int part, const Body 
         const Rects q = frame_rects(r, inner);
         const int total = q.total();
         if (total == 0) return OCN_OK;
+        if (batching(s)) {
+            int rc = OCN_OK;
+            auto *e = batch_entry<FrameBatch<Body>>((const void *)&k_frame<Body>, rc);
+            e->q.push_back(q);
+            e->total.push_back(total);
+            e->bodies.push_back(body);
+            return rc;
+        }
         hipLaunchKernelGGL(k_frame<Body>, dim3((unsigned)((total + OCN_FRAME_WG - 1) / OCN_FRAME_WG)), dim3(OCN_FRAME_WG),
                            0, s, q, total, body);
         return check_launch();
@@ -251,6 +419,8 @@ template <class B> struct HasPrologue<B, std::void_t<decltype(B::kPrologue)>> { 
 template <class B, class = void> struct HasGate { static constexpr bool v = false; };
 template <class B> struct HasGate<B, std::void_t<decltype(B::kGate)>> { static constexpr bool v = B::kGate; };
 
+template <class Body> __device__ __forceinline__ void march_tile(const MarchRect &R, int tile, const Body &body);
+
 template <class Body>
 __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Body body)
 {
@@ -264,7 +434,81 @@ __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Bo
 #endif
     int k = 0;   // workgroup-uniform
     while (k + 1 < g.nr && tile >= g.r[k].tiles) { tile -= g.r[k].tiles; ++k; }
-    const MarchRect R = g.r[k];
+    march_tile(g.r[k], tile, body);
+}
+
+// batched (ocn_internal.h Batcher): every block's rects in one grid, rect k marched with body blk[k]
+struct MarchGridB { int nr, ntiles; MarchRect r[kBatchMax]; int blk[kBatchMax]; };
+template <class Body>
+__global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march_b(MarchGridB g, Pack<Body> bodies)
+{
+    int tile = (int)blockIdx.x;
+#if OCN_XCD_REMAP
+    const int per = (g.ntiles + 7) / 8;
+    tile = (tile % 8) * per + tile / 8;
+    if (tile >= g.ntiles) return;
+#endif
+    int k = 0;   // workgroup-uniform
+    while (k + 1 < g.nr && tile >= g.r[k].tiles) { tile -= g.r[k].tiles; ++k; }
+    const Body &body = bodies.b[__builtin_amdgcn_readfirstlane(g.blk[k])];
+    if constexpr (HasGate<Body>::v)
+        if (!body.enabled()) return;
+    march_tile(g.r[k], tile, body);
+}
+
+template <class Body> struct MarchBatch : BatchEntry {
+    std::vector<Body> bodies;
+    std::vector<MarchRect> rects;
+    std::vector<int> blk;
+    int flush(hipStream_t s) override
+    {
+        constexpr int P = kPack<Body> < kBatchMax / 4 ? kPack<Body> : kBatchMax / 4;   // (a body has <= 4 rects)
+        for (size_t i = 0; i < bodies.size(); i += P) {
+            const size_t n = std::min(bodies.size() - i, (size_t)P);
+            if (n == 1) {   // one body: its rects (at most 4) in the plain launch
+                MarchGrid g{};
+                for (size_t j = 0; j < rects.size(); ++j)
+                    if (blk[j] == (int)i && g.nr < 4) { g.r[g.nr++] = rects[j]; g.ntiles += rects[j].tiles; }
+                if (!g.nr) continue;
+                const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
+                hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, bodies[i]);
+                RC_KB(check_launch());
+                continue;
+            }
+            MarchGridB g{};
+            const PackBuf<Body> pk(&bodies[i], n);
+            for (size_t j = 0; j < rects.size(); ++j)
+                if (blk[j] >= (int)i && blk[j] < (int)(i + n)) {
+                    g.r[g.nr] = rects[j]; g.blk[g.nr] = blk[j] - (int)i; g.ntiles += rects[j].tiles; ++g.nr;
+                }
+            if (!g.nr) continue;
+            const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
+            hipLaunchKernelGGL(k_march_b<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, pk.get());
+            RC_KB(check_launch());
+        }
+        return OCN_OK;
+    }
+};
+
+// a march launch of grid g with one body: issued, or added to the active batch
+template <class Body> static int issue_march(const MarchGrid &g, const Body &body, hipStream_t s)
+{
+    if (!g.nr) return OCN_OK;
+    if (batching(s)) {
+        int rc = OCN_OK;
+        auto *e = batch_entry<MarchBatch<Body>>((const void *)&k_march<Body>, rc);
+        const int i = (int)e->bodies.size();
+        e->bodies.push_back(body);
+        for (int k = 0; k < g.nr; ++k) { e->rects.push_back(g.r[k]); e->blk.push_back(i); }
+        return rc;
+    }
+    const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
+    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, body);
+    return check_launch();
+}
+
+template <class Body> __device__ __forceinline__ void march_tile(const MarchRect &R, int tile, const Body &body)
+{
     const int tx = tile % R.ntx, ty = tile / R.ntx;
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -337,10 +581,7 @@ static int launch_march_rects(const ocn_block *b, const Range *rs, int nr, const
             g.ntiles += g.r[g.nr].tiles;
             ++g.nr;
         }
-    if (!g.nr) return OCN_OK;
-    const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
-    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, body);
-    return check_launch();
+    return issue_march(g, body, s);
 }
 
 template <typename Body>
@@ -1972,9 +2213,7 @@ template <class Body> static int launch_step(const ocn_block *b, const Range &r,
     g.r[0] = march_rect<Body>(b, r, step_rows<Body>(r, OCN_STEP_VERT != 0), OCN_STEP_VERT != 0);
     g.nr = 1;
     g.ntiles = g.r[0].tiles;
-    const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
-    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, body);
-    return check_launch();
+    return issue_march(g, body, s);
 }
 
 // The one-pass step over the frame of `all` outside `inner` (up to 4 bands in one launch: the
@@ -1998,10 +2237,7 @@ static int launch_step_frame(const ocn_block *b, const Range &all, const Range &
         g.ntiles += g.r[g.nr].tiles;
         ++g.nr;
     }
-    if (!g.nr) return OCN_OK;
-    const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
-    hipLaunchKernelGGL(k_march<Body>, dim3((unsigned)nblocks), dim3(256), 0, s, g, body);
-    return check_launch();
+    return issue_march(g, body, s);
 }
 
 // D's fallback points within r +- 1 (the points the one-pass step over r may take D from
@@ -2118,6 +2354,51 @@ int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, 
 
 size_t row_table_size(unsigned nrows) { return row_table_floats(nrows); }
 
+Batcher::~Batcher()
+{
+    for (BatchEntry *e : entries) delete e;
+}
+
+int Batcher::flush()
+{
+    const bool was = active;
+    active = false;   // the flush's own launches are issued, not collected
+    int rc = OCN_OK;
+    for (BatchEntry *e : entries) {
+        if (rc == OCN_OK) rc = e->flush(s);
+        delete e;
+    }
+    entries.clear();
+    cur = -1;
+    active = was;
+    return rc;
+}
+
+void batch_begin(Batcher *bt, hipStream_t s)
+{
+    if (!bt) return;
+    for (BatchEntry *e : bt->entries) delete e;
+    bt->entries.clear();
+    bt->s = s;
+    bt->cur = -1;
+    bt->active = true;
+    g_batcher = bt;
+}
+
+int batch_end(Batcher *bt)
+{
+    if (!bt) return OCN_OK;
+    const int rc = bt->flush();
+    bt->active = false;
+    g_batcher = nullptr;
+    return rc;
+}
+
+int batch_violation()
+{
+    return set_error(OCN_ERR_STATE, "a kernel launch bypassed the open block batch (sw_kernels.hip Batcher)");
+}
+
 int launch_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows, int32_t *flags, hipStream_t s,
                    unsigned own)
 {
@@ -2157,7 +2438,7 @@ int ocn_sw_update_ssh(const ocn_block *b, double tau, const float *lu, const flo
 {
     CHECK(lu, dx, dy, dxh, dyh, hhu, hhv, sshn, sshp, ubrtr, vbrtr);
     SwUpdateSsh<false> k{geo(b), tau, lu, dx, dy, dxh, dyh, hhu, hhv, sshn, sshp, ubrtr, vbrtr};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_hh_update(const ocn_block *b, const float *lu, const float *llu, const float *llv, const float *luh,
@@ -2168,7 +2449,7 @@ int ocn_hh_update(const ocn_block *b, const float *lu, const float *llu, const f
     CHECK(lu, llu, llv, luh, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, hqn, hun, hvn, hhn, sh, h_r);
     HhUpdate<false> k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end,
                Interp<false>{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh, hqn, hun, hvn, hhn, sh, h_r};
-    return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream);
+    return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_uv_trans_vort(const ocn_block *b, const float *luu, const float *dxt, const float *dyt, const float *dxb,
@@ -2176,7 +2457,7 @@ int ocn_uv_trans_vort(const ocn_block *b, const float *luu, const float *dxt, co
 {
     CHECK(luu, dxt, dyt, dxb, dyb, u, v, vort);
     UvTransVort<false> k{geo(b), luu, dxt, dyt, dxb, dyb, u, v, vort};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_uv_trans(const ocn_block *b, const float *lcu, const float *lcv, const float *luu, const float *dxh,
@@ -2186,7 +2467,7 @@ int ocn_uv_trans(const ocn_block *b, const float *lcu, const float *lcv, const f
     (void)hq;
     CHECK(lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy);
     UvTrans<false> k{geo(b), lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_stress_components(const ocn_block *b, const float *lu, const float *luu, const float *dx, const float *dy,
@@ -2196,7 +2477,7 @@ int ocn_stress_components(const ocn_block *b, const float *lu, const float *luu,
 {
     CHECK(lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s);
     StressComponents<false> k{geo(b), lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_uv_diff2(const ocn_block *b, const float *lcu, const float *lcv, const float *dx, const float *dy,
@@ -2207,7 +2488,7 @@ int ocn_uv_diff2(const ocn_block *b, const float *lcu, const float *lcv, const f
     (void)hu; (void)hv;
     CHECK(lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy);
     UvDiff2<false> k{geo(b), lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_sw_update_uv(const ocn_block *b, double tau, const float *lcu, const float *lcv, const float *dxt,
@@ -2224,7 +2505,7 @@ int ocn_sw_update_uv(const ocn_block *b, double tau, const float *lcu, const flo
     SwUpdateUv<false> k{geo(b), tau, lcu, lcv, dxt, dyt, dxh, dyh, dxb, dyb, hhu, hhun, hhup, hhv, hhvn, hhvp, hhh, ssh,
                  ubrtr, ubrtrn, ubrtrp, vbrtr, vbrtrn, vbrtrp, rdis, rlh_s, RHSx, RHSy, RHSx_adv, RHSy_adv,
                  RHSx_dif, RHSy_dif};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_sw_next_step(const ocn_block *b, double time_smooth, const float *lu, const float *lcu, const float *lcv,
@@ -2233,7 +2514,7 @@ int ocn_sw_next_step(const ocn_block *b, double time_smooth, const float *lu, co
 {
     CHECK(lu, lcu, lcv, ssh, sshn, sshp, ubrtr, ubrtrn, ubrtrp, vbrtr, vbrtrn, vbrtrp);
     SwNextStep<false> k{geo(b), time_smooth, lu, lcu, lcv, ssh, sshn, sshp, ubrtr, ubrtrn, ubrtrp, vbrtr, vbrtrn, vbrtrp};
-    return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream);
+    return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_hh_shift(const ocn_block *b, double time_smooth, const float *lu, const float *llu, const float *llv,
@@ -2242,7 +2523,7 @@ int ocn_hh_shift(const ocn_block *b, double time_smooth, const float *lu, const 
 {
     CHECK(lu, llu, llv, luh, hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn);
     HhShift<false> k{geo(b), time_smooth, lu, llu, llv, luh, hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn};
-    return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream);
+    return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_hh_init(const ocn_block *b, int32_t full_free_surface, const float *lu, const float *llu,
@@ -2257,7 +2538,7 @@ int ocn_hh_init(const ocn_block *b, int32_t full_free_surface, const float *lu, 
     HhInit<false> k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)full_free_surface, true,
              Interp<false>{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh,
              hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn, sh, shp, h_r};
-    return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream);
+    return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_tran_diff_fluxes(const ocn_block *b, const float *lcu, const float *lcv, const float *dxt, const float *dyt,
@@ -2268,7 +2549,7 @@ int ocn_tran_diff_fluxes(const ocn_block *b, const float *lcu, const float *lcv,
     (void)ffp;   // passed and unused by the reference kernel ("Try ff instead of ffp")
     CHECK(lcu, lcv, dxt, dyt, dxh, dyh, hhu, hhv, ff, uu, vv, mu, flux_x, flux_y);
     TranDiffFluxes<false> k{geo(b), factor_mu, lcu, lcv, dxt, dyt, dxh, dyh, hhu, hhv, ff, uu, vv, mu, flux_x, flux_y};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_tran_diff_tracer(const ocn_block *b, const float *lu, const float *dx, const float *dy, double tau,
@@ -2277,7 +2558,7 @@ int ocn_tran_diff_tracer(const ocn_block *b, const float *lu, const float *dx, c
 {
     CHECK(lu, dx, dy, hhqn, hhqp, flux_x, flux_y, ffp, ffn);
     TranDiffTracer<false> k{geo(b), tau, lu, dx, dy, hhqn, hhqp, flux_x, flux_y, ffp, ffn};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_tracer_next_step(const ocn_block *b, double time_smooth, const float *lu, const double *ffn, double *ffp,
@@ -2285,14 +2566,14 @@ int ocn_tracer_next_step(const ocn_block *b, double time_smooth, const float *lu
 {
     CHECK(lu, ffn, ffp, ff);
     TracerNextStep<false> k{geo(b), time_smooth, lu, ffn, ffp, ff};
-    return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream);
+    return launch_range(b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, k, (hipStream_t)stream, b->nx_start);
 }
 
 int ocn_check_ssh_err(const ocn_block *b, const float *lu, const double *ssh, int32_t *nbad_device, void *stream)
 {
     CHECK(lu, ssh, nbad_device);
     CheckSshErr<false> k{geo(b), lu, ssh, (int *)nbad_device};
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream);
+    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
 }
 
 }  // extern "C"

@@ -218,6 +218,12 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_X2, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_batch(self, on: bool = True):
+        """Block batching (default): with several blocks on the device, each launch group of a step
+        is issued once for all of them instead of once per block."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_BATCH, int(on)), "ocn_ctx_set_option")
+        return self
+
     @property
     def x2_active(self) -> bool:
         """Whether the last step() used one-pass steps with 2-deep state exchanges."""

@@ -1,11 +1,11 @@
 #!/bin/bash
 # A/B timing on one box: bench.py alternating between the in-tree library and each
-# build_variants/lib_*.so, ROUNDS times; prints ms/step and the one-pass launch mean per run.
+# build_variants/lib_*.so (or the libraries VARIANTS names), ROUNDS times; prints ms/step and the one-pass launch mean per run.
 set -u
 OUT=${OUT:-gpurun_out/ab}
 mkdir -p "$OUT"
 for r in $(seq 1 ${ROUNDS:-3}); do
-  for lib in ocean_model_arch_amd/libocn_sw.so $(ls build_variants/lib_*.so 2>/dev/null); do
+  for lib in ocean_model_arch_amd/libocn_sw.so $(ls ${VARIANTS:-build_variants/lib_*.so} 2>/dev/null); do
     n=$(basename $lib .so)
     OCN_LIB_PATH=$(pwd)/$lib timeout -k 10 200 python bench.py --no-cpu-baseline --steps ${STEPS:-40} ${BENCH_ARGS:-} \
       > "$OUT/${n}_$r.log" 2>&1; rc=$?
