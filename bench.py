@@ -30,6 +30,11 @@ STAGE_BYTES = {"sw_update_ssh": 68, "hh_update": 96, "uv_trans_vort": 44, "uv_tr
                "stress_components": 72, "uv_diff2": 96, "sw_update_uv": 200, "sw_next_step": 132,
                "hh_shift": 176, "hh_init": 168}
 B_ALG = sum(STAGE_BYTES.values())
+# the same stages over the compact tables (ocn_ctx envoke with OCN_OPT_COMPACT): the real(4) masks
+# as one mask byte per point, the metrics as per-row values (bytes per cell: the real(8) arrays + 1)
+STAGE_BYTES_COMPACT = {"sw_update_ssh": 49, "hh_update": 49, "uv_trans_vort": 25, "uv_trans": 65,
+                       "stress_components": 33, "uv_diff2": 57, "sw_update_uv": 161, "sw_next_step": 121,
+                       "hh_shift": 161, "hh_init": 121}
 # Distinct arrays read + written once per interior cell by each launch kind, for
 # the bench's sw.par (all three flags on), with the compact static fields (index 0) or the 2-D
 # real(4) arrays (index 1).  "reuse" = a step that is neither the first nor the last of its
@@ -396,8 +401,10 @@ def main():
     if rank == 0:
         ring = bx * by > 1
         ntr = sw.tracer_num if sw.use_tracers > 0 else 0
-        kbytes = STAGE_BYTES if args.stages else fused_bytes(compact, calls, flip, rc, ring, one, ntr, one_zero, lazy)
-        b_path = B_ALG if args.stages else step_bytes(compact, calls, flip, rc, ring, one, ntr, one_zero, lazy)
+        stage_tab = STAGE_BYTES_COMPACT if compact else STAGE_BYTES
+        kbytes = stage_tab if args.stages else fused_bytes(compact, calls, flip, rc, ring, one, ntr, one_zero, lazy)
+        b_path = sum(stage_tab.values()) if args.stages else step_bytes(compact, calls, flip, rc, ring, one, ntr,
+                                                                          one_zero, lazy)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:   # the dominant kernel: the most device time over the timed steps
@@ -443,6 +450,10 @@ def main():
                                               "note": "bytes the reference's 11 stages would move at this step "
                                                       "rate; not moved by this path, not a roofline fraction"},
                "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()}}
+        if args.stages:   # each stage's rate on the reference's bytes and on the bytes it moves
+            out["stage_frac"] = {s: {"survey_B": round(STAGE_BYTES[s] * local_cells / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                     "moved_B": round(kbytes[s] * local_cells / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                                 for s, v in stage_ms.items()}
         if world > 1:
             out["multi_gpu_parity_512"] = parity
         if world == 1 and not args.no_cpu_baseline:

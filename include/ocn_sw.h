@@ -311,7 +311,8 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_STAGE_TIMING: bracket every launch group with HIP events on the context stream.
  *  OCN_OPT_FUSED (default 1): ocn_ctx_step runs the step as 4 fused launch groups and 3 halo
  *  syncs (same results and final state bit for bit); 0 = the 11 envoke stages of the reference.
- *  OCN_OPT_COMPACT (default 1): the fused step reads the real(4) masks as one bit-packed byte
+ *  OCN_OPT_COMPACT (default 1): the fused step -- and the reference stages run by ocn_ctx_step
+ *  with OCN_OPT_FUSED 0 or by ocn_ctx_stage -- read the real(4) masks as one bit-packed byte
  *  per point and the grid metrics as one value per row, when that is exact for the current
  *  real(4) fields (checked when they were last set; same results bit for bit).  Handing out a
  *  real(4) pointer with ocn_ctx_field disables this until it is set to 1 again, which also

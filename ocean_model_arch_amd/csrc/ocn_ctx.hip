@@ -993,6 +993,10 @@ static int stage_kernel(ocn_ctx *c, const LBlock &b, int stage, double tau)
 {
     const ocn_block *g = &b.g;
     void *s = c->stream;
+    if (c->compact) {   // the compact tables (prepare_static): mask bytes and row metrics
+        const Compact t{b.bits, b.rows, c->march};
+        return launch_stage(g, b.ptr.data(), (int)b.ptr.size(), &t, stage, c->sw, tau, c->d_nbad, c->stream);
+    }
 #define R4(id) b.f<const float>(id)
 #define R8(id) b.f<double>(id)
     switch (stage) {
@@ -2407,6 +2411,7 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     c->alt_ok = false;
     c->hh_consistent = false;
     c->fb_state = kFbUnchecked;
+    RC(prepare_static(c));
     return envoke(c, stage_id, tau);
 }
 
@@ -2420,7 +2425,7 @@ static void drop_graphs(ocn_ctx *c)
 static int run_step(ocn_ctx *c, double tau, const StepKind &k)
 {
     RC(c->fused ? one_step_fused(c, tau, k) : one_step(c, tau, k.check));
-    return expl_tracer(c, tau, c->fused && c->compact);
+    return expl_tracer(c, tau, c->compact);
 }
 
 // one step as a replayed hipGraph, captured once per (tau, step kind, compact, role, one-pass
@@ -2606,7 +2611,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         }
         RC(complete_open(c));
     }
-    if (c->fused) RC(prepare_static(c));
+    RC(prepare_static(c));   // (the stage path reads the compact tables too)
     // with RCCL every rank takes part in the decisions (check_coherence reduces the verdicts)
     const bool eligible = flip_eligible(c);
     const bool x2_here = x2_local(c);
@@ -2862,7 +2867,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_STAGE_TIMING: *value = c->stage_timing; return OCN_OK;
     case OCN_OPT_FUSED: *value = c->fused; return OCN_OK;
     case OCN_OPT_OVERLAP: *value = overlap_level(c); return OCN_OK;
-    case OCN_OPT_COMPACT: *value = c->fused && c->compact; return OCN_OK;
+    case OCN_OPT_COMPACT: *value = c->compact; return OCN_OK;
     case OCN_OPT_MARCH: *value = c->march; return OCN_OK;
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
     case OCN_OPT_RECOMPUTE: *value = c->recompute && c->rc_used; return OCN_OK;

@@ -150,6 +150,10 @@ int launch_rows_ext(const ocn_block *b, const float *rows, float *rows_x, const 
                     hipStream_t s);
 constexpr int kCompactEdgeRingSea = 16;   // sw_stencils.h OCN_COMPACT_EDGE_RING_SEA
 // Tracer stage `stage` (OCN_TSTAGE_*) of tracer k (1-based) on one block.
+// one reference stage (OCN_STAGE_*) over the compact tables: the ocn_<stage> entry's write set
+// and results (sw_kernels.hip KStage; hh_init as the register march with cp->march)
+int launch_stage(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, const ocn_sw_params &sw,
+                 double tau, int32_t *nbad, hipStream_t s);
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);
 // ORs 1 into *flags (device int) if a buffer pair of the role-flip step differs outside the

@@ -816,6 +816,74 @@ template <bool C1F, bool RC = false, bool ALT = false> struct MarchFusedB {
     }
 };
 
+// a4 uv_trans alone (the reference stage over the compact tables, ocn_ctx envoke) as a register
+// march (offset layout): its six real(8) operands are read at up to six neighbours each, which
+// one thread per point issues as 26 loads per cell; here each is loaded once per cell.
+struct MarchViewT {
+    RowsD<true, true> rU, rV, rHV;        // ubrtr, vbrtr, hhv: rows n-1 .. n+1
+    RowsD<false, true> rHU;               // hhu: rows n, n+1
+    RowsD<true, false> rVORT, rHH;        // vort, hhh: rows n-1, n
+    BitRows<true, false> bits;            // mask bytes: rows n-1, n
+    MetRows met;
+    OCN_MV(u, rU) OCN_MV(v, rV) OCN_MV(hu, rHU) OCN_MV(hv, rHV) OCN_MV(vort, rVORT) OCN_MV(hh, rHH)
+    OCN_MG_ALL
+    __device__ __forceinline__ float luu(int dx, int dy) const
+    {
+        if (dx != 0) ocn_march_bad_access();
+        return (bits.at(0, dy) & (1u << OCN_LUU)) ? 1.0f : 0.0f;
+    }
+};
+struct MarchUvTrans {
+    static constexpr bool kAligned = false;
+    static constexpr int kHalo = 1;
+    ocn_block b; Tab<true> t;
+    using View = MarchViewT;
+    struct Fn {
+        UvTrans<true> k; const Tab<true> &t;
+        // row n: ubrtr, vbrtr, hhv, hhu at n+1; vort, hhh, the mask byte at n; metric row n+1
+        struct Batch { double nn[4], c[2]; unsigned bits; float g[kRowTable]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n), cn = k.I(L.m, n + 1);
+            q.nn[0] = ld(k.u, cn); q.nn[1] = ld(k.v, cn); q.nn[2] = ld(k.hv, cn); q.nn[3] = ld(k.hu, cn);
+            q.c[0] = ld(k.vort, c); q.c[1] = ld(k.hh, c);
+            q.bits = ld(t.bits, c);
+            MetRows::load(q.g, t.rows, t.nrows, cn.r);
+        }
+        __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n);
+            x.rVORT.s = x.rVORT.c; x.rHH.s = x.rHH.c;
+            x.met.shift(q.g);
+            x.rU.nn = q.nn[0]; x.rV.nn = q.nn[1]; x.rHV.nn = q.nn[2]; x.rHU.nn = q.nn[3];
+            x.rVORT.c = q.c[0]; x.rHH.c = q.c[1];
+            x.bits.s = x.bits.c; x.bits.c = q.bits;
+            double rx, ry;
+            uv_trans_math(x, rx, ry);
+            if (L.out) {
+                const unsigned bc = x.bits.c;
+                if (bc & (1u << OCN_LCU)) st(k.RHSx, c, rx);
+                if (bc & (1u << OCN_LCV)) st(k.RHSy, c, ry);
+            }
+            x.rU.rotate(); x.rV.rotate(); x.rHV.rotate(); x.rHU.rotate();
+        }
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{make_uv_trans(&b, t), t};
+        View x{};
+        const Pt s = f.k.I(L.m, nb - 1), c = f.k.I(L.m, nb);   // rows kept from before the first row
+        x.rU.s = ld(f.k.u, s); x.rU.c = ld(f.k.u, c);
+        x.rV.s = ld(f.k.v, s); x.rV.c = ld(f.k.v, c);
+        x.rHV.s = ld(f.k.hv, s); x.rHV.c = ld(f.k.hv, c);
+        x.rHU.c = ld(f.k.hu, c);
+        x.rVORT.c = ld(f.k.vort, s); x.rHH.c = ld(f.k.hh, s);
+        x.bits.c = ld(t.bits, s);
+        x.met.preload(t.rows, t.nrows, s.r, c.r);
+        march_rows(f, x, L, nb, ne);
+    }
+};
+
 // The view of fused A's stages (sw_stencils.h sw_update_ssh_math, hh_update_math,
 // uv_trans_vort_math, stress_components_math) over the march registers.  Arrays read at m-1 or
 // m+1 keep edge values (aligned layout).
@@ -2342,6 +2410,62 @@ int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact 
     case OCN_TSTAGE_TRACER_NEXT_STEP:
         return launch_fused<KTracerNextStep>(rr, rr, OCN_PART_ALL, b, ptr, nptr, cp, k, s, ts);
     default: return set_error(OCN_ERR_ARG, "bad tracer stage id");
+    }
+}
+
+// One reference stage over the compact tables (ocn_ctx.hip envoke, OCN_OPT_COMPACT): the stage
+// functor is built on the device from the block's field table, as the fused launches build theirs,
+// and reads the mask byte and the per-row metrics instead of the real(4) arrays -- the same
+// operands (launch_prepare checked every point of a row carries the row's metric bits), so the
+// same results as the ocn_<stage> entries on the 2-D arrays.
+template <int S> struct KStage {
+    ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; int32_t *nbad;
+    OCN_HD void operator()(int m, int n) const
+    {
+        if constexpr (S == OCN_STAGE_SW_UPDATE_SSH) make_sw_update_ssh(&b, t, tau)(m, n);
+        else if constexpr (S == OCN_STAGE_HH_UPDATE) make_hh_update(&b, t)(m, n);
+        else if constexpr (S == OCN_STAGE_UV_TRANS_VORT) make_uv_trans_vort(&b, t)(m, n);
+        else if constexpr (S == OCN_STAGE_UV_TRANS) make_uv_trans(&b, t)(m, n);
+        else if constexpr (S == OCN_STAGE_STRESS_COMPONENTS) make_stress_components(&b, t)(m, n);
+        else if constexpr (S == OCN_STAGE_UV_DIFF2) make_uv_diff2(&b, t)(m, n);
+        else if constexpr (S == OCN_STAGE_SW_UPDATE_UV) make_sw_update_uv(&b, t, tau)(m, n);
+        else if constexpr (S == OCN_STAGE_SW_NEXT_STEP) make_sw_next_step(&b, t, sw.time_smooth)(m, n);
+        else if constexpr (S == OCN_STAGE_HH_SHIFT) make_hh_shift(&b, t, sw.time_smooth)(m, n);
+        else if constexpr (S == OCN_STAGE_HH_INIT) make_hh_init(&b, t, (int)sw.full_free_surface, true)(m, n);
+        else make_check_ssh_err(&b, t, nbad)(m, n);
+    }
+};
+template <int S>
+static int launch_stage_k(const ocn_block *b, const Tab<true> &t, const Range &r, const ocn_sw_params &sw, double tau,
+                          int32_t *nbad, hipStream_t s)
+{
+    return launch_range(r.m0, r.m1, r.n0, r.n1, KStage<S>{*b, t, sw, tau, nbad}, s, b->nx_start);
+}
+
+int launch_stage(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, const ocn_sw_params &sw,
+                 double tau, int32_t *nbad, hipStream_t s)
+{
+    RC_K(check_block(b));
+    if (!cp) return set_error(OCN_ERR_ARG, "launch_stage: the compact tables");
+    const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
+    const Range ri = range_interior(b), rr = range_ring(b), rb = range_bnd(b);
+    switch (stage) {
+    case OCN_STAGE_SW_UPDATE_SSH: return launch_stage_k<OCN_STAGE_SW_UPDATE_SSH>(b, t, ri, sw, tau, nbad, s);
+    case OCN_STAGE_HH_UPDATE: return launch_stage_k<OCN_STAGE_HH_UPDATE>(b, t, rb, sw, tau, nbad, s);
+    case OCN_STAGE_UV_TRANS_VORT: return launch_stage_k<OCN_STAGE_UV_TRANS_VORT>(b, t, ri, sw, tau, nbad, s);
+    case OCN_STAGE_UV_TRANS:
+        if (use_march(cp)) return launch_march(b, ri, MarchUvTrans{*b, t}, s);
+        return launch_stage_k<OCN_STAGE_UV_TRANS>(b, t, ri, sw, tau, nbad, s);
+    case OCN_STAGE_STRESS_COMPONENTS: return launch_stage_k<OCN_STAGE_STRESS_COMPONENTS>(b, t, ri, sw, tau, nbad, s);
+    case OCN_STAGE_UV_DIFF2: return launch_stage_k<OCN_STAGE_UV_DIFF2>(b, t, ri, sw, tau, nbad, s);
+    case OCN_STAGE_SW_UPDATE_UV: return launch_stage_k<OCN_STAGE_SW_UPDATE_UV>(b, t, ri, sw, tau, nbad, s);
+    case OCN_STAGE_SW_NEXT_STEP: return launch_stage_k<OCN_STAGE_SW_NEXT_STEP>(b, t, rr, sw, tau, nbad, s);
+    case OCN_STAGE_HH_SHIFT: return launch_stage_k<OCN_STAGE_HH_SHIFT>(b, t, rr, sw, tau, nbad, s);
+    case OCN_STAGE_HH_INIT:   // every level (full): the register march where the tables allow it
+        if (use_march(cp)) return launch_march(b, rb, MarchHhInit{*b, t, (int)sw.full_free_surface, true}, s);
+        return launch_stage_k<OCN_STAGE_HH_INIT>(b, t, rb, sw, tau, nbad, s);
+    case OCN_STAGE_CHECK_SSH_ERR: return launch_stage_k<OCN_STAGE_CHECK_SSH_ERR>(b, t, ri, sw, tau, nbad, s);
+    default: return set_error(OCN_ERR_ARG, "unknown stage id");
     }
 }
 

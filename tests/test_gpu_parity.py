@@ -112,7 +112,7 @@ def test_tracer_kernels_match_reference(amd, geom):
 
 
 def build_model(amd, case, graph=False, fused=True, compact=True, overlap=None, march=True, flip=True,
-                recompute=True, rank=0, nranks=1, onepass=True, onepass_last=True, x2=True):
+                recompute=True, rank=0, nranks=1, onepass=True, onepass_last=True, x2=True, batch=True):
     b = case["basin"]
     basin = amd.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"], rlat=b["rlat"],
                             curve_grid=b["curve_grid"], mask=case["mask"],
@@ -130,6 +130,7 @@ def build_model(amd, case, graph=False, fused=True, compact=True, overlap=None, 
     m.set_onepass(onepass)
     m.set_onepass_last(onepass_last)
     m.set_x2(x2)
+    m.set_batch(batch)
     if graph:
         m.set_graph(True)
     return m
@@ -156,7 +157,7 @@ def compare_case(m, case, name, whole=True):
 
 
 @pytest.mark.parametrize("mode", ["compact", "nox2", "noonepass", "nolast", "norecompute", "noflip", "pointwise",
-                                  "fused", "stages", "serial", "overlap2"])
+                                  "fused", "stages", "stages_compact", "serial", "overlap2", "nobatch"])
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES + cases.TOPO_CASES)
 def test_end_to_end_matches_reference(amd, name, mode):
     """compact = the default: the fused step reading the compact static fields, fused A / B /
@@ -171,27 +172,30 @@ def test_end_to_end_matches_reference(amd, name, mode):
     pointwise = compact with every launch one thread per point; overlap2 = compact with the
     role-flip steps' exchanges overlapped too (OCN_OPT_OVERLAP = 2); fused =
     the 4-launch step on the 2-D real(4) arrays; serial = compact without the overlap; stages =
-    the reference's 11 envoke stages."""
+    the reference's 11 envoke stages on the 2-D real(4) arrays (the ocn_<stage> kernel entries);
+    stages_compact = the 11 stages over the compact tables (hh_init as the register march); nobatch = compact with one launch per block and launch group
+    (every other mode batches the blocks of a device, OCN_OPT_BATCH)."""
     case = cases.load_e2e(name)
     compact = mode in ("compact", "nox2", "noonepass", "nolast", "norecompute", "noflip", "serial", "pointwise",
-                       "overlap2")
-    m = build_model(amd, case, fused=mode != "stages", compact=compact,
+                       "overlap2", "nobatch", "stages_compact")
+    m = build_model(amd, case, fused=mode not in ("stages", "stages_compact"), compact=compact,
                     overlap=2 if mode == "overlap2" else int(mode != "serial"),
                     march=mode != "pointwise", flip=mode != "noflip", recompute=mode != "norecompute",
-                    onepass=mode != "noonepass", onepass_last=mode != "nolast", x2=mode != "nox2")
+                    onepass=mode != "noonepass", onepass_last=mode != "nolast", x2=mode != "nox2",
+                    batch=mode != "nobatch")
     m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
     assert m.compact_active == compact
     bad = compare_case(m, case, name)
     flip_used, one_used, x2_used = m.flip_active, m.onepass_active, m.x2_active
     m.close()
     assert not bad, f"{name}: fields differ from the reference: {bad}"
-    if mode in ("compact", "nox2", "noonepass", "nolast", "norecompute", "serial", "overlap2"):   # tracer runs included
+    if mode in ("compact", "nox2", "noonepass", "nolast", "norecompute", "serial", "overlap2", "nobatch"):   # tracer runs included
         assert flip_used, f"{name}: role-flip steps not used"
     full_sw = case["sw"]["trans_terms"] > 0 and case["sw"]["ksw_lat"] > 0 and not case["sw"].get("use_tracers", 0)
     one_block = tuple(case["bxy"]) == (1, 1)
     if mode == "compact" and one_block and full_sw:
         assert one_used, f"{name}: one-pass steps not used"
-    if mode == "compact" and not one_block and full_sw and case["steps"] >= 3:
+    if mode in ("compact", "nobatch") and not one_block and full_sw and case["steps"] >= 3:
         assert x2_used, f"{name}: x2 steps not used"
     if mode in ("nox2", "nolast"):
         assert not x2_used
@@ -671,3 +675,22 @@ def test_user_sync_of_second_buffer_fields(amd):
         m.field_ptr(0, nm)   # the values return to the fields' own buffers
         check_sync(nm)
     m.close()
+
+
+@pytest.mark.parametrize("name", ["bs_b4x2_tr_s60", "box70x54_b3x2_s20"])
+def test_block_batching_cuts_launches(amd, name):
+    """OCN_OPT_BATCH: with several blocks on the device each launch group goes out once for all of
+    them -- fewer launches per step than one per block, and the same bits (the e2e `nobatch` mode
+    covers the unbatched path against the reference too)."""
+    case = cases.load_e2e(name)
+    counts, digests = [], []
+    for batch in (False, True):
+        m = build_model(amd, case, batch=batch).init()
+        m.step(2, tau=1.0, check_every=1).synchronize()    # the one-time checks and tables
+        n0 = amd._lib.launch_count()
+        m.step(case["steps"] - 2, tau=1.0, check_every=1).synchronize()
+        counts.append(amd._lib.launch_count() - n0)
+        digests.append(compare_case(m, case, name))
+        m.close()
+    assert digests == [[], []], digests
+    assert counts[1] < counts[0], counts
