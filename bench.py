@@ -250,6 +250,36 @@ def load_traffic(amd, stage: str, cells: int, compact: bool, box, blocks):
         return None
 
 
+SHADER_CLOCK_GHZ = 2.4          # MI355X peak engine clock (MI355X_MICROARCH.md)
+SIMDS = 256 * 4
+
+
+def load_valu(amd, stage: str, launch_ms: float, box, blocks):
+    """The dominant kernel's VALU issue from the committed SQ counter pass (profiles/sq_valu.json,
+    scripts/sq_valu.py) -- only for the one-pass step, and only when that pass was taken on this
+    exact library build and workload.  issue_floor_ms: its VALU instructions spread over the
+    1024 SIMDs at one wave64 instruction per quad-cycle at the peak clock (the time the launch
+    would take if VALU issue were its only limit); issue_frac = that floor / the live launch time."""
+    if stage != "onepass":
+        return None
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "sq_valu.json")))
+        if (d.get("build_id") != amd.build_id() or list(d.get("box", [])) != list(box) or
+                list(d.get("blocks", [])) != list(blocks)):
+            return None
+        pl, pw = d["per_launch"], d["per_wave"]
+        floor_ms = pl["SQ_INSTS_VALU"] * 4.0 / SIMDS / (SHADER_CLOCK_GHZ * 1e9) * 1e3
+        wc = pw["SQ_WAVE_CYCLES"]
+        return {"insts_per_launch": int(pl["SQ_INSTS_VALU"]), "issue_floor_ms": round(floor_ms, 4),
+                "issue_frac": round(floor_ms / launch_ms, 4),
+                "per_wave_frac": {"valu_active": round(pw["SQ_ACTIVE_INST_VALU"] / wc, 4),
+                                  "wait_inst_any": round(pw["SQ_WAIT_INST_ANY"] / wc, 4),
+                                  "wait_any": round(pw["SQ_WAIT_ANY"] / wc, 4)},
+                "source": "profiles/sq_valu.json"}
+    except Exception:
+        return None
+
+
 def launch_ranks(n: int) -> int:
     """torch.distributed.run with n processes on this node (127.0.0.1 rendezvous), each running
     this script with the same arguments; returns its exit status.  The parent stays GPU-free."""
@@ -414,6 +444,7 @@ def main():
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": load_traffic(amd, dom, local_cells, compact, [nxbox, nybox], [bx, by]),
+                    "valu": load_valu(amd, dom, stage_ms[dom], [nxbox, nybox], [bx, by]),
                     "alg_bytes_per_launch": int(alg), "launch_ms": round(stage_ms[dom], 4)}
         step_gbs = B_ALG * cells * args.steps / dt / 1e9 / world
         moved = b_path * cells * args.steps / dt / 1e9 / world

@@ -1422,12 +1422,16 @@ __device__ __forceinline__ double rcp_count(unsigned c)
 #ifndef OCN_STEP_CARRY
 #define OCN_STEP_CARRY 1   // shifted weights / v kept in the ring (no second shift), sh * ffs as sh
 #endif
+#ifndef OCN_STEP_NBAD_ACC
+#define OCN_STEP_NBAD_ACC 0   // 1: check_ssh_err counted per lane over the tile, one atomic at its end (no per-row branch)
+#endif
 #ifndef OCN_STEP_MZ_FORCE
 #define OCN_STEP_MZ_FORCE 0   // A/B only: the known-constant variant assumes mu = +0 (a measurement of that saving)
 #endif
 #ifndef OCN_STEP_PF2
 #define OCN_STEP_PF2 0   // 1: the known-constant variant issues each row's loads two rows ahead (measured: no gain)
 #endif
+static_assert(!(OCN_STEP_NBAD_ACC && OCN_STEP_PF2), "OCN_STEP_NBAD_ACC: the one-row-ahead loop only");
 // StepRegs::Win: 4 rows, written out for kRing phases (MarchStep::march); even with OCN_STEP_PF2,
 // so that the batch a phase takes (phase parity) is known in every unrolled phase
 constexpr int kRing = OCN_STEP_PF2 ? 6 : 5;
@@ -1464,6 +1468,7 @@ struct StepRegs {
     unsigned nrows, rn;               // table stride, row index of n (n - bnd_y1)
     double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
     double tau, inv_tau, f;
+    int nbad_cnt;                      // OCN_STEP_NBAD_ACC: this lane's check_ssh_err count of the tile
     double hr0, mu0;                   // known-constant variant: the uniform h_r and mu (MarchStep::kc)
     const __attribute__((address_space(3))) double *lds;   // OCN_STEP_LDS: the workgroup's row constants
     unsigned rlo;                                            // table row of lds row 0
@@ -1752,6 +1757,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct M
         bool lu = false, cu = false, cv = false, uu = false;   // uu: luu (LAST's vort / str_s)
         double sshn = 0.0, fx = 0.0, un = 0.0, fa = 0.0, vn = 0.0, fb = 0.0;
         double vort = 0.0, sts = 0.0, stt = 0.0, rxa = 0.0, rxd = 0.0, rya = 0.0, ryd = 0.0;   // LAST
+        int dbad = 0;   // OCN_STEP_NBAD_ACC: the row's change to the lane's check_ssh_err count
     };
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
     // uv_trans_math, uv_diff2_math, sw_update_uv_math written out over the shared products)
@@ -1864,7 +1870,8 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct M
             }
             // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
             const bool bd = o.lu && !(sshn < 10000.0 && sshn > -10000.0);
-            if (__builtin_expect(nbad && bd != (E && bad), 0)) atomicAdd(nbad, bd ? 1 : -1);
+            if (OCN_STEP_NBAD_ACC) o.dbad = (int)bd - (int)(E && bad);   // (the re-run replaces the first count)
+            else if (__builtin_expect(nbad && bd != (E && bad), 0)) atomicAdd(nbad, bd ? 1 : -1);
             bad = bd;
             return;
         }
@@ -2018,6 +2025,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct M
                 x.rotate();
             }
         }
+        if (OCN_STEP_NBAD_ACC && nbad && x.nbad_cnt != 0) atomicAdd(nbad, x.nbad_cnt);
 #else
         if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
             for (int n = n0;; n += kRing) {
@@ -2099,6 +2107,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct M
 #endif
 #if OCN_STEP_BUFST
         store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
+        if (OCN_STEP_NBAD_ACC) x.nbad_cnt += o.dbad;
 #endif
         ++x.rn;
         fb = fbn;

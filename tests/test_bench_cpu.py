@@ -70,3 +70,20 @@ def test_traffic_needs_matching_stamp(tmp_path, monkeypatch):
     assert bench.load_traffic(_Amd("abc"), "onepass", 4096, True, [64, 64], [2, 1]) is None
     assert bench.load_traffic(_Amd("abc"), "onepass", 2048, True, [64, 64], [1, 1]) is None
     assert bench.load_traffic(_Amd("abc"), "fused_b", 4096, True, [64, 64], [1, 1]) is None
+
+
+def test_valu_needs_matching_stamp(tmp_path, monkeypatch):
+    """roofline.valu: the one-pass kernel's VALU issue floor from the committed SQ pass, only on the
+    build and workload it was taken on; 1024 SIMDs x 1 wave64 instruction per quad-cycle at 2.4 GHz."""
+    per_launch = {"SQ_INSTS_VALU": 1024 * 2.4e6 / 4, "SQ_WAVES": 10}     # 1 ms of issue
+    per_wave = {"SQ_WAVE_CYCLES": 100.0, "SQ_ACTIVE_INST_VALU": 60.0, "SQ_WAIT_INST_ANY": 30.0, "SQ_WAIT_ANY": 10.0}
+    rec = {"build_id": "abc", "box": [64, 64], "blocks": [1, 1], "per_launch": per_launch, "per_wave": per_wave}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "sq_valu.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    v = bench.load_valu(_Amd("abc"), "onepass", 2.0, [64, 64], [1, 1])
+    assert v["issue_floor_ms"] == 1.0 and v["issue_frac"] == 0.5
+    assert v["per_wave_frac"] == {"valu_active": 0.6, "wait_inst_any": 0.3, "wait_any": 0.1}
+    assert bench.load_valu(_Amd("other"), "onepass", 2.0, [64, 64], [1, 1]) is None
+    assert bench.load_valu(_Amd("abc"), "onepass", 2.0, [64, 64], [2, 1]) is None
+    assert bench.load_valu(_Amd("abc"), "hh_init", 2.0, [64, 64], [1, 1]) is None
