@@ -56,6 +56,8 @@ LAUNCH_BYTES = {
     # the same with the forcing RHSx / RHSy known to be zero and h_r, mu known to be uniform
     # (checked once per call chain; taken as kernel constants, not read)
     "onepass_z": (97, 97), "onepass_last_z": (153, 153),
+    # ... with h_r read (a non-uniform rest depth: the OCN_KC_KNOWN_HR variant)
+    "onepass_h": (105, 105), "onepass_last_h": (161, 161),
     "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
     # tracer runs: CA also stores hh_init's hhq_p (read by tran_diff_tracer); per tracer and step:
     # tran_diff_fluxes (lcu, lcv, hhu, hhv, ff, ffp, ubrtr, vbrtr, mu in; flux_x, flux_y out),
@@ -64,6 +66,12 @@ LAUNCH_BYTES = {
     "hqp": (8, 8),
     "tr_fluxes": (73, 97), "tr_tracer": (57, 69), "tr_next": (41, 44),
 }
+
+
+def _kc(zero) -> str:
+    """The one-pass launch kind's suffix: zero = True (the known-constant variant), "h" (known
+    constants, h_r read), False (the general variant)."""
+    return "_z" if zero is True else "_h" if zero == "h" else ""
 
 
 def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
@@ -85,9 +93,9 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
                         ("tracer_next_step", "tr_next")] * tracers
         return out
     if one and lazy:   # an open one-pass sequence (OCN_OPT_LAZY_TAIL): every step one launch, no tail
-        return [("onepass", "onepass" + ("_z" if zero else ""))] * steps
+        return [("onepass", "onepass" + _kc(zero))] * steps
     if one and flip and steps >= 2:   # steps 1 .. K-1 (the state is unchanged since the last call / init)
-        z = "_z" if zero else ""
+        z = _kc(zero)
         out = [("onepass", "onepass" + z)] * (steps - 1)
         if ring:   # several blocks: CA + the standard last step
             out += [("fused_ca", "ca_hh"), ("fused_b", "b_full"), ("fused_c1", "c1"), ("hh_init", "c2_full")]
@@ -129,7 +137,7 @@ def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one:
     for n in calls:
         out += call_launches(n, flip, rc, ring, one, tracers, zero=zero, lazy=lazy)
     if lazy and one:
-        out += [(t, k + ("_z" if zero and t == "onepass" else "")) for t, k in TAIL_LAUNCHES]
+        out += [(t, k + (_kc(zero) if t == "onepass" else "")) for t, k in TAIL_LAUNCHES]
     return out
 
 
@@ -322,6 +330,9 @@ def main():
                     help="halo exchanges beside inner launches: 0 never, 1 standard steps and the one-pass steps' side "
                          "chain, 2 role-flip steps too, "
                          "-1 the library default (2 with RCCL peers, else 1)")
+    ap.add_argument("--topography", action="store_true",
+                    help="a non-uniform rest depth (a synthetic smooth basin, 20..180 m) instead of 100 m everywhere: "
+                         "the one-pass steps read h_r (what a real-depth basin runs)")
     ap.add_argument("--no-batch", action="store_true",
                     help="several blocks on a GPU: one launch per block and launch group (no block batching)")
     ap.add_argument("--blocks", default=None,
@@ -354,6 +365,12 @@ def main():
         nxbox, nybox = (n, n) if args.scaling == "strong" else (n * bx, n * by)
         basin, sw = amd.BasinConfig(nx=nxbox + 4, ny=nybox + 4), amd.SWConfig()
         workload = f"{nxbox}x{nybox} box"
+        if args.topography:   # float32 (nx-4, ny-4), Fortran order, as a basin.par topography file holds it
+            import numpy as np
+            x = np.linspace(-1.0, 1.0, nxbox, dtype=np.float64)[:, None]
+            y = np.linspace(-1.0, 1.0, nybox, dtype=np.float64)[None, :]
+            basin.topography = np.asfortranarray((100.0 + 80.0 * np.cos(np.pi * x) * np.cos(np.pi * y)).astype(np.float32))
+            workload += ", topography"
     else:
         # the Black Sea basin: mask bits and basin / sw.par parameters exactly as the reference's
         # run uses them (input data of the golden fixture; nothing of the reference runs here)
@@ -417,7 +434,7 @@ def main():
     flip = model.flip_active
     rc = model.recompute_active
     one = model.onepass_active
-    one_zero = model.onepass_zero
+    one_zero = True if model.onepass_zero else "h" if model.onepass_hr else False
     model_overlap = model.overlap_level
     if world > 1:
         t = torch.tensor([dt], device="cuda")
@@ -451,7 +468,9 @@ def main():
         out = {"metric": METRIC, "value": value, "unit": "cell-updates/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
                "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
-               "data": ("synthetic (Gaussian SSH hump in a closed flat-bottom box, SURVEY.md 8d)" if args.basin == "box"
+               "data": (("synthetic (Gaussian SSH hump in a closed box with a smooth synthetic bottom, 20..180 m)"
+                         if args.topography else
+                         "synthetic (Gaussian SSH hump in a closed flat-bottom box, SURVEY.md 8d)") if args.basin == "box"
                         else "the reference's data/BS mask and basin parameters, its Gaussian initial state"),
                "config": {"workload": f"{workload}, {bx}x{by} blocks ({bx * by // world} per GPU), "
                                       f"{'sw.par defaults' if args.basin == 'box' else 'BS sw.par'}, tau=1s",
@@ -461,7 +480,10 @@ def main():
                           "static_fields": "compact" if compact else "2-D arrays",
                           "march": bool(compact and not args.stages and not args.no_march),
                           "role_flip_steps": flip, "recompute_steps": rc, "onepass_steps": one,
-                          "onepass_known_constants": one_zero,
+                          "onepass_known_constants": one_zero is True,
+                          "onepass_variant": ("known constants" if one_zero is True else
+                                              "known constants, h_r read" if one_zero == "h" else "general")
+                                             if one else None,
                           "steps_per_call": spc, "calls": len(calls),
                           "call_tail": ("pending between calls (OCN_OPT_LAZY_TAIL), formed once by ocn_ctx_complete "
                                         "inside the timed region") if lazy else "formed by every call",

@@ -367,7 +367,8 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
  * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
  * the forcing and fallback values known to be zero and h_r, mu known to be uniform, taken as
- * kernel constants instead of being read). */
+ * kernel constants instead of being read; 3: the same with h_r read -- a non-uniform rest depth,
+ * e.g. a topography file). */
 int ocn_ctx_set_option(ocn_ctx *ctx, int32_t key, int64_t value);
 int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,

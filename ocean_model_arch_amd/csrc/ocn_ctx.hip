@@ -245,7 +245,7 @@ struct StepKind {
 }  // namespace ocn
 
 // ocn_ctx::fb_state
-enum { kFbUnchecked = 0, kFbDevice = 1, kFbZero = 2, kFbGeneral = 3 };
+enum { kFbUnchecked = 0, kFbDevice = 1, kFbZero = 2, kFbGeneral = 3, kFbHr = 4 };
 
 #ifndef OCN_COMM_PRIO
 #define OCN_COMM_PRIO 1   // the comm stream at the device's highest stream priority
@@ -316,7 +316,8 @@ struct ocn_ctx {
     // and forcing +0.0, h_r and mu uniform): kFbUnchecked until a check ran after the arrays last
     // changed from outside the step; kFbDevice = its verdict is in device memory (d_fbz; both
     // variants are launched and the device picks, ocn_ctx.hip never waits for it) until a host
-    // sync the caller makes anyway reads it (learn_fb): kFbZero / kFbGeneral
+    // sync the caller makes anyway reads it (learn_fb): kFbZero / kFbHr (all but h_r: a
+    // non-uniform rest depth, read by the OCN_KC_KNOWN_HR variant) / kFbGeneral
     mutable int fb_state = 0;
     int kc_mode = 0;             // OCN_KC_* of the current call's one-pass launches
     int32_t *d_fbz = nullptr;    // the check's verdict word
@@ -2494,7 +2495,7 @@ static void learn_fb(ocn_ctx *c)
     if (c->fb_state != kFbDevice) return;
     int32_t f = 0;
     if (hipMemcpy(&f, c->d_fbz, sizeof(f), hipMemcpyDeviceToHost) != hipSuccess) return;
-    c->fb_state = f == 0 ? kFbZero : kFbGeneral;
+    c->fb_state = f == 0 ? kFbZero : f == 1 ? kFbHr : kFbGeneral;
 }
 
 // The one-pass variant of this call (OCN_KC_*): the known-constant one only when its precondition
@@ -2521,7 +2522,8 @@ static int prepare_kc(ocn_ctx *c, bool x2 = false)
         c->fb_state = kFbDevice;
         c->fb_x2 = x2;
     }
-    c->kc_mode = c->fb_state == kFbZero ? OCN_KC_KNOWN : c->fb_state == kFbGeneral ? OCN_KC_GENERAL : OCN_KC_DEVICE;
+    c->kc_mode = c->fb_state == kFbZero ? OCN_KC_KNOWN : c->fb_state == kFbHr ? OCN_KC_KNOWN_HR
+               : c->fb_state == kFbGeneral ? OCN_KC_GENERAL : OCN_KC_DEVICE;
     return OCN_OK;
 }
 
@@ -2872,10 +2874,11 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_FLIP: *value = c->flip && c->flip_used; return OCN_OK;
     case OCN_OPT_RECOMPUTE: *value = c->recompute && c->rc_used; return OCN_OK;
     case OCN_OPT_ONEPASS: {
-        // 2: the known-constant variant ran (chosen by the host, or by the device check whose verdict
-        // the host has read since)
+        // 2: the known-constant variant ran, 3: the known-constant variant reading h_r (chosen by the
+        // host, or by the device check whose verdict the host has read since)
         const bool z = c->kc_mode == OCN_KC_KNOWN || (c->kc_mode == OCN_KC_DEVICE && c->fb_state == kFbZero);
-        *value = c->onepass && c->one_used ? (z ? 2 : 1) : 0;
+        const bool h = c->kc_mode == OCN_KC_KNOWN_HR || (c->kc_mode == OCN_KC_DEVICE && c->fb_state == kFbHr);
+        *value = c->onepass && c->one_used ? (z ? 2 : h ? 3 : 1) : 0;
         return OCN_OK;
     }
     case OCN_OPT_KNOWN_CONSTANTS: *value = c->known_const; return OCN_OK;

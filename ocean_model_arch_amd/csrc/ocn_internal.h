@@ -122,9 +122,10 @@ int launch_fill_field(const ocn_block &g, double *p, double v, hipStream_t s);
 // interior whose stencils stay off the halos the exchanges fill.
 // kc: which variant -- OCN_KC_GENERAL reads h_r, mu, the forcing and D's fallback values;
 // OCN_KC_KNOWN takes them as +0.0 / the uniform values kc[0], kc[1] (device memory, written by
-// launch_fallback_check); OCN_KC_DEVICE launches both, each running only if the device verdict
-// *flag (launch_fallback_check's) is its own -- no host wait for the check.
-enum { OCN_KC_GENERAL = 0, OCN_KC_KNOWN = 1, OCN_KC_DEVICE = 2 };
+// launch_fallback_check); OCN_KC_KNOWN_HR the same but reads h_r (a non-uniform rest depth:
+// topography); OCN_KC_DEVICE launches all three, each running only if the device verdict *flag
+// (launch_fallback_check's: bit 0 h_r varies, bit 1 anything else) is its own -- no host wait.
+enum { OCN_KC_GENERAL = 0, OCN_KC_KNOWN = 1, OCN_KC_DEVICE = 2, OCN_KC_KNOWN_HR = 3 };
 struct OnepassKC { int mode; const int32_t *flag; const double *kc; };
 // own (sw_stencils.h own_class bits, not with last): the halo points neighbour blocks own hold the
 // neighbours' state two points deep -- D there is formed as on their interior (MarchStep X2).

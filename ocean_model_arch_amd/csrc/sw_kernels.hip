@@ -1561,7 +1561,7 @@ struct StepRegs {
 // the neighbours' state two points deep (ocn_ctx.hip one_step_x2: one 2-deep exchange per step),
 // so D there is formed here as the neighbour forms it on its interior -- what the reference's
 // exchanges of D deliver -- and the march covers the whole interior.
-template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct MarchStep {
+template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR = false> struct MarchStep {
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
     static constexpr int kWaves = OCN_STEP_WAVES;
@@ -1573,11 +1573,13 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct M
     const double *kc; const int32_t *fbz; int gate;
     unsigned own;   // X2: own_class bits of the halo points neighbour blocks own
     static constexpr bool kGate = true;
+    // gate (OCN_KC_DEVICE): which verdict of the check (launch_fallback_check's flag word: bit 0 =
+    // h_r not uniform, bit 1 = anything else) this launch is for -- 1: none, 3: h_r only, 2: bit 1
     __device__ __forceinline__ bool enabled() const
     {
         if (gate == 0) return true;
         const int f = *(const volatile int32_t *)fbz;
-        return gate == 1 ? f == 0 : f != 0;
+        return gate == 1 ? f == 0 : gate == 3 ? f == 1 : (f & 2) != 0;
     }
 
     // a / tau (sw_update_uv_math qtau).  P2: tau is a power of two, so a / tau is a * (1 / tau) bit
@@ -1592,7 +1594,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct M
         const Pt c = I(m, n), c1 = I(m, n + 1), c2 = I(m, n + 2);
         q.u = ld(t.f(OCN_UBRTR), c2); q.up = ld(t.f(OCN_UBRTRP), c2);
         q.ssh = ld(t.f(OCN_SSH), c2); q.shp = ld(t.f(OCN_SSHP), c2);
-        q.hr = ZF ? x.hr0 : ld(t.f(OCN_HHQ_REST), c2);
+        q.hr = ZF && !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c2);
         q.bits = ld(t.bits, c2);
         q.v = ld(t.f(OCN_VBRTR), c1); q.vp = ld(t.f(OCN_VBRTRP), c1); q.mu = ZF ? x.mu0 : ld(t.f(OCN_MU), c1);
         if (ZF) q.rhsx = q.rhsy = 0.0;
@@ -1969,7 +1971,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false> struct M
         {
             const Pt c = I(L.m, n0), c1 = I(L.m, n0 + 1);
             x.up.s<0>(2) = ld(t.f(OCN_UBRTRP), c1); x.ssh.s<0>(2) = ld(t.f(OCN_SSH), c1);
-            x.shp.s<0>(2) = ld(t.f(OCN_SSHP), c1); x.hr.s<0>(2) = ZF ? x.hr0 : ld(t.f(OCN_HHQ_REST), c1);
+            x.shp.s<0>(2) = ld(t.f(OCN_SSHP), c1); x.hr.s<0>(2) = ZF && !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c1);
             x.bits.s<0>(2) = ld(t.bits, c1); x.u.s<0>(2) = ld(t.f(OCN_UBRTR), c1);
             x.vp.s<0>(1) = ld(t.f(OCN_VBRTRP), c);
             // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
@@ -2329,9 +2331,9 @@ struct FallbackCheck {
     {
         const Pt c = geo(&b)(m, n), c0 = geo(&b)(r.m0, r.n0);
         if (m == r.m0 && n == r.n0) { kc[0] = ld(hr, c0); kc[1] = ld(mu, c0); }
-        if (fbits64(ld(hr, c)) != fbits64(ld(hr, c0))) OCN_ATOMIC_OR(flag, 1);
+        if (fbits64(ld(hr, c)) != fbits64(ld(hr, c0))) OCN_ATOMIC_OR(flag, 1);   // bit 0: h_r varies
         if (m < r.m0 - 1 || m > r.m1 + 1 || n < r.n0 - 1 || n > r.n1 + 1) return;   // the ring of r +- 2
-        if (fbits64(ld(mu, c)) != fbits64(ld(mu, c0))) OCN_ATOMIC_OR(flag, 1);
+        if (fbits64(ld(mu, c)) != fbits64(ld(mu, c0))) OCN_ATOMIC_OR(flag, 2);
         const unsigned bc = ld(bits, c);
         const bool owned = (own >> (own_class(m, b.nx_start, b.nx_end) * 3u + own_class(n, b.ny_start, b.ny_end))) & 1u;
         const bool hh_rng = owned || (m >= b.nx_start - 1 && m <= b.nx_end && n >= b.ny_start - 1 && n <= b.ny_end);
@@ -2344,7 +2346,7 @@ struct FallbackCheck {
         if (!(in && (bc & (1u << OCN_LUU)))) bad |= nz(vort) || nz(sts);
         if (!(in && (bc & (1u << OCN_LU)))) bad |= nz(stt);
         if (m >= r.m0 && m <= r.m1 && n >= r.n0 && n <= r.n1) bad |= nz(rx) || nz(ry);
-        if (bad) OCN_ATOMIC_OR(flag, 1);
+        if (bad) OCN_ATOMIC_OR(flag, 2);   // bit 1: a fallback value or the forcing is not +0.0, or mu varies
     }
 };
 
@@ -2382,24 +2384,29 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
     // OCN_KC_DEVICE: the known-constant variant runs if the device check found its conditions, the
     // general one otherwise (each launch's workgroups read the verdict and return at once if it
     // is not theirs)
-    const int gz = kc.mode == OCN_KC_DEVICE ? 1 : 0, gg = kc.mode == OCN_KC_DEVICE ? 2 : 0;
-#define OCN_STEP_LAUNCH(P, L, Z, X, G)                                                                           \
+    const bool dev = kc.mode == OCN_KC_DEVICE;
+    const int gz = dev ? 1 : 0, gh = dev ? 3 : 0, gg = dev ? 2 : 0;
+#define OCN_STEP_LAUNCH(P, L, Z, X, H, G)                                                                        \
     do {                                                                                                          \
-        const MarchStep<P, L, Z, X> k_{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out, kc.kc, kc.flag, G, own};   \
+        const MarchStep<P, L, Z, X, H> k_{*b, t, sw, tau, nbad, sshp_out, up_out, vp_out, kc.kc, kc.flag, G, own}; \
         RC_K(frame_of ? launch_step_frame(b, r, *frame_of, k_, s) : launch_step(b, r, k_, s));                   \
     } while (0)
-#define OCN_STEP_VARIANT(Z, G)                                                                                   \
+#define OCN_STEP_VARIANT(Z, H, G)                                                                                \
     do {                                                                                                         \
-        if (own) { if (p2) OCN_STEP_LAUNCH(true, false, Z, true, G); else OCN_STEP_LAUNCH(false, false, Z, true, G); } \
-        else if (last) { if (p2) OCN_STEP_LAUNCH(true, true, Z, false, G); else OCN_STEP_LAUNCH(false, true, Z, false, G); } \
-        else if (p2) OCN_STEP_LAUNCH(true, false, Z, false, G);                                                    \
-        else OCN_STEP_LAUNCH(false, false, Z, false, G);                                                           \
+        if (own) { if (p2) OCN_STEP_LAUNCH(true, false, Z, true, H, G); else OCN_STEP_LAUNCH(false, false, Z, true, H, G); } \
+        else if (last) { if (p2) OCN_STEP_LAUNCH(true, true, Z, false, H, G); else OCN_STEP_LAUNCH(false, true, Z, false, H, G); } \
+        else if (p2) OCN_STEP_LAUNCH(true, false, Z, false, H, G);                                                 \
+        else OCN_STEP_LAUNCH(false, false, Z, false, H, G);                                                        \
     } while (0)
-    if (kc.mode != OCN_KC_GENERAL) {
-        OCN_STEP_VARIANT(true, gz);
-        if (kc.mode == OCN_KC_KNOWN) return OCN_OK;
+    if (kc.mode == OCN_KC_KNOWN || dev) {
+        OCN_STEP_VARIANT(true, false, gz);
+        if (!dev) return OCN_OK;
     }
-    OCN_STEP_VARIANT(false, gg);
+    if (kc.mode == OCN_KC_KNOWN_HR || dev) {
+        OCN_STEP_VARIANT(true, true, gh);
+        if (!dev) return OCN_OK;
+    }
+    OCN_STEP_VARIANT(false, false, gg);
 #undef OCN_STEP_VARIANT
 #undef OCN_STEP_LAUNCH
     return OCN_OK;

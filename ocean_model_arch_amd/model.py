@@ -267,6 +267,12 @@ class OceanModel:
         return self.option(_lib.OPT_ONEPASS) == 2
 
     @property
+    def onepass_hr(self) -> bool:
+        """Whether those steps took the forcing and the fallback values as known zeros and mu as a
+        known uniform value, but read a non-uniform h_r (a topography)."""
+        return self.option(_lib.OPT_ONEPASS) == 3
+
+    @property
     def compact_active(self) -> bool:
         """Whether the last step() read the compact static fields."""
         return bool(self.option(_lib.OPT_COMPACT))

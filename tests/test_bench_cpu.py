@@ -87,3 +87,13 @@ def test_valu_needs_matching_stamp(tmp_path, monkeypatch):
     assert bench.load_valu(_Amd("other"), "onepass", 2.0, [64, 64], [1, 1]) is None
     assert bench.load_valu(_Amd("abc"), "onepass", 2.0, [64, 64], [2, 1]) is None
     assert bench.load_valu(_Amd("abc"), "hh_init", 2.0, [64, 64], [1, 1]) is None
+
+
+def test_hr_variant_bytes():
+    """The known-constant one-pass variant that reads h_r (a topography) moves 8 B per cell more
+    than the one with h_r a constant and 24 B less than the general one (101 one-pass launches in
+    100 steps: the tail re-runs one)."""
+    z = bench.step_bytes(True, [100], flip=True, one=True, zero=True, lazy=True)
+    h = bench.step_bytes(True, [100], flip=True, one=True, zero="h", lazy=True)
+    g = bench.step_bytes(True, [100], flip=True, one=True, zero=False, lazy=True)
+    assert abs(h - z - 8.0 * 1.01) < 1e-9 and abs(g - h - 24.0 * 1.01) < 1e-9

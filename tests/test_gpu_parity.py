@@ -202,22 +202,24 @@ def test_end_to_end_matches_reference(amd, name, mode):
 
 
 @pytest.mark.parametrize("name", cases.TOPO_CASES)
-def test_topography_general_variant_matches_reference(amd, name):
+def test_topography_variants_match_reference(amd, name):
     """A non-uniform rest depth from a basin.par topography file (control/init_data.f90:115-120):
-    the one-pass steps run their general variant (h_r read, not a kernel constant) -- on one block,
-    and with x2 steps (h_r's second halo ring from the neighbours) on several -- bitwise against the
-    reference run that read the same file; also in 1-step calls (lazy tail)."""
+    the one-pass steps run their known-constant variant that reads h_r (OCN_KC_KNOWN_HR; the
+    forcing and fallback values known zeros, mu uniform) -- and with OCN_OPT_KNOWN_CONSTANTS 0 the
+    general variant -- on one block, and with x2 steps (h_r's second halo ring from the neighbours)
+    on several, bitwise against the reference run that read the same file; also in 1-step calls
+    (lazy tail)."""
     case = cases.load_e2e(name)
-    for calls in ([case["steps"]], [1] * case["steps"]):
-        m = build_model(amd, case).init()
+    for kc, calls in ((True, [case["steps"]]), (True, [1] * case["steps"]), (False, [case["steps"]])):
+        m = build_model(amd, case).set_known_constants(kc).init()
         for n in calls:
             m.step(n, tau=1.0, check_every=1)
         m.synchronize()
-        one, zero, x2 = m.onepass_active, m.onepass_zero, m.x2_active
+        one, zero, hr, x2 = m.onepass_active, m.onepass_zero, m.onepass_hr, m.x2_active
         bad = compare_case(m, case, name)
         m.close()
-        assert not bad, f"{name} ({len(calls)} calls): fields differ from the reference: {bad}"
-        assert one and not zero, (one, zero)
+        assert not bad, f"{name} ({len(calls)} calls, kc {kc}): fields differ from the reference: {bad}"
+        assert one and not zero and hr == kc, (one, zero, hr, kc)
         assert x2 == ("_b1x1_" not in name), x2
 
 
