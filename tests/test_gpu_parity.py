@@ -696,3 +696,21 @@ def test_block_batching_cuts_launches(amd, name):
         m.close()
     assert digests == [[], []], digests
     assert counts[1] < counts[0], counts
+
+
+@pytest.mark.parametrize("name", ["box70x54_b3x2_s20", "bs_b4x2_tr_s60"])
+def test_rccl_single_rank_matches_reference(amd, name):
+    """RCCL on the hardware: one pool box has one GPU and RCCL refuses two ranks on one device, so
+    the production communicator is exercised as a world of one -- ncclCommInitRank through
+    ocn_ctx_attach_comm, the step's vote as ncclAllReduce, the halo plans' grouped calls (all
+    exchanges local) and the per-call h_r refresh of a communicating context -- bitwise against the
+    reference fixture."""
+    case = cases.load_e2e(name)
+    m = build_model(amd, case)
+    m.attach_comm(amd.make_unique_id())
+    m.init().step(case["steps"], tau=1.0, check_every=1).synchronize()
+    bad = compare_case(m, case, name)
+    flip = m.flip_active
+    m.close()
+    assert not bad, f"{name}: fields differ from the reference over an RCCL communicator: {bad}"
+    assert flip
