@@ -75,6 +75,11 @@ def main():
             agg[stage][c] += d.get(c, [])
         agg[stage]["names"].add(name)
     for stage, d in agg.items():
+        # the launches that ran: the one-pass step's first call also launches the variants the device
+        # verdict does not select, whose workgroups return at once (a few KB each) -- left out
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            top = max(d[c], default=0.0)
+            d[c] = [v for v in d[c] if v > 0.05 * top]
         if not d["FETCH_SIZE"] or not d["WRITE_SIZE"]:
             continue
         rd = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * scale
