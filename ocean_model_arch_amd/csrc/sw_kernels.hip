@@ -2267,17 +2267,20 @@ int launch_fused_ca(const ocn_block *b, void *const *ptr, int nptr, const Compac
 #endif
 // Rows per wave tile of the one-pass step: a wave spends rows + 2 (warm-up) iterations, and the
 // launch runs in ceil(waves / slots) rounds of 2 waves per SIMD (256 CUs x 4 SIMDs); the tile
-// height in [2, OCN_STEP_ROWS] with the fewest iterations in total.  (A launch of 2.25 rounds
+// height in [OCN_STEP_MIN_ROWS, OCN_STEP_ROWS] with the fewest iterations in total.  (A launch of 2.25 rounds
 // spends a third of its time in a quarter-full last round.)
 #ifndef OCN_STEP_SLOTS
 #define OCN_STEP_SLOTS 2048
+#endif
+#ifndef OCN_STEP_MIN_ROWS
+#define OCN_STEP_MIN_ROWS 1   // the shortest tile the cost model may pick (1: Black Sea 0.0159 -> 0.0148 ms per step)
 #endif
 template <class Body> static int step_rows(const Range &r, bool vert)
 {
     const long wx = (r.m1 - r.m0 + 60) / 60, h = r.n1 - r.n0 + 1, wgx = (r.m1 - r.m0 + 240) / 240;
     int best = OCN_STEP_ROWS;
     long cost = -1;
-    for (int rows = OCN_STEP_ROWS; rows >= 2; --rows) {
+    for (int rows = OCN_STEP_ROWS; rows >= OCN_STEP_MIN_ROWS; --rows) {
         // vert: 4 vertically stacked waves per workgroup; else 4 side by side (240 columns)
         const long tiles = vert ? (h + 4 * rows - 1) / (4 * rows) : (h + rows - 1) / rows;
         const long waves = vert ? 4 * tiles * wx : 4 * tiles * wgx, rounds = (waves + OCN_STEP_SLOTS - 1) / OCN_STEP_SLOTS;
