@@ -313,6 +313,10 @@ __device__ __forceinline__ unsigned lane_shift(unsigned x, unsigned e, int dx)
 {
     return dx == 0 ? x : (unsigned)dpp_shift((int)x, (int)e, dx);
 }
+__device__ __forceinline__ float lane_shift(float x, float e, int dx)
+{
+    return dx == 0 ? x : __int_as_float(dpp_shift(__float_as_int(x), __float_as_int(e), dx));
+}
 
 // Never defined: a view access outside the rows a march keeps fails to link.
 extern "C" __device__ void ocn_march_bad_access();
@@ -331,6 +335,7 @@ template <class T, bool S, bool N, bool E = false> struct Rows {
     __device__ __forceinline__ void rotate() { s = c; c = nn; es = ec; ec = enn; }
 };
 template <bool S, bool N, bool E = false> using RowsD = Rows<double, S, N, E>;
+template <bool S, bool N, bool E = false> using RowsF = Rows<float, S, N, E>;   // a real(4) 2-D array
 // mask bytes of the compact tables: bit id of the byte
 template <bool S, bool N, bool E = false> struct BitRows : Rows<unsigned, S, N, E> {
     __device__ __forceinline__ float mask(int id, int dx, int dy) const
@@ -340,14 +345,16 @@ template <bool S, bool N, bool E = false> struct BitRows : Rows<unsigned, S, N, 
 };
 
 // value of an array read only at (m, n)
-struct Here {
-    double v;
-    __device__ __forceinline__ double at(int dx, int dy) const
+template <class T> struct HereT {
+    T v;
+    __device__ __forceinline__ T at(int dx, int dy) const
     {
         if (dx != 0 || dy != 0) ocn_march_bad_access();
         return v;
     }
 };
+using Here = HereT<double>;
+using HereF = HereT<float>;
 
 // per-row metrics of the compact tables (wave-uniform) for rows n-1, n, n+1
 struct MetRows {
@@ -1072,6 +1079,295 @@ struct MarchHhInit {
             x.rHR.ec = ld(f.k.h_r, e); x.rSH.ec = ld(f.k.sh, e); x.rSHP.ec = ld(f.k.shp, e); x.bits.ec = ld(t.bits, e);
         }
         x.met.preload(t.rows, t.nrows, c.r, c.r);
+        march_rows(f, x, L, nb, ne);
+    }
+};
+
+// ------------------------------------------------------------------ kernel entries on 2-D arrays
+// The ocn_hh_init / ocn_uv_trans kernel entries read the real(4) masks and metrics the caller
+// passes (2-D arrays, no compact tables): the same register marches as MarchHhInit / MarchUvTrans
+// with those arrays in rings of their own (one load per array and cell; m+-1 by DPP).
+
+// a10 hh_init (sw_stencils.h HhInit<false>, every level) as an aligned register march over any
+// part of the bnd range (row n+1 clamped to bnd_y2: its values are used only where n <= end)
+struct MarchViewH2 {
+    RowsD<false, true, true> rHR, rSH, rSHP;           // h_r, ssh, sshp: rows n, n+1, columns m, m+1
+    RowsF<false, true, true> rLU, rDX, rDY;            // lu, dx, dy at the same corners
+    HereF dxt_, dyt_, dxh_, dyh_, dxb_, dyb_;
+    OCN_MV(h_r, rHR) OCN_MV(sh, rSH) OCN_MV(shp, rSHP)
+    __device__ __forceinline__ float lu(int dx, int dy) const { return rLU.at(dx, dy); }
+    __device__ __forceinline__ float dx(int i, int j) const { return rDX.at(i, j); }
+    __device__ __forceinline__ float dy(int i, int j) const { return rDY.at(i, j); }
+    __device__ __forceinline__ float dxt(int i, int j) const { return dxt_.at(i, j); }
+    __device__ __forceinline__ float dyt(int i, int j) const { return dyt_.at(i, j); }
+    __device__ __forceinline__ float dxh(int i, int j) const { return dxh_.at(i, j); }
+    __device__ __forceinline__ float dyh(int i, int j) const { return dyh_.at(i, j); }
+    __device__ __forceinline__ float dxb(int i, int j) const { return dxb_.at(i, j); }
+    __device__ __forceinline__ float dyb(int i, int j) const { return dyb_.at(i, j); }
+};
+struct MarchHhInit2D {
+    static constexpr bool kAligned = true;
+    static constexpr int kHalo = 0;
+    HhInit<false> k; int ylast;
+    using View = MarchViewH2;
+    struct Fn {
+        const HhInit<false> &k; int ylast;
+        // row n: h_r, ssh, sshp, lu, dx, dy at row n+1 (+ edge values); the centre-only metrics and
+        // the level masks at row n
+        struct Batch { double nn[3], enn[3]; float fn[3], efn[3], c[9]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
+        {
+            const Interp<false> &W = k.W;
+            const Pt cn = k.I(L.m, min(n + 1, ylast)), c = k.I(L.m, n);
+            q.nn[0] = ld(k.h_r, cn); q.nn[1] = ld(k.sh, cn); q.nn[2] = ld(k.shp, cn);
+            q.fn[0] = ld(W.lu, cn); q.fn[1] = ld(W.dx, cn); q.fn[2] = ld(W.dy, cn);
+            for (int i = 0; i < 3; ++i) { q.enn[i] = 0.0; q.efn[i] = 0.0f; }
+            if (L.edge) {
+                const Pt en = k.I(L.me, min(n + 1, ylast));
+                q.enn[0] = ld(k.h_r, en); q.enn[1] = ld(k.sh, en); q.enn[2] = ld(k.shp, en);
+                q.efn[0] = ld(W.lu, en); q.efn[1] = ld(W.dx, en); q.efn[2] = ld(W.dy, en);
+            }
+            q.c[0] = ld(W.dxt, c); q.c[1] = ld(W.dyt, c); q.c[2] = ld(W.dxh, c); q.c[3] = ld(W.dyh, c);
+            q.c[4] = ld(W.dxb, c); q.c[5] = ld(W.dyb, c);
+            q.c[6] = ld(k.llu, c); q.c[7] = ld(k.llv, c); q.c[8] = ld(k.luh, c);
+        }
+        __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n);
+            const double f = k.f;
+            x.rHR.nn = q.nn[0]; x.rSH.nn = q.nn[1]; x.rSHP.nn = q.nn[2];
+            x.rHR.enn = q.enn[0]; x.rSH.enn = q.enn[1]; x.rSHP.enn = q.enn[2];
+            x.rLU.nn = q.fn[0]; x.rDX.nn = q.fn[1]; x.rDY.nn = q.fn[2];
+            x.rLU.enn = q.efn[0]; x.rDX.enn = q.efn[1]; x.rDY.enn = q.efn[2];
+            x.dxt_.v = q.c[0]; x.dyt_.v = q.c[1]; x.dxh_.v = q.c[2]; x.dyh_.v = q.c[3];
+            x.dxb_.v = q.c[4]; x.dyb_.v = q.c[5];
+            const double r00 = x.rHR.c;
+            if (L.out) {
+                st(k.hq, c, r00 + x.rSH.c * f);
+                if (k.full) { st(k.hqp, c, r00 + x.rSHP.c * f); st(k.hqn, c, r00); }
+            }
+            if (n >= k.j0 && n <= k.j1) {   // wave-uniform
+                HhInitOut o;
+                hh_init_math(x, f, k.full, o);
+                if (L.out && L.m >= k.i0 && L.m <= k.i1) {
+                    const bool bu = q.c[6] > 0.5f, bv = q.c[7] > 0.5f, bh = q.c[8] > 0.5f;
+                    if (bu) { st(k.hu, c, o.u[0]); st(k.hup, c, o.u[1]); }
+                    if (bv) { st(k.hv, c, o.v[0]); st(k.hvp, c, o.v[1]); }
+                    if (bh) { st(k.hh, c, o.h[0]); st(k.hhp, c, o.h[1]); }
+                    if (k.full) {
+                        if (bu) st(k.hun, c, o.u[2]);
+                        if (bv) st(k.hvn, c, o.v[2]);
+                        if (bh) st(k.hhn, c, o.h[2]);
+                    }
+                }
+            }
+            x.rHR.rotate(); x.rSH.rotate(); x.rSHP.rotate(); x.rLU.rotate(); x.rDX.rotate(); x.rDY.rotate();
+        }
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{k, ylast};
+        View x{};
+        const Interp<false> &W = k.W;
+        const Pt c = k.I(L.m, nb);
+        x.rHR.c = ld(k.h_r, c); x.rSH.c = ld(k.sh, c); x.rSHP.c = ld(k.shp, c);
+        x.rLU.c = ld(W.lu, c); x.rDX.c = ld(W.dx, c); x.rDY.c = ld(W.dy, c);
+        if (L.edge) {
+            const Pt e = k.I(L.me, nb);
+            x.rHR.ec = ld(k.h_r, e); x.rSH.ec = ld(k.sh, e); x.rSHP.ec = ld(k.shp, e);
+            x.rLU.ec = ld(W.lu, e); x.rDX.ec = ld(W.dx, e); x.rDY.ec = ld(W.dy, e);
+        }
+        march_rows(f, x, L, nb, ne);
+    }
+};
+
+// a4 uv_trans (sw_stencils.h UvTrans<false>) as an offset-layout register march
+struct MarchViewT2 {
+    RowsD<true, true> rU, rV, rHV;        // ubrtr, vbrtr, hhv: rows n-1 .. n+1
+    RowsD<false, true> rHU;               // hhu: rows n, n+1
+    RowsD<true, false> rVORT, rHH;        // vort, hhh: rows n-1, n
+    RowsF<true, true> rDXH;               // dxh: rows n-1 .. n+1
+    RowsF<false, true> rDYH;              // dyh: rows n, n+1
+    RowsF<true, false> rLUU;              // luu: rows n-1, n
+    OCN_MV(u, rU) OCN_MV(v, rV) OCN_MV(hu, rHU) OCN_MV(hv, rHV) OCN_MV(vort, rVORT) OCN_MV(hh, rHH)
+    __device__ __forceinline__ float dxh(int i, int j) const { return rDXH.at(i, j); }
+    __device__ __forceinline__ float dyh(int i, int j) const { return rDYH.at(i, j); }
+    __device__ __forceinline__ float luu(int i, int j) const { return rLUU.at(i, j); }
+};
+struct MarchUvTrans2D {
+    static constexpr bool kAligned = false;
+    static constexpr int kHalo = 1;
+    UvTrans<false> k;
+    using View = MarchViewT2;
+    struct Fn {
+        const UvTrans<false> &k;
+        // row n: ubrtr, vbrtr, hhv, hhu, dxh, dyh at n+1; vort, hhh, luu, lcu, lcv at n
+        struct Batch { double nn[4], c[2]; float fn[2], fc[3]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n), cn = k.I(L.m, n + 1);
+            q.nn[0] = ld(k.u, cn); q.nn[1] = ld(k.v, cn); q.nn[2] = ld(k.hv, cn); q.nn[3] = ld(k.hu, cn);
+            q.fn[0] = ld(k.dxh, cn); q.fn[1] = ld(k.dyh, cn);
+            q.c[0] = ld(k.vort, c); q.c[1] = ld(k.hh, c);
+            q.fc[0] = ld(k.luu, c); q.fc[1] = ld(k.lcu, c); q.fc[2] = ld(k.lcv, c);
+        }
+        __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n);
+            x.rVORT.s = x.rVORT.c; x.rHH.s = x.rHH.c; x.rLUU.s = x.rLUU.c;
+            x.rU.nn = q.nn[0]; x.rV.nn = q.nn[1]; x.rHV.nn = q.nn[2]; x.rHU.nn = q.nn[3];
+            x.rDXH.nn = q.fn[0]; x.rDYH.nn = q.fn[1];
+            x.rVORT.c = q.c[0]; x.rHH.c = q.c[1]; x.rLUU.c = q.fc[0];
+            double rx, ry;
+            uv_trans_math(x, rx, ry);
+            if (L.out) {
+                if (q.fc[1] > 0.5f) st(k.RHSx, c, rx);
+                if (q.fc[2] > 0.5f) st(k.RHSy, c, ry);
+            }
+            x.rU.rotate(); x.rV.rotate(); x.rHV.rotate(); x.rHU.rotate(); x.rDXH.rotate(); x.rDYH.rotate();
+        }
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{k};
+        View x{};
+        const Pt s = k.I(L.m, nb - 1), c = k.I(L.m, nb);   // rows kept from before the first row
+        x.rU.s = ld(k.u, s); x.rU.c = ld(k.u, c);
+        x.rV.s = ld(k.v, s); x.rV.c = ld(k.v, c);
+        x.rHV.s = ld(k.hv, s); x.rHV.c = ld(k.hv, c);
+        x.rHU.c = ld(k.hu, c);
+        x.rDXH.s = ld(k.dxh, s); x.rDXH.c = ld(k.dxh, c);
+        x.rDYH.c = ld(k.dyh, c);
+        x.rVORT.c = ld(k.vort, s); x.rHH.c = ld(k.hh, s); x.rLUU.c = ld(k.luu, s);
+        march_rows(f, x, L, nb, ne);
+    }
+};
+
+// a6 uv_diff2 (sw_stencils.h UvDiff2<false>) as an offset-layout register march
+struct MarchViewD2 {
+    RowsD<true, true> rMU;                // mu: rows n-1 .. n+1
+    RowsD<false, true> rHQ, rSTT;         // hhq, str_t: rows n, n+1
+    RowsD<true, false> rHH, rSTS;         // hhh, str_s: rows n-1, n
+    RowsF<false, false> rDY, rDYB;        // dy, dyb: row n (m-1 .. m+1)
+    RowsF<false, true> rDX;               // dx: rows n, n+1
+    RowsF<true, false> rDXB;              // dxb: rows n-1, n
+    HereF dxt_, dyt_, dxh_, dyh_;
+    __device__ __forceinline__ double quot(double a, double b, int, int) const { return a / b; }
+    OCN_MV(mu, rMU) OCN_MV(hq, rHQ) OCN_MV(str_t, rSTT) OCN_MV(hh, rHH) OCN_MV(str_s, rSTS)
+    __device__ __forceinline__ float dx(int i, int j) const { return rDX.at(i, j); }
+    __device__ __forceinline__ float dy(int i, int j) const { return rDY.at(i, j); }
+    __device__ __forceinline__ float dxb(int i, int j) const { return rDXB.at(i, j); }
+    __device__ __forceinline__ float dyb(int i, int j) const { return rDYB.at(i, j); }
+    __device__ __forceinline__ float dxt(int i, int j) const { return dxt_.at(i, j); }
+    __device__ __forceinline__ float dyt(int i, int j) const { return dyt_.at(i, j); }
+    __device__ __forceinline__ float dxh(int i, int j) const { return dxh_.at(i, j); }
+    __device__ __forceinline__ float dyh(int i, int j) const { return dyh_.at(i, j); }
+};
+struct MarchUvDiff2D {
+    static constexpr bool kAligned = false;
+    static constexpr int kHalo = 1;
+    UvDiff2<false> k;
+    using View = MarchViewD2;
+    struct Fn {
+        const UvDiff2<false> &k;
+        // row n: mu, hhq, str_t, dx at n+1; hhh, str_s, dy, dyb, dxb, the centre metrics and lcu, lcv at n
+        struct Batch { double nn[3], c[2]; float fn, fc[9]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n), cn = k.I(L.m, n + 1);
+            q.nn[0] = ld(k.mu, cn); q.nn[1] = ld(k.hq, cn); q.nn[2] = ld(k.str_t, cn);
+            q.fn = ld(k.dx, cn);
+            q.c[0] = ld(k.hh, c); q.c[1] = ld(k.str_s, c);
+            q.fc[0] = ld(k.dy, c); q.fc[1] = ld(k.dyb, c); q.fc[2] = ld(k.dxb, c);
+            q.fc[3] = ld(k.dxt, c); q.fc[4] = ld(k.dyt, c); q.fc[5] = ld(k.dxh, c); q.fc[6] = ld(k.dyh, c);
+            q.fc[7] = ld(k.lcu, c); q.fc[8] = ld(k.lcv, c);
+        }
+        __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n);
+            x.rHH.s = x.rHH.c; x.rSTS.s = x.rSTS.c; x.rDXB.s = x.rDXB.c;
+            x.rMU.nn = q.nn[0]; x.rHQ.nn = q.nn[1]; x.rSTT.nn = q.nn[2]; x.rDX.nn = q.fn;
+            x.rHH.c = q.c[0]; x.rSTS.c = q.c[1];
+            x.rDY.c = q.fc[0]; x.rDYB.c = q.fc[1]; x.rDXB.c = q.fc[2];
+            x.dxt_.v = q.fc[3]; x.dyt_.v = q.fc[4]; x.dxh_.v = q.fc[5]; x.dyh_.v = q.fc[6];
+            double rx, ry;
+            uv_diff2_math(x, rx, ry);
+            if (L.out) {
+                if (q.fc[7] > 0.5f) st(k.RHSx, c, rx);
+                if (q.fc[8] > 0.5f) st(k.RHSy, c, ry);
+            }
+            x.rMU.rotate(); x.rHQ.rotate(); x.rSTT.rotate(); x.rDX.rotate();
+        }
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{k};
+        View x{};
+        const Pt s = k.I(L.m, nb - 1), c = k.I(L.m, nb);   // rows kept from before the first row
+        x.rMU.s = ld(k.mu, s); x.rMU.c = ld(k.mu, c);
+        x.rHQ.c = ld(k.hq, c); x.rSTT.c = ld(k.str_t, c); x.rDX.c = ld(k.dx, c);
+        x.rHH.c = ld(k.hh, s); x.rSTS.c = ld(k.str_s, s); x.rDXB.c = ld(k.dxb, s);
+        march_rows(f, x, L, nb, ne);
+    }
+};
+
+// a5 stress_components (sw_stencils.h StressComponents<false>) as an offset-layout register march
+struct MarchViewS2 {
+    RowsD<false, true> rUP;               // ubrtrp: rows n, n+1
+    RowsD<true, false> rVP;               // vbrtrp: rows n-1, n
+    RowsF<false, false> rDYH, rDYT;       // dyh, dyt: row n (m-1 .. m+1)
+    RowsF<true, false> rDXH;              // dxh: rows n-1, n
+    RowsF<false, true> rDXT;              // dxt: rows n, n+1
+    float rat[4];                         // dy/dx, dx/dy, dxb/dyb, dyb/dxb at the point (mixing.f90:33-34, 43-44)
+    OCN_MV(up, rUP) OCN_MV(vp, rVP)
+    __device__ __forceinline__ float sratio(int k) const { return rat[k]; }
+    __device__ __forceinline__ float dyh(int i, int j) const { return rDYH.at(i, j); }
+    __device__ __forceinline__ float dyt(int i, int j) const { return rDYT.at(i, j); }
+    __device__ __forceinline__ float dxh(int i, int j) const { return rDXH.at(i, j); }
+    __device__ __forceinline__ float dxt(int i, int j) const { return rDXT.at(i, j); }
+};
+struct MarchStress2D {
+    static constexpr bool kAligned = false;
+    static constexpr int kHalo = 1;
+    StressComponents<false> k;
+    using View = MarchViewS2;
+    struct Fn {
+        const StressComponents<false> &k;
+        // row n: ubrtrp, dxt at n+1; vbrtrp, dyh, dyt, dxh, dx, dy, dxb, dyb, lu, luu at n
+        struct Batch { double nn, c; float fn, fc[10]; };
+        __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n), cn = k.I(L.m, n + 1);
+            q.nn = ld(k.u, cn); q.fn = ld(k.dxt, cn);
+            q.c = ld(k.v, c);
+            q.fc[0] = ld(k.dyh, c); q.fc[1] = ld(k.dyt, c); q.fc[2] = ld(k.dxh, c);
+            q.fc[3] = ld(k.dx, c); q.fc[4] = ld(k.dy, c); q.fc[5] = ld(k.dxb, c); q.fc[6] = ld(k.dyb, c);
+            q.fc[7] = ld(k.lu, c); q.fc[8] = ld(k.luu, c);
+        }
+        __device__ __forceinline__ void row(View &x, const Batch &q, const Lane &L, int n) const
+        {
+            const Pt c = k.I(L.m, n);
+            x.rVP.s = x.rVP.c; x.rDXH.s = x.rDXH.c;
+            x.rUP.nn = q.nn; x.rDXT.nn = q.fn;
+            x.rVP.c = q.c; x.rDYH.c = q.fc[0]; x.rDYT.c = q.fc[1]; x.rDXH.c = q.fc[2];
+            const float dx = q.fc[3], dy = q.fc[4], dxb = q.fc[5], dyb = q.fc[6];
+            x.rat[0] = dy / dx; x.rat[1] = dx / dy; x.rat[2] = dxb / dyb; x.rat[3] = dyb / dxb;
+            double vt, vs;
+            stress_components_math(x, vt, vs);
+            if (L.out) {
+                if (q.fc[7] > 0.5f) st(k.str_t, c, vt);
+                if (q.fc[8] > 0.5f) st(k.str_s, c, vs);
+            }
+            x.rUP.rotate(); x.rDXT.rotate();
+        }
+    };
+    __device__ void march(const Lane &L, int nb, int ne) const
+    {
+        const Fn f{k};
+        View x{};
+        const Pt s = k.I(L.m, nb - 1), c = k.I(L.m, nb);   // rows kept from before the first row
+        x.rUP.c = ld(k.u, c); x.rDXT.c = ld(k.dxt, c);
+        x.rVP.c = ld(k.v, s); x.rDXH.c = ld(k.dxh, s);
         march_rows(f, x, L, nb, ne);
     }
 };
@@ -2573,6 +2869,13 @@ int launch_rows_ext(const ocn_block *b, const float *rows, float *rows_x, const 
 
 using namespace ocn;
 
+// ocn_hh_init, ocn_uv_trans, ocn_uv_diff2, ocn_stress_components as register marches over the
+// arrays they are given (MarchHhInit2D, MarchUvTrans2D, MarchUvDiff2D, MarchStress2D); 0: one
+// thread per point like the other entries
+#ifndef OCN_ENTRY_MARCH
+#define OCN_ENTRY_MARCH 1
+#endif
+
 extern "C" {
 
 int ocn_sw_update_ssh(const ocn_block *b, double tau, const float *lu, const float *dx, const float *dy,
@@ -2610,7 +2913,11 @@ int ocn_uv_trans(const ocn_block *b, const float *lcu, const float *lcv, const f
     (void)hq;
     CHECK(lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy);
     UvTrans<false> k{geo(b), lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy};
+#if OCN_ENTRY_MARCH
+    return launch_march(b, range_interior(b), MarchUvTrans2D{k}, (hipStream_t)stream);
+#else
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
+#endif
 }
 
 int ocn_stress_components(const ocn_block *b, const float *lu, const float *luu, const float *dx, const float *dy,
@@ -2620,7 +2927,11 @@ int ocn_stress_components(const ocn_block *b, const float *lu, const float *luu,
 {
     CHECK(lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s);
     StressComponents<false> k{geo(b), lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s};
+#if OCN_ENTRY_MARCH
+    return launch_march(b, range_interior(b), MarchStress2D{k}, (hipStream_t)stream);
+#else
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
+#endif
 }
 
 int ocn_uv_diff2(const ocn_block *b, const float *lcu, const float *lcv, const float *dx, const float *dy,
@@ -2631,7 +2942,11 @@ int ocn_uv_diff2(const ocn_block *b, const float *lcu, const float *lcv, const f
     (void)hu; (void)hv;
     CHECK(lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy);
     UvDiff2<false> k{geo(b), lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy};
+#if OCN_ENTRY_MARCH
+    return launch_march(b, range_interior(b), MarchUvDiff2D{k}, (hipStream_t)stream);
+#else
     return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
+#endif
 }
 
 int ocn_sw_update_uv(const ocn_block *b, double tau, const float *lcu, const float *lcv, const float *dxt,
@@ -2681,7 +2996,11 @@ int ocn_hh_init(const ocn_block *b, int32_t full_free_surface, const float *lu, 
     HhInit<false> k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)full_free_surface, true,
              Interp<false>{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh,
              hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn, sh, shp, h_r};
+#if OCN_ENTRY_MARCH
+    return launch_march(b, range_bnd(b), MarchHhInit2D{k, b->bnd_y2}, (hipStream_t)stream);
+#else
     return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream, b->nx_start);
+#endif
 }
 
 int ocn_tran_diff_fluxes(const ocn_block *b, const float *lcu, const float *lcv, const float *dxt, const float *dyt,

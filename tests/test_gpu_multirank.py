@@ -292,3 +292,20 @@ def test_initial_state_matches_reference(amd, name):
     finally:
         m.close()
     assert not bad, f"{name}: initial fields differ from the reference: {bad}"
+
+
+@pytest.mark.parametrize("name,nranks", [("bs_topo_b4x2_s60", 8), ("box70x54_topo_b3x2_s20", 6)])
+def test_ranks_topography_match_reference(amd, name, nranks):
+    """A topography (non-uniform h_r) over loopback ranks: x2 steps with the h_r-reading
+    known-constant variant, h_r's second halo ring exchanged from the neighbour ranks every call
+    (refresh_hrx), the verdicts voted -- bitwise against the reference run that read the file."""
+    case = cases.load_e2e(name)
+    models, flips = run_ranks_case(amd, case, nranks)
+    try:
+        bad = check_ranks(models, case, name)
+        hr = {m.onepass_hr for m in models}
+    finally:
+        for m in models:
+            m.close()
+    assert not bad, f"{name} over {nranks} ranks: fields differ from the reference: {bad}"
+    assert run_ranks_case.x2 == [True] * nranks and hr == {True}, (run_ranks_case.x2, hr)
