@@ -58,6 +58,9 @@ LAUNCH_BYTES = {
     "onepass_z": (97, 97), "onepass_last_z": (153, 153),
     # ... with h_r read (a non-uniform rest depth: the OCN_KC_KNOWN_HR variant)
     "onepass_h": (105, 105), "onepass_last_h": (161, 161),
+    # two one-pass steps in one launch (OCN_OPT_PAIR): one step's reads and writes, the mask byte
+    # read by both wave roles (+ h_r by both in the _h variant) -- per launch, i.e. per two steps
+    "onepass2_z": (98, 98), "onepass2_h": (114, 114),
     "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
     # tracer runs: CA also stores hh_init's hhq_p (read by tran_diff_tracer); per tracer and step:
     # tran_diff_fluxes (lcu, lcv, hhu, hhv, ff, ffp, ubrtr, vbrtr, mu in; flux_x, flux_y out),
@@ -74,8 +77,17 @@ def _kc(zero) -> str:
     return "_z" if zero is True else "_h" if zero == "h" else ""
 
 
+def _one_launches(n: int, z: str, pair: bool):
+    """n consecutive one-pass steps of a call whose steps after them are not one-pass steps of an
+    open sequence: with pairs (ocn_ctx.hip step_impl), steps 1 + 2i and 2 + 2i in one launch while
+    the second is not the call's last step run -- (n - 1) // 2 pairs, the rest single."""
+    p = (n - 1) // 2 if pair else 0
+    return [("onepass2", "onepass2" + z)] * p + [("onepass", "onepass" + z)] * (n - 2 * p)
+
+
 def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
-                  tracers: int = 0, full_c2: bool = False, zero: bool = False, lazy: bool = False):
+                  tracers: int = 0, full_c2: bool = False, zero: bool = False, lazy: bool = False,
+                  pair: bool = False):
     """The launches of one ocn_ctx_step call of `steps` steps, as (timer, launch kind) pairs --
     ocn_ctx.hip ocn_ctx_step / one_step_fused for one block (role-flip calls fuse each step's
     hh_init with the next step's A when full_free_surface = 1, as in sw.par; ring = the ring
@@ -93,10 +105,10 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
                         ("tracer_next_step", "tr_next")] * tracers
         return out
     if one and lazy:   # an open one-pass sequence (OCN_OPT_LAZY_TAIL): every step one launch, no tail
-        return [("onepass", "onepass" + _kc(zero))] * steps
+        return _one_launches(steps, _kc(zero), pair)
     if one and flip and steps >= 2:   # steps 1 .. K-1 (the state is unchanged since the last call / init)
         z = _kc(zero)
-        out = [("onepass", "onepass" + z)] * (steps - 1)
+        out = _one_launches(steps - 1, z, pair and not ring)
         if ring:   # several blocks: CA + the standard last step
             out += [("fused_ca", "ca_hh"), ("fused_b", "b_full"), ("fused_c1", "c1"), ("hh_init", "c2_full")]
             swaps = steps - 1
@@ -130,34 +142,34 @@ TAIL_LAUNCHES = [("onepass", "onepass_last"), ("copy", "copy3"), ("hh_init", "c2
 
 
 def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
-                    tracers: int = 0, zero: bool = False, lazy: bool = False):
+                    tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False):
     """The launches of a timed region: ocn_ctx_step calls of calls[i] steps each, then (lazy) the
     pending tail formed by ocn_ctx_complete."""
     out = []
     for n in calls:
-        out += call_launches(n, flip, rc, ring, one, tracers, zero=zero, lazy=lazy)
+        out += call_launches(n, flip, rc, ring, one, tracers, zero=zero, lazy=lazy, pair=pair)
     if lazy and one:
         out += [(t, k + (_kc(zero) if t == "onepass" else "")) for t, k in TAIL_LAUNCHES]
     return out
 
 
 def fused_bytes(compact: bool, calls, flip: bool = False, rc: bool = True, ring: bool = False,
-                one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False):
+                one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False):
     """Mean bytes per interior cell per launch of each timer over the timed region's calls."""
     i = 0 if compact else 1
     tot, cnt = {}, {}
-    for timer, kind in region_launches(calls, flip, rc, ring, one, tracers, zero, lazy):
+    for timer, kind in region_launches(calls, flip, rc, ring, one, tracers, zero, lazy, pair):
         tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
         cnt[timer] = cnt.get(timer, 0) + (kind != "hqp")   # "hqp": bytes of the launch before it
     return {t: tot[t] / cnt[t] for t in tot}
 
 
 def step_bytes(compact: bool, calls, flip: bool = False, rc: bool = True, ring: bool = False,
-               one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False):
+               one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False):
     """Bytes per interior cell per step moved by the timed region's calls."""
     i = 0 if compact else 1
     return sum(LAUNCH_BYTES[kind][i] for _, kind in region_launches(calls, flip, rc, ring, one, tracers, zero,
-                                                                    lazy)) / sum(calls)
+                                                                    lazy, pair)) / sum(calls)
 
 
 def dims_create(n: int):
@@ -333,6 +345,8 @@ def main():
     ap.add_argument("--topography", action="store_true",
                     help="a non-uniform rest depth (a synthetic smooth basin, 20..180 m) instead of 100 m everywhere: "
                          "the one-pass steps read h_r (what a real-depth basin runs)")
+    ap.add_argument("--pair", type=int, default=1, choices=[0, 1, 2],
+                    help="two one-pass steps per launch (OCN_OPT_PAIR): 1 = on blocks >= 512^2 (default), 2 = always, 0 = never")
     ap.add_argument("--no-batch", action="store_true",
                     help="several blocks on a GPU: one launch per block and launch group (no block batching)")
     ap.add_argument("--blocks", default=None,
@@ -402,6 +416,7 @@ def main():
     model.set_overlap(args.overlap)
     model.set_lazy_tail(not args.no_lazy_tail)
     model.set_batch(not args.no_batch)
+    model.set_pair(args.pair)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -435,6 +450,7 @@ def main():
     rc = model.recompute_active
     one = model.onepass_active
     one_zero = True if model.onepass_zero else "h" if model.onepass_hr else False
+    pair = model.pair_active
     model_overlap = model.overlap_level
     if world > 1:
         t = torch.tensor([dt], device="cuda")
@@ -449,9 +465,10 @@ def main():
         ring = bx * by > 1
         ntr = sw.tracer_num if sw.use_tracers > 0 else 0
         stage_tab = STAGE_BYTES_COMPACT if compact else STAGE_BYTES
-        kbytes = stage_tab if args.stages else fused_bytes(compact, calls, flip, rc, ring, one, ntr, one_zero, lazy)
+        kbytes = stage_tab if args.stages else fused_bytes(compact, calls, flip, rc, ring, one, ntr, one_zero, lazy,
+                                                           pair)
         b_path = sum(stage_tab.values()) if args.stages else step_bytes(compact, calls, flip, rc, ring, one, ntr,
-                                                                          one_zero, lazy)
+                                                                          one_zero, lazy, pair)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:   # the dominant kernel: the most device time over the timed steps
@@ -484,6 +501,8 @@ def main():
                           "onepass_variant": ("known constants" if one_zero is True else
                                               "known constants, h_r read" if one_zero == "h" else "general")
                                              if one else None,
+                          "onepass_pairs": ("two one-pass steps per launch (OCN_OPT_PAIR): the first step's "
+                                            "new state kept on chip") if pair else False,
                           "steps_per_call": spc, "calls": len(calls),
                           "call_tail": ("pending between calls (OCN_OPT_LAZY_TAIL), formed once by ocn_ctx_complete "
                                         "inside the timed region") if lazy else "formed by every call",

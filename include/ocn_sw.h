@@ -363,6 +363,12 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  too when the context exchanges only with blocks of its own process.
  *  OCN_OPT_BATCH (default 1): with several blocks on the device, each launch group of a step is
  *  issued once for all of them (the blocks' tiles in one grid) instead of once per block.
+ *  OCN_OPT_PAIR (default 1): two one-pass steps in one launch where both are plain one-pass steps
+ *  of a single-block context without exchanges, the known-constant variant has been selected by a
+ *  verdict the host read, and the second is not the call's last step run -- the first step's new
+ *  state stays on chip (97 B per cell for two steps); 1: on blocks of at least 512 x 512 interior
+ *  points, 2: on any block, 0: never.  Same results bit for bit.  ocn_ctx_get_option: 2 if the last
+ *  ocn_ctx_step ran such launches, else whether the option is on.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
  * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
@@ -374,13 +380,14 @@ int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9,
        OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13,
-       OCN_OPT_BATCH = 14 };
+       OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,
  * then the one-pass steps. */
 enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_TIMER_TRACER,
-       OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_TIMER_ONEPASS, OCN_NUM_TIMERS };
+       OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_TIMER_ONEPASS, OCN_TIMER_ONEPASS2,
+       OCN_NUM_TIMERS };
 
 /* Per-timer device time (ms, summed) and launch counts since the last call, from the HIP
  * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_TIMERS entries.  Synchronises. */

@@ -230,15 +230,17 @@ namespace ocn {
 // x2 = the one-pass step as one_step_x2 (2-deep state exchange, whole-interior march); x2_save = the
 // first of a sequence (the reference's second halo ring of the state is saved first); x2_end = a
 // last step after such a sequence (that ring restored and the state's first ring exchanged first).
+// pair = this one-pass step and the next as one launch (one_step_pair), check2 = the next one's check.
 struct StepKind {
     bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next, one, next_one, one_last;
     bool x2, x2_save, x2_end;
+    bool pair = false, check2 = false;
     bool operator==(const StepKind &o) const
     {
         return check == o.check && first == o.first && last == o.last && flip == o.flip && a_done == o.a_done &&
                next_a == o.next_a && next_reuse == o.next_reuse && rc == o.rc && rc_next == o.rc_next &&
                one == o.one && next_one == o.next_one && one_last == o.one_last && x2 == o.x2 &&
-               x2_save == o.x2_save && x2_end == o.x2_end;
+               x2_save == o.x2_save && x2_end == o.x2_end && pair == o.pair && check2 == o.check2;
     }
 };
 
@@ -301,6 +303,10 @@ struct ocn_ctx {
     bool udiv_ok = true;    // every row divisor of the one-pass step in [2^-60, 2^60] (Prepare)
     bool recompute = true;  // OCN_OPT_RECOMPUTE: recompute steps in role-flip calls
     bool onepass = true;    // OCN_OPT_ONEPASS: one-pass steps in single-block role-flip calls
+    // OCN_OPT_PAIR: two one-pass steps per launch (one_step_pair) -- 0 never, 1 on blocks of at least
+    // kPairMinCells interior points, 2 on any block; pair_used: a call ran one
+    int pair = 1;
+    bool pair_used = false;
     bool known_const = true;   // OCN_OPT_KNOWN_CONSTANTS: the one-pass step's known-constant variant
     bool last_hybrid = true;   // OCN_OPT_ONEPASS_LAST: one-pass last steps with exchanges / ring work too
     bool one_used = false;
@@ -1742,8 +1748,44 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
     return OCN_OK;
 }
 
+// Two one-pass steps as one launch per block (sw_kernels.hip MarchStep PAIR): the first step's new
+// state stays in LDS, the second's is written where a single step writes -- so the pair is one role
+// flip of the pairs and of the second buffers, as a single one-pass step is.  Single block, no
+// exchange, a known-constant verdict the host has read (pair_ok); 97 B per cell for two steps.
+static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
+{
+    ocn_ctx::Rec rec;
+    hipStream_t s = c->stream;
+    RC(timer_begin(c, OCN_TIMER_ONEPASS2, rec));
+    RC(each_block(c, s, [&](const LBlock &b) {
+        const Compact t{b.bits, b.rows, c->march};
+        return launch_onepass_pair(&b.g, b.ptr.data(), (int)b.ptr.size(), &t, c->sw, tau, k.check ? c->d_nbad : nullptr,
+                                   k.check2 ? c->d_nbad : nullptr, (double *)b.sshp_alt, (double *)b.up_alt,
+                                   (double *)b.vp_alt, s, kc_of(c, b));
+    }));
+    RC(timer_end(c, rec));
+    swap_alt3(c);
+    swap_roles(c);
+    return OCN_OK;
+}
+
+// one_step_pair possible in this call: one block without exchanges or ring work, the compact tables
+// and the march, the known-constant variant chosen by the host (kc_mode), OCN_OPT_PAIR
+#ifndef OCN_PAIR_MIN_CELLS
+#define OCN_PAIR_MIN_CELLS (512L * 512L)
+#endif
+static bool pair_ok(ocn_ctx *c)
+{
+    if (!c->pair || c->blocks.size() != 1 || has_exchange(c) || has_comm(c) || c->ring_sea || !c->compact || !c->march)
+        return false;
+    if (c->kc_mode != OCN_KC_KNOWN && c->kc_mode != OCN_KC_KNOWN_HR) return false;
+    const ocn_block &g = c->blocks[0].g;
+    return c->pair >= 2 || (long)(g.nx_end - g.nx_start + 1) * (g.ny_end - g.ny_start + 1) >= OCN_PAIR_MIN_CELLS;
+}
+
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
+    if (k.pair) return one_step_pair(c, tau, k);
     if (k.x2) return one_step_x2(c, tau, k);
     if (k.one_last && k.x2_end) RC(x2_end(c, c->stream));
     if (k.one_last) return has_exchange(c) || c->ring_sea ? one_step_hybrid(c, tau, k, true) : one_step_last(c, tau, k);
@@ -2594,18 +2636,26 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     if (nsteps < 0) return set_error(OCN_ERR_ARG, "nsteps < 0");
     if (nsteps == 0) return OCN_OK;
     const bool graph_ok = c->use_graph && !has_comm(c) && !c->stage_timing;   // RCCL / events stay outside graphs
+    c->pair_used = false;
     if (c->open) {
         if (tau == c->open_tau && c->onepass && lazy_allowed(c, c->open_x2)) {
             // the open sequence goes on: every step of this call is a one-pass step (the state and
             // the constants are what its last step left), and the tail stays pending; a device
             // verdict the host has read since selects one variant
             RC(prepare_kc(c, c->open_x2));
+            const bool pairs = !c->open_x2 && pair_ok(c);
             int rc = OCN_OK;
             for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
                 StepKind k{};
                 k.check = check_every > 0 && (s % check_every == 0);
                 k.flip = k.one = k.next_one = k.a_done = true;
                 k.x2 = c->open_x2;
+                if (pairs && s + 1 < nsteps) {   // (the call's last step stays single: the tail redoes it)
+                    k.pair = true;
+                    k.check2 = check_every > 0 && ((s + 1) % check_every == 0);
+                    ++s;
+                    c->pair_used = true;
+                }
                 rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
             }
             if (rc) { c->open = false; return finish_call(c, rc); }
@@ -2680,6 +2730,14 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
             HIPCHK(hipMemcpyAsync(b.sshp_alt, b.ptr[field_slot(OCN_SSHP)], field_bytes(b), hipMemcpyDeviceToDevice,
                                   c->stream));
     RC(join_sync(c));
+    // two one-pass steps per launch where both are plain one-pass steps and the second is not the
+    // last one run (a lazy tail redoes that one from the state before it, which a pair never writes)
+    const bool pairs = one_call && !x2_call && pair_ok(c);
+    auto plain_one = [&](int s) {   // step s is a one-pass step that needs nothing around its launch
+        const bool one = one_call && (s >= 2 || first_one) && s <= N - 1, next_one = one_call && s + 1 <= N - 1;
+        const bool next_a = ca && flip_call && s != N && !next_one && !(last_one && s + 1 == N);
+        return one && !next_a && !(last_one && s == N);
+    };
     int rc = OCN_OK;
     for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
         StepKind k;
@@ -2700,6 +2758,14 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         k.x2_end = k.one_last && c->ring2_saved;
         if (k.x2_save) c->ring2_saved = true;
         if (k.x2_end) c->ring2_saved = false;
+        if (pairs && k.one && s + 1 < nsteps && plain_one(s + 1)) {
+            k.pair = true;
+            k.check2 = check_every > 0 && ((s + 1) % check_every == 0);
+            k.next_one = one_call && s + 2 <= N - 1;
+            k.next_a = k.next_reuse = false;
+            ++s;
+            c->pair_used = true;
+        }
         rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
     }
     if (lazy_end && rc == OCN_OK) {   // the pending tail: complete_open
@@ -2848,6 +2914,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         return OCN_OK;
     case OCN_OPT_LAZY_TAIL: c->lazy = value != 0; return OCN_OK;
     case OCN_OPT_X2: c->x2 = value != 0; c->coherent_known = false; return OCN_OK;
+    case OCN_OPT_PAIR: c->pair = value < 0 ? 0 : value > 2 ? 2 : (int)value; return OCN_OK;
     case OCN_OPT_BATCH:
         if (c->batch != (value != 0)) drop_graphs(c);
         c->batch = value != 0;
@@ -2886,6 +2953,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_LAZY_TAIL: *value = c->open ? 2 : c->lazy; return OCN_OK;
     case OCN_OPT_X2: *value = c->x2 && c->x2_used; return OCN_OK;
     case OCN_OPT_BATCH: *value = c->batch; return OCN_OK;
+    case OCN_OPT_PAIR: *value = c->pair_used ? 2 : c->pair > 0; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

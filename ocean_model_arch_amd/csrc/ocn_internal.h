@@ -134,6 +134,13 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
                    double tau, int32_t *nbad, double *sshp_out, double *up_out, double *vp_out, hipStream_t s,
                    const Range *range, bool last, const OnepassKC &kc, unsigned own = 0,
                    const Range *frame_of = nullptr);
+// Two one-pass steps in one launch (sw_kernels.hip MarchStep PAIR): single block, no exchange,
+// the known-constant variants only (kc.mode OCN_KC_KNOWN / OCN_KC_KNOWN_HR, a verdict the host has
+// read); reads the state where a single step reads it and writes the second step's new state where
+// a single step writes (one role flip); nbad1 / nbad2: the steps' check_ssh_err counts (null: none)
+int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                        double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
+                        hipStream_t s, const OnepassKC &kc);
 // the known-constant precondition of launch_onepass over r (sw_kernels.hip FallbackCheck: the
 // fallback points and the forcing hold +0.0, h_r and mu are uniform): ORs 1 into *flag where it
 // does not hold; writes h_r and mu at (r.m0, r.n0) to kc[0], kc[1]

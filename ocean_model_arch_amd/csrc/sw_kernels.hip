@@ -400,7 +400,11 @@ struct MetRows {
 // One lane of a march: its loaded column m, its edge column me (aligned layout: lane 0 m-1,
 // lane 63 m+1, both clamped into the block array), whether it is an edge lane, whether it
 // produces output.
-struct Lane { int m, me; bool edge, out; };
+// Staged stores (a body's kStage, horizontal workgroups whose 4 waves all produce output): wgm =
+// the workgroup's first output column (else -1), wave = this wave's index in it.
+// Two-step launches (a body's kPair): pr = 1 for the producer waves, 2 for the consumers, j = the
+// lane's column in the workgroup's LDS ring.
+struct Lane { int m, me; bool edge, out; int wgm = -1, wave = 0, pr = 0, j = 0; };
 
 // Loaded columns are clamped to [mlo, mhi] (inside the block array); a lane whose column was
 // clamped never produces output and its value is read by no output lane.
@@ -420,6 +424,13 @@ template <class B> struct WavesOf<B, std::void_t<decltype(B::kWaves)>> { static 
 // a body with a workgroup prologue (Body::prologue(R, ty), called by all 4 waves of a workgroup)
 template <class B, class = void> struct HasPrologue { static constexpr bool v = false; };
 template <class B> struct HasPrologue<B, std::void_t<decltype(B::kPrologue)>> { static constexpr bool v = B::kPrologue; };
+// a body that may stage a row's outputs through LDS so that whole 128-B lines are stored
+// (Body::kStage; march_tile sets Lane::wgm where the workgroup qualifies)
+template <class B, class = void> struct HasStage { static constexpr bool v = false; };
+template <class B> struct HasStage<B, std::void_t<decltype(B::kStage)>> { static constexpr bool v = B::kStage; };
+// a two-step body (Body::kPair: MarchStep PAIR; march_tile deals its waves the two roles)
+template <class B, class = void> struct HasPair { static constexpr bool v = false; };
+template <class B> struct HasPair<B, std::void_t<decltype(B::kPair)>> { static constexpr bool v = B::kPair; };
 // a body whose launch may be void at run time (Body::enabled(), a device-side predicate read by
 // every workgroup before anything else: the one-pass step's two variants, one of which a device
 // check selected -- ocn_ctx.hip launches both and never waits for the verdict)
@@ -523,6 +534,23 @@ template <class Body> __device__ __forceinline__ void march_tile(const MarchRect
     const int mw = R.w0 + (R.vert ? tx : tx * 4 + wave) * cols;   // first output column of this wave
     const int nb = R.n0 + (R.vert ? ty * 4 + wave : ty) * R.rows, ne = min(R.n1, nb + R.rows - 1);
     if constexpr (HasPrologue<Body>::v) body.prologue(R, ty);     // all 4 waves (a barrier)
+    if constexpr (HasPair<Body>::v) {
+        // two steps in one launch (MarchStep PAIR): 4 waves side by side, waves 0 / 1 produce the
+        // first step on columns [c0 - 2, c0 + 118) (60 each, into LDS), waves 2 / 3 the second on
+        // [c0, c0 + 116) from there -- every wave of the workgroup takes part in its barriers
+        if (nb > R.n1) return;   // workgroup-uniform
+        const int c0 = R.w0 + tx * Body::kPairCols, p = wave & 1;
+        const bool prod = wave < 2;
+        const int m = (prod ? c0 - 2 + 60 * p : c0 + 60 * p) - 2 + lane;
+        Lane L;
+        L.pr = prod ? 1 : 2;
+        L.j = min(max(m - (c0 - 2), 0), 2 * 60 - 1);
+        L.out = lane >= 2 && lane < 62 && m >= R.m0 && m <= (prod ? R.m1 : min(R.m1, c0 + Body::kPairCols - 1));
+        L.m = L.me = min(max(m, R.mlo), R.mhi);
+        L.edge = false;
+        body.march(L, nb, ne);
+        return;
+    }
     if (mw > R.m1 || nb > R.n1) return;                            // wave-uniform
     Lane L;
     if (Body::kAligned) {
@@ -536,6 +564,10 @@ template <class Body> __device__ __forceinline__ void march_tile(const MarchRect
         L.out = lane >= Body::kHalo && lane < 64 - Body::kHalo && m <= R.m1;
         L.m = L.me = min(max(m, R.mlo), R.mhi);
         L.edge = false;
+    }
+    if constexpr (HasStage<Body>::v) {   // workgroup-uniform: 4 waves side by side, the last one full
+        const int wg0 = R.w0 + tx * 4 * cols;
+        if (!R.vert && wg0 + 4 * cols - 1 <= R.m1) { L.wgm = wg0; L.wave = wave; }
     }
     body.march(L, nb, ne);
 }
@@ -1635,7 +1667,23 @@ __device__ __forceinline__ double udiv(double x, double d, double rd)
     return __builtin_fma(-t, rd, q);
 }
 // the smallest frexp exponent of the dividends of a row (0 for x = 0)
-__device__ __forceinline__ void exp_check(int &acc, double x) { acc = min(acc, __builtin_amdgcn_frexp_exp(x)); }
+#ifndef OCN_DIAG_NOBAR
+#define OCN_DIAG_NOBAR 0   // timing diagnostics only: staged stores without the workgroup barrier
+#endif
+#ifndef OCN_DIAG_NOSTORE
+#define OCN_DIAG_NOSTORE 0   // timing diagnostics only: the one-pass march stores nothing (outputs summed)
+#endif
+#ifndef OCN_DIAG_NOLOAD
+#define OCN_DIAG_NOLOAD 0    // timing diagnostics only: the one-pass march reads no state rows
+#endif
+#ifndef OCN_DIAG_NOCHK
+#define OCN_DIAG_NOCHK 0   // A/B timing diagnostics only (results unchecked): 1 = no range checks and no
+#endif                     // re-run branches in the one-pass march, 2 = checks kept, branches removed
+__device__ __forceinline__ void exp_check(int &acc, double x)
+{
+    if (OCN_DIAG_NOCHK == 1) return;
+    acc = min(acc, __builtin_amdgcn_frexp_exp(x));
+}
 constexpr int kUdivMinExp = -899;   // frexp exponent >= -899  <=>  |x| >= 2^-900
 
 // The row-uniform operands of the one-pass step, per row r, as the doubles the arithmetic uses
@@ -1660,6 +1708,29 @@ constexpr int kStepLdsRows = 4 * OCN_STEP_ROWS + 4;   // a workgroup's 4 stacked
 #if OCN_STEP_LDS
 __shared__ double g_step_rc[kStepLdsRows * kRowC];   // the workgroup's rows [nb - 2, ne + 2]
 __shared__ unsigned g_step_rlo;                       // table row of its first row
+#endif
+// Staged stores (OCN_STEP_STAGE, the known-constant variant): a wave's 60 output columns are
+// 480 B, so every wave boundary splits a 128-B line between two waves, and such stores cost HBM
+// bandwidth (scripts/linebench.hip, the one-pass step's 6 + 6 array mix streamed in the march
+// shape: 4.19 TB/s in the 60-column layout, 4.73 with whole lines; write-only 3.65 vs 4.70).  With
+// 4 waves side by side a workgroup's 240 output columns are 15 whole lines: each wave puts its
+// row of outputs into LDS, and after a workgroup barrier wave w stores columns [64 w, 64 w + 64)
+// of each array -- whole 128-B lines (the interior starts on a 256-B boundary, ocn_ctx.hip
+// allocate).  Two buffers alternate by row parity (a buffer is rewritten two barriers later).
+#ifndef OCN_STEP_STAGE
+#define OCN_STEP_STAGE 0   // measured slower: 0.407-0.424 vs 0.391 ms per 4096^2 launch (the barrier per row)
+#endif
+// Two steps per launch (OCN_STEP_PAIR, MarchStep PAIR): the producer waves' new state (ssh, sshp,
+// ubrtr, ubrtrp, vbrtr, vbrtrp after the first step, by row parity mod 4) for the consumer waves
+#ifndef OCN_STEP_PAIR
+#define OCN_STEP_PAIR 1
+#endif
+#if OCN_STEP_PAIR
+__shared__ double g_pair[4][6][120];
+#endif
+#if OCN_STEP_STAGE
+__shared__ double g_step_out[2][6][240];       // sshn, sshp', ubrtrn, ubrtrp', vbrtrn, vbrtrp' of a row
+__shared__ unsigned char g_step_on[2][240];    // their store flags: lu | lcu << 1 | lcv << 2
 #endif
 
 // row constant k of table row r (rows[(id - OCN_DX) * nrows + r], real(4)); r + 1 for RC_RDNEXT
@@ -1724,6 +1795,9 @@ __device__ __forceinline__ double rcp_count(unsigned c)
 #ifndef OCN_STEP_MZ_FORCE
 #define OCN_STEP_MZ_FORCE 0   // A/B only: the known-constant variant assumes mu = +0 (a measurement of that saving)
 #endif
+#ifndef OCN_STEP_ILP
+#define OCN_STEP_ILP 1   // independent quotients of a row issued stage by stage together (MarchStep::dvn)
+#endif
 #ifndef OCN_STEP_PF2
 #define OCN_STEP_PF2 0   // 1: the known-constant variant issues each row's loads two rows ahead (measured: no gain)
 #endif
@@ -1765,6 +1839,11 @@ struct StepRegs {
     double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
     double tau, inv_tau, f;
     int nbad_cnt;                      // OCN_STEP_NBAD_ACC: this lane's check_ssh_err count of the tile
+    int dacc;                          // OCN_DIAG_NOCHK 2: the smallest dividend exponent of the tile
+    double dsink;                      // OCN_DIAG_NOSTORE: the sum of the outputs not stored
+    int32_t *nbp;                      // where this wave's check_ssh_err count goes (null: unchecked)
+    bool cnt;                          // the row is counted (PAIR producers: their workgroup's rows only)
+    int pj;                            // PAIR: the lane's column in the workgroup's LDS ring
     double hr0, mu0;                   // known-constant variant: the uniform h_r and mu (MarchStep::kc)
     const __attribute__((address_space(3))) double *lds;   // OCN_STEP_LDS: the workgroup's row constants
     unsigned rlo;                                            // table row of lds row 0
@@ -1857,7 +1936,11 @@ struct StepRegs {
 // the neighbours' state two points deep (ocn_ctx.hip one_step_x2: one 2-deep exchange per step),
 // so D there is formed here as the neighbour forms it on its interior -- what the reference's
 // exchanges of D deliver -- and the march covers the whole interior.
-template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR = false> struct MarchStep {
+template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR = false, bool PAIR = false>
+struct MarchStep {
+    static_assert(!PAIR || (ZF && !LAST && !X2), "two-step launches: the known-constant variant, no last step, no x2");
+    static constexpr bool kPair = PAIR;
+    static constexpr int kPairCols = 116;   // PAIR: a workgroup's output columns (2 x 60 produced, less 2 each side)
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
     static constexpr int kWaves = OCN_STEP_WAVES;
@@ -1868,6 +1951,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
     // check's verdict *fbz is 0 / nonzero (both variants launched, the device picks: no host wait)
     const double *kc; const int32_t *fbz; int gate;
     unsigned own;   // X2: own_class bits of the halo points neighbour blocks own
+    int32_t *nbad2 = nullptr;   // PAIR: the second step's check_ssh_err count (nbad: the first step's)
     static constexpr bool kGate = true;
     // gate (OCN_KC_DEVICE): which verdict of the check (launch_fallback_check's flag word: bit 0 =
     // h_r not uniform, bit 1 = anything else) this launch is for -- 1: none, 3: h_r only, 2: bit 1
@@ -1884,10 +1968,35 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
 
     // one row's loads for iteration n (rows of the state the march adds)
     struct Batch { double u, v, up, vp, ssh, shp, hr, mu, rhsx, rhsy; unsigned bits; };
-    __device__ __forceinline__ void load(const StepRegs &x, Batch &q, int m, int n) const
+    // RO (PAIR): 1 = a producer wave (rows clamped into the block's arrays: its tile reaches 4 rows
+    // past the consumers'), 2 = a consumer wave (the state rows from the LDS ring)
+    __device__ __forceinline__ int rowc(int r, int RO) const { return RO == 1 ? min(max(r, b.bnd_y1), b.bnd_y2) : r; }
+    template <int RO = 0> __device__ __forceinline__ void load(const StepRegs &x, Batch &q, int m, int n) const
     {
+#if OCN_STEP_PAIR
+        if constexpr (RO == 2) {
+            const Geo I = geo(&b);
+            const Pt c2 = I(m, n + 2);
+            q.ssh = g_pair[(n + 2) & 3][0][x.pj]; q.shp = g_pair[(n + 2) & 3][1][x.pj];
+            q.u = g_pair[(n + 2) & 3][2][x.pj]; q.up = g_pair[(n + 2) & 3][3][x.pj];
+            q.v = g_pair[(n + 1) & 3][4][x.pj]; q.vp = g_pair[(n + 1) & 3][5][x.pj];
+            q.hr = !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c2);
+            q.bits = ld(t.bits, c2);
+            q.mu = x.mu0;
+            q.rhsx = q.rhsy = 0.0;
+            return;
+        }
+#endif
+#if OCN_DIAG_NOLOAD   // (timing diagnostic only) the row's state made up from its index, nothing read
+        if (ZF && !HR) {
+            const double a = (double)(n & 7) * 0.125 + (double)(m & 3) * 0.25;
+            q.u = a * 0.01; q.up = a * 0.011; q.ssh = a * 0.1; q.shp = a * 0.09; q.hr = x.hr0; q.bits = 0xffu;
+            q.v = a * 0.012; q.vp = a * 0.013; q.mu = x.mu0; q.rhsx = q.rhsy = 0.0;
+            return;
+        }
+#endif
         const Geo I = geo(&b);
-        const Pt c = I(m, n), c1 = I(m, n + 1), c2 = I(m, n + 2);
+        const Pt c = I(m, rowc(n, RO)), c1 = I(m, rowc(n + 1, RO)), c2 = I(m, rowc(n + 2, RO));
         q.u = ld(t.f(OCN_UBRTR), c2); q.up = ld(t.f(OCN_UBRTRP), c2);
         q.ssh = ld(t.f(OCN_SSH), c2); q.shp = ld(t.f(OCN_SSHP), c2);
         q.hr = ZF && !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c2);
@@ -1964,6 +2073,26 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         if constexpr (E) return a / d;
         else return udiv(a, d, rd);
     }
+    // N independent quotients x[i] / d[i], each stage of udiv issued for all N before the next
+    // (OCN_STEP_ILP): the same operations on the same operands as N separate udivs, written so
+    // that N dependency chains are in flight at once rather than one after another
+    template <bool E, int N>
+    __device__ __forceinline__ static void dvn(const double (&a)[N], const double (&d)[N], const double (&rd)[N],
+                                               double (&out)[N])
+    {
+        if constexpr (E) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) out[i] = a[i] / d[i];
+        } else {
+            double q[N], t[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) q[i] = a[i] * rd[i];
+#pragma unroll
+            for (int i = 0; i < N; ++i) t[i] = __builtin_fma(q[i], d[i], -a[i]);
+#pragma unroll
+            for (int i = 0; i < N; ++i) out[i] = __builtin_fma(-t[i], rd[i], q[i]);
+        }
+    }
     template <bool E, int PH>
     __device__ __forceinline__ void derive(StepRegs &x, const Fallback &fb, int &acc, double &qb_next,
                                            double &qc_next) const
@@ -2001,11 +2130,22 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
             exp_check(acc, a_u0); exp_check(acc, a_v0); exp_check(acc, a_h0); exp_check(acc, a_u1);
             exp_check(acc, a_v1); exp_check(acc, x.up.s<PH>(2)); exp_check(acc, x.vp.s<PH>(2)); exp_check(acc, x.up.s<PH>(3));
         }
+#if OCN_STEP_ILP
+        // the nine first quotients (hh_init's five, a5's four) at once, then the five second ones
+        double q1[9], q2[5];
+        dvn<E, 9>({a_u0, a_v0, a_h0, a_u1, a_v1, x.up.s<PH>(2), x.vp.s<PH>(2), x.up.s<PH>(3), x.vp.s<PH>(2)},
+                  {dxt, dxh, dxb, dxt, dxh, dyh, dxh, x.cst<kLds>(RC_DXT, 2), dyt},
+                  {rxt, rxh, x.cst<kLds>(RC_RDXB, 1), rxt, rxh, ryh, rxh, x.cst<kLds>(RC_RDXT, 2), ryt}, q1);
+        dvn<E, 5>({q1[0], q1[1], q1[2], q1[3], q1[4]}, {dyh, dyt, dyb, dyh, dyt},
+                  {ryh, ryt, x.cst<kLds>(RC_RDYB, 1), ryh, ryt}, q2);
+        const double u0 = q2[0], v0 = q2[1], h0 = q2[2], u1 = q2[3], v1 = q2[4];
+#else
         const double u0 = dv<E>(dv<E>(a_u0, dxt, rxt), dyh, ryh);
         const double v0 = dv<E>(dv<E>(a_v0, dxh, rxh), dyt, ryt);
         const double h0 = dv<E>(dv<E>(a_h0, dxb, x.cst<kLds>(RC_RDXB, 1)), dyb, x.cst<kLds>(RC_RDYB, 1));
         const double u1 = dv<E>(dv<E>(a_u1, dxt, rxt), dyh, ryh);
         const double v1 = dv<E>(dv<E>(a_v1, dxh, rxh), dyt, ryt);
+#endif
         // a3 uv_trans_vort (vel_ssh.f90:247-281, sw_stencils.h uv_trans_vort_math)
         const double u_0 = x.u.s<PH>(2), u_1 = x.u.s<PH>(3), v_0 = x.v.s<PH>(2), v_r = shz(v_0, 1);
 #if OCN_STEP_CARRY
@@ -2017,8 +2157,12 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         // up/dyh at m-1 is the left lane's up/dyh (dyh is constant along the row), vp/dxh at n-1
         // is the previous row's, up/dxt at n+1 the next row's (formed here, kept for the next
         // row), vp/dyt at m+1 the right lane's -- the same operands, so the same values
+#if OCN_STEP_ILP
+        const double qa = q1[5], qb = q1[6], qc1 = q1[7], qe = q1[8];
+#else
         const double qa = dv<E>(x.up.s<PH>(2), dyh, ryh), qb = dv<E>(x.vp.s<PH>(2), dxh, rxh);
         const double qc1 = dv<E>(x.up.s<PH>(3), x.cst<kLds>(RC_DXT, 2), x.cst<kLds>(RC_RDXT, 2)), qe = dv<E>(x.vp.s<PH>(2), dyt, ryt);
+#endif
         const double st = x.cst<kLds>(RC_RAT0, 1) * (qa - shz(qa, -1)) - x.cst<kLds>(RC_RAT1, 1) * (qb - x.qb);
         const double ss = x.cst<kLds>(RC_RAT2, 1) * (qc1 - x.qc) + x.cst<kLds>(RC_RAT3, 1) * (shz(qe, 1) - qe);
         qb_next = qb;
@@ -2071,7 +2215,9 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         const double t1 = u * hu * dyh;
         const double a_ssh = t1 - shz(t1, -1) + x.t3.s<PH>(1) - x.t3.s<PH>(0);
         if (!E) exp_check(acc, a_ssh);
+#if !OCN_STEP_ILP
         const double sshn = x.shp.s<PH>(1) + 2.0 * x.tau * (-dv<E>(a_ssh, x.cst<kLds>(RC_AREA, 0), x.cst<kLds>(RC_RAREA, 0)));
+#endif
         // a4 uv_trans (vel_ssh.f90:283-373)
         const double u_r = shz(u, 1), u_l = shz(u, -1), u_n = x.u.s<PH>(2), u_s = x.u.s<PH>(0);
 #if OCN_STEP_CARRY
@@ -2100,6 +2246,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         }
         // a6 uv_diff2 (vel_ssh.f90:375-452)
         double rxd, ryd;
+        double q_ssh = 0.0;   // (OCN_STEP_ILP) a1's a_ssh / area
         {
             // ZF: mu is one value over the step's reach, so its neighbours are that value (the lane
             // shifts differ only on the edge lanes, which produce no output and whose mu terms no
@@ -2119,14 +2266,28 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
             if (ZF) {   // (A/B measurement only) mu = +0: a1..a4 are +-0 or NaN, a / d = a for the metrics
                 rxd = a1 + a2;
                 ryd = -a3 + a4;
+                q_ssh = dv<E>(a_ssh, x.cst<kLds>(RC_AREA, 0), x.cst<kLds>(RC_RAREA, 0));
             } else
 #endif
             {
                 if (!E) { exp_check(acc, a1); exp_check(acc, a2); exp_check(acc, a3); exp_check(acc, a4); }
+#if OCN_STEP_ILP   // a1's quotient with uv_diff2's four, stage by stage (dvn)
+                double qd[5];
+                dvn<E, 5>({a_ssh, a1, a2, a3, a4}, {x.cst<kLds>(RC_AREA, 0), dyh, dxt, dxh, dyt},
+                          {x.cst<kLds>(RC_RAREA, 0), x.cst<kLds>(RC_RDYH, 0), x.cst<kLds>(RC_RDXT, 0),
+                           x.cst<kLds>(RC_RDXH, 0), x.cst<kLds>(RC_RDYT, 0)}, qd);
+                q_ssh = qd[0];
+                rxd = qd[1] + qd[2];
+                ryd = -qd[3] + qd[4];
+#else
                 rxd = dv<E>(a1, dyh, x.cst<kLds>(RC_RDYH, 0)) + dv<E>(a2, dxt, x.cst<kLds>(RC_RDXT, 0));
                 ryd = -dv<E>(a3, dxh, x.cst<kLds>(RC_RDXH, 0)) + dv<E>(a4, dyt, x.cst<kLds>(RC_RDYT, 0));
+#endif
             }
         }
+#if OCN_STEP_ILP
+        const double sshn = x.shp.s<PH>(1) + 2.0 * x.tau * (-q_ssh);
+#endif
         // a7 sw_update_uv (vel_ssh.f90:108-195); hun = hu, hvn = hv (the reuse identity)
         double un, vn;
         {
@@ -2169,7 +2330,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
             // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
             const bool bd = o.lu && !(sshn < 10000.0 && sshn > -10000.0);
             if (OCN_STEP_NBAD_ACC) o.dbad = (int)bd - (int)(E && bad);   // (the re-run replaces the first count)
-            else if (__builtin_expect(nbad && bd != (E && bad), 0)) atomicAdd(nbad, bd ? 1 : -1);
+            else if (__builtin_expect(x.nbp && x.cnt && bd != (E && bad), 0)) atomicAdd(x.nbp, bd ? 1 : -1);
             bad = bd;
             return;
         }
@@ -2187,7 +2348,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
             st(sshp_out, c, fx);
             // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
             const bool b = !(sshn < 10000.0 && sshn > -10000.0);
-            if (nbad && b != (E && bad)) atomicAdd(nbad, b ? 1 : -1);
+            if (x.nbp && x.cnt && b != (E && bad)) atomicAdd(x.nbp, b ? 1 : -1);
             bad = b;
         }
         if (bc & (1u << OCN_LCU)) { st(t.f(OCN_UBRTRN), c, un); st(up_out, c, fa); }
@@ -2216,6 +2377,68 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         }
     }
 
+    static constexpr bool kStage = OCN_STEP_STAGE && ZF && !LAST && !PAIR;
+#if OCN_STEP_PAIR
+    // PAIR: the workgroup's barrier between iterations (LDS only: the row loads stay in flight)
+    __device__ __forceinline__ static void pair_barrier()
+    {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    }
+    // PAIR producer: row n of the first step's new state into the ring -- the value formed where
+    // the step updates the point (the store flags), the state it read elsewhere: what the buffers
+    // the second step reads hold there (outside a8's write sets the pairs and the second buffers
+    // agree with the ones read: MarchStep, one_step_fused)
+    template <int PH> __device__ __forceinline__ void pair_put(const StepRegs &x, const Out &o, int n) const
+    {
+        const int lane = (int)threadIdx.x & 63;
+        if (lane >= kHalo && lane < 64 - kHalo) {
+            double(*r)[120] = g_pair[n & 3];
+            r[0][x.pj] = o.lu ? o.sshn : x.ssh.s<PH>(1);
+            r[1][x.pj] = o.lu ? o.fx : x.shp.s<PH>(1);
+            r[2][x.pj] = o.cu ? o.un : x.u.s<PH>(1);
+            r[3][x.pj] = o.cu ? o.fa : x.up.s<PH>(1);
+            r[4][x.pj] = o.cv ? o.vn : x.v.s<PH>(1);
+            r[5][x.pj] = o.cv ? o.fb : x.vp.s<PH>(1);
+        }
+    }
+#endif
+#if OCN_STEP_STAGE
+    // (kStage, a full horizontal workgroup) row n's outputs through LDS, stored as whole lines
+    __device__ __forceinline__ void store_staged(const Out &o, const Lane &L, int n) const
+    {
+        const int lane = (int)threadIdx.x & 63, buf = n & 1;
+        if (L.out) {   // lanes kHalo .. 63 - kHalo: columns 60 wave .. 60 wave + 59 of the workgroup's
+            const int col = L.wave * 60 + lane - kHalo;
+            g_step_out[buf][0][col] = o.sshn;
+            g_step_out[buf][1][col] = o.fx;
+            g_step_out[buf][2][col] = o.un;
+            g_step_out[buf][3][col] = o.fa;
+            g_step_out[buf][4][col] = o.vn;
+            g_step_out[buf][5][col] = o.fb;
+            g_step_on[buf][col] = (unsigned char)((o.lu ? 1u : 0u) | (o.cu ? 2u : 0u) | (o.cv ? 4u : 0u));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   // LDS only: no wait for the
+#if !OCN_DIAG_NOBAR                                                       // row loads in flight
+        __builtin_amdgcn_s_barrier();
+#endif
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        const int col = L.wave * 64 + lane, cc = min(col, 239);
+        const unsigned f = col < 240 ? (unsigned)g_step_on[buf][cc] : 0u;
+        Out p;
+        p.lu = (f & 1u) != 0;
+        p.cu = (f & 2u) != 0;
+        p.cv = (f & 4u) != 0;
+        p.sshn = g_step_out[buf][0][cc];
+        p.fx = g_step_out[buf][1][cc];
+        p.un = g_step_out[buf][2][cc];
+        p.fa = g_step_out[buf][3][cc];
+        p.vn = g_step_out[buf][4][cc];
+        p.fb = g_step_out[buf][5][cc];
+        store_out(p, geo(&b)(L.wgm + cc, n).c);
+    }
+#endif
     static constexpr bool kLds = OCN_STEP_LDS && (ZF || OCN_STEP_LDS_GENERAL);
     // the march unrolled over the register ring (StepRegs::Win) -- the known-constant variant; the
     // general one (loaded h_r, mu, forcing, fallback values) keeps the rotating loop: unrolled,
@@ -2231,8 +2454,9 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
     {
         const int h = R.vert ? 4 * R.rows : R.rows, nb = R.n0 + ty * h;
         if (nb > R.n1) return;   // workgroup-uniform
-        const int ne = min(R.n1, nb + h - 1), lo = nb - 2 - b.bnd_y1, i = (int)threadIdx.x;
-        if (i < ne - nb + 5) {   // a thread per row
+        // rows [nb - 2, ne + 2]; PAIR: [nb - 5, ne + 4] (the producers' rows reach 2 past the consumers')
+        const int ne = min(R.n1, nb + h - 1), lo = nb - (PAIR ? 5 : 2) - b.bnd_y1, i = (int)threadIdx.x;
+        if (i < ne - nb + (PAIR ? 10 : 5)) {   // a thread per row
             const unsigned r = (unsigned)min(max(lo + i, 0), (int)t.nrows - 1);
 #pragma unroll
             for (int k = 0; k < kRowC; ++k) g_step_rc[i * kRowC + k] = row_const(t.rows, t.nrows, r, k);
@@ -2242,10 +2466,40 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
     }
 #endif
 
+    // PAIR (two steps in one launch, single block, known constants): the producer waves march the
+    // first step over the workgroup's rows +- 2 and put its new state into the LDS ring, the
+    // consumer waves march the second step over the workgroup's rows from there, 6 iterations
+    // behind (an iteration's ring reads are rows the producers finished before the last barrier);
+    // every wave passes R + 8 barriers (R = the tile's rows): at barrier interval t the producers
+    // write row nb - 4 + t, the consumers read rows nb - 5 + t and nb - 6 + t (their first reads,
+    // rows nb - 2 .. nb, in interval 5), so a ring of 4 rows is never read and written at once.  The launch writes
+    // the second step's new state where a single step writes (the new-state and second buffers):
+    // the pair is one role flip -- the first step's new state never reaches memory
     __device__ void march(const Lane &L, int nb, int ne) const
+    {
+#if OCN_STEP_PAIR
+        if constexpr (PAIR) {
+            if (L.pr == 1) {
+                march_role<1>(L, nb - 2, ne + 2);
+                pair_barrier();
+                pair_barrier();
+            } else {   // (march_role<2> has one more before its loop: after its first ring reads)
+#pragma unroll
+                for (int k = 0; k < 5; ++k) pair_barrier();
+                march_role<2>(L, nb, ne);
+            }
+            return;
+        }
+#endif
+        march_role<0>(L, nb, ne);
+    }
+    template <int RO> __device__ void march_role(const Lane &L, int nb, int ne) const
     {
         const Geo I = geo(&b);
         StepRegs x{};
+        x.nbp = RO == 2 ? nbad2 : nbad;
+        x.cnt = true;
+        x.pj = L.j;
 #if OCN_STEP_LDS
         if (kLds) {
             x.lds = (const __attribute__((address_space(3))) double *)g_step_rc;
@@ -2265,11 +2519,21 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         // h_r, bits at n0+1; vp at n0; metric rows n0, n0+1; the weights of row n0+1.
         const int n0 = nb - 2;
         {
-            const Pt c = I(L.m, n0), c1 = I(L.m, n0 + 1);
-            x.up.s<0>(2) = ld(t.f(OCN_UBRTRP), c1); x.ssh.s<0>(2) = ld(t.f(OCN_SSH), c1);
-            x.shp.s<0>(2) = ld(t.f(OCN_SSHP), c1); x.hr.s<0>(2) = ZF && !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c1);
-            x.bits.s<0>(2) = ld(t.bits, c1); x.u.s<0>(2) = ld(t.f(OCN_UBRTR), c1);
-            x.vp.s<0>(1) = ld(t.f(OCN_VBRTRP), c);
+            const Pt c = I(L.m, rowc(n0, RO)), c1 = I(L.m, rowc(n0 + 1, RO));
+#if OCN_STEP_PAIR
+            if constexpr (RO == 2) {   // the first step's new state from the ring
+                x.ssh.s<0>(2) = g_pair[(n0 + 1) & 3][0][x.pj]; x.shp.s<0>(2) = g_pair[(n0 + 1) & 3][1][x.pj];
+                x.u.s<0>(2) = g_pair[(n0 + 1) & 3][2][x.pj]; x.up.s<0>(2) = g_pair[(n0 + 1) & 3][3][x.pj];
+                x.vp.s<0>(1) = g_pair[n0 & 3][5][x.pj];
+            } else
+#endif
+            {
+                x.up.s<0>(2) = ld(t.f(OCN_UBRTRP), c1); x.ssh.s<0>(2) = ld(t.f(OCN_SSH), c1);
+                x.shp.s<0>(2) = ld(t.f(OCN_SSHP), c1); x.u.s<0>(2) = ld(t.f(OCN_UBRTR), c1);
+                x.vp.s<0>(1) = ld(t.f(OCN_VBRTRP), c);
+            }
+            x.hr.s<0>(2) = ZF && !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c1);
+            x.bits.s<0>(2) = ld(t.bits, c1);
             // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
             x.qb = x.vp.s<0>(1) / x.cst<kLds>(RC_DXH, 0);
             x.qc = x.up.s<0>(2) / x.cst<kLds>(RC_DXT, 1);
@@ -2278,7 +2542,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         Fallback fb;
         fallback<0>(x, fb, L.m, n0 + 1, 2);
 #if OCN_STEP_ONEBLOCK && OCN_STEP_PF2 && OCN_STEP_BUFST
-        if constexpr (kUnroll) {   // two batches in flight: iteration n takes qs[n - n0 & 1], loaded at n - 2
+        if constexpr (kUnroll && RO == 0) {   // two batches in flight: iteration n takes qs[n - n0 & 1], loaded at n - 2
             Batch qs[2];
             load(x, qs[0], L.m, n0);
             store_out(Out{}, 0u);   // (every lane dropped: the same operations after each batch's loads as
@@ -2298,32 +2562,38 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         }
 #endif
         Batch q;
-        load(x, q, L.m, n0);
+        load<RO>(x, q, L.m, n0);
 #if OCN_STEP_BUFST
-        store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
+        if (RO != 1) store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
+#endif
+#if OCN_STEP_PAIR
+        // PAIR consumer: its first ring reads (rows nb - 2 .. nb, finished by the producers 2 barriers
+        // ago) precede the barrier after which the producers overwrite row nb - 2's slot with nb + 2
+        if constexpr (RO == 2) pair_barrier();
 #endif
 #if OCN_STEP_ONEBLOCK
         // the two warm-up rows (D only), then rows nb .. ne with D and S in one basic block
-        iteration<0, true>(x, fb, q, L, n0, nb, ne);
+        iteration<0, true, RO>(x, fb, q, L, n0, nb, ne);
         if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
-            iteration<1, true>(x, fb, q, L, n0 + 1, nb, ne);
+            iteration<1, true, RO>(x, fb, q, L, n0 + 1, nb, ne);
             for (int n = nb;; n += kRing) {
-                if (iteration<2>(x, fb, q, L, n, nb, ne)) break;
-                if (iteration<3>(x, fb, q, L, n + 1, nb, ne)) break;
-                if (iteration<4>(x, fb, q, L, n + 2, nb, ne)) break;
-                if (iteration<0>(x, fb, q, L, n + 3, nb, ne)) break;
-                if (iteration<1>(x, fb, q, L, n + 4, nb, ne)) break;
+                if (iteration<2, false, RO>(x, fb, q, L, n, nb, ne)) break;
+                if (iteration<3, false, RO>(x, fb, q, L, n + 1, nb, ne)) break;
+                if (iteration<4, false, RO>(x, fb, q, L, n + 2, nb, ne)) break;
+                if (iteration<0, false, RO>(x, fb, q, L, n + 3, nb, ne)) break;
+                if (iteration<1, false, RO>(x, fb, q, L, n + 4, nb, ne)) break;
             }
         } else {
             x.rotate();
-            iteration<0, true>(x, fb, q, L, n0 + 1, nb, ne);
+            iteration<0, true, RO>(x, fb, q, L, n0 + 1, nb, ne);
             x.rotate();
             for (int n = nb;; ++n) {
-                if (iteration<0>(x, fb, q, L, n, nb, ne)) break;
+                if (iteration<0, false, RO>(x, fb, q, L, n, nb, ne)) break;
                 x.rotate();
             }
         }
         if (OCN_STEP_NBAD_ACC && nbad && x.nbad_cnt != 0) atomicAdd(nbad, x.nbad_cnt);
+        if (OCN_DIAG_NOCHK == 2 && nbad && x.dacc < -5000) atomicAdd(nbad, 1);   // (never: keeps the checks)
 #else
         if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
             for (int n = n0;; n += kRing) {
@@ -2347,7 +2617,7 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
     // block (no branch between them: the scheduler interleaves S's work with D's division chains)
     // and one wave-uniform test after both re-runs the two with IEEE divisions if any dividend of
     // either was out of udiv's range (nothing is stored before: store_out follows)
-    template <int PH, bool WARM = false>
+    template <int PH, bool WARM = false, int RO = 0>
     __device__ __forceinline__ bool iteration(StepRegs &x, Fallback &fb, Batch &q, const Lane &L0, int n, int nb,
                                               int ne) const
     {
@@ -2355,12 +2625,27 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
         // where used, not held per phase across the unrolled loop
         Lane L = L0;
         asm volatile("" : "+v"(L.m));
+        if (RO == 1) {   // PAIR producer: rows outside the interior keep their state; the count is
+            L.out = L.out && n >= b.ny_start && n <= b.ny_end;   // the workgroup's own rows' (nb + 2 .. ne - 2)
+            x.cnt = n >= nb + 2 && n <= ne - 2;
+        }
         take<PH>(x, q);
         Fallback fbn;
         if (n < ne) fallback<PH>(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
-        if (n + kAhead - 1 < ne) load(x, q, L.m, n + kAhead);   // in flight while this row (and the next) is computed
+        if (n + kAhead - 1 < ne) load<RO>(x, q, L.m, n + kAhead);   // in flight while this row (and the next) is computed
         Out o;
-#if OCN_STEP_ONEBLOCK
+#if OCN_DIAG_NOCHK
+        {
+            int acc = 0;
+            double qb, qc;
+            bool bad = false;
+            derive<false, PH>(x, fb, acc, qb, qc);
+            if (!WARM) step<false, PH>(x, L, n, acc, bad, o);
+            x.dacc = min(x.dacc, acc);
+            x.qb = qb;
+            x.qc = qc;
+        }
+#elif OCN_STEP_ONEBLOCK
         {
             int acc = 0;
             double qb, qc;
@@ -2403,9 +2688,30 @@ template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR 
             if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) step<true, PH>(x, L, n, acc, bad, o);
         }
 #endif
+#if OCN_STEP_PAIR
+        if constexpr (RO == 1) {   // the producers' row goes into the ring, not to memory
+            if (!WARM) pair_put<PH>(x, o, n);
+            pair_barrier();
+            ++x.rn;
+            fb = fbn;
+            return n >= ne;
+        }
+#endif
 #if OCN_STEP_BUFST
-        store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
+#if OCN_DIAG_NOSTORE   // (timing diagnostic only) the row's outputs summed, not stored
+        x.dsink += o.sshn + o.fx + o.un + o.fa + o.vn + o.fb;
+        if (n == ne && x.dsink == 1.2345e-300) store_out(o, geo(&b)(L.m, n).c);
+#else
+#if OCN_STEP_STAGE
+        if (kStage && !WARM && L.wgm >= 0) store_staged(o, L, n);   // (wave-uniform; workgroup-uniform)
+        else
+#endif
+            store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
+#endif
         if (OCN_STEP_NBAD_ACC) x.nbad_cnt += o.dbad;
+#endif
+#if OCN_STEP_PAIR
+        if constexpr (RO == 2) pair_barrier();
 #endif
         ++x.rn;
         fb = fbn;
@@ -2588,7 +2894,8 @@ template <class Body> static int step_rows(const Range &r, bool vert)
 template <class Body> static int launch_step(const ocn_block *b, const Range &r, const Body &body, hipStream_t s)
 {
     MarchGrid g{};
-    g.r[0] = march_rect<Body>(b, r, step_rows<Body>(r, OCN_STEP_VERT != 0), OCN_STEP_VERT != 0);
+    const bool vert = OCN_STEP_VERT != 0 && !Body::kStage;   // staged stores: waves side by side
+    g.r[0] = march_rect<Body>(b, r, step_rows<Body>(r, vert), vert);
     g.nr = 1;
     g.ntiles = g.r[0].tiles;
     return issue_march(g, body, s);
@@ -2709,6 +3016,60 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 #undef OCN_STEP_VARIANT
 #undef OCN_STEP_LAUNCH
     return OCN_OK;
+}
+
+// Rows per workgroup tile of the two-step launch: the fewest iterations in total, counting
+// ceil(waves / slots) rounds of rows + 8 iterations each (MarchStep::march)
+static int pair_rows(const Range &r, int cols)
+{
+    const long wx = (r.m1 - r.m0 + cols) / cols, h = r.n1 - r.n0 + 1;
+    int best = 8;
+    long cost = -1;
+    for (int rows = 8; rows <= kStepLdsRows - 10; ++rows) {
+        const long tiles = (h + rows - 1) / rows, waves = 4 * tiles * wx,
+                   rounds = (waves + OCN_STEP_SLOTS - 1) / OCN_STEP_SLOTS, c = rounds * (rows + 8);
+        if (cost < 0 || c < cost) { cost = c; best = rows; }
+    }
+    return best;
+}
+
+int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                        double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
+                        hipStream_t s, const OnepassKC &kc)
+{
+#if OCN_STEP_PAIR
+    if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
+        !up_out || !vp_out)
+        return set_error(OCN_ERR_ARG, "two-step launch: compact tables, march, full_free_surface = 1, trans_terms and "
+                                      "ksw_lat on, three second buffers");
+    if ((kc.mode != OCN_KC_KNOWN && kc.mode != OCN_KC_KNOWN_HR) || !kc.kc)
+        return set_error(OCN_ERR_ARG, "two-step launch: a known-constant verdict");
+    RC_K(check_block(b));
+    const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
+    const Range r = range_interior(b);
+    if (range_empty(r)) return OCN_OK;
+    using KP = MarchStep<true, false, true, false, false, true>;
+    const int cols = KP::kPairCols, rows = pair_rows(r, cols);
+    MarchGrid g{};
+    const int ntx = (r.m1 - r.m0 + cols) / cols;
+    g.r[0] = MarchRect{r.m0, r.m1, r.n0, r.n1, r.m0, ntx, ntx * ((r.n1 - r.n0 + rows) / rows), max(r.m0 - 4, b->bnd_x1),
+                       min(r.m1 + 4, b->bnd_x2), rows, 0};
+    g.nr = 1;
+    g.ntiles = g.r[0].tiles;
+    int ex;
+    const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
+#define OCN_PAIR_LAUNCH(P, H)                                                                                    \
+    return issue_march(g, MarchStep<P, false, true, false, H, true>{*b, t, sw, tau, nbad1, sshp_out, up_out, vp_out, \
+                                                                    kc.kc, nullptr, 0, 0u, nbad2}, s)
+    if (kc.mode == OCN_KC_KNOWN_HR) { if (p2) OCN_PAIR_LAUNCH(true, true); OCN_PAIR_LAUNCH(false, true); }
+    if (p2) OCN_PAIR_LAUNCH(true, false);
+    OCN_PAIR_LAUNCH(false, false);
+#undef OCN_PAIR_LAUNCH
+#else
+    (void)b; (void)ptr; (void)nptr; (void)cp; (void)sw; (void)tau; (void)nbad1; (void)nbad2; (void)sshp_out;
+    (void)up_out; (void)vp_out; (void)s; (void)kc;
+    return set_error(OCN_ERR_ARG, "two-step launch: not built (OCN_STEP_PAIR 0)");
+#endif
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy

@@ -224,6 +224,18 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_BATCH, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_pair(self, mode: int = 1):
+        """Two one-pass steps per launch (default 1: on single blocks of at least 512 x 512 interior
+        points; 2: any block; 0: never): the first step's new state stays on chip; same results bit
+        for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_PAIR, int(mode)), "ocn_ctx_set_option")
+        return self
+
+    @property
+    def pair_active(self) -> bool:
+        """Whether the last step() ran two one-pass steps per launch."""
+        return self.option(_lib.OPT_PAIR) == 2
+
     @property
     def x2_active(self) -> bool:
         """Whether the last step() used one-pass steps with 2-deep state exchanges."""

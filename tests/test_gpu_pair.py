@@ -1,0 +1,103 @@
+"""GPU parity of the two-step launches (OCN_OPT_PAIR, sw_kernels.hip MarchStep PAIR): two one-pass
+steps per launch on one block -- the producer waves' first step kept in LDS, the consumer waves'
+second step written where a single step writes -- bitwise against the reference fixtures.
+
+A pair needs the known-constant verdict on the host, which a synchronising call hands it
+(ocn_ctx_synchronize reads the device check): so the runs below make a first short call, a
+synchronize(), then the rest -- the lazy tail keeps the one-pass sequence open across them, and
+every call's steps but its last run as pairs.  Tolerance: none (fp64, the reference's order).
+"""
+import pytest
+
+from tests.golden import cases
+from tests.test_gpu_parity import build_model, compare_case
+
+pytestmark = pytest.mark.gpu
+
+# single-block cases with every SW term on (the one-pass step's conditions)
+PAIR_CASES = ["box70x54_b1x1_s20", "box48x40_cart_s10", "bs_b1x1_s60", "bs_b1x1_s604", "box70x54_topo_b1x1_s20",
+              "box1024_b1x1_s10", "box4096_b1x1_s6", "box1521x1111_b1x1_s604"]
+
+
+@pytest.fixture(scope="module")
+def amd():
+    import ocean_model_arch_amd as amd
+    amd.lib()
+    return amd
+
+
+def _splits(steps, pattern):
+    if pattern == "2+rest":
+        return [2, steps - 2]
+    if pattern == "1,odd,even":   # pairs over odd and even call lengths, calls of 1 between
+        a = max(1, (steps - 2) // 2) | 1
+        return [1, a, 1, steps - a - 2] if steps - a - 2 > 0 else [1, steps - 1]
+    raise ValueError(pattern)
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["stream", "graph"])
+@pytest.mark.parametrize("pattern", ["2+rest", "1,odd,even"])
+@pytest.mark.parametrize("name", PAIR_CASES)
+def test_pair_steps_match_reference(amd, name, pattern, graph):
+    case = cases.load_e2e(name)
+    if graph and case["steps"] > 100:
+        pytest.skip("long runs: stream only")
+    m = build_model(amd, case, graph=graph).set_pair(2).init()
+    used = []
+    try:
+        for i, n in enumerate(_splits(case["steps"], pattern)):
+            m.step(n, tau=1.0, check_every=1)
+            if i == 0:
+                m.synchronize()   # the known-constant verdict reaches the host
+            used.append(m.pair_active)
+        m.synchronize()
+        bad = compare_case(m, case, name)
+        one = m.onepass_active
+    finally:
+        m.close()
+    assert not bad, f"{name} ({pattern}, graph {graph}): fields differ from the reference: {bad}"
+    assert one
+    # a call of n >= 3 steps after the verdict runs pairs (its last step stays single)
+    calls = _splits(case["steps"], pattern)
+    assert all(u == (i > 0 and n >= 3) for i, (u, n) in enumerate(zip(used, calls))), (used, calls)
+
+
+@pytest.mark.parametrize("name", ["box70x54_b1x1_s20", "box1024_b1x1_s10"])
+def test_pair_default_threshold(amd, name):
+    """OCN_OPT_PAIR 1 (the default): pairs on blocks of at least 512 x 512 interior points only;
+    0: never -- both bitwise."""
+    case = cases.load_e2e(name)
+    for mode in (1, 0):
+        m = build_model(amd, case).set_pair(mode).init()
+        try:
+            m.step(2, tau=1.0, check_every=1).synchronize()
+            m.step(case["steps"] - 2, tau=1.0, check_every=1).synchronize()
+            used = m.pair_active
+            bad = compare_case(m, case, name)
+        finally:
+            m.close()
+        assert not bad, f"{name} (pair {mode}): fields differ from the reference: {bad}"
+        assert used == (mode == 1 and name.startswith("box1024")), (mode, used)
+
+
+def test_pair_counts_blowup_points_once(amd):
+    """check_ssh_err_kernel (vel_ssh.f90:40-67) in pair launches: each step counts its points once
+    (the producers count only their workgroup's own rows) -- the reported count equals the single
+    launches' count."""
+    msgs = []
+    for mode in (2, 0):
+        m = amd.OceanModel(amd.box_config(200)).set_pair(mode).init()
+        m.step(2, check_every=1).synchronize()
+        s = m.download(0, "ssh")
+        s[60:140, 60:140] = 2.0e4   # an 80 x 80 patch: it crosses workgroup row tiles
+        for nm in ("ssh", "sshn", "sshp"):
+            m.upload(0, nm, s)
+        # the upload re-checks the known constants: a call without counts hands the verdict over
+        m.step(1, check_every=0).synchronize()
+        with pytest.raises(amd.OcnError) as e:
+            m.step(4, check_every=1).synchronize()
+        used = m.pair_active
+        msgs.append(str(e.value))
+        m.close()
+        assert used == (mode == 2), (mode, used)
+    assert msgs[0] == msgs[1], msgs
