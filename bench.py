@@ -276,18 +276,18 @@ SIMDS = 256 * 4
 
 def load_valu(amd, stage: str, launch_ms: float, box, blocks):
     """The dominant kernel's VALU issue from the committed SQ counter pass (profiles/sq_valu.json,
-    scripts/sq_valu.py) -- only for the one-pass step, and only when that pass was taken on this
+    scripts/sq_valu.py) -- only for the one-pass launches (single and pair), and only when that pass was taken on this
     exact library build and workload.  issue_floor_ms: its VALU instructions spread over the
     1024 SIMDs at one wave64 instruction per quad-cycle at the peak clock (the time the launch
     would take if VALU issue were its only limit); issue_frac = that floor / the live launch time."""
-    if stage != "onepass":
+    if stage not in ("onepass", "onepass2"):
         return None
     try:
         d = json.load(open(os.path.join(REPO, "profiles", "sq_valu.json")))
         if (d.get("build_id") != amd.build_id() or list(d.get("box", [])) != list(box) or
                 list(d.get("blocks", [])) != list(blocks)):
             return None
-        pl, pw = d["per_launch"], d["per_wave"]
+        pl, pw = d["kernels"][stage]["per_launch"], d["kernels"][stage]["per_wave"]
         floor_ms = pl["SQ_INSTS_VALU"] * 4.0 / SIMDS / (SHADER_CLOCK_GHZ * 1e9) * 1e3
         wc = pw["SQ_WAVE_CYCLES"]
         return {"insts_per_launch": int(pl["SQ_INSTS_VALU"]), "issue_floor_ms": round(floor_ms, 4),

@@ -23,6 +23,7 @@
 
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -404,7 +405,7 @@ struct MetRows {
 // the workgroup's first output column (else -1), wave = this wave's index in it.
 // Two-step launches (a body's kPair): pr = 1 for the producer waves, 2 for the consumers, j = the
 // lane's column in the workgroup's LDS ring.
-struct Lane { int m, me; bool edge, out; int wgm = -1, wave = 0, pr = 0, j = 0; };
+struct Lane { int m, me; bool edge, out; int wgm = -1, wave = 0, pr = 0, j = 0; bool ccol = true; };
 
 // Loaded columns are clamped to [mlo, mhi] (inside the block array); a lane whose column was
 // clamped never produces output and its value is read by no output lane.
@@ -546,6 +547,7 @@ template <class Body> __device__ __forceinline__ void march_tile(const MarchRect
         L.pr = prod ? 1 : 2;
         L.j = min(max(m - (c0 - 2), 0), 2 * 60 - 1);
         L.out = lane >= 2 && lane < 62 && m >= R.m0 && m <= (prod ? R.m1 : min(R.m1, c0 + Body::kPairCols - 1));
+        L.ccol = m >= c0 && m < c0 + Body::kPairCols;   // a producer counts its workgroup's columns only
         L.m = L.me = min(max(m, R.mlo), R.mhi);
         L.edge = false;
         body.march(L, nb, ne);
@@ -1703,7 +1705,11 @@ enum RowC { RC_DX, RC_DY, RC_DXT, RC_DYT, RC_DXH, RC_DYH, RC_DXB, RC_DYB, RC_RDX
 #ifndef OCN_STEP_LDS_GENERAL
 #define OCN_STEP_LDS_GENERAL 0   // also in the general variant (its VGPRs spill: 0.83 vs 0.64 ms at 4096^2)
 #endif
-constexpr int kStepLdsRows = 4 * OCN_STEP_ROWS + 4;   // a workgroup's 4 stacked tiles + 2 rows each side
+#ifndef OCN_PAIR_MAX_ROWS
+#define OCN_PAIR_MAX_ROWS 150   // the tallest workgroup tile of the two-step launch (its rows +- 5 in LDS)
+#endif
+// a workgroup's 4 stacked tiles + 2 rows each side; a two-step workgroup's tile + 5 above, 4 below
+constexpr int kStepLdsRows = 4 * OCN_STEP_ROWS + 4 > OCN_PAIR_MAX_ROWS + 10 ? 4 * OCN_STEP_ROWS + 4 : OCN_PAIR_MAX_ROWS + 10;
 
 #if OCN_STEP_LDS
 __shared__ double g_step_rc[kStepLdsRows * kRowC];   // the workgroup's rows [nb - 2, ne + 2]
@@ -1795,6 +1801,9 @@ __device__ __forceinline__ double rcp_count(unsigned c)
 #ifndef OCN_STEP_MZ_FORCE
 #define OCN_STEP_MZ_FORCE 0   // A/B only: the known-constant variant assumes mu = +0 (a measurement of that saving)
 #endif
+#ifndef OCN_STEP_FACE
+#define OCN_STEP_FACE 1   // each flux across a row face / lane face formed once (MarchStep::step, face)
+#endif
 #ifndef OCN_STEP_ILP
 #define OCN_STEP_ILP 1   // independent quotients of a row issued stage by stage together (MarchStep::dvn)
 #endif
@@ -1802,6 +1811,7 @@ __device__ __forceinline__ double rcp_count(unsigned c)
 #define OCN_STEP_PF2 0   // 1: the known-constant variant issues each row's loads two rows ahead (measured: no gain)
 #endif
 static_assert(!(OCN_STEP_NBAD_ACC && OCN_STEP_PF2), "OCN_STEP_NBAD_ACC: the one-row-ahead loop only");
+static_assert(!OCN_STEP_FACE || (OCN_STEP_ONEBLOCK && !OCN_DIAG_NOCHK), "OCN_STEP_FACE: the OCN_STEP_ONEBLOCK iteration");
 // StepRegs::Win: 4 rows, written out for kRing phases (MarchStep::march); even with OCN_STEP_PF2,
 // so that the batch a phase takes (phase parity) is known in every unrolled phase
 constexpr int kRing = OCN_STEP_PF2 ? 6 : 5;
@@ -1842,8 +1852,9 @@ struct StepRegs {
     int dacc;                          // OCN_DIAG_NOCHK 2: the smallest dividend exponent of the tile
     double dsink;                      // OCN_DIAG_NOSTORE: the sum of the outputs not stored
     int32_t *nbp;                      // where this wave's check_ssh_err count goes (null: unchecked)
-    bool cnt;                          // the row is counted (PAIR producers: their workgroup's rows only)
+    bool cnt;                          // the point is counted (PAIR producers: their workgroup's points only)
     int pj;                            // PAIR: the lane's column in the workgroup's LDS ring
+    double fyx, fyy, vht, a2t;         // OCN_STEP_FACE: row n-1's n faces (MarchStep::face)
     double hr0, mu0;                   // known-constant variant: the uniform h_r and mu (MarchStep::kc)
     const __attribute__((address_space(3))) double *lds;   // OCN_STEP_LDS: the workgroup's row constants
     unsigned rlo;                                            // table row of lds row 0
@@ -2194,11 +2205,34 @@ struct MarchStep {
         x.dxq.s<PH>(2) = x.cst<kLds>(RC_DX2, 1) * x.mu.s<PH>(2) * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
     }
 
+#if OCN_STEP_FACE
+    // (the warm-up row n = nb - 1, after D(nb)) the n+1 faces of row n that S(nb) takes from the
+    // row before -- the expressions S(n) forms them with (step)
+    template <int PH> __device__ __forceinline__ void face(StepRegs &x) const
+    {
+        const double u = x.u.s<PH>(1), v = x.v.s<PH>(1), u_n = x.u.s<PH>(2), v_n = x.v.s<PH>(2);
+#if OCN_STEP_CARRY
+        const double v_r = x.vr.s<PH>(1);
+#else
+        const double v_r = shz(v, 1);
+#endif
+        const double pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2), luu = D(x.mk<PH>(OCN_LUU, 0, 0));
+        x.fyx = (pv + shz(pv, 1)) / 2.0 * (u_n + u) / 2.0 * luu;
+        x.vht = x.vh.s<PH>(1) * (v_r + v);
+        x.fyy = (pv + pvn) / 2.0 * (v + v_n) / 2.0;
+        if constexpr (ZF) {   // (uv_diff2_math's muh_p with mu one value: its lane shifts are the value)
+            const double mu = x.mu.s<PH>(1), mu_n = x.mu.s<PH>(2), muh_p = (mu + mu + mu_n + mu_n) / 4.0;
+            x.a2t = x.cst<kLds>(RC_DXB2, 0) * muh_p * x.hh.s<PH>(1) * x.sts.s<PH>(1);
+        }
+    }
+#endif
+
     // a row's outputs and where they are stored (OCN_STEP_BUFST: stored after S's branch)
     struct Out {
         bool lu = false, cu = false, cv = false, uu = false;   // uu: luu (LAST's vort / str_s)
         double sshn = 0.0, fx = 0.0, un = 0.0, fa = 0.0, vn = 0.0, fb = 0.0;
         double vort = 0.0, sts = 0.0, stt = 0.0, rxa = 0.0, rxd = 0.0, rya = 0.0, ryd = 0.0;   // LAST
+        double fyx = 0.0, fyy = 0.0, vht = 0.0, a2t = 0.0;   // OCN_STEP_FACE: row n's n+1 faces (see face)
         int dbad = 0;   // OCN_STEP_NBAD_ACC: the row's change to the lane's check_ssh_err count
     };
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
@@ -2228,6 +2262,30 @@ struct MarchStep {
         const double pu = x.pu.s<PH>(1), pun = x.pu.s<PH>(2), pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2), pvs = x.pv.s<PH>(0);
         const double luu = D(x.mk<PH>(OCN_LUU, 0, 0)), luus = D(x.mk<PH>(OCN_LUU, 0, -1));
         double rxa, rya;
+#if OCN_STEP_FACE
+        // each face's flux once: the m-1 face is the left lane's m+1 face and the n-1 face the row
+        // before's n+1 face (carried in x, face<PH>) -- the same operands, the sums' terms swapped
+        // (IEEE addition commutes), so the same values bit for bit
+        (void)luus; (void)u_l; (void)v_l; (void)u_s; (void)v_s; (void)v_sr; (void)pvs;
+        {
+            const double fx_p = (pu + shz(pu, 1)) / 2.0 * (u + u_r) / 2.0;
+            const double fx_m = shz(fx_p, -1);
+            const double fy_p = (pv + shz(pv, 1)) / 2.0 * (u_n + u) / 2.0 * luu;
+            const double cor = x.vh.s<PH>(1) * (v_r + v);
+            rxa = -(fx_p - fx_m + fy_p - x.fyx) + (cor + x.vht) / 4.0;
+            o.fyx = fy_p;
+            o.vht = cor;
+        }
+        {
+            const double fy_p = (pv + pvn) / 2.0 * (v + v_n) / 2.0;
+            const double sn = pu + pun;
+            const double fx_p = sn / 2.0 * (v_r + v) / 2.0;
+            const double fx_m = shz(fx_p, -1);
+            const double q = x.vh.s<PH>(1) * (u_n + u);
+            rya = -(fx_p - fx_m + fy_p - x.fyy) - (q + shz(q, -1)) / 4.0;
+            o.fyy = fy_p;
+        }
+#else
         {
             const double fx_p = (pu + shz(pu, 1)) / 2.0 * (u + u_r) / 2.0;
             const double fx_m = (pu + shz(pu, -1)) / 2.0 * (u + u_l) / 2.0;
@@ -2244,6 +2302,7 @@ struct MarchStep {
             const double q = x.vh.s<PH>(1) * (u_n + u);
             rya = -(fx_p - fx_m + fy_p - fy_m) - (q + shz(q, -1)) / 4.0;
         }
+#endif
         // a6 uv_diff2 (vel_ssh.f90:375-452)
         double rxd, ryd;
         double q_ssh = 0.0;   // (OCN_STEP_ILP) a1's a_ssh / area
@@ -2259,9 +2318,26 @@ struct MarchStep {
             const double dxb2 = x.cst<kLds>(RC_DXB2, 0), dxb2m = x.cst<kLds>(RC_DXB2, -1), dyb2 = x.cst<kLds>(RC_DYB2, 0);
             const double sts = x.sts.s<PH>(1);
             const double dtc = x.dt.s<PH>(1);
+#if OCN_STEP_FACE
+            // ZF: the three averages are one value, so a2's second term is the row before's first
+            // (carried) and a4's the left lane's first -- the same operands, the same values
+            double a2, a4;
+            if constexpr (ZF) {
+                (void)dxb2m; (void)muh_m; (void)muh_m2;
+                const double a2p = dxb2 * muh_p * hh * sts, a4p = dyb2 * muh_p * hh * sts;
+                a2 = a2p - x.a2t;
+                a4 = a4p - shz(a4p, -1);
+                o.a2t = a2p;
+            } else {
+                a2 = dxb2 * muh_p * hh * sts - dxb2m * muh_m * x.hh.s<PH>(0) * x.sts.s<PH>(0);
+                a4 = dyb2 * muh_p * hh * sts - dyb2 * muh_m2 * shz(hh, -1) * shz(sts, -1);
+            }
+            const double a1 = shz(dtc, 1) - dtc, a3 = x.dxq.s<PH>(2) - x.dxq.s<PH>(1);
+#else
             const double a1 = shz(dtc, 1) - dtc, a2 = dxb2 * muh_p * hh * sts - dxb2m * muh_m * x.hh.s<PH>(0) * x.sts.s<PH>(0);
             const double a3 = x.dxq.s<PH>(2) - x.dxq.s<PH>(1),
                          a4 = dyb2 * muh_p * hh * sts - dyb2 * muh_m2 * shz(hh, -1) * shz(sts, -1);
+#endif
 #if OCN_STEP_MZ_FORCE
             if (ZF) {   // (A/B measurement only) mu = +0: a1..a4 are +-0 or NaN, a / d = a for the metrics
                 rxd = a1 + a2;
@@ -2625,9 +2701,9 @@ struct MarchStep {
         // where used, not held per phase across the unrolled loop
         Lane L = L0;
         asm volatile("" : "+v"(L.m));
-        if (RO == 1) {   // PAIR producer: rows outside the interior keep their state; the count is
-            L.out = L.out && n >= b.ny_start && n <= b.ny_end;   // the workgroup's own rows' (nb + 2 .. ne - 2)
-            x.cnt = n >= nb + 2 && n <= ne - 2;
+        if (RO == 1) {   // PAIR producer: rows outside the interior keep their state; the count is the
+            L.out = L.out && n >= b.ny_start && n <= b.ny_end;   // workgroup's own points' (its columns,
+            x.cnt = L.ccol && n >= nb + 2 && n <= ne - 2;        // rows nb + 2 .. ne - 2)
         }
         take<PH>(x, q);
         Fallback fbn;
@@ -2658,6 +2734,9 @@ struct MarchStep {
             if (WARM) {
                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0))
                     derive<true, PH>(x, fb, acc, qb, qc);
+#if OCN_STEP_FACE
+                if (n == nb - 1) face<PH>(x);
+#endif
             } else {
                 bool bad = false;
 #if OCN_STEP_SCHEDB >= 0
@@ -2668,6 +2747,12 @@ struct MarchStep {
                     if (OCN_STEP_JOINT) derive<true, PH>(x, fb, acc, qb, qc);
                     step<true, PH>(x, L, n, acc, bad, o);
                 }
+#if OCN_STEP_FACE
+                x.fyx = o.fyx;
+                x.fyy = o.fyy;
+                x.vht = o.vht;
+                if (ZF) x.a2t = o.a2t;
+#endif
             }
             x.qb = qb;
             x.qc = qc;
@@ -3023,9 +3108,11 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 static int pair_rows(const Range &r, int cols)
 {
     const long wx = (r.m1 - r.m0 + cols) / cols, h = r.n1 - r.n0 + 1;
+    if (const char *e = getenv("OCN_PAIR_ROWS"))   // (a tuning override: a fixed tile height)
+        if (const int v = atoi(e); v >= 8 && v <= OCN_PAIR_MAX_ROWS) return v;
     int best = 8;
     long cost = -1;
-    for (int rows = 8; rows <= kStepLdsRows - 10; ++rows) {
+    for (int rows = 8; rows <= OCN_PAIR_MAX_ROWS; ++rows) {
         const long tiles = (h + rows - 1) / rows, waves = 4 * tiles * wx,
                    rounds = (waves + OCN_STEP_SLOTS - 1) / OCN_STEP_SLOTS, c = rounds * (rows + 8);
         if (cost < 0 || c < cost) { cost = c; best = rows; }

@@ -69,6 +69,9 @@ def main():
         m = re.search(r"ocn::(\w+)", k.replace("k_range<ocn::", "").replace("k_march<ocn::", ""))
         name = m.group(1) if m else k
         stage = STAGE.get(name)
+        t = re.search(r"MarchStep<([^>]*)>", k)
+        if t and [a.strip() for a in t.group(1).split(",")][5:6] == ["true"]:   # MarchStep PAIR: two steps
+            stage, name = "onepass2", "MarchStep(pair)"
         if not stage:
             continue
         for c in ("FETCH_SIZE", "WRITE_SIZE"):

@@ -77,7 +77,8 @@ def test_valu_needs_matching_stamp(tmp_path, monkeypatch):
     build and workload it was taken on; 1024 SIMDs x 1 wave64 instruction per quad-cycle at 2.4 GHz."""
     per_launch = {"SQ_INSTS_VALU": 1024 * 2.4e6 / 4, "SQ_WAVES": 10}     # 1 ms of issue
     per_wave = {"SQ_WAVE_CYCLES": 100.0, "SQ_ACTIVE_INST_VALU": 60.0, "SQ_WAIT_INST_ANY": 30.0, "SQ_WAIT_ANY": 10.0}
-    rec = {"build_id": "abc", "box": [64, 64], "blocks": [1, 1], "per_launch": per_launch, "per_wave": per_wave}
+    rec = {"build_id": "abc", "box": [64, 64], "blocks": [1, 1],
+           "kernels": {"onepass": {"per_launch": per_launch, "per_wave": per_wave}}}
     (tmp_path / "profiles").mkdir()
     (tmp_path / "profiles" / "sq_valu.json").write_text(json.dumps(rec))
     monkeypatch.setattr(bench, "REPO", str(tmp_path))

@@ -92,8 +92,9 @@ def test_pair_counts_blowup_points_once(amd):
         s[60:140, 60:140] = 2.0e4   # an 80 x 80 patch: it crosses workgroup row tiles
         for nm in ("ssh", "sshn", "sshp"):
             m.upload(0, nm, s)
-        # the upload re-checks the known constants: a call without counts hands the verdict over
-        m.step(1, check_every=0).synchronize()
+        # the upload re-checks the known constants: a one-pass call without counts hands the
+        # verdict over (a call of 3: one-pass steps whatever hh_init's state)
+        m.step(3, check_every=0).synchronize()
         with pytest.raises(amd.OcnError) as e:
             m.step(4, check_every=1).synchronize()
         used = m.pair_active
