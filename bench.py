@@ -145,11 +145,17 @@ def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one:
                     tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False):
     """The launches of a timed region: ocn_ctx_step calls of calls[i] steps each, then (lazy) the
     pending tail formed by ocn_ctx_complete."""
-    out = []
+    out, total = [], sum(calls)
+    if lazy and one and pair:   # an open sequence with pairs: every two steps one launch, across calls
+        out += [("onepass2", "onepass2" + _kc(zero))] * (sum(calls) // 2)
+        calls = []
     for n in calls:
         out += call_launches(n, flip, rc, ring, one, tracers, zero=zero, lazy=lazy, pair=pair)
     if lazy and one:
-        out += [(t, k + (_kc(zero) if t == "onepass" else "")) for t, k in TAIL_LAUNCHES]
+        tail = TAIL_LAUNCHES
+        if pair:   # the last launch a pair: its first step again, then the tail; an odd step left
+            tail = TAIL_LAUNCHES if total % 2 else [("onepass", "onepass")] + TAIL_LAUNCHES   # runs as the last
+        out += [(t, k + (_kc(zero) if t == "onepass" else "")) for t, k in tail]
     return out
 
 

@@ -264,6 +264,11 @@ struct ocn_ctx {
     hipStream_t stream = nullptr;
     hipStream_t comm_stream = nullptr;  // halo exchanges overlapped with interior compute
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // the known-constant check's verdict copied to pinned host memory behind an event: a later call
+    // reads it once the event has completed (hipEventQuery: no wait), learn_fb_async
+    hipEvent_t ev_fb = nullptr;
+    int32_t *h_fbz = nullptr;
+    bool fb_copy = false;
     int overlap = -1;            // OCN_OPT_OVERLAP: 0 none, 1 standard steps, 2 + role-flip steps, -1 auto
     int32_t *d_nbad = nullptr;
     ncclComm_t comm = nullptr;
@@ -333,6 +338,13 @@ struct ocn_ctx {
     // intact in the other buffers, as the call's last step), so 1-step calls run one-pass steps
     bool lazy = true, open = false, open_x2 = false;
     double open_tau = 0.0;
+    // pairs in an open sequence (one_step_pair): open_pair = its last launch was a pair (the state
+    // before it is two steps back: complete_open redoes the pair's first step single, then the tail);
+    // deferred = one step of the sequence not yet run (a call's odd step waits for the next call's
+    // first to run as a pair; complete_open runs it as the last step, synchronize as a plain one)
+    bool open_pair = false;
+    int deferred = 0;
+    bool deferred_check = false;
     // one_step_x2 (OCN_OPT_X2): its static conditions (ext_ok: the real(4) fields are init_state's,
     // so the ext rows are the neighbours' metric rows; rows_x_ok: their divisors in udiv's range;
     // edge_ring_sea: a8 / a9 work on a halo ring no neighbour fills), the device checks of the last
@@ -2220,6 +2232,8 @@ int ocn_ctx_create(const ocn_basin *basin, const ocn_sw_params *sw, const ocn_de
     }
     if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming), "hipEventCreate");
     if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming), "hipEventCreate");
+    if (!rc) rc = check_hip(hipEventCreateWithFlags(&c->ev_fb, hipEventDisableTiming), "hipEventCreate");
+    if (!rc) rc = check_hip(hipHostMalloc((void **)&c->h_fbz, sizeof(int32_t), hipHostMallocDefault), "hipHostMalloc");
     if (!rc) rc = decompose(c);
     if (!rc) rc = allocate(c);
     if (!rc) rc = prebuild_plans(c);
@@ -2312,6 +2326,8 @@ int ocn_ctx_destroy(ocn_ctx *c)
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_fb) (void)hipEventDestroy(c->ev_fb);
+    if (c->h_fbz) (void)hipHostFree(c->h_fbz);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -2416,6 +2432,8 @@ int ocn_ctx_init_state(ocn_ctx *c)
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
     c->open = false;   // a pending call tail is void: every field is formed again
+    c->open_pair = false;
+    c->deferred = 0;
     c->coherent_known = false;
     c->alt_ok = false;
     c->fb_state = kFbUnchecked;
@@ -2538,6 +2556,18 @@ static void learn_fb(ocn_ctx *c)
     int32_t f = 0;
     if (hipMemcpy(&f, c->d_fbz, sizeof(f), hipMemcpyDeviceToHost) != hipSuccess) return;
     c->fb_state = f == 0 ? kFbZero : f == 1 ? kFbHr : kFbGeneral;
+    c->fb_copy = false;
+}
+
+// Without a synchronising call: the verdict's copy (prepare_kc) has arrived if its event has
+// completed -- a query, never a wait -- so a caller of 1-step calls gets the host-chosen variant
+// (and pair launches) a few calls after the check.
+static void learn_fb_async(ocn_ctx *c)
+{
+    if (c->fb_state != kFbDevice || !c->fb_copy || hipEventQuery(c->ev_fb) != hipSuccess) return;
+    const int32_t f = *(volatile int32_t *)c->h_fbz;
+    c->fb_state = f == 0 ? kFbZero : f == 1 ? kFbHr : kFbGeneral;
+    c->fb_copy = false;
 }
 
 // The one-pass variant of this call (OCN_KC_*): the known-constant one only when its precondition
@@ -2552,6 +2582,7 @@ static void learn_fb(ocn_ctx *c)
 static int prepare_kc(ocn_ctx *c, bool x2 = false)
 {
     if (!c->known_const || c->r8_handed) { c->kc_mode = OCN_KC_GENERAL; return OCN_OK; }
+    learn_fb_async(c);
     if (c->fb_state != kFbUnchecked && x2 && !c->fb_x2) c->fb_state = kFbUnchecked;
     if (c->fb_state == kFbUnchecked) {
         HIPCHK(hipMemsetAsync(c->d_fbz, 0, sizeof(int32_t), c->stream));
@@ -2560,6 +2591,11 @@ static int prepare_kc(ocn_ctx *c, bool x2 = false)
             if (x2) tab[field_slot(OCN_HHQ_REST)] = b.hr_x;
             const Range r = x2 ? Range{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end} : onepass_inner(b, 1);
             RC(launch_fallback_check(&b.g, tab.data(), b.bits, r, c->d_fbz, b.kc, c->stream, x2 ? b.own : 0u));
+        }
+        if (!c->capturing) {   // the verdict to pinned host memory, learn_fb_async
+            HIPCHK(hipMemcpyAsync(c->h_fbz, c->d_fbz, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipEventRecord(c->ev_fb, c->stream));
+            c->fb_copy = true;
         }
         c->fb_state = kFbDevice;
         c->fb_x2 = x2;
@@ -2620,8 +2656,22 @@ static int complete_open(ocn_ctx *c)
     if (!c->open) return OCN_OK;
     c->open = false;
     HIPCHK(hipSetDevice(c->dec.device));
+    if (c->deferred) {   // a step not yet run: it is the last one, from the current state
+        c->deferred = 0;
+        c->open_pair = false;
+        StepKind k{};
+        k.last = k.one_last = true;
+        k.check = c->deferred_check;
+        return finish_call(c, one_step_fused(c, c->open_tau, k));
+    }
     swap_roles(c);
     swap_alt3(c);
+    if (c->open_pair) {   // the last launch was a pair (one flip, two steps): its first step again
+        c->open_pair = false;
+        StepKind k1{};
+        k1.flip = k1.one = k1.next_one = k1.a_done = true;   // (counted the first time: no check)
+        if (const int rc = run_step(c, c->open_tau, k1)) return finish_call(c, rc);
+    }
     StepKind k{};
     k.last = k.one_last = true;
     k.x2_end = c->ring2_saved;   // x2 steps: the second ring restored, the first exchanged (x2_end)
@@ -2645,20 +2695,44 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
             RC(prepare_kc(c, c->open_x2));
             const bool pairs = !c->open_x2 && pair_ok(c);
             int rc = OCN_OK;
-            for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
-                StepKind k{};
-                k.check = check_every > 0 && (s % check_every == 0);
-                k.flip = k.one = k.next_one = k.a_done = true;
-                k.x2 = c->open_x2;
-                if (pairs && s + 1 < nsteps) {   // (the call's last step stays single: the tail redoes it)
-                    k.pair = true;
-                    k.check2 = check_every > 0 && ((s + 1) % check_every == 0);
-                    ++s;
-                    c->pair_used = true;
+            if (pairs) {   // every two steps one launch -- a step deferred by the last call first -- and
+                           // an odd one left deferred to the next call (or to complete_open)
+                std::vector<char> chk;
+                if (c->deferred) chk.push_back(c->deferred_check);
+                for (int s = 1; s <= nsteps; ++s) chk.push_back(check_every > 0 && (s % check_every == 0));
+                c->deferred = 0;
+                size_t i = 0;
+                for (; i + 1 < chk.size() && rc == OCN_OK; i += 2) {
+                    StepKind k{};
+                    k.check = chk[i];
+                    k.check2 = chk[i + 1];
+                    k.flip = k.one = k.next_one = k.a_done = k.pair = true;
+                    rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
+                    c->open_pair = c->pair_used = true;
                 }
-                rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
+                if (rc == OCN_OK && i < chk.size()) {
+                    c->deferred = 1;
+                    c->deferred_check = chk[i];
+                }
+            } else {
+                if (c->deferred) {   // (pairs no longer possible: the deferred step runs first)
+                    StepKind k{};
+                    k.check = c->deferred_check;
+                    k.flip = k.one = k.next_one = k.a_done = true;
+                    k.x2 = c->open_x2;
+                    c->deferred = 0;
+                    rc = run_step(c, tau, k);
+                }
+                for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
+                    StepKind k{};
+                    k.check = check_every > 0 && (s % check_every == 0);
+                    k.flip = k.one = k.next_one = k.a_done = true;
+                    k.x2 = c->open_x2;
+                    rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
+                    c->open_pair = false;
+                }
             }
-            if (rc) { c->open = false; return finish_call(c, rc); }
+            if (rc) { c->open = false; c->deferred = 0; c->open_pair = false; return finish_call(c, rc); }
             return OCN_OK;
         }
         RC(complete_open(c));
@@ -2770,6 +2844,8 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     }
     if (lazy_end && rc == OCN_OK) {   // the pending tail: complete_open
         c->open = true;
+        c->open_pair = false;   // (the call's last step ran single)
+        c->deferred = 0;
         c->open_tau = tau;
         c->open_x2 = x2_call;
         return OCN_OK;
@@ -2793,6 +2869,14 @@ int ocn_ctx_synchronize(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
+    if (c->open && c->deferred) {   // a deferred step runs now (its check_ssh_err count is looked at)
+        StepKind k{};
+        k.check = c->deferred_check;
+        k.flip = k.one = k.next_one = k.a_done = true;
+        c->deferred = 0;
+        c->open_pair = false;
+        if (const int rc = run_step(c, c->open_tau, k)) { c->open = false; return finish_call(c, rc); }
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     learn_fb(c);
     int32_t nbad = 0;

@@ -2,10 +2,11 @@
 steps per launch on one block -- the producer waves' first step kept in LDS, the consumer waves'
 second step written where a single step writes -- bitwise against the reference fixtures.
 
-A pair needs the known-constant verdict on the host, which a synchronising call hands it
-(ocn_ctx_synchronize reads the device check): so the runs below make a first short call, a
-synchronize(), then the rest -- the lazy tail keeps the one-pass sequence open across them, and
-every call's steps but its last run as pairs.  Tolerance: none (fp64, the reference's order).
+A pair needs the known-constant verdict on the host: a synchronising call hands it over (and, without
+one, its copy in pinned memory once its event has completed), so the runs below make a first short
+call, a synchronize(), then the rest -- the lazy tail keeps the one-pass sequence open across calls,
+every two steps run as one launch and an odd one waits for the next call (a synchronize() runs it
+alone, a read of the fields as the last step).  Tolerance: none (fp64, the reference's order).
 """
 import pytest
 
@@ -57,9 +58,13 @@ def test_pair_steps_match_reference(amd, name, pattern, graph):
         m.close()
     assert not bad, f"{name} ({pattern}, graph {graph}): fields differ from the reference: {bad}"
     assert one
-    # a call of n >= 3 steps after the verdict runs pairs (its last step stays single)
-    calls = _splits(case["steps"], pattern)
-    assert all(u == (i > 0 and n >= 3) for i, (u, n) in enumerate(zip(used, calls))), (used, calls)
+    # after the verdict every two steps run as one launch, an odd step waiting for the next call's
+    # first (a call with a step deferred from the last one and n new ones takes d + n)
+    calls, want, d = _splits(case["steps"], pattern), [], 0
+    for i, n in enumerate(calls):
+        want.append(i > 0 and d + n >= 2)
+        d = (d + n) % 2 if i > 0 else 0
+    assert used == want, (used, want, calls)
 
 
 @pytest.mark.parametrize("name", ["box70x54_b1x1_s20", "box1024_b1x1_s10"])
@@ -102,3 +107,23 @@ def test_pair_counts_blowup_points_once(amd):
         m.close()
         assert used == (mode == 2), (mode, used)
     assert msgs[0] == msgs[1], msgs
+
+
+@pytest.mark.parametrize("name", ["box1024_b1x1_s10", "box1521x1111_b1x1_s604"])
+def test_pair_one_step_calls(amd, name):
+    """The reference's cadence (model.f90:146: one expl_shallow_water per step) with pairs: 1-step
+    calls and no synchronising call -- the verdict arrives through its pinned copy, then every
+    second call runs two steps in one launch -- bitwise; the tail formed by the reads."""
+    case = cases.load_e2e(name)
+    m = build_model(amd, case).init()
+    used = []
+    try:
+        for _ in range(case["steps"]):
+            m.step(1, tau=1.0, check_every=1)
+            used.append(m.pair_active)
+        bad = compare_case(m, case, name)
+        m.synchronize()
+    finally:
+        m.close()
+    assert not bad, f"{name} (1-step calls): fields differ from the reference: {bad}"
+    assert any(used), "no pair launch"
