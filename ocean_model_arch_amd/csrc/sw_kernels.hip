@@ -401,11 +401,9 @@ struct MetRows {
 // One lane of a march: its loaded column m, its edge column me (aligned layout: lane 0 m-1,
 // lane 63 m+1, both clamped into the block array), whether it is an edge lane, whether it
 // produces output.
-// Staged stores (a body's kStage, horizontal workgroups whose 4 waves all produce output): wgm =
-// the workgroup's first output column (else -1), wave = this wave's index in it.
 // Two-step launches (a body's kPair): pr = 1 for the producer waves, 2 for the consumers, j = the
-// lane's column in the workgroup's LDS ring.
-struct Lane { int m, me; bool edge, out; int wgm = -1, wave = 0, pr = 0, j = 0; bool ccol = true; };
+// lane's column in the workgroup's LDS ring, ccol = the lane's column is the workgroup's (counted).
+struct Lane { int m, me; bool edge, out; int pr = 0, j = 0; bool ccol = true; };
 
 // Loaded columns are clamped to [mlo, mhi] (inside the block array); a lane whose column was
 // clamped never produces output and its value is read by no output lane.
@@ -425,10 +423,6 @@ template <class B> struct WavesOf<B, std::void_t<decltype(B::kWaves)>> { static 
 // a body with a workgroup prologue (Body::prologue(R, ty), called by all 4 waves of a workgroup)
 template <class B, class = void> struct HasPrologue { static constexpr bool v = false; };
 template <class B> struct HasPrologue<B, std::void_t<decltype(B::kPrologue)>> { static constexpr bool v = B::kPrologue; };
-// a body that may stage a row's outputs through LDS so that whole 128-B lines are stored
-// (Body::kStage; march_tile sets Lane::wgm where the workgroup qualifies)
-template <class B, class = void> struct HasStage { static constexpr bool v = false; };
-template <class B> struct HasStage<B, std::void_t<decltype(B::kStage)>> { static constexpr bool v = B::kStage; };
 // a two-step body (Body::kPair: MarchStep PAIR; march_tile deals its waves the two roles)
 template <class B, class = void> struct HasPair { static constexpr bool v = false; };
 template <class B> struct HasPair<B, std::void_t<decltype(B::kPair)>> { static constexpr bool v = B::kPair; };
@@ -566,10 +560,6 @@ template <class Body> __device__ __forceinline__ void march_tile(const MarchRect
         L.out = lane >= Body::kHalo && lane < 64 - Body::kHalo && m <= R.m1;
         L.m = L.me = min(max(m, R.mlo), R.mhi);
         L.edge = false;
-    }
-    if constexpr (HasStage<Body>::v) {   // workgroup-uniform: 4 waves side by side, the last one full
-        const int wg0 = R.w0 + tx * 4 * cols;
-        if (!R.vert && wg0 + 4 * cols - 1 <= R.m1) { L.wgm = wg0; L.wave = wave; }
     }
     body.march(L, nb, ne);
 }
@@ -1669,9 +1659,6 @@ __device__ __forceinline__ double udiv(double x, double d, double rd)
     return __builtin_fma(-t, rd, q);
 }
 // the smallest frexp exponent of the dividends of a row (0 for x = 0)
-#ifndef OCN_DIAG_NOBAR
-#define OCN_DIAG_NOBAR 0   // timing diagnostics only: staged stores without the workgroup barrier
-#endif
 #ifndef OCN_DIAG_NOSTORE
 #define OCN_DIAG_NOSTORE 0   // timing diagnostics only: the one-pass march stores nothing (outputs summed)
 #endif
@@ -1715,28 +1702,15 @@ constexpr int kStepLdsRows = 4 * OCN_STEP_ROWS + 4 > OCN_PAIR_MAX_ROWS + 10 ? 4 
 __shared__ double g_step_rc[kStepLdsRows * kRowC];   // the workgroup's rows [nb - 2, ne + 2]
 __shared__ unsigned g_step_rlo;                       // table row of its first row
 #endif
-// Staged stores (OCN_STEP_STAGE, the known-constant variant): a wave's 60 output columns are
-// 480 B, so every wave boundary splits a 128-B line between two waves, and such stores cost HBM
-// bandwidth (scripts/linebench.hip, the one-pass step's 6 + 6 array mix streamed in the march
-// shape: 4.19 TB/s in the 60-column layout, 4.73 with whole lines; write-only 3.65 vs 4.70).  With
-// 4 waves side by side a workgroup's 240 output columns are 15 whole lines: each wave puts its
-// row of outputs into LDS, and after a workgroup barrier wave w stores columns [64 w, 64 w + 64)
-// of each array -- whole 128-B lines (the interior starts on a 256-B boundary, ocn_ctx.hip
-// allocate).  Two buffers alternate by row parity (a buffer is rewritten two barriers later).
-#ifndef OCN_STEP_STAGE
-#define OCN_STEP_STAGE 0   // measured slower: 0.407-0.424 vs 0.391 ms per 4096^2 launch (the barrier per row)
-#endif
 // Two steps per launch (OCN_STEP_PAIR, MarchStep PAIR): the producer waves' new state (ssh, sshp,
-// ubrtr, ubrtrp, vbrtr, vbrtrp after the first step, by row parity mod 4) for the consumer waves
+// ubrtr, ubrtrp, vbrtr, vbrtrp after the first step, by row mod 4) for the consumer waves.
+// (Measured and dropped: a wave's 60-column output rows stored as whole 128-B lines through LDS,
+// a workgroup barrier per row -- 0.407-0.424 against 0.391 ms per 4096^2 single launch.)
 #ifndef OCN_STEP_PAIR
 #define OCN_STEP_PAIR 1
 #endif
 #if OCN_STEP_PAIR
 __shared__ double g_pair[4][6][120];
-#endif
-#if OCN_STEP_STAGE
-__shared__ double g_step_out[2][6][240];       // sshn, sshp', ubrtrn, ubrtrp', vbrtrn, vbrtrp' of a row
-__shared__ unsigned char g_step_on[2][240];    // their store flags: lu | lcu << 1 | lcv << 2
 #endif
 
 // row constant k of table row r (rows[(id - OCN_DX) * nrows + r], real(4)); r + 1 for RC_RDNEXT
@@ -2453,7 +2427,6 @@ struct MarchStep {
         }
     }
 
-    static constexpr bool kStage = OCN_STEP_STAGE && ZF && !LAST && !PAIR;
 #if OCN_STEP_PAIR
     // PAIR: the workgroup's barrier between iterations (LDS only: the row loads stay in flight)
     __device__ __forceinline__ static void pair_barrier()
@@ -2478,41 +2451,6 @@ struct MarchStep {
             r[4][x.pj] = o.cv ? o.vn : x.v.s<PH>(1);
             r[5][x.pj] = o.cv ? o.fb : x.vp.s<PH>(1);
         }
-    }
-#endif
-#if OCN_STEP_STAGE
-    // (kStage, a full horizontal workgroup) row n's outputs through LDS, stored as whole lines
-    __device__ __forceinline__ void store_staged(const Out &o, const Lane &L, int n) const
-    {
-        const int lane = (int)threadIdx.x & 63, buf = n & 1;
-        if (L.out) {   // lanes kHalo .. 63 - kHalo: columns 60 wave .. 60 wave + 59 of the workgroup's
-            const int col = L.wave * 60 + lane - kHalo;
-            g_step_out[buf][0][col] = o.sshn;
-            g_step_out[buf][1][col] = o.fx;
-            g_step_out[buf][2][col] = o.un;
-            g_step_out[buf][3][col] = o.fa;
-            g_step_out[buf][4][col] = o.vn;
-            g_step_out[buf][5][col] = o.fb;
-            g_step_on[buf][col] = (unsigned char)((o.lu ? 1u : 0u) | (o.cu ? 2u : 0u) | (o.cv ? 4u : 0u));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   // LDS only: no wait for the
-#if !OCN_DIAG_NOBAR                                                       // row loads in flight
-        __builtin_amdgcn_s_barrier();
-#endif
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        const int col = L.wave * 64 + lane, cc = min(col, 239);
-        const unsigned f = col < 240 ? (unsigned)g_step_on[buf][cc] : 0u;
-        Out p;
-        p.lu = (f & 1u) != 0;
-        p.cu = (f & 2u) != 0;
-        p.cv = (f & 4u) != 0;
-        p.sshn = g_step_out[buf][0][cc];
-        p.fx = g_step_out[buf][1][cc];
-        p.un = g_step_out[buf][2][cc];
-        p.fa = g_step_out[buf][3][cc];
-        p.vn = g_step_out[buf][4][cc];
-        p.fb = g_step_out[buf][5][cc];
-        store_out(p, geo(&b)(L.wgm + cc, n).c);
     }
 #endif
     static constexpr bool kLds = OCN_STEP_LDS && (ZF || OCN_STEP_LDS_GENERAL);
@@ -2787,11 +2725,7 @@ struct MarchStep {
         x.dsink += o.sshn + o.fx + o.un + o.fa + o.vn + o.fb;
         if (n == ne && x.dsink == 1.2345e-300) store_out(o, geo(&b)(L.m, n).c);
 #else
-#if OCN_STEP_STAGE
-        if (kStage && !WARM && L.wgm >= 0) store_staged(o, L, n);   // (wave-uniform; workgroup-uniform)
-        else
-#endif
-            store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
+        store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
 #endif
         if (OCN_STEP_NBAD_ACC) x.nbad_cnt += o.dbad;
 #endif
@@ -2979,8 +2913,7 @@ template <class Body> static int step_rows(const Range &r, bool vert)
 template <class Body> static int launch_step(const ocn_block *b, const Range &r, const Body &body, hipStream_t s)
 {
     MarchGrid g{};
-    const bool vert = OCN_STEP_VERT != 0 && !Body::kStage;   // staged stores: waves side by side
-    g.r[0] = march_rect<Body>(b, r, step_rows<Body>(r, vert), vert);
+    g.r[0] = march_rect<Body>(b, r, step_rows<Body>(r, OCN_STEP_VERT != 0), OCN_STEP_VERT != 0);
     g.nr = 1;
     g.ntiles = g.r[0].tiles;
     return issue_march(g, body, s);
