@@ -127,3 +127,49 @@ def test_pair_one_step_calls(amd, name):
         m.close()
     assert not bad, f"{name} (1-step calls): fields differ from the reference: {bad}"
     assert any(used), "no pair launch"
+
+
+def _ops_run(amd, pair, ops):
+    """One context driven through `ops` -- ("step", n, tau) / ("sync",) / ("read", field) /
+    ("bump", field): a download, a small change, an upload -- then every field of every block."""
+    import numpy as np
+    m = amd.OceanModel(amd.box_config(600)).set_pair(pair).init()
+    used = False
+    try:
+        for op in ops:
+            if op[0] == "step":
+                m.step(op[1], tau=op[2], check_every=1)
+                used |= m.pair_active
+            elif op[0] == "sync":
+                m.synchronize()
+            elif op[0] == "read":
+                m.download(0, op[1])
+            elif op[0] == "bump":
+                a = m.download(0, op[1])
+                a[300, 280] += 1.0e-3
+                m.upload(0, op[1], a)
+        m.synchronize()
+        out = {nm: m.download(0, nm) for nm in m.field_names}
+    finally:
+        m.close()
+    assert all(np.isfinite(v).all() for v in out.values())
+    return out, used
+
+
+@pytest.mark.parametrize("seq", ["tau", "reads", "upload"])
+def test_pair_deferral_matches_single_launches(amd, seq):
+    """Pairs across calls under the entries that end or look into an open sequence -- a change of
+    tau with a step deferred (it runs as the last step of the old tau), reads of fields between
+    calls (the tail formed: after a pair its first step again, a deferred step as the last), an
+    upload between calls, synchronize() with a step deferred (it runs alone) -- bitwise the same
+    fields as one launch per step."""
+    base = [("step", 2, 1.0), ("sync",), ("step", 3, 1.0)]   # the verdict, then a pair + 1 deferred
+    more = {"tau": [("step", 1, 0.5), ("step", 3, 0.5), ("step", 1, 1.0)],
+            "reads": [("read", "ssh"), ("step", 1, 1.0), ("step", 2, 1.0), ("read", "ubrtr"), ("step", 5, 1.0),
+                      ("sync",), ("step", 1, 1.0)],
+            "upload": [("bump", "ssh"), ("step", 2, 1.0), ("sync",), ("step", 3, 1.0), ("step", 1, 1.0)]}[seq]
+    a, used = _ops_run(amd, 1, base + more)
+    b, _ = _ops_run(amd, 0, base + more)
+    assert used
+    bad = [nm for nm in a if a[nm].tobytes() != b[nm].tobytes()]
+    assert not bad, f"{seq}: fields differ between pair and single launches: {bad}"
