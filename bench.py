@@ -146,15 +146,16 @@ def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one:
     """The launches of a timed region: ocn_ctx_step calls of calls[i] steps each, then (lazy) the
     pending tail formed by ocn_ctx_complete."""
     out, total = [], sum(calls)
-    if lazy and one and pair:   # an open sequence with pairs: every two steps one launch, across calls
-        out += [("onepass2", "onepass2" + _kc(zero))] * (sum(calls) // 2)
+    if lazy and one and pair:   # an open sequence with pairs: two steps per launch across calls while
+        # 3 or more are pending; the last 1 or 2 run by ocn_ctx_complete
+        out += [("onepass2", "onepass2" + _kc(zero))] * ((total - 1) // 2)
         calls = []
     for n in calls:
         out += call_launches(n, flip, rc, ring, one, tracers, zero=zero, lazy=lazy, pair=pair)
     if lazy and one:
         tail = TAIL_LAUNCHES
-        if pair:   # the last launch a pair: its first step again, then the tail; an odd step left
-            tail = TAIL_LAUNCHES if total % 2 else [("onepass", "onepass")] + TAIL_LAUNCHES   # runs as the last
+        if pair:   # the steps left pending run as the last ones: 1 (the tail) or 2 (a single + the tail)
+            tail = TAIL_LAUNCHES if total % 2 else [("onepass", "onepass")] + TAIL_LAUNCHES
         out += [(t, k + (_kc(zero) if t == "onepass" else "")) for t, k in tail]
     return out
 
@@ -456,7 +457,8 @@ def main():
     rc = model.recompute_active
     one = model.onepass_active
     one_zero = True if model.onepass_zero else "h" if model.onepass_hr else False
-    pair = model.pair_active
+    # pair launches ran in the timed region: their timer counted them (graph replays: no timers)
+    pair = ("onepass2" in times) if times else model.pair_active
     model_overlap = model.overlap_level
     if world > 1:
         t = torch.tensor([dt], device="cuda")

@@ -340,11 +340,13 @@ struct ocn_ctx {
     double open_tau = 0.0;
     // pairs in an open sequence (one_step_pair): open_pair = its last launch was a pair (the state
     // before it is two steps back: complete_open redoes the pair's first step single, then the tail);
-    // deferred = one step of the sequence not yet run (a call's odd step waits for the next call's
-    // first to run as a pair; complete_open runs it as the last step, synchronize as a plain one)
+    // deferred = the last 1 or 2 steps of the sequence, not yet run: a call runs pairs while 3 or
+    // more steps are pending and leaves the rest to the next call -- the 1-step cadence runs a pair
+    // every second call -- or to complete_open, which runs them as the last steps (a single + the
+    // last step, or the last step: no step run twice); synchronize runs them (as a pair or alone)
     bool open_pair = false;
     int deferred = 0;
-    bool deferred_check = false;
+    bool deferred_check[2] = {false, false};
     // one_step_x2 (OCN_OPT_X2): its static conditions (ext_ok: the real(4) fields are init_state's,
     // so the ext rows are the neighbours' metric rows; rows_x_ok: their divisors in udiv's range;
     // edge_ring_sea: a8 / a9 work on a halo ring no neighbour fills), the device checks of the last
@@ -2656,12 +2658,19 @@ static int complete_open(ocn_ctx *c)
     if (!c->open) return OCN_OK;
     c->open = false;
     HIPCHK(hipSetDevice(c->dec.device));
-    if (c->deferred) {   // a step not yet run: it is the last one, from the current state
+    if (c->deferred) {   // steps not yet run: the last ones, from the current state
+        const int d = c->deferred;
         c->deferred = 0;
         c->open_pair = false;
+        if (d == 2) {
+            StepKind k1{};
+            k1.check = c->deferred_check[0];
+            k1.flip = k1.one = k1.next_one = k1.a_done = true;
+            if (const int rc = run_step(c, c->open_tau, k1)) return finish_call(c, rc);
+        }
         StepKind k{};
         k.last = k.one_last = true;
-        k.check = c->deferred_check;
+        k.check = c->deferred_check[d - 1];
         return finish_call(c, one_step_fused(c, c->open_tau, k));
     }
     swap_roles(c);
@@ -2695,14 +2704,13 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
             RC(prepare_kc(c, c->open_x2));
             const bool pairs = !c->open_x2 && pair_ok(c);
             int rc = OCN_OK;
-            if (pairs) {   // every two steps one launch -- a step deferred by the last call first -- and
-                           // an odd one left deferred to the next call (or to complete_open)
-                std::vector<char> chk;
-                if (c->deferred) chk.push_back(c->deferred_check);
+            if (pairs) {   // two steps per launch -- the steps deferred by the last call first -- while
+                           // 3 or more are pending; the last 1 or 2 deferred (next call, complete_open)
+                std::vector<char> chk(c->deferred_check, c->deferred_check + c->deferred);
                 for (int s = 1; s <= nsteps; ++s) chk.push_back(check_every > 0 && (s % check_every == 0));
                 c->deferred = 0;
                 size_t i = 0;
-                for (; i + 1 < chk.size() && rc == OCN_OK; i += 2) {
+                for (; i + 2 < chk.size() && rc == OCN_OK; i += 2) {
                     StepKind k{};
                     k.check = chk[i];
                     k.check2 = chk[i + 1];
@@ -2710,19 +2718,19 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
                     rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
                     c->open_pair = c->pair_used = true;
                 }
-                if (rc == OCN_OK && i < chk.size()) {
-                    c->deferred = 1;
-                    c->deferred_check = chk[i];
+                if (rc == OCN_OK) {
+                    c->deferred = (int)(chk.size() - i);   // 1 or 2
+                    for (int j = 0; j < c->deferred; ++j) c->deferred_check[j] = chk[i + j];
                 }
             } else {
-                if (c->deferred) {   // (pairs no longer possible: the deferred step runs first)
+                for (int j = 0; j < c->deferred && rc == OCN_OK; ++j) {   // (no pairs now: deferred steps first)
                     StepKind k{};
-                    k.check = c->deferred_check;
+                    k.check = c->deferred_check[j];
                     k.flip = k.one = k.next_one = k.a_done = true;
                     k.x2 = c->open_x2;
-                    c->deferred = 0;
                     rc = run_step(c, tau, k);
                 }
+                c->deferred = 0;
                 for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
                     StepKind k{};
                     k.check = check_every > 0 && (s % check_every == 0);
@@ -2869,12 +2877,14 @@ int ocn_ctx_synchronize(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
-    if (c->open && c->deferred) {   // a deferred step runs now (its check_ssh_err count is looked at)
+    if (c->open && c->deferred) {   // deferred steps run now (their check_ssh_err counts are looked at)
         StepKind k{};
-        k.check = c->deferred_check;
+        k.check = c->deferred_check[0];
         k.flip = k.one = k.next_one = k.a_done = true;
+        k.pair = c->deferred == 2;   // (a pair only where pairs ran: pair_ok held when they were deferred)
+        k.check2 = k.pair && c->deferred_check[1];
+        c->open_pair = k.pair;
         c->deferred = 0;
-        c->open_pair = false;
         if (const int rc = run_step(c, c->open_tau, k)) { c->open = false; return finish_call(c, rc); }
     }
     HIPCHK(hipStreamSynchronize(c->stream));

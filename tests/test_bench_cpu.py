@@ -103,12 +103,12 @@ def test_hr_variant_bytes():
 @pytest.mark.parametrize("calls", [[1], [2], [3], [4], [100], [1] * 100, [1] * 7])
 def test_pair_region_launches(calls):
     """Two one-pass steps per launch in an open sequence (OCN_OPT_PAIR, ocn_ctx.hip step_impl):
-    every two steps one launch across calls; then the tail -- after a pair its first step again,
-    an odd step left over runs as the last; a pair moves one step's bytes plus the mask byte again."""
+    pairs across calls while 3 or more steps are pending; the last 1 or 2 are run by the tail (a
+    single and the last step, or the last step) -- no step runs twice."""
     steps = sum(calls)
     one = bench.region_launches(calls, flip=True, one=True, zero=True, lazy=True, pair=True)
     kinds = [k for _, k in one]
-    p = steps // 2
+    p = (steps - 1) // 2
     assert kinds[:p] == ["onepass2_z"] * p
     tail = ["onepass_last_z", "copy3", "c2_full"]
     assert kinds[p:] == (tail if steps % 2 else ["onepass_z"] + tail)

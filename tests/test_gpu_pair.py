@@ -5,8 +5,8 @@ second step written where a single step writes -- bitwise against the reference 
 A pair needs the known-constant verdict on the host: a synchronising call hands it over (and, without
 one, its copy in pinned memory once its event has completed), so the runs below make a first short
 call, a synchronize(), then the rest -- the lazy tail keeps the one-pass sequence open across calls,
-every two steps run as one launch and an odd one waits for the next call (a synchronize() runs it
-alone, a read of the fields as the last step).  Tolerance: none (fp64, the reference's order).
+a call runs two steps per launch while 3 or more are pending and leaves the last 1 or 2 to the next
+call (a synchronize() runs them, a read of the fields runs them as the last steps).  Tolerance: none (fp64, the reference's order).
 """
 import pytest
 
@@ -58,12 +58,13 @@ def test_pair_steps_match_reference(amd, name, pattern, graph):
         m.close()
     assert not bad, f"{name} ({pattern}, graph {graph}): fields differ from the reference: {bad}"
     assert one
-    # after the verdict every two steps run as one launch, an odd step waiting for the next call's
-    # first (a call with a step deferred from the last one and n new ones takes d + n)
+    # after the verdict a call runs pairs while 3 or more steps are pending (the 1 or 2 it defers
+    # from the last call first) and defers the last 1 or 2
     calls, want, d = _splits(case["steps"], pattern), [], 0
     for i, n in enumerate(calls):
-        want.append(i > 0 and d + n >= 2)
-        d = (d + n) % 2 if i > 0 else 0
+        t = d + n
+        want.append(i > 0 and t >= 3)
+        d = (t - 2 * ((t - 1) // 2)) if i > 0 else 0
     assert used == want, (used, want, calls)
 
 
