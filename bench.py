@@ -61,6 +61,8 @@ LAUNCH_BYTES = {
     # two one-pass steps in one launch (OCN_OPT_PAIR): one step's reads and writes, the mask byte
     # read by both wave roles (+ h_r by both in the _h variant) -- per launch, i.e. per two steps
     "onepass2_z": (98, 98), "onepass2_h": (114, 114),
+    # general variant: h_r, mu and the forcing read by both roles (the consumers' state from LDS)
+    "onepass2": (162, 162),
     "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
     # tracer runs: CA also stores hh_init's hhq_p (read by tran_diff_tracer); per tracer and step:
     # tran_diff_fluxes (lcu, lcv, hhu, hhv, ff, ffp, ubrtr, vbrtr, mu in; flux_x, flux_y out),
@@ -353,7 +355,8 @@ def main():
                     help="a non-uniform rest depth (a synthetic smooth basin, 20..180 m) instead of 100 m everywhere: "
                          "the one-pass steps read h_r (what a real-depth basin runs)")
     ap.add_argument("--pair", type=int, default=1, choices=[0, 1, 2],
-                    help="two one-pass steps per launch (OCN_OPT_PAIR): 1 = on blocks >= 512^2 (default), 2 = always, 0 = never")
+                    help="two one-pass steps per launch (OCN_OPT_PAIR): 1 = known-constant variants on blocks >= 512^2 "
+                         "(default), 2 = always (the general variant too), 0 = never")
     ap.add_argument("--no-batch", action="store_true",
                     help="several blocks on a GPU: one launch per block and launch group (no block batching)")
     ap.add_argument("--blocks", default=None,

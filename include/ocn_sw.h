@@ -364,10 +364,11 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_BATCH (default 1): with several blocks on the device, each launch group of a step is
  *  issued once for all of them (the blocks' tiles in one grid) instead of once per block.
  *  OCN_OPT_PAIR (default 1): two one-pass steps in one launch where both are plain one-pass steps
- *  of a single-block context without exchanges, the known-constant variant has been selected by a
- *  verdict the host read, and the second is not the call's last step run -- the first step's new
- *  state stays on chip (97 B per cell for two steps); 1: on blocks of at least 512 x 512 interior
- *  points, 2: on any block, 0: never.  Same results bit for bit.  ocn_ctx_get_option: 2 if the last
+ *  of a single-block context without exchanges, the one-pass variant is chosen on the host (a
+ *  known-constant verdict the host read, or the general variant), and the second is not the call's
+ *  last step run -- the first step's new state stays on chip (98 B per cell for two steps in the
+ *  known-constant variant); 1: the known-constant variants on blocks of at least 512 x 512 interior
+ *  points, 2: any variant on any block, 0: never.  Same results bit for bit.  ocn_ctx_get_option: 2 if the last
  *  ocn_ctx_step ran such launches, else whether the option is on.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE

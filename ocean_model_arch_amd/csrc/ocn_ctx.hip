@@ -1784,7 +1784,8 @@ static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
 }
 
 // one_step_pair possible in this call: one block without exchanges or ring work, the compact tables
-// and the march, the known-constant variant chosen by the host (kc_mode), OCN_OPT_PAIR
+// and the march, the one-pass variant chosen by the host (kc_mode not OCN_KC_DEVICE; OCN_OPT_PAIR 1:
+// a known-constant one on blocks of 512^2 or more, 2: any)
 #ifndef OCN_PAIR_MIN_CELLS
 #define OCN_PAIR_MIN_CELLS (512L * 512L)
 #endif
@@ -1792,9 +1793,13 @@ static bool pair_ok(ocn_ctx *c)
 {
     if (!c->pair || c->blocks.size() != 1 || has_exchange(c) || has_comm(c) || c->ring_sea || !c->compact || !c->march)
         return false;
-    if (c->kc_mode != OCN_KC_KNOWN && c->kc_mode != OCN_KC_KNOWN_HR) return false;
+    if (c->kc_mode == OCN_KC_DEVICE) return false;   // (the variant the launches run is chosen on the device)
+    if (c->pair >= 2) return true;
+    // the default: the known-constant variants only -- the general variant's pair is VALU bound at
+    // twice its single launch (4096^2: 1.09 vs 0.54 ms), no faster
+    if (c->kc_mode == OCN_KC_GENERAL) return false;
     const ocn_block &g = c->blocks[0].g;
-    return c->pair >= 2 || (long)(g.nx_end - g.nx_start + 1) * (g.ny_end - g.ny_start + 1) >= OCN_PAIR_MIN_CELLS;
+    return (long)(g.nx_end - g.nx_start + 1) * (g.ny_end - g.ny_start + 1) >= OCN_PAIR_MIN_CELLS;
 }
 
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)

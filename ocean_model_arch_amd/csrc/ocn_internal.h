@@ -135,8 +135,7 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
                    const Range *range, bool last, const OnepassKC &kc, unsigned own = 0,
                    const Range *frame_of = nullptr);
 // Two one-pass steps in one launch (sw_kernels.hip MarchStep PAIR): single block, no exchange,
-// the known-constant variants only (kc.mode OCN_KC_KNOWN / OCN_KC_KNOWN_HR, a verdict the host has
-// read); reads the state where a single step reads it and writes the second step's new state where
+// a variant chosen on the host (kc.mode OCN_KC_KNOWN / OCN_KC_KNOWN_HR / OCN_KC_GENERAL); reads the state where a single step reads it and writes the second step's new state where
 // a single step writes (one role flip); nbad1 / nbad2: the steps' check_ssh_err counts (null: none)
 int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                         double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,

@@ -1873,14 +1873,20 @@ struct StepRegs {
         default: return 0.0;
         }
     }
+    // table row of row n + dy, clamped into the table (PAIR producers: their rows reach 2 past the
+    // block's; what they compute there is not used)
+    __device__ __forceinline__ unsigned row(int dy) const
+    {
+        return min((unsigned)__builtin_amdgcn_readfirstlane(rn + dy), (unsigned)nrows - 1u);
+    }
     __device__ __forceinline__ float met(int id, int dy) const
     {
-        return rows[(unsigned)(id - OCN_DX) * nrows + __builtin_amdgcn_readfirstlane(rn + dy)];
+        return rows[(unsigned)(id - OCN_DX) * nrows + row(dy)];
     }
     // 1 / (double)g of row n + dy for the divisor OCN_RC_* k (wave-uniform scalar load)
     __device__ __forceinline__ double rc(int k, int dy) const
     {
-        return rcp[(unsigned)k * nrows + __builtin_amdgcn_readfirstlane(rn + dy)];
+        return rcp[(unsigned)k * nrows + row(dy)];
     }
     // the rotating form (every iteration in phase 0): rows n-1 .. n+2 move down one slot
     __device__ __forceinline__ void rotate()
@@ -1923,7 +1929,7 @@ struct StepRegs {
 // exchanges of D deliver -- and the march covers the whole interior.
 template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR = false, bool PAIR = false>
 struct MarchStep {
-    static_assert(!PAIR || (ZF && !LAST && !X2), "two-step launches: the known-constant variant, no last step, no x2");
+    static_assert(!PAIR || (!LAST && !X2), "two-step launches: no last step, no x2");
     static constexpr bool kPair = PAIR;
     static constexpr int kPairCols = 116;   // PAIR: a workgroup's output columns (2 x 60 produced, less 2 each side)
     static constexpr bool kAligned = false;
@@ -1965,10 +1971,16 @@ struct MarchStep {
             q.ssh = g_pair[(n + 2) & 3][0][x.pj]; q.shp = g_pair[(n + 2) & 3][1][x.pj];
             q.u = g_pair[(n + 2) & 3][2][x.pj]; q.up = g_pair[(n + 2) & 3][3][x.pj];
             q.v = g_pair[(n + 1) & 3][4][x.pj]; q.vp = g_pair[(n + 1) & 3][5][x.pj];
-            q.hr = !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c2);
+            q.hr = ZF && !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c2);
             q.bits = ld(t.bits, c2);
-            q.mu = x.mu0;
-            q.rhsx = q.rhsy = 0.0;
+            if (ZF) {
+                q.mu = x.mu0;
+                q.rhsx = q.rhsy = 0.0;
+            } else {   // (the general variant: mu and the forcing read as a single step reads them)
+                q.mu = ld(t.f(OCN_MU), I(m, n + 1));
+                q.rhsx = ld(t.f(OCN_RHSX), I(m, n));
+                q.rhsy = ld(t.f(OCN_RHSY), I(m, n));
+            }
             return;
         }
 #endif
@@ -2024,9 +2036,10 @@ struct MarchStep {
         bool llu, llv, luh, vt, st, ss;   // the computed value is used
         double hu, hv, hh, hu1, hv1, vort, stt, sts;
     };
-    template <int PH> __device__ __forceinline__ void fallback(const StepRegs &x, Fallback &f, int m, int r, int slot) const
+    template <int PH, int RO = 0>
+    __device__ __forceinline__ void fallback(const StepRegs &x, Fallback &f, int m, int r, int slot) const
     {
-        const Pt c = geo(&b)(m, r);
+        const Pt c = geo(&b)(m, rowc(r, RO));   // (PAIR producers: their rows reach past the arrays)
         const unsigned bc = x.bits.s<PH>(slot);
         bool hh_rng = m >= b.nx_start - 1 && m <= b.nx_end && r >= b.ny_start - 1 && r <= b.ny_end;
         bool in = m >= b.nx_start && m <= b.nx_end && r >= b.ny_start && r <= b.ny_end;
@@ -2554,7 +2567,7 @@ struct MarchStep {
             weights<0>(x, 1);
         }
         Fallback fb;
-        fallback<0>(x, fb, L.m, n0 + 1, 2);
+        fallback<0, RO>(x, fb, L.m, n0 + 1, 2);
 #if OCN_STEP_ONEBLOCK && OCN_STEP_PF2 && OCN_STEP_BUFST
         if constexpr (kUnroll && RO == 0) {   // two batches in flight: iteration n takes qs[n - n0 & 1], loaded at n - 2
             Batch qs[2];
@@ -2645,7 +2658,7 @@ struct MarchStep {
         }
         take<PH>(x, q);
         Fallback fbn;
-        if (n < ne) fallback<PH>(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
+        if (n < ne) fallback<PH, RO>(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
         if (n + kAhead - 1 < ne) load<RO>(x, q, L.m, n + kAhead);   // in flight while this row (and the next) is computed
         Out o;
 #if OCN_DIAG_NOCHK
@@ -3062,8 +3075,8 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
         !up_out || !vp_out)
         return set_error(OCN_ERR_ARG, "two-step launch: compact tables, march, full_free_surface = 1, trans_terms and "
                                       "ksw_lat on, three second buffers");
-    if ((kc.mode != OCN_KC_KNOWN && kc.mode != OCN_KC_KNOWN_HR) || !kc.kc)
-        return set_error(OCN_ERR_ARG, "two-step launch: a known-constant verdict");
+    if (kc.mode == OCN_KC_DEVICE || (kc.mode != OCN_KC_GENERAL && !kc.kc))
+        return set_error(OCN_ERR_ARG, "two-step launch: a variant chosen on the host");
     RC_K(check_block(b));
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
     const Range r = range_interior(b);
@@ -3078,12 +3091,13 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
     g.ntiles = g.r[0].tiles;
     int ex;
     const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
-#define OCN_PAIR_LAUNCH(P, H)                                                                                    \
-    return issue_march(g, MarchStep<P, false, true, false, H, true>{*b, t, sw, tau, nbad1, sshp_out, up_out, vp_out, \
-                                                                    kc.kc, nullptr, 0, 0u, nbad2}, s)
-    if (kc.mode == OCN_KC_KNOWN_HR) { if (p2) OCN_PAIR_LAUNCH(true, true); OCN_PAIR_LAUNCH(false, true); }
-    if (p2) OCN_PAIR_LAUNCH(true, false);
-    OCN_PAIR_LAUNCH(false, false);
+#define OCN_PAIR_LAUNCH(P, Z, H)                                                                                 \
+    return issue_march(g, MarchStep<P, false, Z, false, H, true>{*b, t, sw, tau, nbad1, sshp_out, up_out, vp_out,    \
+                                                                 kc.kc, nullptr, 0, 0u, nbad2}, s)
+    if (kc.mode == OCN_KC_GENERAL) { if (p2) OCN_PAIR_LAUNCH(true, false, false); OCN_PAIR_LAUNCH(false, false, false); }
+    if (kc.mode == OCN_KC_KNOWN_HR) { if (p2) OCN_PAIR_LAUNCH(true, true, true); OCN_PAIR_LAUNCH(false, true, true); }
+    if (p2) OCN_PAIR_LAUNCH(true, true, false);
+    OCN_PAIR_LAUNCH(false, true, false);
 #undef OCN_PAIR_LAUNCH
 #else
     (void)b; (void)ptr; (void)nptr; (void)cp; (void)sw; (void)tau; (void)nbad1; (void)nbad2; (void)sshp_out;

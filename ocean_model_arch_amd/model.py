@@ -225,9 +225,9 @@ class OceanModel:
         return self
 
     def set_pair(self, mode: int = 1):
-        """Two one-pass steps per launch (default 1: on single blocks of at least 512 x 512 interior
-        points; 2: any block; 0: never): the first step's new state stays on chip; same results bit
-        for bit."""
+        """Two one-pass steps per launch (default 1: the known-constant variants on single blocks of
+        at least 512 x 512 interior points; 2: any variant, any block; 0: never): the first step's
+        new state stays on chip; same results bit for bit."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_PAIR, int(mode)), "ocn_ctx_set_option")
         return self
 

@@ -2,7 +2,7 @@
 steps per launch on one block -- the producer waves' first step kept in LDS, the consumer waves'
 second step written where a single step writes -- bitwise against the reference fixtures.
 
-A pair needs the known-constant verdict on the host: a synchronising call hands it over (and, without
+A pair needs the variant chosen on the host -- the known-constant verdict: a synchronising call hands it over (and, without
 one, its copy in pinned memory once its event has completed), so the runs below make a first short
 call, a synchronize(), then the rest -- the lazy tail keeps the one-pass sequence open across calls,
 a call runs two steps per launch while 3 or more are pending and leaves the last 1 or 2 to the next
@@ -66,6 +66,52 @@ def test_pair_steps_match_reference(amd, name, pattern, graph):
         want.append(i > 0 and t >= 3)
         d = (t - 2 * ((t - 1) // 2)) if i > 0 else 0
     assert used == want, (used, want, calls)
+
+
+@pytest.mark.parametrize("pattern", ["whole", "1,odd,even"])
+@pytest.mark.parametrize("name", ["box70x54_b1x1_s20", "bs_b1x1_s60", "box70x54_topo_b1x1_s20", "box1024_b1x1_s10",
+                                  "box1521x1111_b1x1_s604"])
+def test_pair_general_variant(amd, name, pattern):
+    """Pairs of the general one-pass variant (known constants off: h_r, mu and the forcing read by
+    both roles, D's fallback values from memory): no verdict to wait for, so pairs from the first
+    call -- bitwise."""
+    case = cases.load_e2e(name)
+    calls = [case["steps"]] if pattern == "whole" else _splits(case["steps"], pattern)
+    m = build_model(amd, case).set_known_constants(False).set_pair(2).init()
+    used = []
+    try:
+        for n in calls:
+            m.step(n, tau=1.0, check_every=1)
+            used.append(m.pair_active)
+        m.synchronize()
+        bad = compare_case(m, case, name)
+        one, zero = m.onepass_active, m.onepass_zero
+    finally:
+        m.close()
+    assert not bad, f"{name} ({pattern}, general variant): fields differ from the reference: {bad}"
+    assert one and not zero
+    # as after the verdict, from the first call on (a first call of 1 step runs it: the sequence's
+    # first step is not a plain one-pass step)
+    want, d = [], 0
+    for i, n in enumerate(calls):
+        t = d + n
+        want.append(t >= 3)
+        d = 0 if i == 0 and n == 1 else t - 2 * ((t - 1) // 2)
+    assert used == want, (used, want, calls)
+
+
+def test_pair_default_skips_general_variant(amd):
+    """OCN_OPT_PAIR 1 (the default) leaves the general variant's steps single (its pair is no
+    faster: VALU bound) -- bitwise either way."""
+    case = cases.load_e2e("box1024_b1x1_s10")
+    m = build_model(amd, case).set_known_constants(False).init()
+    try:
+        m.step(case["steps"], tau=1.0, check_every=1).synchronize()
+        used, one = m.pair_active, m.onepass_active
+        bad = compare_case(m, case, "box1024_b1x1_s10")
+    finally:
+        m.close()
+    assert not bad and one and not used, (bad, one, used)
 
 
 @pytest.mark.parametrize("name", ["box70x54_b1x1_s20", "box1024_b1x1_s10"])
