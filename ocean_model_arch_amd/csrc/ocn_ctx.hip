@@ -1765,7 +1765,8 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
 // Two one-pass steps as one launch per block (sw_kernels.hip MarchStep PAIR): the first step's new
 // state stays in LDS, the second's is written where a single step writes -- so the pair is one role
 // flip of the pairs and of the second buffers, as a single one-pass step is.  Single block, no
-// exchange, a known-constant verdict the host has read (pair_ok); 97 B per cell for two steps.
+// exchange, a variant chosen on the host (pair_ok); 98 B per cell for two steps in the known-constant
+// variant, 162 in the general one.
 static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
 {
     ocn_ctx::Rec rec;

@@ -2493,7 +2493,7 @@ struct MarchStep {
     }
 #endif
 
-    // PAIR (two steps in one launch, single block, known constants): the producer waves march the
+    // PAIR (two steps in one launch, single block, a variant chosen on the host): the producer waves march the
     // first step over the workgroup's rows +- 2 and put its new state into the LDS ring, the
     // consumer waves march the second step over the workgroup's rows from there, 6 iterations
     // behind (an iteration's ring reads are rows the producers finished before the last barrier);
