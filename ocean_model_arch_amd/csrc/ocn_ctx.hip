@@ -272,6 +272,7 @@ struct ocn_ctx {
     int overlap = -1;            // OCN_OPT_OVERLAP: 0 none, 1 standard steps, 2 + role-flip steps, -1 auto
     int32_t *d_nbad = nullptr;
     ncclComm_t comm = nullptr;
+    bool comm_aborted = false;         // fail_fatal aborted the communicator: calls with exchanges fail
     Loopback *lb = nullptr;            // test transport between contexts of one process (ocn_ctx_attach_loopback)
     hipEvent_t lb_ev_a = nullptr, lb_ev_b = nullptr;
     std::map<std::vector<int>, HaloPlan> plans;
@@ -591,7 +592,8 @@ static int allocate(ocn_ctx *c)
         RC(allocate_x2(c, b));
     }
     // d_nbad words: 0 check_ssh_err's count, 16 the fallback check's verdict (d_fbz), 32..47 flags and
-    // the vote (d_flags), 48..63 the loopback vote's reduction; then per block h_r, mu (LBlock::kc)
+    // the vote (d_flags), 48..55 the loopback vote's reduction, 56 the count's maximum over the ranks
+    // (sync_impl); then per block h_r, mu (LBlock::kc)
     const size_t kcb = 16 * c->blocks.size();
     HIPCHK(hipMalloc(&c->d_nbad, 256 + kcb));
     c->allocs.push_back(c->d_nbad);
@@ -783,7 +785,11 @@ static int nccl_rc(ncclResult_t r, const char *what)
     return set_error(OCN_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-static bool has_comm(const ocn_ctx *c) { return c->comm || c->lb; }
+static bool has_comm(const ocn_ctx *c) { return c->comm || c->lb || c->comm_aborted; }
+static int comm_gone(const ocn_ctx *c)
+{
+    return set_error(OCN_ERR_COMM, "the RCCL communicator was aborted after an earlier fatal error");
+}
 // OCN_OPT_OVERLAP in effect: by default (-1) the role-flip steps' exchanges overlap their inner
 // launches (2) when exchanges go to other ranks (RCCL: latency, not copy bandwidth), and run
 // between the launches (1) when every exchange is a local device copy -- there the frame bands
@@ -800,6 +806,23 @@ static int lb_fail_on_error(ocn_ctx *c, int rc)
         std::lock_guard<std::mutex> g(c->lb->mu);
         c->lb->failed = true;
         c->lb->cv.notify_all();
+    }
+    return rc;
+}
+
+// An error inside a call that takes part in collectives (step, init_state, synchronize): the
+// loopback group's waits are released (lb_fail_on_error), and a fatal one (HIP, RCCL, state) aborts
+// the RCCL communicator -- its queued sends / receives are cancelled and nothing of this rank waits
+// on a peer that will not come; the host then ends the job, as abort_model's mpi_abort does
+// (shared/errors.f90:30-37).  OCN_ERR_BLOWUP is not fatal here: every rank returns it from the same
+// synchronize (sync_impl reduces the counts), and OCN_ERR_ARG is raised before any collective.
+static int fail_fatal(ocn_ctx *c, int rc)
+{
+    rc = lb_fail_on_error(c, rc);
+    if (rc && rc != OCN_ERR_BLOWUP && rc != OCN_ERR_ARG && c->comm) {
+        (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+        c->comm_aborted = true;
     }
     return rc;
 }
@@ -889,6 +912,7 @@ __global__ void k_vote_max(VotePtrs v, int32_t *out)
 constexpr int kVoteWords = 8;   // the role-flip vote (check_coherence): one 0/1 word per condition
 static int allreduce_max(ocn_ctx *c, int32_t *word, hipStream_t s, int words = 1)
 {
+    if (c->comm_aborted) return comm_gone(c);
     if (c->comm)
         return nccl_rc(ncclAllReduce(word, word, (size_t)words, ncclInt32, ncclMax, c->comm, s), "ncclAllReduce");
     if (!c->lb) return OCN_OK;
@@ -942,6 +966,7 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
     if (!stream) stream = c->stream;
     if (!p->peers.empty()) {
         if (!has_comm(c)) return set_error(OCN_ERR_COMM, "remote neighbours but no RCCL communicator attached");
+        if (c->comm_aborted) return comm_gone(c);
         hipLaunchKernelGGL(k_segments, dim3(p->n_pack, p->ch_pack), dim3(kSegChunk), 0, stream, p->d_pack, p->n_pack);
         RC(check_launch());
         if (c->lb) {
@@ -1231,11 +1256,15 @@ static int prepare_static(ocn_ctx *c)
 //   join | C1.frame | C2.frame | fork: sync C2 || C2.inner | join
 // Every halo write of an exchange lands on points the concurrent inner launches neither read
 // nor write, and every value it sends was produced by the frame launch before the fork.
-static bool has_exchange(ocn_ctx *c)
+// Whether any exchange has strips: some local block has a neighbour block (local or on another
+// rank) in one of the 8 directions -- exactly when plan_entries enumerates an entry.  Decided from
+// the decomposition alone (no plan is built, so nothing can fail inside a graph capture).
+static bool has_exchange(const ocn_ctx *c)
 {
-    HaloPlan *p = nullptr;
-    if (get_plan(c, c->sync_a, p) || !p) return false;
-    return p->n_local > 0 || !p->peers.empty();
+    for (const LBlock &b : c->blocks)
+        for (int d = 0; d < 8; ++d)
+            if (b.nbr_rank[d] >= 0) return true;
+    return false;
 }
 
 // An exchange forked onto the comm stream stays pending until join_sync (a no-op without one);
@@ -2392,7 +2421,9 @@ int ocn_ctx_attach_comm(ocn_ctx *c, const void *unique_id, int32_t nbytes)
     HIPCHK(hipSetDevice(c->dec.device));
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
+    if (c->comm) return set_error(OCN_ERR_STATE, "a communicator is attached already");
     RC(nccl_rc(ncclCommInitRank(&c->comm, c->dec.nranks, id, c->dec.rank), "ncclCommInitRank"));
+    c->comm_aborted = false;
     return OCN_OK;
 }
 
@@ -2442,10 +2473,11 @@ int ocn_ctx_init_state(ocn_ctx *c)
     c->open = false;   // a pending call tail is void: every field is formed again
     c->open_pair = false;
     c->deferred = 0;
+    c->ring2_saved = false;   // (a saved second ring of an x2 sequence is void: init forms it again)
     c->coherent_known = false;
     c->alt_ok = false;
     c->fb_state = kFbUnchecked;
-    const int rc = lb_fail_on_error(c, init_state(c));
+    const int rc = fail_fatal(c, init_state(c));
     c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // init_data.f90:60-63 ran hh_init last
     return rc;
 }
@@ -2618,6 +2650,9 @@ static int prepare_kc(ocn_ctx *c, bool x2 = false)
 static int finish_call(ocn_ctx *c, int rc)
 {
     if (const int rj = join_sync(c); rc == OCN_OK) rc = rj;
+    // a failed call drops its sequence: a saved second halo ring (x2 steps) must not be restored
+    // over what the host uploads or init_state forms next
+    if (rc != OCN_OK) c->ring2_saved = false;
     if (c->role & 1) swap_roles(c);
     if (c->role & 2) {   // sshp's buffers are not equal: the current one is copied into the field's own buffer
         for (LBlock &b : c->blocks)
@@ -2639,7 +2674,7 @@ static int finish_call(ocn_ctx *c, int rc)
 static bool lazy_allowed(const ocn_ctx *c, bool x2)
 {
     return c->lazy && !has_comm(c) && !c->r8_handed && c->sw.use_tracers <= 0 &&
-           (x2 || (!c->ring_sea && !has_exchange(const_cast<ocn_ctx *>(c))));
+           (x2 || (!c->ring_sea && !has_exchange(c)));
 }
 
 // one_step_x2's static conditions on this rank (the device checks come from check_coherence):
@@ -2647,7 +2682,7 @@ static bool lazy_allowed(const ocn_ctx *c, bool x2)
 // fills, every block of the grid at least 2 x 2 (its 2-deep strips lie in its interior)
 static bool x2_local(const ocn_ctx *c)
 {
-    if (!c->x2 || !c->compact || !c->rows_x_ok || c->edge_ring_sea || !has_exchange(const_cast<ocn_ctx *>(c)))
+    if (!c->x2 || !c->compact || !c->rows_x_ok || c->edge_ring_sea || !has_exchange(c))
         return false;
     for (const GBlock &g : c->gblocks)
         if (g.rank >= 0 && (g.g.nx_end - g.g.nx_start < 1 || g.g.ny_end - g.g.ny_start < 1)) return false;
@@ -2870,7 +2905,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
 int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
-    return lb_fail_on_error(c, step_impl(c, tau, nsteps, check_every));
+    return fail_fatal(c, step_impl(c, tau, nsteps, check_every));
 }
 
 int ocn_ctx_complete(ocn_ctx *c)
@@ -2879,32 +2914,59 @@ int ocn_ctx_complete(ocn_ctx *c)
     return complete_open(c);
 }
 
-int ocn_ctx_synchronize(ocn_ctx *c)
+// The steps an open sequence deferred (ocn_ctx_step leaves up to two requested steps not yet
+// enqueued while pairs run), run now -- by the calls that look at what the steps did (their
+// check_ssh_err counts, their launch times): as a pair or alone, the tail stays pending.
+static int run_deferred(ocn_ctx *c)
 {
-    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    if (!c->open || !c->deferred) return OCN_OK;
+    StepKind k{};
+    k.check = c->deferred_check[0];
+    k.flip = k.one = k.next_one = k.a_done = true;
+    k.pair = c->deferred == 2;   // (a pair only where pairs ran: pair_ok held when they were deferred)
+    k.check2 = k.pair && c->deferred_check[1];
+    c->open_pair = k.pair;
+    c->deferred = 0;
+    if (const int rc = run_step(c, c->open_tau, k)) { c->open = false; return finish_call(c, rc); }
+    return OCN_OK;
+}
+
+// check_ssh_err_kernel's verdict (vel_ssh.f90:40-67): abort_model -> mpi_abort on the cart
+// communicator (shared/errors.f90:30-37) stops every rank together, so with ranks the counts are
+// max-reduced (one int32: ncclAllReduce, or the loopback vote) and every rank returns
+// OCN_ERR_BLOWUP from the same synchronize.
+static int sync_impl(ocn_ctx *c)
+{
     HIPCHK(hipSetDevice(c->dec.device));
-    if (c->open && c->deferred) {   // deferred steps run now (their check_ssh_err counts are looked at)
-        StepKind k{};
-        k.check = c->deferred_check[0];
-        k.flip = k.one = k.next_one = k.a_done = true;
-        k.pair = c->deferred == 2;   // (a pair only where pairs ran: pair_ok held when they were deferred)
-        k.check2 = k.pair && c->deferred_check[1];
-        c->open_pair = k.pair;
-        c->deferred = 0;
-        if (const int rc = run_step(c, c->open_tau, k)) { c->open = false; return finish_call(c, rc); }
+    RC(run_deferred(c));
+    int32_t *cnt = c->d_nbad;
+    if (has_comm(c)) {   // every rank's synchronize takes part (the collective of the check)
+        cnt = c->d_nbad + 56;
+        HIPCHK(hipMemcpyAsync(cnt, c->d_nbad, sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+        RC(allreduce_max(c, cnt, c->stream));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     learn_fb(c);
     int32_t nbad = 0;
-    HIPCHK(hipMemcpy(&nbad, c->d_nbad, sizeof(nbad), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&nbad, cnt, sizeof(nbad), hipMemcpyDeviceToHost));
     if (nbad) return set_error(OCN_ERR_BLOWUP, "SIGFPRE predict error: |ssh| >= 1e4 on " + std::to_string(nbad) +
-                                                   " sea points (check_ssh_err_kernel)");
+                                                   (has_comm(c) ? " sea points of a block (the most of any rank;"
+                                                                  " check_ssh_err_kernel)"
+                                                                : " sea points (check_ssh_err_kernel)"));
     return OCN_OK;
+}
+
+int ocn_ctx_synchronize(ocn_ctx *c)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return fail_fatal(c, sync_impl(c));
 }
 
 int ocn_ctx_stage_times(ocn_ctx *c, double *ms, int64_t *counts)
 {
     if (!c || !ms || !counts) return set_error(OCN_ERR_ARG, "null argument");
+    HIPCHK(hipSetDevice(c->dec.device));
+    RC(run_deferred(c));   // (their launches belong to this report, not the next one)
     HIPCHK(hipStreamSynchronize(c->stream));
     learn_fb(c);
     for (auto &r : c->recs) {

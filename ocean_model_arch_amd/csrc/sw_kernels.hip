@@ -3054,8 +3054,13 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 static int pair_rows(const Range &r, int cols)
 {
     const long wx = (r.m1 - r.m0 + cols) / cols, h = r.n1 - r.n0 + 1;
-    if (const char *e = getenv("OCN_PAIR_ROWS"))   // (a tuning override: a fixed tile height)
-        if (const int v = atoi(e); v >= 8 && v <= OCN_PAIR_MAX_ROWS) return v;
+    // a tuning override (a fixed tile height), read once per process -- not a libc call per launch
+    static const int fixed = [] {
+        const char *e = getenv("OCN_PAIR_ROWS");
+        const int v = e ? atoi(e) : 0;
+        return v >= 8 && v <= OCN_PAIR_MAX_ROWS ? v : 0;
+    }();
+    if (fixed) return fixed;
     int best = 8;
     long cost = -1;
     for (int rows = 8; rows <= OCN_PAIR_MAX_ROWS; ++rows) {

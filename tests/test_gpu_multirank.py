@@ -198,6 +198,42 @@ def test_ranks_upload_on_one_rank_votes_together(amd):
     assert not bad, bad
 
 
+def test_ranks_blowup_stops_every_rank(amd):
+    """check_ssh_err_kernel on one rank (vel_ssh.f90:52-66 abort_model -> mpi_abort on the cart
+    communicator, shared/errors.f90:16-37): |ssh| >= 1e4 on one sea point of one block of 8 ranks --
+    every rank raises OcnError (OCN_ERR_BLOWUP) from the same synchronize (the counts are reduced
+    over the ranks), and no rank waits for a peer (no 120 s rendezvous timeout)."""
+    import time
+    n, nranks, hot = 128, 8, 5
+    par = amd.ParallelConfig(4, 2)
+    models = [amd.OceanModel(amd.box_config(n), par=par, rank=r, nranks=nranks) for r in range(nranks)]
+    amd.OceanModel.attach_loopback(models)
+
+    def body(m):
+        m.init().step(2).synchronize()
+        if m.rank == hot:
+            k = m.blocks[0].k
+            s = m.download(k, "ssh")
+            s[s.shape[0] // 2, s.shape[1] // 2] = 2.0e4
+            for nm in ("ssh", "sshn", "sshp"):
+                m.upload(k, nm, s)
+        t0 = time.perf_counter()
+        try:
+            m.step(3, check_every=1).synchronize()
+        except amd.OcnError as e:
+            return ("raised", str(e), time.perf_counter() - t0)
+        return ("ok", "", time.perf_counter() - t0)
+
+    try:
+        res = amd.run_ranks(models, body)
+    finally:
+        for m in models:
+            m.close()
+    assert [r[0] for r in res] == ["raised"] * nranks, res
+    assert all("1e4" in r[1] for r in res), res
+    assert max(r[2] for r in res) < 60.0, res
+
+
 # ---------------------------------------------------------------- BASELINE.json configs, full size
 def _full(amd, name, **opts):
     case = cases.load_e2e(name)

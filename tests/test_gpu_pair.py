@@ -11,7 +11,7 @@ call (a synchronize() runs them, a read of the fields runs them as the last step
 import pytest
 
 from tests.golden import cases
-from tests.test_gpu_parity import build_model, compare_case
+from tests.test_gpu_parity import OracleTwin, build_model, compare_case
 
 pytestmark = pytest.mark.gpu
 
@@ -98,6 +98,41 @@ def test_pair_general_variant(amd, name, pattern):
         want.append(t >= 3)
         d = 0 if i == 0 and n == 1 else t - 2 * ((t - 1) // 2)
     assert used == want, (used, want, calls)
+
+
+@pytest.mark.parametrize("forcing", ["RHSx", "RHSy"])
+def test_pair_general_variant_with_forcing(amd, forcing):
+    """Pairs of the general variant with a wind forcing on the sea (RHSx / RHSy read by both roles:
+    sw_update_uv, vel_ssh.f90:108-195) and a nonuniform mu (uv_diff2, vel_ssh.f90:375-452): bitwise
+    against the oracle given the same uploads, the steps split across calls."""
+    import numpy as np
+    n = 600
+    m = amd.OceanModel(amd.box_config(n)).set_known_constants(False).set_pair(2).init()
+    ref = OracleTwin(n)
+    b = m.blocks[0]
+    lu = m.download(0, "lu")
+    a = np.zeros(b.shape)
+    a[lu > 0.5] = 2e-7 if forcing == "RHSx" else -3e-7
+    a[200:260, 100:180] *= 4.0
+    m.upload(0, forcing, a)
+    ref.upload(b, forcing, a)
+    mu = np.full(b.shape, 0.0)
+    mu[150:400, 150:400] = 2.0
+    m.upload(0, "mu", mu)
+    ref.upload(b, "mu", mu)
+    used = []
+    try:
+        for k in (1, 4, 3, 1):
+            m.step(k, tau=1.0, check_every=1)
+            used.append(m.pair_active)
+        m.synchronize()
+        ref.run(9)
+        bad = ref.mismatches(m)
+        one, zero = m.onepass_active, m.onepass_zero
+    finally:
+        m.close()
+    assert not bad, f"general-variant pairs with a {forcing} forcing differ from the oracle: {bad}"
+    assert one and not zero and any(used), (one, zero, used)
 
 
 def test_pair_default_skips_general_variant(amd):
@@ -220,3 +255,13 @@ def test_pair_deferral_matches_single_launches(amd, seq):
     assert used
     bad = [nm for nm in a if a[nm].tobytes() != b[nm].tobytes()]
     assert not bad, f"{seq}: fields differ between pair and single launches: {bad}"
+    # and both against the oracle given the same steps, taus and bumps
+    ref = OracleTwin(600)
+    f = ref.om.f[0]
+    for op in base + more:
+        if op[0] == "step":
+            ref.run(op[1], op[2])
+        elif op[0] == "bump":
+            f[op[1]][300, 280] += 1.0e-3
+    bad = [nm for nm in a if nm in f and a[nm].tobytes(order="F") != f[nm].tobytes(order="F")]
+    assert not bad, f"{seq}: fields differ from the oracle: {bad}"

@@ -30,6 +30,39 @@ def bits_equal(a, b):
         np.ascontiguousarray(a.ravel(order="F")).tobytes() == np.ascontiguousarray(b.ravel(order="F")).tobytes()
 
 
+class OracleTwin:
+    """The CPU oracle (oracle/oracle.py: the reference's algorithm layer over oracle/sw_oracle.c,
+    pinned bit for bit to the compiled reference by tests/test_oracle_pinned.py) run beside a GPU
+    model on the same box and block grid and given the same uploads -- so the parity corners the
+    golden fixtures do not reach (arbitrary uploaded state, a forcing, tau changes, calls split
+    anywhere) are checked against the reference's algorithm, not only between two HIP paths."""
+
+    def __init__(self, n, blocks=(1, 1)):
+        from oracle import oracle as O
+        self.om = O.OracleModel(O.BasinConfig(nx=n + 4, ny=n + 4), O.SWConfig(), *blocks).init()
+
+    def k(self, b):
+        return [i for i, ob in enumerate(self.om.blocks) if (ob.bm, ob.bn) == (b.bm, b.bn)][0]
+
+    def upload(self, b, nm, a):
+        self.om.f[self.k(b)][nm][...] = a
+
+    def run(self, steps, tau=1.0):
+        self.om.run(steps, tau)
+
+    def mismatches(self, m, names=None):
+        """Fields of GPU model m that differ from the oracle's (every field by default)."""
+        bad = []
+        for b in m.blocks:
+            f = self.om.f[self.k(b)]
+            for nm in names or f:
+                if nm in ("lu1", "rlh_c"):
+                    continue
+                if not bits_equal(m.download(b.k, nm), f[nm]):
+                    bad.append(f"({b.bm},{b.bn}):{nm}")
+        return bad
+
+
 @pytest.fixture(scope="module")
 def amd():
     import ocean_model_arch_amd as amd
@@ -510,6 +543,7 @@ def test_onepass_with_nonzero_fallback_values(amd, blocks):
     for onepass in (True, False):
         m = amd.OceanModel(amd.box_config(n), par=amd.ParallelConfig(*blocks)).set_onepass(onepass)
         m.init()
+        ref = OracleTwin(n, blocks)
         for b in m.blocks:
             lu = m.download(b.k, "lu")
             for nm, v in (("hhu", 0.25), ("hhv", 0.5), ("hhh", 0.75), ("vort", 1e-3), ("str_t", 2e-3),
@@ -517,19 +551,19 @@ def test_onepass_with_nonzero_fallback_values(amd, blocks):
                 a = m.download(b.k, nm)
                 a[lu < 0.5] = v            # land and the land halo
                 m.upload(b.k, nm, a)
+                ref.upload(b, nm, a)
             for nm, v in (("RHSx", 2e-7), ("RHSy", -3e-7)):   # a wind forcing on the sea
                 a = m.download(b.k, nm)
                 a[lu > 0.5] = v
                 m.upload(b.k, nm, a)
+                ref.upload(b, nm, a)
         m.step(steps, tau=1.0, check_every=1).synchronize()
         assert m.onepass_active == onepass
-        out[onepass] = [{nm: m.download(x.k, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp",
-                                                            "vbrtr", "vbrtrn", "vbrtrp", "hhu", "hhv", "hhh",
-                                                            "vort", "str_t", "str_s", "RHSx_dif", "RHSy_adv")}
-                        for x in m.blocks]
+        ref.run(steps)
+        out[onepass] = ref.mismatches(m)
         m.close()
-    bad = [(k, nm) for k, d in enumerate(out[True]) for nm, a in d.items() if not bits_equal(a, out[False][k][nm])]
-    assert not bad, f"one-pass with nonzero fallback values differs from the role-flip path: {bad}"
+    assert not out[True], f"one-pass with nonzero fallback values differs from the oracle: {out[True]}"
+    assert not out[False], f"role-flip path with nonzero fallback values differs from the oracle: {out[False]}"
 
 
 @pytest.mark.gpu
@@ -538,18 +572,16 @@ def test_known_constants_option(amd):
     forcing and D's fallback values read from the arrays) -- the same results bit for bit as the
     known-constant variant the check selects by default."""
     n, steps = 130, 9
-    out = {}
+    ref = OracleTwin(n)
+    ref.run(steps)
     for kc in (True, False):
         m = amd.OceanModel(amd.box_config(n)).set_known_constants(kc)
         m.init()
         m.step(steps, tau=1.0, check_every=1).synchronize()
         assert m.onepass_active and m.onepass_zero == kc
-        out[kc] = {nm: m.download(0, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp", "vbrtr",
-                                                   "vbrtrn", "vbrtrp", "hhu", "hhv", "hhh", "vort", "str_t",
-                                                   "str_s", "RHSx_dif", "RHSy_adv")}
+        bad = ref.mismatches(m)
         m.close()
-    bad = [nm for nm, a in out[True].items() if not bits_equal(a, out[False][nm])]
-    assert not bad, f"known-constant and general one-pass variants differ: {bad}"
+        assert not bad, f"one-pass variant (known constants {kc}) differs from the oracle: {bad}"
 
 
 @pytest.mark.parametrize("what", ["forcing", "mu", "h_r"])
@@ -560,27 +592,29 @@ def test_graph_replay_sees_uploads_between_calls(amd, what):
     device check picks the variant, the captured step's key holds the variant mode) -- bitwise as
     the same run on the stream."""
     n = 96
-    out = {}
     for graph in (True, False):
         m = amd.OceanModel(amd.box_config(n)).init()
+        ref = OracleTwin(n)
         m.set_graph(graph)
         m.step(6, check_every=1).synchronize()
+        ref.run(6)
         b = m.blocks[0]
         if what == "forcing":
             a = np.zeros(b.shape)
             a[20:40, 30:50] = 2.5e-7
-            m.upload(0, "RHSx", a)
+            nm = "RHSx"
         else:
             nm = "mu" if what == "mu" else "hhq_rest"
-            m.upload(0, nm, np.full(b.shape, 3.0 if what == "mu" else 80.0))
+            a = np.full(b.shape, 3.0 if what == "mu" else 80.0)
+        m.upload(0, nm, a)
+        ref.upload(b, nm, a)
         m.step(5, check_every=1)
         m.step(4, check_every=1).synchronize()
-        out[graph] = {nm: m.download(0, nm) for nm in ("ssh", "sshp", "ubrtr", "ubrtrp", "vbrtr", "vbrtrp", "hhu",
-                                                       "vort", "str_t", "RHSx_dif")}
+        ref.run(9)
         assert m.onepass_active
+        bad = ref.mismatches(m)
         m.close()
-    bad = [nm for nm, a in out[True].items() if not bits_equal(a, out[False][nm])]
-    assert not bad, f"graph replay vs stream after a {what} upload: {bad}"
+        assert not bad, f"graph {graph}: steps after a {what} upload differ from the oracle: {bad}"
 
 
 @pytest.mark.gpu
@@ -591,24 +625,23 @@ def test_onepass_rows_rerun_with_ieee_divisions(amd, kc):
     a wave-uniform branch no other test takes); the results must still be the role-flip path's
     bit for bit, in both variants (known constants / general)."""
     n, steps = 130, 6
-    out = {}
     for onepass in (True, False):
         m = amd.OceanModel(amd.box_config(n)).set_onepass(onepass).set_known_constants(kc)
         m.init()
+        ref = OracleTwin(n)
         rng = np.random.default_rng(7)
         for nms in (("ubrtr", "ubrtrn"), ("ubrtrp",), ("vbrtr", "vbrtrn"), ("vbrtrp",)):
             a = m.download(0, nms[0])
             a[:, 40:60] = 1e-290 * (1.0 + rng.random(a[:, 40:60].shape))   # rows 40..59 (at rest: 0 before)
             for nm in nms:   # both buffers of a role-flip pair (they agree, as the reference leaves them)
                 m.upload(0, nm, a)
+                ref.upload(m.blocks[0], nm, a)
         m.step(steps, tau=1.0, check_every=1).synchronize()
         assert m.onepass_active == onepass
-        out[onepass] = {nm: m.download(0, nm) for nm in ("ssh", "sshn", "sshp", "ubrtr", "ubrtrn", "ubrtrp", "vbrtr",
-                                                        "vbrtrn", "vbrtrp", "hhu", "hhv", "hhh", "vort", "str_t",
-                                                        "str_s", "RHSx_dif", "RHSy_adv")}
+        ref.run(steps)
+        bad = ref.mismatches(m)
         m.close()
-    bad = [nm for nm, a in out[True].items() if not bits_equal(a, out[False][nm])]
-    assert not bad, f"one-pass rows re-run with IEEE divisions differ from the role-flip path: {bad}"
+        assert not bad, f"rows with dividends below udiv's range (one-pass {onepass}) differ from the oracle: {bad}"
 
 
 def test_second_buffers_across_calls(amd):
