@@ -654,25 +654,18 @@ static int launch_march_part(const ocn_block *b, const Range &all, int part, con
     return launch_march(b, all, body, s);
 }
 
-// Software pipelining of the marches (OCN_MARCH_PF = 1): the loads a row needs ("batch" of
-// row n: the arrays' row n+1 or n values, its mask bytes and metric row n+1) are issued one
-// iteration ahead, so a wave's loads for row n+1 are in flight while it computes row n.
-#ifndef OCN_MARCH_PF
-#define OCN_MARCH_PF 0
-#endif
-
 // The march loop shared by every march body F: F::Batch holds one row's loads, F::load fills it,
-// F::row consumes it (rotate the kept rows, compute, store).
+// F::row consumes it (rotate the kept rows, compute, store).  Row n+1's loads are issued after row
+// n's compute (issuing them before it, one iteration ahead, was measured slower: register pressure).
 template <class F, class V>
 __device__ __forceinline__ void march_rows(const F &k, V &x, const Lane &L, int nb, int ne)
 {
     typename F::Batch cur, nxt;
     k.load(cur, L, nb);
     for (int n = nb; n <= ne; ++n) {
-        if (OCN_MARCH_PF && n < ne) k.load(nxt, L, n + 1);   // wave-uniform branch
         k.row(x, cur, L, n);
         if (n < ne) {
-            if (!OCN_MARCH_PF) k.load(nxt, L, n + 1);
+            k.load(nxt, L, n + 1);
             cur = nxt;
         }
     }
@@ -1581,18 +1574,6 @@ template <bool HH, bool SKIP> struct MarchCA {
 #ifndef OCN_STEP_WAVES
 #define OCN_STEP_WAVES 2   // waves per SIMD asked of the register allocator
 #endif
-#ifndef OCN_STEP_BUFST
-#define OCN_STEP_BUFST 1   // the step's stores as st_on (no exec branches around them)
-#endif
-#ifndef OCN_STEP_ONEBLOCK
-#define OCN_STEP_ONEBLOCK 1   // D(n+1) and S(n) in one basic block, warm-up rows peeled (MarchStep::iteration)
-#endif
-#ifndef OCN_STEP_JOINT
-#define OCN_STEP_JOINT 0   // 1: one IEEE re-run test after D and S (else D's before S, as without ONEBLOCK)
-#endif
-#ifndef OCN_STEP_SCHEDB
-#define OCN_STEP_SCHEDB -1   // (JOINT) sched_barrier mask between D and S: only LDS reads and SALU cross (-1: none)
-#endif
 // A whole role-flip step in one register march (ocn_ctx.hip one_step_fused, "one-pass" steps of
 // a single-block call): the state (ssh, sshp, ubrtr, ubrtrp, vbrtr, vbrtrp; h_r, mu, RHSx, RHSy)
 // is read once and the next state written once -- 10 + 6 arrays, against fused B + CA's 22 + 12.
@@ -1659,26 +1640,16 @@ __device__ __forceinline__ double udiv(double x, double d, double rd)
     return __builtin_fma(-t, rd, q);
 }
 // the smallest frexp exponent of the dividends of a row (0 for x = 0)
-#ifndef OCN_DIAG_NOSTORE
-#define OCN_DIAG_NOSTORE 0   // timing diagnostics only: the one-pass march stores nothing (outputs summed)
-#endif
-#ifndef OCN_DIAG_NOLOAD
-#define OCN_DIAG_NOLOAD 0    // timing diagnostics only: the one-pass march reads no state rows
-#endif
-#ifndef OCN_DIAG_NOCHK
-#define OCN_DIAG_NOCHK 0   // A/B timing diagnostics only (results unchecked): 1 = no range checks and no
-#endif                     // re-run branches in the one-pass march, 2 = checks kept, branches removed
 __device__ __forceinline__ void exp_check(int &acc, double x)
 {
-    if (OCN_DIAG_NOCHK == 1) return;
     acc = min(acc, __builtin_amdgcn_frexp_exp(x));
 }
 constexpr int kUdivMinExp = -899;   // frexp exponent >= -899  <=>  |x| >= 2^-900
 
 // The row-uniform operands of the one-pass step, per row r, as the doubles the arithmetic uses
 // (each formed exactly as the step forms it from the real(4) row table: promoted metrics, the
-// real(4) products and sums of metrics, the reciprocals of udiv's divisors).  OCN_STEP_LDS: a
-// workgroup forms them once for its rows into LDS (MarchStep::prologue, a thread per row) and
+// real(4) products and sums of metrics, the reciprocals of udiv's divisors).  The known-constant
+// variant (MarchStep::kLds): a workgroup forms them once for its rows into LDS (MarchStep::prologue, a thread per row) and
 // its waves read them there (broadcast ds_read: no scalar loads, conversions or SGPR spills;
 // 0.554 -> 0.480 ms per 4096^2 step); else they are formed from scalar loads of the row table
 // where used.  The general variant keeps the scalar loads: with its loaded h_r, mu, forcing and
@@ -1686,32 +1657,19 @@ constexpr int kUdivMinExp = -899;   // frexp exponent >= -899  <=>  |x| >= 2^-90
 enum RowC { RC_DX, RC_DY, RC_DXT, RC_DYT, RC_DXH, RC_DYH, RC_DXB, RC_DYB, RC_RDXT, RC_RDYH, RC_RDXH, RC_RDYT,
             RC_RDXB, RC_RDYB, RC_RAT0, RC_RAT1, RC_RAT2, RC_RAT3, RC_RLH, RC_DY2, RC_DX2, RC_AREA, RC_RAREA,
             RC_DXB2, RC_DYB2, RC_RDSELF, RC_RDNEXT, kRowC };
-#ifndef OCN_STEP_LDS
-#define OCN_STEP_LDS 1
-#endif
-#ifndef OCN_STEP_LDS_GENERAL
-#define OCN_STEP_LDS_GENERAL 0   // also in the general variant (its VGPRs spill: 0.83 vs 0.64 ms at 4096^2)
-#endif
 #ifndef OCN_PAIR_MAX_ROWS
 #define OCN_PAIR_MAX_ROWS 150   // the tallest workgroup tile of the two-step launch (its rows +- 5 in LDS)
 #endif
 // a workgroup's 4 stacked tiles + 2 rows each side; a two-step workgroup's tile + 5 above, 4 below
 constexpr int kStepLdsRows = 4 * OCN_STEP_ROWS + 4 > OCN_PAIR_MAX_ROWS + 10 ? 4 * OCN_STEP_ROWS + 4 : OCN_PAIR_MAX_ROWS + 10;
 
-#if OCN_STEP_LDS
 __shared__ double g_step_rc[kStepLdsRows * kRowC];   // the workgroup's rows [nb - 2, ne + 2]
 __shared__ unsigned g_step_rlo;                       // table row of its first row
-#endif
-// Two steps per launch (OCN_STEP_PAIR, MarchStep PAIR): the producer waves' new state (ssh, sshp,
-// ubrtr, ubrtrp, vbrtr, vbrtrp after the first step, by row mod 4) for the consumer waves.
+// Two steps per launch (MarchStep PAIR): the producer waves' new state (ssh, sshp, ubrtr, ubrtrp,
+// vbrtr, vbrtrp after the first step, by row mod 4) for the consumer waves.
 // (Measured and dropped: a wave's 60-column output rows stored as whole 128-B lines through LDS,
 // a workgroup barrier per row -- 0.407-0.424 against 0.391 ms per 4096^2 single launch.)
-#ifndef OCN_STEP_PAIR
-#define OCN_STEP_PAIR 1
-#endif
-#if OCN_STEP_PAIR
 __shared__ double g_pair[4][6][120];
-#endif
 
 // row constant k of table row r (rows[(id - OCN_DX) * nrows + r], real(4)); r + 1 for RC_RDNEXT
 __device__ __forceinline__ double row_const(const float *rows, unsigned nrows, unsigned r, int k)
@@ -1763,32 +1721,8 @@ __device__ __forceinline__ double rcp_count(unsigned c)
     return __builtin_bit_cast(double, (unsigned long long)hi << 32);
 }
 
-#ifndef OCN_STEP_UNROLL
-#define OCN_STEP_UNROLL 1
-#endif
-#ifndef OCN_STEP_CARRY
-#define OCN_STEP_CARRY 1   // shifted weights / v kept in the ring (no second shift), sh * ffs as sh
-#endif
-#ifndef OCN_STEP_NBAD_ACC
-#define OCN_STEP_NBAD_ACC 0   // 1: check_ssh_err counted per lane over the tile, one atomic at its end (no per-row branch)
-#endif
-#ifndef OCN_STEP_MZ_FORCE
-#define OCN_STEP_MZ_FORCE 0   // A/B only: the known-constant variant assumes mu = +0 (a measurement of that saving)
-#endif
-#ifndef OCN_STEP_FACE
-#define OCN_STEP_FACE 1   // each flux across a row face / lane face formed once (MarchStep::step, face)
-#endif
-#ifndef OCN_STEP_ILP
-#define OCN_STEP_ILP 1   // independent quotients of a row issued stage by stage together (MarchStep::dvn)
-#endif
-#ifndef OCN_STEP_PF2
-#define OCN_STEP_PF2 0   // 1: the known-constant variant issues each row's loads two rows ahead (measured: no gain)
-#endif
-static_assert(!(OCN_STEP_NBAD_ACC && OCN_STEP_PF2), "OCN_STEP_NBAD_ACC: the one-row-ahead loop only");
-static_assert(!OCN_STEP_FACE || (OCN_STEP_ONEBLOCK && !OCN_DIAG_NOCHK), "OCN_STEP_FACE: the OCN_STEP_ONEBLOCK iteration");
-// StepRegs::Win: 4 rows, written out for kRing phases (MarchStep::march); even with OCN_STEP_PF2,
-// so that the batch a phase takes (phase parity) is known in every unrolled phase
-constexpr int kRing = OCN_STEP_PF2 ? 6 : 5;
+// StepRegs::Win: rows n-1 .. n+2 in a ring of kRing slots, written out for kRing phases (MarchStep::march)
+constexpr int kRing = 5;
 
 struct StepRegs {
     // rows n-1, n, n+1, n+2 at this lane's column: a ring of kRing slots, row n + k - 1 in slot
@@ -1814,7 +1748,7 @@ struct StepRegs {
     // products shared between lanes / rows (each the reference's own sub-expression, see derive)
     Win<double> w0, w1;               // interp weights ((h * dx) * dy) * lu of levels 0 / 1 (rows n+1, n+2)
     Win<double> pu, pv, vh, t3, cx, rr, dt, dxq;
-    Win<double> w0r, vr;              // OCN_STEP_CARRY: w0 and v shifted one lane left (their m+1 values)
+    Win<double> w0r, vr;              // w0 and v shifted one lane left (their m+1 values): shifted once per row
     // metric rows: read where used, as wave-uniform scalar loads from the (read-only) row table
     // through the constant address space -- no table of 4 rows x 14 values held in SGPRs
     const __attribute__((address_space(4))) float *rows;
@@ -1822,15 +1756,12 @@ struct StepRegs {
     unsigned nrows, rn;               // table stride, row index of n (n - bnd_y1)
     double qb, qc;                     // stress quotients of D's previous row (vp/dxh) and next row (up/dxt)
     double tau, inv_tau, f;
-    int nbad_cnt;                      // OCN_STEP_NBAD_ACC: this lane's check_ssh_err count of the tile
-    int dacc;                          // OCN_DIAG_NOCHK 2: the smallest dividend exponent of the tile
-    double dsink;                      // OCN_DIAG_NOSTORE: the sum of the outputs not stored
     int32_t *nbp;                      // where this wave's check_ssh_err count goes (null: unchecked)
     bool cnt;                          // the point is counted (PAIR producers: their workgroup's points only)
     int pj;                            // PAIR: the lane's column in the workgroup's LDS ring
-    double fyx, fyy, vht, a2t;         // OCN_STEP_FACE: row n-1's n faces (MarchStep::face)
+    double fyx, fyy, vht, a2t;         // row n-1's n faces (MarchStep::face)
     double hr0, mu0;                   // known-constant variant: the uniform h_r and mu (MarchStep::kc)
-    const __attribute__((address_space(3))) double *lds;   // OCN_STEP_LDS: the workgroup's row constants
+    const __attribute__((address_space(3))) double *lds;   // (kLds) the workgroup's row constants
     unsigned rlo;                                            // table row of lds row 0
     // row constant k (RowC) of row n + dy, from LDS or from scalar loads
     template <bool LDS> __device__ __forceinline__ double cst(int k, int dy) const
@@ -1848,7 +1779,7 @@ struct StepRegs {
         }
         return row_const_s(k, dy);
     }
-    // (OCN_STEP_LDS 0) row constant k from scalar loads
+    // (the general variant) row constant k from scalar loads
     __device__ __forceinline__ double row_const_s(int k, int dy) const
     {
         auto g = [&](int id) { return met(id, dy); };
@@ -1964,7 +1895,6 @@ struct MarchStep {
     __device__ __forceinline__ int rowc(int r, int RO) const { return RO == 1 ? min(max(r, b.bnd_y1), b.bnd_y2) : r; }
     template <int RO = 0> __device__ __forceinline__ void load(const StepRegs &x, Batch &q, int m, int n) const
     {
-#if OCN_STEP_PAIR
         if constexpr (RO == 2) {
             const Geo I = geo(&b);
             const Pt c2 = I(m, n + 2);
@@ -1983,15 +1913,6 @@ struct MarchStep {
             }
             return;
         }
-#endif
-#if OCN_DIAG_NOLOAD   // (timing diagnostic only) the row's state made up from its index, nothing read
-        if (ZF && !HR) {
-            const double a = (double)(n & 7) * 0.125 + (double)(m & 3) * 0.25;
-            q.u = a * 0.01; q.up = a * 0.011; q.ssh = a * 0.1; q.shp = a * 0.09; q.hr = x.hr0; q.bits = 0xffu;
-            q.v = a * 0.012; q.vp = a * 0.013; q.mu = x.mu0; q.rhsx = q.rhsy = 0.0;
-            return;
-        }
-#endif
         const Geo I = geo(&b);
         const Pt c = I(m, rowc(n, RO)), c1 = I(m, rowc(n + 1, RO)), c2 = I(m, rowc(n + 2, RO));
         q.u = ld(t.f(OCN_UBRTR), c2); q.up = ld(t.f(OCN_UBRTRP), c2);
@@ -2019,14 +1940,10 @@ struct MarchStep {
         const int k = dy + 1;
         const double gx = x.cst<kLds>(RC_DX, dy), gy = x.cst<kLds>(RC_DY, dy);
         const double l = D(x.mk<PH>(OCN_LU, 0, dy));
-#if OCN_STEP_CARRY   // ffs = 1 (launch_onepass requires it): sh * ffs is sh bit for bit
+        // ffs = 1 (launch_onepass requires it): sh * ffs is sh bit for bit
         x.w0.s<PH>(k) = (x.hr.s<PH>(k) + x.ssh.s<PH>(k)) * gx * gy * l;
         x.w1.s<PH>(k) = (x.hr.s<PH>(k) + x.shp.s<PH>(k)) * gx * gy * l;
         x.w0r.s<PH>(k) = shz(x.w0.s<PH>(k), 1);   // its right lane's weight: the corner (m+1) weight
-#else
-        x.w0.s<PH>(k) = (x.hr.s<PH>(k) + x.ssh.s<PH>(k) * x.f) * gx * gy * l;
-        x.w1.s<PH>(k) = (x.hr.s<PH>(k) + x.shp.s<PH>(k) * x.f) * gx * gy * l;
-#endif
     }
 
     // Where D takes the value in memory (mask 0 or outside the stage's range): those loads, issued
@@ -2072,7 +1989,7 @@ struct MarchStep {
         else return udiv(a, d, rd);
     }
     // N independent quotients x[i] / d[i], each stage of udiv issued for all N before the next
-    // (OCN_STEP_ILP): the same operations on the same operands as N separate udivs, written so
+    // (MarchStep::derive, step): the same operations on the same operands as N separate udivs, written so
     // that N dependency chains are in flight at once rather than one after another
     template <bool E, int N>
     __device__ __forceinline__ static void dvn(const double (&a)[N], const double (&d)[N], const double (&rd)[N],
@@ -2103,33 +2020,25 @@ struct MarchStep {
         const unsigned cu = b00 + b10, cv = b00 + b01, ch = cu + b01 + b11;
         const double dxt = x.cst<kLds>(RC_DXT, 1), dyt = x.cst<kLds>(RC_DYT, 1), dxh = x.cst<kLds>(RC_DXH, 1),
                      dyh = x.cst<kLds>(RC_DYH, 1), dxb = x.cst<kLds>(RC_DXB, 1), dyb = x.cst<kLds>(RC_DYB, 1);
-#if OCN_STEP_CARRY   // the right lane's weights, shifted once per row (weights) and kept in the ring
+        // the right lane's weights, shifted once per row (weights) and kept in the ring
         const double w00 = x.w0.s<PH>(2), w10 = x.w0r.s<PH>(2), w01 = x.w0.s<PH>(3), w11 = x.w0r.s<PH>(3);
-#else
-        const double w00 = x.w0.s<PH>(2), w10 = shz(w00, 1), w01 = x.w0.s<PH>(3), w11 = shz(w01, 1);
-#endif
         const double p00 = x.w1.s<PH>(2), p10 = shz(p00, 1), p01 = x.w1.s<PH>(3);
         const double s0 = w00 + w10;
         const double rxt = x.cst<kLds>(RC_RDXT, 1), ryh = x.cst<kLds>(RC_RDYH, 1), rxh = x.cst<kLds>(RC_RDXH, 1),
                      ryt = x.cst<kLds>(RC_RDYT, 1);
         const double ru = rcp_count(cu), rv = rcp_count(cv);
         const double a_u0 = s0 * ru, a_v0 = (w00 + w01) * rv, a_u1 = (p00 + p10) * ru, a_v1 = (p00 + p01) * rv;
-#if OCN_STEP_ONEBLOCK
         // a / 3 (three sea corners): udiv by 3 (the same correctly rounded quotient: its dividend's
         // range is checked with the others below), IEEE division in the re-run -- per lane, no branch
         const double sh = s0 + w01 + w11;
         const double a_h0 = ch == 3 ? (E ? sh / 3.0 : udiv(sh, 3.0, 1.0 / 3.0)) : sh * rcp_count(ch);
         if (!E) exp_check(acc, sh);
-#else
-        const double a_h0 = __builtin_expect(__builtin_amdgcn_ballot_w64(ch == 3) != 0, 0) ? (s0 + w01 + w11) / D(ch)
-                                                                 : (s0 + w01 + w11) * rcp_count(ch);
-#endif
         if (!E) {   // (a / g1) / g2: a's range bounds a / g1's (|g1| <= 2^60)
             exp_check(acc, a_u0); exp_check(acc, a_v0); exp_check(acc, a_h0); exp_check(acc, a_u1);
             exp_check(acc, a_v1); exp_check(acc, x.up.s<PH>(2)); exp_check(acc, x.vp.s<PH>(2)); exp_check(acc, x.up.s<PH>(3));
         }
-#if OCN_STEP_ILP
         // the nine first quotients (hh_init's five, a5's four) at once, then the five second ones
+        // (each stage of udiv issued for all of them: independent chains in flight together)
         double q1[9], q2[5];
         dvn<E, 9>({a_u0, a_v0, a_h0, a_u1, a_v1, x.up.s<PH>(2), x.vp.s<PH>(2), x.up.s<PH>(3), x.vp.s<PH>(2)},
                   {dxt, dxh, dxb, dxt, dxh, dyh, dxh, x.cst<kLds>(RC_DXT, 2), dyt},
@@ -2137,30 +2046,16 @@ struct MarchStep {
         dvn<E, 5>({q1[0], q1[1], q1[2], q1[3], q1[4]}, {dyh, dyt, dyb, dyh, dyt},
                   {ryh, ryt, x.cst<kLds>(RC_RDYB, 1), ryh, ryt}, q2);
         const double u0 = q2[0], v0 = q2[1], h0 = q2[2], u1 = q2[3], v1 = q2[4];
-#else
-        const double u0 = dv<E>(dv<E>(a_u0, dxt, rxt), dyh, ryh);
-        const double v0 = dv<E>(dv<E>(a_v0, dxh, rxh), dyt, ryt);
-        const double h0 = dv<E>(dv<E>(a_h0, dxb, x.cst<kLds>(RC_RDXB, 1)), dyb, x.cst<kLds>(RC_RDYB, 1));
-        const double u1 = dv<E>(dv<E>(a_u1, dxt, rxt), dyh, ryh);
-        const double v1 = dv<E>(dv<E>(a_v1, dxh, rxh), dyt, ryt);
-#endif
         // a3 uv_trans_vort (vel_ssh.f90:247-281, sw_stencils.h uv_trans_vort_math)
         const double u_0 = x.u.s<PH>(2), u_1 = x.u.s<PH>(3), v_0 = x.v.s<PH>(2), v_r = shz(v_0, 1);
-#if OCN_STEP_CARRY
         x.vr.s<PH>(2) = v_r;   // S reads it at rows n and n-1 (the same shift of the same values)
-#endif
         const double vort = (v_r * dyt - v_0 * dyt) - (u_1 * x.cst<kLds>(RC_DXT, 2) - u_0 * dxt)
                             - ((v_r - v_0) * dyb - (u_1 - u_0) * dxb);
         // a5 (mixing.f90:33-44, sw_stencils.h stress_components_math) with its quotients shared:
         // up/dyh at m-1 is the left lane's up/dyh (dyh is constant along the row), vp/dxh at n-1
         // is the previous row's, up/dxt at n+1 the next row's (formed here, kept for the next
         // row), vp/dyt at m+1 the right lane's -- the same operands, so the same values
-#if OCN_STEP_ILP
         const double qa = q1[5], qb = q1[6], qc1 = q1[7], qe = q1[8];
-#else
-        const double qa = dv<E>(x.up.s<PH>(2), dyh, ryh), qb = dv<E>(x.vp.s<PH>(2), dxh, rxh);
-        const double qc1 = dv<E>(x.up.s<PH>(3), x.cst<kLds>(RC_DXT, 2), x.cst<kLds>(RC_RDXT, 2)), qe = dv<E>(x.vp.s<PH>(2), dyt, ryt);
-#endif
         const double st = x.cst<kLds>(RC_RAT0, 1) * (qa - shz(qa, -1)) - x.cst<kLds>(RC_RAT1, 1) * (qb - x.qb);
         const double ss = x.cst<kLds>(RC_RAT2, 1) * (qc1 - x.qc) + x.cst<kLds>(RC_RAT3, 1) * (shz(qe, 1) - qe);
         qb_next = qb;
@@ -2183,26 +2078,17 @@ struct MarchStep {
         const double rr = x.cst<kLds>(RC_RLH, 1) * hh * dxb * dyb;   // sw_update_uv: rlh_s * hhh * dxb * dyb
         x.rr.s<PH>(2) = rr;
         x.cx.s<PH>(2) = rr * (v_r + v_0);                                //   ... * (vbrtr(1,0) + vbrtr)
-#if OCN_STEP_CARRY
         const double hq = x.hr.s<PH>(2) + x.ssh.s<PH>(2);                    // depth.f90:48 hq = h_r + sh*ffs (ffs = 1)
-#else
-        const double hq = x.hr.s<PH>(2) + x.ssh.s<PH>(2) * x.f;              // depth.f90:48 hq = h_r + sh*ffs
-#endif
         x.dt.s<PH>(2) = x.cst<kLds>(RC_DY2, 1) * x.mu.s<PH>(2) * hq * stt;         // uv_diff2: dy**2 * mu * hq * str_t
         x.dxq.s<PH>(2) = x.cst<kLds>(RC_DX2, 1) * x.mu.s<PH>(2) * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
     }
 
-#if OCN_STEP_FACE
     // (the warm-up row n = nb - 1, after D(nb)) the n+1 faces of row n that S(nb) takes from the
     // row before -- the expressions S(n) forms them with (step)
     template <int PH> __device__ __forceinline__ void face(StepRegs &x) const
     {
         const double u = x.u.s<PH>(1), v = x.v.s<PH>(1), u_n = x.u.s<PH>(2), v_n = x.v.s<PH>(2);
-#if OCN_STEP_CARRY
         const double v_r = x.vr.s<PH>(1);
-#else
-        const double v_r = shz(v, 1);
-#endif
         const double pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2), luu = D(x.mk<PH>(OCN_LUU, 0, 0));
         x.fyx = (pv + shz(pv, 1)) / 2.0 * (u_n + u) / 2.0 * luu;
         x.vht = x.vh.s<PH>(1) * (v_r + v);
@@ -2212,23 +2098,20 @@ struct MarchStep {
             x.a2t = x.cst<kLds>(RC_DXB2, 0) * muh_p * x.hh.s<PH>(1) * x.sts.s<PH>(1);
         }
     }
-#endif
 
-    // a row's outputs and where they are stored (OCN_STEP_BUFST: stored after S's branch)
+    // a row's outputs and where they are stored (store_out, after S's branch)
     struct Out {
         bool lu = false, cu = false, cv = false, uu = false;   // uu: luu (LAST's vort / str_s)
         double sshn = 0.0, fx = 0.0, un = 0.0, fa = 0.0, vn = 0.0, fb = 0.0;
         double vort = 0.0, sts = 0.0, stt = 0.0, rxa = 0.0, rxd = 0.0, rya = 0.0, ryd = 0.0;   // LAST
-        double fyx = 0.0, fyy = 0.0, vht = 0.0, a2t = 0.0;   // OCN_STEP_FACE: row n's n+1 faces (see face)
-        int dbad = 0;   // OCN_STEP_NBAD_ACC: the row's change to the lane's check_ssh_err count
+        double fyx = 0.0, fyy = 0.0, vht = 0.0, a2t = 0.0;   // row n's n+1 faces (see face)
     };
     // S at row n: a1, fused B, a8's filters, check_ssh_err (sw_stencils.h sw_update_ssh_math,
     // uv_trans_math, uv_diff2_math, sw_update_uv_math written out over the shared products)
     template <bool E, int PH>
     __device__ __forceinline__ void step(const StepRegs &x, const Lane &L, int n, int &acc, bool &bad, Out &o) const
     {
-        const Geo I = geo(&b);
-        const Pt c = I(L.m, n);
+        (void)n;
         const double u = x.u.s<PH>(1), v = x.v.s<PH>(1), hu = x.hu.s<PH>(1), hv = x.hv.s<PH>(1), hh = x.hh.s<PH>(1);
         const double dxt = x.cst<kLds>(RC_DXT, 0), dyt = x.cst<kLds>(RC_DYT, 0), dxh = x.cst<kLds>(RC_DXH, 0),
                      dyh = x.cst<kLds>(RC_DYH, 0);
@@ -2236,24 +2119,15 @@ struct MarchStep {
         const double t1 = u * hu * dyh;
         const double a_ssh = t1 - shz(t1, -1) + x.t3.s<PH>(1) - x.t3.s<PH>(0);
         if (!E) exp_check(acc, a_ssh);
-#if !OCN_STEP_ILP
-        const double sshn = x.shp.s<PH>(1) + 2.0 * x.tau * (-dv<E>(a_ssh, x.cst<kLds>(RC_AREA, 0), x.cst<kLds>(RC_RAREA, 0)));
-#endif
         // a4 uv_trans (vel_ssh.f90:283-373)
-        const double u_r = shz(u, 1), u_l = shz(u, -1), u_n = x.u.s<PH>(2), u_s = x.u.s<PH>(0);
-#if OCN_STEP_CARRY
-        const double v_r = x.vr.s<PH>(1), v_l = shz(v, -1), v_n = x.v.s<PH>(2), v_s = x.v.s<PH>(0), v_sr = x.vr.s<PH>(0);
-#else
-        const double v_r = shz(v, 1), v_l = shz(v, -1), v_n = x.v.s<PH>(2), v_s = x.v.s<PH>(0), v_sr = shz(v_s, 1);
-#endif
-        const double pu = x.pu.s<PH>(1), pun = x.pu.s<PH>(2), pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2), pvs = x.pv.s<PH>(0);
-        const double luu = D(x.mk<PH>(OCN_LUU, 0, 0)), luus = D(x.mk<PH>(OCN_LUU, 0, -1));
+        const double u_r = shz(u, 1), u_n = x.u.s<PH>(2);
+        const double v_r = x.vr.s<PH>(1), v_n = x.v.s<PH>(2);
+        const double pu = x.pu.s<PH>(1), pun = x.pu.s<PH>(2), pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2);
+        const double luu = D(x.mk<PH>(OCN_LUU, 0, 0));
         double rxa, rya;
-#if OCN_STEP_FACE
         // each face's flux once: the m-1 face is the left lane's m+1 face and the n-1 face the row
         // before's n+1 face (carried in x, face<PH>) -- the same operands, the sums' terms swapped
         // (IEEE addition commutes), so the same values bit for bit
-        (void)luus; (void)u_l; (void)v_l; (void)u_s; (void)v_s; (void)v_sr; (void)pvs;
         {
             const double fx_p = (pu + shz(pu, 1)) / 2.0 * (u + u_r) / 2.0;
             const double fx_m = shz(fx_p, -1);
@@ -2272,27 +2146,9 @@ struct MarchStep {
             rya = -(fx_p - fx_m + fy_p - x.fyy) - (q + shz(q, -1)) / 4.0;
             o.fyy = fy_p;
         }
-#else
-        {
-            const double fx_p = (pu + shz(pu, 1)) / 2.0 * (u + u_r) / 2.0;
-            const double fx_m = (pu + shz(pu, -1)) / 2.0 * (u + u_l) / 2.0;
-            const double fy_p = (pv + shz(pv, 1)) / 2.0 * (u_n + u) / 2.0 * luu;
-            const double fy_m = (pvs + shz(pvs, 1)) / 2.0 * (u_s + u) / 2.0 * luus;
-            rxa = -(fx_p - fx_m + fy_p - fy_m) + (x.vh.s<PH>(1) * (v_r + v) + x.vh.s<PH>(0) * (v_sr + v_s)) / 4.0;
-        }
-        {
-            const double fy_p = (pv + pvn) / 2.0 * (v + v_n) / 2.0;
-            const double fy_m = (pv + pvs) / 2.0 * (v + v_s) / 2.0;
-            const double sn = pu + pun;
-            const double fx_p = sn / 2.0 * (v_r + v) / 2.0;
-            const double fx_m = shz(sn, -1) / 2.0 * (v_l + v) / 2.0;
-            const double q = x.vh.s<PH>(1) * (u_n + u);
-            rya = -(fx_p - fx_m + fy_p - fy_m) - (q + shz(q, -1)) / 4.0;
-        }
-#endif
         // a6 uv_diff2 (vel_ssh.f90:375-452)
         double rxd, ryd;
-        double q_ssh = 0.0;   // (OCN_STEP_ILP) a1's a_ssh / area
+        double q_ssh = 0.0;   // a1's a_ssh / area
         {
             // ZF: mu is one value over the step's reach, so its neighbours are that value (the lane
             // shifts differ only on the edge lanes, which produce no output and whose mu terms no
@@ -2305,7 +2161,6 @@ struct MarchStep {
             const double dxb2 = x.cst<kLds>(RC_DXB2, 0), dxb2m = x.cst<kLds>(RC_DXB2, -1), dyb2 = x.cst<kLds>(RC_DYB2, 0);
             const double sts = x.sts.s<PH>(1);
             const double dtc = x.dt.s<PH>(1);
-#if OCN_STEP_FACE
             // ZF: the three averages are one value, so a2's second term is the row before's first
             // (carried) and a4's the left lane's first -- the same operands, the same values
             double a2, a4;
@@ -2320,21 +2175,9 @@ struct MarchStep {
                 a4 = dyb2 * muh_p * hh * sts - dyb2 * muh_m2 * shz(hh, -1) * shz(sts, -1);
             }
             const double a1 = shz(dtc, 1) - dtc, a3 = x.dxq.s<PH>(2) - x.dxq.s<PH>(1);
-#else
-            const double a1 = shz(dtc, 1) - dtc, a2 = dxb2 * muh_p * hh * sts - dxb2m * muh_m * x.hh.s<PH>(0) * x.sts.s<PH>(0);
-            const double a3 = x.dxq.s<PH>(2) - x.dxq.s<PH>(1),
-                         a4 = dyb2 * muh_p * hh * sts - dyb2 * muh_m2 * shz(hh, -1) * shz(sts, -1);
-#endif
-#if OCN_STEP_MZ_FORCE
-            if (ZF) {   // (A/B measurement only) mu = +0: a1..a4 are +-0 or NaN, a / d = a for the metrics
-                rxd = a1 + a2;
-                ryd = -a3 + a4;
-                q_ssh = dv<E>(a_ssh, x.cst<kLds>(RC_AREA, 0), x.cst<kLds>(RC_RAREA, 0));
-            } else
-#endif
             {
                 if (!E) { exp_check(acc, a1); exp_check(acc, a2); exp_check(acc, a3); exp_check(acc, a4); }
-#if OCN_STEP_ILP   // a1's quotient with uv_diff2's four, stage by stage (dvn)
+                // a1's quotient with uv_diff2's four, stage by stage (dvn)
                 double qd[5];
                 dvn<E, 5>({a_ssh, a1, a2, a3, a4}, {x.cst<kLds>(RC_AREA, 0), dyh, dxt, dxh, dyt},
                           {x.cst<kLds>(RC_RAREA, 0), x.cst<kLds>(RC_RDYH, 0), x.cst<kLds>(RC_RDXT, 0),
@@ -2342,15 +2185,9 @@ struct MarchStep {
                 q_ssh = qd[0];
                 rxd = qd[1] + qd[2];
                 ryd = -qd[3] + qd[4];
-#else
-                rxd = dv<E>(a1, dyh, x.cst<kLds>(RC_RDYH, 0)) + dv<E>(a2, dxt, x.cst<kLds>(RC_RDXT, 0));
-                ryd = -dv<E>(a3, dxh, x.cst<kLds>(RC_RDXH, 0)) + dv<E>(a4, dyt, x.cst<kLds>(RC_RDYT, 0));
-#endif
             }
         }
-#if OCN_STEP_ILP
         const double sshn = x.shp.s<PH>(1) + 2.0 * x.tau * (-q_ssh);
-#endif
         // a7 sw_update_uv (vel_ssh.f90:108-195); hun = hu, hvn = hv (the reuse identity)
         double un, vn;
         {
@@ -2378,44 +2215,21 @@ struct MarchStep {
         const double ts = sw.time_smooth;
         const double fx = asselin(x.ssh.s<PH>(1), sshn, x.shp.s<PH>(1), ts);
         const double fa = asselin(u, un, x.up.s<PH>(1), ts), fb = asselin(v, vn, x.vp.s<PH>(1), ts);
-#if OCN_STEP_BUFST
-        {   // the row's stores are issued after the branch (iteration, st_on)
-            const unsigned bc = x.bits.s<PH>(1);
-            o.lu = L.out && (bc & (1u << OCN_LU));
-            o.cu = L.out && (bc & (1u << OCN_LCU));
-            o.cv = L.out && (bc & (1u << OCN_LCV));
-            o.sshn = sshn; o.fx = fx; o.un = un; o.fa = fa; o.vn = vn; o.fb = fb;
-            if (LAST) {
-                o.uu = L.out && (bc & (1u << OCN_LUU));
-                o.vort = x.vort.s<PH>(1); o.sts = x.sts.s<PH>(1); o.stt = x.stt.s<PH>(1);
-                o.rxa = rxa; o.rxd = rxd; o.rya = rya; o.ryd = ryd;
-            }
-            // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
-            const bool bd = o.lu && !(sshn < 10000.0 && sshn > -10000.0);
-            if (OCN_STEP_NBAD_ACC) o.dbad = (int)bd - (int)(E && bad);   // (the re-run replaces the first count)
-            else if (__builtin_expect(x.nbp && x.cnt && bd != (E && bad), 0)) atomicAdd(x.nbp, bd ? 1 : -1);
-            bad = bd;
-            return;
-        }
-#endif
-        if (!L.out) return;
+        // the row's stores are issued after the branch (iteration, store_out)
         const unsigned bc = x.bits.s<PH>(1);
+        o.lu = L.out && (bc & (1u << OCN_LU));
+        o.cu = L.out && (bc & (1u << OCN_LCU));
+        o.cv = L.out && (bc & (1u << OCN_LCV));
+        o.sshn = sshn; o.fx = fx; o.un = un; o.fa = fa; o.vn = vn; o.fb = fb;
         if (LAST) {
-            if (bc & (1u << OCN_LUU)) { st(t.f(OCN_VORT), c, x.vort.s<PH>(1)); st(t.f(OCN_STR_S), c, x.sts.s<PH>(1)); }
-            if (bc & (1u << OCN_LU)) st(t.f(OCN_STR_T), c, x.stt.s<PH>(1));
-            if (bc & (1u << OCN_LCU)) { st(t.f(OCN_RHSX_ADV), c, rxa); st(t.f(OCN_RHSX_DIF), c, rxd); }
-            if (bc & (1u << OCN_LCV)) { st(t.f(OCN_RHSY_ADV), c, rya); st(t.f(OCN_RHSY_DIF), c, ryd); }
+            o.uu = L.out && (bc & (1u << OCN_LUU));
+            o.vort = x.vort.s<PH>(1); o.sts = x.sts.s<PH>(1); o.stt = x.stt.s<PH>(1);
+            o.rxa = rxa; o.rxd = rxd; o.rya = rya; o.ryd = ryd;
         }
-        if (bc & (1u << OCN_LU)) {
-            st(t.f(OCN_SSHN), c, sshn);
-            st(sshp_out, c, fx);
-            // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
-            const bool b = !(sshn < 10000.0 && sshn > -10000.0);
-            if (x.nbp && x.cnt && b != (E && bad)) atomicAdd(x.nbp, b ? 1 : -1);
-            bad = b;
-        }
-        if (bc & (1u << OCN_LCU)) { st(t.f(OCN_UBRTRN), c, un); st(up_out, c, fa); }
-        if (bc & (1u << OCN_LCV)) { st(t.f(OCN_VBRTRN), c, vn); st(vp_out, c, fb); }
+        // check_ssh_err counts each point once: the re-run (E) corrects the first pass's count
+        const bool bd = o.lu && !(sshn < 10000.0 && sshn > -10000.0);
+        if (__builtin_expect(x.nbp && x.cnt && bd != (E && bad), 0)) atomicAdd(x.nbp, bd ? 1 : -1);
+        bad = bd;
     }
 
     // a row's six stores, issued by every iteration (warm-up rows with every lane dropped) and by
@@ -2440,7 +2254,6 @@ struct MarchStep {
         }
     }
 
-#if OCN_STEP_PAIR
     // PAIR: the workgroup's barrier between iterations (LDS only: the row loads stay in flight)
     __device__ __forceinline__ static void pair_barrier()
     {
@@ -2465,15 +2278,14 @@ struct MarchStep {
             r[5][x.pj] = o.cv ? o.fb : x.vp.s<PH>(1);
         }
     }
-#endif
-    static constexpr bool kLds = OCN_STEP_LDS && (ZF || OCN_STEP_LDS_GENERAL);
+    // row constants in LDS: the known-constant variant (the general one keeps scalar loads of the row
+    // table -- with its loaded h_r, mu, forcing and fallback values the LDS operands spill VGPRs:
+    // 0.83 vs 0.64 ms at 4096^2)
+    static constexpr bool kLds = ZF;
     // the march unrolled over the register ring (StepRegs::Win) -- the known-constant variant; the
     // general one (loaded h_r, mu, forcing, fallback values) keeps the rotating loop: unrolled,
     // its scalar and vector registers spill
-    static constexpr bool kUnroll = ZF && OCN_STEP_UNROLL;
-    // rows ahead a batch is loaded (MarchStep::march): 2 in the unrolled variant with OCN_STEP_PF2
-    static constexpr int kAhead = OCN_STEP_PF2 && OCN_STEP_ONEBLOCK && OCN_STEP_BUFST && kUnroll ? 2 : 1;
-#if OCN_STEP_LDS
+    static constexpr bool kUnroll = ZF;
     static constexpr bool kPrologue = kLds;
     // the row constants of the workgroup's rows into LDS (rows fit: launch_step's tiles have at
     // most OCN_STEP_ROWS rows)
@@ -2491,7 +2303,6 @@ struct MarchStep {
         if (threadIdx.x == 0) g_step_rlo = (unsigned)lo;
         __syncthreads();
     }
-#endif
 
     // PAIR (two steps in one launch, single block, a variant chosen on the host): the producer waves march the
     // first step over the workgroup's rows +- 2 and put its new state into the LDS ring, the
@@ -2504,7 +2315,6 @@ struct MarchStep {
     // the pair is one role flip -- the first step's new state never reaches memory
     __device__ void march(const Lane &L, int nb, int ne) const
     {
-#if OCN_STEP_PAIR
         if constexpr (PAIR) {
             if (L.pr == 1) {
                 march_role<1>(L, nb - 2, ne + 2);
@@ -2517,7 +2327,6 @@ struct MarchStep {
             }
             return;
         }
-#endif
         march_role<0>(L, nb, ne);
     }
     template <int RO> __device__ void march_role(const Lane &L, int nb, int ne) const
@@ -2527,12 +2336,10 @@ struct MarchStep {
         x.nbp = RO == 2 ? nbad2 : nbad;
         x.cnt = true;
         x.pj = L.j;
-#if OCN_STEP_LDS
         if (kLds) {
             x.lds = (const __attribute__((address_space(3))) double *)g_step_rc;
             x.rlo = g_step_rlo;
         }
-#endif
         x.rows = (const __attribute__((address_space(4))) float *)t.rows;
         x.rcp = (const __attribute__((address_space(4))) double *)(t.rows + recip_offset(t.nrows));
         x.nrows = t.nrows;
@@ -2547,14 +2354,11 @@ struct MarchStep {
         const int n0 = nb - 2;
         {
             const Pt c = I(L.m, rowc(n0, RO)), c1 = I(L.m, rowc(n0 + 1, RO));
-#if OCN_STEP_PAIR
             if constexpr (RO == 2) {   // the first step's new state from the ring
                 x.ssh.s<0>(2) = g_pair[(n0 + 1) & 3][0][x.pj]; x.shp.s<0>(2) = g_pair[(n0 + 1) & 3][1][x.pj];
                 x.u.s<0>(2) = g_pair[(n0 + 1) & 3][2][x.pj]; x.up.s<0>(2) = g_pair[(n0 + 1) & 3][3][x.pj];
                 x.vp.s<0>(1) = g_pair[n0 & 3][5][x.pj];
-            } else
-#endif
-            {
+            } else {
                 x.up.s<0>(2) = ld(t.f(OCN_UBRTRP), c1); x.ssh.s<0>(2) = ld(t.f(OCN_SSH), c1);
                 x.shp.s<0>(2) = ld(t.f(OCN_SSHP), c1); x.u.s<0>(2) = ld(t.f(OCN_UBRTR), c1);
                 x.vp.s<0>(1) = ld(t.f(OCN_VBRTRP), c);
@@ -2568,37 +2372,12 @@ struct MarchStep {
         }
         Fallback fb;
         fallback<0, RO>(x, fb, L.m, n0 + 1, 2);
-#if OCN_STEP_ONEBLOCK && OCN_STEP_PF2 && OCN_STEP_BUFST
-        if constexpr (kUnroll && RO == 0) {   // two batches in flight: iteration n takes qs[n - n0 & 1], loaded at n - 2
-            Batch qs[2];
-            load(x, qs[0], L.m, n0);
-            store_out(Out{}, 0u);   // (every lane dropped: the same operations after each batch's loads as
-            load(x, qs[1], L.m, n0 + 1);   // in the loop, so its waits stay vmcnt(19))
-            store_out(Out{}, 0u);
-            iteration<0, true>(x, fb, qs[0], L, n0, nb, ne);
-            iteration<1, true>(x, fb, qs[1], L, n0 + 1, nb, ne);
-            for (int n = nb;; n += kRing) {
-                if (iteration<2>(x, fb, qs[0], L, n, nb, ne)) break;
-                if (iteration<3>(x, fb, qs[1], L, n + 1, nb, ne)) break;
-                if (iteration<4>(x, fb, qs[0], L, n + 2, nb, ne)) break;
-                if (iteration<5 % kRing>(x, fb, qs[1], L, n + 3, nb, ne)) break;
-                if (iteration<0>(x, fb, qs[0], L, n + 4, nb, ne)) break;
-                if (iteration<1>(x, fb, qs[1], L, n + 5, nb, ne)) break;
-            }
-            return;
-        }
-#endif
         Batch q;
         load<RO>(x, q, L.m, n0);
-#if OCN_STEP_BUFST
         if (RO != 1) store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
-#endif
-#if OCN_STEP_PAIR
         // PAIR consumer: its first ring reads (rows nb - 2 .. nb, finished by the producers 2 barriers
         // ago) precede the barrier after which the producers overwrite row nb - 2's slot with nb + 2
         if constexpr (RO == 2) pair_barrier();
-#endif
-#if OCN_STEP_ONEBLOCK
         // the two warm-up rows (D only), then rows nb .. ne with D and S in one basic block
         iteration<0, true, RO>(x, fb, q, L, n0, nb, ne);
         if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
@@ -2619,31 +2398,13 @@ struct MarchStep {
                 x.rotate();
             }
         }
-        if (OCN_STEP_NBAD_ACC && nbad && x.nbad_cnt != 0) atomicAdd(nbad, x.nbad_cnt);
-        if (OCN_DIAG_NOCHK == 2 && nbad && x.dacc < -5000) atomicAdd(nbad, 1);   // (never: keeps the checks)
-#else
-        if constexpr (kUnroll) {   // unrolled kRing times: iteration n runs in phase (n - n0) % kRing
-            for (int n = n0;; n += kRing) {
-                if (iteration<0>(x, fb, q, L, n, nb, ne)) break;
-                if (iteration<1>(x, fb, q, L, n + 1, nb, ne)) break;
-                if (iteration<2>(x, fb, q, L, n + 2, nb, ne)) break;
-                if (iteration<3>(x, fb, q, L, n + 3, nb, ne)) break;
-                if (iteration<4>(x, fb, q, L, n + 4, nb, ne)) break;
-            }
-        } else {
-            for (int n = n0;; ++n) {
-                if (iteration<0>(x, fb, q, L, n, nb, ne)) break;
-                x.rotate();
-            }
-        }
-#endif
     }
 
     // iteration n (phase PH): D(n+1), and S(n) from n = nb on; true after the last (n = ne).
-    // OCN_STEP_ONEBLOCK: WARM = a warm-up row (n < nb: D only); else D(n+1) and S(n) are one basic
-    // block (no branch between them: the scheduler interleaves S's work with D's division chains)
-    // and one wave-uniform test after both re-runs the two with IEEE divisions if any dividend of
-    // either was out of udiv's range (nothing is stored before: store_out follows)
+    // WARM = a warm-up row (n < nb: D only); else D(n+1) and S(n) are one basic block (no branch
+    // between them: the scheduler interleaves S's work with D's division chains), each followed by
+    // a wave-uniform test that re-runs it with IEEE divisions if any of its dividends was out of
+    // udiv's range (nothing is stored before: store_out follows)
     template <int PH, bool WARM = false, int RO = 0>
     __device__ __forceinline__ bool iteration(StepRegs &x, Fallback &fb, Batch &q, const Lane &L0, int n, int nb,
                                               int ne) const
@@ -2659,92 +2420,39 @@ struct MarchStep {
         take<PH>(x, q);
         Fallback fbn;
         if (n < ne) fallback<PH, RO>(x, fbn, L.m, n + 2, 3);   // consumed by the next iteration
-        if (n + kAhead - 1 < ne) load<RO>(x, q, L.m, n + kAhead);   // in flight while this row (and the next) is computed
+        if (n < ne) load<RO>(x, q, L.m, n + 1);   // in flight while this row is computed
         Out o;
-#if OCN_DIAG_NOCHK
-        {
-            int acc = 0;
-            double qb, qc;
-            bool bad = false;
-            derive<false, PH>(x, fb, acc, qb, qc);
-            if (!WARM) step<false, PH>(x, L, n, acc, bad, o);
-            x.dacc = min(x.dacc, acc);
-            x.qb = qb;
-            x.qc = qc;
-        }
-#elif OCN_STEP_ONEBLOCK
         {
             int acc = 0;
             double qb, qc;
             derive<false, PH>(x, fb, acc, qb, qc);
-#if !OCN_STEP_JOINT
             if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0))
                 derive<true, PH>(x, fb, acc, qb, qc);
             acc = 0;
-#endif
             if (WARM) {
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0))
-                    derive<true, PH>(x, fb, acc, qb, qc);
-#if OCN_STEP_FACE
                 if (n == nb - 1) face<PH>(x);
-#endif
             } else {
                 bool bad = false;
-#if OCN_STEP_SCHEDB >= 0
-                __builtin_amdgcn_sched_barrier(OCN_STEP_SCHEDB);   // what may move between D and S
-#endif
                 step<false, PH>(x, L, n, acc, bad, o);
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) {
-                    if (OCN_STEP_JOINT) derive<true, PH>(x, fb, acc, qb, qc);
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0))
                     step<true, PH>(x, L, n, acc, bad, o);
-                }
-#if OCN_STEP_FACE
                 x.fyx = o.fyx;
                 x.fyy = o.fyy;
                 x.vht = o.vht;
                 if (ZF) x.a2t = o.a2t;
-#endif
             }
             x.qb = qb;
             x.qc = qc;
         }
-#else
-        {   // D(n+1) with udiv; again with IEEE divisions if a dividend is out of its range
-            int acc = 0;
-            double qb, qc;
-            derive<false, PH>(x, fb, acc, qb, qc);
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) derive<true, PH>(x, fb, acc, qb, qc);
-            x.qb = qb;
-            x.qc = qc;
-        }
-        if (n >= nb) {   // wave-uniform
-            int acc = 0;
-            bool bad = false;
-            step<false, PH>(x, L, n, acc, bad, o);
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(acc < kUdivMinExp) != 0, 0)) step<true, PH>(x, L, n, acc, bad, o);
-        }
-#endif
-#if OCN_STEP_PAIR
-        if constexpr (RO == 1) {   // the producers' row goes into the ring, not to memory
+        if constexpr (RO == 1) {   // PAIR producer: the row goes into the ring, not to memory
             if (!WARM) pair_put<PH>(x, o, n);
             pair_barrier();
             ++x.rn;
             fb = fbn;
             return n >= ne;
         }
-#endif
-#if OCN_STEP_BUFST
-#if OCN_DIAG_NOSTORE   // (timing diagnostic only) the row's outputs summed, not stored
-        x.dsink += o.sshn + o.fx + o.un + o.fa + o.vn + o.fb;
-        if (n == ne && x.dsink == 1.2345e-300) store_out(o, geo(&b)(L.m, n).c);
-#else
         store_out(o, geo(&b)(L.m, n).c);   // warm-up rows: every lane dropped
-#endif
-        if (OCN_STEP_NBAD_ACC) x.nbad_cnt += o.dbad;
-#endif
-#if OCN_STEP_PAIR
         if constexpr (RO == 2) pair_barrier();
-#endif
         ++x.rn;
         fb = fbn;
         return n >= ne;
@@ -3075,7 +2783,6 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
                         double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
                         hipStream_t s, const OnepassKC &kc)
 {
-#if OCN_STEP_PAIR
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
         return set_error(OCN_ERR_ARG, "two-step launch: compact tables, march, full_free_surface = 1, trans_terms and "
@@ -3104,11 +2811,6 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
     if (p2) OCN_PAIR_LAUNCH(true, true, false);
     OCN_PAIR_LAUNCH(false, true, false);
 #undef OCN_PAIR_LAUNCH
-#else
-    (void)b; (void)ptr; (void)nptr; (void)cp; (void)sw; (void)tau; (void)nbad1; (void)nbad2; (void)sshp_out;
-    (void)up_out; (void)vp_out; (void)s; (void)kc;
-    return set_error(OCN_ERR_ARG, "two-step launch: not built (OCN_STEP_PAIR 0)");
-#endif
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy
@@ -3269,12 +2971,9 @@ int launch_rows_ext(const ocn_block *b, const float *rows, float *rows_x, const 
 
 using namespace ocn;
 
-// ocn_hh_init, ocn_uv_trans, ocn_uv_diff2, ocn_stress_components as register marches over the
-// arrays they are given (MarchHhInit2D, MarchUvTrans2D, MarchUvDiff2D, MarchStress2D); 0: one
-// thread per point like the other entries
-#ifndef OCN_ENTRY_MARCH
-#define OCN_ENTRY_MARCH 1
-#endif
+// ocn_hh_init, ocn_uv_trans, ocn_uv_diff2, ocn_stress_components run as register marches over the
+// arrays they are given (MarchHhInit2D, MarchUvTrans2D, MarchUvDiff2D, MarchStress2D); the other
+// entries one thread per point
 
 extern "C" {
 
@@ -3313,11 +3012,7 @@ int ocn_uv_trans(const ocn_block *b, const float *lcu, const float *lcv, const f
     (void)hq;
     CHECK(lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy);
     UvTrans<false> k{geo(b), lcu, lcv, luu, dxh, dyh, u, v, vort, hu, hv, hh, RHSx, RHSy};
-#if OCN_ENTRY_MARCH
     return launch_march(b, range_interior(b), MarchUvTrans2D{k}, (hipStream_t)stream);
-#else
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
-#endif
 }
 
 int ocn_stress_components(const ocn_block *b, const float *lu, const float *luu, const float *dx, const float *dy,
@@ -3327,11 +3022,7 @@ int ocn_stress_components(const ocn_block *b, const float *lu, const float *luu,
 {
     CHECK(lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s);
     StressComponents<false> k{geo(b), lu, luu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, u, v, str_t, str_s};
-#if OCN_ENTRY_MARCH
     return launch_march(b, range_interior(b), MarchStress2D{k}, (hipStream_t)stream);
-#else
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
-#endif
 }
 
 int ocn_uv_diff2(const ocn_block *b, const float *lcu, const float *lcv, const float *dx, const float *dy,
@@ -3342,11 +3033,7 @@ int ocn_uv_diff2(const ocn_block *b, const float *lcu, const float *lcv, const f
     (void)hu; (void)hv;
     CHECK(lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy);
     UvDiff2<false> k{geo(b), lcu, lcv, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb, mu, str_t, str_s, hq, hh, RHSx, RHSy};
-#if OCN_ENTRY_MARCH
     return launch_march(b, range_interior(b), MarchUvDiff2D{k}, (hipStream_t)stream);
-#else
-    return launch_range(b->nx_start, b->nx_end, b->ny_start, b->ny_end, k, (hipStream_t)stream, b->nx_start);
-#endif
 }
 
 int ocn_sw_update_uv(const ocn_block *b, double tau, const float *lcu, const float *lcv, const float *dxt,
@@ -3396,11 +3083,7 @@ int ocn_hh_init(const ocn_block *b, int32_t full_free_surface, const float *lu, 
     HhInit<false> k{geo(b), b->nx_start - 1, b->nx_end, b->ny_start - 1, b->ny_end, (double)full_free_surface, true,
              Interp<false>{lu, dx, dy, dxt, dyt, dxh, dyh, dxb, dyb}, llu, llv, luh,
              hq, hqp, hqn, hu, hup, hun, hv, hvp, hvn, hh, hhp, hhn, sh, shp, h_r};
-#if OCN_ENTRY_MARCH
     return launch_march(b, range_bnd(b), MarchHhInit2D{k, b->bnd_y2}, (hipStream_t)stream);
-#else
-    return launch_range(b->bnd_x1, b->bnd_x2, b->bnd_y1, b->bnd_y2, k, (hipStream_t)stream, b->nx_start);
-#endif
 }
 
 int ocn_tran_diff_fluxes(const ocn_block *b, const float *lcu, const float *lcv, const float *dxt, const float *dyt,
