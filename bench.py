@@ -63,6 +63,9 @@ LAUNCH_BYTES = {
     "onepass2_z": (98, 98), "onepass2_h": (114, 114),
     # general variant: h_r, mu and the forcing read by both roles (the consumers' state from LDS)
     "onepass2": (162, 162),
+    # the pending tail's last two steps in one launch, the second the call's last step (OCN_TIMER_ONEPASS2_LAST):
+    # + vort, str_t, str_s and the four RHS terms out
+    "onepass2_last_z": (154, 154), "onepass2_last_h": (170, 170), "onepass2_last": (218, 218),
     "copy3": (48, 48),   # end of a call with an odd number of one-pass steps: 3 fields copied back
     # tracer runs: CA also stores hh_init's hhq_p (read by tran_diff_tracer); per tracer and step:
     # tran_diff_fluxes (lcu, lcv, hhu, hhv, ff, ffp, ubrtr, vbrtr, mu in; flux_x, flux_y out),
@@ -156,9 +159,10 @@ def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one:
         out += call_launches(n, flip, rc, ring, one, tracers, zero=zero, lazy=lazy, pair=pair)
     if lazy and one:
         tail = TAIL_LAUNCHES
-        if pair:   # the steps left pending run as the last ones: 1 (the tail) or 2 (a single + the tail)
-            tail = TAIL_LAUNCHES if total % 2 else [("onepass", "onepass")] + TAIL_LAUNCHES
-        out += [(t, k + (_kc(zero) if t == "onepass" else "")) for t, k in tail]
+        if pair:   # the steps left pending run as the last ones: 1 (the tail) or 2 (one launch: the pair
+            # whose second step is the last, + a8's copies and hh_init)
+            tail = TAIL_LAUNCHES if total % 2 else [("onepass2_last", "onepass2_last")] + TAIL_LAUNCHES[1:]
+        out += [(t, k + (_kc(zero) if t.startswith("onepass") else "")) for t, k in tail]
     return out
 
 
@@ -461,7 +465,7 @@ def main():
     one = model.onepass_active
     one_zero = True if model.onepass_zero else "h" if model.onepass_hr else False
     # pair launches ran in the timed region: their timer counted them (graph replays: no timers)
-    pair = ("onepass2" in times) if times else model.pair_active
+    pair = ("onepass2" in times or "onepass2_last" in times) if times else model.pair_active
     model_overlap = model.overlap_level
     if world > 1:
         t = torch.tensor([dt], device="cuda")

@@ -385,10 +385,11 @@ enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,
- * then the one-pass steps. */
+ * then the one-pass steps: one step, two steps per launch, two steps the second of which is the
+ * call's last (the tail of an open sequence, ocn_ctx_complete). */
 enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_TIMER_TRACER,
        OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_TIMER_ONEPASS, OCN_TIMER_ONEPASS2,
-       OCN_NUM_TIMERS };
+       OCN_TIMER_ONEPASS2_LAST, OCN_NUM_TIMERS };
 
 /* Per-timer device time (ms, summed) and launch counts since the last call, from the HIP
  * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_TIMERS entries.  Synchronises. */

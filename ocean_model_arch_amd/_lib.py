@@ -66,7 +66,7 @@ STAGES = ["sw_update_ssh", "hh_update", "uv_trans_vort", "uv_trans", "stress_com
 STAGE_ID = {n: i for i, n in enumerate(STAGES)}
 TSTAGES = ["tran_diff_fluxes", "tran_diff_tracer", "tracer_next_step"]
 TSTAGE_ID = {n: i for i, n in enumerate(TSTAGES)}
-TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES + ["fused_ca", "onepass", "onepass2"]    # OCN_NUM_TIMERS slots
+TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES + ["fused_ca", "onepass", "onepass2", "onepass2_last"]    # OCN_NUM_TIMERS slots
 OPT_GRAPH = 1
 OPT_OVERLAP = 2
 OPT_STAGE_TIMING = 3

@@ -1625,6 +1625,29 @@ static int hybrid_tail(ocn_ctx *c, double tau, const StepKind &k, bool last)
 // both buffers of each pair end equal, as the reference leaves them), then hh_init with every
 // level (a10; a9's results on its range are rewritten by it).  Replaces CA + fused B + C1 +
 // hh_init of the standard last step.
+// what follows the last step's march (one block, no exchange; the roles swapped): a8's copies
+// (ssh := sshn, ubrtr := ubrtrn, vbrtr := vbrtrn, whole arrays: both buffers of each pair end equal,
+// as the reference leaves them) and hh_init with every level (a10, depth.f90:14-99)
+static int last_finish(ocn_ctx *c)
+{
+    hipStream_t s = c->stream;
+    ocn_ctx::Rec rec;
+    Compact t;
+    auto cp = [c](const LBlock &b, Compact &tt) -> const Compact * {
+        tt = Compact{b.bits, b.rows, c->march};
+        return &tt;
+    };
+    for (const LBlock &b : c->blocks)
+        for (const auto &pr : {std::make_pair(OCN_SSH, OCN_SSHN), std::make_pair(OCN_UBRTR, OCN_UBRTRN),
+                               std::make_pair(OCN_VBRTR, OCN_VBRTRN)})
+            HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr.second)], b.ptr[field_slot(pr.first)], field_bytes(b),
+                                  hipMemcpyDeviceToDevice, s));
+    RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
+    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_ALL, c->sw, true, s); }));
+    RC(timer_end(c, rec));
+    return OCN_OK;
+}
+
 static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
 {
     const ocn_sw_params &sw = c->sw;
@@ -1642,15 +1665,7 @@ static int one_step_last(ocn_ctx *c, double tau, const StepKind &k)
     RC(timer_end(c, rec));
     swap_alt3(c);
     swap_roles(c);
-    for (const LBlock &b : c->blocks)
-        for (const auto &pr : {std::make_pair(OCN_SSH, OCN_SSHN), std::make_pair(OCN_UBRTR, OCN_UBRTRN),
-                               std::make_pair(OCN_VBRTR, OCN_VBRTRN)})
-            HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr.second)], b.ptr[field_slot(pr.first)], field_bytes(b),
-                                  hipMemcpyDeviceToDevice, s));
-    RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_ALL, sw, true, s); }));
-    RC(timer_end(c, rec));
-    return OCN_OK;
+    return last_finish(c);
 }
 
 // ------------------------------------------------------------------ one-pass steps with one exchange
@@ -1795,22 +1810,25 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
 // state stays in LDS, the second's is written where a single step writes -- so the pair is one role
 // flip of the pairs and of the second buffers, as a single one-pass step is.  Single block, no
 // exchange, a variant chosen on the host (pair_ok); 98 B per cell for two steps in the known-constant
-// variant, 162 in the general one.
+// variant, 162 in the general one.  k.one_last: the second step is the call's last (the pending tail's
+// last two steps in one launch, complete_open): its consumer waves also store vort, the stresses and
+// the RHS terms (MarchStep PAIR + LAST), then last_finish -- in place of a single one-pass step + the
+// last step's own march.
 static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
 {
     ocn_ctx::Rec rec;
     hipStream_t s = c->stream;
-    RC(timer_begin(c, OCN_TIMER_ONEPASS2, rec));
+    RC(timer_begin(c, k.one_last ? OCN_TIMER_ONEPASS2_LAST : OCN_TIMER_ONEPASS2, rec));
     RC(each_block(c, s, [&](const LBlock &b) {
         const Compact t{b.bits, b.rows, c->march};
         return launch_onepass_pair(&b.g, b.ptr.data(), (int)b.ptr.size(), &t, c->sw, tau, k.check ? c->d_nbad : nullptr,
                                    k.check2 ? c->d_nbad : nullptr, (double *)b.sshp_alt, (double *)b.up_alt,
-                                   (double *)b.vp_alt, s, kc_of(c, b));
+                                   (double *)b.vp_alt, s, kc_of(c, b), k.one_last);
     }));
     RC(timer_end(c, rec));
     swap_alt3(c);
     swap_roles(c);
-    return OCN_OK;
+    return k.one_last ? last_finish(c) : OCN_OK;
 }
 
 // one_step_pair possible in this call: one block without exchanges or ring work, the compact tables
@@ -2703,6 +2721,13 @@ static int complete_open(ocn_ctx *c)
         const int d = c->deferred;
         c->deferred = 0;
         c->open_pair = false;
+        if (d == 2 && pair_ok(c)) {   // both in one launch, the second as the last step (pair + LAST)
+            StepKind k{};
+            k.last = k.one_last = k.pair = true;
+            k.check = c->deferred_check[0];
+            k.check2 = c->deferred_check[1];
+            return finish_call(c, one_step_fused(c, c->open_tau, k));
+        }
         if (d == 2) {
             StepKind k1{};
             k1.check = c->deferred_check[0];
@@ -2716,10 +2741,15 @@ static int complete_open(ocn_ctx *c)
     }
     swap_roles(c);
     swap_alt3(c);
-    if (c->open_pair) {   // the last launch was a pair (one flip, two steps): its first step again
-        c->open_pair = false;
+    if (c->open_pair) {   // the last launch was a pair (one flip, two steps): both again, from the state
+        c->open_pair = false;   // before it, the second as the last step (counted the first time: no checks)
+        if (pair_ok(c)) {
+            StepKind k{};
+            k.last = k.one_last = k.pair = true;
+            return finish_call(c, one_step_fused(c, c->open_tau, k));
+        }
         StepKind k1{};
-        k1.flip = k1.one = k1.next_one = k1.a_done = true;   // (counted the first time: no check)
+        k1.flip = k1.one = k1.next_one = k1.a_done = true;
         if (const int rc = run_step(c, c->open_tau, k1)) return finish_call(c, rc);
     }
     StepKind k{};

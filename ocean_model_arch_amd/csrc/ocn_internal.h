@@ -137,9 +137,11 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 // Two one-pass steps in one launch (sw_kernels.hip MarchStep PAIR): single block, no exchange,
 // a variant chosen on the host (kc.mode OCN_KC_KNOWN / OCN_KC_KNOWN_HR / OCN_KC_GENERAL); reads the state where a single step reads it and writes the second step's new state where
 // a single step writes (one role flip); nbad1 / nbad2: the steps' check_ssh_err counts (null: none)
+// last: the second step is the call's last step (MarchStep LAST: the consumers also store vort, the
+// stresses and the RHS terms the reference's last step leaves)
 int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                         double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
-                        hipStream_t s, const OnepassKC &kc);
+                        hipStream_t s, const OnepassKC &kc, bool last = false);
 // the known-constant precondition of launch_onepass over r (sw_kernels.hip FallbackCheck: the
 // fallback points and the forcing hold +0.0, h_r and mu are uniform): ORs 1 into *flag where it
 // does not hold; writes h_r and mu at (r.m0, r.n0) to kc[0], kc[1]

@@ -1860,7 +1860,7 @@ struct StepRegs {
 // exchanges of D deliver -- and the march covers the whole interior.
 template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR = false, bool PAIR = false>
 struct MarchStep {
-    static_assert(!PAIR || (!LAST && !X2), "two-step launches: no last step, no x2");
+    static_assert(!PAIR || !X2, "two-step launches: no x2");
     static constexpr bool kPair = PAIR;
     static constexpr int kPairCols = 116;   // PAIR: a workgroup's output columns (2 x 60 produced, less 2 each side)
     static constexpr bool kAligned = false;
@@ -2781,7 +2781,7 @@ static int pair_rows(const Range &r, int cols)
 
 int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                         double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
-                        hipStream_t s, const OnepassKC &kc)
+                        hipStream_t s, const OnepassKC &kc, bool last)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
@@ -2803,13 +2803,17 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
     g.ntiles = g.r[0].tiles;
     int ex;
     const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
-#define OCN_PAIR_LAUNCH(P, Z, H)                                                                                 \
-    return issue_march(g, MarchStep<P, false, Z, false, H, true>{*b, t, sw, tau, nbad1, sshp_out, up_out, vp_out,    \
-                                                                 kc.kc, nullptr, 0, 0u, nbad2}, s)
-    if (kc.mode == OCN_KC_GENERAL) { if (p2) OCN_PAIR_LAUNCH(true, false, false); OCN_PAIR_LAUNCH(false, false, false); }
-    if (kc.mode == OCN_KC_KNOWN_HR) { if (p2) OCN_PAIR_LAUNCH(true, true, true); OCN_PAIR_LAUNCH(false, true, true); }
-    if (p2) OCN_PAIR_LAUNCH(true, true, false);
-    OCN_PAIR_LAUNCH(false, true, false);
+#define OCN_PAIR_LAUNCH(P, L, Z, H)                                                                              \
+    return issue_march(g, MarchStep<P, L, Z, false, H, true>{*b, t, sw, tau, nbad1, sshp_out, up_out, vp_out,        \
+                                                             kc.kc, nullptr, 0, 0u, nbad2}, s)
+#define OCN_PAIR_VARIANT(L)                                                                                      \
+    if (kc.mode == OCN_KC_GENERAL) { if (p2) OCN_PAIR_LAUNCH(true, L, false, false); OCN_PAIR_LAUNCH(false, L, false, false); } \
+    if (kc.mode == OCN_KC_KNOWN_HR) { if (p2) OCN_PAIR_LAUNCH(true, L, true, true); OCN_PAIR_LAUNCH(false, L, true, true); }    \
+    if (p2) OCN_PAIR_LAUNCH(true, L, true, false);                                                                \
+    OCN_PAIR_LAUNCH(false, L, true, false)
+    if (last) { OCN_PAIR_VARIANT(true); }
+    OCN_PAIR_VARIANT(false);
+#undef OCN_PAIR_VARIANT
 #undef OCN_PAIR_LAUNCH
 }
 

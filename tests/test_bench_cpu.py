@@ -103,14 +103,14 @@ def test_hr_variant_bytes():
 @pytest.mark.parametrize("calls", [[1], [2], [3], [4], [100], [1] * 100, [1] * 7])
 def test_pair_region_launches(calls):
     """Two one-pass steps per launch in an open sequence (OCN_OPT_PAIR, ocn_ctx.hip step_impl):
-    pairs across calls while 3 or more steps are pending; the last 1 or 2 are run by the tail (a
-    single and the last step, or the last step) -- no step runs twice."""
+    pairs across calls while 3 or more steps are pending; the last 1 or 2 are run by the tail (one
+    launch whose second step is the last, or the last step) -- no step runs twice."""
     steps = sum(calls)
     one = bench.region_launches(calls, flip=True, one=True, zero=True, lazy=True, pair=True)
     kinds = [k for _, k in one]
     p = (steps - 1) // 2
     assert kinds[:p] == ["onepass2_z"] * p
-    tail = ["onepass_last_z", "copy3", "c2_full"]
-    assert kinds[p:] == (tail if steps % 2 else ["onepass_z"] + tail)
+    tail = ["copy3", "c2_full"]
+    assert kinds[p:] == (["onepass_last_z"] + tail if steps % 2 else ["onepass2_last_z"] + tail)
     non_lazy = [k for _, k in bench.call_launches(20, flip=True, one=True, zero=True, pair=True)]
     assert non_lazy[:10] == ["onepass2_z"] * 9 + ["onepass_z"] and non_lazy[10] == "onepass_last_z"

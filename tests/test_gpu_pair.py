@@ -211,6 +211,34 @@ def test_pair_one_step_calls(amd, name):
     assert any(used), "no pair launch"
 
 
+@pytest.mark.parametrize("how", ["deferred", "redo"])
+@pytest.mark.parametrize("name", ["box1024_b1x1_s10", "bs_b1x1_s60"])
+def test_pair_last_tail(amd, name, how):
+    """The pending tail's last two steps as ONE launch, the second as the call's last step (MarchStep
+    PAIR + LAST: the consumer waves also store vort, the stresses and the RHS terms), then a8's copies
+    and hh_init -- "deferred": the two steps a call left pending run that way when the fields are read;
+    "redo": synchronize() ran them as a pair, so the read re-runs that pair from the state before it as
+    the pair + LAST launch.  Bitwise against the reference; the timer shows the launch."""
+    case = cases.load_e2e(name)
+    m = build_model(amd, case).set_pair(2).init()
+    steps = case["steps"]
+    try:
+        m.step(2, tau=1.0, check_every=1)
+        m.synchronize()                       # the verdict reaches the host
+        m.set_stage_timing(True)
+        m.stage_times()
+        m.step(steps - 2, tau=1.0, check_every=1)   # an even count: pairs, the last two pending
+        if how == "redo":
+            m.synchronize()                   # runs the two pending steps as a plain pair
+        bad = compare_case(m, case, name)     # reads: the tail forms
+        times = m.stage_times()
+    finally:
+        m.close()
+    assert not bad, f"{name} ({how}): fields differ from the reference: {bad}"
+    assert times.get("onepass2_last", (0, 0))[1] == 1, times
+    assert "onepass" not in times, times      # no single one-pass launch in the tail
+
+
 def _ops_run(amd, pair, ops):
     """One context driven through `ops` -- ("step", n, tau) / ("sync",) / ("read", field) /
     ("bump", field): a download, a small change, an upload -- then every field of every block."""
