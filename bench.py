@@ -147,10 +147,17 @@ TAIL_LAUNCHES = [("onepass", "onepass_last"), ("copy", "copy3"), ("hh_init", "c2
 
 
 def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
-                    tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False):
+                    tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False,
+                    multi: bool = False):
     """The launches of a timed region: ocn_ctx_step calls of calls[i] steps each, then (lazy) the
-    pending tail formed by ocn_ctx_complete."""
+    pending tail formed by ocn_ctx_complete.  multi: each call of an open sequence as one cooperative
+    launch of its steps (OCN_OPT_MULTI; kind "<one-pass kind>*n" = n steps' bytes in one launch)."""
     out, total = [], sum(calls)
+    if lazy and one and multi and not pair:
+        z = _kc(zero)
+        for n in calls:
+            out += [("onepass_multi", f"onepass{z}*{n}")] if n >= 2 else [("onepass", "onepass" + z)]
+        return out + [(t, k + (z if t == "onepass" else "")) for t, k in TAIL_LAUNCHES]
     if lazy and one and pair:   # an open sequence with pairs: two steps per launch across calls while
         # 3 or more are pending; the last 1 or 2 run by ocn_ctx_complete
         out += [("onepass2", "onepass2" + _kc(zero))] * ((total - 1) // 2)
@@ -166,23 +173,31 @@ def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one:
     return out
 
 
+def _bytes(kind: str, i: int) -> int:
+    """LAUNCH_BYTES of a launch kind; "<kind>*n": n launches' bytes in one (a multi-step launch)."""
+    base, _, n = kind.partition("*")
+    return LAUNCH_BYTES[base][i] * (int(n) if n else 1)
+
+
 def fused_bytes(compact: bool, calls, flip: bool = False, rc: bool = True, ring: bool = False,
-                one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False):
+                one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False,
+                multi: bool = False):
     """Mean bytes per interior cell per launch of each timer over the timed region's calls."""
     i = 0 if compact else 1
     tot, cnt = {}, {}
-    for timer, kind in region_launches(calls, flip, rc, ring, one, tracers, zero, lazy, pair):
-        tot[timer] = tot.get(timer, 0) + LAUNCH_BYTES[kind][i]
+    for timer, kind in region_launches(calls, flip, rc, ring, one, tracers, zero, lazy, pair, multi):
+        tot[timer] = tot.get(timer, 0) + _bytes(kind, i)
         cnt[timer] = cnt.get(timer, 0) + (kind != "hqp")   # "hqp": bytes of the launch before it
     return {t: tot[t] / cnt[t] for t in tot}
 
 
 def step_bytes(compact: bool, calls, flip: bool = False, rc: bool = True, ring: bool = False,
-               one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False):
+               one: bool = False, tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False,
+               multi: bool = False):
     """Bytes per interior cell per step moved by the timed region's calls."""
     i = 0 if compact else 1
-    return sum(LAUNCH_BYTES[kind][i] for _, kind in region_launches(calls, flip, rc, ring, one, tracers, zero,
-                                                                    lazy, pair)) / sum(calls)
+    return sum(_bytes(kind, i) for _, kind in region_launches(calls, flip, rc, ring, one, tracers, zero,
+                                                              lazy, pair, multi)) / sum(calls)
 
 
 def dims_create(n: int):
@@ -361,6 +376,8 @@ def main():
     ap.add_argument("--pair", type=int, default=1, choices=[0, 1, 2],
                     help="two one-pass steps per launch (OCN_OPT_PAIR): 1 = known-constant variants on blocks >= 512^2 "
                          "(default), 2 = always (the general variant too), 0 = never")
+    ap.add_argument("--no-multi", action="store_true",
+                    help="small single blocks: one launch per step (no cooperative multi-step launch, OCN_OPT_MULTI)")
     ap.add_argument("--no-batch", action="store_true",
                     help="several blocks on a GPU: one launch per block and launch group (no block batching)")
     ap.add_argument("--blocks", default=None,
@@ -431,6 +448,7 @@ def main():
     model.set_lazy_tail(not args.no_lazy_tail)
     model.set_batch(not args.no_batch)
     model.set_pair(args.pair)
+    model.set_multi(not args.no_multi)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -466,6 +484,7 @@ def main():
     one_zero = True if model.onepass_zero else "h" if model.onepass_hr else False
     # pair launches ran in the timed region: their timer counted them (graph replays: no timers)
     pair = ("onepass2" in times or "onepass2_last" in times) if times else model.pair_active
+    multi = ("onepass_multi" in times) if times else model.multi_active
     model_overlap = model.overlap_level
     if world > 1:
         t = torch.tensor([dt], device="cuda")
@@ -481,9 +500,9 @@ def main():
         ntr = sw.tracer_num if sw.use_tracers > 0 else 0
         stage_tab = STAGE_BYTES_COMPACT if compact else STAGE_BYTES
         kbytes = stage_tab if args.stages else fused_bytes(compact, calls, flip, rc, ring, one, ntr, one_zero, lazy,
-                                                           pair)
+                                                           pair, multi)
         b_path = sum(stage_tab.values()) if args.stages else step_bytes(compact, calls, flip, rc, ring, one, ntr,
-                                                                          one_zero, lazy, pair)
+                                                                          one_zero, lazy, pair, multi)
         stage_ms = {s: ms / cnt for s, (ms, cnt) in times.items() if s in kbytes}
         roof = None
         if stage_ms:   # the dominant kernel: the most device time over the timed steps
@@ -518,6 +537,8 @@ def main():
                                              if one else None,
                           "onepass_pairs": ("two one-pass steps per launch (OCN_OPT_PAIR): the first step's "
                                             "new state kept on chip") if pair else False,
+                          "multi_step_launch": ("a call's steps in one cooperative launch, a grid barrier between "
+                                                "steps (OCN_OPT_MULTI)") if multi else False,
                           "steps_per_call": spc, "calls": len(calls),
                           "call_tail": ("pending between calls (OCN_OPT_LAZY_TAIL), formed once by ocn_ctx_complete "
                                         "inside the timed region") if lazy else "formed by every call",
@@ -527,6 +548,7 @@ def main():
                           "parallelism": (f"block-decomposition {bx}x{by}, RCCL halos" if world > 1 else
                                           "1 block" if bx * by == 1 else f"{bx}x{by} blocks, local halo copies")},
                "build_id": amd.build_id(),
+               **({"pair_rows_override": os.environ["OCN_PAIR_ROWS"]} if os.environ.get("OCN_PAIR_ROWS") else {}),
                "roofline": roof,
                # whole-step rates (not the roofline, which is `roofline`: the dominant kernel's bytes
                # over its own time): the bytes this path moves per step, and -- for comparison with

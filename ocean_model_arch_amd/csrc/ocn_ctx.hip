@@ -231,16 +231,18 @@ namespace ocn {
 // first of a sequence (the reference's second halo ring of the state is saved first); x2_end = a
 // last step after such a sequence (that ring restored and the state's first ring exchanged first).
 // pair = this one-pass step and the next as one launch (one_step_pair), check2 = the next one's check.
+// multi = this many one-pass steps in one cooperative launch (one_step_multi), each checked if check.
 struct StepKind {
     bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next, one, next_one, one_last;
     bool x2, x2_save, x2_end;
     bool pair = false, check2 = false;
+    int multi = 0;
     bool operator==(const StepKind &o) const
     {
         return check == o.check && first == o.first && last == o.last && flip == o.flip && a_done == o.a_done &&
                next_a == o.next_a && next_reuse == o.next_reuse && rc == o.rc && rc_next == o.rc_next &&
                one == o.one && next_one == o.next_one && one_last == o.one_last && x2 == o.x2 &&
-               x2_save == o.x2_save && x2_end == o.x2_end && pair == o.pair && check2 == o.check2;
+               x2_save == o.x2_save && x2_end == o.x2_end && pair == o.pair && check2 == o.check2 && multi == o.multi;
     }
 };
 
@@ -313,6 +315,9 @@ struct ocn_ctx {
     // kPairMinCells interior points, 2 on any block; pair_used: a call ran one
     int pair = 1;
     bool pair_used = false;
+    // OCN_OPT_MULTI: the one-pass steps of a small single block as one cooperative launch per call
+    // (one_step_multi); multi_used: the last call ran one
+    bool multi = true, multi_used = false;
     bool known_const = true;   // OCN_OPT_KNOWN_CONSTANTS: the one-pass step's known-constant variant
     bool last_hybrid = true;   // OCN_OPT_ONEPASS_LAST: one-pass last steps with exchanges / ring work too
     bool one_used = false;
@@ -593,7 +598,8 @@ static int allocate(ocn_ctx *c)
     }
     // d_nbad words: 0 check_ssh_err's count, 16 the fallback check's verdict (d_fbz), 32..47 flags and
     // the vote (d_flags), 48..55 the loopback vote's reduction, 56 the count's maximum over the ranks
-    // (sync_impl); then per block h_r, mu (LBlock::kc)
+    // (sync_impl), 60 the multi-step launch's barrier counter, 61 its timeout flag; then per block h_r,
+    // mu (LBlock::kc)
     const size_t kcb = 16 * c->blocks.size();
     HIPCHK(hipMalloc(&c->d_nbad, 256 + kcb));
     c->allocs.push_back(c->d_nbad);
@@ -1831,6 +1837,28 @@ static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
     return k.one_last ? last_finish(c) : OCN_OK;
 }
 
+// Several one-pass steps as one cooperative launch (sw_kernels.hip k_march_multi: a grid barrier
+// between the steps; the block's tiles resident together): single small block, no exchange, a
+// variant chosen on the host (multi_ok).  Step parity alternates the buffers as the role flips of
+// single launches do, so the host flips the roles k.multi times.
+static int one_step_multi(ocn_ctx *c, double tau, const StepKind &k)
+{
+    ocn_ctx::Rec rec;
+    hipStream_t s = c->stream;
+    const LBlock &b = c->blocks[0];
+    const Compact t{b.bits, b.rows, c->march};
+    RC(timer_begin(c, OCN_TIMER_ONEPASS_MULTI, rec));
+    RC(launch_onepass_multi(&b.g, b.ptr.data(), (int)b.ptr.size(), &t, c->sw, tau, k.multi, k.check ? c->d_nbad : nullptr,
+                            (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, (unsigned *)(c->d_nbad + 60),
+                            c->d_nbad + 61, s, kc_of(c, b)));
+    RC(timer_end(c, rec));
+    if (k.multi & 1) {
+        swap_alt3(c);
+        swap_roles(c);
+    }
+    return OCN_OK;
+}
+
 // one_step_pair possible in this call: one block without exchanges or ring work, the compact tables
 // and the march, the one-pass variant chosen by the host (kc_mode not OCN_KC_DEVICE; OCN_OPT_PAIR 1:
 // a known-constant one on blocks of 512^2 or more, 2: any)
@@ -1850,8 +1878,19 @@ static bool pair_ok(ocn_ctx *c)
     return (long)(g.nx_end - g.nx_start + 1) * (g.ny_end - g.ny_start + 1) >= OCN_PAIR_MIN_CELLS;
 }
 
+// one_step_multi possible in this call (an open sequence, pairs not used): one block without exchanges or
+// ring work, the compact tables and the march, the variant chosen on the host, every step checked or
+// none, and a block small enough that its grid is resident at once -- the launch-latency-bound case
+static bool multi_ok(ocn_ctx *c, int32_t check_every)
+{
+    return c->multi && c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) && !c->ring_sea && c->compact &&
+           c->march && c->kc_mode != OCN_KC_DEVICE && (check_every == 0 || check_every == 1) &&
+           onepass_multi_fits(&c->blocks[0].g);
+}
+
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
+    if (k.multi) return one_step_multi(c, tau, k);
     if (k.pair) return one_step_pair(c, tau, k);
     if (k.x2) return one_step_x2(c, tau, k);
     if (k.one_last && k.x2_end) RC(x2_end(c, c->stream));
@@ -2767,6 +2806,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     if (nsteps == 0) return OCN_OK;
     const bool graph_ok = c->use_graph && !has_comm(c) && !c->stage_timing;   // RCCL / events stay outside graphs
     c->pair_used = false;
+    c->multi_used = false;
     if (c->open) {
         if (tau == c->open_tau && c->onepass && lazy_allowed(c, c->open_x2)) {
             // the open sequence goes on: every step of this call is a one-pass step (the state and
@@ -2802,13 +2842,23 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
                     rc = run_step(c, tau, k);
                 }
                 c->deferred = 0;
-                for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
-                    StepKind k{};
-                    k.check = check_every > 0 && (s % check_every == 0);
+                if (!c->open_x2 && !graph_ok && nsteps >= 2 && rc == OCN_OK && multi_ok(c, check_every)) {
+                    StepKind k{};   // all the call's steps in one cooperative launch
+                    k.check = check_every == 1;
                     k.flip = k.one = k.next_one = k.a_done = true;
-                    k.x2 = c->open_x2;
-                    rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
+                    k.multi = nsteps;
+                    rc = run_step(c, tau, k);
                     c->open_pair = false;
+                    c->multi_used = true;
+                } else {
+                    for (int s = 1; s <= nsteps && rc == OCN_OK; ++s) {
+                        StepKind k{};
+                        k.check = check_every > 0 && (s % check_every == 0);
+                        k.flip = k.one = k.next_one = k.a_done = true;
+                        k.x2 = c->open_x2;
+                        rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
+                        c->open_pair = false;
+                    }
                 }
             }
             if (rc) { c->open = false; c->deferred = 0; c->open_pair = false; return finish_call(c, rc); }
@@ -2977,8 +3027,10 @@ static int sync_impl(ocn_ctx *c)
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     learn_fb(c);
-    int32_t nbad = 0;
+    int32_t nbad = 0, berr = 0;
     HIPCHK(hipMemcpy(&nbad, cnt, sizeof(nbad), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&berr, c->d_nbad + 61, sizeof(berr), hipMemcpyDeviceToHost));
+    if (berr) return set_error(OCN_ERR_HIP, "multi-step launch: a grid barrier timed out (results invalid)");
     if (nbad) return set_error(OCN_ERR_BLOWUP, "SIGFPRE predict error: |ssh| >= 1e4 on " + std::to_string(nbad) +
                                                    (has_comm(c) ? " sea points of a block (the most of any rank;"
                                                                   " check_ssh_err_kernel)"
@@ -3107,6 +3159,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     case OCN_OPT_LAZY_TAIL: c->lazy = value != 0; return OCN_OK;
     case OCN_OPT_X2: c->x2 = value != 0; c->coherent_known = false; return OCN_OK;
     case OCN_OPT_PAIR: c->pair = value < 0 ? 0 : value > 2 ? 2 : (int)value; return OCN_OK;
+    case OCN_OPT_MULTI: c->multi = value != 0; return OCN_OK;
     case OCN_OPT_BATCH:
         if (c->batch != (value != 0)) drop_graphs(c);
         c->batch = value != 0;
@@ -3146,6 +3199,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_X2: *value = c->x2 && c->x2_used; return OCN_OK;
     case OCN_OPT_BATCH: *value = c->batch; return OCN_OK;
     case OCN_OPT_PAIR: *value = c->pair_used ? 2 : c->pair > 0; return OCN_OK;
+    case OCN_OPT_MULTI: *value = c->multi_used ? 2 : c->multi; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

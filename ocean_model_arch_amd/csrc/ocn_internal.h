@@ -142,6 +142,15 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                         double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
                         hipStream_t s, const OnepassKC &kc, bool last = false);
+// nsteps one-pass steps in one cooperative launch (sw_kernels.hip k_march_multi): single small block,
+// no exchange, a variant chosen on the host; step 1 reads the table's buffers, each step the buffers
+// the previous one wrote (the role pairs and sshp / ubrtrp / vbrtrp against *_alt, alternating);
+// ctr: a device word for the grid barrier (zeroed on the stream first); err: ORed 1 if a barrier
+// timed out.  onepass_multi_fits: the block's grid is small enough for one resident launch.
+int onepass_multi_fits(const ocn_block *b);
+int launch_onepass_multi(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                         double tau, int nsteps, int32_t *nbad, double *sshp_alt, double *up_alt, double *vp_alt,
+                         unsigned *ctr, int32_t *err, hipStream_t s, const OnepassKC &kc);
 // the known-constant precondition of launch_onepass over r (sw_kernels.hip FallbackCheck: the
 // fallback points and the forcing hold +0.0, h_r and mu are uniform): ORs 1 into *flag where it
 // does not hold; writes h_r and mu at (r.m0, r.n0) to kc[0], kc[1]

@@ -432,7 +432,7 @@ template <class B> struct HasPair<B, std::void_t<decltype(B::kPair)>> { static c
 template <class B, class = void> struct HasGate { static constexpr bool v = false; };
 template <class B> struct HasGate<B, std::void_t<decltype(B::kGate)>> { static constexpr bool v = B::kGate; };
 
-template <class Body> __device__ __forceinline__ void march_tile(const MarchRect &R, int tile, const Body &body);
+template <class Body, bool PRO = true> __device__ __forceinline__ void march_tile(const MarchRect &R, int tile, const Body &body);
 
 template <class Body>
 __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Body body)
@@ -520,7 +520,8 @@ template <class Body> static int issue_march(const MarchGrid &g, const Body &bod
     return check_launch();
 }
 
-template <class Body> __device__ __forceinline__ void march_tile(const MarchRect &R, int tile, const Body &body)
+// PRO = false: the body's workgroup prologue has run already (k_march_multi: once for all its steps)
+template <class Body, bool PRO> __device__ __forceinline__ void march_tile(const MarchRect &R, int tile, const Body &body)
 {
     const int tx = tile % R.ntx, ty = tile / R.ntx;
     const int lane = (int)threadIdx.x & 63;
@@ -528,7 +529,7 @@ template <class Body> __device__ __forceinline__ void march_tile(const MarchRect
     constexpr int cols = Body::kAligned ? 64 : 64 - 2 * Body::kHalo;
     const int mw = R.w0 + (R.vert ? tx : tx * 4 + wave) * cols;   // first output column of this wave
     const int nb = R.n0 + (R.vert ? ty * 4 + wave : ty) * R.rows, ne = min(R.n1, nb + R.rows - 1);
-    if constexpr (HasPrologue<Body>::v) body.prologue(R, ty);     // all 4 waves (a barrier)
+    if constexpr (PRO && HasPrologue<Body>::v) body.prologue(R, ty);   // all 4 waves (a barrier)
     if constexpr (HasPair<Body>::v) {
         // two steps in one launch (MarchStep PAIR): 4 waves side by side, waves 0 / 1 produce the
         // first step on columns [c0 - 2, c0 + 118) (60 each, into LDS), waves 2 / 3 the second on
@@ -2755,6 +2756,117 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 #undef OCN_STEP_VARIANT
 #undef OCN_STEP_LAUNCH
     return OCN_OK;
+}
+
+// ------------------------------------------------------------------ several steps per launch
+// Small single blocks (the Black Sea basin's 285 x 159: a one-pass launch of a few microseconds) are
+// launch-latency bound: the host's enqueue and the gap between dependent launches cost more than the
+// march.  k_march_multi runs nsteps one-pass steps in ONE cooperative launch: every workgroup keeps
+// its tile through the steps (its row constants formed once), and a grid-wide barrier separates the
+// steps (each step reads at +-2 points what the previous one wrote).  Step s runs body b[s & 1]: the
+// two bodies differ only in the buffers of the role pairs and the second buffers, swapped, as the
+// host's role flips between single launches swap them.  The barrier: every wave's stores done
+// (__syncthreads), the XCD's L2 written back (agent-scope release fence), a device-scope counter
+// incremented; then the counter awaited with a bounded spin -- a workgroup that waits ~0.5 s ORs 1
+// into *err and ends (every wave reaches an exit: no hang; the host reports OCN_ERR_HIP) -- and the
+// caches invalidated (acquire) before the next step's loads.  All workgroups are resident together
+// (hipLaunchCooperativeKernel refuses a grid that is not).
+__device__ __forceinline__ bool grid_barrier(unsigned *ctr, unsigned target, int32_t *err)
+{
+    __shared__ int ok_s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int n = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++n < (1 << 20))
+            __builtin_amdgcn_s_sleep(1);
+        const bool ok = n < (1 << 20);
+        if (!ok) atomicOr(err, 1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        ok_s = ok;
+    }
+    __syncthreads();
+    return ok_s != 0;
+}
+
+template <class Body>
+__global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march_multi(MarchGrid g, Body b0, Body b1, int nsteps,
+                                                                       unsigned *ctr, int32_t *err)
+{
+    const MarchRect &R = g.r[0];
+    const int tile = (int)blockIdx.x;   // one tile per workgroup (gridDim.x = R.tiles)
+    if constexpr (HasPrologue<Body>::v) b0.prologue(R, tile / R.ntx);   // the same rows every step
+    for (int s = 0; s < nsteps; ++s) {
+        if (s & 1) march_tile<Body, false>(R, tile, b1);
+        else march_tile<Body, false>(R, tile, b0);
+        if (s + 1 < nsteps && !grid_barrier(ctr, (unsigned)(s + 1) * gridDim.x, err)) return;
+    }
+}
+
+// rows per wave tile of a multi-step launch: the shortest tile whose grid (4 vertically stacked
+// waves per workgroup) stays within kMultiMaxTiles workgroups, or 0 if none up to 16 rows does
+static constexpr int kMultiMaxTiles = 256;   // one workgroup per CU: resident with room to spare
+static int multi_rows(const Range &r)
+{
+    const long wx = (r.m1 - r.m0 + 60) / 60, h = r.n1 - r.n0 + 1;
+    for (int rows = 1; rows <= 16; ++rows)
+        if (wx * ((h + 4 * rows - 1) / (4 * rows)) <= kMultiMaxTiles) return rows;
+    return 0;
+}
+
+int onepass_multi_fits(const ocn_block *b) { return multi_rows(range_interior(b)) > 0; }
+
+int launch_onepass_multi(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                         double tau, int nsteps, int32_t *nbad, double *sshp_alt, double *up_alt, double *vp_alt,
+                         unsigned *ctr, int32_t *err, hipStream_t s, const OnepassKC &kc)
+{
+    if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_alt ||
+        !up_alt || !vp_alt || !ctr || !err || nsteps < 1)
+        return set_error(OCN_ERR_ARG, "multi-step launch: compact tables, march, full_free_surface = 1, trans_terms "
+                                      "and ksw_lat on, three second buffers, barrier words");
+    if (kc.mode == OCN_KC_DEVICE || (kc.mode != OCN_KC_GENERAL && !kc.kc))
+        return set_error(OCN_ERR_ARG, "multi-step launch: a variant chosen on the host");
+    RC_K(check_block(b));
+    const Range r = range_interior(b);
+    if (range_empty(r)) return OCN_OK;
+    const int rows = multi_rows(r);
+    if (!rows) return set_error(OCN_ERR_ARG, "multi-step launch: block too large for one resident grid");
+    // the odd steps' table: the role pairs and the second buffers swapped (ocn_ctx.hip swap_roles / swap_alt3)
+    std::vector<void *> odd(ptr, ptr + nptr);
+    for (const auto &pr : {std::make_pair(OCN_SSH, OCN_SSHN), std::make_pair(OCN_UBRTR, OCN_UBRTRN),
+                           std::make_pair(OCN_VBRTR, OCN_VBRTRN)})
+        std::swap(odd[ocn_field_slot(pr.first)], odd[ocn_field_slot(pr.second)]);
+    double *alt[3] = {sshp_alt, up_alt, vp_alt};
+    const int ids[3] = {OCN_SSHP, OCN_UBRTRP, OCN_VBRTRP};
+    for (int i = 0; i < 3; ++i) std::swap(odd[ocn_field_slot(ids[i])], *(void **)&alt[i]);
+    const Tab<true> t0 = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0);
+    const Tab<true> t1 = make_tab<true>(odd.data(), nptr, cp->bits, cp->rows, block_rows(b), 0);
+    MarchGrid g{};
+    g.r[0] = MarchRect{};
+    int ex;
+    const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
+    if (batching(s)) return batch_violation();   // (a cooperative launch is not batched)
+    RC_K(check_hip(hipMemsetAsync(ctr, 0, sizeof(unsigned), s), "multi-step launch: barrier word"));
+    auto go = [&](auto k0, auto k1) -> int {
+        using Body = decltype(k0);
+        g.r[0] = march_rect<Body>(b, r, rows, true);
+        g.nr = 1;
+        g.ntiles = g.r[0].tiles;
+        void *args[] = {&g, &k0, &k1, &nsteps, &ctr, &err};
+        count_launch();
+        return check_hip(hipLaunchCooperativeKernel((const void *)k_march_multi<Body>, dim3((unsigned)g.ntiles),
+                                                    dim3(256), args, 0, s),
+                         "multi-step launch (cooperative)");
+    };
+#define OCN_MULTI(P, Z, H)                                                                                       \
+    return go(MarchStep<P, false, Z, false, H>{*b, t0, sw, tau, nbad, sshp_alt, up_alt, vp_alt, kc.kc, nullptr, 0, 0u}, \
+              MarchStep<P, false, Z, false, H>{*b, t1, sw, tau, nbad, alt[0], alt[1], alt[2], kc.kc, nullptr, 0, 0u})
+    if (kc.mode == OCN_KC_GENERAL) { if (p2) OCN_MULTI(true, false, false); OCN_MULTI(false, false, false); }
+    if (kc.mode == OCN_KC_KNOWN_HR) { if (p2) OCN_MULTI(true, true, true); OCN_MULTI(false, true, true); }
+    if (p2) OCN_MULTI(true, true, false);
+    OCN_MULTI(false, true, false);
+#undef OCN_MULTI
 }
 
 // Rows per workgroup tile of the two-step launch: the fewest iterations in total, counting

@@ -224,12 +224,23 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_BATCH, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_multi(self, on: bool = True):
+        """Small single blocks: the steps of a call (in an open sequence) as one cooperative launch
+        with a grid-wide barrier between them (default on); same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MULTI, int(on)), "ocn_ctx_set_option")
+        return self
+
     def set_pair(self, mode: int = 1):
         """Two one-pass steps per launch (default 1: the known-constant variants on single blocks of
         at least 512 x 512 interior points; 2: any variant, any block; 0: never): the first step's
         new state stays on chip; same results bit for bit."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_PAIR, int(mode)), "ocn_ctx_set_option")
         return self
+
+    @property
+    def multi_active(self) -> bool:
+        """Whether the last step() ran its steps as one cooperative multi-step launch."""
+        return self.option(_lib.OPT_MULTI) == 2
 
     @property
     def pair_active(self) -> bool:

@@ -1,0 +1,105 @@
+"""GPU parity of the multi-step launch (OCN_OPT_MULTI, sw_kernels.hip k_march_multi): the one-pass
+steps of a call of a small single block -- the Black Sea basin as one block, config 1 on the GPU --
+in ONE cooperative launch with a grid-wide barrier between the steps, bitwise against the reference
+fixtures (model.f90:135-160 runs expl_shallow_water once per step; the launch runs the same steps).
+
+A multi-step launch needs an open sequence (OCN_OPT_LAZY_TAIL: the call continues a one-pass sequence)
+and the variant chosen on the host, so the runs below make a first short call and a synchronize()
+first.  Tolerance: none (fp64, the reference's order).
+"""
+import pytest
+
+from tests.golden import cases
+from tests.test_gpu_parity import OracleTwin, build_model, compare_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def amd():
+    import ocean_model_arch_amd as amd
+    amd.lib()
+    return amd
+
+
+def _run(amd, name, calls, multi=True, timing=False):
+    case = cases.load_e2e(name)
+    m = build_model(amd, case).set_multi(multi).init()
+    used, times = [], {}
+    try:
+        m.step(calls[0], tau=1.0, check_every=1)
+        m.synchronize()   # the known-constant verdict reaches the host
+        if timing:
+            m.set_stage_timing(True)
+            m.stage_times()
+        for n in calls[1:]:
+            m.step(n, tau=1.0, check_every=1)
+            used.append(m.multi_active)
+        if timing:
+            times = m.stage_times()
+        bad = compare_case(m, case, name)
+    finally:
+        m.close()
+    return bad, used, times
+
+
+@pytest.mark.parametrize("name,calls", [("bs_b1x1_s60", [2, 58]), ("bs_b1x1_s60", [1, 7, 1, 2, 49]),
+                                        ("bs_b1x1_s604", [4, 300, 300]), ("box70x54_b1x1_s20", [3, 17]),
+                                        ("box48x40_cart_s10", [2, 3, 5]), ("box70x54_topo_b1x1_s20", [2, 18])])
+def test_multi_steps_match_reference(amd, name, calls):
+    bad, used, times = _run(amd, name, calls, timing=True)
+    assert not bad, f"{name} {calls}: fields differ from the reference: {bad}"
+    assert used == [n >= 2 for n in calls[1:]], used
+    assert times.get("onepass_multi", (0, 0))[1] == sum(n >= 2 for n in calls[1:]), times
+
+
+def test_multi_off_is_per_step(amd):
+    bad, used, times = _run(amd, "bs_b1x1_s60", [2, 58], multi=False, timing=True)
+    assert not bad and used == [False] and "onepass_multi" not in times, (bad, used, times)
+
+
+def test_multi_counts_blowup_like_single_launches(amd):
+    """check_ssh_err_kernel (vel_ssh.f90:40-67) inside the multi-step launch: every step counts its
+    points, as single launches do -- the same error message (count) either way."""
+    msgs = []
+    for multi in (True, False):
+        m = amd.OceanModel(amd.box_config(100)).set_multi(multi).init()
+        m.step(2, check_every=1).synchronize()
+        s = m.download(0, "ssh")
+        s[30:60, 40:70] = 2.0e4
+        for nm in ("ssh", "sshn", "sshp"):
+            m.upload(0, nm, s)
+        m.step(3, check_every=0).synchronize()   # the re-check's verdict reaches the host
+        with pytest.raises(amd.OcnError) as e:
+            m.step(4, check_every=1).synchronize()
+        used = m.multi_active
+        msgs.append(str(e.value))
+        m.close()
+        assert used == multi
+    assert msgs[0] == msgs[1], msgs
+
+
+def test_multi_with_uploads_and_forcing_matches_oracle(amd):
+    """The multi-step launch in its general variant (a forcing on the sea: RHSx read) and across an
+    upload between calls, against the oracle given the same uploads."""
+    import numpy as np
+    n = 120
+    m = amd.OceanModel(amd.box_config(n)).init()
+    ref = OracleTwin(n)
+    b = m.blocks[0]
+    m.step(2, check_every=1).synchronize()
+    ref.run(2)
+    a = np.zeros(b.shape)
+    a[m.download(0, "lu") > 0.5] = 3e-7
+    m.upload(0, "RHSx", a)
+    ref.upload(b, "RHSx", a)
+    m.step(2, check_every=1).synchronize()
+    m.step(9, check_every=1)
+    used = m.multi_active
+    m.synchronize()
+    ref.run(11)
+    bad = ref.mismatches(m)
+    zero = m.onepass_zero
+    m.close()
+    assert used and not zero, (used, zero)
+    assert not bad, f"multi-step launch (general variant) differs from the oracle: {bad}"
