@@ -375,6 +375,12 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  enough for its whole grid to be resident (the launch-latency-bound case: the Black Sea basin as one
  *  block), single block without exchanges, the variant chosen on the host, check_every 0 or 1, no
  *  graph replay.  Same results bit for bit.  ocn_ctx_get_option: 2 if the last ocn_ctx_step ran one.
+ *  OCN_OPT_TRACER_STEP (default 1): tracer runs (use_tracers) with one-pass steps -- each step's
+ *  expl_tracer as one launch per tracer that forms hh_init's depths it reads from the state, run with
+ *  the next step (after its exchange, which carries the tracers one point deep); the call's last step
+ *  runs the standard tracer stages.  Needs the call's first step to be a one-pass step, and with
+ *  exchanges the x2 steps; no graph replay.  Same results bit for bit.  ocn_ctx_get_option: 2 if the
+ *  last ocn_ctx_step used them.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
  * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
@@ -386,16 +392,16 @@ int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9,
        OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13,
-       OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16 };
+       OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16, OCN_OPT_TRACER_STEP = 17 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,
  * then the one-pass steps: one step, two steps per launch, two steps the second of which is the
  * call's last (the tail of an open sequence, ocn_ctx_complete), several steps in one cooperative
- * launch (OCN_OPT_MULTI). */
+ * launch (OCN_OPT_MULTI), the tracer step of one-pass sequences (OCN_OPT_TRACER_STEP). */
 enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_TIMER_TRACER,
        OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_TIMER_ONEPASS, OCN_TIMER_ONEPASS2,
-       OCN_TIMER_ONEPASS2_LAST, OCN_TIMER_ONEPASS_MULTI, OCN_NUM_TIMERS };
+       OCN_TIMER_ONEPASS2_LAST, OCN_TIMER_ONEPASS_MULTI, OCN_TIMER_TRACER_STEP, OCN_NUM_TIMERS };
 
 /* Per-timer device time (ms, summed) and launch counts since the last call, from the HIP
  * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_TIMERS entries.  Synchronises. */

@@ -66,7 +66,7 @@ STAGES = ["sw_update_ssh", "hh_update", "uv_trans_vort", "uv_trans", "stress_com
 STAGE_ID = {n: i for i, n in enumerate(STAGES)}
 TSTAGES = ["tran_diff_fluxes", "tran_diff_tracer", "tracer_next_step"]
 TSTAGE_ID = {n: i for i, n in enumerate(TSTAGES)}
-TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES + ["fused_ca", "onepass", "onepass2", "onepass2_last", "onepass_multi"]    # OCN_NUM_TIMERS slots
+TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES + ["fused_ca", "onepass", "onepass2", "onepass2_last", "onepass_multi", "tracer_step"]    # OCN_NUM_TIMERS slots
 OPT_GRAPH = 1
 OPT_OVERLAP = 2
 OPT_STAGE_TIMING = 3
@@ -83,6 +83,7 @@ OPT_X2 = 13
 OPT_BATCH = 14
 OPT_PAIR = 15
 OPT_MULTI = 16
+OPT_TRACER_STEP = 17
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",

@@ -167,6 +167,7 @@ struct LBlock {
     float *rows = nullptr;             // and metric row tables
     void *sshp_alt = nullptr;          // second sshp buffer of the recompute steps (one_step_fused)
     void *up_alt = nullptr, *vp_alt = nullptr;   // second ubrtrp / vbrtrp buffers of the one-pass steps
+    std::vector<void *> ffp_alt;       // second ff1p buffer of every tracer (one-pass steps' tracer step)
     double *kc = nullptr;              // device: h_r, mu of the one-pass step's known-constant variant
     // one_step_x2 (one 2-deep state exchange per one-pass step, the march over the whole interior):
     unsigned own = 0;                  // halo points neighbour blocks own (sw_stencils.h own_class bits)
@@ -318,6 +319,13 @@ struct ocn_ctx {
     // OCN_OPT_MULTI: the one-pass steps of a small single block as one cooperative launch per call
     // (one_step_multi); multi_used: the last call ran one
     bool multi = true, multi_used = false;
+    // OCN_OPT_TRACER_STEP: tracer runs with one-pass steps -- expl_tracer of each step as one launch per
+    // tracer (run_tracer_step), run with the next step, after its exchange; tr_call: this call does;
+    // tr_pending: the current state's tracer step has not run yet; tr_alt_ok: the second ff1p
+    // buffers agree with the fields outside the tracer step's write set.  Role bits 8 (ff1 / ff1n
+    // traded) and 16 (ff1p / its second buffer traded), for every tracer at once.
+    bool tr_step = true, tr_call = false, tr_pending = false;
+    mutable bool tr_alt_ok = false;
     bool known_const = true;   // OCN_OPT_KNOWN_CONSTANTS: the one-pass step's known-constant variant
     bool last_hybrid = true;   // OCN_OPT_ONEPASS_LAST: one-pass last steps with exchanges / ring work too
     bool one_used = false;
@@ -555,9 +563,9 @@ static int allocate(ocn_ctx *c)
         // OCN_FIELD_SKEW (bytes, multiple of 256): extra gap between consecutive fields
         const long r8b = ((n * 8 + 16 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW;
         const long r4b = ((n * 4 + 8 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW;
-        const int nr8 = num_r8(c);
-        // + the three second buffers of the role-flip / one-pass steps
-        const size_t total = (size_t)(nr8 + 3) * r8b + (size_t)OCN_NUM_R4 * r4b + 256;
+        const int nr8 = num_r8(c), ntr = c->sw.use_tracers > 0 ? c->sw.tracer_num : 0;
+        // + the three second buffers of the role-flip / one-pass steps, one per tracer (ff1p)
+        const size_t total = (size_t)(nr8 + 3 + ntr) * r8b + (size_t)OCN_NUM_R4 * r4b + 256;
         HIPCHK(hipMalloc(&b.slab, total));
         c->allocs.push_back(b.slab);
         HIPCHK(hipMemsetAsync(b.slab, 0, total, c->stream));
@@ -573,12 +581,15 @@ static int allocate(ocn_ctx *c)
                                   OCN_HHQ_REST, OCN_VORT, OCN_STR_T, OCN_STR_S, OCN_MU, OCN_RHSX, OCN_RHSY};
         for (int id = OCN_SSH; id < OCN_SSH + nr8; ++id)
             if (std::find(order.begin(), order.end(), id) == order.end()) order.push_back(id);
+        for (int k = 1; k <= ntr; ++k) order.push_back(-3 - k);
+        b.ffp_alt.assign((size_t)ntr, nullptr);
         for (int id : order) {
             char *p = base + off + 256 - 16;
             off += r8b;
             if (id == -1) b.sshp_alt = p;
             else if (id == -2) b.up_alt = p;
             else if (id == -3) b.vp_alt = p;
+            else if (id < -3) b.ffp_alt[(size_t)(-4 - id)] = p;
             else b.ptr[field_slot(id)] = p;
         }
         for (int id = 0; id < OCN_NUM_R4; ++id) {
@@ -653,6 +664,12 @@ static void halo_layer(const ocn_block &rcv, const ocn_block &src, int d, int j,
     else { hr = {hx0, hx1, rcv.ny_start, rcv.ny_end}; br = {sx0, sx1, src.ny_start, src.ny_end}; }
 }
 
+// a tracer field (ff1 / ff1p / ff1n of some tracer)
+static bool is_tracer_field(int id) { return id >= OCN_TRACER_BASE; }
+// Depth of field id in an exchange of `depth`: the tracer fields are exchanged one point deep in
+// every exchange (one_step_x2 sends them with the state's two-deep strips: one message per peer)
+static int field_depth(int id, int depth) { return is_tracer_field(id) ? 1 : depth; }
+
 static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::vector<PlanEntry> &out,
                         int depth = 1)
 {
@@ -669,10 +686,12 @@ static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::v
             if (r < 0) continue;
             const GBlock &src = c->gblocks[b.nbr_gid[d - 1]];
             for (int j = 1; j <= depth; ++j) {
-                Rect hr, br;
-                halo_layer(b.g, src.g, d, j, depth, hr, br);
-                const int cnt = (hr.x1 - hr.x0 + 1) * (hr.y1 - hr.y0 + 1);
                 for (int id : fields) {
+                    const int fd = field_depth(id, depth);
+                    if (j > fd) continue;
+                    Rect hr, br;
+                    halo_layer(b.g, src.g, d, j, fd, hr, br);
+                    const int cnt = (hr.x1 - hr.x0 + 1) * (hr.y1 - hr.y0 + 1);
                     if (r == c->dec.rank)
                         out.push_back(PlanEntry{OCN_HALO_LOCAL, r, k, k_of_gid.at(b.nbr_gid[d - 1]), id, hr, br, 0, cnt});
                     else {
@@ -694,10 +713,12 @@ static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::v
             if (c->gblocks[sg].rank != c->dec.rank) continue;
             const int ks = k_of_gid.at(sg);
             for (int j = 1; j <= depth; ++j) {
-                Rect hr, br;
-                halo_layer(rb.g, c->blocks[ks].g, d, j, depth, hr, br);
-                const int cnt = (br.x1 - br.x0 + 1) * (br.y1 - br.y0 + 1);
                 for (int id : fields) {
+                    const int fd = field_depth(id, depth);
+                    if (j > fd) continue;
+                    Rect hr, br;
+                    halo_layer(rb.g, c->blocks[ks].g, d, j, fd, hr, br);
+                    const int cnt = (br.x1 - br.x0 + 1) * (br.y1 - br.y0 + 1);
                     out.push_back(PlanEntry{OCN_HALO_SEND, rb.rank, -1, ks, id, hr, br, send_count[rb.rank], cnt});
                     send_count[rb.rank] += cnt;
                 }
@@ -772,7 +793,9 @@ static int get_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan *&out, 
     // a plan holds the buffers its fields had when it was built: the pair roles (bit 1), and for
     // sshp / ubrtrp / vbrtrp the second buffers' roles (bit 4: they persist between one-pass calls)
     const bool alt = std::any_of(fields.begin(), fields.end(), [](int id) { return is_alt_field(id); });
-    key.push_back(-1 - (c->role & 1) - (alt ? (c->role & 4) : 0));
+    // (tracer fields: the tracer steps' role bits 8 -- ff1 / ff1n -- and 16 -- ff1p's second buffer)
+    const bool tr = std::any_of(fields.begin(), fields.end(), [](int id) { return is_tracer_field(id); });
+    key.push_back(-1 - (c->role & 1) - (alt ? (c->role & 4) : 0) - (tr ? (c->role & 24) : 0));
     if (depth != 1 || priv) key.push_back(-100 - depth - 10 * priv);
     auto it = c->plans.find(key);
     if (it == c->plans.end()) {
@@ -1318,13 +1341,28 @@ static void swap_alt3(ocn_ctx *c)
     }
     c->role ^= 4;
 }
+// tracer steps (run_tracer_step): every tracer's ff1 and ff1n trade places (role bit 8, the role-flip
+// form of tracer_next_step's ff := ffn), and ff1p with its second buffer (role bit 16)
+static void swap_tracer_roles(ocn_ctx *c)
+{
+    for (LBlock &b : c->blocks)
+        for (int k = 1; k <= c->sw.tracer_num; ++k)
+            std::swap(b.ptr[field_slot(OCN_FF1(k))], b.ptr[field_slot(OCN_FF1N(k))]);
+    c->role ^= 8;
+}
+static void swap_tracer_alt(ocn_ctx *c)
+{
+    for (LBlock &b : c->blocks)
+        for (int k = 1; k <= c->sw.tracer_num; ++k) std::swap(b.ptr[field_slot(OCN_FF1P(k))], b.ffp_alt[(size_t)k - 1]);
+    c->role ^= 16;
+}
 static size_t field_bytes(const LBlock &b) { return (size_t)b.g.pitch * (b.g.bnd_y2 - b.g.bnd_y1 + 1) * 8; }
 static bool is_alt_field(int id) { return id == OCN_SSHP || id == OCN_UBRTRP || id == OCN_VBRTRP; }
 static bool is_flip_field(int id)
 {
     for (const auto &pr : kFlipPairs)
         if (id == pr[0] || id == pr[1]) return true;
-    return false;
+    return id >= OCN_TRACER_BASE && (id - OCN_TRACER_BASE) % 3 != 1;   // a tracer's ff1 / ff1n (tracer steps)
 }
 
 // Whether role-flip steps are exact for the current state (synchronises):
@@ -1409,6 +1447,11 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
     HIPCHK(hipMemcpyAsync(c->d_flags, host, sizeof(host), hipMemcpyHostToDevice, c->stream));
     if (in.eligible)
         RC(each_block(c, c->stream, [&](const LBlock &b) { return launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream); }));
+    if (in.eligible && c->sw.use_tracers > 0 && c->tr_step)   // the tracer steps' ff1 / ff1n pairs too
+        for (int t = 1; t <= c->sw.tracer_num; ++t)
+            RC(each_block(c, c->stream, [&](const LBlock &b) {
+                return launch_tracer_coherence(&b.g, b.ptr.data(), b.bits, t, c->d_flags, c->stream);
+            }));
     const bool exch = has_exchange(c);
     if (exch) RC(run_sync(c, kHaloCheck, c->stream, c->d_flags));
     if (exch && c->x2) {   // one_step_x2: the rest of the state's first halo ring, and the unexchanged halos
@@ -1447,6 +1490,11 @@ static bool flip_eligible(ocn_ctx *c)
 {
     return c->flip && c->fused && c->compact && c->march;
 }
+
+// tracer steps (run_tracer_step, below): the pending one of the current state, and the tracer fields
+// the exchanges of a one-pass call carry with the state
+static int run_tracer_step(ocn_ctx *c, double tau);
+static std::vector<int> with_tracers(const ocn_ctx *c, const std::vector<int> &fields);
 
 // block b's one-pass variant for the current call (ctx kc_mode, the device verdict, its constants)
 static OnepassKC kc_of(const ocn_ctx *c, const LBlock &b) { return OnepassKC{c->kc_mode, c->d_fbz, b.kc}; }
@@ -1704,7 +1752,7 @@ static int ring2_run(ocn_ctx *c, bool save, hipStream_t s)
 static int x2_end(ocn_ctx *c, hipStream_t s)
 {
     RC(ring2_run(c, false, s));
-    return run_sync(c, kStateX2, s);
+    return run_sync(c, with_tracers(c, kStateX2), s);
 }
 
 // hr_x = h_r with the neighbours' second ring (the general variant of one_step_x2 reads it there)
@@ -1791,7 +1839,7 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
         RC(timer_end(c, rec));
         HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
         if (k.x2_save) RC(ring2_run(c, true, c->comm_stream));
-        RC(run_sync(c, kStateX2, c->comm_stream, nullptr, 2));   // the state two points deep
+        RC(run_sync(c, with_tracers(c, kStateX2), c->comm_stream, nullptr, 2));   // the state two points deep
         RC(each_block(c, c->comm_stream, [&](const LBlock &b) -> int {
             const Range in = x2_inner(b);
             RC(march(b, c->comm_stream, nullptr, &in));
@@ -1802,11 +1850,14 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
         RC(join_sync(c));
     } else {
         if (k.x2_save) RC(ring2_run(c, true, s));
-        RC(run_sync(c, kStateX2, s, nullptr, 2));   // the state two points deep
+        RC(run_sync(c, with_tracers(c, kStateX2), s, nullptr, 2));   // the state two points deep
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
         RC(each_block(c, s, [&](const LBlock &b) { return march(b, s, nullptr, nullptr); }));
         RC(timer_end(c, rec));
     }
+    // the previous state's tracer step: it reads that state (untouched by the march) and the tracers
+    // with their first halo ring, both just exchanged
+    RC(run_tracer_step(c, tau));
     swap_alt3(c);
     swap_roles(c);
     return OCN_OK;
@@ -1867,7 +1918,8 @@ static int one_step_multi(ocn_ctx *c, double tau, const StepKind &k)
 #endif
 static bool pair_ok(ocn_ctx *c)
 {
-    if (!c->pair || c->blocks.size() != 1 || has_exchange(c) || has_comm(c) || c->ring_sea || !c->compact || !c->march)
+    if (!c->pair || c->blocks.size() != 1 || has_exchange(c) || has_comm(c) || c->ring_sea || !c->compact || !c->march ||
+        c->sw.use_tracers > 0)
         return false;
     if (c->kc_mode == OCN_KC_DEVICE) return false;   // (the variant the launches run is chosen on the device)
     if (c->pair >= 2) return true;
@@ -1883,7 +1935,8 @@ static bool pair_ok(ocn_ctx *c)
 // none, and a block small enough that its grid is resident at once -- the launch-latency-bound case
 static bool multi_ok(ocn_ctx *c, int32_t check_every)
 {
-    return c->multi && c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) && !c->ring_sea && c->compact &&
+    return c->multi && c->sw.use_tracers <= 0 && c->blocks.size() == 1 && !has_exchange(c) && !has_comm(c) &&
+           !c->ring_sea && c->compact &&
            c->march && c->kc_mode != OCN_KC_DEVICE && (check_every == 0 || check_every == 1) &&
            onepass_multi_fits(&c->blocks[0].g);
 }
@@ -1894,6 +1947,10 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
     if (k.pair) return one_step_pair(c, tau, k);
     if (k.x2) return one_step_x2(c, tau, k);
     if (k.one_last && k.x2_end) RC(x2_end(c, c->stream));
+    if (k.one_last && c->tr_pending) {   // the previous state's tracer step, then its tracers' halos
+        RC(run_tracer_step(c, tau));
+        if (has_exchange(c)) RC(run_sync(c, with_tracers(c, {})));
+    }
     if (k.one_last) return has_exchange(c) || c->ring_sea ? one_step_hybrid(c, tau, k, true) : one_step_last(c, tau, k);
     const bool check = k.check, first = k.first, last = k.last, flip = k.flip;
     const ocn_sw_params &sw = c->sw;
@@ -2090,6 +2147,41 @@ static int expl_tracer(ocn_ctx *c, double tau, bool compact)
     for (int k = 1; k <= c->sw.tracer_num; ++k)
         for (int stage = 0; stage < OCN_NUM_TSTAGES; ++stage) RC(tracer_stage(c, stage, k, tau, compact));
     return OCN_OK;
+}
+
+// Tracer runs with one-pass steps (OCN_OPT_TRACER_STEP): a one-pass step keeps hh_init's depths in
+// registers, so expl_tracer after it (control/tracer.f90:33-62, model.f90:156) runs later, as ONE
+// launch per tracer (sw_kernels.hip launch_tracer_step, sw_stencils.h TracerStep) that forms the
+// depths it reads from the state with hh_init's own functions -- with the next step, after that
+// step's exchange (which carries the tracers' ff1 / ff1p one point deep with the state: with_tracers)
+// and before anything writes the state it reads.  Its ffn goes to the ff1n buffer and the roles of
+// ff1 / ff1n trade (tracer_next_step's ff := ffn); the filtered ff1p to the second buffer.  The call's
+// last step (standard hh_init with every level) runs the standard stages after it.
+static int run_tracer_step(ocn_ctx *c, double tau)
+{
+    if (!c->tr_pending) return OCN_OK;
+    c->tr_pending = false;
+    ocn_ctx::Rec rec;
+    RC(timer_begin(c, OCN_TIMER_TRACER_STEP, rec));
+    for (int k = 1; k <= c->sw.tracer_num; ++k)
+        RC(each_block(c, c->stream, [&](const LBlock &b) -> int {
+            const Compact t{b.bits, b.rows, c->march};
+            return launch_tracer_step(&b.g, b.ptr.data(), (int)b.ptr.size(), c->compact ? &t : nullptr, k, tau,
+                                      c->sw.time_smooth, (double *)b.ptr[field_slot(OCN_FF1N(k))],
+                                      (double *)b.ffp_alt[(size_t)k - 1], b.own, c->stream);
+        }));
+    RC(timer_end(c, rec));
+    swap_tracer_roles(c);
+    swap_tracer_alt(c);
+    return OCN_OK;
+}
+
+static std::vector<int> with_tracers(const ocn_ctx *c, const std::vector<int> &fields)
+{
+    if (!c->tr_call) return fields;
+    std::vector<int> out = fields;
+    for (int k = 1; k <= c->sw.tracer_num; ++k) { out.push_back(OCN_FF1(k)); out.push_back(OCN_FF1P(k)); }
+    return out;
 }
 
 // ------------------------------------------------------------------ initial state
@@ -2456,6 +2548,7 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
     if (!is_r4(id) && alt_home(w) != OCN_OK) return nullptr;
     if (is_flip_field(id)) { c->r8_escaped = true; c->coherent_known = false; }
     if (is_alt_field(id)) c->alt_ok = false;
+    if (is_tracer_field(id)) c->tr_alt_ok = false;
     if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_state = kFbUnchecked; c->hrx_ok = false; }
     if (is_alt_field(id) || id == OCN_HHQ_REST) { c->r8_escaped = true; c->coherent_known = false; }
     return c->blocks[k].ptr[field_slot(id)];
@@ -2531,8 +2624,9 @@ int ocn_ctx_init_state(ocn_ctx *c)
     c->open_pair = false;
     c->deferred = 0;
     c->ring2_saved = false;   // (a saved second ring of an x2 sequence is void: init forms it again)
+    c->tr_pending = false;
     c->coherent_known = false;
-    c->alt_ok = false;
+    c->alt_ok = false; c->tr_alt_ok = false;
     c->fb_state = kFbUnchecked;
     const int rc = fail_fatal(c, init_state(c));
     c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // init_data.f90:60-63 ran hh_init last
@@ -2556,6 +2650,7 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
     if (field_id == OCN_HHQ_REST) c->hrx_ok = false;
     // the current buffer's halos change; the one-pass steps' second buffer must be copied again
     if (is_alt_field(field_id)) c->alt_ok = false;
+    if (is_tracer_field(field_id)) c->tr_alt_ok = false;
     return run_sync(c, {field_id});
 }
 
@@ -2566,7 +2661,7 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     if (stage_id < 0 || stage_id >= OCN_NUM_STAGES) return set_error(OCN_ERR_ARG, "bad stage id");
     RC(complete_open(c));
     c->coherent_known = false;
-    c->alt_ok = false;
+    c->alt_ok = false; c->tr_alt_ok = false;
     c->hh_consistent = false;
     c->fb_state = kFbUnchecked;
     RC(prepare_static(c));
@@ -2582,7 +2677,15 @@ static void drop_graphs(ocn_ctx *c)
 // one model step (model.f90:146-160): expl_shallow_water, then expl_tracer
 static int run_step(ocn_ctx *c, double tau, const StepKind &k)
 {
+    // tracer steps (OCN_OPT_TRACER_STEP): a one-pass step's tracer step runs with the next step; the
+    // pending one of the state a single-block one-pass step reads runs before its march (x2 steps
+    // and the last step: after their exchanges, one_step_x2 / one_step_fused)
+    if (c->tr_call && k.one && !k.x2) RC(run_tracer_step(c, tau));
     RC(c->fused ? one_step_fused(c, tau, k) : one_step(c, tau, k.check));
+    if (c->tr_call && k.one) {
+        c->tr_pending = true;
+        return OCN_OK;
+    }
     return expl_tracer(c, tau, c->compact);
 }
 
@@ -2720,6 +2823,18 @@ static int finish_call(ocn_ctx *c, int rc)
     // one-pass steps: sshp / ubrtrp / vbrtrp stay in the second buffers (every access goes through
     // the field table) unless a raw r8 pointer was handed out: then back into the fields' buffers
     if ((c->role & 4) && c->r8_handed) RC(alt_home(c));
+    // tracer steps: the last step's standard tracer stages leave ff1 = ff1n everywhere (tracer_next_step's
+    // ff := ffn where tran_diff_tracer wrote ffn and its exchange delivered it, both untouched elsewhere):
+    // the roles return with no copy; the current ff1p is copied into the field's own buffer
+    if (c->role & 8) swap_tracer_roles(c);
+    if (c->role & 16) {
+        for (LBlock &b : c->blocks)
+            for (int t = 1; t <= c->sw.tracer_num; ++t)
+                HIPCHK(hipMemcpyAsync(b.ffp_alt[(size_t)t - 1], b.ptr[field_slot(OCN_FF1P(t))], field_bytes(b),
+                                      hipMemcpyDeviceToDevice, c->stream));
+        swap_tracer_alt(c);
+    }
+    c->tr_pending = false;
     c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // the last step ran a full hh_init
     return rc;
 }
@@ -2730,7 +2845,7 @@ static int finish_call(ocn_ctx *c, int rc)
 // halo ring: the redone step must find the previous state intact).
 static bool lazy_allowed(const ocn_ctx *c, bool x2)
 {
-    return c->lazy && !has_comm(c) && !c->r8_handed && c->sw.use_tracers <= 0 &&
+    return c->lazy && !has_comm(c) && !c->r8_handed && (c->sw.use_tracers <= 0 || c->tr_step) &&
            (x2 || (!c->ring_sea && !has_exchange(c)));
 }
 
@@ -2780,6 +2895,7 @@ static int complete_open(ocn_ctx *c)
     }
     swap_roles(c);
     swap_alt3(c);
+    c->tr_pending = false;   // (the tracer step of the state before the last step has run)
     if (c->open_pair) {   // the last launch was a pair (one flip, two steps): both again, from the state
         c->open_pair = false;   // before it, the second as the last step (counted the first time: no checks)
         if (pair_ok(c)) {
@@ -2804,7 +2920,8 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
     if (nsteps < 0) return set_error(OCN_ERR_ARG, "nsteps < 0");
     if (nsteps == 0) return OCN_OK;
-    const bool graph_ok = c->use_graph && !has_comm(c) && !c->stage_timing;   // RCCL / events stay outside graphs
+    // (RCCL / events stay outside graphs; so do the tracer steps' calls: their launches follow pending state)
+    const bool graph_ok = c->use_graph && !has_comm(c) && !c->stage_timing && !(c->sw.use_tracers > 0 && c->tr_step);
     c->pair_used = false;
     c->multi_used = false;
     if (c->open) {
@@ -2882,6 +2999,10 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         x2_ok = x2_here && v.x2_ok;
     }
     bool flip_call = false, ca = false, one_call = false;
+    // tracer runs with one-pass steps (tracer steps): the call's first step a one-pass step too, and
+    // with exchanges the x2 steps (their exchange carries the tracers); one block: no ring work
+    const bool tr_ok = c->sw.use_tracers <= 0 ||
+                       (c->tr_step && first_one && (has_exchange(c) ? x2_ok && c->last_hybrid : !c->ring_sea));
     auto decide = [&](int n) {
         flip_call = n >= 2 && eligible && c->coherent;
         // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A;
@@ -2892,7 +3013,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         // hhq_p, which a one-pass step keeps in registers; row divisors in udiv's range) -- the first
         // step too when hh_init's stored depths match the state (hh_consistent)
         one_call = ca && c->onepass && (n >= 3 || (n >= 2 && first_one)) && c->sw.trans_terms > 0 &&
-                   c->sw.ksw_lat > 0 && c->sw.use_tracers <= 0 && udiv_ok;
+                   c->sw.ksw_lat > 0 && tr_ok && udiv_ok;
     };
     decide(N);
     // one-pass steps with one 2-deep exchange each (one_step_x2) where there are exchanges
@@ -2903,6 +3024,15 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     if (!lazy_end && N != nsteps) decide(N = nsteps);
     c->x2_used = x2_call && one_call;
     c->flip_used = flip_call;
+    c->tr_call = c->sw.use_tracers > 0 && one_call;
+    c->tr_pending = false;
+    if (c->tr_call && !c->tr_alt_ok) {   // the second ff1p buffers start as copies
+        for (const LBlock &b : c->blocks)
+            for (int t = 1; t <= c->sw.tracer_num; ++t)
+                HIPCHK(hipMemcpyAsync(b.ffp_alt[(size_t)t - 1], b.ptr[field_slot(OCN_FF1P(t))], field_bytes(b),
+                                      hipMemcpyDeviceToDevice, c->stream));
+        c->tr_alt_ok = true;
+    }
     c->hh_consistent = false;   // until this call's last step has run
     // the last step as one march + hh_init too (single block, no exchange, no ring work)
     // (with exchanges or ring work: the hybrid last step, OCN_OPT_ONEPASS_LAST)
@@ -3120,6 +3250,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     // (the x2 checks also cover sshp / ubrtrp / vbrtrp and h_r: check_coherence)
     if (is_flip_field(id) || is_alt_field(id) || id == OCN_HHQ_REST) c->coherent_known = false;
     if (is_alt_field(id)) c->alt_ok = false;
+    if (is_tracer_field(id)) c->tr_alt_ok = false;
     if (id == OCN_HHQ_REST) c->hrx_ok = false;
     c->hh_consistent = false;
     c->fb_state = kFbUnchecked;
@@ -3160,6 +3291,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     case OCN_OPT_X2: c->x2 = value != 0; c->coherent_known = false; return OCN_OK;
     case OCN_OPT_PAIR: c->pair = value < 0 ? 0 : value > 2 ? 2 : (int)value; return OCN_OK;
     case OCN_OPT_MULTI: c->multi = value != 0; return OCN_OK;
+    case OCN_OPT_TRACER_STEP: c->tr_step = value != 0; return OCN_OK;
     case OCN_OPT_BATCH:
         if (c->batch != (value != 0)) drop_graphs(c);
         c->batch = value != 0;
@@ -3200,6 +3332,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_BATCH: *value = c->batch; return OCN_OK;
     case OCN_OPT_PAIR: *value = c->pair_used ? 2 : c->pair > 0; return OCN_OK;
     case OCN_OPT_MULTI: *value = c->multi_used ? 2 : c->multi; return OCN_OK;
+    case OCN_OPT_TRACER_STEP: *value = c->tr_call ? 2 : c->tr_step; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -174,9 +174,17 @@ int launch_stage(const ocn_block *b, void *const *ptr, int nptr, const Compact *
                  double tau, int32_t *nbad, hipStream_t s);
 int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int stage, int k, double tau,
                   double ts, hipStream_t s);
+// the three tracer stages of tracer k as one launch in a one-pass sequence (sw_stencils.h TracerStep:
+// hh_init's hhu / hhv / hhq_p formed from the state): ffn into ffn_out, the filtered ffp into ffp_out;
+// own: the halo points neighbour blocks own (their fluxes formed here, as the exchange delivers them)
+int launch_tracer_step(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int k, double tau,
+                       double ts, double *ffn_out, double *ffp_out, unsigned own, hipStream_t s);
 // ORs 1 into *flags (device int) if a buffer pair of the role-flip step differs outside the
 // pair's write set (sw_stencils.h Coherence).
 int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int32_t *flags, hipStream_t s);
+// the same for tracer k's ff1 / ff1n (the tracer steps' role pair) outside the ring range's lu points
+int launch_tracer_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int k, int32_t *flags,
+                            hipStream_t s);
 // Prepare's flag bit reporting mask bits on the halo ring (sw_stencils.h OCN_COMPACT_RING_SEA)
 constexpr int kCompactRingSea = 4;
 constexpr int kCompactDivisorRange = 8;   // sw_stencils.h OCN_COMPACT_DIVISOR_RANGE

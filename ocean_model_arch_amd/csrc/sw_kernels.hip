@@ -2946,6 +2946,16 @@ int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact 
     }
 }
 
+// expl_tracer of tracer k as one launch in a one-pass sequence (sw_stencils.h TracerStep): the full
+// free surface factor is 1 (the one-pass steps require it), factor_mu 1.0d0 (tracer_interface.f90:47)
+int launch_tracer_step(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int k, double tau,
+                       double ts, double *ffn_out, double *ffp_out, unsigned own, hipStream_t s)
+{
+    if (!ffn_out || !ffp_out) return set_error(OCN_ERR_ARG, "tracer step: output buffers");
+    const Range ri = range_interior(b);
+    return launch_fused<KTracerStep>(ri, ri, OCN_PART_ALL, b, ptr, nptr, cp, k, s, tau, ts, own, ffn_out, ffp_out);
+}
+
 // One reference stage over the compact tables (ocn_ctx.hip envoke, OCN_OPT_COMPACT): the stage
 // functor is built on the device from the block's field table, as the fused launches build theirs,
 // and reads the mask byte and the per-row metrics instead of the real(4) arrays -- the same
@@ -3007,6 +3017,20 @@ int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, 
     RC_K(check_block(b));
     const Range r = range_bnd(b);
     return launch_range(r.m0, r.m1, r.n0, r.n1, make_coherence(b, ptr, bits, (int *)flags), s);
+}
+
+// the tracer steps' pairs: ff1 and ff1n of tracer k agree outside the ring range's lu points (what the
+// reference's tran_diff_tracer / its exchange and tracer_next_step write: the interior and the halo ring)
+int launch_tracer_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int k, int32_t *flags,
+                            hipStream_t s)
+{
+    RC_K(check_block(b));
+    const double *ff = (const double *)ptr[ocn_field_slot(OCN_FF1(k))];
+    const double *ffn = (const double *)ptr[ocn_field_slot(OCN_FF1N(k))];
+    const Coherence q{geo(b), b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, bits,
+                      {ff, ff, ff}, {ffn, ff, ff}, (int *)flags};   // (pairs 2, 3: trivially equal)
+    const Range r = range_bnd(b);
+    return launch_range(r.m0, r.m1, r.n0, r.n1, q, s);
 }
 
 size_t row_table_size(unsigned nrows) { return row_table_floats(nrows); }

@@ -673,6 +673,91 @@ template <bool C> struct TracerNextStep {
     }
 };
 
+// expl_tracer for ONE tracer in one launch over the interior, in one-pass sequences (the one-pass
+// steps store no hh_init depths): control/tracer.f90:33-62 runs tran_diff_fluxes, tran_diff_tracer
+// and tracer_next_step (leapfrog_tracer.f90:13-170) after each step, reading hh_init's hhu, hhv
+// (level 0), hhq_n (= h_r) and hhq_p (= h_r + sshp * ffs, depth.f90:48-50) of the new state.  At an
+// interior point under lu: the fluxes at the point and at its west / south neighbours -- formed
+// here with tran_diff_fluxes' expressions where that stage stores them (the interior, and the halo
+// points neighbour blocks own: what their exchange delivers), from hhu / hhv formed with hh_init's
+// own interp_u / interp_v where hh_init stores them ([start-1, end]^2 under llu / llv), else the
+// arrays' values (never written there) -- then ffn = (bp0 * ffp + rhs) / bp and the time filter.
+// Writes ffn (the ffn buffer: it becomes ff with the role flip ff <-> ffn, ff := ffn of
+// tracer_next_step) and the filtered ffp (into a second buffer: ffp is read at this point only,
+// but the role pairs of every buffer trade places together).  Each value is the reference's
+// expression on the same operands: bitwise the stages' results.
+OCN_HD inline unsigned own_class(int v, int lo, int hi);
+template <bool C> struct TracerStep {
+    Geo I; double tau, ts, f, factor_mu;
+    int nxs, nxe, nys, nye; unsigned own;   // interior; halo points neighbour blocks own (own_class bits)
+    Interp<C> W;
+    Msk<C> llu, llv, lcu, lcv;
+    const double *__restrict__ ssh, *__restrict__ sshp, *__restrict__ h_r, *__restrict__ uu, *__restrict__ vv;
+    const double *__restrict__ mu, *__restrict__ hhu, *__restrict__ hhv, *__restrict__ flux_x, *__restrict__ flux_y;
+    const double *__restrict__ ff, *__restrict__ ffp;
+    double *__restrict__ ffn_out, *__restrict__ ffp_out;
+    struct View {
+        const TracerStep &k; Pt c;
+        OCN_VIEW_INTERP
+    };
+    OCN_HD OCN_INLINE bool owned(int m, int n) const
+    {
+        return (own >> (own_class(m, nxs, nxe) * 3u + own_class(n, nys, nye))) & 1u;
+    }
+    OCN_HD OCN_INLINE double a0(Pt c) const { return ld(h_r, c) + ld(ssh, c) * f; }   // hh_init level 0
+    // hh_init's hhu / hhv at (m, n) (depth.f90:52-97 on [start-1, end]^2; the array's value elsewhere)
+    OCN_HD OCN_INLINE double hu_at(int m, int n) const
+    {
+        const Pt c = I(m, n);
+        const bool rng = owned(m, n) || (m >= nxs - 1 && m <= nxe && n >= nys - 1 && n <= nye);
+        if (!(rng && ld(llu, c) > 0.5f)) return ld(hhu, c);
+        return interp_u(View{*this, c}, a0(c), a0(I.e(c)));
+    }
+    OCN_HD OCN_INLINE double hv_at(int m, int n) const
+    {
+        const Pt c = I(m, n);
+        const bool rng = owned(m, n) || (m >= nxs - 1 && m <= nxe && n >= nys - 1 && n <= nye);
+        if (!(rng && ld(llv, c) > 0.5f)) return ld(hhv, c);
+        return interp_v(View{*this, c}, a0(c), a0(I.n(c)));
+    }
+    // tran_diff_fluxes' flux_x / flux_y at (m, n): TranDiffFluxes' expressions where it stores them
+    OCN_HD OCN_INLINE bool in_fluxes(int m, int n) const
+    {
+        return owned(m, n) || (m >= nxs && m <= nxe && n >= nys && n <= nye);
+    }
+    OCN_HD OCN_INLINE double fx_at(int m, int n) const
+    {
+        const Pt c = I(m, n), e = I.e(c);
+        if (!(in_fluxes(m, n) && ld(lcu, c) > 0.5f)) return ld(flux_x, c);
+        const double fc = ld(ff, c), fe = ld(ff, e), mc = ld(mu, c), hu = hu_at(m, n);
+        const double mux = (mc + ld(mu, e)) / 2.0 * factor_mu * D(ld(W.dyh, c)) / D(ld(W.dxt, c));
+        return -ld(uu, c) * hu * D(ld(W.dyh, c)) * (fc + fe) / 2.0 + mux * hu * (fe - fc) + 0.0;
+    }
+    OCN_HD OCN_INLINE double fy_at(int m, int n) const
+    {
+        const Pt c = I(m, n), nn = I.n(c);
+        if (!(in_fluxes(m, n) && ld(lcv, c) > 0.5f)) return ld(flux_y, c);
+        const double fc = ld(ff, c), fn = ld(ff, nn), mc = ld(mu, c), hv = hv_at(m, n);
+        const double muy = (mc + ld(mu, nn)) / 2.0 * factor_mu * D(ld(W.dxh, c)) / D(ld(W.dyt, c));
+        return -ld(vv, c) * hv * D(ld(W.dxh, c)) * (fc + fn) / 2.0 + muy * hv * (fn - fc) + 0.0;
+    }
+    OCN_HD void operator()(int m, int n) const
+    {
+        const Pt c = I(m, n);
+        if (!(ld(W.lu, c) > 0.5f)) return;
+        // tran_diff_tracer (leapfrog_tracer.f90:94-136): hhq_n = h_r, hhq_p = h_r + sshp * ffs
+        const double hqn = ld(h_r, c), hqp = ld(h_r, c) + ld(sshp, c) * f;
+        const double bp = hqn * D(ld(W.dx, c)) * D(ld(W.dy, c)) / tau / 2.0;
+        const double bp0 = hqp * D(ld(W.dx, c)) * D(ld(W.dy, c)) / tau / 2.0;
+        const double rhs = fx_at(m, n) - fx_at(m - 1, n) + fy_at(m, n) - fy_at(m, n - 1);
+        const double xn = (bp0 * ld(ffp, c) + rhs) / bp;
+        // tracer_next_step (leapfrog_tracer.f90:138-168)
+        const double x = ld(ff, c), xp = ld(ffp, c);
+        st(ffp_out, c, x + ts * (xn - 2.0 * x + xp) / 2.0);
+        st(ffn_out, c, xn);
+    }
+};
+
 // ================================================================== fused step groups
 // The step's 10 stages regrouped into 4 launches with the same results, write sets and halo
 // state as the stage-by-stage reference order (shallow_water.f90:36-92):
@@ -1163,6 +1248,19 @@ template <bool C> struct KTranDiffTracer {
 template <bool C> struct KTracerNextStep {
     ocn_block b; Tab<C> t; double ts;
     OCN_HD void operator()(int m, int n) const { make_tracer_next_step(&b, t, 1, ts)(m, n); }
+};
+// TracerStep of the table's tracer (one-pass sequences), its outputs into ffn_out / ffp_out
+template <bool C> struct KTracerStep {
+    ocn_block b; Tab<C> t; double tau, ts; unsigned own; double *ffn_out, *ffp_out;
+    OCN_HD void operator()(int m, int n) const
+    {
+        const TracerStep<C> k{geo(&b), tau, ts, 1.0, 1.0, b.nx_start, b.nx_end, b.ny_start, b.ny_end, own,
+                              make_interp(t), t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LCU), t.m(OCN_LCV),
+                              t.f(OCN_SSH), t.f(OCN_SSHP), t.f(OCN_HHQ_REST), t.f(OCN_UBRTR), t.f(OCN_VBRTR),
+                              t.f(OCN_MU), t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_FLUX_X), t.f(OCN_FLUX_Y),
+                              t.f(OCN_FF1(1)), t.f(OCN_FF1P(1)), ffn_out, ffp_out};
+        k(m, n);
+    }
 };
 
 }  // namespace ocn

@@ -230,6 +230,17 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MULTI, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_tracer_step(self, on: bool = True):
+        """Tracer runs with one-pass steps: expl_tracer of each step as one launch per tracer (the depths
+        it reads formed from the state), run with the next step (default on); same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_TRACER_STEP, int(on)), "ocn_ctx_set_option")
+        return self
+
+    @property
+    def tracer_step_active(self) -> bool:
+        """Whether the last step() ran the tracers as tracer steps with one-pass steps."""
+        return self.option(_lib.OPT_TRACER_STEP) == 2
+
     def set_pair(self, mode: int = 1):
         """Two one-pass steps per launch (default 1: the known-constant variants on single blocks of
         at least 512 x 512 interior points; 2: any variant, any block; 0: never): the first step's

@@ -82,7 +82,7 @@ def test_field_ids_match_header():
     assert _lib.FIELD_ID["flux_x"] == 64 and _lib.FIELD_ID["flux_y"] == 65
     assert [_lib.FIELD_ID[n] for n in ("ff1_1", "ff1p_1", "ff1n_1", "ff1_2")] == [66, 67, 68, 69]
     assert _lib.FIELD_ID.name(71) == "ff1n_2"
-    assert len(_lib.TIMERS) == 11 + 3 + 3 + 5   # + fused_ca, onepass, onepass2, onepass2_last, onepass_multi
+    assert len(_lib.TIMERS) == 11 + 3 + 3 + 6   # + fused_ca, onepass, onepass2, onepass2_last, onepass_multi, tracer_step
 
 
 def test_abi_version_and_loud_failure_without_device(lib):

@@ -103,3 +103,62 @@ def test_multi_with_uploads_and_forcing_matches_oracle(amd):
     m.close()
     assert used and not zero, (used, zero)
     assert not bad, f"multi-step launch (general variant) differs from the oracle: {bad}"
+
+
+# ---------------------------------------------------------------- tracer steps (OCN_OPT_TRACER_STEP)
+@pytest.mark.parametrize("calls", ["one", "split", "per_step"])
+@pytest.mark.parametrize("name", ["box40x32_tr2_s5", "box70x54_b3x2_tr_s20", "bs_b4x2_tr_s60", "bs_b4x2_tr_s604"])
+def test_tracer_steps_match_reference(amd, name, calls):
+    """Tracer runs with one-pass steps: expl_tracer (control/tracer.f90:33-62) of each step as one
+    launch per tracer (sw_stencils.h TracerStep: hh_init's depths formed from the state), run with the
+    next step after its exchange (x2 steps carry the tracers one point deep); the last step the
+    standard stages -- bitwise against the reference, in one call, split calls and 1-step calls."""
+    case = cases.load_e2e(name)
+    steps = case["steps"]
+    plan = {"one": [steps], "split": [2, steps - 5, 3] if steps > 5 else [2, steps - 2],
+            "per_step": [1] * steps}[calls]
+    m = build_model(amd, case).init()
+    used = []
+    try:
+        for n in plan:
+            m.step(n, tau=1.0, check_every=1)
+            used.append(m.tracer_step_active)
+        m.synchronize()
+        bad = compare_case(m, case, name)
+        x2 = m.x2_active
+    finally:
+        m.close()
+    assert not bad, f"{name} ({calls}): fields differ from the reference: {bad}"
+    assert used[0], used
+    if "tr2" not in name:   # several blocks: the x2 steps carry the tracers
+        assert x2, name
+
+
+def test_tracer_steps_off_is_the_role_flip_path(amd):
+    case = cases.load_e2e("bs_b4x2_tr_s60")
+    m = build_model(amd, case).set_tracer_step(False).init()
+    try:
+        m.step(case["steps"], tau=1.0, check_every=1).synchronize()
+        bad = compare_case(m, case, "bs_b4x2_tr_s60")
+        used, one = m.tracer_step_active, m.onepass_active
+    finally:
+        m.close()
+    assert not bad and not used and not one, (bad, used, one)
+
+
+def test_tracer_steps_launches(amd):
+    """Config 5's layout on one GPU (Black Sea + tracer, 4x2 blocks): x2 steps with the tracer steps,
+    block-batched -- a few launches per step instead of the role-flip path's 22."""
+    case = cases.load_e2e("bs_b4x2_tr_s60")
+    m = build_model(amd, case).init()
+    try:
+        m.step(4, tau=1.0, check_every=1).synchronize()
+        n0 = amd._lib.launch_count()
+        m.step(40, tau=1.0, check_every=1)
+        per_step = (amd._lib.launch_count() - n0) / 40
+        used, x2 = m.tracer_step_active, m.x2_active
+        m.synchronize()
+    finally:
+        m.close()
+    assert used and x2, (used, x2)
+    assert per_step <= 8, per_step
