@@ -72,6 +72,9 @@ LAUNCH_BYTES = {
     # tran_diff_tracer (lu, hhq_n, hhq_p, flux_x, flux_y, ffp in; ffn out), tracer_next_step (lu,
     # ffn, ffp, ff in; ffp, ff out)
     "hqp": (8, 8),
+    # tracer step (one-pass sequences, OCN_OPT_TRACER_STEP), per tracer: ssh, sshp, h_r, ubrtr, vbrtr, mu,
+    # ff, ffp + mask byte in (hh_init's depths and the fluxes formed, their fallback values +0.0); ffn, ffp out
+    "tr_step": (81, 81),
     "tr_fluxes": (73, 97), "tr_tracer": (57, 69), "tr_next": (41, 44),
 }
 
@@ -99,6 +102,17 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
     launch runs, i.e. a8 / a9 have work on the halo ring: blocks with neighbours; one = one-pass
     steps 1..K-1 (the first one too: nothing changes the state between the bench's calls); tracers = expl_tracer's three launches per tracer after every step, and
     hh_init's hhq_p stored by every CA / hh_init)."""
+    if tracers and one:   # tracer steps: one-pass steps, each step's tracer step run with the next step
+        z = _kc(zero)
+        out = []
+        for s in range(steps if lazy else steps - 1):
+            out.append(("onepass", "onepass" + z))
+            if s:
+                out += [("tracer_step", "tr_step")] * tracers
+        if not lazy:   # the last step, after the previous step's tracer step; the standard stages after it
+            out += [("tracer_step", "tr_step")] * tracers + [(t, k + (z if t == "onepass" else ""))
+                                                             for t, k in TAIL_LAUNCHES] + TRACER_STAGES * tracers
+        return out
     if tracers:
         out = []
         for timer, kind in call_launches(steps, flip, rc, ring, False, full_c2=True):
@@ -144,6 +158,7 @@ def call_launches(steps: int, flip: bool, rc: bool = True, ring: bool = False, o
 # the tail of an open one-pass sequence, formed by ocn_ctx_complete: the last step run again as the
 # call's last step (+ vort, the stresses, the RHS terms), a8's copies, hh_init with every level
 TAIL_LAUNCHES = [("onepass", "onepass_last"), ("copy", "copy3"), ("hh_init", "c2_full")]
+TRACER_STAGES = [("tran_diff_fluxes", "tr_fluxes"), ("tran_diff_tracer", "tr_tracer"), ("tracer_next_step", "tr_next")]
 
 
 def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one: bool = False,
@@ -162,6 +177,11 @@ def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one:
         # 3 or more are pending; the last 1 or 2 run by ocn_ctx_complete
         out += [("onepass2", "onepass2" + _kc(zero))] * ((total - 1) // 2)
         calls = []
+    if lazy and one and tracers:   # an open sequence with tracer steps: one tracer step per step but the
+        # first; the tail: the last step again, a8's copies, hh_init, the standard tracer stages
+        z = _kc(zero)
+        out += [("onepass", "onepass" + z)] * total + [("tracer_step", "tr_step")] * ((total - 1) * tracers)
+        return out + [(t, k + (z if t == "onepass" else "")) for t, k in TAIL_LAUNCHES] + TRACER_STAGES * tracers
     for n in calls:
         out += call_launches(n, flip, rc, ring, one, tracers, zero=zero, lazy=lazy, pair=pair)
     if lazy and one:

@@ -31,8 +31,11 @@ def test_step_bytes_orders():
     onez = bench.step_bytes(True, [20], flip=True, one=True, zero=True)
     assert std > flip > one > onez
     assert round(one, 2) == 140.25 and round(onez, 2) == 108.25
-    assert bench.step_bytes(True, [20], flip=True, one=True, tracers=1) == bench.step_bytes(True, [20], flip=True,
-                                                                                             tracers=1)
+    # tracer runs: the tracer steps (one-pass steps, a tracer step per step) move far less than the
+    # role-flip path with the standard tracer stages
+    trs = bench.step_bytes(True, [20], flip=True, one=True, zero=True, tracers=1)
+    trf = bench.step_bytes(True, [20], flip=True, tracers=1)
+    assert trs < trf / 2, (trs, trf)
 
 
 def test_lazy_region_launches():
