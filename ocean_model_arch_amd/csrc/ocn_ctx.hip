@@ -1192,11 +1192,19 @@ static int prebuild_plans(ocn_ctx *c)
     return OCN_OK;
 }
 
+// Timer events (OCN_OPT_STAGE_TIMING) only measure: no system-scope fence when they are recorded --
+// the default record writes back and invalidates the caches, which showed as a ~10 us gap before
+// every timed launch (rocprofv3 kernel trace) and slowed the launch after it.  A pool is made when
+// timing is switched on, so no event is created inside a timed region.
+static int make_timer_event(hipEvent_t &e)
+{
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    return OCN_OK;
+}
 static int get_event(ocn_ctx *c, hipEvent_t &e)
 {
     if (!c->event_pool.empty()) { e = c->event_pool.back(); c->event_pool.pop_back(); return OCN_OK; }
-    HIPCHK(hipEventCreate(&e));
-    return OCN_OK;
+    return make_timer_event(e);
 }
 
 static int timer_begin(ocn_ctx *c, int id, ocn_ctx::Rec &rec)
@@ -2880,7 +2888,7 @@ static int complete_open(ocn_ctx *c)
             k.last = k.one_last = k.pair = true;
             k.check = c->deferred_check[0];
             k.check2 = c->deferred_check[1];
-            return finish_call(c, one_step_fused(c, c->open_tau, k));
+            return finish_call(c, run_step(c, c->open_tau, k));
         }
         if (d == 2) {
             StepKind k1{};
@@ -2891,7 +2899,7 @@ static int complete_open(ocn_ctx *c)
         StepKind k{};
         k.last = k.one_last = true;
         k.check = c->deferred_check[d - 1];
-        return finish_call(c, one_step_fused(c, c->open_tau, k));
+        return finish_call(c, run_step(c, c->open_tau, k));
     }
     swap_roles(c);
     swap_alt3(c);
@@ -2901,7 +2909,7 @@ static int complete_open(ocn_ctx *c)
         if (pair_ok(c)) {
             StepKind k{};
             k.last = k.one_last = k.pair = true;
-            return finish_call(c, one_step_fused(c, c->open_tau, k));
+            return finish_call(c, run_step(c, c->open_tau, k));
         }
         StepKind k1{};
         k1.flip = k1.one = k1.next_one = k1.a_done = true;
@@ -2911,7 +2919,7 @@ static int complete_open(ocn_ctx *c)
     k.last = k.one_last = true;
     k.x2_end = c->ring2_saved;   // x2 steps: the second ring restored, the first exchanged (x2_end)
     c->ring2_saved = false;
-    return finish_call(c, one_step_fused(c, c->open_tau, k));
+    return finish_call(c, run_step(c, c->open_tau, k));
 }
 
 static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
@@ -3267,7 +3275,15 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     }
     switch (key) {
     case OCN_OPT_GRAPH: c->use_graph = value != 0; return OCN_OK;
-    case OCN_OPT_STAGE_TIMING: c->stage_timing = value != 0; return OCN_OK;
+    case OCN_OPT_STAGE_TIMING:
+        c->stage_timing = value != 0;
+        if (c->stage_timing) HIPCHK(hipSetDevice(c->dec.device));
+        while (c->stage_timing && c->event_pool.size() < 256) {
+            hipEvent_t e;
+            RC(make_timer_event(e));
+            c->event_pool.push_back(e);
+        }
+        return OCN_OK;
     case OCN_OPT_FUSED:
         if (c->fused != (value != 0)) drop_graphs(c);
         c->fused = value != 0;

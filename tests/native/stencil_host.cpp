@@ -135,6 +135,21 @@ extern "C" long hst_tracer(int stage, const ocn_block *b, void *const *ptr, int 
     return g_oob;
 }
 
+// The tracer step of tracer k (sw_kernels.hip launch_tracer_step: KTracerStep over the interior),
+// its ffn / filtered ffp into ffn_out / ffp_out; own = the halo points neighbour blocks own.
+extern "C" long hst_tracer_step(const ocn_block *b, void *const *ptr, int nptr, const uint8_t *bits,
+                                const float *rows, int k, double tau, double ts, unsigned own, double *ffn_out,
+                                double *ffp_out)
+{
+    g_oob = 0;
+    ocn_host_limit = (unsigned)(b->pitch * (int64_t)(b->bnd_y2 - b->bnd_y1 + 1));
+    if (bits) run(range_interior(b), KTracerStep<true>{*b, make_tab<true>(ptr, nptr, bits, rows, block_rows(b), k),
+                                                        tau, ts, own, ffn_out, ffp_out});
+    else run(range_interior(b), KTracerStep<false>{*b, make_tab<false>(ptr, nptr, nullptr, nullptr, 0, k), tau, ts,
+                                                   own, ffn_out, ffp_out});
+    return g_oob;
+}
+
 // The compact tables of a block (Prepare, thread grid = bnd range); returns the OCN_COMPACT_* flags.
 extern "C" int hst_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits, float *rows)
 {

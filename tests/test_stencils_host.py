@@ -52,6 +52,9 @@ def hst():
     L.hst_tracer.restype = C.c_long
     L.hst_tracer.argtypes = [C.c_int, C.POINTER(Block), C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                              C.c_double, C.c_double, C.c_double]
+    L.hst_tracer_step.restype = C.c_long
+    L.hst_tracer_step.argtypes = [C.POINTER(Block), C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_double,
+                                  C.c_double, C.c_uint, C.c_void_p, C.c_void_p]
     L.hst_prepare.restype = C.c_int
     L.hst_prepare.argtypes = [C.POINTER(Block), C.c_void_p, C.c_void_p, C.c_void_p]
     return L
@@ -298,3 +301,58 @@ def test_compact_row_window_is_what_the_stencils_read(hst):
 def test_frame_inner_split_partitions_the_range(hst, r, inner):
     """The halo-overlap split: frame + inner cover every point of the launch range exactly once."""
     assert hst.hst_split_ok(*r, *inner) == 1
+
+
+def _own_bits(om, b):
+    """sw_stencils.h own_class bits of block b's halo points that neighbour blocks own."""
+    own = 0
+    for d, (dm, dn) in O.DIRS.items():
+        if d in b.nbr:
+            own |= 1 << ((2 if dm > 0 else 0 if dm < 0 else 1) * 3 + (2 if dn > 0 else 0 if dn < 0 else 1))
+    return own
+
+
+@pytest.mark.parametrize("compact", [False, True])
+@pytest.mark.parametrize("name", cases.TRACER_E2E_CASES)
+def test_tracer_step_matches_expl_tracer(hst, name, compact):
+    """The tracer step (sw_stencils.h TracerStep, one launch per tracer in one-pass sequences) on the
+    state a step leaves, against the oracle's expl_tracer (control/tracer.f90:33-62: the three stages
+    with hh_init's stored depths and their exchanges) on the same state: its ffn and filtered ffp at
+    every interior sea point bit for bit, after a few steps (a moving state, nonzero fluxes)."""
+    case = cases.load_e2e(name)
+    b = case["basin"]
+    om = O.OracleModel(O.BasinConfig(nx=b["nx"], ny=b["ny"], dxst=b["dxst"], dyst=b["dyst"], rlon=b["rlon"],
+                                     rlat=b["rlat"], curve_grid=b["curve_grid"], mask=case["mask"]),
+                       O.SWConfig(**case["sw"]), *case["bxy"]).init()
+    om.run(3)
+    tau, ts = 1.0, om.sw.time_smooth
+    # step 4's shallow-water part (model.f90:146), then expl_tracer on copies
+    ntr = om.sw.tracer_num
+    expl = om.expl_tracer
+    om.expl_tracer = lambda tau=1.0: None
+    om.step(tau)
+    om.expl_tracer = expl
+    state = [{nm: a.copy(order="F") for nm, a in f.items()} for f in om.f]
+    tabs = compact_tables(hst, om) if compact else None
+    om.expl_tracer(tau)
+    bad = []
+    for k, blkk in enumerate(om.blocks):
+        g = blkk.args
+        bb = blk(g)
+        for t in range(1, ntr + 1):
+            ffn_out = state[k][f"ff1n_{t}"].copy(order="F")
+            ffp_out = state[k][f"ff1p_{t}"].copy(order="F")
+            tab = table(state[k], ntr)
+            bits, rows = (tabs[k][0].ctypes.data, tabs[k][1].ctypes.data) if compact else (None, None)
+            oob = hst.hst_tracer_step(C.byref(bb), tab, len(tab), bits, rows, t, tau, ts, _own_bits(om, blkk),
+                                      ffn_out.ctypes.data, ffp_out.ctypes.data)
+            assert oob == 0, oob
+            lu = om.f[k]["lu"] > 0.5
+            inner = np.zeros_like(lu)
+            inner[g[0] - g[4]:g[1] - g[4] + 1, g[2] - g[6]:g[3] - g[6] + 1] = True
+            sea = lu & inner
+            for nm, got, want in ((f"ff1n_{t}", ffn_out, om.f[k][f"ff1n_{t}"]), (f"ff1p_{t}", ffp_out, om.f[k][f"ff1p_{t}"]),
+                                  (f"ff1_{t}", ffn_out, om.f[k][f"ff1_{t}"])):
+                if got[sea].tobytes() != want[sea].tobytes():
+                    bad.append(f"({blkk.bm},{blkk.bn}):{nm} {int((got[sea] != want[sea]).sum())}/{int(sea.sum())}")
+    assert not bad, bad
