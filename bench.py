@@ -398,6 +398,8 @@ def main():
                          "(default), 2 = always (the general variant too), 0 = never")
     ap.add_argument("--no-multi", action="store_true",
                     help="small single blocks: one launch per step (no cooperative multi-step launch, OCN_OPT_MULTI)")
+    ap.add_argument("--no-tracer-step", action="store_true",
+                    help="tracer runs: the role-flip path with the standard tracer stages (no tracer steps, OCN_OPT_TRACER_STEP)")
     ap.add_argument("--no-batch", action="store_true",
                     help="several blocks on a GPU: one launch per block and launch group (no block batching)")
     ap.add_argument("--blocks", default=None,
@@ -469,6 +471,7 @@ def main():
     model.set_batch(not args.no_batch)
     model.set_pair(args.pair)
     model.set_multi(not args.no_multi)
+    model.set_tracer_step(not args.no_tracer_step)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -559,6 +562,7 @@ def main():
                                             "new state kept on chip") if pair else False,
                           "multi_step_launch": ("a call's steps in one cooperative launch, a grid barrier between "
                                                 "steps (OCN_OPT_MULTI)") if multi else False,
+                          "tracer_steps": model.tracer_step_active if sw.use_tracers > 0 else None,
                           "steps_per_call": spc, "calls": len(calls),
                           "call_tail": ("pending between calls (OCN_OPT_LAZY_TAIL), formed once by ocn_ctx_complete "
                                         "inside the timed region") if lazy else "formed by every call",
