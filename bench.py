@@ -165,7 +165,7 @@ def region_launches(calls, flip: bool, rc: bool = True, ring: bool = False, one:
                     tracers: int = 0, zero: bool = False, lazy: bool = False, pair: bool = False,
                     multi: bool = False):
     """The launches of a timed region: ocn_ctx_step calls of calls[i] steps each, then (lazy) the
-    pending tail formed by ocn_ctx_complete.  multi: each call of an open sequence as one cooperative
+    pending tail formed by ocn_ctx_complete.  multi: each call of an open sequence as one
     launch of its steps (OCN_OPT_MULTI; kind "<one-pass kind>*n" = n steps' bytes in one launch)."""
     out, total = [], sum(calls)
     if lazy and one and multi and not pair:
@@ -338,12 +338,20 @@ def load_valu(amd, stage: str, launch_ms: float, box, blocks):
         pl, pw = d["kernels"][stage]["per_launch"], d["kernels"][stage]["per_wave"]
         floor_ms = pl["SQ_INSTS_VALU"] * 4.0 / SIMDS / (SHADER_CLOCK_GHZ * 1e9) * 1e3
         wc = pw["SQ_WAVE_CYCLES"]
-        return {"insts_per_launch": int(pl["SQ_INSTS_VALU"]), "issue_floor_ms": round(floor_ms, 4),
-                "issue_frac": round(floor_ms / launch_ms, 4),
-                "per_wave_frac": {"valu_active": round(pw["SQ_ACTIVE_INST_VALU"] / wc, 4),
-                                  "wait_inst_any": round(pw["SQ_WAIT_INST_ANY"] / wc, 4),
-                                  "wait_any": round(pw["SQ_WAIT_ANY"] / wc, 4)},
-                "source": "profiles/sq_valu.json"}
+        out = {"insts_per_launch": int(pl["SQ_INSTS_VALU"]), "issue_floor_ms": round(floor_ms, 4),
+               "issue_frac": round(floor_ms / launch_ms, 4),
+               "per_wave_frac": {"valu_active": round(pw["SQ_ACTIVE_INST_VALU"] / wc, 4),
+                                 "wait_inst_any": round(pw["SQ_WAIT_INST_ANY"] / wc, 4),
+                                 "wait_any": round(pw["SQ_WAIT_ANY"] / wc, 4)},
+               "source": "profiles/sq_valu.json"}
+        clk = d["kernels"][stage].get("clock")
+        if clk:   # the counter pass's effective shader clock (GRBM_GUI_ACTIVE / 8 / launch time) and the
+            # VALU issue floor at that clock
+            floor_clk = pl["SQ_INSTS_VALU"] * 4.0 / SIMDS / (clk["clock_ghz"] * 1e9) * 1e3
+            out["effective_clock_ghz"] = clk["clock_ghz"]
+            out["issue_floor_ms_at_clock"] = round(floor_clk, 4)
+            out["issue_frac_at_clock"] = round(floor_clk / launch_ms, 4)
+        return out
     except Exception:
         return None
 
@@ -397,7 +405,7 @@ def main():
                     help="two one-pass steps per launch (OCN_OPT_PAIR): 1 = known-constant variants on blocks >= 512^2 "
                          "(default), 2 = always (the general variant too), 0 = never")
     ap.add_argument("--no-multi", action="store_true",
-                    help="small single blocks: one launch per step (no cooperative multi-step launch, OCN_OPT_MULTI)")
+                    help="small single blocks: one launch per step (no multi-step launch, OCN_OPT_MULTI)")
     ap.add_argument("--no-tracer-step", action="store_true",
                     help="tracer runs: the role-flip path with the standard tracer stages (no tracer steps, OCN_OPT_TRACER_STEP)")
     ap.add_argument("--no-batch", action="store_true",
@@ -560,7 +568,7 @@ def main():
                                              if one else None,
                           "onepass_pairs": ("two one-pass steps per launch (OCN_OPT_PAIR): the first step's "
                                             "new state kept on chip") if pair else False,
-                          "multi_step_launch": ("a call's steps in one cooperative launch, a grid barrier between "
+                          "multi_step_launch": ("a call's steps in one launch, a grid barrier between "
                                                 "steps (OCN_OPT_MULTI)") if multi else False,
                           "tracer_steps": model.tracer_step_active if sw.use_tracers > 0 else None,
                           "steps_per_call": spc, "calls": len(calls),

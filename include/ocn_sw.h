@@ -371,7 +371,7 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  points, 2: any variant on any block, 0: never.  Same results bit for bit.  ocn_ctx_get_option: 2 if the last
  *  ocn_ctx_step ran such launches, else whether the option is on.
  *  OCN_OPT_MULTI (default 1): in an open sequence (OCN_OPT_LAZY_TAIL) without pairs, all steps of a
- *  call in ONE cooperative launch with a grid-wide barrier between the steps, where the block is small
+ *  call in ONE launch with a grid-wide barrier between the steps, where the block is small
  *  enough for its whole grid to be resident (the launch-latency-bound case: the Black Sea basin as one
  *  block), single block without exchanges, the variant chosen on the host, check_every 0 or 1, no
  *  graph replay.  Same results bit for bit.  ocn_ctx_get_option: 2 if the last ocn_ctx_step ran one.
@@ -397,8 +397,8 @@ enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,
  * then the one-pass steps: one step, two steps per launch, two steps the second of which is the
- * call's last (the tail of an open sequence, ocn_ctx_complete), several steps in one cooperative
- * launch (OCN_OPT_MULTI), the tracer step of one-pass sequences (OCN_OPT_TRACER_STEP). */
+ * call's last (the tail of an open sequence, ocn_ctx_complete), several steps in one launch
+ * (OCN_OPT_MULTI), the tracer step of one-pass sequences (OCN_OPT_TRACER_STEP). */
 enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_TIMER_TRACER,
        OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_TIMER_ONEPASS, OCN_TIMER_ONEPASS2,
        OCN_TIMER_ONEPASS2_LAST, OCN_TIMER_ONEPASS_MULTI, OCN_TIMER_TRACER_STEP, OCN_NUM_TIMERS };

@@ -232,7 +232,7 @@ namespace ocn {
 // first of a sequence (the reference's second halo ring of the state is saved first); x2_end = a
 // last step after such a sequence (that ring restored and the state's first ring exchanged first).
 // pair = this one-pass step and the next as one launch (one_step_pair), check2 = the next one's check.
-// multi = this many one-pass steps in one cooperative launch (one_step_multi), each checked if check.
+// multi = this many one-pass steps in one launch (one_step_multi), each checked if check.
 struct StepKind {
     bool check, first, last, flip, a_done, next_a, next_reuse, rc, rc_next, one, next_one, one_last;
     bool x2, x2_save, x2_end;
@@ -274,6 +274,7 @@ struct ocn_ctx {
     bool fb_copy = false;
     int overlap = -1;            // OCN_OPT_OVERLAP: 0 none, 1 standard steps, 2 + role-flip steps, -1 auto
     int32_t *d_nbad = nullptr;
+    unsigned *d_bar = nullptr;   // the multi-step launch's grid-barrier words (kMultiBarBytes)
     ncclComm_t comm = nullptr;
     bool comm_aborted = false;         // fail_fatal aborted the communicator: calls with exchanges fail
     Loopback *lb = nullptr;            // test transport between contexts of one process (ocn_ctx_attach_loopback)
@@ -316,7 +317,7 @@ struct ocn_ctx {
     // kPairMinCells interior points, 2 on any block; pair_used: a call ran one
     int pair = 1;
     bool pair_used = false;
-    // OCN_OPT_MULTI: the one-pass steps of a small single block as one cooperative launch per call
+    // OCN_OPT_MULTI: the one-pass steps of a small single block as one launch per call
     // (one_step_multi); multi_used: the last call ran one
     bool multi = true, multi_used = false;
     // OCN_OPT_TRACER_STEP: tracer runs with one-pass steps -- expl_tracer of each step as one launch per
@@ -609,11 +610,12 @@ static int allocate(ocn_ctx *c)
     }
     // d_nbad words: 0 check_ssh_err's count, 16 the fallback check's verdict (d_fbz), 32..47 flags and
     // the vote (d_flags), 48..55 the loopback vote's reduction, 56 the count's maximum over the ranks
-    // (sync_impl), 60 the multi-step launch's barrier counter, 61 its timeout flag; then per block h_r,
-    // mu (LBlock::kc)
+    // (sync_impl), 61 the multi-step launch's barrier timeout flag; then per block h_r, mu (LBlock::kc)
     const size_t kcb = 16 * c->blocks.size();
     HIPCHK(hipMalloc(&c->d_nbad, 256 + kcb));
     c->allocs.push_back(c->d_nbad);
+    HIPCHK(hipMalloc(&c->d_bar, kMultiBarBytes));
+    c->allocs.push_back(c->d_bar);
     HIPCHK(hipMemsetAsync(c->d_nbad, 0, 256 + kcb, c->stream));
     c->d_fbz = c->d_nbad + 16;
     c->d_flags = c->d_nbad + 32;
@@ -1896,7 +1898,7 @@ static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
     return k.one_last ? last_finish(c) : OCN_OK;
 }
 
-// Several one-pass steps as one cooperative launch (sw_kernels.hip k_march_multi: a grid barrier
+// Several one-pass steps as one launch (sw_kernels.hip k_march_multi: a grid barrier
 // between the steps; the block's tiles resident together): single small block, no exchange, a
 // variant chosen on the host (multi_ok).  Step parity alternates the buffers as the role flips of
 // single launches do, so the host flips the roles k.multi times.
@@ -1908,7 +1910,7 @@ static int one_step_multi(ocn_ctx *c, double tau, const StepKind &k)
     const Compact t{b.bits, b.rows, c->march};
     RC(timer_begin(c, OCN_TIMER_ONEPASS_MULTI, rec));
     RC(launch_onepass_multi(&b.g, b.ptr.data(), (int)b.ptr.size(), &t, c->sw, tau, k.multi, k.check ? c->d_nbad : nullptr,
-                            (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, (unsigned *)(c->d_nbad + 60),
+                            (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, c->d_bar,
                             c->d_nbad + 61, s, kc_of(c, b)));
     RC(timer_end(c, rec));
     if (k.multi & 1) {
@@ -2968,7 +2970,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
                 }
                 c->deferred = 0;
                 if (!c->open_x2 && !graph_ok && nsteps >= 2 && rc == OCN_OK && multi_ok(c, check_every)) {
-                    StepKind k{};   // all the call's steps in one cooperative launch
+                    StepKind k{};   // all the call's steps in one launch
                     k.check = check_every == 1;
                     k.flip = k.one = k.next_one = k.a_done = true;
                     k.multi = nsteps;

@@ -142,11 +142,13 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                         double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
                         hipStream_t s, const OnepassKC &kc, bool last = false);
-// nsteps one-pass steps in one cooperative launch (sw_kernels.hip k_march_multi): single small block,
-// no exchange, a variant chosen on the host; step 1 reads the table's buffers, each step the buffers
+// nsteps one-pass steps in one launch (sw_kernels.hip k_march_multi): single small block, no
+// exchange, a variant chosen on the host; step 1 reads the table's buffers, each step the buffers
 // the previous one wrote (the role pairs and sshp / ubrtrp / vbrtrp against *_alt, alternating);
-// ctr: a device word for the grid barrier (zeroed on the stream first); err: ORed 1 if a barrier
-// timed out.  onepass_multi_fits: the block's grid is small enough for one resident launch.
+// ctr: kMultiBarBytes of device words for the grid barrier, at the start of their own allocation
+// (zeroed on the stream first); err: ORed 1 if a barrier timed out.  onepass_multi_fits: the block's
+// grid is small enough for one resident launch.
+constexpr size_t kMultiBarBytes = 17 * 128;   // the top counter, 8 group counters, 8 group generations
 int onepass_multi_fits(const ocn_block *b);
 int launch_onepass_multi(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                          double tau, int nsteps, int32_t *nbad, double *sshp_alt, double *up_alt, double *vp_alt,

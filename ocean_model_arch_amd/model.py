@@ -225,7 +225,7 @@ class OceanModel:
         return self
 
     def set_multi(self, on: bool = True):
-        """Small single blocks: the steps of a call (in an open sequence) as one cooperative launch
+        """Small single blocks: the steps of a call (in an open sequence) as one launch
         with a grid-wide barrier between them (default on); same results bit for bit."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MULTI, int(on)), "ocn_ctx_set_option")
         return self
@@ -250,7 +250,7 @@ class OceanModel:
 
     @property
     def multi_active(self) -> bool:
-        """Whether the last step() ran its steps as one cooperative multi-step launch."""
+        """Whether the last step() ran its steps as one multi-step launch."""
         return self.option(_lib.OPT_MULTI) == 2
 
     @property

@@ -6,9 +6,9 @@ set -u
 OUT=${OUT:-gpurun_out/sqv}
 R=$(pwd)
 mkdir -p "$OUT"
-C="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
+C="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
 ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $C --kernel-trace --output-format csv \
-    -d "$R/$OUT/sq" -o run -- python3 "$R/bench.py" --steps 6 --warmup 1 --no-cpu-baseline ${SQ_ARGS:-} ) \
+    -d "$R/$OUT/sq" -o run -- python3 "$R/bench.py" ${SQ_STEPS:---steps 20 --warmup 5} --no-cpu-baseline ${SQ_ARGS:-} ) \
     > "$OUT/sq.log" 2>&1
 rc=$?; echo "[sq valu] rc=$rc"; case $rc in 0) ;; *) exit $rc ;; esac
 python3 scripts/sq_valu.py "$OUT/sq" --box ${SQ_BOX:-4096x4096} --blocks ${SQ_BLOCKS:-1x1} > "$OUT/sq_valu.json" && cat "$OUT/sq_valu.json"

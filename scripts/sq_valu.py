@@ -4,8 +4,9 @@ JSON bench.py reads for roofline.valu.
     python scripts/sq_valu.py <sq pmc dir> --box NXxNY --blocks BXxBY > profiles/sq_valu.json
 
 Counters (one pass, scripts/gpu_sq_valu.sh): SQ_WAVES, SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU,
-SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_WAIT_INST_ANY, SQ_WAIT_ANY, SQ_ACTIVE_INST_ANY, per dispatch of
-the known-constant one-pass kernels (k_march<MarchStep<true, false, true, false, false, PAIR>>: tau a
+SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_WAIT_INST_ANY, SQ_WAIT_ANY, SQ_ACTIVE_INST_ANY and GRBM_GUI_ACTIVE
+(the effective clock of each dispatch), per dispatch of
+the known-constant one-pass kernels (k_march<MarchStep<true, false, true, false, false, PAIR, false>>: tau a
 power of two, not a last step, h_r / mu / forcing / fallback values known, one block; PAIR = two steps
 per launch) that ran -- the
 first call's gated-off variant launches (their workgroups return at once) are left out.  SQ_*_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles
@@ -22,28 +23,42 @@ from collections import defaultdict
 
 # the known-constant one-pass kernels (P2, !LAST, ZF, !X2, h_r a constant): a single step and two
 # steps per launch (PAIR)
-KERNELS = {"onepass": "MarchStep<true, false, true, false, false, false>",
-           "onepass2": "MarchStep<true, false, true, false, false, true>"}
+KERNELS = {"onepass": "MarchStep<true, false, true, false, false, false, false>",
+           "onepass2": "MarchStep<true, false, true, false, false, true, false>"}
 
 
 def summary(sq, kernel):
     # per dispatch (counters summed over the dimensions rocprofv3 reports them in)
     disp = defaultdict(lambda: defaultdict(float))
+    dur = {}
     for f in glob.glob(os.path.join(sq, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             if row.get("Kernel_Name", "").startswith(f"void ocn::k_march<ocn::{kernel}"):
                 disp[row.get("Dispatch_Id")][row["Counter_Name"]] += float(row["Counter_Value"])
+                if row.get("Start_Timestamp") and row.get("End_Timestamp"):
+                    dur[row.get("Dispatch_Id")] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9
     if not disp:
         return None
+    # the effective shader clock of each dispatch: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 / its
+    # time (MI355X_MICROARCH.md 'DVFS give-back')
+    for i, d in disp.items():
+        if "GRBM_GUI_ACTIVE" in d and dur.get(i):
+            d["clock_ghz"] = d.pop("GRBM_GUI_ACTIVE") / 8.0 / dur[i] / 1e9
+            d["launch_ms"] = dur[i] * 1e3
     # the launches that ran: with the device-side variant choice the first call also launches the
     # variants whose workgroups see another verdict and return at once
     top = max(d.get("SQ_INSTS_VALU", 0.0) for d in disp.values())
     ran = [d for d in disp.values() if d.get("SQ_INSTS_VALU", 0.0) > 0.5 * top]
     n = len(ran)
     per = {k: sum(d.get(k, 0.0) for d in ran) / n for k in ran[0]}
+    clk = {k: per.pop(k) for k in ("clock_ghz", "launch_ms") if k in per}
     waves = per.get("SQ_WAVES", 0.0)
-    return {"kernel": kernel, "dispatches": n, "per_launch": {k: round(v) for k, v in sorted(per.items())},
-            "per_wave": {k: round(v / waves, 1) for k, v in sorted(per.items())} if waves else {}}
+    out = {"kernel": kernel, "dispatches": n, "per_launch": {k: round(v) for k, v in sorted(per.items())},
+           "per_wave": {k: round(v / waves, 1) for k, v in sorted(per.items())} if waves else {}}
+    if clk:   # mean over the pass's dispatches (counter passes serialize dispatches: profiled clocks)
+        out["clock"] = {k: round(v, 4) for k, v in clk.items()}
+        out["clock"]["per_dispatch_ghz"] = [round(d["clock_ghz"], 3) for d in ran if "clock_ghz" in d]
+    return out
 
 
 def main():

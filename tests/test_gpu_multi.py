@@ -1,6 +1,6 @@
 """GPU parity of the multi-step launch (OCN_OPT_MULTI, sw_kernels.hip k_march_multi): the one-pass
 steps of a call of a small single block -- the Black Sea basin as one block, config 1 on the GPU --
-in ONE cooperative launch with a grid-wide barrier between the steps, bitwise against the reference
+in ONE launch with a grid-wide barrier between the steps, bitwise against the reference
 fixtures (model.f90:135-160 runs expl_shallow_water once per step; the launch runs the same steps).
 
 A multi-step launch needs an open sequence (OCN_OPT_LAZY_TAIL: the call continues a one-pass sequence)
