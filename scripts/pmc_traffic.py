@@ -70,8 +70,10 @@ def main():
         name = m.group(1) if m else k
         stage = STAGE.get(name)
         t = re.search(r"MarchStep<([^>]*)>", k)
-        if t and [a.strip() for a in t.group(1).split(",")][5:6] == ["true"]:   # MarchStep PAIR: two steps
-            stage, name = "onepass2", "MarchStep(pair)"
+        targs = [a.strip() for a in t.group(1).split(",")] if t else []
+        if targs[5:6] == ["true"]:   # MarchStep PAIR: two steps (LAST: the second is the call's last)
+            stage, name = ("onepass2_last", "MarchStep(pair, last)") if targs[1:2] == ["true"] else \
+                ("onepass2", "MarchStep(pair)")
         if not stage:
             continue
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
