@@ -385,6 +385,9 @@ def main():
                          "and parameters, as stored in tests/golden), without / with the tracer (configs 1 and 5)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--graph", action="store_true", help="replay steps as hipGraphs (single process)")
+    ap.add_argument("--no-stage-timing", action="store_true",
+                    help="no HIP events around the launches (diagnostic: the roofline's live launch time is then "
+                         "not measured)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stages", action="store_true", help="run the 11 reference stages instead of the fused step")
     ap.add_argument("--no-compact", action="store_true", help="fused step on the 2-D real(4) arrays")
@@ -484,7 +487,7 @@ def main():
         model.set_graph(True)
     model.init()
     model.step(args.warmup, check_every=1).synchronize()
-    model.set_stage_timing(not args.graph)
+    model.set_stage_timing(not args.graph and not args.no_stage_timing)
     model.stage_times()
 
     def barrier():
