@@ -338,6 +338,13 @@ struct ocn_ctx {
     // call may then be a one-pass step too, as a reuse step.  Never again once an r8 field's
     // device pointer was handed out (it may be written behind our back).
     mutable bool hh_consistent = false, r8_handed = false;
+    // hh_init's n level -- hqn = h_r and its interpolations hun / hvn / hhn (depth.f90:14-99 with
+    // ffs; no ssh in it) -- is what those arrays hold: a full hh_init wrote them from the current
+    // h_r, masks and metrics, and nothing has written them since (the one-pass, pair and
+    // multi-step launches never do).  last_finish's hh_init then leaves them as they are (32 B
+    // per cell of its 96 B of stores).  Cleared by every other step kind, by any upload, stage,
+    // sync or init, and never trusted once a raw pointer was handed out.
+    mutable bool hn_fresh = false;
     // the one-pass step's known-constant precondition (sw_kernels.hip FallbackCheck: fallback points
     // and forcing +0.0, h_r and mu uniform): kFbUnchecked until a check ran after the arrays last
     // changed from outside the step; kFbDevice = its verdict is in device memory (d_fbz; both
@@ -1706,9 +1713,12 @@ static int last_finish(ocn_ctx *c)
                                std::make_pair(OCN_VBRTR, OCN_VBRTRN)})
             HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr.second)], b.ptr[field_slot(pr.first)], field_bytes(b),
                                   hipMemcpyDeviceToDevice, s));
+    // (not while capturing a graph: the replays would not see hn_fresh)
+    const bool keep_n = c->hn_fresh && !c->capturing && !c->r8_handed && !c->r4_escaped;
     RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_ALL, c->sw, true, s); }));
+    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_ALL, c->sw, true, s, keep_n); }));
     RC(timer_end(c, rec));
+    c->hn_fresh = !c->capturing;
     return OCN_OK;
 }
 
@@ -1955,6 +1965,9 @@ static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
     if (k.multi) return one_step_multi(c, tau, k);
     if (k.pair) return one_step_pair(c, tau, k);
+    // every other step kind may write the n-level depths (hh_update, hh_shift, hh_init), except a
+    // single-block one-pass step (not followed by the fused hh_init + A) and the last step's march
+    if (!((k.one || k.one_last) && !k.x2 && !k.next_a && !has_exchange(c) && !c->ring_sea)) c->hn_fresh = false;
     if (k.x2) return one_step_x2(c, tau, k);
     if (k.one_last && k.x2_end) RC(x2_end(c, c->stream));
     if (k.one_last && c->tr_pending) {   // the previous state's tracer step, then its tracers' halos
@@ -2560,6 +2573,7 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
     if (is_alt_field(id)) c->alt_ok = false;
     if (is_tracer_field(id)) c->tr_alt_ok = false;
     if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_state = kFbUnchecked; c->hrx_ok = false; }
+    c->hn_fresh = false;
     if (is_alt_field(id) || id == OCN_HHQ_REST) { c->r8_escaped = true; c->coherent_known = false; }
     return c->blocks[k].ptr[field_slot(id)];
 }
@@ -2637,9 +2651,11 @@ int ocn_ctx_init_state(ocn_ctx *c)
     c->tr_pending = false;
     c->coherent_known = false;
     c->alt_ok = false; c->tr_alt_ok = false;
+    c->hn_fresh = false;
     c->fb_state = kFbUnchecked;
     const int rc = fail_fatal(c, init_state(c));
     c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // init_data.f90:60-63 ran hh_init last
+    c->hn_fresh = c->hh_consistent && !c->r4_escaped;    // (every level: the n one from h_r)
     return rc;
 }
 
@@ -2656,6 +2672,7 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
     RC(complete_open(c));
     c->coherent_known = false;
     c->hh_consistent = false;
+    c->hn_fresh = false;
     c->fb_state = kFbUnchecked;
     if (field_id == OCN_HHQ_REST) c->hrx_ok = false;
     // the current buffer's halos change; the one-pass steps' second buffer must be copied again
@@ -2673,6 +2690,7 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     c->coherent_known = false;
     c->alt_ok = false; c->tr_alt_ok = false;
     c->hh_consistent = false;
+    c->hn_fresh = false;
     c->fb_state = kFbUnchecked;
     RC(prepare_static(c));
     return envoke(c, stage_id, tau);
@@ -2691,6 +2709,7 @@ static int run_step(ocn_ctx *c, double tau, const StepKind &k)
     // pending one of the state a single-block one-pass step reads runs before its march (x2 steps
     // and the last step: after their exchanges, one_step_x2 / one_step_fused)
     if (c->tr_call && k.one && !k.x2) RC(run_tracer_step(c, tau));
+    if (!c->fused) c->hn_fresh = false;   // (the reference's stages)
     RC(c->fused ? one_step_fused(c, tau, k) : one_step(c, tau, k.check));
     if (c->tr_call && k.one) {
         c->tr_pending = true;
@@ -2705,6 +2724,7 @@ static int run_step(ocn_ctx *c, double tau, const StepKind &k)
 // by the launches, so a replay sees their current values.
 static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
 {
+    c->hn_fresh = false;   // (a replay runs whatever the captured step ran)
     for (const auto &g : c->graphs)
         if (g.tau == tau && g.kind == k && g.compact == c->compact && g.march == c->march && g.ring_sea == c->ring_sea &&
             g.role == c->role && g.kc_mode == c->kc_mode) {
@@ -3263,6 +3283,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     if (is_tracer_field(id)) c->tr_alt_ok = false;
     if (id == OCN_HHQ_REST) c->hrx_ok = false;
     c->hh_consistent = false;
+    c->hn_fresh = false;
     c->fb_state = kFbUnchecked;
     return upload_field(c, c->blocks[k], id, host, false);
 }

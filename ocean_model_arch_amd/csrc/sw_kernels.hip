@@ -1036,10 +1036,12 @@ struct MarchViewH {
 struct MarchHhInit {
     static constexpr bool kAligned = true;
     static constexpr int kHalo = 0;
-    ocn_block b; Tab<true> t; int ffs; bool full;
+    // keep_n (with full): the n level (hqn = h_r and its interpolations hun / hvn / hhn) is not
+    // stored -- the arrays hold exactly those values already (ocn_ctx.hip last_finish, hn_fresh)
+    ocn_block b; Tab<true> t; int ffs; bool full; bool keep_n = false;
     using View = MarchViewH;
     struct Fn {
-        HhInit<true> k; const Tab<true> &t; int ylast;
+        HhInit<true> k; const Tab<true> &t; int ylast; bool keep_n;
         // row n: h_r, ssh, sshp, mask bytes (+ edge values) and metrics at row n+1
         struct Batch { double nn[3], enn[3]; unsigned bits, ebits; float g[kRowTable]; };
         __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
@@ -1065,18 +1067,21 @@ struct MarchHhInit {
             const double r00 = x.rHR.c;
             if (L.out) {
                 st(k.hq, c, r00 + x.rSH.c * f);
-                if (k.full) { st(k.hqp, c, r00 + x.rSHP.c * f); st(k.hqn, c, r00); }
+                if (k.full) {
+                    st(k.hqp, c, r00 + x.rSHP.c * f);
+                    if (!keep_n) st(k.hqn, c, r00);
+                }
             }
             if (n >= k.j0 && n <= k.j1) {   // wave-uniform
                 HhInitOut o;
-                hh_init_math(x, f, k.full, o);
+                hh_init_math(x, f, k.full && !keep_n, o);
                 if (L.out && L.m >= k.i0 && L.m <= k.i1) {
                     const unsigned bc = x.bits.c;
                     const bool bu = bc & (1u << OCN_LLU), bv = bc & (1u << OCN_LLV), bh = bc & (1u << OCN_LUH);
                     if (bu) { st(k.hu, c, o.u[0]); st(k.hup, c, o.u[1]); }
                     if (bv) { st(k.hv, c, o.v[0]); st(k.hvp, c, o.v[1]); }
                     if (bh) { st(k.hh, c, o.h[0]); st(k.hhp, c, o.h[1]); }
-                    if (k.full) {
+                    if (k.full && !keep_n) {
                         if (bu) st(k.hun, c, o.u[2]);
                         if (bv) st(k.hvn, c, o.v[2]);
                         if (bh) st(k.hhn, c, o.h[2]);
@@ -1088,7 +1093,7 @@ struct MarchHhInit {
     };
     __device__ void march(const Lane &L, int nb, int ne) const
     {
-        const Fn f{make_hh_init(&b, t, ffs, full), t, b.bnd_y2};
+        const Fn f{make_hh_init(&b, t, ffs, full), t, b.bnd_y2, keep_n};
         View x{};
         const Pt c = f.k.I(L.m, nb);
         x.rHR.c = ld(f.k.h_r, c); x.rSH.c = ld(f.k.sh, c); x.rSHP.c = ld(f.k.shp, c); x.bits.c = ld(t.bits, c);
@@ -2577,12 +2582,12 @@ int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compac
 }
 
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, bool full, hipStream_t s)
+                    const ocn_sw_params &sw, bool full, hipStream_t s, bool keep_n)
 {
     if (use_march(cp)) {
         RC_K(check_block(b));
         const MarchHhInit k{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0),
-                            (int)sw.full_free_surface, full};
+                            (int)sw.full_free_surface, full, keep_n && full};
         return launch_march_part(b, range_bnd(b), part, k, s);
     }
     return launch_fused<KHhInit>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s,

@@ -293,3 +293,37 @@ def test_pair_deferral_matches_single_launches(amd, seq):
             f[op[1]][300, 280] += 1.0e-3
     bad = [nm for nm in a if nm in f and a[nm].tobytes(order="F") != f[nm].tobytes(order="F")]
     assert not bad, f"{seq}: fields differ from the oracle: {bad}"
+
+
+def test_tail_keeps_n_level_only_while_it_holds(amd):
+    """The call tail's hh_init (last_finish) leaves hqn / hun / hvn / hhn as they are while they hold
+    hh_init's n level (depth.f90:14-99: formed from h_r alone; ocn_ctx.hip hn_fresh) -- tails after
+    pairs, then an upload of h_r (the n level changes: the next tail stores it again), more tails --
+    every field against the oracle given the same uploads, after each tail."""
+    import numpy as np
+    n = 600
+    m = amd.OceanModel(amd.box_config(n)).init()
+    ref = OracleTwin(n)
+    b = m.blocks[0]
+    try:
+        m.step(3, check_every=1).synchronize()
+        ref.run(3)
+        bad = []
+        for k, calls in enumerate([[6], [6, 1], [5], [6], [2, 3]]):
+            if k == 3:   # a non-uniform rest depth from here on (the pair's h_r-reading variant)
+                h = m.download(0, "hhq_rest")
+                i, j = np.meshgrid(np.arange(h.shape[0]), np.arange(h.shape[1]), indexing="ij")
+                bump = 5.0 * np.exp(-((i - 300.0) ** 2 + (j - 250.0) ** 2) / 2.0e3)
+                h = h + np.where(h > 0.0, bump, 0.0)
+                m.upload(0, "hhq_rest", h)
+                ref.upload(b, "hhq_rest", h)
+            used = False
+            for c in calls:
+                m.step(c, check_every=1)
+                used = used or m.pair_active
+                ref.run(c)
+            bad += [f"tail {k}: {x}" for x in ref.mismatches(m)]   # (the reads form the tail)
+            assert used or k == 3, k   # (after the upload the first call waits for the variant's verdict)
+    finally:
+        m.close()
+    assert not bad, f"fields differ from the oracle: {bad}"
