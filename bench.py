@@ -349,6 +349,9 @@ def load_valu(amd, stage: str, launch_ms: float, box, blocks):
             # VALU issue floor at that clock
             floor_clk = pl["SQ_INSTS_VALU"] * 4.0 / SIMDS / (clk["clock_ghz"] * 1e9) * 1e3
             out["effective_clock_ghz"] = clk["clock_ghz"]
+            out["clock_source"] = ("GRBM_GUI_ACTIVE / 8 XCDs / dispatch time, mean over the SQ pass's dispatches of this "
+                                   "kernel (rocprofv3 --pmc over bench.py " + d.get("bench_args", "--steps 20 --warmup 5") +
+                                   "; counter passes serialize dispatches)")
             out["issue_floor_ms_at_clock"] = round(floor_clk, 4)
             out["issue_frac_at_clock"] = round(floor_clk / launch_ms, 4)
         return out
