@@ -1708,15 +1708,25 @@ static int last_finish(ocn_ctx *c)
         tt = Compact{b.bits, b.rows, c->march};
         return &tt;
     };
-    for (const LBlock &b : c->blocks)
-        for (const auto &pr : {std::make_pair(OCN_SSH, OCN_SSHN), std::make_pair(OCN_UBRTR, OCN_UBRTRN),
-                               std::make_pair(OCN_VBRTR, OCN_VBRTRN)})
-            HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr.second)], b.ptr[field_slot(pr.first)], field_bytes(b),
-                                  hipMemcpyDeviceToDevice, s));
+    // a8's copies sshn := ssh, ubrtrn := ubrtr, vbrtrn := vbrtr (the new state is in the first
+    // buffers): in the hh_init march, which reads ssh anyway (one pass instead of three copies)
+    auto copy_of = [](const LBlock &b) {
+        auto p = [&](int id) { return (double *)b.ptr[field_slot(id)]; };
+        return TailCopy{{p(OCN_SSH), p(OCN_UBRTR), p(OCN_VBRTR)}, {p(OCN_SSHN), p(OCN_UBRTRN), p(OCN_VBRTRN)}};
+    };
+    if (!c->march)
+        for (const LBlock &b : c->blocks)
+            for (const auto &pr : {std::make_pair(OCN_SSH, OCN_SSHN), std::make_pair(OCN_UBRTR, OCN_UBRTRN),
+                                   std::make_pair(OCN_VBRTR, OCN_VBRTRN)})
+                HIPCHK(hipMemcpyAsync(b.ptr[field_slot(pr.second)], b.ptr[field_slot(pr.first)], field_bytes(b),
+                                      hipMemcpyDeviceToDevice, s));
     // (not while capturing a graph: the replays would not see hn_fresh)
     const bool keep_n = c->hn_fresh && !c->capturing && !c->r8_handed && !c->r4_escaped;
     RC(timer_begin(c, OCN_STAGE_HH_INIT, rec));
-    RC(each_block(c, s, [&](const LBlock &b) { return launch_fused_c2(FT(b), OCN_PART_ALL, c->sw, true, s, keep_n); }));
+    RC(each_block(c, s, [&](const LBlock &b) {
+        const TailCopy tc = copy_of(b);
+        return launch_fused_c2(FT(b), OCN_PART_ALL, c->sw, true, s, keep_n, c->march ? &tc : nullptr);
+    }));
     RC(timer_end(c, rec));
     c->hn_fresh = !c->capturing;
     return OCN_OK;

@@ -78,9 +78,12 @@ int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compac
                     const ocn_sw_params &sw, int32_t *nbad, hipStream_t s, const double *sshp_in = nullptr,
                     const double *up_in = nullptr, const double *vp_in = nullptr);
 // keep_n (march path, full): hqn / hun / hvn / hhn already hold hh_init's n level (from h_r) and
-// are not stored again
+// are not stored again.  copy (march path, whole bnd range): also dst[k] := src[k] (the call tail's
+// a8 copies sshn := ssh, ubrtrn := ubrtr, vbrtrn := vbrtr; src[0] the ssh hh_init reads)
+struct TailCopy { const double *src[3]; double *dst[3]; };
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, bool full, hipStream_t s, bool keep_n = false);
+                    const ocn_sw_params &sw, bool full, hipStream_t s, bool keep_n = false,
+                    const TailCopy *copy = nullptr);
 // Role-flip calls: step k's hh_init (non-final) and step k+1's fused A in one launch
 // (sw_kernels.hip MarchCA); next_reuse = step k+1 is a reuse step (else A's a2 stores too);
 // skip_rc = step k+1 is a recompute step (hhq on the interior, hhu_p, hhv_p not stored).

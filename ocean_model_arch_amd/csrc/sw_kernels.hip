@@ -1025,6 +1025,7 @@ struct MarchViewH {
     RowsD<false, true, true> rHR, rSH, rSHP;           // h_r, ssh, sshp
     BitRows<false, true, true> bits;
     MetRows met;
+    double cu = 0.0, cv = 0.0;                          // (copies) ubrtr, vbrtr at row n
     OCN_MV(h_r, rHR) OCN_MV(sh, rSH) OCN_MV(shp, rSHP)
     OCN_MG_ALL
     __device__ __forceinline__ float lu(int dx, int dy) const { return bits.mask(OCN_LU, dx, dy); }
@@ -1038,12 +1039,18 @@ struct MarchHhInit {
     static constexpr int kHalo = 0;
     // keep_n (with full): the n level (hqn = h_r and its interpolations hun / hvn / hhn) is not
     // stored -- the arrays hold exactly those values already (ocn_ctx.hip last_finish, hn_fresh)
+    // copy (the call tail's a8 copies, ocn_ctx.hip last_finish): sshn := ssh, ubrtrn := ubrtr,
+    // vbrtrn := vbrtr over the bnd range with the march -- ssh is the value hh_init reads anyway
     ocn_block b; Tab<true> t; int ffs; bool full; bool keep_n = false;
+    const double *cu_src = nullptr, *cv_src = nullptr;
+    double *csh_dst = nullptr, *cu_dst = nullptr, *cv_dst = nullptr;
     using View = MarchViewH;
     struct Fn {
         HhInit<true> k; const Tab<true> &t; int ylast; bool keep_n;
-        // row n: h_r, ssh, sshp, mask bytes (+ edge values) and metrics at row n+1
-        struct Batch { double nn[3], enn[3]; unsigned bits, ebits; float g[kRowTable]; };
+        const double *cu_src, *cv_src; double *csh_dst, *cu_dst, *cv_dst;
+        // row n: h_r, ssh, sshp, mask bytes (+ edge values) and metrics at row n+1 (copies: ubrtr,
+        // vbrtr there too)
+        struct Batch { double nn[3], enn[3], uv[2]; unsigned bits, ebits; float g[kRowTable]; };
         __device__ __forceinline__ void load(Batch &q, const Lane &L, int n) const
         {
             const int r = min(n + 1, ylast);
@@ -1051,6 +1058,8 @@ struct MarchHhInit {
             q.enn[0] = q.enn[1] = q.enn[2] = 0.0;
             q.ebits = 0;
             q.nn[0] = ld(k.h_r, cn); q.nn[1] = ld(k.sh, cn); q.nn[2] = ld(k.shp, cn); q.bits = ld(t.bits, cn);
+            q.uv[0] = q.uv[1] = 0.0;
+            if (csh_dst) { q.uv[0] = ld(cu_src, cn); q.uv[1] = ld(cv_src, cn); }   // (a kernel argument: uniform)
             if (L.edge) {
                 const Pt en = k.I(L.me, r);
                 q.enn[0] = ld(k.h_r, en); q.enn[1] = ld(k.sh, en); q.enn[2] = ld(k.shp, en); q.ebits = ld(t.bits, en);
@@ -1065,6 +1074,8 @@ struct MarchHhInit {
             x.rHR.nn = q.nn[0]; x.rSH.nn = q.nn[1]; x.rSHP.nn = q.nn[2]; x.bits.nn = q.bits;
             x.rHR.enn = q.enn[0]; x.rSH.enn = q.enn[1]; x.rSHP.enn = q.enn[2]; x.bits.enn = q.ebits;
             const double r00 = x.rHR.c;
+            if (csh_dst && L.out) { st(csh_dst, c, x.rSH.c); st(cu_dst, c, x.cu); st(cv_dst, c, x.cv); }
+            x.cu = q.uv[0]; x.cv = q.uv[1];
             if (L.out) {
                 st(k.hq, c, r00 + x.rSH.c * f);
                 if (k.full) {
@@ -1093,10 +1104,11 @@ struct MarchHhInit {
     };
     __device__ void march(const Lane &L, int nb, int ne) const
     {
-        const Fn f{make_hh_init(&b, t, ffs, full), t, b.bnd_y2, keep_n};
+        const Fn f{make_hh_init(&b, t, ffs, full), t, b.bnd_y2, keep_n, cu_src, cv_src, csh_dst, cu_dst, cv_dst};
         View x{};
         const Pt c = f.k.I(L.m, nb);
         x.rHR.c = ld(f.k.h_r, c); x.rSH.c = ld(f.k.sh, c); x.rSHP.c = ld(f.k.shp, c); x.bits.c = ld(t.bits, c);
+        if (csh_dst) { x.cu = ld(cu_src, c); x.cv = ld(cv_src, c); }
         if (L.edge) {
             const Pt e = f.k.I(L.me, nb);
             x.rHR.ec = ld(f.k.h_r, e); x.rSH.ec = ld(f.k.sh, e); x.rSHP.ec = ld(f.k.shp, e); x.bits.ec = ld(t.bits, e);
@@ -2582,14 +2594,21 @@ int launch_fused_c1(const ocn_block *b, void *const *ptr, int nptr, const Compac
 }
 
 int launch_fused_c2(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int part,
-                    const ocn_sw_params &sw, bool full, hipStream_t s, bool keep_n)
+                    const ocn_sw_params &sw, bool full, hipStream_t s, bool keep_n, const TailCopy *copy)
 {
     if (use_march(cp)) {
         RC_K(check_block(b));
-        const MarchHhInit k{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0),
-                            (int)sw.full_free_surface, full, keep_n && full};
+        MarchHhInit k{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), 0),
+                      (int)sw.full_free_surface, full, keep_n && full};
+        if (copy) {
+            if (part != OCN_PART_ALL || copy->src[0] != ptr[ocn_field_slot(OCN_SSH)])
+                return set_error(OCN_ERR_ARG, "hh_init with the tail's copies: the whole bnd range, ssh as read");
+            k.cu_src = copy->src[1]; k.cv_src = copy->src[2];
+            k.csh_dst = copy->dst[0]; k.cu_dst = copy->dst[1]; k.cv_dst = copy->dst[2];
+        }
         return launch_march_part(b, range_bnd(b), part, k, s);
     }
+    if (copy) return set_error(OCN_ERR_ARG, "hh_init with the tail's copies: the march path only");
     return launch_fused<KHhInit>(range_bnd(b), inner_interior_shrunk(b), part, b, ptr, nptr, cp, 0, s,
                                  (int)sw.full_free_surface, full);
 }
