@@ -11,7 +11,7 @@ call (a synchronize() runs them, a read of the fields runs them as the last step
 import pytest
 
 from tests.golden import cases
-from tests.test_gpu_parity import OracleTwin, build_model, compare_case
+from tests.test_gpu_parity import OracleTwin, bits_equal, build_model, compare_case
 
 pytestmark = pytest.mark.gpu
 
@@ -327,3 +327,58 @@ def test_tail_keeps_n_level_only_while_it_holds(amd):
     finally:
         m.close()
     assert not bad, f"fields differ from the oracle: {bad}"
+
+
+@pytest.mark.parametrize("seed", [2, 3, 4, 5, 6])
+def test_random_call_sequences_match_oracle(amd, seed):
+    """Seeded random sequences of the entries that drive or look into an open sequence -- calls of
+    1..7 steps, tau changes, synchronize(), field reads (the tail formed), uploads of ssh and of a
+    non-uniform h_r (the variant's verdict, the tail's n level), the known-constant option toggled
+    -- on a box large enough for pairs: every field against the oracle given the same steps, taus
+    and uploads, at every read and at the end (the reference's state after each call,
+    model.f90:135-160)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    n = 600
+    m = amd.OceanModel(amd.box_config(n)).init()
+    ref = OracleTwin(n)
+    b = m.blocks[0]
+    bad, used, log = [], False, []
+    try:
+        m.step(2, check_every=1).synchronize()
+        ref.run(2)
+        for _ in range(20):
+            op = str(rng.choice(["step", "step", "step", "step", "tau", "sync", "sync", "read", "ssh", "hr", "kc"]))
+            log.append(op)
+            if op in ("step", "tau"):
+                k, tau = int(rng.integers(1, 8)), (0.5 if op == "tau" else 1.0)
+                m.step(k, tau=tau, check_every=1)
+                used = used or m.pair_active
+                log[-1] += f"{k}{'p' if m.pair_active else ''}"
+                ref.run(k, tau)
+            elif op == "sync":
+                m.synchronize()
+            elif op == "read":
+                nm = str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp"]))
+                if not bits_equal(m.download(0, nm), ref.om.f[0][nm]):
+                    bad.append(f"read {nm}")
+            elif op == "ssh":
+                s = m.download(0, "ssh")
+                s[int(rng.integers(100, 500)), int(rng.integers(100, 500))] += 1.0e-3
+                m.upload(0, "ssh", s)
+                ref.upload(b, "ssh", s)
+            elif op == "hr":
+                h = m.download(0, "hhq_rest")
+                i, j = np.meshgrid(np.arange(h.shape[0]), np.arange(h.shape[1]), indexing="ij")
+                h = h + 2.0 * np.exp(-((i - rng.integers(150, 450)) ** 2 + (j - rng.integers(150, 450)) ** 2) / 3.0e3)
+                m.upload(0, "hhq_rest", h)
+                ref.upload(b, "hhq_rest", h)
+            else:
+                on = bool(rng.integers(0, 2))
+                m.set_known_constants(on)
+                log[-1] += str(int(on))
+        bad += ref.mismatches(m)
+    finally:
+        m.close()
+    assert not bad, f"seed {seed}: fields differ from the oracle: {bad} ({log})"
+    assert used, f"no pair launch ran: {log}"
