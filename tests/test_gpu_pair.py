@@ -329,20 +329,25 @@ def test_tail_keeps_n_level_only_while_it_holds(amd):
     assert not bad, f"fields differ from the oracle: {bad}"
 
 
-@pytest.mark.parametrize("seed", [2, 3, 4, 5, 6])
-def test_random_call_sequences_match_oracle(amd, seed):
+# (seeds whose sequences reach each path: a known-constant option switched off keeps the pairs off,
+# and an h_r upload whose halos do not match the neighbour blocks keeps the x2 steps off -- the
+# library's own checks; the fields match the oracle either way)
+@pytest.mark.parametrize("layout,seed", [("pair", 3), ("pair", 5), ("pair", 6), ("pair", 8),
+                                         ("multi", 2), ("multi", 3), ("x2", 3), ("x2", 5), ("x2", 6)])
+def test_random_call_sequences_match_oracle(amd, layout, seed):
     """Seeded random sequences of the entries that drive or look into an open sequence -- calls of
     1..7 steps, tau changes, synchronize(), field reads (the tail formed), uploads of ssh and of a
     non-uniform h_r (the variant's verdict, the tail's n level), the known-constant option toggled
-    -- on a box large enough for pairs: every field against the oracle given the same steps, taus
-    and uploads, at every read and at the end (the reference's state after each call,
+    -- on a box large enough for pairs ("pair"), a small one (several steps per launch, "multi") and
+    a 3x2-block box (x2 steps with exchanges, "x2"): every field against the oracle given the same
+    steps, taus and uploads, at every read and at the end (the reference's state after each call,
     model.f90:135-160)."""
     import numpy as np
     rng = np.random.default_rng(seed)
-    n = 600
-    m = amd.OceanModel(amd.box_config(n)).init()
-    ref = OracleTwin(n)
-    b = m.blocks[0]
+    n, blocks, active = {"pair": (600, (1, 1), "pair_active"), "multi": (100, (1, 1), "multi_active"),
+                         "x2": (120, (3, 2), "x2_active")}[layout]
+    m = amd.OceanModel(amd.box_config(n), par=amd.ParallelConfig(*blocks)).init()
+    ref = OracleTwin(n, blocks)
     bad, used, log = [], False, []
     try:
         m.step(2, check_every=1).synchronize()
@@ -353,26 +358,28 @@ def test_random_call_sequences_match_oracle(amd, seed):
             if op in ("step", "tau"):
                 k, tau = int(rng.integers(1, 8)), (0.5 if op == "tau" else 1.0)
                 m.step(k, tau=tau, check_every=1)
-                used = used or m.pair_active
-                log[-1] += f"{k}{'p' if m.pair_active else ''}"
+                on = getattr(m, active)
+                used = used or on
+                log[-1] += f"{k}{'*' if on else ''}"
                 ref.run(k, tau)
             elif op == "sync":
                 m.synchronize()
             elif op == "read":
                 nm = str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp"]))
-                if not bits_equal(m.download(0, nm), ref.om.f[0][nm]):
-                    bad.append(f"read {nm}")
-            elif op == "ssh":
-                s = m.download(0, "ssh")
-                s[int(rng.integers(100, 500)), int(rng.integers(100, 500))] += 1.0e-3
-                m.upload(0, "ssh", s)
-                ref.upload(b, "ssh", s)
-            elif op == "hr":
-                h = m.download(0, "hhq_rest")
-                i, j = np.meshgrid(np.arange(h.shape[0]), np.arange(h.shape[1]), indexing="ij")
-                h = h + 2.0 * np.exp(-((i - rng.integers(150, 450)) ** 2 + (j - rng.integers(150, 450)) ** 2) / 3.0e3)
-                m.upload(0, "hhq_rest", h)
-                ref.upload(b, "hhq_rest", h)
+                for bl in m.blocks:
+                    if not bits_equal(m.download(bl.k, nm), ref.om.f[ref.k(bl)][nm]):
+                        bad.append(f"read {nm} ({bl.bm},{bl.bn})")
+            elif op in ("ssh", "hr"):
+                nm = "ssh" if op == "ssh" else "hhq_rest"
+                for bl in m.blocks:
+                    a = m.download(bl.k, nm)
+                    if op == "ssh":
+                        a[a.shape[0] // 2, a.shape[1] // 3] += 1.0e-3
+                    else:
+                        i, j = np.meshgrid(np.arange(a.shape[0]), np.arange(a.shape[1]), indexing="ij")
+                        a = a + 2.0 * np.exp(-((i - a.shape[0] / 2) ** 2 + (j - a.shape[1] / 2) ** 2) / (a.size / 40.0))
+                    m.upload(bl.k, nm, a)
+                    ref.upload(bl, nm, a)
             else:
                 on = bool(rng.integers(0, 2))
                 m.set_known_constants(on)
@@ -380,5 +387,5 @@ def test_random_call_sequences_match_oracle(amd, seed):
         bad += ref.mismatches(m)
     finally:
         m.close()
-    assert not bad, f"seed {seed}: fields differ from the oracle: {bad} ({log})"
-    assert used, f"no pair launch ran: {log}"
+    assert not bad, f"{layout} seed {seed}: fields differ from the oracle: {bad} ({log})"
+    assert used, f"{layout}: the path never ran: {log}"
