@@ -345,6 +345,10 @@ struct ocn_ctx {
     // per cell of its 96 B of stores).  Cleared by every other step kind, by any upload, stage,
     // sync or init, and never trusted once a raw pointer was handed out.
     mutable bool hn_fresh = false;
+    // hhq_n may differ from h_r (an upload of either, or a raw pointer): every hh_init stores
+    // hhq_n = h_r, but the role-flip steps' fused hh_init + A (CA) does not, so the standard tracer
+    // stages after such a step copy it first (expl_tracer)
+    mutable bool hqn_stale = false;
     // the one-pass step's known-constant precondition (sw_kernels.hip FallbackCheck: fallback points
     // and forcing +0.0, h_r and mu uniform): kFbUnchecked until a check ran after the arrays last
     // changed from outside the step; kFbDevice = its verdict is in device memory (d_fbz; both
@@ -2177,6 +2181,15 @@ static int expl_tracer(ocn_ctx *c, double tau, bool compact)
 {
     if (c->sw.use_tracers <= 0) return OCN_OK;
     RC(join_sync(c));   // an exchange a role-flip step left in flight (hh_init's hhu / hhv halos)
+    // tran_diff_tracer reads hhq_n, which the step's hh_init set to h_r (depth.f90:14-99, whole
+    // array) -- the role-flip steps' CA leaves it as it was, which is h_r unless one of them was
+    // uploaded or written through a raw pointer since the last hh_init that stored it
+    if (c->hqn_stale || c->r8_handed || c->capturing) {
+        for (const LBlock &b : c->blocks)
+            HIPCHK(hipMemcpyAsync(b.ptr[field_slot(OCN_HHQ_N)], b.ptr[field_slot(OCN_HHQ_REST)], field_bytes(b),
+                                  hipMemcpyDeviceToDevice, c->stream));
+        if (!c->capturing) c->hqn_stale = false;
+    }
     for (int k = 1; k <= c->sw.tracer_num; ++k)
         for (int stage = 0; stage < OCN_NUM_TSTAGES; ++stage) RC(tracer_stage(c, stage, k, tau, compact));
     return OCN_OK;
@@ -3292,6 +3305,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     if (is_alt_field(id)) c->alt_ok = false;
     if (is_tracer_field(id)) c->tr_alt_ok = false;
     if (id == OCN_HHQ_REST) c->hrx_ok = false;
+    if (id == OCN_HHQ_REST || id == OCN_HHQ_N) c->hqn_stale = true;
     c->hh_consistent = false;
     c->hn_fresh = false;
     c->fb_state = kFbUnchecked;

@@ -162,3 +162,37 @@ def test_tracer_steps_launches(amd):
         m.close()
     assert used and x2, (used, x2)
     assert per_step <= 8, per_step
+
+
+@pytest.mark.parametrize("path", ["tracer_steps", "role_flip", "fused"])
+def test_tracers_after_rest_depth_upload_match_oracle(amd, path):
+    """tran_diff_tracer reads hhq_n, which every hh_init sets to h_r (depth.f90:14-99) -- after an
+    upload of a non-uniform h_r the role-flip steps' fused hh_init + A (which does not store it)
+    must not leave the tracers the old one (ocn_ctx.hip expl_tracer, hqn_stale): calls of 2 and 3
+    steps after the upload, every field against the oracle given the same upload."""
+    import numpy as np
+    from tests.test_gpu_parity import OracleTwin
+    n = 100
+    sw = amd.SWConfig(use_tracers=1, tracer_num=2)
+    m = amd.OceanModel(amd.box_config(n), sw=sw)
+    if path != "tracer_steps":
+        m.set_tracer_step(False)
+    if path == "fused":
+        m.set_onepass(False)
+    m.init()
+    ref = OracleTwin(n, (1, 1), 2)
+    try:
+        m.step(2, check_every=1).synchronize()
+        ref.run(2)
+        h = m.download(0, "hhq_rest")
+        i, j = np.meshgrid(np.arange(h.shape[0]), np.arange(h.shape[1]), indexing="ij")
+        h = h + 2.0 * np.exp(-((i - 52.0) ** 2 + (j - 40.0) ** 2) / 300.0)
+        m.upload(0, "hhq_rest", h)
+        ref.upload(m.blocks[0], "hhq_rest", h)
+        for k in (2, 3):
+            m.step(k, check_every=1)
+            ref.run(k)
+        bad = ref.mismatches(m)
+    finally:
+        m.close()
+    assert not bad, f"{path}: fields differ from the oracle: {bad}"

@@ -333,7 +333,8 @@ def test_tail_keeps_n_level_only_while_it_holds(amd):
 # and an h_r upload whose halos do not match the neighbour blocks keeps the x2 steps off -- the
 # library's own checks; the fields match the oracle either way)
 @pytest.mark.parametrize("layout,seed", [("pair", 3), ("pair", 5), ("pair", 6), ("pair", 8),
-                                         ("multi", 2), ("multi", 3), ("x2", 3), ("x2", 5), ("x2", 6)])
+                                         ("multi", 2), ("multi", 3), ("x2", 3), ("x2", 5), ("x2", 6),
+                                         ("tracer", 2), ("tracer", 3), ("tracer_x2", 3), ("tracer_x2", 5)])
 def test_random_call_sequences_match_oracle(amd, layout, seed):
     """Seeded random sequences of the entries that drive or look into an open sequence -- calls of
     1..7 steps, tau changes, synchronize(), field reads (the tail formed), uploads of ssh and of a
@@ -345,9 +346,12 @@ def test_random_call_sequences_match_oracle(amd, layout, seed):
     import numpy as np
     rng = np.random.default_rng(seed)
     n, blocks, active = {"pair": (600, (1, 1), "pair_active"), "multi": (100, (1, 1), "multi_active"),
-                         "x2": (120, (3, 2), "x2_active")}[layout]
-    m = amd.OceanModel(amd.box_config(n), par=amd.ParallelConfig(*blocks)).init()
-    ref = OracleTwin(n, blocks)
+                         "x2": (120, (3, 2), "x2_active"), "tracer": (100, (1, 1), "tracer_step_active"),
+                         "tracer_x2": (120, (3, 2), "tracer_step_active")}[layout]
+    tracers = 2 if layout.startswith("tracer") else 0
+    sw = amd.SWConfig(use_tracers=1, tracer_num=tracers) if tracers else amd.SWConfig()
+    m = amd.OceanModel(amd.box_config(n), sw=sw, par=amd.ParallelConfig(*blocks)).init()
+    ref = OracleTwin(n, blocks, tracers)
     bad, used, log = [], False, []
     try:
         m.step(2, check_every=1).synchronize()
@@ -365,7 +369,7 @@ def test_random_call_sequences_match_oracle(amd, layout, seed):
             elif op == "sync":
                 m.synchronize()
             elif op == "read":
-                nm = str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp"]))
+                nm = str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp"] + (["ff1_1", "ff1p_2"] if tracers else [])))
                 for bl in m.blocks:
                     if not bits_equal(m.download(bl.k, nm), ref.om.f[ref.k(bl)][nm]):
                         bad.append(f"read {nm} ({bl.bm},{bl.bn})")
