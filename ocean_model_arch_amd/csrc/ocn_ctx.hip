@@ -1477,6 +1477,9 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
     if (exch) RC(run_sync(c, kHaloCheck, c->stream, c->d_flags));
     if (exch && c->x2) {   // one_step_x2: the rest of the state's first halo ring, and the unexchanged halos
         RC(run_sync(c, {OCN_SSHP, OCN_UBRTRP, OCN_VBRTRP}, c->stream, c->d_flags + kVoteX2));
+        // tracer steps form tran_diff_fluxes' fluxes at the halo points neighbours own (the reference
+        // exchanges them) from mu there: its first halo ring must hold the neighbours' values too
+        if (c->sw.use_tracers > 0 && c->tr_step) RC(run_sync(c, {OCN_MU}, c->stream, c->d_flags + kVoteX2));
         RC(launch_halo_zero(c, c->d_flags + kVoteX2));
     }
     RC(allreduce_max(c, c->d_flags, c->stream, kVoteUsed));
@@ -2597,7 +2600,7 @@ void *ocn_ctx_field(const ocn_ctx *c, int k, int id)
     if (is_tracer_field(id)) c->tr_alt_ok = false;
     if (!is_r4(id)) { c->r8_handed = true; c->hh_consistent = false; c->fb_state = kFbUnchecked; c->hrx_ok = false; }
     c->hn_fresh = false;
-    if (is_alt_field(id) || id == OCN_HHQ_REST) { c->r8_escaped = true; c->coherent_known = false; }
+    if (is_alt_field(id) || id == OCN_HHQ_REST || id == OCN_MU) { c->r8_escaped = true; c->coherent_known = false; }
     return c->blocks[k].ptr[field_slot(id)];
 }
 
@@ -3301,7 +3304,7 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     HIPCHK(hipStreamSynchronize(c->stream));
     if (is_r4(id)) { c->static_dirty = true; c->ext_ok = false; }
     // (the x2 checks also cover sshp / ubrtrp / vbrtrp and h_r: check_coherence)
-    if (is_flip_field(id) || is_alt_field(id) || id == OCN_HHQ_REST) c->coherent_known = false;
+    if (is_flip_field(id) || is_alt_field(id) || id == OCN_HHQ_REST || id == OCN_MU) c->coherent_known = false;
     if (is_alt_field(id)) c->alt_ok = false;
     if (is_tracer_field(id)) c->tr_alt_ok = false;
     if (id == OCN_HHQ_REST) c->hrx_ok = false;

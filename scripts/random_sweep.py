@@ -1,0 +1,24 @@
+"""Many seeds of tests/test_gpu_pair.py's random entry sequences (a bug hunt, GPU): prints the
+failures with their op logs."""
+import sys
+sys.path.insert(0, ".")
+import ocean_model_arch_amd as amd
+from tests.test_gpu_pair import _random_sequence
+
+amd.lib()
+OPS = ["step", "step", "step", "step", "tau", "sync", "read", "ssh", "hr", "kc", "uv", "mu", "rhs", "hqn", "opt",
+       "opt", "graph"]
+lo, hi = int(sys.argv[1]), int(sys.argv[2])
+nfail = 0
+for layout in ("pair", "multi", "x2", "tracer", "tracer_x2"):
+    for seed in range(lo, hi):
+        try:
+            _random_sequence(amd, layout, seed, OPS, need_path=False)
+        except AssertionError as e:
+            nfail += 1
+            print("FAIL", layout, seed, str(e)[:1500], flush=True)
+        except Exception as e:   # an OcnError etc.
+            nfail += 1
+            print("ERROR", layout, seed, type(e).__name__, str(e)[:800], flush=True)
+    print("done", layout, flush=True)
+print("failures", nfail)

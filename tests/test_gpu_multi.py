@@ -196,3 +196,33 @@ def test_tracers_after_rest_depth_upload_match_oracle(amd, path):
     finally:
         m.close()
     assert not bad, f"{path}: fields differ from the oracle: {bad}"
+
+
+def test_tracer_steps_after_inconsistent_mu_upload_match_oracle(amd):
+    """Tracer steps form tran_diff_fluxes' fluxes at the halo points neighbour blocks own (the
+    reference computes them there and exchanges them, tracer.f90:33-62) from mu at those points: a
+    per-block mu whose halos are not the neighbours' values (an upload) must not be used -- the
+    x2 check covers mu's first halo ring for tracer runs (ocn_ctx.hip check_coherence), and the
+    run takes the role-flip path: every field against the oracle, in calls of 2."""
+    import numpy as np
+    from tests.test_gpu_parity import OracleTwin
+    n, blocks = 120, (3, 2)
+    m = amd.OceanModel(amd.box_config(n), sw=amd.SWConfig(use_tracers=1, tracer_num=2),
+                       par=amd.ParallelConfig(*blocks)).init()
+    ref = OracleTwin(n, blocks, 2)
+    try:
+        m.step(2, check_every=1).synchronize()
+        ref.run(2)
+        for b in m.blocks:   # a bump per block, centred in it: the halos differ from the neighbours
+            a = m.download(b.k, "mu")
+            i, j = np.meshgrid(np.arange(a.shape[0]), np.arange(a.shape[1]), indexing="ij")
+            a = a + 50.0 * np.exp(-((i - a.shape[0] / 2) ** 2 + (j - a.shape[1] / 2) ** 2) / (a.size / 40.0))
+            m.upload(b.k, "mu", a)
+            ref.upload(b, "mu", a)
+        for k in (2, 2, 3):
+            m.step(k, check_every=1)
+            ref.run(k)
+        bad = ref.mismatches(m)
+    finally:
+        m.close()
+    assert not bad, f"fields differ from the oracle: {bad}"

@@ -340,9 +340,25 @@ def test_random_call_sequences_match_oracle(amd, layout, seed):
     1..7 steps, tau changes, synchronize(), field reads (the tail formed), uploads of ssh and of a
     non-uniform h_r (the variant's verdict, the tail's n level), the known-constant option toggled
     -- on a box large enough for pairs ("pair"), a small one (several steps per launch, "multi") and
-    a 3x2-block box (x2 steps with exchanges, "x2"): every field against the oracle given the same
-    steps, taus and uploads, at every read and at the end (the reference's state after each call,
-    model.f90:135-160)."""
+    a 3x2-block box (x2 steps with exchanges, "x2"), with and without 2 tracers: every field against
+    the oracle given the same steps, taus and uploads, at every read and at the end (the
+    reference's state after each call, model.f90:135-160)."""
+    _random_sequence(amd, layout, seed, ["step", "step", "step", "step", "tau", "sync", "sync", "read", "ssh",
+                                         "hr", "kc"], need_path=True)
+
+
+@pytest.mark.parametrize("layout,seed", [(lay, sd) for lay in ("pair", "multi", "x2", "tracer", "tracer_x2")
+                                         for sd in (11, 12, 13)])
+def test_random_entry_sequences_match_oracle(amd, layout, seed):
+    """The same with every entry the library offers between calls: uploads of the velocities, mu
+    and the forcing RHSx (the known-constant variant's verdict), of hhq_n, and every step option
+    switched at random (one-pass, pairs, several steps per launch, tracer steps, lazy tail, role
+    flip, graph replay) -- the fields are the reference's whatever path runs."""
+    _random_sequence(amd, layout, seed, ["step", "step", "step", "step", "tau", "sync", "read", "ssh", "hr",
+                                         "kc", "uv", "mu", "rhs", "hqn", "opt", "opt", "graph"], need_path=False)
+
+
+def _random_sequence(amd, layout, seed, ops, need_path):
     import numpy as np
     rng = np.random.default_rng(seed)
     n, blocks, active = {"pair": (600, (1, 1), "pair_active"), "multi": (100, (1, 1), "multi_active"),
@@ -353,11 +369,24 @@ def test_random_call_sequences_match_oracle(amd, layout, seed):
     m = amd.OceanModel(amd.box_config(n), sw=sw, par=amd.ParallelConfig(*blocks)).init()
     ref = OracleTwin(n, blocks, tracers)
     bad, used, log = [], False, []
+    reads = ["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp", "hhq_n"] + (["ff1_1", "ff1p_2"] if tracers else [])
+
+    def bump(nm, f):
+        for bl in m.blocks:
+            a = m.download(bl.k, nm)
+            a = f(a)
+            m.upload(bl.k, nm, a)
+            ref.upload(bl, nm, a)
+
+    def smooth(a, amp):
+        i, j = np.meshgrid(np.arange(a.shape[0]), np.arange(a.shape[1]), indexing="ij")
+        return amp * np.exp(-((i - a.shape[0] / 2) ** 2 + (j - a.shape[1] / 2) ** 2) / (a.size / 40.0))
+
     try:
         m.step(2, check_every=1).synchronize()
         ref.run(2)
         for _ in range(20):
-            op = str(rng.choice(["step", "step", "step", "step", "tau", "sync", "sync", "read", "ssh", "hr", "kc"]))
+            op = str(rng.choice(ops))
             log.append(op)
             if op in ("step", "tau"):
                 k, tau = int(rng.integers(1, 8)), (0.5 if op == "tau" else 1.0)
@@ -369,21 +398,36 @@ def test_random_call_sequences_match_oracle(amd, layout, seed):
             elif op == "sync":
                 m.synchronize()
             elif op == "read":
-                nm = str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp"] + (["ff1_1", "ff1p_2"] if tracers else [])))
+                nm = str(rng.choice(reads))
                 for bl in m.blocks:
                     if not bits_equal(m.download(bl.k, nm), ref.om.f[ref.k(bl)][nm]):
-                        bad.append(f"read {nm} ({bl.bm},{bl.bn})")
-            elif op in ("ssh", "hr"):
-                nm = "ssh" if op == "ssh" else "hhq_rest"
-                for bl in m.blocks:
-                    a = m.download(bl.k, nm)
-                    if op == "ssh":
-                        a[a.shape[0] // 2, a.shape[1] // 3] += 1.0e-3
-                    else:
-                        i, j = np.meshgrid(np.arange(a.shape[0]), np.arange(a.shape[1]), indexing="ij")
-                        a = a + 2.0 * np.exp(-((i - a.shape[0] / 2) ** 2 + (j - a.shape[1] / 2) ** 2) / (a.size / 40.0))
-                    m.upload(bl.k, nm, a)
-                    ref.upload(bl, nm, a)
+                        bad.append(f"read {nm} ({bl.bm},{bl.bn}) after {log}")
+            elif op == "ssh":
+                def f(a):
+                    a[a.shape[0] // 2, a.shape[1] // 3] += 1.0e-3
+                    return a
+                bump("ssh", f)
+            elif op == "hr":
+                bump("hhq_rest", lambda a: a + smooth(a, 2.0))
+            elif op == "uv":
+                bump(str(rng.choice(["ubrtr", "vbrtr"])), lambda a: a + smooth(a, 1.0e-4))
+            elif op == "mu":
+                bump("mu", lambda a: a + smooth(a, 50.0))
+            elif op == "rhs":
+                bump("RHSx", lambda a: a + smooth(a, 1.0e-7))
+            elif op == "hqn":
+                bump("hhq_n", lambda a: a + 1.0)
+            elif op == "opt":
+                which = str(rng.choice(["onepass", "pair", "multi", "tracer_step", "lazy_tail", "flip"]))
+                val = int(rng.integers(0, 3 if which == "pair" else 2))
+                {"onepass": m.set_onepass, "multi": m.set_multi, "tracer_step": m.set_tracer_step,
+                 "lazy_tail": m.set_lazy_tail, "flip": m.set_flip}.get(which, lambda v: m.set_pair(int(v)))(
+                    val if which == "pair" else bool(val))
+                log[-1] += f"-{which}{val}"
+            elif op == "graph":
+                on = bool(rng.integers(0, 2))
+                m.set_graph(on)
+                log[-1] += str(int(on))
             else:
                 on = bool(rng.integers(0, 2))
                 m.set_known_constants(on)
@@ -391,5 +435,6 @@ def test_random_call_sequences_match_oracle(amd, layout, seed):
         bad += ref.mismatches(m)
     finally:
         m.close()
-    assert not bad, f"{layout} seed {seed}: fields differ from the oracle: {bad} ({log})"
-    assert used, f"{layout}: the path never ran: {log}"
+    assert not bad, f"{layout}: fields differ from the oracle: {bad} ({log})"
+    if need_path:
+        assert used, f"{layout}: the path never ran: {log}"
