@@ -10,7 +10,8 @@ OPS = ["step", "step", "step", "step", "tau", "sync", "read", "ssh", "hr", "kc",
        "opt", "graph"]
 lo, hi = int(sys.argv[1]), int(sys.argv[2])
 nfail = 0
-for layout in ("pair", "multi", "x2", "tracer", "tracer_x2"):
+LAYOUTS = sys.argv[3].split(",") if len(sys.argv) > 3 else ["pair", "multi", "x2", "tracer", "tracer_x2"]
+for layout in LAYOUTS:
     for seed in range(lo, hi):
         try:
             _random_sequence(amd, layout, seed, OPS, need_path=False)

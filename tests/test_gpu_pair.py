@@ -348,7 +348,9 @@ def test_random_call_sequences_match_oracle(amd, layout, seed):
 
 
 @pytest.mark.parametrize("layout,seed", [(lay, sd) for lay in ("pair", "multi", "x2", "tracer", "tracer_x2")
-                                         for sd in (11, 12, 13)])
+                                         for sd in (11, 12, 13)] +
+                         [(lay, 21) for lay in ("island_pair", "island_multi", "island_x2", "island_tracer",
+                                                "island_tracer_x2")])
 def test_random_entry_sequences_match_oracle(amd, layout, seed):
     """The same with every entry the library offers between calls: uploads of the velocities, mu
     and the forcing RHSx (the known-constant variant's verdict), of hhq_n, and every step option
@@ -361,13 +363,21 @@ def test_random_entry_sequences_match_oracle(amd, layout, seed):
 def _random_sequence(amd, layout, seed, ops, need_path):
     import numpy as np
     rng = np.random.default_rng(seed)
+    base = layout.replace("island_", "")
     n, blocks, active = {"pair": (600, (1, 1), "pair_active"), "multi": (100, (1, 1), "multi_active"),
                          "x2": (120, (3, 2), "x2_active"), "tracer": (100, (1, 1), "tracer_step_active"),
-                         "tracer_x2": (120, (3, 2), "tracer_step_active")}[layout]
-    tracers = 2 if layout.startswith("tracer") else 0
+                         "tracer_x2": (120, (3, 2), "tracer_step_active")}[base]
+    tracers = 2 if base.startswith("tracer") else 0
     sw = amd.SWConfig(use_tracers=1, tracer_num=tracers) if tracers else amd.SWConfig()
-    m = amd.OceanModel(amd.box_config(n), sw=sw, par=amd.ParallelConfig(*blocks)).init()
-    ref = OracleTwin(n, blocks, tracers)
+    mask = None
+    if layout.startswith("island_"):   # land islands (mask 1), some across block boundaries
+        mask = np.zeros((n + 4, n + 4), dtype=np.int32, order="F")
+        mask[:2, :] = 1; mask[-2:, :] = 1; mask[:, :2] = 1; mask[:, -2:] = 1
+        for _ in range(4):
+            i0, j0 = int(rng.integers(4, n - 10)), int(rng.integers(4, n - 10))
+            mask[i0:i0 + int(rng.integers(1, 9)), j0:j0 + int(rng.integers(1, 9))] = 1
+    m = amd.OceanModel(amd.box_config(n, mask=mask), sw=sw, par=amd.ParallelConfig(*blocks)).init()
+    ref = OracleTwin(n, blocks, tracers, mask)
     bad, used, log = [], False, []
     reads = ["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp", "hhq_n"] + (["ff1_1", "ff1p_2"] if tracers else [])
 

@@ -37,10 +37,10 @@ class OracleTwin:
     golden fixtures do not reach (arbitrary uploaded state, a forcing, tau changes, calls split
     anywhere) are checked against the reference's algorithm, not only between two HIP paths."""
 
-    def __init__(self, n, blocks=(1, 1), tracers=0):
+    def __init__(self, n, blocks=(1, 1), tracers=0, mask=None):
         from oracle import oracle as O
         sw = O.SWConfig(use_tracers=1, tracer_num=tracers) if tracers else O.SWConfig()
-        self.om = O.OracleModel(O.BasinConfig(nx=n + 4, ny=n + 4), sw, *blocks).init()
+        self.om = O.OracleModel(O.BasinConfig(nx=n + 4, ny=n + 4, mask=mask), sw, *blocks).init()
 
     def k(self, b):
         return [i for i, ob in enumerate(self.om.blocks) if (ob.bm, ob.bn) == (b.bm, b.bn)][0]
