@@ -345,3 +345,112 @@ def test_ranks_topography_match_reference(amd, name, nranks):
             m.close()
     assert not bad, f"{name} over {nranks} ranks: fields differ from the reference: {bad}"
     assert run_ranks_case.x2 == [True] * nranks and hr == {True}, (run_ranks_case.x2, hr)
+
+
+@pytest.mark.parametrize("tracers,seed", [(0, 600), (0, 601), (2, 600), (2, 601)])
+def test_random_rank_sequences_match_oracle(amd, tracers, seed):
+    """Seeded random sequences of host entries (calls, tau changes, synchronize, reads, uploads of
+    ssh, u, mu, RHSx, hhq_n and h_r, option toggles incl. the overlap level) run by every rank of 4
+    loopback ranks (2x2 blocks: the RCCL path's plans, votes and exchanges) on its block, then
+    replayed on the oracle: every field of every block, and every read, bitwise."""
+    _ranks_sequence(amd, seed, 20, tracers=tracers)
+
+
+def _ranks_sequence(amd, seed, nops=20, tracers=0, n=120, grid=(2, 2)):
+    """The same over loopback ranks (one block per rank, the RCCL path's plans, votes and
+    exchanges): every rank runs the same seeded op list on its block; the oracle replays it after."""
+    import numpy as np
+    from tests.test_gpu_parity import OracleTwin, bits_equal
+    rng = np.random.default_rng(seed)
+    nranks = grid[0] * grid[1]
+    ops = []
+    for _ in range(nops):
+        op = str(rng.choice(["step", "step", "step", "tau", "sync", "read", "ssh", "hr", "kc", "uv", "mu", "rhs",
+                             "hqn", "opt"]))
+        if op in ("step", "tau"):
+            ops.append((op, int(rng.integers(1, 8)), 0.5 if op == "tau" else 1.0))
+        elif op == "read":
+            ops.append((op, str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp", "hhq_n"]))))
+        elif op == "opt":
+            w = str(rng.choice(["onepass", "tracer_step", "lazy_tail", "flip", "overlap"]))
+            ops.append((op, w, int(rng.integers(0, 2))))
+        elif op == "kc":
+            ops.append((op, int(rng.integers(0, 2))))
+        else:
+            ops.append((op,))
+    sw = amd.SWConfig(use_tracers=1, tracer_num=tracers) if tracers else amd.SWConfig()
+    models = [amd.OceanModel(amd.box_config(n), sw=sw, par=amd.ParallelConfig(*grid), rank=r, nranks=nranks)
+              for r in range(nranks)]
+    amd.OceanModel.attach_loopback(models)
+    rec = {}
+
+    def smooth(a, amp):
+        i, j = np.meshgrid(np.arange(a.shape[0]), np.arange(a.shape[1]), indexing="ij")
+        return amp * np.exp(-((i - a.shape[0] / 2) ** 2 + (j - a.shape[1] / 2) ** 2) / (a.size / 40.0))
+
+    fn = {"ssh": ("ssh", lambda a: a + np.where(np.arange(a.size).reshape(a.shape, order="F") == a.size // 2, 1e-3, 0.0)),
+          "hr": ("hhq_rest", lambda a: a + smooth(a, 2.0)), "uv": ("ubrtr", lambda a: a + smooth(a, 1.0e-4)),
+          "mu": ("mu", lambda a: a + smooth(a, 50.0)), "rhs": ("RHSx", lambda a: a + smooth(a, 1.0e-7)),
+          "hqn": ("hhq_n", lambda a: a + 1.0)}
+
+    def body(m):
+        m.init().step(2, check_every=1).synchronize()
+        for i, op in enumerate(ops):
+            if op[0] in ("step", "tau"):
+                m.step(op[1], tau=op[2], check_every=1)
+            elif op[0] == "sync":
+                m.synchronize()
+            elif op[0] == "read":
+                for b in m.blocks:
+                    rec[(i, b.bm, b.bn)] = m.download(b.k, op[1])
+            elif op[0] == "kc":
+                m.set_known_constants(bool(op[1]))
+            elif op[0] == "opt":
+                if op[1] == "overlap":
+                    m.set_overlap(1 if op[2] else 2)
+                else:
+                    {"onepass": m.set_onepass, "tracer_step": m.set_tracer_step, "lazy_tail": m.set_lazy_tail,
+                     "flip": m.set_flip}[op[1]](bool(op[2]))
+            else:
+                nm, f = fn[op[0]]
+                for b in m.blocks:
+                    a = f(m.download(b.k, nm))
+                    m.upload(b.k, nm, a)
+                    rec[(i, b.bm, b.bn)] = a
+        out = {}
+        for b in m.blocks:
+            for nm in m.field_names:
+                if nm in ("lu1", "rlh_c"):
+                    continue
+                out[(b.bm, b.bn, nm)] = m.download(b.k, nm)
+        return out
+
+    try:
+        res = amd.run_ranks(models, body)
+    finally:
+        for m in models:
+            m.close()
+    ref = OracleTwin(n, grid, tracers)
+    om = ref.om
+    ob = {(b.bm, b.bn): k for k, b in enumerate(om.blocks)}
+    ref.run(2)
+    bad = []
+    for i, op in enumerate(ops):
+        if op[0] in ("step", "tau"):
+            ref.run(op[1], op[2])
+        elif op[0] == "read":
+            for (bm, bn), k in ob.items():
+                if (i, bm, bn) in rec and not bits_equal(rec[(i, bm, bn)], om.f[k][op[1]]):
+                    bad.append(f"read {op[1]} ({bm},{bn}) at op {i}")
+        elif op[0] in fn:
+            nm = fn[op[0]][0]
+            for (bm, bn), k in ob.items():
+                om.f[k][nm][...] = rec[(i, bm, bn)]
+    for out in res:
+        for (bm, bn, nm), a in out.items():
+            if nm in om.f[ob[(bm, bn)]] and not bits_equal(a, om.f[ob[(bm, bn)]][nm]):
+                bad.append(f"({bm},{bn}):{nm}")
+    if bad:
+        raise AssertionError(f"ranks: fields differ from the oracle: {bad[:12]} ({ops})")
+
+

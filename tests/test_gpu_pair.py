@@ -360,7 +360,7 @@ def test_random_entry_sequences_match_oracle(amd, layout, seed):
                                          "kc", "uv", "mu", "rhs", "hqn", "opt", "opt", "graph"], need_path=False)
 
 
-def _random_sequence(amd, layout, seed, ops, need_path):
+def _random_sequence(amd, layout, seed, ops, need_path, nops=20):
     import numpy as np
     rng = np.random.default_rng(seed)
     base = layout.replace("island_", "")
@@ -395,7 +395,7 @@ def _random_sequence(amd, layout, seed, ops, need_path):
     try:
         m.step(2, check_every=1).synchronize()
         ref.run(2)
-        for _ in range(20):
+        for _ in range(nops):
             op = str(rng.choice(ops))
             log.append(op)
             if op in ("step", "tau"):
