@@ -271,7 +271,7 @@ def cpu_baseline(n_full: int = 4096):
                       "value = the all-cores leg"}
 
 
-def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for):
+def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for, watchdog=0.0):
     """Run-time check of the N > 1 path: a 512^2 box on the N-GPU block grid (RCCL halos) for
     5 steps; rank 0 recomputes the same block grid inside one process on its GPU (device-local
     halo copies, the path tests/test_gpu_parity.py pins to the reference) and compares every
@@ -281,6 +281,8 @@ def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for):
     m = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(bx, by), rank=rank, nranks=world,
                        device=local_rank)
     m.attach_comm(uid_for())
+    if watchdog > 0:
+        m.set_watchdog(watchdog)
     m.init().step(steps).synchronize()
     mine = {(b.bm, b.bn): {f: m.download(b.k, f) for f in ("ssh", "ubrtr", "vbrtr", "hhu", "str_s")}
             for b in m.blocks}
@@ -299,6 +301,31 @@ def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for):
                     ok &= a.tobytes() == ref.download(b.k, f).tobytes()
     ref.close()
     return bool(ok)
+
+
+def rccl_report(rank_info, steps: int):
+    """The multi-GPU line's `rccl` object from every rank's timed-region record: the transport
+    (ncclGetVersion, ncclCommCount), halo-exchange groups per step, each group's time on the stream
+    it ran on (pack, ncclGroupStart ... ncclGroupEnd, unpack: HIP events), and how much of it the
+    inner march hid (exposed = the comm chain's end past the inner march's end, per overlapped step)."""
+    r0 = rank_info[0]
+    grp = [r["group_ms_sum"] / r["timed_groups"] for r in rank_info if r["timed_groups"]]
+    tot_g = sum(r["group_ms_sum"] for r in rank_info)
+    tot_e = sum(r["exposed_ms_sum"] for r in rank_info)
+    return {"transport": r0["comm"]["transport"], "version": r0["comm"]["version"],
+            "comm_size": r0["comm"]["comm_size"],
+            "groups_per_step": round(max(r["groups"] for r in rank_info) / steps, 3),
+            "group_ms": {"mean": round(sum(grp) / len(grp), 4) if grp else None,
+                         "max": round(max(r["group_ms_max"] for r in rank_info), 4)},
+            "exposed_ms_per_step": round(max(r["exposed_ms_sum"] for r in rank_info) / steps, 4),
+            "hidden_frac": round(1.0 - tot_e / tot_g, 4) if tot_g > 0 else None,
+            "watchdog_s": r0["comm"]["watchdog_s"],
+            "per_rank": [{"rank": r["rank"], "groups": r["groups"],
+                          "group_ms_mean": round(r["group_ms_sum"] / r["timed_groups"], 4) if r["timed_groups"] else None,
+                          "group_ms_max": round(r["group_ms_max"], 4),
+                          "exposed_ms_per_step": round(r["exposed_ms_sum"] / steps, 4)} for r in rank_info],
+            "source": "HIP events on the stream of each exchange (OCN_TIMER_EXCHANGE / OCN_TIMER_EXPOSED, "
+                      "ocn_ctx_stage_stats); groups = ocn_ctx_comm_info exchanges in the timed region"}
 
 
 def load_traffic(amd, stage: str, cells: int, compact: bool, box, blocks):
@@ -416,6 +443,10 @@ def main():
                     help="tracer runs: the role-flip path with the standard tracer stages (no tracer steps, OCN_OPT_TRACER_STEP)")
     ap.add_argument("--no-batch", action="store_true",
                     help="several blocks on a GPU: one launch per block and launch group (no block batching)")
+    ap.add_argument("--watchdog", type=float, default=120.0,
+                    help="N > 1: seconds a library call that may wait on a peer (step, synchronize, ...) may take "
+                         "before the rank's watchdog aborts the RCCL communicator and the rank exits non-zero "
+                         "(ocn_ctx_set_watchdog; 0 = off)")
     ap.add_argument("--blocks", default=None,
                     help="block grid BXxBY (default: one block per GPU); with one GPU, several blocks on it "
                          "exercise the halo-exchange path without RCCL")
@@ -472,7 +503,9 @@ def main():
             dist.broadcast_object_list(uid, src=0)
             return uid[0]
         model.attach_comm(uid_for())
-        parity = multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for)
+        if args.watchdog > 0:   # a rank stuck on a peer ends with a message, not a silent time-out
+            model.set_watchdog(args.watchdog)
+        parity = multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for, args.watchdog)
     model.set_fused(not args.stages)
     model.set_compact(not args.no_compact)
     model.set_march(not args.no_march)
@@ -492,6 +525,7 @@ def main():
     model.step(args.warmup, check_every=1).synchronize()
     model.set_stage_timing(not args.graph and not args.no_stage_timing)
     model.stage_times()
+    xchg0 = model.comm_info()["exchanges"]
 
     def barrier():
         if world > 1:
@@ -513,7 +547,8 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     launches = amd._lib.launch_count() - n_launch0
-    times = model.stage_times()
+    stats = model.stage_stats()
+    times = {k: (v[0], v[1]) for k, v in stats.items()}
     compact = model.compact_active
     flip = model.flip_active
     rc = model.recompute_active
@@ -523,10 +558,20 @@ def main():
     pair = ("onepass2" in times or "onepass2_last" in times) if times else model.pair_active
     multi = ("onepass_multi" in times) if times else model.multi_active
     model_overlap = model.overlap_level
+    rank_info = None
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        # per rank: the exchanges of the timed region (events on the stream each runs on) and the
+        # dominant launch's time, for the rccl object and the per-GPU roofline (rank 0 reports)
+        ci = model.comm_info()
+        ex, exp_ = stats.get("exchange", (0.0, 0, 0.0)), stats.get("exposed", (0.0, 0, 0.0))
+        mine = {"rank": rank, "comm": ci, "groups": ci["exchanges"] - xchg0, "timed_groups": ex[1],
+                "group_ms_sum": ex[0], "group_ms_max": ex[2], "exposed_ms_sum": exp_[0], "exposed_n": exp_[1],
+                "stage_ms": {s: v[0] / v[1] for s, v in stats.items() if v[1]}, "cells": model.interior_cells}
+        rank_info = [None] * world
+        dist.all_gather_object(rank_info, mine)
 
     cells = nxbox * nybox
     value = cells * args.steps / dt
@@ -603,8 +648,18 @@ def main():
                                  for s, v in stage_ms.items()}
         if world > 1:
             out["multi_gpu_parity_512"] = parity
+            out["rccl"] = rccl_report(rank_info, args.steps)
+            if roof:   # the dominant launch on every GPU (its own block's cells, its own launch time)
+                roof["per_gpu"] = [
+                    {"rank": r["rank"], "launch_ms": round(r["stage_ms"][roof["kernel"]], 4),
+                     "frac": round(kbytes[roof["kernel"]] * r["cells"] / (r["stage_ms"][roof["kernel"]] * 1e-3) / 1e9 /
+                                   HBM_PEAK_GBS, 4)}
+                    for r in rank_info if roof["kernel"] in r["stage_ms"]]
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
+        elif world > 1:
+            out["cpu_baseline"] = {"value": None, "reason": "timed at N=1 only (the same host CPU path; the "
+                                                            "N=1 line of the scaling run carries it)"}
     model.close()
     if world > 1:
         dist.destroy_process_group()

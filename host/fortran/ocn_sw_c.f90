@@ -30,6 +30,15 @@ module ocn_sw_c
     integer(c_int), parameter :: OCN_STAGE_CHECK_SSH_ERR = 10
     integer(c_int), parameter :: OCN_TSTAGE_TRAN_DIFF_FLUXES = 0, OCN_TSTAGE_TRAN_DIFF_TRACER = 1, &
                                  OCN_TSTAGE_TRACER_NEXT_STEP = 2
+    ! execution options (ocn_ctx_set_option / ocn_ctx_get_option)
+    integer(c_int32_t), parameter :: OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3,        &
+                                     OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5, OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7,  &
+                                     OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9, OCN_OPT_KNOWN_CONSTANTS = 10,     &
+                                     OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13,           &
+                                     OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16,                    &
+                                     OCN_OPT_TRACER_STEP = 17, OCN_OPT_MULTI_SPIN = 18
+    integer(c_int32_t), parameter :: OCN_HALO_LOCAL = 0, OCN_HALO_SEND = 1, OCN_HALO_RECV = 2
+    integer, parameter :: OCN_UNIQUE_ID_BYTES = 128   ! sizeof(ncclUniqueId)
 
     type, bind(C) :: ocn_block
         integer(c_int32_t) :: nx_start, nx_end, ny_start, ny_end
@@ -58,6 +67,22 @@ module ocn_sw_c
         type(ocn_block) :: geom
         integer(c_int32_t) :: bm, bn
         integer(c_int32_t) :: nbr_rank(8), nbr_k(8)
+    end type
+
+    ! one copy / message of a halo exchange (ocn_halo_schedule)
+    type, bind(C) :: ocn_halo_msg
+        integer(c_int32_t) :: kind, peer, k, k_src, field
+        integer(c_int32_t) :: dst_x0, dst_x1, dst_y0, dst_y1
+        integer(c_int32_t) :: src_x0, src_x1, src_y0, src_y1
+        integer(c_int32_t) :: count
+        integer(c_int64_t) :: offset
+    end type
+
+    ! the transport of a context (ocn_ctx_comm_info): 0 none, 1 RCCL, 2 loopback
+    type, bind(C) :: ocn_comm_info
+        integer(c_int32_t) :: transport, nccl_version, comm_size, comm_rank
+        integer(c_int64_t) :: exchanges, exchanges_done
+        real(c_double) :: watchdog_s
     end type
 
     interface
@@ -217,6 +242,67 @@ module ocn_sw_c
             integer(c_int), value :: k, id
             real(c_float), value :: undef
             type(c_ptr), value :: host
+        end function
+        integer(c_int) function ocn_ctx_upload(ctx, k, id, host) bind(C, name='ocn_ctx_upload')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: ctx
+            integer(c_int), value :: k, id
+            type(c_ptr), value :: host
+        end function
+        integer(c_int) function ocn_ctx_set_option(ctx, key, val) bind(C, name='ocn_ctx_set_option')
+            import :: c_int, c_int32_t, c_int64_t, c_ptr
+            type(c_ptr), value :: ctx
+            integer(c_int32_t), value :: key
+            integer(c_int64_t), value :: val
+        end function
+        integer(c_int) function ocn_ctx_get_option(ctx, key, val) bind(C, name='ocn_ctx_get_option')
+            import :: c_int, c_int32_t, c_int64_t, c_ptr
+            type(c_ptr), value :: ctx
+            integer(c_int32_t), value :: key
+            integer(c_int64_t), intent(out) :: val
+        end function
+        ! ---------------------------------------------------------------- ranks (shared/mpp/mpp.f90:64-221)
+        ! host-only: the blocks rank dec%rank owns (core/decomposition.f90:614-669), and one exchange's
+        ! copies / messages (shared/mpp/syncborder_block2D_gen_all.fi)
+        integer(c_int) function ocn_decompose(basin, dec, mask, out, cap, count) bind(C, name='ocn_decompose')
+            import :: c_int, c_int32_t, c_ptr, ocn_basin, ocn_decomp
+            type(ocn_basin), intent(in) :: basin
+            type(ocn_decomp), intent(in) :: dec
+            type(c_ptr), value :: mask, out
+            integer(c_int32_t), value :: cap
+            integer(c_int32_t), intent(out) :: count
+        end function
+        integer(c_int) function ocn_halo_schedule(basin, dec, mask, field_ids, nfields, out, cap, count) &
+                                                  bind(C, name='ocn_halo_schedule')
+            import :: c_int, c_int32_t, c_ptr, ocn_basin, ocn_decomp
+            type(ocn_basin), intent(in) :: basin
+            type(ocn_decomp), intent(in) :: dec
+            type(c_ptr), value :: mask, field_ids
+            integer(c_int32_t), value :: nfields
+            type(c_ptr), value :: out
+            integer(c_int32_t), value :: cap
+            integer(c_int32_t), intent(out) :: count
+        end function
+        ! RCCL: rank 0 makes the unique id (128 bytes), the host hands it to every rank, each attaches
+        integer(c_int) function ocn_comm_unique_id(out_id, nbytes) bind(C, name='ocn_comm_unique_id')
+            import :: c_int, c_int32_t, c_ptr
+            type(c_ptr), value :: out_id
+            integer(c_int32_t), value :: nbytes
+        end function
+        integer(c_int) function ocn_ctx_attach_comm(ctx, unique_id, nbytes) bind(C, name='ocn_ctx_attach_comm')
+            import :: c_int, c_int32_t, c_ptr
+            type(c_ptr), value :: ctx, unique_id
+            integer(c_int32_t), value :: nbytes
+        end function
+        integer(c_int) function ocn_ctx_comm_info(ctx, info) bind(C, name='ocn_ctx_comm_info')
+            import :: c_int, c_ptr, ocn_comm_info
+            type(c_ptr), value :: ctx
+            type(ocn_comm_info), intent(out) :: info
+        end function
+        integer(c_int) function ocn_ctx_set_watchdog(ctx, seconds) bind(C, name='ocn_ctx_set_watchdog')
+            import :: c_int, c_double, c_ptr
+            type(c_ptr), value :: ctx
+            real(c_double), value :: seconds
         end function
         type(c_ptr) function ocn_last_error() bind(C, name='ocn_last_error')
             import :: c_ptr

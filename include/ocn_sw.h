@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define OCN_ABI_VERSION 4
+#define OCN_ABI_VERSION 5
 
 enum {
     OCN_OK = 0,
@@ -256,13 +256,34 @@ void *ocn_ctx_stream(const ocn_ctx *ctx);
 /* RCCL: unique id (128 bytes) made on rank 0, broadcast by the host, then attached. */
 int ocn_comm_unique_id(void *out_id, int32_t nbytes);
 int ocn_ctx_attach_comm(ocn_ctx *ctx, const void *unique_id, int32_t nbytes);
-/* Test transport: the n ranks of one decomposition as n contexts of ONE process on one device
+/* Test transport: the n ranks of one decomposition as n contexts of ONE process on one device (n >= 1)
  * (ctxs[i] = rank i of nranks = n), each then driven by its own host thread.  Replaces only the
  * RCCL calls (the per-peer ncclRecv/ncclSend of an exchange become device copies between the
  * contexts' message buffers behind event handshakes; the role-flip vote's ncclAllReduce a device
  * max over the contexts); every other part of the multi-rank path is the production one.  Call
  * before ocn_ctx_init_state; the contexts may be destroyed in any order. */
 int ocn_ctx_attach_loopback(ocn_ctx *const *ctxs, int32_t n);
+
+/* What a multi-rank run reports about its transport (bench.py's `rccl` object): transport 0 = none,
+ * 1 = RCCL (nccl_version = ncclGetVersion, comm_size / comm_rank = ncclCommCount /
+ * ncclCommUserRank), 2 = loopback; exchanges = halo exchanges with remote peers enqueued so far (one
+ * ncclGroupStart ... ncclGroupEnd group each), exchanges_done = the id of the last of them whose end
+ * the device has reached (polled from events while a watchdog is set, else -1). */
+typedef struct ocn_comm_info {
+    int32_t transport, nccl_version, comm_size, comm_rank;
+    int64_t exchanges, exchanges_done;
+    double watchdog_s;
+} ocn_comm_info;
+int ocn_ctx_comm_info(ocn_ctx *ctx, ocn_comm_info *out);
+/* Host-side watchdog (seconds > 0; 0 = off): a thread of the context watches every call that may
+ * take part in a collective (init_state, step, complete, synchronize, sync, stage, tracer_stage,
+ * download, upload, output_r4).  One that has not returned after `seconds` is ended: the watchdog
+ * prints "ocn watchdog: rank R of N: <call> ... last completed exchange id D of E" to stderr, aborts
+ * the RCCL communicator (ncclCommAbort: RCCL's kernels waiting on a peer exit) or fails the loopback
+ * group, and the call returns OCN_ERR_COMM with that message; if it still has not returned 10 s
+ * later, the watchdog ends the process with exit status 3 (no exec).  The reference's analogue is
+ * abort_model -> mpi_abort (shared/errors.f90:30-37), which has no timeout of its own. */
+int ocn_ctx_set_watchdog(ocn_ctx *ctx, double seconds);
 
 /* Bottom topography (basin.par line 20, control/init_data.f90:111-121): the real(4) file's values,
  * the (nx-4) x (ny-4) interior points in Fortran order (tools/io.f90:84-176 read_data2D_real4);
@@ -281,7 +302,13 @@ int ocn_ctx_tracer_stage(ocn_ctx *ctx, int stage_id, int tracer, double tau);
 /* nsteps model steps (model.f90:146-160): expl_shallow_water(tau), then expl_tracer(tau) when
  * use_tracers > 0.  check_every: run check_ssh_err every N steps (0 = never). */
 int ocn_ctx_step(ocn_ctx *ctx, double tau, int32_t nsteps, int32_t check_every);
-/* Wait for the context's stream; returns OCN_ERR_BLOWUP if a check found |ssh| >= 1e4. */
+/* Wait for the context's stream; returns OCN_ERR_BLOWUP if a check found |ssh| >= 1e4, and
+ * OCN_ERR_HIP if a multi-step launch's grid barrier timed out since the last synchronize (the
+ * results are invalid; ocn_ctx_init_state starts over).  With a communicator attached (RCCL or
+ * loopback) this is a COLLECTIVE: the blow-up counts are max-reduced over the ranks
+ * (check_ssh_err_kernel -> abort_model stops every rank, shared/errors.f90:30-37), so every rank
+ * must call it, in the same order relative to its steps; a rank that skips it leaves the others
+ * waiting in the reduction. */
 int ocn_ctx_synchronize(ocn_ctx *ctx);
 /* Form a pending call tail now (OCN_OPT_LAZY_TAIL): afterwards every array holds what the
  * reference leaves after the last step run.  Every entry that reads or writes fields, hands out a
@@ -381,6 +408,10 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  runs the standard tracer stages.  Needs the call's first step to be a one-pass step, and with
  *  exchanges the x2 steps; no graph replay.  Same results bit for bit.  ocn_ctx_get_option: 2 if the
  *  last ocn_ctx_step used them.
+ *  OCN_OPT_MULTI_SPIN (diagnostics; default 1 << 20, about 0.5 s): the multi-step launch's grid
+ *  barrier gives up after this many polls -- the launch's workgroups end and ocn_ctx_synchronize
+ *  returns OCN_ERR_HIP instead of the device hanging if the grid was not co-resident.  Tests set it
+ *  to 1 to exercise that path.
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
  * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
@@ -392,20 +423,29 @@ int ocn_ctx_get_option(const ocn_ctx *ctx, int32_t key, int64_t *value);
 enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT_FUSED = 4, OCN_OPT_COMPACT = 5,
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9,
        OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13,
-       OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16, OCN_OPT_TRACER_STEP = 17 };
+       OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16, OCN_OPT_TRACER_STEP = 17,
+       OCN_OPT_MULTI_SPIN = 18 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,
  * then the one-pass steps: one step, two steps per launch, two steps the second of which is the
  * call's last (the tail of an open sequence, ocn_ctx_complete), several steps in one launch
- * (OCN_OPT_MULTI), the tracer step of one-pass sequences (OCN_OPT_TRACER_STEP). */
+ * (OCN_OPT_MULTI), the tracer step of one-pass sequences (OCN_OPT_TRACER_STEP), then the halo
+ * exchanges with remote peers and the exposed part of the overlapped ones (ocn_ctx_stage_stats). */
 enum { OCN_TIMER_FUSED_A = OCN_NUM_STAGES, OCN_TIMER_FUSED_B, OCN_TIMER_FUSED_C1, OCN_TIMER_TRACER,
        OCN_TIMER_FUSED_CA = OCN_TIMER_TRACER + OCN_NUM_TSTAGES, OCN_TIMER_ONEPASS, OCN_TIMER_ONEPASS2,
-       OCN_TIMER_ONEPASS2_LAST, OCN_TIMER_ONEPASS_MULTI, OCN_TIMER_TRACER_STEP, OCN_NUM_TIMERS };
+       OCN_TIMER_ONEPASS2_LAST, OCN_TIMER_ONEPASS_MULTI, OCN_TIMER_TRACER_STEP, OCN_TIMER_EXCHANGE,
+       OCN_TIMER_EXPOSED, OCN_NUM_TIMERS };
 
 /* Per-timer device time (ms, summed) and launch counts since the last call, from the HIP
  * events of OCN_OPT_STAGE_TIMING; arrays of OCN_NUM_TIMERS entries.  Synchronises. */
 int ocn_ctx_stage_times(ocn_ctx *ctx, double *ms, int64_t *counts);
+/* The same, plus the longest single record per timer (ms_max; may be NULL).  OCN_TIMER_EXCHANGE:
+ * one halo exchange with remote peers (pack, the RCCL group / loopback copies, unpack) on the
+ * stream that runs it; OCN_TIMER_EXPOSED: per overlapped step, how long the comm stream's chain
+ * (exchange + frame march) outlasted the compute stream's inner march -- the part of the exchange
+ * not hidden (0 when hidden). */
+int ocn_ctx_stage_stats(ocn_ctx *ctx, double *ms, int64_t *counts, double *ms_max);
 
 const char *ocn_last_error(void);
 int ocn_abi_version(void);

@@ -66,7 +66,8 @@ STAGES = ["sw_update_ssh", "hh_update", "uv_trans_vort", "uv_trans", "stress_com
 STAGE_ID = {n: i for i, n in enumerate(STAGES)}
 TSTAGES = ["tran_diff_fluxes", "tran_diff_tracer", "tracer_next_step"]
 TSTAGE_ID = {n: i for i, n in enumerate(TSTAGES)}
-TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES + ["fused_ca", "onepass", "onepass2", "onepass2_last", "onepass_multi", "tracer_step"]    # OCN_NUM_TIMERS slots
+TIMERS = STAGES + ["fused_a", "fused_b", "fused_c1"] + TSTAGES + ["fused_ca", "onepass", "onepass2", "onepass2_last", "onepass_multi", "tracer_step",
+                                                                       "exchange", "exposed"]    # OCN_NUM_TIMERS slots
 OPT_GRAPH = 1
 OPT_OVERLAP = 2
 OPT_STAGE_TIMING = 3
@@ -84,6 +85,7 @@ OPT_BATCH = 14
 OPT_PAIR = 15
 OPT_MULTI = 16
 OPT_TRACER_STEP = 17
+OPT_MULTI_SPIN = 18
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",
@@ -93,7 +95,8 @@ KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "oc
 CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_destroy", "ocn_ctx_block_count", "ocn_ctx_block_info",
                "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm", "ocn_ctx_attach_loopback",
                "ocn_ctx_set_topography", "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
-               "ocn_ctx_download", "ocn_ctx_complete", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_last_error", "ocn_abi_version",
+               "ocn_ctx_download", "ocn_ctx_complete", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_ctx_stage_stats",
+               "ocn_ctx_comm_info", "ocn_ctx_set_watchdog", "ocn_last_error", "ocn_abi_version",
                "ocn_build_id", "ocn_launch_count"]
 ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
 
@@ -141,6 +144,12 @@ class OcnHaloMsg(C.Structure):
                 ("field", C.c_int32), ("dst_x0", C.c_int32), ("dst_x1", C.c_int32), ("dst_y0", C.c_int32),
                 ("dst_y1", C.c_int32), ("src_x0", C.c_int32), ("src_x1", C.c_int32), ("src_y0", C.c_int32),
                 ("src_y1", C.c_int32), ("count", C.c_int32), ("offset", C.c_int64)]
+
+
+class OcnCommInfo(C.Structure):
+    _fields_ = [("transport", C.c_int32), ("nccl_version", C.c_int32), ("comm_size", C.c_int32),
+                ("comm_rank", C.c_int32), ("exchanges", C.c_int64), ("exchanges_done", C.c_int64),
+                ("watchdog_s", C.c_double)]
 
 
 HALO_LOCAL, HALO_SEND, HALO_RECV = 0, 1, 2
@@ -200,6 +209,9 @@ def lib() -> C.CDLL:
     L.ocn_ctx_set_option.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
     L.ocn_ctx_get_option.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]
     L.ocn_ctx_stage_times.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ocn_ctx_stage_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ocn_ctx_comm_info.argtypes = [C.c_void_p, C.POINTER(OcnCommInfo)]
+    L.ocn_ctx_set_watchdog.argtypes = [C.c_void_p, C.c_double]
     L.ocn_ctx_attach_comm.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     L.ocn_comm_unique_id.argtypes = [C.c_void_p, C.c_int32]
     L.ocn_ctx_attach_loopback.argtypes = [C.POINTER(C.c_void_p), C.c_int32]

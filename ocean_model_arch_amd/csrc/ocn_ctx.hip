@@ -19,10 +19,14 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ocn_internal.h"
@@ -384,6 +388,28 @@ struct ocn_ctx {
     bool ring2_saved = false, x2_used = false;
     bool fb_x2 = false;          // the known-constant check's verdict is for the x2 range / tables
     mutable bool coherent_known = false, r8_escaped = false;
+    int multi_spin = kMultiSpin;   // OCN_OPT_MULTI_SPIN (the multi-step launch's barrier bound)
+    double stage_max[OCN_NUM_TIMERS] = {0};   // longest record per timer (ocn_ctx_stage_stats)
+    // halo exchanges with remote peers (run_sync): how many were enqueued; while a watchdog is set an
+    // event after each (xq, under xmu) tells it the id of the last one the device completed (xdone)
+    int64_t xchg = 0, xdone = -1;
+    std::mutex xmu;
+    std::deque<std::pair<int64_t, hipEvent_t>> xq;
+    std::vector<hipEvent_t> xpool;
+    // host-side watchdog (ocn_ctx_set_watchdog): the thread, the call it watches (call_depth > 0: a
+    // guarded entry is running since call_t0), and whether it fired (wd_msg: what the calls return)
+    double wd_s = 0;
+    std::thread wd;
+    std::mutex wd_mu;
+    std::condition_variable wd_cv;
+    bool wd_stop = false;
+    int call_depth = 0;
+    std::chrono::steady_clock::time_point call_t0;
+    const char *call_name = "";
+    std::atomic<bool> wd_fired{false};
+    std::string wd_msg;
+    std::mutex comm_mu;          // the communicator is aborted once: by the watchdog or by fail_fatal
+    bool comm_abort_done = false;
     int role = 0;
     int steps_run = 0;           // launches statistics of the last call (ocn_ctx_get_option OCN_OPT_LAUNCHES)
     int64_t launches = 0;
@@ -861,10 +887,113 @@ static int lb_fail_on_error(ocn_ctx *c, int rc)
 static int fail_fatal(ocn_ctx *c, int rc)
 {
     rc = lb_fail_on_error(c, rc);
-    if (rc && rc != OCN_ERR_BLOWUP && rc != OCN_ERR_ARG && c->comm) {
+    if ((rc && rc != OCN_ERR_BLOWUP && rc != OCN_ERR_ARG) || c->wd_fired.load()) {
+        std::lock_guard<std::mutex> g(c->comm_mu);
+        if (c->comm) {
+            if (!c->comm_abort_done) (void)ncclCommAbort(c->comm);   // (the watchdog may have)
+            c->comm_abort_done = true;
+            c->comm = nullptr;
+            c->comm_aborted = true;
+        }
+    }
+    return rc;
+}
+
+// ------------------------------------------------------------------ host-side watchdog
+// ocn_ctx_set_watchdog: a thread per context watches the entries that may take part in a collective
+// (guarded below).  One that has not returned after wd_s is ended: the message names the call and the
+// last exchange with remote peers the device completed (polled from c->xq), the RCCL communicator is
+// aborted (RCCL's kernels waiting on a peer exit, so the call's stream wait returns) or the loopback
+// group failed (its rendezvous return), and the call returns OCN_ERR_COMM with the message.  A call
+// still stuck 10 s later ends the process (exit status 3).
+static int64_t poll_xdone(ocn_ctx *c)
+{
+    std::lock_guard<std::mutex> g(c->xmu);
+    while (!c->xq.empty() && hipEventQuery(c->xq.front().second) == hipSuccess) {
+        c->xdone = c->xq.front().first;
+        c->xpool.push_back(c->xq.front().second);
+        c->xq.pop_front();
+    }
+    return c->xdone;
+}
+
+static void wd_fire(ocn_ctx *c, const char *call, double waited)
+{
+    const int64_t done = poll_xdone(c);
+    char buf[512];
+    std::snprintf(buf, sizeof buf,
+                  "ocn watchdog: rank %d of %d: %s has not returned after %.1f s (limit %.1f s); last completed "
+                  "exchange id %lld of %lld enqueued; %s",
+                  c->dec.rank, c->dec.nranks, call, waited, c->wd_s, (long long)done, (long long)c->xchg,
+                  c->lb ? "failing the loopback group" : c->comm ? "aborting the RCCL communicator" : "no communicator");
+    c->wd_msg = buf;
+    c->wd_fired.store(true);
+    std::fprintf(stderr, "%s\n", buf);
+    std::fflush(stderr);
+    if (c->lb) {
+        std::lock_guard<std::mutex> g(c->lb->mu);
+        c->lb->failed = true;
+        c->lb->cv.notify_all();
+    }
+    std::lock_guard<std::mutex> g(c->comm_mu);
+    if (c->comm && !c->comm_abort_done) {
         (void)ncclCommAbort(c->comm);
-        c->comm = nullptr;
-        c->comm_aborted = true;
+        c->comm_abort_done = true;
+    }
+}
+
+static void wd_loop(ocn_ctx *c)
+{
+    (void)hipSetDevice(c->dec.device);
+    std::unique_lock<std::mutex> g(c->wd_mu);
+    while (!c->wd_stop) {
+        c->wd_cv.wait_for(g, std::chrono::milliseconds(100));
+        if (c->wd_stop || c->call_depth == 0 || c->wd_fired.load() || c->wd_s <= 0) continue;
+        const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - c->call_t0).count();
+        if (waited < c->wd_s) continue;
+        const char *call = c->call_name;
+        g.unlock();
+        wd_fire(c, call, waited);
+        g.lock();
+        if (!c->wd_cv.wait_for(g, std::chrono::seconds(10), [c] { return c->wd_stop || c->call_depth == 0; })) {
+            std::fprintf(stderr, "ocn watchdog: rank %d: %s still blocked 10 s after the abort; exiting (status 3)\n",
+                         c->dec.rank, call);
+            std::fflush(stderr);
+            std::_Exit(3);
+        }
+    }
+}
+
+// An entry that may take part in a collective, watched while a watchdog is set
+struct CallGuard {
+    ocn_ctx *c;
+    CallGuard(ocn_ctx *ctx, const char *name) : c(ctx)
+    {
+        std::lock_guard<std::mutex> g(c->wd_mu);
+        if (c->call_depth++ == 0) {
+            c->call_t0 = std::chrono::steady_clock::now();
+            c->call_name = name;
+        }
+    }
+    ~CallGuard()
+    {
+        std::lock_guard<std::mutex> g(c->wd_mu);
+        --c->call_depth;
+        c->wd_cv.notify_all();
+    }
+};
+template <class F> static int guarded(ocn_ctx *c, const char *name, F &&f)
+{
+    if (c->wd_fired.load()) return set_error(OCN_ERR_COMM, c->wd_msg);
+    int rc;
+    {
+        CallGuard g(c, name);
+        rc = f();
+    }
+    if (c->wd_fired.load()) {   // (the call returned because the watchdog ended it)
+        std::lock_guard<std::mutex> g(c->comm_mu);
+        if (c->comm) { c->comm = nullptr; c->comm_aborted = true; }
+        return set_error(OCN_ERR_COMM, c->wd_msg);
     }
     return rc;
 }
@@ -955,6 +1084,7 @@ constexpr int kVoteWords = 8;   // the role-flip vote (check_coherence): one 0/1
 static int allreduce_max(ocn_ctx *c, int32_t *word, hipStream_t s, int words = 1)
 {
     if (c->comm_aborted) return comm_gone(c);
+    if (c->wd_fired.load()) return set_error(OCN_ERR_COMM, c->wd_msg);
     if (c->comm)
         return nccl_rc(ncclAllReduce(word, word, (size_t)words, ncclInt32, ncclMax, c->comm, s), "ncclAllReduce");
     if (!c->lb) return OCN_OK;
@@ -998,6 +1128,33 @@ static int allreduce_max(ocn_ctx *c, int32_t *word, hipStream_t s, int words = 1
     return OCN_OK;
 }
 
+static int get_event(ocn_ctx *c, hipEvent_t &e);
+
+// The end of an exchange with remote peers on `stream`: its timer record, and while a watchdog is set
+// an event the watchdog polls for the last completed exchange (c->xq; completed events are recycled)
+static int exchange_done(ocn_ctx *c, ocn_ctx::Rec &xrec, hipStream_t stream)
+{
+    if (c->capturing) return OCN_OK;
+    if (xrec.b) {
+        HIPCHK(hipEventRecord(xrec.b, stream));
+        c->recs.push_back(xrec);
+    }
+    if (c->wd_s <= 0) return OCN_OK;
+    std::lock_guard<std::mutex> g(c->xmu);
+    while (!c->xq.empty() && (c->xq.size() > 256 || hipEventQuery(c->xq.front().second) == hipSuccess)) {
+        if (hipEventQuery(c->xq.front().second) == hipSuccess) c->xdone = c->xq.front().first;
+        else HIPCHK(hipEventSynchronize(c->xq.front().second));   // (256 in flight: the oldest has to finish)
+        c->xpool.push_back(c->xq.front().second);
+        c->xq.pop_front();
+    }
+    hipEvent_t e;
+    if (!c->xpool.empty()) { e = c->xpool.back(); c->xpool.pop_back(); }
+    else HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPCHK(hipEventRecord(e, stream));
+    c->xq.emplace_back(c->xchg, e);
+    return OCN_OK;
+}
+
 // cmp != nullptr: compare the halos with what the exchange would deliver instead of writing them
 // (ORs 1 into *cmp where they differ); same messages, so every rank must take part.
 static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stream = nullptr, int32_t *cmp = nullptr,
@@ -1006,9 +1163,17 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
     HaloPlan *p;
     RC(get_plan(c, fields, p, depth, priv));
     if (!stream) stream = c->stream;
-    if (!p->peers.empty()) {
+    ocn_ctx::Rec xrec{OCN_TIMER_EXCHANGE, nullptr, nullptr};
+    const bool remote = !p->peers.empty();
+    if (remote) {
         if (!has_comm(c)) return set_error(OCN_ERR_COMM, "remote neighbours but no RCCL communicator attached");
         if (c->comm_aborted) return comm_gone(c);
+        if (c->wd_fired.load()) return set_error(OCN_ERR_COMM, c->wd_msg);
+        if (c->stage_timing && !c->capturing) {   // the exchange on its stream: pack, group, unpack
+            RC(get_event(c, xrec.a)); RC(get_event(c, xrec.b));
+            HIPCHK(hipEventRecord(xrec.a, stream));
+        }
+        ++c->xchg;
         hipLaunchKernelGGL(k_segments, dim3(p->n_pack, p->ch_pack), dim3(kSegChunk), 0, stream, p->d_pack, p->n_pack);
         RC(check_launch());
         if (c->lb) {
@@ -1041,6 +1206,7 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
                            p->n_unpack);
         RC(check_launch());
     }
+    if (remote) RC(exchange_done(c, xrec, stream));
     return OCN_OK;
 }
 
@@ -1874,6 +2040,11 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
             return OCN_OK;
         }));
         RC(timer_end(c, rec));
+        ocn_ctx::Rec xrec{OCN_TIMER_EXPOSED, nullptr, nullptr};   // inner march end -> comm chain end
+        if (c->stage_timing) {
+            RC(get_event(c, xrec.a)); RC(get_event(c, xrec.b));
+            HIPCHK(hipEventRecord(xrec.a, s));
+        }
         HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
         if (k.x2_save) RC(ring2_run(c, true, c->comm_stream));
         RC(run_sync(c, with_tracers(c, kStateX2), c->comm_stream, nullptr, 2));   // the state two points deep
@@ -1882,6 +2053,10 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
             RC(march(b, c->comm_stream, nullptr, &in));
             return OCN_OK;
         }));
+        if (xrec.b) {
+            HIPCHK(hipEventRecord(xrec.b, c->comm_stream));
+            c->recs.push_back(xrec);
+        }
         HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
         c->sync_pending = true;
         RC(join_sync(c));
@@ -1938,7 +2113,7 @@ static int one_step_multi(ocn_ctx *c, double tau, const StepKind &k)
     RC(timer_begin(c, OCN_TIMER_ONEPASS_MULTI, rec));
     RC(launch_onepass_multi(&b.g, b.ptr.data(), (int)b.ptr.size(), &t, c->sw, tau, k.multi, k.check ? c->d_nbad : nullptr,
                             (double *)b.sshp_alt, (double *)b.up_alt, (double *)b.vp_alt, c->d_bar,
-                            c->d_nbad + 61, s, kc_of(c, b)));
+                            c->d_nbad + 61, s, kc_of(c, b), c->multi_spin));
     RC(timer_end(c, rec));
     if (k.multi & 1) {
         swap_alt3(c);
@@ -2538,12 +2713,22 @@ int ocn_halo_schedule(const ocn_basin *basin, const ocn_decomp *dec, const int32
 int ocn_ctx_destroy(ocn_ctx *c)
 {
     if (!c) return OCN_OK;
+    if (c->wd.joinable()) {   // the watchdog first: nothing is watched from here on
+        {
+            std::lock_guard<std::mutex> g(c->wd_mu);
+            c->wd_stop = true;
+            c->wd_cv.notify_all();
+        }
+        c->wd.join();
+    }
     (void)hipSetDevice(c->dec.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto &g : c->graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto &r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
-    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->comm && !c->comm_abort_done) ncclCommDestroy(c->comm);
+    for (auto &x : c->xq) (void)hipEventDestroy(x.second);
+    for (hipEvent_t e : c->xpool) (void)hipEventDestroy(e);
     if (c->lb) {
         Loopback *L = c->lb;
         bool last;
@@ -2629,7 +2814,7 @@ int ocn_ctx_attach_comm(ocn_ctx *c, const void *unique_id, int32_t nbytes)
 
 int ocn_ctx_attach_loopback(ocn_ctx *const *ctxs, int32_t n)
 {
-    if (!ctxs || n < 2 || n > 64) return set_error(OCN_ERR_ARG, "loopback: 2..64 contexts");
+    if (!ctxs || n < 1 || n > 64) return set_error(OCN_ERR_ARG, "loopback: 1..64 contexts");
     for (int i = 0; i < n; ++i) {
         const ocn_ctx *c = ctxs[i];
         if (!c || c->dec.nranks != n || c->dec.rank != i || c->dec.device != ctxs[0]->dec.device)
@@ -2656,6 +2841,47 @@ int ocn_ctx_attach_loopback(ocn_ctx *const *ctxs, int32_t n)
     return OCN_OK;
 }
 
+int ocn_ctx_comm_info(ocn_ctx *c, ocn_comm_info *out)
+{
+    if (!c || !out) return set_error(OCN_ERR_ARG, "null argument");
+    *out = ocn_comm_info{};
+    out->comm_size = 1;
+    if (c->lb) {
+        out->transport = 2;
+        out->comm_size = c->lb->n;
+        out->comm_rank = c->dec.rank;
+    } else if (c->comm || c->comm_aborted) {
+        out->transport = 1;
+        int v = 0, n = 0, r = 0;
+        if (ncclGetVersion(&v) == ncclSuccess) out->nccl_version = v;
+        std::lock_guard<std::mutex> g(c->comm_mu);
+        if (c->comm && !c->comm_abort_done && ncclCommCount(c->comm, &n) == ncclSuccess &&
+            ncclCommUserRank(c->comm, &r) == ncclSuccess) {
+            out->comm_size = n;
+            out->comm_rank = r;
+        } else {
+            out->comm_size = c->dec.nranks;
+            out->comm_rank = c->dec.rank;
+        }
+    }
+    out->exchanges = c->xchg;
+    out->exchanges_done = c->wd_s > 0 ? poll_xdone(c) : -1;
+    out->watchdog_s = c->wd_s;
+    return OCN_OK;
+}
+
+int ocn_ctx_set_watchdog(ocn_ctx *c, double seconds)
+{
+    if (!c || !(seconds >= 0)) return set_error(OCN_ERR_ARG, "watchdog: null ctx or seconds < 0");
+    {
+        std::lock_guard<std::mutex> g(c->wd_mu);
+        c->wd_s = seconds;
+        c->call_t0 = std::chrono::steady_clock::now();   // (a call under way is timed from now)
+    }
+    if (seconds > 0 && !c->wd.joinable()) c->wd = std::thread(wd_loop, c);
+    return OCN_OK;
+}
+
 int ocn_ctx_set_topography(ocn_ctx *c, const float *h, int64_t count)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
@@ -2666,7 +2892,7 @@ int ocn_ctx_set_topography(ocn_ctx *c, const float *h, int64_t count)
     return OCN_OK;
 }
 
-int ocn_ctx_init_state(ocn_ctx *c)
+static int init_state_entry(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
@@ -2679,13 +2905,21 @@ int ocn_ctx_init_state(ocn_ctx *c)
     c->alt_ok = false; c->tr_alt_ok = false;
     c->hn_fresh = false;
     c->fb_state = kFbUnchecked;
+    // a multi-step launch's barrier timeout not yet reported is void too: the state is formed again
+    if (c->d_nbad) HIPCHK(hipMemsetAsync(c->d_nbad + 61, 0, sizeof(int32_t), c->stream));
     const int rc = fail_fatal(c, init_state(c));
     c->hh_consistent = rc == OCN_OK && !c->r8_handed;   // init_data.f90:60-63 ran hh_init last
     c->hn_fresh = c->hh_consistent && !c->r4_escaped;    // (every level: the n one from h_r)
     return rc;
 }
 
-int ocn_ctx_sync(ocn_ctx *c, int field_id)
+int ocn_ctx_init_state(ocn_ctx *c)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return guarded(c, "ocn_ctx_init_state", [&] { return init_state_entry(c); });
+}
+
+static int sync_entry(ocn_ctx *c, int field_id)
 {
     if (!c || !has_r8(c, field_id)) return set_error(OCN_ERR_ARG, "sync: bad ctx or non-real(8) field");
     HIPCHK(hipSetDevice(c->dec.device));
@@ -2707,7 +2941,13 @@ int ocn_ctx_sync(ocn_ctx *c, int field_id)
     return run_sync(c, {field_id});
 }
 
-int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
+int ocn_ctx_sync(ocn_ctx *c, int field_id)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return guarded(c, "ocn_ctx_sync", [&] { return sync_entry(c, field_id); });
+}
+
+static int stage_entry(ocn_ctx *c, int stage_id, double tau)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
@@ -2720,6 +2960,12 @@ int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
     c->fb_state = kFbUnchecked;
     RC(prepare_static(c));
     return envoke(c, stage_id, tau);
+}
+
+int ocn_ctx_stage(ocn_ctx *c, int stage_id, double tau)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return guarded(c, "ocn_ctx_stage", [&] { return stage_entry(c, stage_id, tau); });
 }
 
 static void drop_graphs(ocn_ctx *c)
@@ -2779,7 +3025,7 @@ static int graph_step(ocn_ctx *c, double tau, const StepKind &k)
     return OCN_OK;
 }
 
-int ocn_ctx_tracer_stage(ocn_ctx *c, int stage_id, int tracer, double tau)
+static int tracer_stage_entry(ocn_ctx *c, int stage_id, int tracer, double tau)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     HIPCHK(hipSetDevice(c->dec.device));
@@ -2788,6 +3034,12 @@ int ocn_ctx_tracer_stage(ocn_ctx *c, int stage_id, int tracer, double tau)
     if (stage_id < 0 || stage_id >= OCN_NUM_TSTAGES) return set_error(OCN_ERR_ARG, "bad tracer stage id");
     RC(complete_open(c));
     return tracer_stage(c, stage_id, tracer, tau, false);
+}
+
+int ocn_ctx_tracer_stage(ocn_ctx *c, int stage_id, int tracer, double tau)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return guarded(c, "ocn_ctx_tracer_stage", [&] { return tracer_stage_entry(c, stage_id, tracer, tau); });
 }
 
 // the current sshp / ubrtrp / vbrtrp (in the second buffers after one-pass steps: role bit 4)
@@ -2973,7 +3225,6 @@ static int complete_open(ocn_ctx *c)
 static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
 {
     HIPCHK(hipSetDevice(c->dec.device));
-    if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
     if (nsteps < 0) return set_error(OCN_ERR_ARG, "nsteps < 0");
     if (nsteps == 0) return OCN_OK;
     // (RCCL / events stay outside graphs; so do the tracer steps' calls: their launches follow pending state)
@@ -3057,8 +3308,11 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     bool flip_call = false, ca = false, one_call = false;
     // tracer runs with one-pass steps (tracer steps): the call's first step a one-pass step too, and
     // with exchanges the x2 steps (their exchange carries the tracers); one block: no ring work
+    // and the last step a one-pass step (last_one below: it runs the pending tracer step)
     const bool tr_ok = c->sw.use_tracers <= 0 ||
-                       (c->tr_step && first_one && (has_exchange(c) ? x2_ok && c->last_hybrid : !c->ring_sea));
+                       (c->tr_step && first_one &&
+                        (has_exchange(c) ? x2_ok && c->last_hybrid
+                                         : !c->ring_sea && (c->last_hybrid || (c->blocks.size() == 1 && !has_comm(c)))));
     auto decide = [&](int n) {
         flip_call = n >= 2 && eligible && c->coherent;
         // role-flip calls with full_free_surface = 1 fuse each step's hh_init with the next step's A;
@@ -3168,16 +3422,30 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     return finish_call(c, rc);
 }
 
+static int step_entry(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    // (a usage error before any collective: no peer waits on this rank yet, the communicator stays)
+    if (!c->initialized) return set_error(OCN_ERR_STATE, "ocn_ctx_init_state not called");
+    return fail_fatal(c, step_impl(c, tau, nsteps, check_every));
+}
+
 int ocn_ctx_step(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
-    return fail_fatal(c, step_impl(c, tau, nsteps, check_every));
+    return guarded(c, "ocn_ctx_step", [&] { return step_entry(c, tau, nsteps, check_every); });
+}
+
+static int complete_entry(ocn_ctx *c)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return complete_open(c);
 }
 
 int ocn_ctx_complete(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
-    return complete_open(c);
+    return guarded(c, "ocn_ctx_complete", [&] { return complete_entry(c); });
 }
 
 // The steps an open sequence deferred (ocn_ctx_step leaves up to two requested steps not yet
@@ -3216,7 +3484,10 @@ static int sync_impl(ocn_ctx *c)
     int32_t nbad = 0, berr = 0;
     HIPCHK(hipMemcpy(&nbad, cnt, sizeof(nbad), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&berr, c->d_nbad + 61, sizeof(berr), hipMemcpyDeviceToHost));
-    if (berr) return set_error(OCN_ERR_HIP, "multi-step launch: a grid barrier timed out (results invalid)");
+    if (berr) {   // reported once: the flag is cleared (ocn_ctx_init_state starts the state over)
+        HIPCHK(hipMemset(c->d_nbad + 61, 0, sizeof(berr)));
+        return set_error(OCN_ERR_HIP, "multi-step launch: a grid barrier timed out (results invalid)");
+    }
     if (nbad) return set_error(OCN_ERR_BLOWUP, "SIGFPRE predict error: |ssh| >= 1e4 on " + std::to_string(nbad) +
                                                    (has_comm(c) ? " sea points of a block (the most of any rank;"
                                                                   " check_ssh_err_kernel)"
@@ -3224,13 +3495,21 @@ static int sync_impl(ocn_ctx *c)
     return OCN_OK;
 }
 
-int ocn_ctx_synchronize(ocn_ctx *c)
+static int synchronize_entry(ocn_ctx *c)
 {
     if (!c) return set_error(OCN_ERR_ARG, "null ctx");
     return fail_fatal(c, sync_impl(c));
 }
 
-int ocn_ctx_stage_times(ocn_ctx *c, double *ms, int64_t *counts)
+int ocn_ctx_synchronize(ocn_ctx *c)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return guarded(c, "ocn_ctx_synchronize", [&] { return synchronize_entry(c); });
+}
+
+int ocn_ctx_stage_times(ocn_ctx *c, double *ms, int64_t *counts) { return ocn_ctx_stage_stats(c, ms, counts, nullptr); }
+
+int ocn_ctx_stage_stats(ocn_ctx *c, double *ms, int64_t *counts, double *ms_max)
 {
     if (!c || !ms || !counts) return set_error(OCN_ERR_ARG, "null argument");
     HIPCHK(hipSetDevice(c->dec.device));
@@ -3239,18 +3518,26 @@ int ocn_ctx_stage_times(ocn_ctx *c, double *ms, int64_t *counts)
     learn_fb(c);
     for (auto &r : c->recs) {
         float t = 0.f;
-        HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
+        if (r.stage == OCN_TIMER_EXPOSED) {   // events on two streams: the comm chain may end first
+            if (hipEventElapsedTime(&t, r.a, r.b) != hipSuccess || !(t > 0.f)) t = 0.f;
+        } else {
+            HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
+        }
         c->stage_ms[r.stage] += t;
         c->stage_n[r.stage] += 1;
+        c->stage_max[r.stage] = std::max(c->stage_max[r.stage], (double)t);
         c->event_pool.push_back(r.a); c->event_pool.push_back(r.b);
     }
     c->recs.clear();
-    for (int i = 0; i < OCN_NUM_TIMERS; ++i) { ms[i] = c->stage_ms[i]; counts[i] = c->stage_n[i]; }
-    for (int i = 0; i < OCN_NUM_TIMERS; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
+    for (int i = 0; i < OCN_NUM_TIMERS; ++i) {
+        ms[i] = c->stage_ms[i]; counts[i] = c->stage_n[i];
+        if (ms_max) ms_max[i] = c->stage_max[i];
+    }
+    for (int i = 0; i < OCN_NUM_TIMERS; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; c->stage_max[i] = 0; }
     return OCN_OK;
 }
 
-int ocn_ctx_download(ocn_ctx *c, int k, int id, void *host)
+static int download_entry(ocn_ctx *c, int k, int id, void *host)
 {
     if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
         return set_error(OCN_ERR_ARG, "download: bad argument");
@@ -3266,7 +3553,13 @@ int ocn_ctx_download(ocn_ctx *c, int k, int id, void *host)
     return OCN_OK;
 }
 
-int ocn_ctx_output_r4(ocn_ctx *c, int k, int id, float undef, float *host)
+int ocn_ctx_download(ocn_ctx *c, int k, int id, void *host)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return guarded(c, "ocn_ctx_download", [&] { return download_entry(c, k, id, host); });
+}
+
+static int output_r4_entry(ocn_ctx *c, int k, int id, float undef, float *host)
 {
     if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
         return set_error(OCN_ERR_ARG, "output_r4: bad argument");
@@ -3295,7 +3588,13 @@ int ocn_ctx_output_r4(ocn_ctx *c, int k, int id, float undef, float *host)
     return rc;
 }
 
-int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
+int ocn_ctx_output_r4(ocn_ctx *c, int k, int id, float undef, float *host)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return guarded(c, "ocn_ctx_output_r4", [&] { return output_r4_entry(c, k, id, undef, host); });
+}
+
+static int upload_entry(ocn_ctx *c, int k, int id, const void *host)
 {
     if (!c || !host || k < 0 || k >= (int)c->blocks.size() || !has_field(c, id))
         return set_error(OCN_ERR_ARG, "upload: bad argument");
@@ -3313,6 +3612,12 @@ int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
     c->hn_fresh = false;
     c->fb_state = kFbUnchecked;
     return upload_field(c, c->blocks[k], id, host, false);
+}
+
+int ocn_ctx_upload(ocn_ctx *c, int k, int id, const void *host)
+{
+    if (!c) return set_error(OCN_ERR_ARG, "null ctx");
+    return guarded(c, "ocn_ctx_upload", [&] { return upload_entry(c, k, id, host); });
 }
 
 int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
@@ -3357,7 +3662,11 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     case OCN_OPT_X2: c->x2 = value != 0; c->coherent_known = false; return OCN_OK;
     case OCN_OPT_PAIR: c->pair = value < 0 ? 0 : value > 2 ? 2 : (int)value; return OCN_OK;
     case OCN_OPT_MULTI: c->multi = value != 0; return OCN_OK;
-    case OCN_OPT_TRACER_STEP: c->tr_step = value != 0; return OCN_OK;
+    case OCN_OPT_TRACER_STEP:   // (the x2 vote checks mu's halo only for tracer steps: vote again)
+        c->tr_step = value != 0;
+        c->coherent_known = false;
+        return OCN_OK;
+    case OCN_OPT_MULTI_SPIN: c->multi_spin = value < 1 ? 1 : value > kMultiSpin ? kMultiSpin : (int)value; return OCN_OK;
     case OCN_OPT_BATCH:
         if (c->batch != (value != 0)) drop_graphs(c);
         c->batch = value != 0;
@@ -3399,6 +3708,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_PAIR: *value = c->pair_used ? 2 : c->pair > 0; return OCN_OK;
     case OCN_OPT_MULTI: *value = c->multi_used ? 2 : c->multi; return OCN_OK;
     case OCN_OPT_TRACER_STEP: *value = c->tr_call ? 2 : c->tr_step; return OCN_OK;
+    case OCN_OPT_MULTI_SPIN: *value = c->multi_spin; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

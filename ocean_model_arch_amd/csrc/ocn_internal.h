@@ -152,12 +152,15 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
 // the previous one wrote (the role pairs and sshp / ubrtrp / vbrtrp against *_alt, alternating);
 // ctr: kMultiBarBytes of device words for the grid barrier, at the start of their own allocation
 // (zeroed on the stream first); err: ORed 1 if a barrier timed out.  onepass_multi_fits: the block's
-// grid is small enough for one resident launch.
+// grid is small enough for one resident launch on the current device (its tile count against every
+// variant's occupancy x the device's CUs, queried once per device).  spin: the barrier's bound on
+// polls before it gives up (kMultiSpin; tests force it low to exercise the timeout path).
 constexpr size_t kMultiBarBytes = 17 * 128;   // the top counter, 8 group counters, 8 group generations
+constexpr int kMultiSpin = 1 << 20;           // ~0.5 s of s_sleep(1) polls
 int onepass_multi_fits(const ocn_block *b);
 int launch_onepass_multi(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                          double tau, int nsteps, int32_t *nbad, double *sshp_alt, double *up_alt, double *vp_alt,
-                         unsigned *ctr, int32_t *err, hipStream_t s, const OnepassKC &kc);
+                         unsigned *ctr, int32_t *err, hipStream_t s, const OnepassKC &kc, int spin = kMultiSpin);
 // the known-constant precondition of launch_onepass over r (sw_kernels.hip FallbackCheck: the
 // fallback points and the forcing hold +0.0, h_r and mu are uniform): ORs 1 into *flag where it
 // does not hold; writes h_r and mu at (r.m0, r.n0) to kc[0], kc[1]

@@ -25,6 +25,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "ocn_internal.h"
@@ -2813,7 +2815,7 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 // group g's arrivals, the group's last arriver adds to bar[0] and, once all groups are in, publishes
 // the epoch in bar[32 (9 + g)], which the group's other workgroups await -- 8 words polled instead of
 // one, and each atomic queue 1/8 as long.  (Words 128 B apart.)
-__device__ __forceinline__ bool grid_barrier(unsigned *bar, unsigned epoch, int32_t *err)
+__device__ __forceinline__ bool grid_barrier(unsigned *bar, unsigned epoch, int32_t *err, int spin)
 {
     __shared__ int ok_s;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores reached memory
@@ -2824,15 +2826,15 @@ __device__ __forceinline__ bool grid_barrier(unsigned *bar, unsigned epoch, int3
         int k = 0;
         if (t + 1 == ng * epoch) {   // the group's last arrival of this epoch
             __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < groups * epoch && ++k < (1 << 20))
+            while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < groups * epoch && ++k < spin)
                 __builtin_amdgcn_s_sleep(1);
             __hip_atomic_store(bar + 32 * (9 + g), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             while (__hip_atomic_load(bar + 32 * (9 + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch &&
-                   ++k < (1 << 20))
+                   ++k < spin)
                 __builtin_amdgcn_s_sleep(1);
         }
-        const bool ok = k < (1 << 20);
+        const bool ok = k < spin;
         if (!ok) atomicOr(err, 1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // drop stale lines: the next step's loads
         ok_s = ok;
@@ -2844,7 +2846,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned *bar, unsigned epoch, int3
 template <class Body> struct BodyPair { Body b[2]; };
 template <class Body>
 __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march_multi(MarchGrid g, BodyPair<Body> bp, int nsteps,
-                                                                       unsigned *ctr, int32_t *err)
+                                                                       unsigned *ctr, int32_t *err, int spin)
 {
     const MarchRect &R = g.r[0];
     const int tile = (int)blockIdx.x;   // one tile per workgroup (gridDim.x = R.tiles)
@@ -2852,7 +2854,7 @@ __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march_multi(MarchGrid
     for (int s = 0; s < nsteps; ++s) {
         // ONE inlined march, the step's body picked at run time (two inlined copies: 93 KB of code)
         march_tile<Body, false>(R, tile, bp.b[__builtin_amdgcn_readfirstlane(s & 1)]);
-        if (s + 1 < nsteps && !grid_barrier(ctr, (unsigned)(s + 1), err)) return;
+        if (s + 1 < nsteps && !grid_barrier(ctr, (unsigned)(s + 1), err, spin)) return;
     }
 }
 
@@ -2867,11 +2869,49 @@ static int multi_rows(const Range &r)
     return 0;
 }
 
-int onepass_multi_fits(const ocn_block *b) { return multi_rows(range_interior(b)) > 0; }
+// The multi-step kernels' resident capacity on the current device, in workgroups: the fewest of any
+// variant's occupancy x the device's CUs (a device with fewer CUs, a partition mode, another
+// compile of the march), queried once per device; 0 if a query fails (no multi-step launch then)
+template <bool P, bool Z, bool H> using MultiBody = MarchStep<P, false, Z, false, H, false, true>;
+static long multi_capacity()
+{
+    static std::mutex mu;
+    static std::map<int, long> cap;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> g(mu);
+    const auto it = cap.find(dev);
+    if (it != cap.end()) return it->second;
+    long c = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? LONG_MAX : 0;
+    auto occ = [&](auto kern) {
+        int per = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) != hipSuccess) per = 0;
+        c = std::min(c, (long)per * cus);
+    };
+    occ(k_march_multi<MultiBody<true, false, false>>);
+    occ(k_march_multi<MultiBody<false, false, false>>);
+    occ(k_march_multi<MultiBody<true, true, true>>);
+    occ(k_march_multi<MultiBody<false, true, true>>);
+    occ(k_march_multi<MultiBody<true, true, false>>);
+    occ(k_march_multi<MultiBody<false, true, false>>);
+    return cap[dev] = c;
+}
+
+static long multi_tiles(const Range &r, int rows)
+{
+    return (long)((r.m1 - r.m0 + 60) / 60) * ((r.n1 - r.n0 + 4 * rows) / (4 * rows));
+}
+
+int onepass_multi_fits(const ocn_block *b)
+{
+    const Range r = range_interior(b);
+    const int rows = multi_rows(r);
+    return rows > 0 && multi_tiles(r, rows) <= multi_capacity();
+}
 
 int launch_onepass_multi(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                          double tau, int nsteps, int32_t *nbad, double *sshp_alt, double *up_alt, double *vp_alt,
-                         unsigned *ctr, int32_t *err, hipStream_t s, const OnepassKC &kc)
+                         unsigned *ctr, int32_t *err, hipStream_t s, const OnepassKC &kc, int spin)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_alt ||
         !up_alt || !vp_alt || !ctr || !err || nsteps < 1)
@@ -2906,18 +2946,12 @@ int launch_onepass_multi(const ocn_block *b, void *const *ptr, int nptr, const C
         g.nr = 1;
         g.ntiles = g.r[0].tiles;
         // residency from the grid size alone (a plain launch: hipLaunchCooperativeKernel's check costs
-        // 15-20 us per launch): at most kMultiMaxTiles workgroups against the resident capacity
-        static const long cap = [] {
-            int dev = 0, per = 0, cus = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_march_multi<Body>, 256, 0) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                return 0L;
-            return (long)per * cus;
-        }();
-        if (g.ntiles > cap) return set_error(OCN_ERR_ARG, "multi-step launch: grid larger than the resident capacity");
+        // 15-20 us per launch): the callers ask onepass_multi_fits first; this is the assert
+        if (g.ntiles != multi_tiles(r, rows) || g.ntiles > multi_capacity())
+            return set_error(OCN_ERR_ARG, "multi-step launch: grid larger than the resident capacity");
         count_launch();
-        k_march_multi<Body><<<dim3((unsigned)g.ntiles), dim3(256), 0, s>>>(g, BodyPair<Body>{{k0, k1}}, nsteps, ctr, err);
+        k_march_multi<Body><<<dim3((unsigned)g.ntiles), dim3(256), 0, s>>>(g, BodyPair<Body>{{k0, k1}}, nsteps, ctr, err,
+                                                                             spin < 1 ? 1 : spin);
         return check_hip(hipGetLastError(), "multi-step launch");
     };
 #define OCN_MULTI(P, Z, H)                                                                                       \

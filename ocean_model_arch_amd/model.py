@@ -144,6 +144,35 @@ class OceanModel:
         check(lib().ocn_ctx_stage_times(self.ctx, ms, n), "ocn_ctx_stage_times")
         return {s: (ms[i], n[i]) for i, s in enumerate(_lib.TIMERS) if n[i]}
 
+    def stage_stats(self) -> dict:
+        """{stage: (total_ms, launches, max_ms)} from HIP events since the last call (synchronises);
+        "exchange": the halo exchanges with remote peers, "exposed": per overlapped step, how long the
+        exchange chain outlasted the inner march (ocn_ctx_stage_stats)."""
+        ms = (C.c_double * len(_lib.TIMERS))()
+        mx = (C.c_double * len(_lib.TIMERS))()
+        n = (C.c_int64 * len(_lib.TIMERS))()
+        check(lib().ocn_ctx_stage_stats(self.ctx, ms, n, mx), "ocn_ctx_stage_stats")
+        return {s: (ms[i], n[i], mx[i]) for i, s in enumerate(_lib.TIMERS) if n[i]}
+
+    def set_watchdog(self, seconds: float):
+        """Host-side watchdog (ocn_ctx_set_watchdog): a call that may take part in a collective and has
+        not returned after `seconds` is ended (RCCL communicator aborted / loopback group failed; the
+        call raises OcnError with the rank's last completed exchange id).  0 = off."""
+        check(lib().ocn_ctx_set_watchdog(self.ctx, float(seconds)), "ocn_ctx_set_watchdog")
+        return self
+
+    def comm_info(self) -> dict:
+        """ocn_ctx_comm_info: transport ("none" / "rccl" / "loopback"), RCCL version and communicator
+        size / rank, exchanges enqueued and the last completed (-1 without a watchdog)."""
+        i = _lib.OcnCommInfo()
+        check(lib().ocn_ctx_comm_info(self.ctx, C.byref(i)), "ocn_ctx_comm_info")
+        v = int(i.nccl_version)
+        return {"transport": ("none", "rccl", "loopback")[i.transport],
+                "version": (f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v else None), "version_code": v,
+                "comm_size": int(i.comm_size), "comm_rank": int(i.comm_rank),
+                "exchanges": int(i.exchanges), "exchanges_done": int(i.exchanges_done),
+                "watchdog_s": float(i.watchdog_s)}
+
     def set_fused(self, on: bool = True):
         """Fused step groups (default) or the reference's 11 envoke stages; same results bit for bit."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FUSED, int(on)), "ocn_ctx_set_option")
@@ -228,6 +257,12 @@ class OceanModel:
         """Small single blocks: the steps of a call (in an open sequence) as one launch
         with a grid-wide barrier between them (default on); same results bit for bit."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MULTI, int(on)), "ocn_ctx_set_option")
+        return self
+
+    def set_multi_spin(self, polls: int):
+        """Diagnostics: the multi-step launch's grid barrier gives up after `polls` polls (default
+        1 << 20, about 0.5 s); the next synchronize() then raises OCN_ERR_HIP."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MULTI_SPIN, int(polls)), "ocn_ctx_set_option")
         return self
 
     def set_tracer_step(self, on: bool = True):

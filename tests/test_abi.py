@@ -44,7 +44,8 @@ def test_python_binding_covers_header(lib):
 
 
 STRUCTS = {"ocn_block": "OcnBlock", "ocn_basin": "OcnBasin", "ocn_sw_params": "OcnSwParams",
-           "ocn_decomp": "OcnDecomp", "ocn_block_info": "OcnBlockInfo", "ocn_halo_msg": "OcnHaloMsg"}
+           "ocn_decomp": "OcnDecomp", "ocn_block_info": "OcnBlockInfo", "ocn_halo_msg": "OcnHaloMsg",
+           "ocn_comm_info": "OcnCommInfo"}
 
 
 def test_struct_layouts(tmp_path):
@@ -82,12 +83,13 @@ def test_field_ids_match_header():
     assert _lib.FIELD_ID["flux_x"] == 64 and _lib.FIELD_ID["flux_y"] == 65
     assert [_lib.FIELD_ID[n] for n in ("ff1_1", "ff1p_1", "ff1n_1", "ff1_2")] == [66, 67, 68, 69]
     assert _lib.FIELD_ID.name(71) == "ff1n_2"
-    assert len(_lib.TIMERS) == 11 + 3 + 3 + 6   # + fused_ca, onepass, onepass2, onepass2_last, onepass_multi, tracer_step
+    # + fused_ca, onepass, onepass2, onepass2_last, onepass_multi, tracer_step, exchange, exposed
+    assert len(_lib.TIMERS) == 11 + 3 + 3 + 8
 
 
 def test_abi_version_and_loud_failure_without_device(lib):
     import ocean_model_arch_amd as amd
-    assert lib.ocn_abi_version() == 4
+    assert lib.ocn_abi_version() == 5
     bid = amd.build_id()
     assert len(bid) == 16 and int(bid, 16) >= 0, bid   # Makefile: sha256 of sources + flags
     try:

@@ -117,3 +117,19 @@ def test_pair_region_launches(calls):
     assert kinds[p:] == (["onepass_last_z"] + tail if steps % 2 else ["onepass2_last_z"] + tail)
     non_lazy = [k for _, k in bench.call_launches(20, flip=True, one=True, zero=True, pair=True)]
     assert non_lazy[:10] == ["onepass2_z"] * 9 + ["onepass_z"] and non_lazy[10] == "onepass_last_z"
+
+
+def test_rccl_report_from_rank_records():
+    """The N-GPU line's `rccl` object (bench.rccl_report) from per-rank timed-region records: groups per
+    step and the exposed time are the worst rank's, the group time's max the largest of any rank,
+    hidden_frac = 1 - exposed / group time over all ranks."""
+    comm = {"transport": "rccl", "version": "2.27.7", "comm_size": 2, "watchdog_s": 120.0}
+    recs = [{"rank": 0, "comm": comm, "groups": 22, "timed_groups": 22, "group_ms_sum": 0.44, "group_ms_max": 0.05,
+             "exposed_ms_sum": 0.044, "exposed_n": 19},
+            {"rank": 1, "comm": comm, "groups": 22, "timed_groups": 22, "group_ms_sum": 0.66, "group_ms_max": 0.08,
+             "exposed_ms_sum": 0.066, "exposed_n": 19}]
+    r = bench.rccl_report(recs, 20)
+    assert r["version"] == "2.27.7" and r["comm_size"] == 2 and r["transport"] == "rccl"
+    assert r["groups_per_step"] == 1.1 and r["group_ms"] == {"mean": 0.025, "max": 0.08}
+    assert r["exposed_ms_per_step"] == 0.0033 and r["hidden_frac"] == 0.9
+    assert [p["groups"] for p in r["per_rank"]] == [22, 22]

@@ -226,3 +226,108 @@ def test_tracer_steps_after_inconsistent_mu_upload_match_oracle(amd):
     finally:
         m.close()
     assert not bad, f"fields differ from the oracle: {bad}"
+
+
+# ---------------------------------------------------------------- advisor regressions (round 4)
+def test_multi_barrier_timeout_reports_and_recovers(amd):
+    """The multi-step launch's grid barrier is bounded (sw_kernels.hip grid_barrier): forced to give up
+    after one poll (OCN_OPT_MULTI_SPIN 1), every workgroup ends, synchronize() reports OCN_ERR_HIP once
+    (no hang), and init() starts over: the next run is bitwise the oracle's."""
+    n = 100
+    m = amd.OceanModel(amd.box_config(n)).init()
+    try:
+        m.step(2, check_every=1).synchronize()   # the verdict reaches the host: the next call is multi
+        m.set_multi_spin(1)
+        m.step(12, check_every=1)
+        used = m.multi_active
+        with pytest.raises(amd.OcnError, match="grid barrier timed out"):
+            m.synchronize()
+        m.synchronize()   # reported once
+        m.set_multi_spin(1 << 20)
+        m.init()
+        ref = OracleTwin(n)
+        m.step(2, check_every=1).synchronize()
+        m.step(9, check_every=1)
+        used2 = m.multi_active
+        m.synchronize()
+        ref.run(11)
+        bad = ref.mismatches(m)
+    finally:
+        m.close()
+    assert used and used2, (used, used2)
+    assert not bad, f"after the timeout and init(): fields differ from the oracle: {bad}"
+
+
+def test_tracer_step_toggle_revotes_mu_halo(amd):
+    """A cached coherence vote taken with tracer steps off does not check mu's halo (only tracer steps
+    read it at neighbour-owned points): turning tracer steps on must vote again -- a per-block mu upload
+    between them, then every field against the oracle."""
+    import numpy as np
+    n, blocks = 120, (3, 2)
+    m = amd.OceanModel(amd.box_config(n), sw=amd.SWConfig(use_tracers=1, tracer_num=1),
+                       par=amd.ParallelConfig(*blocks)).init()
+    ref = OracleTwin(n, blocks, 1)
+    try:
+        m.set_tracer_step(False)
+        m.step(2, check_every=1).synchronize()
+        ref.run(2)
+        for b in m.blocks:
+            a = m.download(b.k, "mu")
+            i, j = np.meshgrid(np.arange(a.shape[0]), np.arange(a.shape[1]), indexing="ij")
+            a = a + 50.0 * np.exp(-((i - a.shape[0] / 2) ** 2 + (j - a.shape[1] / 2) ** 2) / (a.size / 40.0))
+            m.upload(b.k, "mu", a)
+            ref.upload(b, "mu", a)
+        m.step(3, check_every=1).synchronize()   # a vote with tracer steps off (cached)
+        ref.run(3)
+        m.set_tracer_step(True)
+        for k in (3, 2):
+            m.step(k, check_every=1)
+            ref.run(k)
+        bad = ref.mismatches(m)
+    finally:
+        m.close()
+    assert not bad, f"fields differ from the oracle: {bad}"
+
+
+def test_tracer_steps_with_comm_and_standard_last_step(amd):
+    """One block, a (loopback, one-rank) communicator attached and OCN_OPT_ONEPASS_LAST 0: the call's
+    last step is a standard step, which does not run a pending tracer step -- so tracer steps are not
+    used there, and no step's tracer update is dropped (every field against the oracle)."""
+    n = 80
+    m = amd.OceanModel(amd.box_config(n), sw=amd.SWConfig(use_tracers=1, tracer_num=1))
+    amd.OceanModel.attach_loopback([m])
+    m.init()
+    ref = OracleTwin(n, (1, 1), 1)
+    try:
+        m.set_onepass_last(False)
+        for k in (3, 4, 1, 2):
+            m.step(k, check_every=1)
+            ref.run(k)
+        m.synchronize()
+        bad = ref.mismatches(m)
+    finally:
+        m.close()
+    assert not bad, f"fields differ from the oracle: {bad}"
+
+
+def test_step_before_init_keeps_the_communicator(amd):
+    """A step before init_state is a usage error raised before any collective (OCN_ERR_STATE): it
+    must not abort the communicator -- the model still exchanges after init()."""
+    n = 64
+    ms = [amd.OceanModel(amd.box_config(n), par=amd.ParallelConfig(2, 1), rank=r, nranks=2) for r in range(2)]
+    amd.OceanModel.attach_loopback(ms)
+    try:
+        with pytest.raises(amd.OcnError, match="init_state"):
+            ms[0].step(1)
+
+        def body(m):
+            m.init()
+            m.step(4, check_every=1).synchronize()
+        amd.run_ranks(ms, body)
+        ref = OracleTwin(n, (2, 1))
+        ref.run(4)
+        bad = [x for mm in ms for x in ref.mismatches(mm, ["ssh", "ubrtr", "vbrtr", "hhu"])]
+    finally:
+        for mm in ms:
+            mm.close()
+    assert not bad, f"fields differ from the oracle: {bad}"

@@ -454,3 +454,75 @@ def _ranks_sequence(amd, seed, nops=20, tracers=0, n=120, grid=(2, 2)):
         raise AssertionError(f"ranks: fields differ from the oracle: {bad[:12]} ({ops})")
 
 
+
+
+# ---------------------------------------------------------------- watchdog and exchange statistics
+def test_watchdog_ends_every_rank_when_one_stalls(amd):
+    """One rank of four never reaches its step (it sleeps): every other rank is blocked in the
+    exchange's rendezvous.  Their watchdogs (ocn_ctx_set_watchdog, 2 s) end them: each raises OcnError
+    with the watchdog's message (the call and the last completed exchange id) well inside the 120 s
+    rendezvous bound; the stalled rank, arriving later, fails too -- no rank hangs."""
+    import time
+    n, T, stalled = 96, 2.0, 2
+    ms = [amd.OceanModel(amd.box_config(n), par=amd.ParallelConfig(2, 2), rank=r, nranks=4) for r in range(4)]
+    amd.OceanModel.attach_loopback(ms)
+    try:
+        def init(m):
+            m.set_watchdog(T)
+            m.init()
+            m.step(3, check_every=1).synchronize()
+        amd.run_ranks(ms, init)
+
+        def body(m):
+            if m.rank == stalled:
+                time.sleep(3 * T)
+            t0 = time.perf_counter()
+            try:
+                m.step(5, check_every=1)
+                m.synchronize()
+            except amd.OcnError as e:
+                return str(e), time.perf_counter() - t0
+            return None, time.perf_counter() - t0
+        out = amd.run_ranks(ms, body)
+        info = ms[0].comm_info()
+    finally:
+        for m in ms:
+            m.close()
+    for r, (msg, dt) in enumerate(out):
+        assert msg is not None, f"rank {r} did not fail"
+        if r != stalled:
+            assert "ocn watchdog: rank" in msg and "last completed exchange id" in msg, msg
+            assert dt < T + 8.0, (r, dt)
+    assert info["transport"] == "loopback" and info["exchanges"] > 0 and info["exchanges_done"] >= 0, info
+
+
+def test_exchange_stats_and_comm_info(amd):
+    """With stage timing on, every exchange with a remote peer is one OCN_TIMER_EXCHANGE record (its
+    count = the exchanges comm_info counts), and each overlapped x2 step one OCN_TIMER_EXPOSED record
+    -- what bench.py's `rccl` object reports for an N-GPU run; results stay bitwise."""
+    case = cases.load_e2e("box70x54_b3x2_s20")
+    models = [build_model(amd, case, rank=r, nranks=6) for r in range(6)]
+    amd.OceanModel.attach_loopback(models)
+
+    def body(m):
+        m.init()
+        m.step(2, tau=1.0, check_every=1).synchronize()
+        m.set_stage_timing(True)
+        m.stage_times()
+        x0 = m.comm_info()["exchanges"]
+        m.step(18, tau=1.0, check_every=1)
+        m.synchronize()
+        st = m.stage_stats()
+        return st, m.comm_info()["exchanges"] - x0, m.x2_active, m.overlap_level
+    try:
+        out = amd.run_ranks(models, body)
+        bad = check_ranks(models, case, "box70x54_b3x2_s20")
+    finally:
+        for m in models:
+            m.close()
+    assert not bad, bad
+    for st, groups, x2, level in out:
+        assert x2 and level == 2, (x2, level)
+        ex = st.get("exchange")
+        assert ex and ex[1] == groups and groups >= 18 and ex[2] >= ex[0] / ex[1] > 0, (ex, groups)
+        assert "exposed" in st and st["exposed"][1] >= 16, st.get("exposed")
