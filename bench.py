@@ -381,6 +381,16 @@ def load_valu(amd, stage: str, launch_ms: float, box, blocks):
                                    "; counter passes serialize dispatches)")
             out["issue_floor_ms_at_clock"] = round(floor_clk, 4)
             out["issue_frac_at_clock"] = round(floor_clk / launch_ms, 4)
+        vc = d["kernels"][stage].get("valu_classes")
+        if vc:   # by class (SQ_INSTS_VALU_* passes): the reference's f64 arithmetic vs everything else
+            tot = pl["SQ_INSTS_VALU"]
+            clk_ghz = clk["clock_ghz"] if clk else SHADER_CLOCK_GHZ
+            other = tot - vc["f64"]
+            out["classes"] = {"f64_frac": vc["f64_frac"], "per_launch": vc["per_launch"],
+                              "unclassified_frac": vc["unclassified_frac"],
+                              # the non-f64 instructions' share of the issue floor at the pass's clock
+                              "non_f64_issue_ms": round(other * 4.0 / SIMDS / (clk_ghz * 1e9) * 1e3, 4),
+                              "f64_issue_ms": round(vc["f64"] * 4.0 / SIMDS / (clk_ghz * 1e9) * 1e3, 4)}
         return out
     except Exception:
         return None
@@ -441,6 +451,8 @@ def main():
                     help="small single blocks: one launch per step (no multi-step launch, OCN_OPT_MULTI)")
     ap.add_argument("--no-tracer-step", action="store_true",
                     help="tracer runs: the role-flip path with the standard tracer stages (no tracer steps, OCN_OPT_TRACER_STEP)")
+    ap.add_argument("--no-x4", action="store_true",
+                    help="blocks with halo exchanges: x2 single launches (no pairs with one 4-deep exchange, OCN_OPT_X4)")
     ap.add_argument("--no-batch", action="store_true",
                     help="several blocks on a GPU: one launch per block and launch group (no block batching)")
     ap.add_argument("--watchdog", type=float, default=120.0,
@@ -519,6 +531,7 @@ def main():
     model.set_pair(args.pair)
     model.set_multi(not args.no_multi)
     model.set_tracer_step(not args.no_tracer_step)
+    model.set_x4(not args.no_x4)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -591,11 +604,20 @@ def main():
             dom = max(stage_ms, key=lambda s: times[s][0])
             alg = kbytes[dom] * local_cells
             achieved = alg / (stage_ms[dom] * 1e-3) / 1e9
-            roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            valu = load_valu(amd, dom, stage_ms[dom], [nxbox, nybox], [bx, by])
+            frac = achieved / HBM_PEAK_GBS
+            # the bound: VALU issue when its floor (at the clock the counter pass measured) takes a larger
+            # share of the launch than the HBM bytes do; achieved / peak / frac stay the HBM figures
+            issue = valu.get("issue_frac_at_clock", valu.get("issue_frac")) if valu else None
+            roof = {"bound": "valu" if issue is not None and issue > frac else "hbm", "kernel": dom,
+                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(frac, 4),
                     "traffic": load_traffic(amd, dom, local_cells, compact, [nxbox, nybox], [bx, by]),
-                    "valu": load_valu(amd, dom, stage_ms[dom], [nxbox, nybox], [bx, by]),
+                    "valu": valu,
                     "alg_bytes_per_launch": int(alg), "launch_ms": round(stage_ms[dom], 4)}
+            if roof["bound"] == "valu":
+                roof["bound_note"] = ("VALU issue: issue_frac_at_clock (the SQ_INSTS_VALU floor at the measured clock "
+                                      "/ the launch time) exceeds the HBM fraction; frac is the HBM fraction")
         step_gbs = B_ALG * cells * args.steps / dt / 1e9 / world
         moved = b_path * cells * args.steps / dt / 1e9 / world
         out = {"metric": METRIC, "value": value, "unit": "cell-updates/s", "n_gpus": world,

@@ -80,13 +80,14 @@ __global__ __launch_bounds__(256) void k_init_grid(GridInit q)
 }
 
 // The metric values of the rows just outside the block's metric range (bnd_y1 and bnd_y2, where
-// the reference leaves 0) as the neighbour block above / below forms them on its interior -- the
-// same global row, the same arithmetic: the one-pass step forms its halo points' depths and
-// stresses there (ocn_ctx.hip one_step_x2).  Column nx_start - 1 (the compact row tables' column).
+// the reference leaves 0, and the two rows beyond each, outside its arrays) as the neighbour block
+// above / below forms them on its interior -- the same global row, the same arithmetic: the
+// one-pass steps form their halo points' depths and stresses there (ocn_ctx.hip one_step_x2,
+// one_step_x4).  Column nx_start - 1 (the compact row tables' column).
 __global__ void k_ext_rows(GridInit q)
 {
     const int i = (int)threadIdx.x;
-    if (i >= 2) return;
+    if (i >= kExtRows) return;
     grid_metrics(q, q.ext_ct[i], q.ext_cv[i], q.ext_sin_v[i], q.ext_cosy_v[i], q.cos_xu[q.g.nx_start - 1 - q.g.bnd_x1],
                  q.ext + i * (OCN_NUM_R4 - OCN_DX));
 }

@@ -179,6 +179,11 @@ struct LBlock {
     float *rows_x = nullptr;           // the row table with those two rows (launch_rows_ext)
     double *hr_x = nullptr;            // h_r with its second halo ring from the neighbours
     double *ring2 = nullptr;           // the state's second halo ring as the reference leaves it (saved)
+    // one_step_x4 (two one-pass steps per launch, one 4-deep state exchange per pair): mask bytes and the
+    // row table over the block widened by kXRing rings (launch_x4_tables; bits_x4 based at
+    // A(bnd_x1 - kXRing, bnd_y1 - kXRing), pitch g.pitch)
+    uint8_t *bits_x4 = nullptr;
+    float *rows_x4 = nullptr;
     Seg *d_save = nullptr, *d_restore = nullptr;   // its save / restore runs (k_segments)
     int n_save = 0, n_restore = 0, ch_ring2 = 1;
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
@@ -386,6 +391,10 @@ struct ocn_ctx {
     bool x2 = true, rows_x_ok = false, edge_ring_sea = true, x2_dev_ok = false;
     mutable bool ext_ok = false, hrx_ok = false;
     bool ring2_saved = false, x2_used = false;
+    // one_step_x4 (OCN_OPT_X4): pairs of x2 steps with one 4-deep exchange each; x4_tab_ok: its tables
+    // were built from init_state's real(4) fields with every divisor in udiv's range; x4_dev_ok: the
+    // last vote found every rank able to run them (a communicator attached); x4_used: the last call did
+    bool x4 = true, x4_tab_ok = false, x4_dev_ok = false, x4_used = false;
     bool fb_x2 = false;          // the known-constant check's verdict is for the x2 range / tables
     mutable bool coherent_known = false, r8_escaped = false;
     int multi_spin = kMultiSpin;   // OCN_OPT_MULTI_SPIN (the multi-step launch's barrier bound)
@@ -510,7 +519,9 @@ static int decompose(ocn_ctx *c)
         lb.g = g.g;
         lb.bm = g.bm; lb.bn = g.bn; lb.gid = gid;
         const int w = g.g.bnd_x2 - g.g.bnd_x1 + 1;
-        lb.g.pitch = (int64_t)((w + 63) / 64 * 64);   // 512-B aligned rows for r8
+        // 512-B aligned rows for r8, with room for 2 * kXRing more columns (the extra halo rings of
+        // one_step_x4 live in the row padding: column bnd_x1 - j is the previous row's tail)
+        lb.g.pitch = (int64_t)((w + 2 * kXRing + 63) / 64 * 64);
         for (int d = 1; d <= 8; ++d) {
             const int m = g.bm + kDirDm[d], n = g.bn + kDirDn[d];
             if (m < 1 || m > c->bnx || n < 1 || n > c->bny) {
@@ -564,6 +575,10 @@ static int allocate_x2(ocn_ctx *c, LBlock &b)
     const long per = 2L * w + 2L * (h - 2);   // rows bnd_y1, bnd_y2; columns bnd_x1, bnd_x2 between them
     HIPCHK(hipMalloc(&b.ring2, sizeof(double) * (size_t)(6 * per)));
     c->allocs.push_back(b.ring2);
+    HIPCHK(hipMalloc(&b.bits_x4, (size_t)b.g.pitch * (h + 2 * kXRing)));
+    c->allocs.push_back(b.bits_x4);
+    HIPCHK(hipMalloc(&b.rows_x4, row_table_size((unsigned)(h + 2 * kXRing)) * sizeof(float)));
+    c->allocs.push_back(b.rows_x4);
     std::vector<Seg> save, restore;
     const long p = (long)b.g.pitch;
     for (int g = 0; g < 6; ++g) {
@@ -598,8 +613,10 @@ static int allocate(ocn_ctx *c)
         const long n = (long)b.g.pitch * rows;
         // every field padded to a 256-B multiple, based so that A(nx_start, :) rows are
         // 256-B aligned: base offset shifted by (nx_start - bnd_x1) = 2 elements.
-        // OCN_FIELD_SKEW (bytes, multiple of 256): extra gap between consecutive fields
-        const long r8b = ((n * 8 + 16 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW;
+        // OCN_FIELD_SKEW (bytes, multiple of 256): extra gap between consecutive fields.
+        // real(8) fields: kXRing more rows above and below the array (one_step_x4's extra rings)
+        const long xr = (long)kXRing * b.g.pitch * 8;
+        const long r8b = ((n * 8 + 16 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW + 2 * xr;
         const long r4b = ((n * 4 + 8 + 255) / 256) * 256 + 256 + OCN_FIELD_SKEW;
         const int nr8 = num_r8(c), ntr = c->sw.use_tracers > 0 ? c->sw.tracer_num : 0;
         // + the three second buffers of the role-flip / one-pass steps, one per tracer (ff1p)
@@ -622,7 +639,7 @@ static int allocate(ocn_ctx *c)
         for (int k = 1; k <= ntr; ++k) order.push_back(-3 - k);
         b.ffp_alt.assign((size_t)ntr, nullptr);
         for (int id : order) {
-            char *p = base + off + 256 - 16;
+            char *p = base + off + 256 - 16 + xr;
             off += r8b;
             if (id == -1) b.sshp_alt = p;
             else if (id == -2) b.up_alt = p;
@@ -1437,6 +1454,8 @@ static int one_step(ocn_ctx *c, double tau, bool check)
     return OCN_OK;
 }
 
+static bool has_exchange(const ocn_ctx *c);
+
 // (Re)builds the compact static fields when the real(4) fields may have changed, and decides
 // whether the fused step reads them (sw_stencils.h "compact static fields").  Synchronises
 // only when a rebuild was needed (once after init / an upload of a real(4) field).
@@ -1444,17 +1463,29 @@ static int prepare_static(ocn_ctx *c)
 {
     if (!c->compact_req || c->r4_escaped) { c->compact = false; return OCN_OK; }
     if (!c->static_dirty) return OCN_OK;
-    HIPCHK(hipMemsetAsync(c->d_flags, 0, 2 * sizeof(int32_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->d_flags, 0, 3 * sizeof(int32_t), c->stream));
     RC(each_block(c, c->stream, [&](const LBlock &b) { return launch_prepare(&b.g, b.ptr.data(), b.bits, b.rows, c->d_flags, c->stream, b.own); }));
     if (c->ext_ok)   // one_step_x2's row tables: the ext rows' divisor range into the second word
         for (const LBlock &b : c->blocks) RC(launch_rows_ext(&b.g, b.rows, b.rows_x, b.ext, c->d_flags + 1, c->stream));
-    int32_t flags[2] = {0, 0};
+    const bool x4_tabs = c->ext_ok && has_exchange(c);
+    int32_t *d_mask = nullptr;
+    if (x4_tabs) {   // one_step_x4's tables (the neighbours' mask bytes from the basin mask): the third word
+        const size_t nxy = (size_t)c->basin.nx * c->basin.ny;
+        HIPCHK(hipMallocAsync((void **)&d_mask, nxy * sizeof(int32_t), c->stream));
+        HIPCHK(hipMemcpyAsync(d_mask, c->mask.data(), nxy * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        for (const LBlock &b : c->blocks)
+            RC(launch_x4_tables(&b.g, b.bits, b.rows, b.ext, b.bits_x4, b.rows_x4, d_mask, c->basin.nx, c->basin.ny, b.own,
+                                c->d_flags + 2, c->stream));
+        HIPCHK(hipFreeAsync(d_mask, c->stream));
+    }
+    int32_t flags[3] = {0, 0, 0};
     HIPCHK(hipMemcpyAsync(flags, c->d_flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->ring_sea = (flags[0] & kCompactRingSea) != 0;
     c->edge_ring_sea = (flags[0] & kCompactEdgeRingSea) != 0;
     c->udiv_ok = (flags[0] & kCompactDivisorRange) == 0;
     c->rows_x_ok = c->ext_ok && flags[1] == 0;
+    c->x4_tab_ok = x4_tabs && flags[2] == 0;
     c->compact = (flags[0] & ~(kCompactRingSea | kCompactDivisorRange | kCompactEdgeRingSea)) == 0;
     c->static_dirty = false;
     return OCN_OK;
@@ -1564,10 +1595,12 @@ static bool is_flip_field(int id)
 // The vote also carries the other per-rank conditions that decide which launches and exchanges a
 // call runs (one 0/1 word each, max-reduced = OR over the ranks): every rank then takes the same
 // one-pass / hybrid decisions, so the exchange sequences of all ranks match.
-enum { kVoteIncoherent = 0, kVoteIneligible, kVoteUdiv, kVoteHhStale, kVoteX2, kVoteUsed };
+// kVoteX4: this rank cannot run one_step_x4's pairs (its tables, or the known-constant verdict its host
+// has read for the x2 range) -- every rank then runs the same steps and exchanges
+enum { kVoteIncoherent = 0, kVoteIneligible, kVoteUdiv, kVoteHhStale, kVoteX2, kVoteX4, kVoteUsed };
 static_assert(kVoteUsed <= kVoteWords, "vote words");
-struct VoteIn { bool eligible, udiv_ok, hh_consistent, x2_ok; };
-struct VoteOut { bool udiv_ok, hh_consistent, x2_ok; };
+struct VoteIn { bool eligible, udiv_ok, hh_consistent, x2_ok, x4_ok; };
+struct VoteOut { bool udiv_ok, hh_consistent, x2_ok, x4_ok; };
 
 // one_step_x2's condition on the state's halo points that no exchange fills (the rings 1 and 2 of a
 // side, or corner, without a neighbour block): +0.0 in the six state arrays.  The reference never
@@ -1631,6 +1664,7 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
     host[kVoteUdiv] = !in.udiv_ok;
     host[kVoteHhStale] = !in.hh_consistent;
     host[kVoteX2] = !in.x2_ok;
+    host[kVoteX4] = !in.x4_ok;
     HIPCHK(hipMemcpyAsync(c->d_flags, host, sizeof(host), hipMemcpyHostToDevice, c->stream));
     if (in.eligible)
         RC(each_block(c, c->stream, [&](const LBlock &b) { return launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream); }));
@@ -1658,6 +1692,8 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
     out.hh_consistent = w[kVoteHhStale] == 0;
     out.x2_ok = w[kVoteX2] == 0 && exch && c->x2;
     c->x2_dev_ok = out.x2_ok;
+    out.x4_ok = out.x2_ok && w[kVoteX4] == 0;
+    c->x4_dev_ok = out.x4_ok;
     return OCN_OK;
 }
 
@@ -1990,6 +2026,7 @@ static int prebuild_x2(ocn_ctx *c)
         HaloPlan *p;
         rc = get_plan(c, kStateX2, p, 2);
         if (rc == OCN_OK) rc = get_plan(c, kStateX2, p, 1);
+        if (rc == OCN_OK && c->x4 && c->x4_tab_ok) rc = get_plan(c, kStateX2, p, 4);   // (one_step_x4)
         if (i & 2) swap_alt3(c);
         if (i & 1) swap_roles(c);
     }
@@ -2100,6 +2137,39 @@ static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
     return k.one_last ? last_finish(c) : OCN_OK;
 }
 
+// Two x2 steps as one launch per block (sw_kernels.hip MarchStep PAIR + X2): the state exchanged FOUR
+// points deep once (the pair's producers form the first step on the interior and the 2 halo rings
+// neighbours own -- their D 3 deep, from the state 4 deep -- the consumers the second step on the
+// interior), so a block with neighbours runs pairs as a single block does: one exchange and one
+// launch per two steps instead of one each per step.  The extra rings live outside the reference's
+// arrays (allocate: kXRing more rows, the row padding); the second ring is saved / restored around
+// the sequence as for the x2 steps (ring2_run, x2_end).  The known-constant variant (x4_now).
+// (shared/mpp/syncborder_block2D_gen_all.fi:100-129 per stage in the reference: 7 per step)
+static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
+{
+    hipStream_t s = c->stream;
+    ocn_ctx::Rec rec;
+    c->hn_fresh = false;
+    if (k.x2_save) RC(ring2_run(c, true, s));
+    RC(run_sync(c, kStateX2, s, nullptr, 4));   // the state four points deep
+    RC(timer_begin(c, OCN_TIMER_ONEPASS2, rec));
+    RC(each_block(c, s, [&](const LBlock &b) {
+        ocn_block bx = b.g;   // the block widened by kXRing rings, the bases moved to A(bnd_x1 - kXRing, bnd_y1 - kXRing)
+        bx.bnd_x1 -= kXRing; bx.bnd_x2 += kXRing; bx.bnd_y1 -= kXRing; bx.bnd_y2 += kXRing;
+        const long sh = (long)kXRing * b.g.pitch + kXRing;
+        std::vector<void *> tab(b.ptr.size(), nullptr);
+        for (int id = OCN_SSH; id < OCN_SSH + num_r8(c); ++id) tab[field_slot(id)] = b.f<double>(id) - sh;
+        const Compact t{b.bits_x4, b.rows_x4, c->march};
+        return launch_onepass_pair_x4(&bx, tab.data(), (int)tab.size(), &t, c->sw, tau, k.check ? c->d_nbad : nullptr,
+                                      k.check2 ? c->d_nbad : nullptr, (double *)b.sshp_alt - sh, (double *)b.up_alt - sh,
+                                      (double *)b.vp_alt - sh, s, kc_of(c, b), b.own, nullptr, (int)c->blocks.size());
+    }));
+    RC(timer_end(c, rec));
+    swap_alt3(c);
+    swap_roles(c);
+    return OCN_OK;
+}
+
 // Several one-pass steps as one launch (sw_kernels.hip k_march_multi: a grid barrier
 // between the steps; the block's tiles resident together): single small block, no exchange, a
 // variant chosen on the host (multi_ok).  Step parity alternates the buffers as the role flips of
@@ -2156,6 +2226,7 @@ static bool multi_ok(ocn_ctx *c, int32_t check_every)
 static int one_step_fused(ocn_ctx *c, double tau, const StepKind &k)
 {
     if (k.multi) return one_step_multi(c, tau, k);
+    if (k.pair && k.x2) return one_step_x4(c, tau, k);
     if (k.pair) return one_step_pair(c, tau, k);
     // every other step kind may write the n-level depths (hh_update, hh_shift, hh_init), except a
     // single-block one-pass step (not followed by the fused hh_init + A) and the last step's march
@@ -2428,8 +2499,8 @@ struct GridTables {
     std::vector<double> sin_v, cosy_v, cos_xu;         // dsind(yv), dcosd(yv) per row; dcosd(xu) per column
     // the same factors of rows bnd_y1 and bnd_y2 (outside the metric range) from the global row
     // formulas, as the neighbour blocks form them (GridInit ext)
-    float ext_ct[2], ext_cv[2];
-    double ext_sin_v[2], ext_cosy_v[2];
+    float ext_ct[kExtRows], ext_cv[kExtRows];
+    double ext_sin_v[kExtRows], ext_cosy_v[kExtRows];
 };
 static void grid_tables(const ocn_ctx *c, const ocn_block &g, GridTables &t)
 {
@@ -2451,8 +2522,10 @@ static void grid_tables(const ocn_ctx *c, const ocn_block &g, GridTables &t)
         t.cosy_v[r] = dcosd(yv[r]);
     }
     for (int m = g.nx_start - 1; m <= g.nx_end + 1; ++m) t.cos_xu[m - g.bnd_x1] = dcosd(xu[m - g.bnd_x1]);
-    for (int i = 0; i < 2; ++i) {   // grid_base_init on the neighbour: yt(n), yv(n) = (yt(n) + yt(n + 1)) / 2
-        const int n = i == 0 ? g.bnd_y1 : g.bnd_y2;
+    // grid_base_init on the neighbour: yt(n), yv(n) = (yt(n) + yt(n + 1)) / 2 (GridInit ext's rows)
+    const int ext_row[kExtRows] = {g.bnd_y1, g.bnd_y2, g.bnd_y1 - 1, g.bnd_y1 - 2, g.bnd_y2 + 1, g.bnd_y2 + 2};
+    for (int i = 0; i < kExtRows; ++i) {
+        const int n = ext_row[i];
         const double yt_n = bs.rlat + (double)(n - nnn) * bs.dyst, yt_n1 = bs.rlat + (double)(n + 1 - nnn) * bs.dyst;
         const double yv_n = (yt_n + yt_n1) / 2.0;
         t.ext_ct[i] = (float)dcosd(lat_mod(yt_n));
@@ -2523,7 +2596,7 @@ static int init_state(ocn_ctx *c)
         q.cor = 2.0f * kEarthAngVel;
         q.sqrt2 = std::sqrt(2.0f);
         q.curve = bs.curve_grid != 0;
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < kExtRows; ++j) {
             q.ext_ct[j] = t.ext_ct[j]; q.ext_cv[j] = t.ext_cv[j];
             q.ext_sin_v[j] = t.ext_sin_v[j]; q.ext_cosy_v[j] = t.ext_cosy_v[j];
         }
@@ -3169,6 +3242,26 @@ static bool x2_local(const ocn_ctx *c)
     return true;
 }
 
+// one_step_x4's static conditions on this rank (with x2_local's): its tables, no tracers (expl_tracer
+// after every step), the known-constant variant allowed, every block of the grid at least 4 x 4 (its
+// 4-deep strips lie in its interior) and row padding for the extra rings
+static bool x4_local(const ocn_ctx *c)
+{
+    if (!c->x4 || !c->x4_tab_ok || !c->known_const || c->r8_handed || c->sw.use_tracers > 0 || !c->march)
+        return false;
+    for (const GBlock &g : c->gblocks)
+        if (g.rank >= 0 && (g.g.nx_end - g.g.nx_start < 3 || g.g.ny_end - g.g.ny_start < 3)) return false;
+    for (const LBlock &b : c->blocks)
+        if (b.g.pitch < (int64_t)(b.g.bnd_x2 - b.g.bnd_x1 + 1 + 2 * kXRing)) return false;
+    return true;
+}
+// pairs of x2 steps in this call (after prepare_kc): x4_local on every rank (the vote) or this one
+// (one process), the known-constant variant chosen on the host
+static bool x4_now(const ocn_ctx *c)
+{
+    return c->kc_mode == OCN_KC_KNOWN && (has_comm(c) ? c->x4_dev_ok : x4_local(c) && c->fb_x2);
+}
+
 // The pending tail of an open sequence: the last step run (a one-pass step) is run again from the
 // previous state -- untouched in the other buffer of each pair and the other sshp / ubrtrp / vbrtrp
 // buffers -- as the call's last step (one_step_last: the same new state bit for bit, plus vort,
@@ -3194,11 +3287,14 @@ static int complete_open(ocn_ctx *c)
             StepKind k1{};
             k1.check = c->deferred_check[0];
             k1.flip = k1.one = k1.next_one = k1.a_done = true;
+            k1.x2 = c->open_x2;   // (x2 sequences with pairs of x2 steps: one_step_x4 deferred it)
             if (const int rc = run_step(c, c->open_tau, k1)) return finish_call(c, rc);
         }
         StepKind k{};
         k.last = k.one_last = true;
         k.check = c->deferred_check[d - 1];
+        k.x2_end = c->ring2_saved;
+        c->ring2_saved = false;
         return finish_call(c, run_step(c, c->open_tau, k));
     }
     swap_roles(c);
@@ -3213,6 +3309,7 @@ static int complete_open(ocn_ctx *c)
         }
         StepKind k1{};
         k1.flip = k1.one = k1.next_one = k1.a_done = true;
+        k1.x2 = c->open_x2;   // (a pair of x2 steps: its first step again, one_step_x2)
         if (const int rc = run_step(c, c->open_tau, k1)) return finish_call(c, rc);
     }
     StepKind k{};
@@ -3237,7 +3334,9 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
             // the constants are what its last step left), and the tail stays pending; a device
             // verdict the host has read since selects one variant
             RC(prepare_kc(c, c->open_x2));
-            const bool pairs = !c->open_x2 && pair_ok(c);
+            // (x2 sequences: pairs of x2 steps, one_step_x4)
+            const bool pairs = c->open_x2 ? x4_now(c) : pair_ok(c);
+            c->x4_used = c->open_x2 && pairs;
             int rc = OCN_OK;
             if (pairs) {   // two steps per launch -- the steps deferred by the last call first -- while
                            // 3 or more are pending; the last 1 or 2 deferred (next call, complete_open)
@@ -3250,6 +3349,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
                     k.check = chk[i];
                     k.check2 = chk[i + 1];
                     k.flip = k.one = k.next_one = k.a_done = k.pair = true;
+                    k.x2 = c->open_x2;
                     rc = graph_ok ? graph_step(c, tau, k) : run_step(c, tau, k);
                     c->open_pair = c->pair_used = true;
                 }
@@ -3294,13 +3394,16 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     // with RCCL every rank takes part in the decisions (check_coherence reduces the verdicts)
     const bool eligible = flip_eligible(c);
     const bool x2_here = x2_local(c);
+    // one_step_x4 possible on this rank: its static conditions and a known-constant verdict for the x2
+    // range its host has read (the variant the pairs run; kFbZero stays put through prepare_kc(x2))
+    const bool x4_here = x2_here && x4_local(c) && c->fb_state == kFbZero && c->fb_x2;
     // a lazy call is planned as the first nsteps steps of a call of nsteps + 1 (the last deferred)
     const bool lazy_cand = eligible && c->onepass && lazy_allowed(c, x2_here);
     bool udiv_ok = c->udiv_ok, first_one = c->hh_consistent, x2_ok = x2_here && c->x2_dev_ok;
     int N = lazy_cand ? nsteps + 1 : nsteps;
     if (N >= 2 && (eligible || (has_comm(c) && c->flip)) && !c->coherent_known) {
         VoteOut v;
-        RC(check_coherence(c, VoteIn{eligible, c->udiv_ok, c->hh_consistent, x2_here}, v));
+        RC(check_coherence(c, VoteIn{eligible, c->udiv_ok, c->hh_consistent, x2_here, x4_here}, v));
         udiv_ok = v.udiv_ok;
         first_one = v.hh_consistent;
         x2_ok = x2_here && v.x2_ok;
@@ -3375,7 +3478,10 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     RC(join_sync(c));
     // two one-pass steps per launch where both are plain one-pass steps and the second is not the
     // last one run (a lazy tail redoes that one from the state before it, which a pair never writes)
-    const bool pairs = one_call && !x2_call && pair_ok(c);
+    // (with exchanges: pairs of x2 steps with one 4-deep exchange each, one_step_x4)
+    const bool x4_call = one_call && x2_call && x4_now(c);
+    c->x4_used = x4_call;
+    const bool pairs = one_call && (x2_call ? x4_call : pair_ok(c));
     auto plain_one = [&](int s) {   // step s is a one-pass step that needs nothing around its launch
         const bool one = one_call && (s >= 2 || first_one) && s <= N - 1, next_one = one_call && s + 1 <= N - 1;
         const bool next_a = ca && flip_call && s != N && !next_one && !(last_one && s + 1 == N);
@@ -3457,8 +3563,9 @@ static int run_deferred(ocn_ctx *c)
     StepKind k{};
     k.check = c->deferred_check[0];
     k.flip = k.one = k.next_one = k.a_done = true;
-    k.pair = c->deferred == 2;   // (a pair only where pairs ran: pair_ok held when they were deferred)
+    k.pair = c->deferred == 2;   // (a pair only where pairs ran: pair_ok / x4_now held when they were deferred)
     k.check2 = k.pair && c->deferred_check[1];
+    k.x2 = c->open_x2;
     c->open_pair = k.pair;
     c->deferred = 0;
     if (const int rc = run_step(c, c->open_tau, k)) { c->open = false; return finish_call(c, rc); }
@@ -3667,6 +3774,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         c->coherent_known = false;
         return OCN_OK;
     case OCN_OPT_MULTI_SPIN: c->multi_spin = value < 1 ? 1 : value > kMultiSpin ? kMultiSpin : (int)value; return OCN_OK;
+    case OCN_OPT_X4: c->x4 = value != 0; c->coherent_known = false; return OCN_OK;
     case OCN_OPT_BATCH:
         if (c->batch != (value != 0)) drop_graphs(c);
         c->batch = value != 0;
@@ -3709,6 +3817,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_MULTI: *value = c->multi_used ? 2 : c->multi; return OCN_OK;
     case OCN_OPT_TRACER_STEP: *value = c->tr_call ? 2 : c->tr_step; return OCN_OK;
     case OCN_OPT_MULTI_SPIN: *value = c->multi_spin; return OCN_OK;
+    case OCN_OPT_X4: *value = c->x4_used ? 2 : c->x4; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

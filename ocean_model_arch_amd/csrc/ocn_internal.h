@@ -108,13 +108,21 @@ struct GridInit {
     double cos_rot, sin_rot, sin_extr;             // dcosd / dsind(rotation_on_lat), dsind(lat_extr)
     float sx, sy, cor, sqrt2;                      // base steps (m), 2 * EarthAngVel, sqrt(2.0)
     int curve;
-    // rows bnd_y1 / bnd_y2 (outside the metric range): their factors and where their metric values
-    // go (2 x (OCN_NUM_R4 - OCN_DX) floats: OCN_DX .. OCN_R_DISS of each; nullptr: not formed)
-    float ext_ct[2], ext_cv[2];
-    double ext_sin_v[2], ext_cosy_v[2];
+    // rows outside the metric range: their factors and where their metric values go (kExtRows x
+    // (OCN_NUM_R4 - OCN_DX) floats: OCN_DX .. OCN_R_DISS of each; nullptr: not formed) -- rows
+    // bnd_y1, bnd_y2 (the x2 steps' second ring), then bnd_y1 - 1, bnd_y1 - 2, bnd_y2 + 1, bnd_y2 + 2
+    // (the x4 pairs' third and fourth rings, outside the reference's arrays)
+    static constexpr int kExt = 6;
+    float ext_ct[kExt], ext_cv[kExt];
+    double ext_sin_v[kExt], ext_cosy_v[kExt];
     float *ext;
 };
-constexpr int kExtRowFloats = 2 * (OCN_NUM_R4 - OCN_DX);
+constexpr int kExtRows = GridInit::kExt;
+constexpr int kExtRowFloats = kExtRows * (OCN_NUM_R4 - OCN_DX);
+// Extra halo rings of every real(8) field and of the x4 mask bytes beyond the reference's 2
+// (bnd_x1 - kXRing .. bnd_x2 + kXRing, bnd_y1 - kXRing .. bnd_y2 + kXRing addressable): the pair
+// launches with halo exchanges read the state 4 points out (ocn_ctx.hip one_step_x4)
+constexpr int kXRing = 2;
 int launch_init_grid(const GridInit &q, hipStream_t s);
 // gaussian_elimination_kernel (vel_ssh.f90:15-38) into p (zero outside the sea interior)
 int launch_gaussian(const ocn_block &g, double *p, const float *lu, int nx0, int ny0, double sigma, hipStream_t s);
@@ -147,6 +155,21 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                         double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
                         hipStream_t s, const OnepassKC &kc, bool last = false);
+// Two one-pass steps per launch with halo exchanges (sw_kernels.hip MarchStep PAIR + X2; ocn_ctx.hip
+// one_step_x4): bx = the block widened by kXRing rings, ptr / cp over that geometry (launch_x4_tables),
+// the state exchanged 4 deep; the known-constant variant (kc.mode OCN_KC_KNOWN); own: the halo points
+// neighbour blocks own; range: the consumers' points (nullptr: the interior); nblk: blocks of this
+// size batched into the launch (the tile height's cost model)
+int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                           double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
+                           hipStream_t s, const OnepassKC &kc, unsigned own, const Range *range = nullptr,
+                           int nblk = 1);
+// one_step_x4's tables of block g: mask bytes over g widened by kXRing (bits4, its base at
+// A(bnd_x1 - kXRing, bnd_y1 - kXRing), pitch g->pitch) and the row table of those rows (rows4,
+// row_table_size(rows + 2 kXRing)) from the block's own tables, its ext rows and the basin mask
+// (device, nx x ny); ORs OCN_COMPACT_DIVISOR_RANGE into *flags
+int launch_x4_tables(const ocn_block *g, const uint8_t *bits, const float *rows, const float *ext, uint8_t *bits4,
+                     float *rows4, const int32_t *mask, int nx, int ny, unsigned own, int32_t *flags, hipStream_t s);
 // nsteps one-pass steps in one launch (sw_kernels.hip k_march_multi): single small block, no
 // exchange, a variant chosen on the host; step 1 reads the table's buffers, each step the buffers
 // the previous one wrote (the role pairs and sshp / ubrtrp / vbrtrp against *_alt, alternating);

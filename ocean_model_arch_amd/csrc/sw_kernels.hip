@@ -428,6 +428,10 @@ template <class B> struct HasPrologue<B, std::void_t<decltype(B::kPrologue)>> { 
 // a two-step body (Body::kPair: MarchStep PAIR; march_tile deals its waves the two roles)
 template <class B, class = void> struct HasPair { static constexpr bool v = false; };
 template <class B> struct HasPair<B, std::void_t<decltype(B::kPair)>> { static constexpr bool v = B::kPair; };
+// a two-step body with halo exchanges (MarchStep PAIR + X2: ocn_ctx.hip one_step_x4): its producers
+// also update the halo points neighbour blocks own, 2 deep
+template <class B, class = void> struct HasX2 { static constexpr bool v = false; };
+template <class B> struct HasX2<B, std::void_t<decltype(B::kX2)>> { static constexpr bool v = B::kX2; };
 // a body whose launch may be void at run time (Body::enabled(), a device-side predicate read by
 // every workgroup before anything else: the one-pass step's two variants, one of which a device
 // check selected -- ocn_ctx.hip launches both and never waits for the verdict)
@@ -543,8 +547,12 @@ template <class Body, bool PRO> __device__ __forceinline__ void march_tile(const
         Lane L;
         L.pr = prod ? 1 : 2;
         L.j = min(max(m - (c0 - 2), 0), 2 * 60 - 1);
-        L.out = lane >= 2 && lane < 62 && m >= R.m0 && m <= (prod ? R.m1 : min(R.m1, c0 + Body::kPairCols - 1));
-        L.ccol = m >= c0 && m < c0 + Body::kPairCols;   // a producer counts its workgroup's columns only
+        // (X2: the producers' columns reach 2 into the halo; iteration keeps the points neighbours own)
+        constexpr int xh = HasX2<Body>::v ? 2 : 0;
+        L.out = lane >= 2 && lane < 62 &&
+                (prod ? m >= R.m0 - xh && m <= R.m1 + xh : m >= R.m0 && m <= min(R.m1, c0 + Body::kPairCols - 1));
+        // a producer counts its workgroup's (interior) columns only
+        L.ccol = m >= c0 && m < c0 + Body::kPairCols && m >= R.m0 && m <= R.m1;
         L.m = L.me = min(max(m, R.mlo), R.mhi);
         L.edge = false;
         body.march(L, nb, ne);
@@ -1883,12 +1891,18 @@ struct StepRegs {
 // so D there is formed here as the neighbour forms it on its interior -- what the reference's
 // exchanges of D deliver -- and the march covers the whole interior.
 // WT: write-through stores (sc1), for the multi-step launch (k_march_multi)
+// PAIR + X2 (ocn_ctx.hip one_step_x4): two steps per launch on a block with halo exchanges, over the
+// block's geometry widened by kXRing rings (ocn_internal.h; the arrays' bases moved to match): the
+// exchange before it delivered the state 4 points deep, the producers update the halo points
+// neighbours own 2 deep as those neighbours do (their D 3 deep, from the state 4 deep); the known-
+// constant variant only (h_r, mu, the forcing and the fallback values are not read).
 template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR = false, bool PAIR = false,
           bool WT = false>
 struct MarchStep {
-    static_assert(!PAIR || !X2, "two-step launches: no x2");
+    static_assert(!PAIR || !X2 || (ZF && !HR && !LAST), "two-step launches with exchanges: the known-constant variant");
     static constexpr int kStAux = WT ? 16 : 0;
     static constexpr bool kPair = PAIR;
+    static constexpr bool kX2 = X2;
     static constexpr int kPairCols = 116;   // PAIR: a workgroup's output columns (2 x 60 produced, less 2 each side)
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
@@ -2441,8 +2455,19 @@ struct MarchStep {
         Lane L = L0;
         asm volatile("" : "+v"(L.m));
         if (RO == 1) {   // PAIR producer: rows outside the interior keep their state; the count is the
-            L.out = L.out && n >= b.ny_start && n <= b.ny_end;   // workgroup's own points' (its columns,
-            x.cnt = L.ccol && n >= nb + 2 && n <= ne - 2;        // rows nb + 2 .. ne - 2)
+            // workgroup's own points' (its columns, rows nb + 2 .. ne - 2).  X2: a halo point a neighbour
+            // owns is one of its interior points -- updated as it updates it (the pair's exchange
+            // delivered the state 4 deep: one_step_x4)
+            const bool iny = n >= b.ny_start && n <= b.ny_end;
+            if constexpr (X2) {
+                const bool inx = L.m >= b.nx_start && L.m <= b.nx_end;
+                const bool owned =
+                    (own >> (own_class(L.m, b.nx_start, b.nx_end) * 3u + own_class(n, b.ny_start, b.ny_end))) & 1u;
+                L.out = L.out && ((inx && iny) || owned);
+            } else {
+                L.out = L.out && iny;
+            }
+            x.cnt = L.ccol && n >= nb + 2 && n <= ne - 2;
         }
         take<PH>(x, q);
         Fallback fbn;
@@ -2967,8 +2992,9 @@ int launch_onepass_multi(const ocn_block *b, void *const *ptr, int nptr, const C
 }
 
 // Rows per workgroup tile of the two-step launch: the fewest iterations in total, counting
-// ceil(waves / slots) rounds of rows + 8 iterations each (MarchStep::march)
-static int pair_rows(const Range &r, int cols)
+// ceil(waves / slots) rounds of rows + 8 iterations each (MarchStep::march); mult = blocks of this
+// size in one launch (a batch: one_step_x4 on several blocks of a device)
+static int pair_rows(const Range &r, int cols, int mult = 1)
 {
     const long wx = (r.m1 - r.m0 + cols) / cols, h = r.n1 - r.n0 + 1;
     // a tuning override (a fixed tile height), read once per process -- not a libc call per launch
@@ -2981,7 +3007,7 @@ static int pair_rows(const Range &r, int cols)
     int best = 8;
     long cost = -1;
     for (int rows = 8; rows <= OCN_PAIR_MAX_ROWS; ++rows) {
-        const long tiles = (h + rows - 1) / rows, waves = 4 * tiles * wx,
+        const long tiles = (h + rows - 1) / rows, waves = 4 * tiles * wx * mult,
                    rounds = (waves + OCN_STEP_SLOTS - 1) / OCN_STEP_SLOTS, c = rounds * (rows + 8);
         if (cost < 0 || c < cost) { cost = c; best = rows; }
     }
@@ -3024,6 +3050,100 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
     OCN_PAIR_VARIANT(false);
 #undef OCN_PAIR_VARIANT
 #undef OCN_PAIR_LAUNCH
+}
+
+// Two one-pass steps per launch on a block with halo exchanges (ocn_ctx.hip one_step_x4): bx = the
+// block widened by kXRing rings, ptr / cp->bits / cp->rows its tables over that geometry (bases at
+// A(bnd_x1 - kXRing, bnd_y1 - kXRing)), the state exchanged 4 points deep; the known-constant variant.
+// range (default: the interior): the points the consumers write.
+int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
+                           double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
+                           hipStream_t s, const OnepassKC &kc, unsigned own, const Range *range, int nblk)
+{
+    if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
+        !up_out || !vp_out)
+        return set_error(OCN_ERR_ARG, "x4 two-step launch: compact tables, march, full_free_surface = 1, trans_terms "
+                                      "and ksw_lat on, three second buffers");
+    if (kc.mode != OCN_KC_KNOWN || !kc.kc)
+        return set_error(OCN_ERR_ARG, "x4 two-step launch: the known-constant variant chosen on the host");
+    RC_K(check_block(bx));
+    if (bx->bnd_x1 > bx->nx_start - 4 || bx->bnd_x2 < bx->nx_end + 4 || bx->bnd_y1 > bx->ny_start - 4 ||
+        bx->bnd_y2 < bx->ny_end + 4)
+        return set_error(OCN_ERR_ARG, "x4 two-step launch: the geometry must reach 4 points past the interior");
+    const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(bx), 0);
+    const Range r = range ? *range : range_interior(bx);
+    if (range_empty(r)) return OCN_OK;
+    using KP = MarchStep<true, false, true, true, false, true>;
+    // a batch puts up to P blocks' tiles in one launch (MarchBatch): their waves share its rounds
+    constexpr int P = kPack<KP> < kBatchMax / 4 ? kPack<KP> : kBatchMax / 4;
+    const int cols = KP::kPairCols, rows = pair_rows(r, cols, batching(s) ? std::max(1, std::min(nblk, P)) : 1);
+    MarchGrid g{};
+    const int ntx = (r.m1 - r.m0 + cols) / cols;
+    g.r[0] = MarchRect{r.m0, r.m1, r.n0, r.n1, r.m0, ntx, ntx * ((r.n1 - r.n0 + rows) / rows), max(r.m0 - 4, bx->bnd_x1),
+                       min(r.m1 + 4, bx->bnd_x2), rows, 0};
+    g.nr = 1;
+    g.ntiles = g.r[0].tiles;
+    int ex;
+    if (std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020)   // tau = 2^k
+        return issue_march(g, MarchStep<true, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out,
+                                                                             vp_out, kc.kc, nullptr, 0, own, nbad2}, s);
+    return issue_march(g, MarchStep<false, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out,
+                                                                          vp_out, kc.kc, nullptr, 0, own, nbad2}, s);
+}
+
+// mask bytes of one_step_x4 over the widened geometry bx: at the halo points neighbour blocks own
+// (own_class bits), up to kXRing rings past the reference's arrays, lu_init + lu_lv_init of the basin
+// mask as the neighbour's init forms them on its interior (init_kernels.hip k_init_grid); elsewhere
+// inside the arrays the block's own bytes (Prepare); +0 outside.
+__global__ void k_bits_x4(ocn_block bx, ocn_block g, const uint8_t *bits, uint8_t *out, const int32_t *mask, int nx, int ny,
+                          unsigned own)
+{
+    const int w = bx.bnd_x2 - bx.bnd_x1 + 1, h = bx.bnd_y2 - bx.bnd_y1 + 1;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)w * h) return;
+    const int m = bx.bnd_x1 + (int)(i % w), n = bx.bnd_y1 + (int)(i / w);
+    const unsigned cls = own_class(m, g.nx_start, g.nx_end) * 3u + own_class(n, g.ny_start, g.ny_end);
+    unsigned v = 0;
+    if (cls != 4u && ((own >> cls) & 1u) && m >= 1 && m < nx && n >= 1 && n < ny) {
+        auto lu = [&](int mm, int nn) -> unsigned { return mask[(long)(mm - 1) + (long)(nn - 1) * nx] == 0 ? 1u : 0u; };
+        const unsigned a = lu(m, n), b = lu(m + 1, n), c = lu(m, n + 1), d = lu(m + 1, n + 1);
+        v = (a << OCN_LU) | ((a & b & c & d) << OCN_LUU) | ((a | b | c | d) << OCN_LUH) | ((a & b) << OCN_LCU) |
+            ((a & c) << OCN_LCV) | ((a | b) << OCN_LLU) | ((a | c) << OCN_LLV);
+    } else if (m >= g.bnd_x1 && m <= g.bnd_x2 && n >= g.bnd_y1 && n <= g.bnd_y2) {
+        v = bits[(long)(m - g.bnd_x1) + (long)(n - g.bnd_y1) * g.pitch];
+    }
+    out[(long)(m - bx.bnd_x1) + (long)(n - bx.bnd_y1) * bx.pitch] = (uint8_t)v;
+}
+
+// one_step_x4's row table over the widened rows: the block's rows bnd_y1 + 1 .. bnd_y2 - 1 (the metric
+// range) from its compact table, the ext rows (the neighbours' rows bnd_y1 - 2 .. bnd_y1 and bnd_y2 ..
+// bnd_y2 + 2, GridInit ext) around them; ORs OCN_COMPACT_DIVISOR_RANGE into *flags if a divisor is out
+// of udiv's range
+__global__ void k_rows_x4(float *rows4, unsigned nrows4, const float *rows, unsigned nrows, const float *ext, int *flags)
+{
+    const unsigned r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows4) return;
+    float v[kNumRowFields];
+    // ext rows: 0 bnd_y1, 1 bnd_y2, 2 bnd_y1 - 1, 3 bnd_y1 - 2, 4 bnd_y2 + 1, 5 bnd_y2 + 2
+    const int e = r == 0 ? 3 : r == 1 ? 2 : r == 2 ? 0 : r == nrows4 - 3 ? 1 : r == nrows4 - 2 ? 4 : r == nrows4 - 1 ? 5 : -1;
+    for (int k = 0; k < kNumRowFields; ++k)
+        v[k] = e >= 0 ? ext[e * kNumRowFields + k] : rows[(unsigned)k * nrows + (r - kXRing)];
+    if (!write_table_row(rows4, nrows4, r, v)) atomicOr(flags, (int)OCN_COMPACT_DIVISOR_RANGE);
+}
+
+int launch_x4_tables(const ocn_block *g, const uint8_t *bits, const float *rows, const float *ext, uint8_t *bits4,
+                     float *rows4, const int32_t *mask, int nx, int ny, unsigned own, int32_t *flags, hipStream_t s)
+{
+    RC_K(check_block(g));
+    ocn_block bx = *g;
+    bx.bnd_x1 -= kXRing; bx.bnd_x2 += kXRing; bx.bnd_y1 -= kXRing; bx.bnd_y2 += kXRing;
+    const long pts = (long)(bx.bnd_x2 - bx.bnd_x1 + 1) * (bx.bnd_y2 - bx.bnd_y1 + 1);
+    hipLaunchKernelGGL(k_bits_x4, dim3((unsigned)((pts + 255) / 256)), dim3(256), 0, s, bx, *g, bits, bits4, mask, nx, ny,
+                       own);
+    RC_K(check_launch());
+    const unsigned nrows = block_rows(g), nrows4 = block_rows(&bx);
+    hipLaunchKernelGGL(k_rows_x4, dim3((nrows4 + 63) / 64), dim3(64), 0, s, rows4, nrows4, rows, nrows, ext, (int *)flags);
+    return check_launch();
 }
 
 // tracer stage `stage` (OCN_TSTAGE_*) of tracer k on one block; factor_mu = 1.0d0 as the PSy

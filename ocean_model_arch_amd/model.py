@@ -259,6 +259,17 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MULTI, int(on)), "ocn_ctx_set_option")
         return self
 
+    def set_x4(self, on: bool = True):
+        """Blocks with halo exchanges: two x2 steps per launch with one 4-deep state exchange per two
+        steps (default on, OCN_OPT_X4); same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_X4, int(on)), "ocn_ctx_set_option")
+        return self
+
+    @property
+    def x4_active(self) -> bool:
+        """Whether the last step() ran pairs of x2 steps (one_step_x4)."""
+        return self.option(_lib.OPT_X4) == 2
+
     def set_multi_spin(self, polls: int):
         """Diagnostics: the multi-step launch's grid barrier gives up after `polls` polls (default
         1 << 20, about 0.5 s); the next synchronize() then raises OCN_ERR_HIP."""

@@ -61,13 +61,44 @@ def summary(sq, kernel):
     return out
 
 
+def merged(dirs, kernel):
+    """summary() of each counter pass (its own run of the same command: the same launches), merged:
+    the per-launch means of every counter any pass collected (SQ_WAVES, in several, must agree)."""
+    outs = [s for d in dirs if (s := summary(d, kernel))]
+    if not outs:
+        return None
+    out = outs[0]
+    for o in outs[1:]:
+        for k, v in o["per_launch"].items():
+            out["per_launch"].setdefault(k, v)
+        for k, v in o["per_wave"].items():
+            out["per_wave"].setdefault(k, v)
+        out.setdefault("clock", o.get("clock"))
+        out["dispatches_per_pass"] = out.get("dispatches_per_pass", [outs[0]["dispatches"]]) + [o["dispatches"]]
+    pl = out["per_launch"]
+    # VALU instructions by class (SQ_INSTS_VALU_* passes): the f64 arithmetic the reference's order
+    # requires vs the rest (integer / address arithmetic, conversions, moves, DPP shifts, selects)
+    f64 = [k for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                       "SQ_INSTS_VALU_TRANS_F64") if k in pl]
+    if f64 and pl.get("SQ_INSTS_VALU"):
+        tot = pl["SQ_INSTS_VALU"]
+        cls = {k[len("SQ_INSTS_VALU_"):].lower(): pl[k] for k in pl if k.startswith("SQ_INSTS_VALU_")}
+        known = sum(cls.values())
+        out["valu_classes"] = {"per_launch": cls, "f64": sum(pl[k] for k in f64),
+                               "f64_frac": round(sum(pl[k] for k in f64) / tot, 4),
+                               "unclassified": round(tot - known), "unclassified_frac": round((tot - known) / tot, 4),
+                               "note": "SQ_INSTS_VALU_<class> counters; unclassified = SQ_INSTS_VALU - their sum "
+                                       "(moves, DPP shifts, selects, compares, bit ops)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("sq")
+    ap.add_argument("sq", nargs="+", help="one directory per counter pass of the same command")
     ap.add_argument("--box", required=True)
     ap.add_argument("--blocks", required=True)
     a = ap.parse_args()
-    kern = {stage: s for stage, k in KERNELS.items() if (s := summary(a.sq, k))}
+    kern = {stage: s for stage, k in KERNELS.items() if (s := merged(a.sq, k))}
     if not kern:
         raise SystemExit("no dispatches of the one-pass kernels")
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))

@@ -236,8 +236,8 @@ def test_multi_barrier_timeout_reports_and_recovers(amd):
     n = 100
     m = amd.OceanModel(amd.box_config(n)).init()
     try:
+        m.set_multi_spin(1)   # (an option change closes an open sequence: set it first)
         m.step(2, check_every=1).synchronize()   # the verdict reaches the host: the next call is multi
-        m.set_multi_spin(1)
         m.step(12, check_every=1)
         used = m.multi_active
         with pytest.raises(amd.OcnError, match="grid barrier timed out"):
