@@ -1212,7 +1212,8 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
         if (p->n_unpack)
             hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_unpack, p->ch_unpack), dim3(kSegChunk), 0, stream, p->d_unpack,
                                p->n_unpack, cmp);
-        return check_launch();
+        RC(check_launch());
+        return remote ? exchange_done(c, xrec, stream) : OCN_OK;
     }
     if (p->n_local) {
         hipLaunchKernelGGL(k_segments, dim3(p->n_local, p->ch_local), dim3(kSegChunk), 0, stream, p->d_local, p->n_local);
@@ -2145,15 +2146,31 @@ static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
 // arrays (allocate: kXRing more rows, the row padding); the second ring is saved / restored around
 // the sequence as for the x2 steps (ring2_run, x2_end).  The known-constant variant (x4_now).
 // (shared/mpp/syncborder_block2D_gen_all.fi:100-129 per stage in the reference: 7 per step)
+// The part of the interior a pair of x2 steps computes without the exchange: the interior less 4
+// points on every side a neighbour (diagonals included) fills halos of (the pair reads the state 4
+// points out: the producers' D 3 out, from the state 4 out).
+static Range x4_inner(const LBlock &b)
+{
+    auto any = [&](int a, int d1, int d2) { return b.nbr_rank[a - 1] >= 0 || b.nbr_rank[d1 - 1] >= 0 || b.nbr_rank[d2 - 1] >= 0; };
+    Range r{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
+    if (any(1, 5, 6)) r.m1 -= 4;   // E, NE, SE
+    if (any(2, 7, 8)) r.m0 += 4;   // W, NW, SW
+    if (any(3, 5, 7)) r.n1 -= 4;   // N, NE, NW
+    if (any(4, 6, 8)) r.n0 += 4;   // S, SE, SW
+    return r;
+}
+
+// With OCN_OPT_OVERLAP 2 (the default with remote peers; not while capturing): the inner part
+// (x4_inner) on the compute stream beside the exchange on the comm stream (the device's highest
+// priority), then the bands around it there -- the RCCL group's latency hides behind the inner
+// pair; the two launches write disjoint points of the new state (other buffers than the ones read),
+// the exchange writes halos only the bands read.
 static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
 {
     hipStream_t s = c->stream;
     ocn_ctx::Rec rec;
     c->hn_fresh = false;
-    if (k.x2_save) RC(ring2_run(c, true, s));
-    RC(run_sync(c, kStateX2, s, nullptr, 4));   // the state four points deep
-    RC(timer_begin(c, OCN_TIMER_ONEPASS2, rec));
-    RC(each_block(c, s, [&](const LBlock &b) {
+    auto pair = [&](const LBlock &b, hipStream_t st, const Range *range, const Range *frame_of) -> int {
         ocn_block bx = b.g;   // the block widened by kXRing rings, the bases moved to A(bnd_x1 - kXRing, bnd_y1 - kXRing)
         bx.bnd_x1 -= kXRing; bx.bnd_x2 += kXRing; bx.bnd_y1 -= kXRing; bx.bnd_y2 += kXRing;
         const long sh = (long)kXRing * b.g.pitch + kXRing;
@@ -2162,9 +2179,48 @@ static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
         const Compact t{b.bits_x4, b.rows_x4, c->march};
         return launch_onepass_pair_x4(&bx, tab.data(), (int)tab.size(), &t, c->sw, tau, k.check ? c->d_nbad : nullptr,
                                       k.check2 ? c->d_nbad : nullptr, (double *)b.sshp_alt - sh, (double *)b.up_alt - sh,
-                                      (double *)b.vp_alt - sh, s, kc_of(c, b), b.own, nullptr, (int)c->blocks.size());
-    }));
-    RC(timer_end(c, rec));
+                                      (double *)b.vp_alt - sh, st, kc_of(c, b), b.own, range, (int)c->blocks.size(),
+                                      frame_of);
+    };
+    bool inner_ok = true;   // (every block keeps an inner part: the bands around it are disjoint)
+    for (const LBlock &b : c->blocks) {
+        const Range in = x4_inner(b);
+        inner_ok = inner_ok && in.m0 <= in.m1 && in.n0 <= in.n1;
+    }
+    if (overlap_level(c) >= 2 && !c->capturing && inner_ok) {
+        HIPCHK(hipEventRecord(c->ev_fork, s));
+        RC(timer_begin(c, OCN_TIMER_ONEPASS2, rec));
+        RC(each_block(c, s, [&](const LBlock &b) -> int {
+            const Range in = x4_inner(b);
+            return pair(b, s, &in, nullptr);
+        }));
+        RC(timer_end(c, rec));
+        ocn_ctx::Rec xrec{OCN_TIMER_EXPOSED, nullptr, nullptr};   // inner pair end -> comm chain end
+        if (c->stage_timing) {
+            RC(get_event(c, xrec.a)); RC(get_event(c, xrec.b));
+            HIPCHK(hipEventRecord(xrec.a, s));
+        }
+        HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
+        if (k.x2_save) RC(ring2_run(c, true, c->comm_stream));
+        RC(run_sync(c, kStateX2, c->comm_stream, nullptr, 4));   // the state four points deep
+        RC(each_block(c, c->comm_stream, [&](const LBlock &b) -> int {
+            const Range in = x4_inner(b);
+            return pair(b, c->comm_stream, nullptr, &in);
+        }));
+        if (xrec.b) {
+            HIPCHK(hipEventRecord(xrec.b, c->comm_stream));
+            c->recs.push_back(xrec);
+        }
+        HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
+        c->sync_pending = true;
+        RC(join_sync(c));
+    } else {
+        if (k.x2_save) RC(ring2_run(c, true, s));
+        RC(run_sync(c, kStateX2, s, nullptr, 4));   // the state four points deep
+        RC(timer_begin(c, OCN_TIMER_ONEPASS2, rec));
+        RC(each_block(c, s, [&](const LBlock &b) { return pair(b, s, nullptr, nullptr); }));
+        RC(timer_end(c, rec));
+    }
     swap_alt3(c);
     swap_roles(c);
     return OCN_OK;

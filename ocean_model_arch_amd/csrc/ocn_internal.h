@@ -158,12 +158,13 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
 // Two one-pass steps per launch with halo exchanges (sw_kernels.hip MarchStep PAIR + X2; ocn_ctx.hip
 // one_step_x4): bx = the block widened by kXRing rings, ptr / cp over that geometry (launch_x4_tables),
 // the state exchanged 4 deep; the known-constant variant (kc.mode OCN_KC_KNOWN); own: the halo points
-// neighbour blocks own; range: the consumers' points (nullptr: the interior); nblk: blocks of this
-// size batched into the launch (the tile height's cost model)
+// neighbour blocks own; range: the consumers' points (nullptr: the interior), frame_of: only the bands
+// of it outside *frame_of (one launch of up to 4 rects); nblk: blocks of this size batched into the
+// launch (the tile height's cost model)
 int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                            double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
                            hipStream_t s, const OnepassKC &kc, unsigned own, const Range *range = nullptr,
-                           int nblk = 1);
+                           int nblk = 1, const Range *frame_of = nullptr);
 // one_step_x4's tables of block g: mask bytes over g widened by kXRing (bits4, its base at
 // A(bnd_x1 - kXRing, bnd_y1 - kXRing), pitch g->pitch) and the row table of those rows (rows4,
 // row_table_size(rows + 2 kXRing)) from the block's own tables, its ext rows and the basin mask

@@ -3058,7 +3058,8 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
 // range (default: the interior): the points the consumers write.
 int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                            double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
-                           hipStream_t s, const OnepassKC &kc, unsigned own, const Range *range, int nblk)
+                           hipStream_t s, const OnepassKC &kc, unsigned own, const Range *range, int nblk,
+                           const Range *frame_of)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
@@ -3071,18 +3072,32 @@ int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, cons
         bx->bnd_y2 < bx->ny_end + 4)
         return set_error(OCN_ERR_ARG, "x4 two-step launch: the geometry must reach 4 points past the interior");
     const Tab<true> t = make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(bx), 0);
-    const Range r = range ? *range : range_interior(bx);
-    if (range_empty(r)) return OCN_OK;
+    const Range all = range ? *range : range_interior(bx);
+    if (range_empty(all)) return OCN_OK;
     using KP = MarchStep<true, false, true, true, false, true>;
     // a batch puts up to P blocks' tiles in one launch (MarchBatch): their waves share its rounds
     constexpr int P = kPack<KP> < kBatchMax / 4 ? kPack<KP> : kBatchMax / 4;
-    const int cols = KP::kPairCols, rows = pair_rows(r, cols, batching(s) ? std::max(1, std::min(nblk, P)) : 1);
+    const int cols = KP::kPairCols, mult = batching(s) ? std::max(1, std::min(nblk, P)) : 1;
+    // the rects: the range, or (frame_of) its bands outside *frame_of -- one launch, up to 4 rects
+    Range rs[4];
+    int nr = 0;
+    if (!frame_of) {
+        rs[nr++] = all;
+    } else {
+        const Range &in = *frame_of;
+        const Range cand[4] = {{all.m0, all.m1, all.n0, in.n0 - 1}, {all.m0, all.m1, in.n1 + 1, all.n1},
+                               {all.m0, in.m0 - 1, in.n0, in.n1}, {in.m1 + 1, all.m1, in.n0, in.n1}};
+        for (const Range &q : cand)
+            if (!range_empty(q)) rs[nr++] = q;
+    }
     MarchGrid g{};
-    const int ntx = (r.m1 - r.m0 + cols) / cols;
-    g.r[0] = MarchRect{r.m0, r.m1, r.n0, r.n1, r.m0, ntx, ntx * ((r.n1 - r.n0 + rows) / rows), max(r.m0 - 4, bx->bnd_x1),
-                       min(r.m1 + 4, bx->bnd_x2), rows, 0};
-    g.nr = 1;
-    g.ntiles = g.r[0].tiles;
+    for (int i = 0; i < nr; ++i) {
+        const Range &r = rs[i];
+        const int rows = pair_rows(r, cols, mult), ntx = (r.m1 - r.m0 + cols) / cols;
+        g.r[g.nr++] = MarchRect{r.m0, r.m1, r.n0, r.n1, r.m0, ntx, ntx * ((r.n1 - r.n0 + rows) / rows),
+                                max(r.m0 - 4, bx->bnd_x1), min(r.m1 + 4, bx->bnd_x2), rows, 0};
+        g.ntiles += g.r[g.nr - 1].tiles;
+    }
     int ex;
     if (std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020)   // tau = 2^k
         return issue_march(g, MarchStep<true, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out,

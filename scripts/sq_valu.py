@@ -47,8 +47,11 @@ def summary(sq, kernel):
             d["launch_ms"] = dur[i] * 1e3
     # the launches that ran: with the device-side variant choice the first call also launches the
     # variants whose workgroups see another verdict and return at once
-    top = max(d.get("SQ_INSTS_VALU", 0.0) for d in disp.values())
-    ran = [d for d in disp.values() if d.get("SQ_INSTS_VALU", 0.0) > 0.5 * top]
+    # (a pass without SQ_INSTS_VALU: another counter of the launches' work)
+    work = next((k for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU")
+                 if any(k in d for d in disp.values())), "SQ_WAVES")
+    top = max(d.get(work, 0.0) for d in disp.values())
+    ran = [d for d in disp.values() if d.get(work, 0.0) > 0.5 * top]
     n = len(ran)
     per = {k: sum(d.get(k, 0.0) for d in ran) / n for k in ran[0]}
     clk = {k: per.pop(k) for k in ("clock_ghz", "launch_ms") if k in per}

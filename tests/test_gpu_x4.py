@@ -24,9 +24,9 @@ def amd():
     return amd
 
 
-def _run_blocks(amd, name, calls, x4=True):
+def _run_blocks(amd, name, calls, x4=True, overlap=None):
     case = cases.load_e2e(name)
-    m = build_model(amd, case).set_x4(x4).init()
+    m = build_model(amd, case, overlap=overlap).set_x4(x4).init()
     used = []
     try:
         m.step(calls[0], tau=1.0, check_every=1)
@@ -49,6 +49,16 @@ def test_x4_blocks_match_reference(amd, name, calls):
     """Several blocks in one process (local halo copies): pairs of x2 steps inside calls and across
     calls (the reference's 1-step cadence: a pair every second call), every field bitwise."""
     bad, used = _run_blocks(amd, name, calls)
+    assert not bad, f"{name} {calls}: fields differ from the reference: {bad}"
+    assert any(used), used
+
+
+@pytest.mark.parametrize("name,calls", [("box70x54_b3x2_s20", [2, 18]), ("bs_b4x2_s60", [2, 5, 1, 52]),
+                                        ("box4096_b4x2_s4", [1, 3])])
+def test_x4_overlapped_blocks_match_reference(amd, name, calls):
+    """OCN_OPT_OVERLAP 2 (the default with remote peers): each block's inner pair on the compute stream
+    beside the 4-deep exchange, then the bands around it on the comm stream -- bitwise."""
+    bad, used = _run_blocks(amd, name, calls, overlap=2)
     assert not bad, f"{name} {calls}: fields differ from the reference: {bad}"
     assert any(used), used
 
