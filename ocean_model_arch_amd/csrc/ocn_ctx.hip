@@ -335,6 +335,7 @@ struct ocn_ctx {
     // buffers agree with the fields outside the tracer step's write set.  Role bits 8 (ff1 / ff1n
     // traded) and 16 (ff1p / its second buffer traded), for every tracer at once.
     bool tr_step = true, tr_call = false, tr_pending = false;
+    bool tr_forked = false;   // a tracer step runs on the comm stream beside the march (joined by run_step)
     mutable bool tr_alt_ok = false;
     bool known_const = true;   // OCN_OPT_KNOWN_CONSTANTS: the one-pass step's known-constant variant
     bool last_hybrid = true;   // OCN_OPT_ONEPASS_LAST: one-pass last steps with exchanges / ring work too
@@ -1721,6 +1722,7 @@ static bool flip_eligible(ocn_ctx *c)
 // tracer steps (run_tracer_step, below): the pending one of the current state, and the tracer fields
 // the exchanges of a one-pass call carry with the state
 static int run_tracer_step(ocn_ctx *c, double tau);
+static int run_tracer_step(ocn_ctx *c, double tau, hipStream_t st);
 static std::vector<int> with_tracers(const ocn_ctx *c, const std::vector<int> &fields);
 
 // block b's one-pass variant for the current call (ctx kc_mode, the device verdict, its constants)
@@ -2101,6 +2103,17 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
     } else {
         if (k.x2_save) RC(ring2_run(c, true, s));
         RC(run_sync(c, with_tracers(c, kStateX2), s, nullptr, 2));   // the state two points deep
+        if (c->tr_pending && !c->capturing && c->comm_stream) {
+            // the previous state's tracer step beside this step's march (on the comm stream: both read
+            // the state just exchanged, the march writes the other buffers, the tracer step only the
+            // tracers'); joined by the next step (run_step) or the call's end (finish_call)
+            HIPCHK(hipEventRecord(c->ev_fork, s));
+            HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
+            RC(run_tracer_step(c, tau, c->comm_stream));
+            HIPCHK(hipEventRecord(c->ev_join, c->comm_stream));
+            c->sync_pending = true;
+            c->tr_forked = true;
+        }
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
         RC(each_block(c, s, [&](const LBlock &b) { return march(b, s, nullptr, nullptr); }));
         RC(timer_end(c, rec));
@@ -2508,24 +2521,34 @@ static int expl_tracer(ocn_ctx *c, double tau, bool compact)
 // and before anything writes the state it reads.  Its ffn goes to the ff1n buffer and the roles of
 // ff1 / ff1n trade (tracer_next_step's ff := ffn); the filtered ff1p to the second buffer.  The call's
 // last step (standard hh_init with every level) runs the standard stages after it.
-static int run_tracer_step(ocn_ctx *c, double tau)
+// st: the stream it runs on (one_step_x2 forks it onto the comm stream beside the next step's march:
+// the march reads the state the tracer step reads and writes the other buffers; the next step's
+// exchange and march wait for it -- run_step joins first)
+static int run_tracer_step(ocn_ctx *c, double tau, hipStream_t st)
 {
     if (!c->tr_pending) return OCN_OK;
     c->tr_pending = false;
-    ocn_ctx::Rec rec;
-    RC(timer_begin(c, OCN_TIMER_TRACER_STEP, rec));
+    ocn_ctx::Rec rec{OCN_TIMER_TRACER_STEP, nullptr, nullptr};
+    if (c->stage_timing) {
+        RC(get_event(c, rec.a)); RC(get_event(c, rec.b));
+        HIPCHK(hipEventRecord(rec.a, st));
+    }
     for (int k = 1; k <= c->sw.tracer_num; ++k)
-        RC(each_block(c, c->stream, [&](const LBlock &b) -> int {
+        RC(each_block(c, st, [&](const LBlock &b) -> int {
             const Compact t{b.bits, b.rows, c->march};
             return launch_tracer_step(&b.g, b.ptr.data(), (int)b.ptr.size(), c->compact ? &t : nullptr, k, tau,
                                       c->sw.time_smooth, (double *)b.ptr[field_slot(OCN_FF1N(k))],
-                                      (double *)b.ffp_alt[(size_t)k - 1], b.own, c->stream);
+                                      (double *)b.ffp_alt[(size_t)k - 1], b.own, st);
         }));
-    RC(timer_end(c, rec));
+    if (rec.b) {
+        HIPCHK(hipEventRecord(rec.b, st));
+        c->recs.push_back(rec);
+    }
     swap_tracer_roles(c);
     swap_tracer_alt(c);
     return OCN_OK;
 }
+static int run_tracer_step(ocn_ctx *c, double tau) { return run_tracer_step(c, tau, c->stream); }
 
 static std::vector<int> with_tracers(const ocn_ctx *c, const std::vector<int> &fields)
 {
@@ -3106,6 +3129,10 @@ static void drop_graphs(ocn_ctx *c)
 // one model step (model.f90:146-160): expl_shallow_water, then expl_tracer
 static int run_step(ocn_ctx *c, double tau, const StepKind &k)
 {
+    if (c->tr_forked) {   // a tracer step forked beside the previous step's march (one_step_x2)
+        RC(join_sync(c));
+        c->tr_forked = false;
+    }
     // tracer steps (OCN_OPT_TRACER_STEP): a one-pass step's tracer step runs with the next step; the
     // pending one of the state a single-block one-pass step reads runs before its march (x2 steps
     // and the last step: after their exchanges, one_step_x2 / one_step_fused)
@@ -3636,6 +3663,7 @@ static int sync_impl(ocn_ctx *c)
 {
     HIPCHK(hipSetDevice(c->dec.device));
     RC(run_deferred(c));
+    RC(join_sync(c));
     int32_t *cnt = c->d_nbad;
     if (has_comm(c)) {   // every rank's synchronize takes part (the collective of the check)
         cnt = c->d_nbad + 56;
@@ -3677,6 +3705,7 @@ int ocn_ctx_stage_stats(ocn_ctx *c, double *ms, int64_t *counts, double *ms_max)
     if (!c || !ms || !counts) return set_error(OCN_ERR_ARG, "null argument");
     HIPCHK(hipSetDevice(c->dec.device));
     RC(run_deferred(c));   // (their launches belong to this report, not the next one)
+    RC(join_sync(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     learn_fb(c);
     for (auto &r : c->recs) {

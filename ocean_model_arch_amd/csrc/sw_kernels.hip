@@ -3180,12 +3180,104 @@ int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact 
 
 // expl_tracer of tracer k as one launch in a one-pass sequence (sw_stencils.h TracerStep): the full
 // free surface factor is 1 (the one-pass steps require it), factor_mu 1.0d0 (tracer_interface.f90:47)
+// The tracer step one point per thread in 64 x 4 tiles, each face flux formed once: a thread forms
+// the fluxes of its point's east and north faces (TracerStep::fx_at / fy_at at (m, n)) and takes the
+// west / south ones from the neighbour threads through LDS (the tile's west column and south row
+// form theirs themselves) -- the same expressions on the same operands, so the same values as four
+// per point.  The tracer steps of small blocks (the Black Sea as 4 x 2 blocks, 71 x 79 each) are
+// latency-bound launches of few waves: a quarter of the serial work per thread, twice the threads.
+constexpr int kTrRows = 4;
+template <class Body> __device__ __forceinline__ void tracer_tile(const RangeB &R, int tile, const Body &body)
+{
+    __shared__ double sfx[kTrRows][64], sfy[kTrRows][64];
+    const int tx = (int)threadIdx.x, ty = (int)threadIdx.y;
+    const int m = R.w0 + (tile % R.ntx) * 64 + tx, n = R.n0 + (tile / R.ntx) * kTrRows + ty;
+    const bool in = m >= R.m0 && m <= R.m1 && n >= R.n0 && n <= R.n1;
+    const auto k = body.make();
+    double fxe = 0.0, fyn = 0.0;
+    if (in) { fxe = k.fx_at(m, n); fyn = k.fy_at(m, n); }
+    sfx[ty][tx] = fxe;
+    sfy[ty][tx] = fyn;
+    __syncthreads();
+    if (!in || !(ld(k.W.lu, k.I(m, n)) > 0.5f)) return;
+    const double fxw = tx > 0 ? sfx[ty][tx - 1] : k.fx_at(m - 1, n);
+    const double fys = ty > 0 ? sfy[ty - 1][tx] : k.fy_at(m, n - 1);
+    k.finish(m, n, fxe, fxw, fyn, fys);
+}
+template <class Body> __global__ __launch_bounds__(256) void k_tracer_tiles(RangeB R, Body body)
+{
+    int tile = (int)blockIdx.x;
+#if OCN_XCD_REMAP
+    const int per = (R.tiles + 7) / 8;
+    tile = (tile % 8) * per + tile / 8;
+    if (tile >= R.tiles) return;
+#endif
+    tracer_tile(R, tile, body);
+}
+template <class Body> __global__ __launch_bounds__(256) void k_tracer_tiles_b(RangeGridB g, Pack<Body> bodies)
+{
+    int tile = (int)blockIdx.x;
+#if OCN_XCD_REMAP
+    const int per = (g.ntiles + 7) / 8;
+    tile = (tile % 8) * per + tile / 8;
+    if (tile >= g.ntiles) return;
+#endif
+    int k = 0;   // workgroup-uniform
+    while (k + 1 < g.nr && tile >= g.r[k].tiles) { tile -= g.r[k].tiles; ++k; }
+    tracer_tile(g.r[k], tile, bodies.b[__builtin_amdgcn_readfirstlane(g.r[k].blk)]);
+}
+template <typename Body> struct TracerBatch : BatchEntry {
+    std::vector<Body> bodies;
+    std::vector<RangeB> ranges;
+    int flush(hipStream_t s) override
+    {
+        for (size_t i = 0; i < bodies.size(); i += kPack<Body>) {
+            const size_t n = std::min(bodies.size() - i, (size_t)kPack<Body>);
+            RangeGridB g{};
+            const PackBuf<Body> pk(&bodies[i], n);
+            for (size_t j = 0; j < n; ++j) {
+                g.r[g.nr] = ranges[i + j];
+                g.r[g.nr].blk = (int)j;
+                g.ntiles += ranges[i + j].tiles;
+                ++g.nr;
+            }
+            const int nblocks = OCN_XCD_REMAP ? 8 * ((g.ntiles + 7) / 8) : g.ntiles;
+            hipLaunchKernelGGL(k_tracer_tiles_b<Body>, dim3((unsigned)nblocks), dim3(64, kTrRows), 0, s, g, pk.get());
+            RC_KB(check_launch());
+        }
+        return OCN_OK;
+    }
+};
+template <class Body> static int launch_tracer_tiles(const Range &r, const Body &body, hipStream_t s)
+{
+    if (range_empty(r)) return OCN_OK;
+    const int ntx = (r.m1 - r.m0 + 64) / 64, nty = (r.n1 - r.n0 + kTrRows) / kTrRows;
+    const RangeB R{r.m0, r.m0, r.m1, r.n0, r.n1, ntx, ntx * nty, 0};
+    if (batching(s)) {
+        int rc = OCN_OK;
+        auto *e = batch_entry<TracerBatch<Body>>((const void *)&k_tracer_tiles<Body>, rc);
+        RangeB q = R;
+        q.blk = (int)e->bodies.size();
+        e->ranges.push_back(q);
+        e->bodies.push_back(body);
+        return rc;
+    }
+    const int nblocks = OCN_XCD_REMAP ? 8 * ((R.tiles + 7) / 8) : R.tiles;
+    hipLaunchKernelGGL(k_tracer_tiles<Body>, dim3((unsigned)nblocks), dim3(64, kTrRows), 0, s, R, body);
+    return check_launch();
+}
+
 int launch_tracer_step(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int k, double tau,
                        double ts, double *ffn_out, double *ffp_out, unsigned own, hipStream_t s)
 {
     if (!ffn_out || !ffp_out) return set_error(OCN_ERR_ARG, "tracer step: output buffers");
+    RC_K(check_block(b));
     const Range ri = range_interior(b);
-    return launch_fused<KTracerStep>(ri, ri, OCN_PART_ALL, b, ptr, nptr, cp, k, s, tau, ts, own, ffn_out, ffp_out);
+    if (cp)
+        return launch_tracer_tiles(ri, KTracerStep<true>{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), k),
+                                                         tau, ts, own, ffn_out, ffp_out}, s);
+    return launch_tracer_tiles(ri, KTracerStep<false>{*b, make_tab<false>(ptr, nptr, nullptr, nullptr, 0, k), tau, ts,
+                                                      own, ffn_out, ffp_out}, s);
 }
 
 // One reference stage over the compact tables (ocn_ctx.hip envoke, OCN_OPT_COMPACT): the stage

@@ -745,11 +745,18 @@ template <bool C> struct TracerStep {
     {
         const Pt c = I(m, n);
         if (!(ld(W.lu, c) > 0.5f)) return;
+        finish(m, n, fx_at(m, n), fx_at(m - 1, n), fy_at(m, n), fy_at(m, n - 1));
+    }
+    // the point's update from the four face fluxes (fx at m and m - 1, fy at n and n - 1), each
+    // formed by fx_at / fy_at -- here, or by the thread of the neighbour point (k_tracer_tiles)
+    OCN_HD void finish(int m, int n, double fxe, double fxw, double fyn, double fys) const
+    {
+        const Pt c = I(m, n);
         // tran_diff_tracer (leapfrog_tracer.f90:94-136): hhq_n = h_r, hhq_p = h_r + sshp * ffs
         const double hqn = ld(h_r, c), hqp = ld(h_r, c) + ld(sshp, c) * f;
         const double bp = hqn * D(ld(W.dx, c)) * D(ld(W.dy, c)) / tau / 2.0;
         const double bp0 = hqp * D(ld(W.dx, c)) * D(ld(W.dy, c)) / tau / 2.0;
-        const double rhs = fx_at(m, n) - fx_at(m - 1, n) + fy_at(m, n) - fy_at(m, n - 1);
+        const double rhs = fxe - fxw + fyn - fys;
         const double xn = (bp0 * ld(ffp, c) + rhs) / bp;
         // tracer_next_step (leapfrog_tracer.f90:138-168)
         const double x = ld(ff, c), xp = ld(ffp, c);
@@ -1252,15 +1259,15 @@ template <bool C> struct KTracerNextStep {
 // TracerStep of the table's tracer (one-pass sequences), its outputs into ffn_out / ffp_out
 template <bool C> struct KTracerStep {
     ocn_block b; Tab<C> t; double tau, ts; unsigned own; double *ffn_out, *ffp_out;
-    OCN_HD void operator()(int m, int n) const
+    OCN_HD TracerStep<C> make() const
     {
-        const TracerStep<C> k{geo(&b), tau, ts, 1.0, 1.0, b.nx_start, b.nx_end, b.ny_start, b.ny_end, own,
-                              make_interp(t), t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LCU), t.m(OCN_LCV),
-                              t.f(OCN_SSH), t.f(OCN_SSHP), t.f(OCN_HHQ_REST), t.f(OCN_UBRTR), t.f(OCN_VBRTR),
-                              t.f(OCN_MU), t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_FLUX_X), t.f(OCN_FLUX_Y),
-                              t.f(OCN_FF1(1)), t.f(OCN_FF1P(1)), ffn_out, ffp_out};
-        k(m, n);
+        return TracerStep<C>{geo(&b), tau, ts, 1.0, 1.0, b.nx_start, b.nx_end, b.ny_start, b.ny_end, own,
+                             make_interp(t), t.m(OCN_LLU), t.m(OCN_LLV), t.m(OCN_LCU), t.m(OCN_LCV),
+                             t.f(OCN_SSH), t.f(OCN_SSHP), t.f(OCN_HHQ_REST), t.f(OCN_UBRTR), t.f(OCN_VBRTR),
+                             t.f(OCN_MU), t.f(OCN_HHU), t.f(OCN_HHV), t.f(OCN_FLUX_X), t.f(OCN_FLUX_Y),
+                             t.f(OCN_FF1(1)), t.f(OCN_FF1P(1)), ffn_out, ffp_out};
     }
+    OCN_HD void operator()(int m, int n) const { make()(m, n); }
 };
 
 }  // namespace ocn
