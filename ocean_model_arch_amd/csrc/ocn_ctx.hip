@@ -879,7 +879,7 @@ static int comm_gone(const ocn_ctx *c)
 // OCN_OPT_OVERLAP in effect: by default (-1) the role-flip steps' exchanges overlap their inner
 // launches (2) when exchanges go to other ranks (RCCL: latency, not copy bandwidth), and run
 // between the launches (1) when every exchange is a local device copy -- there the frame bands
-// cost as much as the copies they hide
+// cost as much as the copies they hide (HISTORY.md section 5)
 static int overlap_level(const ocn_ctx *c)
 {
     return c->overlap >= 0 ? c->overlap : has_comm(c) && c->dec.nranks > 1 ? 2 : 1;

@@ -72,10 +72,12 @@ __global__ __launch_bounds__(256, OCN_LB_WAVES) void k_range(int w0, int m0, int
 
 // ------------------------------------------------------------------ block batching (ocn_internal.h Batcher)
 // The bodies of a batched launch travel by value in its kernel arguments (as a single body does),
-// kPack<Body> of them per launch within a 3.5 KB argument budget: no copies to device memory, and
-// the launches stay capturable into graphs.
-constexpr int kBatchMax = 16;   // ranges / rects per batched launch
-constexpr int kArgBudget = 3584 - kBatchMax * 48 - 64;
+// kPack<Body> (up to 8) of them per launch within a 12 KB argument block: no copies to device
+// memory, and the launches stay capturable into graphs.  (Plain launches with 16 KB argument blocks
+// run correctly on gfx950 under this ROCm: scripts/kernarg_probe.hip; 8 blocks of a device -- the
+// 4 x 2 layouts -- then take one launch instead of two.)
+constexpr int kBatchMax = 32;   // ranges / rects per batched launch
+constexpr int kArgBudget = 12288 - kBatchMax * 48 - 64;
 template <class Body> constexpr int kPack = (int)(kArgBudget / sizeof(Body)) < 1 ? 1
                                             : (int)(kArgBudget / sizeof(Body)) > 8 ? 8 : (int)(kArgBudget / sizeof(Body));
 template <class Body> struct Pack { Body b[kPack<Body>]; };
