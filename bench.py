@@ -273,17 +273,20 @@ def cpu_baseline(n_full: int = 4096):
 
 def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for, watchdog=0.0):
     """Run-time check of the N > 1 path: a 512^2 box on the N-GPU block grid (RCCL halos) for
-    5 steps; rank 0 recomputes the same block grid inside one process on its GPU (device-local
-    halo copies, the path tests/test_gpu_parity.py pins to the reference) and compares every
-    rank's block bit for bit.  Returns True/False on rank 0, None elsewhere."""
+    2 + 6 steps -- a first call, a synchronize (the known-constant verdict reaches every host, so
+    the second call's vote lets every rank run the x4 pairs: 4-deep exchanges over RCCL); rank 0
+    recomputes the same block grid inside one process on its GPU (device-local halo copies, the path
+    tests/test_gpu_x4.py pins to the reference) and compares every rank's block bit for bit.
+    Returns True/False on rank 0, None elsewhere."""
     import numpy as np
-    n, steps = 512, 5
+    n, calls = 512, (2, 6)
     m = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(bx, by), rank=rank, nranks=world,
                        device=local_rank)
     m.attach_comm(uid_for())
     if watchdog > 0:
         m.set_watchdog(watchdog)
-    m.init().step(steps).synchronize()
+    m.init().step(calls[0]).synchronize()
+    m.step(calls[1]).synchronize()
     mine = {(b.bm, b.bn): {f: m.download(b.k, f) for f in ("ssh", "ubrtr", "vbrtr", "hhu", "str_s")}
             for b in m.blocks}
     m.close()
@@ -292,7 +295,8 @@ def multi_gpu_parity(amd, dist, rank, world, local_rank, bx, by, uid_for, watchd
     if rank != 0:
         return None
     ref = amd.OceanModel(amd.box_config(n), amd.SWConfig(), amd.ParallelConfig(bx, by), device=local_rank)
-    ref.init().step(steps).synchronize()
+    ref.init().step(calls[0]).synchronize()
+    ref.step(calls[1]).synchronize()
     ok = True
     for b in ref.blocks:
         for part in gathered:
@@ -570,6 +574,7 @@ def main():
     # pair launches ran in the timed region: their timer counted them (graph replays: no timers)
     pair = ("onepass2" in times or "onepass2_last" in times) if times else model.pair_active
     multi = ("onepass_multi" in times) if times else model.multi_active
+    x4 = model.x4_active
     model_overlap = model.overlap_level
     rank_info = None
     if world > 1:
@@ -644,6 +649,8 @@ def main():
                           "multi_step_launch": ("a call's steps in one launch, a grid barrier between "
                                                 "steps (OCN_OPT_MULTI)") if multi else False,
                           "tracer_steps": model.tracer_step_active if sw.use_tracers > 0 else None,
+                          "x4_pairs": ("two x2 steps per launch, one 4-deep state exchange per two steps (OCN_OPT_X4)"
+                                       if x4 else False) if bx * by > 1 else None,
                           "steps_per_call": spc, "calls": len(calls),
                           "call_tail": ("pending between calls (OCN_OPT_LAZY_TAIL), formed once by ocn_ctx_complete "
                                         "inside the timed region") if lazy else "formed by every call",
