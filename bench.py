@@ -574,7 +574,8 @@ def main():
     # pair launches ran in the timed region: their timer counted them (graph replays: no timers)
     pair = ("onepass2" in times or "onepass2_last" in times) if times else model.pair_active
     multi = ("onepass_multi" in times) if times else model.multi_active
-    x4 = model.x4_active
+    # (x4 pairs: the pair launches of blocks with exchanges; 1-step calls run one every second call)
+    x4 = (("onepass2" in times) if times else model.x4_active) and bx * by > 1
     model_overlap = model.overlap_level
     rank_info = None
     if world > 1:
