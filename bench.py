@@ -457,6 +457,9 @@ def main():
                     help="tracer runs: the role-flip path with the standard tracer stages (no tracer steps, OCN_OPT_TRACER_STEP)")
     ap.add_argument("--no-x4", action="store_true",
                     help="blocks with halo exchanges: x2 single launches (no pairs with one 4-deep exchange, OCN_OPT_X4)")
+    ap.add_argument("--no-co-launch", action="store_true",
+                    help="tracer runs with x2 steps: the march and the tracer step as two launches on two streams "
+                         "(no co-launch, OCN_OPT_CO_LAUNCH)")
     ap.add_argument("--no-batch", action="store_true",
                     help="several blocks on a GPU: one launch per block and launch group (no block batching)")
     ap.add_argument("--watchdog", type=float, default=120.0,
@@ -536,6 +539,7 @@ def main():
     model.set_multi(not args.no_multi)
     model.set_tracer_step(not args.no_tracer_step)
     model.set_x4(not args.no_x4)
+    model.set_co_launch(not args.no_co_launch)
     if args.graph:
         model.set_graph(True)
     model.init()
@@ -576,6 +580,7 @@ def main():
     multi = ("onepass_multi" in times) if times else model.multi_active
     # (x4 pairs: the pair launches of blocks with exchanges; 1-step calls run one every second call)
     x4 = (("onepass2" in times) if times else model.x4_active) and bx * by > 1
+    co = model.co_launched
     model_overlap = model.overlap_level
     rank_info = None
     if world > 1:
@@ -652,6 +657,8 @@ def main():
                           "tracer_steps": model.tracer_step_active if sw.use_tracers > 0 else None,
                           "x4_pairs": ("two x2 steps per launch, one 4-deep state exchange per two steps (OCN_OPT_X4)"
                                        if x4 else False) if bx * by > 1 else None,
+                          "co_launch": ("each x2 step's march and the previous state's tracer step as one launch "
+                                        "(OCN_OPT_CO_LAUNCH)" if co else False) if sw.use_tracers > 0 and bx * by > 1 else None,
                           "steps_per_call": spc, "calls": len(calls),
                           "call_tail": ("pending between calls (OCN_OPT_LAZY_TAIL), formed once by ocn_ctx_complete "
                                         "inside the timed region") if lazy else "formed by every call",

@@ -414,6 +414,10 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  neighbours; the known-constant variant, no tracers, every block at least 4 x 4; two more halo rings
  *  outside the reference's arrays hold the exchanged state.  Same results bit for bit.
  *  ocn_ctx_get_option: 2 if the last ocn_ctx_step used such launches.
+ *  OCN_OPT_CO_LAUNCH (default 1): tracer runs with x2 steps (one tracer, several blocks on the
+ *  device, block batching): each step's march and the previous state's tracer step go as ONE launch
+ *  (their workgroups in one grid) instead of two beside each other on two streams.  Same results bit
+ *  for bit.  ocn_ctx_get_option: 2 if the last ocn_ctx_step co-launched.
  *  OCN_OPT_MULTI_SPIN (diagnostics; default 1 << 20, about 0.5 s): the multi-step launch's grid
  *  barrier gives up after this many polls -- the launch's workgroups end and ocn_ctx_synchronize
  *  returns OCN_ERR_HIP instead of the device hanging if the grid was not co-resident.  Tests set it
@@ -430,7 +434,7 @@ enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9,
        OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13,
        OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16, OCN_OPT_TRACER_STEP = 17,
-       OCN_OPT_MULTI_SPIN = 18, OCN_OPT_X4 = 19 };
+       OCN_OPT_MULTI_SPIN = 18, OCN_OPT_X4 = 19, OCN_OPT_CO_LAUNCH = 20 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,

@@ -87,6 +87,7 @@ OPT_MULTI = 16
 OPT_TRACER_STEP = 17
 OPT_MULTI_SPIN = 18
 OPT_X4 = 19
+OPT_CO_LAUNCH = 20
 
 # exported symbols (every one declared in include/ocn_sw.h)
 KERNEL_SYMBOLS = ["ocn_sw_update_ssh", "ocn_hh_update", "ocn_uv_trans_vort", "ocn_uv_trans",

@@ -399,6 +399,9 @@ struct ocn_ctx {
     bool fb_x2 = false;          // the known-constant check's verdict is for the x2 range / tables
     mutable bool coherent_known = false, r8_escaped = false;
     int multi_spin = kMultiSpin;   // OCN_OPT_MULTI_SPIN (the multi-step launch's barrier bound)
+    // OCN_OPT_CO_LAUNCH: an x2 step's march and the previous state's tracer step as one launch;
+    // co_used: the last call did
+    bool co_launch = true, co_used = false;
     double stage_max[OCN_NUM_TIMERS] = {0};   // longest record per timer (ocn_ctx_stage_stats)
     // halo exchanges with remote peers (run_sync): how many were enqueued; while a watchdog is set an
     // event after each (xq, under xmu) tells it the id of the last one the device completed (xdone)
@@ -1246,10 +1249,15 @@ static const std::vector<int> kHaloCheck = {OCN_SSH, OCN_UBRTR, OCN_VBRTR, OCN_H
 // on stream s are batched (ocn_internal.h Batcher): each kernel of the loop is launched once for all
 // the blocks (up to kPack of them per launch) instead of once per block.  Only for loops whose
 // launches read and write their own block's arrays, with nothing but batchable launches on s.
-template <class F> static int each_block(ocn_ctx *c, hipStream_t s, F &&f)
+// co: the loop's launches read nothing another writes -- a march batch and the tracer-step batch
+// after it may go as one launch (Batcher::co_launch)
+template <class F> static int each_block(ocn_ctx *c, hipStream_t s, F &&f, bool co = false)
 {
     const bool on = c->batch && c->blocks.size() > 1;
-    if (on) batch_begin(&c->batcher, s);
+    if (on) {
+        batch_begin(&c->batcher, s);
+        c->batcher.co_launch = co;
+    }
     int rc = OCN_OK;
     for (size_t i = 0; i < c->blocks.size() && rc == OCN_OK; ++i) {
         if (on) batch_next(&c->batcher);
@@ -1258,6 +1266,7 @@ template <class F> static int each_block(ocn_ctx *c, hipStream_t s, F &&f)
     if (on) {
         const int r2 = batch_end(&c->batcher);
         if (rc == OCN_OK) rc = r2;
+        if (co && c->batcher.co_launched) c->co_used = true;
     }
     return rc;
 }
@@ -1723,6 +1732,7 @@ static bool flip_eligible(ocn_ctx *c)
 // the exchanges of a one-pass call carry with the state
 static int run_tracer_step(ocn_ctx *c, double tau);
 static int run_tracer_step(ocn_ctx *c, double tau, hipStream_t st);
+static int tracer_step_block(ocn_ctx *c, const LBlock &b, int k, double tau, hipStream_t st);
 static std::vector<int> with_tracers(const ocn_ctx *c, const std::vector<int> &fields);
 
 // block b's one-pass variant for the current call (ctx kc_mode, the device verdict, its constants)
@@ -2103,7 +2113,11 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
     } else {
         if (k.x2_save) RC(ring2_run(c, true, s));
         RC(run_sync(c, with_tracers(c, kStateX2), s, nullptr, 2));   // the state two points deep
-        if (c->tr_pending && !c->capturing && c->comm_stream) {
+        // OCN_OPT_CO_LAUNCH: the previous state's tracer step in the march's launch (one tracer, block
+        // batching: sw_kernels.hip k_march_tracer_b) -- both read the state just exchanged, the march
+        // writes the other buffers, the tracer step only the tracers'
+        const bool co = c->tr_pending && c->co_launch && c->sw.tracer_num == 1 && c->batch && c->blocks.size() > 1;
+        if (c->tr_pending && !co && !c->capturing && c->comm_stream) {
             // the previous state's tracer step beside this step's march (on the comm stream: both read
             // the state just exchanged, the march writes the other buffers, the tracer step only the
             // tracers'); joined by the next step (run_step) or the call's end (finish_call)
@@ -2115,7 +2129,17 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
             c->tr_forked = true;
         }
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
-        RC(each_block(c, s, [&](const LBlock &b) { return march(b, s, nullptr, nullptr); }));
+        if (co) {   // (a variant that cannot co-launch flushes the two batches in order: the same results)
+            RC(each_block(c, s, [&](const LBlock &b) -> int {
+                RC(march(b, s, nullptr, nullptr));
+                return tracer_step_block(c, b, 1, tau, s);
+            }, true));
+            c->tr_pending = false;
+            swap_tracer_roles(c);
+            swap_tracer_alt(c);
+        } else {
+            RC(each_block(c, s, [&](const LBlock &b) { return march(b, s, nullptr, nullptr); }));
+        }
         RC(timer_end(c, rec));
     }
     // the previous state's tracer step: it reads that state (untouched by the march) and the tracers
@@ -2524,6 +2548,13 @@ static int expl_tracer(ocn_ctx *c, double tau, bool compact)
 // st: the stream it runs on (one_step_x2 forks it onto the comm stream beside the next step's march:
 // the march reads the state the tracer step reads and writes the other buffers; the next step's
 // exchange and march wait for it -- run_step joins first)
+// tracer k's tracer step on block b
+static int tracer_step_block(ocn_ctx *c, const LBlock &b, int k, double tau, hipStream_t st)
+{
+    const Compact t{b.bits, b.rows, c->march};
+    return launch_tracer_step(&b.g, b.ptr.data(), (int)b.ptr.size(), c->compact ? &t : nullptr, k, tau, c->sw.time_smooth,
+                              (double *)b.ptr[field_slot(OCN_FF1N(k))], (double *)b.ffp_alt[(size_t)k - 1], b.own, st);
+}
 static int run_tracer_step(ocn_ctx *c, double tau, hipStream_t st)
 {
     if (!c->tr_pending) return OCN_OK;
@@ -2534,12 +2565,7 @@ static int run_tracer_step(ocn_ctx *c, double tau, hipStream_t st)
         HIPCHK(hipEventRecord(rec.a, st));
     }
     for (int k = 1; k <= c->sw.tracer_num; ++k)
-        RC(each_block(c, st, [&](const LBlock &b) -> int {
-            const Compact t{b.bits, b.rows, c->march};
-            return launch_tracer_step(&b.g, b.ptr.data(), (int)b.ptr.size(), c->compact ? &t : nullptr, k, tau,
-                                      c->sw.time_smooth, (double *)b.ptr[field_slot(OCN_FF1N(k))],
-                                      (double *)b.ffp_alt[(size_t)k - 1], b.own, st);
-        }));
+        RC(each_block(c, st, [&](const LBlock &b) { return tracer_step_block(c, b, k, tau, st); }));
     if (rec.b) {
         HIPCHK(hipEventRecord(rec.b, st));
         c->recs.push_back(rec);
@@ -3410,6 +3436,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     // (RCCL / events stay outside graphs; so do the tracer steps' calls: their launches follow pending state)
     const bool graph_ok = c->use_graph && !has_comm(c) && !c->stage_timing && !(c->sw.use_tracers > 0 && c->tr_step);
     c->pair_used = false;
+    c->co_used = false;
     c->multi_used = false;
     if (c->open) {
         if (tau == c->open_tau && c->onepass && lazy_allowed(c, c->open_x2)) {
@@ -3860,6 +3887,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         return OCN_OK;
     case OCN_OPT_MULTI_SPIN: c->multi_spin = value < 1 ? 1 : value > kMultiSpin ? kMultiSpin : (int)value; return OCN_OK;
     case OCN_OPT_X4: c->x4 = value != 0; c->coherent_known = false; return OCN_OK;
+    case OCN_OPT_CO_LAUNCH: c->co_launch = value != 0; return OCN_OK;
     case OCN_OPT_BATCH:
         if (c->batch != (value != 0)) drop_graphs(c);
         c->batch = value != 0;
@@ -3903,6 +3931,7 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_TRACER_STEP: *value = c->tr_call ? 2 : c->tr_step; return OCN_OK;
     case OCN_OPT_MULTI_SPIN: *value = c->multi_spin; return OCN_OK;
     case OCN_OPT_X4: *value = c->x4_used ? 2 : c->x4; return OCN_OK;
+    case OCN_OPT_CO_LAUNCH: *value = c->co_used ? 2 : c->co_launch; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

@@ -233,13 +233,21 @@ constexpr int kCompactDivisorRange = 8;   // sw_stencils.h OCN_COMPACT_DIVISOR_R
 // or one kind twice, flushes the batch first); launches of different blocks may be reordered, so
 // a batched loop must not let one block's launch read what another block's writes.  Any other
 // launch while a batch is open (another kernel, another stream) is an error (check_launch).
+// co_launch: the caller states that no launch of the batch reads what another writes (a one-pass
+// x2 step and the previous state's tracer step: both read the exchanged state, each writes its own
+// buffers), so an entry may issue itself and the next one as ONE launch (co_flush: the x2 march's
+// and the tracer step's workgroups in one grid) instead of two in order.
 struct BatchEntry {
     virtual ~BatchEntry() {}
     virtual int flush(hipStream_t s) = 0;
+    // issue this entry and `next` as one launch; false: not possible (each flushes on its own)
+    virtual bool co_flush(BatchEntry *next, hipStream_t s, int &rc) { (void)next; (void)s; (void)rc; return false; }
     const void *kind = nullptr;   // the kernel type (its host stub's address)
 };
 struct Batcher {
     bool active = false;
+    bool co_launch = false;              // see BatchEntry::co_flush (cleared by batch_begin)
+    int co_launched = 0;                 // launches that issued two entries (the last flush)
     hipStream_t s = nullptr;
     int cur = -1;                        // position of the current block's last entry
     std::vector<BatchEntry *> entries;   // in first-added order

@@ -477,10 +477,21 @@ __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march_b(MarchGridB g,
     march_tile(g.r[k], tile, body);
 }
 
+template <class Body> struct MarchBatch;
+template <class MB> static bool march_tracer_flush(MarchBatch<MB> &m, BatchEntry *next, hipStream_t s, int &rc);
+// a march body whose batch may be co-launched with the tracer step's (k_march_tracer_b)
+template <class B, class = void> struct CoTracer { static constexpr bool v = false; };
+template <class B> struct CoTracer<B, std::void_t<decltype(B::kCoTracer)>> { static constexpr bool v = B::kCoTracer; };
 template <class Body> struct MarchBatch : BatchEntry {
     std::vector<Body> bodies;
     std::vector<MarchRect> rects;
     std::vector<int> blk;
+    bool co_flush(BatchEntry *next, hipStream_t s, int &rc) override
+    {
+        if constexpr (CoTracer<Body>::v) return march_tracer_flush(*this, next, s, rc);
+        (void)next; (void)s; (void)rc;
+        return false;
+    }
     int flush(hipStream_t s) override
     {
         constexpr int P = kPack<Body> < kBatchMax / 4 ? kPack<Body> : kBatchMax / 4;   // (a body has <= 4 rects)
@@ -1905,6 +1916,8 @@ struct MarchStep {
     static constexpr int kStAux = WT ? 16 : 0;
     static constexpr bool kPair = PAIR;
     static constexpr bool kX2 = X2;
+    // the x2 single step of the known-constant variant: co-launched with a tracer step (k_march_tracer_b)
+    static constexpr bool kCoTracer = X2 && ZF && !HR && !LAST && !PAIR && !WT;
     static constexpr int kPairCols = 116;   // PAIR: a workgroup's output columns (2 x 60 produced, less 2 each side)
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
@@ -3189,10 +3202,10 @@ int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact 
 // per point.  The tracer steps of small blocks (the Black Sea as 4 x 2 blocks, 71 x 79 each) are
 // latency-bound launches of few waves: a quarter of the serial work per thread, twice the threads.
 constexpr int kTrRows = 4;
-template <class Body> __device__ __forceinline__ void tracer_tile(const RangeB &R, int tile, const Body &body)
+template <class Body>
+__device__ __forceinline__ void tracer_tile(const RangeB &R, int tile, const Body &body, int tx, int ty)
 {
     __shared__ double sfx[kTrRows][64], sfy[kTrRows][64];
-    const int tx = (int)threadIdx.x, ty = (int)threadIdx.y;
     const int m = R.w0 + (tile % R.ntx) * 64 + tx, n = R.n0 + (tile / R.ntx) * kTrRows + ty;
     const bool in = m >= R.m0 && m <= R.m1 && n >= R.n0 && n <= R.n1;
     const auto k = body.make();
@@ -3214,7 +3227,7 @@ template <class Body> __global__ __launch_bounds__(256) void k_tracer_tiles(Rang
     tile = (tile % 8) * per + tile / 8;
     if (tile >= R.tiles) return;
 #endif
-    tracer_tile(R, tile, body);
+    tracer_tile(R, tile, body, (int)threadIdx.x, (int)threadIdx.y);
 }
 template <class Body> __global__ __launch_bounds__(256) void k_tracer_tiles_b(RangeGridB g, Pack<Body> bodies)
 {
@@ -3226,7 +3239,7 @@ template <class Body> __global__ __launch_bounds__(256) void k_tracer_tiles_b(Ra
 #endif
     int k = 0;   // workgroup-uniform
     while (k + 1 < g.nr && tile >= g.r[k].tiles) { tile -= g.r[k].tiles; ++k; }
-    tracer_tile(g.r[k], tile, bodies.b[__builtin_amdgcn_readfirstlane(g.r[k].blk)]);
+    tracer_tile(g.r[k], tile, bodies.b[__builtin_amdgcn_readfirstlane(g.r[k].blk)], (int)threadIdx.x, (int)threadIdx.y);
 }
 template <typename Body> struct TracerBatch : BatchEntry {
     std::vector<Body> bodies;
@@ -3250,6 +3263,71 @@ template <typename Body> struct TracerBatch : BatchEntry {
         return OCN_OK;
     }
 };
+// BatchEntry::co_flush of a one-pass x2 march batch (MarchStep::kCoTracer) followed by the tracer-step
+// batch of the previous state (ocn_ctx.hip one_step_x2): ONE launch, workgroups [0, march tiles) march
+// the blocks, the rest are tracer tiles (a 256-thread workgroup as the 64 x kTrRows tile) -- in place
+// of the march launch and a tracer launch forked beside it on a second stream (two launches, an event
+// fork and join per step: the Black Sea + tracer as 4 x 2 blocks is latency-bound).  The two read the
+// same exchanged state and write disjoint buffers (Batcher::co_launch).
+template <class MB, class TB>
+__global__ __launch_bounds__(256, WavesOf<MB>::v) void k_march_tracer_b(MarchGridB gm, Pack<MB> mb, RangeGridB gt,
+                                                                         Pack<TB> tb)
+{
+    int tile = (int)blockIdx.x;
+#if OCN_XCD_REMAP
+    const int total = gm.ntiles + gt.ntiles;
+    const int per = (total + 7) / 8;
+    tile = (tile % 8) * per + tile / 8;
+    if (tile >= total) return;
+#endif
+    if (tile < gm.ntiles) {   // (workgroup-uniform)
+        int k = 0;
+        while (k + 1 < gm.nr && tile >= gm.r[k].tiles) { tile -= gm.r[k].tiles; ++k; }
+        const MB &body = mb.b[__builtin_amdgcn_readfirstlane(gm.blk[k])];
+        if constexpr (HasGate<MB>::v)
+            if (!body.enabled()) return;
+        march_tile(gm.r[k], tile, body);
+        return;
+    }
+    tile -= gm.ntiles;
+    int k = 0;
+    while (k + 1 < gt.nr && tile >= gt.r[k].tiles) { tile -= gt.r[k].tiles; ++k; }
+    tracer_tile(gt.r[k], tile, tb.b[__builtin_amdgcn_readfirstlane(gt.r[k].blk)], (int)threadIdx.x & 63,
+                (int)threadIdx.x >> 6);
+}
+// the argument block of a co-launch (two grids, two packs): within the 16 KB plain launches take on
+// gfx950 (scripts/kernarg_probe.hip), with a margin
+constexpr size_t kCoArgMax = 15360;
+template <class MB> static bool march_tracer_flush(MarchBatch<MB> &m, BatchEntry *next, hipStream_t s, int &rc)
+{
+    using TB = KTracerStep<true>;
+    constexpr int P = kPack<MB> < kBatchMax / 4 ? kPack<MB> : kBatchMax / 4;
+    constexpr size_t kArgs = sizeof(MarchGridB) + sizeof(Pack<MB>) + sizeof(RangeGridB) + sizeof(Pack<TB>);
+    if (kArgs > kCoArgMax || next->kind != (const void *)&k_tracer_tiles<TB>) return false;
+    auto *t = static_cast<TracerBatch<TB> *>(next);
+    if (m.bodies.empty() || m.bodies.size() > (size_t)P || m.rects.size() > (size_t)kBatchMax ||
+        t->bodies.size() > (size_t)kPack<TB> || t->ranges.size() > (size_t)kBatchMax)
+        return false;
+    MarchGridB gm{};
+    const PackBuf<MB> pm(m.bodies.data(), m.bodies.size());
+    for (size_t j = 0; j < m.rects.size(); ++j) {
+        gm.r[gm.nr] = m.rects[j]; gm.blk[gm.nr] = m.blk[j]; gm.ntiles += m.rects[j].tiles; ++gm.nr;
+    }
+    RangeGridB gt{};
+    const PackBuf<TB> pt(t->bodies.data(), t->bodies.size());
+    for (size_t j = 0; j < t->ranges.size(); ++j) {
+        gt.r[gt.nr] = t->ranges[j];
+        gt.r[gt.nr].blk = (int)j;
+        gt.ntiles += t->ranges[j].tiles;
+        ++gt.nr;
+    }
+    const int total = gm.ntiles + gt.ntiles;
+    const int nblocks = OCN_XCD_REMAP ? 8 * ((total + 7) / 8) : total;
+    hipLaunchKernelGGL((k_march_tracer_b<MB, TB>), dim3((unsigned)nblocks), dim3(256), 0, s, gm, pm.get(), gt, pt.get());
+    rc = check_launch();
+    return true;
+}
+
 template <class Body> static int launch_tracer_tiles(const Range &r, const Body &body, hipStream_t s)
 {
     if (range_empty(r)) return OCN_OK;
@@ -3371,9 +3449,18 @@ int Batcher::flush()
     const bool was = active;
     active = false;   // the flush's own launches are issued, not collected
     int rc = OCN_OK;
-    for (BatchEntry *e : entries) {
-        if (rc == OCN_OK) rc = e->flush(s);
-        delete e;
+    co_launched = 0;
+    for (size_t i = 0; i < entries.size(); ++i) {
+        if (rc == OCN_OK) {
+            if (co_launch && i + 1 < entries.size() && entries[i]->co_flush(entries[i + 1], s, rc)) {
+                ++co_launched;
+                delete entries[i];
+                ++i;   // (issued with entry i)
+            } else {
+                rc = entries[i]->flush(s);
+            }
+        }
+        delete entries[i];
     }
     entries.clear();
     cur = -1;
@@ -3388,6 +3475,7 @@ void batch_begin(Batcher *bt, hipStream_t s)
     bt->entries.clear();
     bt->s = s;
     bt->cur = -1;
+    bt->co_launch = false;
     bt->active = true;
     g_batcher = bt;
 }

@@ -270,6 +270,17 @@ class OceanModel:
         """Whether the last step() ran pairs of x2 steps (one_step_x4)."""
         return self.option(_lib.OPT_X4) == 2
 
+    def set_co_launch(self, on: bool = True):
+        """Tracer runs with x2 steps: each step's march and the previous state's tracer step as one
+        launch (default on, OCN_OPT_CO_LAUNCH); same results bit for bit."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_CO_LAUNCH, int(on)), "ocn_ctx_set_option")
+        return self
+
+    @property
+    def co_launched(self) -> bool:
+        """Whether the last step() co-launched a march and a tracer step."""
+        return self.option(_lib.OPT_CO_LAUNCH) == 2
+
     def set_multi_spin(self, polls: int):
         """Diagnostics: the multi-step launch's grid barrier gives up after `polls` polls (default
         1 << 20, about 0.5 s); the next synchronize() then raises OCN_ERR_HIP."""

@@ -134,6 +134,30 @@ def test_tracer_steps_match_reference(amd, name, calls):
         assert x2, name
 
 
+@pytest.mark.parametrize("co", [True, False])
+@pytest.mark.parametrize("name", ["box70x54_b3x2_tr_s20", "bs_b4x2_tr_s60"])
+def test_tracer_step_co_launch_matches_reference(amd, name, co):
+    """OCN_OPT_CO_LAUNCH (ocn_ctx.hip one_step_x2, sw_kernels.hip k_march_tracer_b): each x2 step's march
+    and the previous state's tracer step as one launch (on), or two on two streams (off) -- bitwise
+    against the reference either way; the co-launch runs once the known-constant verdict is on the
+    host (a first call and a synchronize)."""
+    case = cases.load_e2e(name)
+    steps = case["steps"]
+    m = build_model(amd, case).set_co_launch(co).init()
+    used = []
+    try:
+        m.step(2, tau=1.0, check_every=1).synchronize()
+        for n in (steps - 5, 1, 2):
+            m.step(n, tau=1.0, check_every=1)
+            used.append(m.co_launched)
+        m.synchronize()
+        bad = compare_case(m, case, name)
+    finally:
+        m.close()
+    assert not bad, f"{name} (co-launch {co}): fields differ from the reference: {bad}"
+    assert any(used) == co, used
+
+
 def test_tracer_steps_off_is_the_role_flip_path(amd):
     case = cases.load_e2e("bs_b4x2_tr_s60")
     m = build_model(amd, case).set_tracer_step(False).init()
@@ -161,7 +185,7 @@ def test_tracer_steps_launches(amd):
     finally:
         m.close()
     assert used and x2, (used, x2)
-    assert per_step <= 8, per_step
+    assert per_step <= 4, per_step   # (co-launched march + tracer step: 3.3 -> ~2.3)
 
 
 @pytest.mark.parametrize("path", ["tracer_steps", "role_flip", "fused"])
