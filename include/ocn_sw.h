@@ -414,10 +414,10 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  neighbours; the known-constant variant, no tracers, every block at least 4 x 4; two more halo rings
  *  outside the reference's arrays hold the exchanged state.  Same results bit for bit.
  *  ocn_ctx_get_option: 2 if the last ocn_ctx_step used such launches.
- *  OCN_OPT_CO_LAUNCH (default 1): tracer runs with x2 steps (one tracer, several blocks on the
- *  device, block batching): each step's march and the previous state's tracer step go as ONE launch
- *  (their workgroups in one grid) instead of two beside each other on two streams.  Same results bit
- *  for bit.  ocn_ctx_get_option: 2 if the last ocn_ctx_step co-launched.
+ *  OCN_OPT_CO_LAUNCH (default 1): tracer runs with x2 steps (one tracer, block batching on): each
+ *  step's march -- with OCN_OPT_OVERLAP 2 the part after the exchange -- and the previous state's
+ *  tracer step go as ONE launch (their workgroups in one grid) instead of two.  Same results bit for
+ *  bit.  ocn_ctx_get_option: 2 if the last ocn_ctx_step co-launched.
  *  OCN_OPT_MULTI_SPIN (diagnostics; default 1 << 20, about 0.5 s): the multi-step launch's grid
  *  barrier gives up after this many polls -- the launch's workgroups end and ocn_ctx_synchronize
  *  returns OCN_ERR_HIP instead of the device hanging if the grid was not co-resident.  Tests set it

@@ -1250,10 +1250,10 @@ static const std::vector<int> kHaloCheck = {OCN_SSH, OCN_UBRTR, OCN_VBRTR, OCN_H
 // the blocks (up to kPack of them per launch) instead of once per block.  Only for loops whose
 // launches read and write their own block's arrays, with nothing but batchable launches on s.
 // co: the loop's launches read nothing another writes -- a march batch and the tracer-step batch
-// after it may go as one launch (Batcher::co_launch)
+// after it may go as one launch (Batcher::co_launch; batched for one block too)
 template <class F> static int each_block(ocn_ctx *c, hipStream_t s, F &&f, bool co = false)
 {
-    const bool on = c->batch && c->blocks.size() > 1;
+    const bool on = c->batch && (c->blocks.size() > 1 || co);
     if (on) {
         batch_begin(&c->batcher, s);
         c->batcher.co_launch = co;
@@ -2081,6 +2081,16 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
         return launch_onepass(&b.g, tab.data(), (int)tab.size(), &t, sw, tau, nbad, (double *)b.sshp_alt,
                               (double *)b.up_alt, (double *)b.vp_alt, st, range, false, kc_of(c, b), b.own, frame_of);
     };
+    // OCN_OPT_CO_LAUNCH: the previous state's tracer step in a march launch after the exchange (one
+    // tracer, block batching: sw_kernels.hip k_march_tracer_b) -- both read the state just exchanged,
+    // the march writes the other buffers, the tracer step only the tracers'.  One block per rank too
+    // (the C5 layout over 8 GPUs: two launches per step become one)
+    const bool co = c->tr_pending && c->co_launch && c->sw.tracer_num == 1 && c->batch;
+    auto co_done = [c] {
+        c->tr_pending = false;
+        swap_tracer_roles(c);
+        swap_tracer_alt(c);
+    };
     if (overlap_level(c) >= 2 && !c->capturing) {
         HIPCHK(hipEventRecord(c->ev_fork, s));
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
@@ -2098,11 +2108,12 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
         HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
         if (k.x2_save) RC(ring2_run(c, true, c->comm_stream));
         RC(run_sync(c, with_tracers(c, kStateX2), c->comm_stream, nullptr, 2));   // the state two points deep
-        RC(each_block(c, c->comm_stream, [&](const LBlock &b) -> int {
+        RC(each_block(c, c->comm_stream, [&](const LBlock &b) -> int {   // the bands (+ the tracer step)
             const Range in = x2_inner(b);
             RC(march(b, c->comm_stream, nullptr, &in));
-            return OCN_OK;
-        }));
+            return co ? tracer_step_block(c, b, 1, tau, c->comm_stream) : OCN_OK;
+        }, co));
+        if (co) co_done();
         if (xrec.b) {
             HIPCHK(hipEventRecord(xrec.b, c->comm_stream));
             c->recs.push_back(xrec);
@@ -2113,10 +2124,6 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
     } else {
         if (k.x2_save) RC(ring2_run(c, true, s));
         RC(run_sync(c, with_tracers(c, kStateX2), s, nullptr, 2));   // the state two points deep
-        // OCN_OPT_CO_LAUNCH: the previous state's tracer step in the march's launch (one tracer, block
-        // batching: sw_kernels.hip k_march_tracer_b) -- both read the state just exchanged, the march
-        // writes the other buffers, the tracer step only the tracers'
-        const bool co = c->tr_pending && c->co_launch && c->sw.tracer_num == 1 && c->batch && c->blocks.size() > 1;
         if (c->tr_pending && !co && !c->capturing && c->comm_stream) {
             // the previous state's tracer step beside this step's march (on the comm stream: both read
             // the state just exchanged, the march writes the other buffers, the tracer step only the
@@ -2134,9 +2141,7 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
                 RC(march(b, s, nullptr, nullptr));
                 return tracer_step_block(c, b, 1, tau, s);
             }, true));
-            c->tr_pending = false;
-            swap_tracer_roles(c);
-            swap_tracer_alt(c);
+            co_done();
         } else {
             RC(each_block(c, s, [&](const LBlock &b) { return march(b, s, nullptr, nullptr); }));
         }

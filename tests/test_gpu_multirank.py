@@ -347,7 +347,7 @@ def test_ranks_topography_match_reference(amd, name, nranks):
     assert run_ranks_case.x2 == [True] * nranks and hr == {True}, (run_ranks_case.x2, hr)
 
 
-@pytest.mark.parametrize("tracers,seed", [(0, 600), (0, 601), (2, 600), (2, 601)])
+@pytest.mark.parametrize("tracers,seed", [(0, 600), (0, 601), (2, 600), (2, 601), (1, 602), (1, 603)])
 def test_random_rank_sequences_match_oracle(amd, tracers, seed):
     """Seeded random sequences of host entries (calls, tau changes, synchronize, reads, uploads of
     ssh, u, mu, RHSx, hhq_n and h_r, option toggles incl. the overlap level) run by every rank of 4
@@ -372,7 +372,7 @@ def _ranks_sequence(amd, seed, nops=20, tracers=0, n=120, grid=(2, 2)):
         elif op == "read":
             ops.append((op, str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp", "hhq_n"]))))
         elif op == "opt":
-            w = str(rng.choice(["onepass", "tracer_step", "lazy_tail", "flip", "overlap"]))
+            w = str(rng.choice(["onepass", "tracer_step", "lazy_tail", "flip", "overlap", "co_launch"]))
             ops.append((op, w, int(rng.integers(0, 2))))
         elif op == "kc":
             ops.append((op, int(rng.integers(0, 2))))
@@ -410,7 +410,7 @@ def _ranks_sequence(amd, seed, nops=20, tracers=0, n=120, grid=(2, 2)):
                     m.set_overlap(1 if op[2] else 2)
                 else:
                     {"onepass": m.set_onepass, "tracer_step": m.set_tracer_step, "lazy_tail": m.set_lazy_tail,
-                     "flip": m.set_flip}[op[1]](bool(op[2]))
+                     "flip": m.set_flip, "co_launch": m.set_co_launch}[op[1]](bool(op[2]))
             else:
                 nm, f = fn[op[0]]
                 for b in m.blocks:

@@ -334,20 +334,22 @@ def test_tail_keeps_n_level_only_while_it_holds(amd):
 # library's own checks; the fields match the oracle either way)
 @pytest.mark.parametrize("layout,seed", [("pair", 3), ("pair", 5), ("pair", 6), ("pair", 8),
                                          ("multi", 2), ("multi", 3), ("x2", 3), ("x2", 5), ("x2", 6),
-                                         ("tracer", 2), ("tracer", 3), ("tracer_x2", 3), ("tracer_x2", 5)])
+                                         ("tracer", 2), ("tracer", 3), ("tracer_x2", 3), ("tracer_x2", 5),
+                                         ("tracer1_x2", 3), ("tracer1_x2", 5)])
 def test_random_call_sequences_match_oracle(amd, layout, seed):
     """Seeded random sequences of the entries that drive or look into an open sequence -- calls of
     1..7 steps, tau changes, synchronize(), field reads (the tail formed), uploads of ssh and of a
     non-uniform h_r (the variant's verdict, the tail's n level), the known-constant option toggled
     -- on a box large enough for pairs ("pair"), a small one (several steps per launch, "multi") and
-    a 3x2-block box (x2 steps with exchanges, "x2"), with and without 2 tracers: every field against
+    a 3x2-block box (x2 steps with exchanges, "x2"), with 2 tracers, 1 tracer (the co-launched tracer
+    step, "tracer1_x2") and none: every field against
     the oracle given the same steps, taus and uploads, at every read and at the end (the
     reference's state after each call, model.f90:135-160)."""
     _random_sequence(amd, layout, seed, ["step", "step", "step", "step", "tau", "sync", "sync", "read", "ssh",
                                          "hr", "kc"], need_path=True)
 
 
-@pytest.mark.parametrize("layout,seed", [(lay, sd) for lay in ("pair", "multi", "x2", "tracer", "tracer_x2")
+@pytest.mark.parametrize("layout,seed", [(lay, sd) for lay in ("pair", "multi", "x2", "tracer", "tracer_x2", "tracer1_x2")
                                          for sd in (11, 12, 13)] +
                          [(lay, 21) for lay in ("island_pair", "island_multi", "island_x2", "island_tracer",
                                                 "island_tracer_x2")])
@@ -366,8 +368,9 @@ def _random_sequence(amd, layout, seed, ops, need_path, nops=20):
     base = layout.replace("island_", "")
     n, blocks, active = {"pair": (600, (1, 1), "pair_active"), "multi": (100, (1, 1), "multi_active"),
                          "x2": (120, (3, 2), "x2_active"), "tracer": (100, (1, 1), "tracer_step_active"),
-                         "tracer_x2": (120, (3, 2), "tracer_step_active")}[base]
-    tracers = 2 if base.startswith("tracer") else 0
+                         "tracer_x2": (120, (3, 2), "tracer_step_active"),
+                         "tracer1_x2": (120, (3, 2), "tracer_step_active")}[base]
+    tracers = 1 if base.startswith("tracer1") else 2 if base.startswith("tracer") else 0
     sw = amd.SWConfig(use_tracers=1, tracer_num=tracers) if tracers else amd.SWConfig()
     mask = None
     if layout.startswith("island_"):   # land islands (mask 1), some across block boundaries
@@ -379,7 +382,7 @@ def _random_sequence(amd, layout, seed, ops, need_path, nops=20):
     m = amd.OceanModel(amd.box_config(n, mask=mask), sw=sw, par=amd.ParallelConfig(*blocks)).init()
     ref = OracleTwin(n, blocks, tracers, mask)
     bad, used, log = [], False, []
-    reads = ["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp", "hhq_n"] + (["ff1_1", "ff1p_2"] if tracers else [])
+    reads = ["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp", "hhq_n"] + (["ff1_1", f"ff1p_{tracers}"] if tracers else [])
 
     def bump(nm, f):
         for bl in m.blocks:
@@ -428,10 +431,12 @@ def _random_sequence(amd, layout, seed, ops, need_path, nops=20):
             elif op == "hqn":
                 bump("hhq_n", lambda a: a + 1.0)
             elif op == "opt":
-                which = str(rng.choice(["onepass", "pair", "multi", "tracer_step", "lazy_tail", "flip"]))
+                which = str(rng.choice(["onepass", "pair", "multi", "tracer_step", "lazy_tail", "flip", "x4",
+                                        "co_launch"]))
                 val = int(rng.integers(0, 3 if which == "pair" else 2))
                 {"onepass": m.set_onepass, "multi": m.set_multi, "tracer_step": m.set_tracer_step,
-                 "lazy_tail": m.set_lazy_tail, "flip": m.set_flip}.get(which, lambda v: m.set_pair(int(v)))(
+                 "lazy_tail": m.set_lazy_tail, "flip": m.set_flip, "x4": m.set_x4,
+                 "co_launch": m.set_co_launch}.get(which, lambda v: m.set_pair(int(v)))(
                     val if which == "pair" else bool(val))
                 log[-1] += f"-{which}{val}"
             elif op == "graph":
