@@ -2049,12 +2049,16 @@ static int prebuild_x2(ocn_ctx *c)
 // The part of the interior an x2 step computes without the exchange: the interior less 2 points
 // on every side a neighbour (diagonals included) fills halos of -- a point's stencil reaches the
 // state 2 points away (D at +-1, formed from the state at +-1).
+constexpr int kX2BandCols = 60;   // a one-pass wave's output columns (sw_kernels.hip MarchStep, kHalo 2)
 static Range x2_inner(const LBlock &b)
 {
     auto any = [&](int a, int d1, int d2) { return b.nbr_rank[a - 1] >= 0 || b.nbr_rank[d1 - 1] >= 0 || b.nbr_rank[d2 - 1] >= 0; };
     Range r{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
-    if (any(1, 5, 6)) r.m1 -= 2;   // E, NE, SE
-    if (any(2, 7, 8)) r.m0 += 2;   // W, NW, SW
+    // (the E / W bands a whole wave wide where the block is wide enough: a band's waves march 60
+    // columns whatever its width, so the wider band takes them off the inner launch for nothing)
+    const int ew = b.g.nx_end - b.g.nx_start + 1 >= 3 * kX2BandCols ? kX2BandCols : 2;
+    if (any(1, 5, 6)) r.m1 -= ew;   // E, NE, SE
+    if (any(2, 7, 8)) r.m0 += ew;   // W, NW, SW
     if (any(3, 5, 7)) r.n1 -= 2;   // N, NE, NW
     if (any(4, 6, 8)) r.n0 += 2;   // S, SE, SW
     return r;
@@ -2191,12 +2195,18 @@ static int one_step_pair(ocn_ctx *c, double tau, const StepKind &k)
 // The part of the interior a pair of x2 steps computes without the exchange: the interior less 4
 // points on every side a neighbour (diagonals included) fills halos of (the pair reads the state 4
 // points out: the producers' D 3 out, from the state 4 out).
+// The E / W bands are a whole pair tile wide (kX4BandCols, where the block is wide enough): a band's
+// tiles cost the same whatever its width up to that (a pair workgroup marches 116 columns), so the
+// wider band takes that many columns off the inner launch for nothing -- one GPU, 2x1 blocks of
+// 4096^2 overlapped: see DESIGN.md 4.4
+constexpr int kX4BandCols = 116;   // sw_kernels.hip MarchStep::kPairCols
 static Range x4_inner(const LBlock &b)
 {
     auto any = [&](int a, int d1, int d2) { return b.nbr_rank[a - 1] >= 0 || b.nbr_rank[d1 - 1] >= 0 || b.nbr_rank[d2 - 1] >= 0; };
     Range r{b.g.nx_start, b.g.nx_end, b.g.ny_start, b.g.ny_end};
-    if (any(1, 5, 6)) r.m1 -= 4;   // E, NE, SE
-    if (any(2, 7, 8)) r.m0 += 4;   // W, NW, SW
+    const int ew = b.g.nx_end - b.g.nx_start + 1 >= 3 * kX4BandCols ? kX4BandCols : 4;
+    if (any(1, 5, 6)) r.m1 -= ew;   // E, NE, SE
+    if (any(2, 7, 8)) r.m0 += ew;   // W, NW, SW
     if (any(3, 5, 7)) r.n1 -= 4;   // N, NE, NW
     if (any(4, 6, 8)) r.n0 += 4;   // S, SE, SW
     return r;

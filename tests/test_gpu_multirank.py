@@ -372,7 +372,7 @@ def _ranks_sequence(amd, seed, nops=20, tracers=0, n=120, grid=(2, 2)):
         elif op == "read":
             ops.append((op, str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp", "hhq_n"]))))
         elif op == "opt":
-            w = str(rng.choice(["onepass", "tracer_step", "lazy_tail", "flip", "overlap", "co_launch"]))
+            w = str(rng.choice(["onepass", "tracer_step", "lazy_tail", "flip", "overlap", "co_launch", "x4"]))
             ops.append((op, w, int(rng.integers(0, 2))))
         elif op == "kc":
             ops.append((op, int(rng.integers(0, 2))))
@@ -410,7 +410,7 @@ def _ranks_sequence(amd, seed, nops=20, tracers=0, n=120, grid=(2, 2)):
                     m.set_overlap(1 if op[2] else 2)
                 else:
                     {"onepass": m.set_onepass, "tracer_step": m.set_tracer_step, "lazy_tail": m.set_lazy_tail,
-                     "flip": m.set_flip, "co_launch": m.set_co_launch}[op[1]](bool(op[2]))
+                     "flip": m.set_flip, "co_launch": m.set_co_launch, "x4": m.set_x4}[op[1]](bool(op[2]))
             else:
                 nm, f = fn[op[0]]
                 for b in m.blocks:
