@@ -63,41 +63,69 @@ int check_hip(hipError_t e, const char *what)
 
 
 // ------------------------------------------------------------------ halo segments
-// One strided 1-D run of doubles: dst[i*dst_stride] = src[i*src_stride], i < count.
+// w strided 1-D runs of doubles side by side: dst[i*dst_stride + j*dst_jstride] =
+// src[i*src_stride + j*src_jstride], i < count, j < w.  A column strip several layers deep is one
+// such segment (merge_columns: w adjacent columns), so a wave's loads take the layers of 64 / w rows
+// from shared cache lines instead of one line per element and layer.
 struct Seg {
     const double *src;
     double *dst;
     long src_stride, dst_stride;
     int count;
+    int w = 1;
+    long src_jstride = 0, dst_jstride = 0;
 };
 
-// Grid: x = segment, y = 64-element chunk of it -- one element per thread and one wave per
-// workgroup, so every load of a strip is in flight at once, spread over many CUs (column strips
-// touch one cache line per element; a loop per workgroup would pay one memory round trip per
-// pass).
+// Grid: one workgroup per 64-element chunk of a segment (SegChunk: the chunk table of the list, so
+// no workgroup of a short segment idles as in a segments x longest-chunks grid); element e of a
+// segment: run j = e % w, row i = e / w -- one element per thread and one wave per workgroup, so
+// every load of a strip is in flight at once, spread over many CUs (a loop per workgroup would pay
+// one memory round trip per pass).
 constexpr int kSegChunk = 64;
-__global__ __launch_bounds__(kSegChunk) void k_segments(const Seg *__restrict__ segs, int nseg)
+struct SegChunk { int seg, e0; };
+__device__ __forceinline__ bool seg_at(const Seg &g, int e, long &si, long &di)
 {
-    const int s = blockIdx.x;
-    const int i = (int)(blockIdx.y * kSegChunk + threadIdx.x);
-    if (s >= nseg || i >= segs[s].count) return;
-    const Seg g = segs[s];
-    g.dst[(long)i * g.dst_stride] = g.src[(long)i * g.src_stride];
+    if (e >= g.count * g.w) return false;
+    const int i = e / g.w, j = e - i * g.w;
+    si = (long)i * g.src_stride + (long)j * g.src_jstride;
+    di = (long)i * g.dst_stride + (long)j * g.dst_jstride;
+    return true;
+}
+__global__ __launch_bounds__(kSegChunk) void k_segments(const Seg *__restrict__ segs, const SegChunk *__restrict__ ch,
+                                                        int nch)
+{
+    const int b = blockIdx.x;
+    if (b >= nch) return;
+    const SegChunk q = ch[b];
+    const Seg g = segs[q.seg];
+    long si, di;
+    if (!seg_at(g, q.e0 + (int)threadIdx.x, si, di)) return;
+    g.dst[di] = g.src[si];
 }
 
 // The same runs compared instead of copied: ORs 1 into *flags where dst differs from src (bits).
-__global__ __launch_bounds__(kSegChunk) void k_segments_cmp(const Seg *__restrict__ segs, int nseg, int32_t *flags)
+__global__ __launch_bounds__(kSegChunk) void k_segments_cmp(const Seg *__restrict__ segs, const SegChunk *__restrict__ ch,
+                                                            int nch, int32_t *flags)
 {
-    const int s = blockIdx.x;
-    const int i = (int)(blockIdx.y * kSegChunk + threadIdx.x);
-    if (s >= nseg || i >= segs[s].count) return;
-    const Seg g = segs[s];
-    const double a = g.dst[(long)i * g.dst_stride], b = g.src[(long)i * g.src_stride];
+    const int k = blockIdx.x;
+    if (k >= nch) return;
+    const SegChunk q = ch[k];
+    const Seg g = segs[q.seg];
+    long si, di;
+    if (!seg_at(g, q.e0 + (int)threadIdx.x, si, di)) return;
+    const double a = g.dst[di], b = g.src[si];
     unsigned long long x, y;
     __builtin_memcpy(&x, &a, 8);
     __builtin_memcpy(&y, &b, 8);
     if (x != y) atomicOr(flags, 1);
 }
+
+// A segment list on the device with its chunk table (make_seglist)
+struct SegList {
+    Seg *d = nullptr;
+    SegChunk *ch = nullptr;
+    int n = 0, nch = 0;
+};
 
 // init_grid_data's bottom topography (control/init_data.f90:115-120): read_data2D_real4 fills the
 // block's interior from the file (tools/io.f90:130-147; the file holds the (nx-4) x (ny-4) interior,
@@ -184,8 +212,7 @@ struct LBlock {
     // A(bnd_x1 - kXRing, bnd_y1 - kXRing), pitch g.pitch)
     uint8_t *bits_x4 = nullptr;
     float *rows_x4 = nullptr;
-    Seg *d_save = nullptr, *d_restore = nullptr;   // its save / restore runs (k_segments)
-    int n_save = 0, n_restore = 0, ch_ring2 = 1;
+    SegList save, restore;   // its save / restore runs (k_segments)
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
@@ -218,14 +245,11 @@ struct Loopback {
 };
 
 struct HaloPlan {
-    Seg *d_local = nullptr;           // intra-process copies
-    int n_local = 0;
+    SegList local;                    // intra-process copies
     // remote: per peer rank, pack segments (into send buffer) and unpack segments (from recv)
     struct Peer { int rank; long count; double *send, *recv; };
     std::vector<Peer> peers;
-    Seg *d_pack = nullptr, *d_unpack = nullptr;
-    int n_pack = 0, n_unpack = 0;
-    int ch_local = 1, ch_pack = 1, ch_unpack = 1;   // kSegChunk-element chunks of the longest segment
+    SegList pack, unpack;
 };
 
 namespace ocn {
@@ -431,6 +455,36 @@ struct ocn_ctx {
     ocn::Batcher batcher;
 };
 
+// v on the device with its chunk table (one entry per kSegChunk elements of each segment), in one
+// allocation freed with the context
+static int make_seglist(ocn_ctx *c, const std::vector<Seg> &v, SegList &out)
+{
+    out = SegList{};
+    std::vector<SegChunk> ch;
+    for (size_t i = 0; i < v.size(); ++i)
+        for (long e = 0; e < (long)v[i].count * v[i].w; e += kSegChunk) ch.push_back(SegChunk{(int)i, (int)e});
+    if (v.empty() || ch.empty()) return OCN_OK;
+    const size_t sb = sizeof(Seg) * v.size(), cb = sizeof(SegChunk) * ch.size();
+    char *d = nullptr;
+    HIPCHK(hipMalloc(&d, sb + cb));
+    c->allocs.push_back(d);
+    HIPCHK(hipMemcpy(d, v.data(), sb, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d + sb, ch.data(), cb, hipMemcpyHostToDevice));
+    out.d = (Seg *)d;
+    out.ch = (SegChunk *)(d + sb);
+    out.n = (int)v.size();
+    out.nch = (int)ch.size();
+    return OCN_OK;
+}
+// the list's copies on s (cmp: compared instead, 1 ORed into *cmp where they differ)
+static int launch_segs(const SegList &l, hipStream_t s, int32_t *cmp = nullptr)
+{
+    if (!l.nch) return OCN_OK;
+    if (cmp) hipLaunchKernelGGL(k_segments_cmp, dim3((unsigned)l.nch), dim3(kSegChunk), 0, s, l.d, l.ch, l.nch, cmp);
+    else hipLaunchKernelGGL(k_segments, dim3((unsigned)l.nch), dim3(kSegChunk), 0, s, l.d, l.ch, l.nch);
+    return check_launch();
+}
+
 namespace ocn {
 
 // real(8) fields of a context: the SW set, then flux_x, flux_y and ff1/ff1p/ff1n per tracer
@@ -598,15 +652,8 @@ static int allocate_x2(ocn_ctx *c, LBlock &b)
             for (void *q : buf) restore.push_back(Seg{area + r[3], (double *)q + r[0], 1, r[1], (int)r[2]});
         }
     }
-    b.ch_ring2 = (std::max(w, h) + kSegChunk - 1) / kSegChunk;
-    b.n_save = (int)save.size();
-    b.n_restore = (int)restore.size();
-    HIPCHK(hipMalloc(&b.d_save, sizeof(Seg) * save.size()));
-    c->allocs.push_back(b.d_save);
-    HIPCHK(hipMalloc(&b.d_restore, sizeof(Seg) * restore.size()));
-    c->allocs.push_back(b.d_restore);
-    HIPCHK(hipMemcpy(b.d_save, save.data(), sizeof(Seg) * save.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(b.d_restore, restore.data(), sizeof(Seg) * restore.size(), hipMemcpyHostToDevice));
+    RC(make_seglist(c, save, b.save));
+    RC(make_seglist(c, restore, b.restore));
     return OCN_OK;
 }
 
@@ -792,6 +839,52 @@ static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::v
     return OCN_OK;
 }
 
+// Column strips (a side with a stride) of the same length whose runs are adjacent columns on a strided
+// side (step +1 or -1), the other side's runs equally spaced -- as the layers of one field's E / W strip
+// are: one segment of w runs (up to kSegMaxW) instead of w, copying the same elements.
+constexpr int kSegMaxW = 8;
+static std::vector<Seg> merge_columns(const std::vector<Seg> &in)
+{
+    std::vector<Seg> out;
+    std::vector<char> used(in.size(), 0);
+    std::map<const double *, size_t> by_src, by_dst;   // the column strips by their strided side
+    for (size_t i = 0; i < in.size(); ++i) {
+        if (in[i].w != 1) continue;
+        if (in[i].src_stride > 1) by_src[in[i].src] = i;
+        else if (in[i].dst_stride > 1) by_dst[in[i].dst] = i;
+    }
+    for (size_t i = 0; i < in.size(); ++i) {
+        if (used[i]) continue;
+        used[i] = 1;
+        Seg g = in[i];
+        const bool sc = g.src_stride > 1, dc = !sc && g.dst_stride > 1;
+        if (g.w == 1 && (sc || dc)) {
+            for (const long step : {1L, -1L}) {
+                if (g.w > 1) break;
+                while (g.w < kSegMaxW) {
+                    auto &idx = sc ? by_src : by_dst;
+                    auto it = idx.find((sc ? (const double *)g.src : (const double *)g.dst) + (long)g.w * step);
+                    if (it == idx.end() || used[it->second]) break;
+                    const Seg &b = in[it->second];
+                    if (b.count != g.count || b.src_stride != g.src_stride || b.dst_stride != g.dst_stride) break;
+                    // the other side's spacing: set by the second run, kept by the rest
+                    const long other = sc ? (long)(b.dst - g.dst) : (long)(b.src - g.src);
+                    if (g.w == 1) {
+                        if (sc) { g.src_jstride = step; g.dst_jstride = other; }
+                        else { g.dst_jstride = step; g.src_jstride = other; }
+                    } else if (other != (long)g.w * (sc ? g.dst_jstride : g.src_jstride)) {
+                        break;
+                    }
+                    used[it->second] = 1;
+                    ++g.w;
+                }
+            }
+        }
+        out.push_back(g);
+    }
+    return out;
+}
+
 static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan, int depth = 1)
 {
     std::vector<PlanEntry> entries;
@@ -826,19 +919,9 @@ static int build_plan(ocn_ctx *c, const std::vector<int> &fields, HaloPlan &plan
             pack.push_back(Seg{sb.f<double>(e.field) + soff, peers.at(e.peer).send + e.buf_off, sstr, 1, scnt});
         }
     }
-    auto upload = [&](const std::vector<Seg> &v, Seg *&d, int &n, int &ch) -> int {
-        n = (int)v.size();
-        ch = 1;
-        for (const Seg &g : v) ch = std::max(ch, (g.count + kSegChunk - 1) / kSegChunk);
-        if (!n) return OCN_OK;
-        HIPCHK(hipMalloc(&d, sizeof(Seg) * v.size()));
-        c->allocs.push_back(d);
-        HIPCHK(hipMemcpy(d, v.data(), sizeof(Seg) * v.size(), hipMemcpyHostToDevice));
-        return OCN_OK;
-    };
-    RC(upload(local, plan.d_local, plan.n_local, plan.ch_local));
-    RC(upload(pack, plan.d_pack, plan.n_pack, plan.ch_pack));
-    RC(upload(unpack, plan.d_unpack, plan.n_unpack, plan.ch_unpack));
+    RC(make_seglist(c, merge_columns(local), plan.local));
+    RC(make_seglist(c, merge_columns(pack), plan.pack));
+    RC(make_seglist(c, merge_columns(unpack), plan.unpack));
     return OCN_OK;
 }
 
@@ -1195,8 +1278,7 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
             HIPCHK(hipEventRecord(xrec.a, stream));
         }
         ++c->xchg;
-        hipLaunchKernelGGL(k_segments, dim3(p->n_pack, p->ch_pack), dim3(kSegChunk), 0, stream, p->d_pack, p->n_pack);
-        RC(check_launch());
+        RC(launch_segs(p->pack, stream));
         if (c->lb) {
             RC(lb_exchange(c, p, stream));
         } else {
@@ -1209,25 +1291,12 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
         }
     }
     if (cmp) {
-        if (p->n_local)
-            hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_local, p->ch_local), dim3(kSegChunk), 0, stream, p->d_local,
-                               p->n_local, cmp);
-        RC(check_launch());
-        if (p->n_unpack)
-            hipLaunchKernelGGL(k_segments_cmp, dim3(p->n_unpack, p->ch_unpack), dim3(kSegChunk), 0, stream, p->d_unpack,
-                               p->n_unpack, cmp);
-        RC(check_launch());
+        RC(launch_segs(p->local, stream, cmp));
+        RC(launch_segs(p->unpack, stream, cmp));
         return remote ? exchange_done(c, xrec, stream) : OCN_OK;
     }
-    if (p->n_local) {
-        hipLaunchKernelGGL(k_segments, dim3(p->n_local, p->ch_local), dim3(kSegChunk), 0, stream, p->d_local, p->n_local);
-        RC(check_launch());
-    }
-    if (p->n_unpack) {
-        hipLaunchKernelGGL(k_segments, dim3(p->n_unpack, p->ch_unpack), dim3(kSegChunk), 0, stream, p->d_unpack,
-                           p->n_unpack);
-        RC(check_launch());
-    }
+    RC(launch_segs(p->local, stream));
+    RC(launch_segs(p->unpack, stream));
     if (remote) RC(exchange_done(c, xrec, stream));
     return OCN_OK;
 }
@@ -1989,13 +2058,7 @@ static const std::vector<int> kStateX2 = {OCN_SSH, OCN_SSHP, OCN_UBRTR, OCN_UBRT
 
 static int ring2_run(ocn_ctx *c, bool save, hipStream_t s)
 {
-    for (const LBlock &b : c->blocks) {
-        const int n = save ? b.n_save : b.n_restore;
-        if (!n) continue;
-        hipLaunchKernelGGL(k_segments, dim3((unsigned)n, (unsigned)b.ch_ring2), dim3(kSegChunk), 0, s,
-                           save ? b.d_save : b.d_restore, n);
-        RC(check_launch());
-    }
+    for (const LBlock &b : c->blocks) RC(launch_segs(save ? b.save : b.restore, s));
     return OCN_OK;
 }
 
@@ -3121,7 +3184,7 @@ static int sync_entry(ocn_ctx *c, int field_id)
     // no neighbour block anywhere (one block, no other rank): the exchange writes nothing, so
     // nothing the step decisions rest on changes and a pending call tail may stay pending -- a
     // PSy-style caller syncing between 1-step calls pays no re-check, host wait or tail for it
-    if (!p->n_local && p->peers.empty()) return OCN_OK;
+    if (!p->local.n && p->peers.empty()) return OCN_OK;
     RC(complete_open(c));
     c->coherent_known = false;
     c->hh_consistent = false;
