@@ -37,7 +37,7 @@ module ocn_sw_c
                                      OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13,           &
                                      OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16,                    &
                                      OCN_OPT_TRACER_STEP = 17, OCN_OPT_MULTI_SPIN = 18, &
-                                     OCN_OPT_X4 = 19
+                                     OCN_OPT_X4 = 19, OCN_OPT_CO_LAUNCH = 20
     integer(c_int32_t), parameter :: OCN_HALO_LOCAL = 0, OCN_HALO_SEND = 1, OCN_HALO_RECV = 2
     integer, parameter :: OCN_UNIQUE_ID_BYTES = 128   ! sizeof(ncclUniqueId)
 
