@@ -332,21 +332,37 @@ def rccl_report(rank_info, steps: int):
                       "ocn_ctx_stage_stats); groups = ocn_ctx_comm_info exchanges in the timed region"}
 
 
+def profile_match(amd, d: dict, rec: dict):
+    """How a committed counter summary applies to the loaded library: "build" (taken on this exact
+    build, ocn_build_id), "kernel code" (the kernel's gfx950 machine code is byte for byte the profiled
+    code: the record's code_sha, ocean_model_arch_amd/_codeobj.py), or None."""
+    if d.get("build_id") == amd.build_id():
+        return "build"
+    try:
+        from ocean_model_arch_amd import _codeobj
+        if rec.get("code_sha") and rec["code_sha"] == _codeobj.kernel_code_sha(amd._lib.LIB_PATH, rec["symbol"]):
+            return "kernel code"
+    except Exception:
+        pass
+    return None
+
+
 def load_traffic(amd, stage: str, cells: int, compact: bool, box, blocks):
     """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, scripts/pmc_traffic.py), or None unless that summary was taken on
-    this exact library build (ocn_build_id) and workload (box, block grid, cells per block)."""
+    this workload (box, block grid, cells per block) and on this exact library build or the same
+    machine code of the kernel (profile_match).  Returns (bytes, match)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
         rec = d["kernels"][stage]
-        if (d.get("build_id") != amd.build_id() or list(d.get("box", [])) != list(box) or
-                list(d.get("blocks", [])) != list(blocks) or int(rec["cells"]) != cells or
-                bool(rec.get("compact")) != compact):
-            return None
-        return float(rec["hbm_bytes_per_launch"])
+        if (list(d.get("box", [])) != list(box) or list(d.get("blocks", [])) != list(blocks) or
+                int(rec["cells"]) != cells or bool(rec.get("compact")) != compact):
+            return None, None
+        match = profile_match(amd, d, rec)
+        return (float(rec["hbm_bytes_per_launch"]), match) if match else (None, None)
     except Exception:
-        return None
+        return None, None
 
 
 SHADER_CLOCK_GHZ = 2.4          # MI355X peak engine clock (MI355X_MICROARCH.md)
@@ -363,8 +379,10 @@ def load_valu(amd, stage: str, launch_ms: float, box, blocks):
         return None
     try:
         d = json.load(open(os.path.join(REPO, "profiles", "sq_valu.json")))
-        if (d.get("build_id") != amd.build_id() or list(d.get("box", [])) != list(box) or
-                list(d.get("blocks", [])) != list(blocks)):
+        if list(d.get("box", [])) != list(box) or list(d.get("blocks", [])) != list(blocks):
+            return None
+        match = profile_match(amd, d, d["kernels"][stage])
+        if not match:
             return None
         pl, pw = d["kernels"][stage]["per_launch"], d["kernels"][stage]["per_wave"]
         floor_ms = pl["SQ_INSTS_VALU"] * 4.0 / SIMDS / (SHADER_CLOCK_GHZ * 1e9) * 1e3
@@ -374,7 +392,9 @@ def load_valu(amd, stage: str, launch_ms: float, box, blocks):
                "per_wave_frac": {"valu_active": round(pw["SQ_ACTIVE_INST_VALU"] / wc, 4),
                                  "wait_inst_any": round(pw["SQ_WAIT_INST_ANY"] / wc, 4),
                                  "wait_any": round(pw["SQ_WAIT_ANY"] / wc, 4)},
-               "source": "profiles/sq_valu.json"}
+               "source": "profiles/sq_valu.json",
+               "profile_match": match if match == "build" else
+               f"{match}: profiled on build {d.get('build_id')}, the kernel's machine code unchanged"}
         clk = d["kernels"][stage].get("clock")
         if clk:   # the counter pass's effective shader clock (GRBM_GUI_ACTIVE / 8 / launch time) and the
             # VALU issue floor at that clock
@@ -620,10 +640,12 @@ def main():
             # the bound: VALU issue when its floor (at the clock the counter pass measured) takes a larger
             # share of the launch than the HBM bytes do; achieved / peak / frac stay the HBM figures
             issue = valu.get("issue_frac_at_clock", valu.get("issue_frac")) if valu else None
+            traffic, tmatch = load_traffic(amd, dom, local_cells, compact, [nxbox, nybox], [bx, by])
             roof = {"bound": "valu" if issue is not None and issue > frac else "hbm", "kernel": dom,
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(frac, 4),
-                    "traffic": load_traffic(amd, dom, local_cells, compact, [nxbox, nybox], [bx, by]),
+                    "traffic": traffic,
+                    **({"traffic_match": tmatch} if tmatch else {}),
                     "valu": valu,
                     "alg_bytes_per_launch": int(alg), "launch_ms": round(stage_ms[dom], 4)}
             if roof["bound"] == "valu":

@@ -64,7 +64,7 @@ def main():
            "fetch_scale": scale, "write_scale": wscale, "kernels": {}}
     # every dispatch of every template instance of a stage's kernel (e.g. MarchFusedB<true, true>
     # and <false, false>), averaged per dispatch like bench.py's per-launch timing
-    agg = defaultdict(lambda: {"FETCH_SIZE": [], "WRITE_SIZE": [], "names": set()})
+    agg = defaultdict(lambda: {"FETCH_SIZE": [], "WRITE_SIZE": [], "names": set(), "full": set()})
     for k, d in values(pmc).items():
         m = re.search(r"ocn::(\w+)", k.replace("k_range<ocn::", "").replace("k_march<ocn::", ""))
         name = m.group(1) if m else k
@@ -79,6 +79,7 @@ def main():
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             agg[stage][c] += d.get(c, [])
         agg[stage]["names"].add(name)
+        agg[stage]["full"].add(k)
     for stage, d in agg.items():
         # the launches that ran: the one-pass step's first call also launches the variants the device
         # verdict does not select, whose workgroups return at once (a few KB each) -- left out
@@ -92,6 +93,12 @@ def main():
         out["kernels"][stage] = {"kernel": "/".join(sorted(d["names"])), "dispatches": len(d["WRITE_SIZE"]),
                                  "cells": cells, "compact": compact, "fetch_bytes": round(rd), "write_bytes": round(wr),
                                  "hbm_bytes_per_launch": round(rd + wr)}
+        if len(d["full"]) == 1:   # one kernel instance: its machine code (bench.py profile_match)
+            from ocean_model_arch_amd._lib import LIB_PATH
+            from ocean_model_arch_amd import _codeobj
+            hit = _codeobj.sha_by_demangled(LIB_PATH, d["full"])
+            if hit:
+                out["kernels"][stage]["symbol"], out["kernels"][stage]["code_sha"] = next(iter(hit.values()))
     print(json.dumps(out, indent=1))
 
 

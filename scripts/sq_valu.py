@@ -105,7 +105,12 @@ def main():
     if not kern:
         raise SystemExit("no dispatches of the one-pass kernels")
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-    from ocean_model_arch_amd._lib import build_id
+    from ocean_model_arch_amd._lib import LIB_PATH, build_id
+    from ocean_model_arch_amd import _codeobj
+    for rec in kern.values():   # the profiled machine code (bench.py profile_match)
+        args = rec["kernel"][rec["kernel"].index("<") + 1:rec["kernel"].rindex(">")]
+        rec["symbol"] = _codeobj.march_step_symbol(args)
+        rec["code_sha"] = _codeobj.kernel_code_sha(LIB_PATH, rec["symbol"])
     out = {"source": "rocprofv3 --pmc SQ counters (one pass) over bench.py; per dispatch of the one-pass kernels",
            "build_id": build_id(), "box": [int(v) for v in a.box.lower().split("x")],
            "blocks": [int(v) for v in a.blocks.lower().split("x")], "kernels": kern}

@@ -68,11 +68,37 @@ def test_traffic_needs_matching_stamp(tmp_path, monkeypatch):
     (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(rec))
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
     ok = bench.load_traffic(_Amd("abc"), "onepass", 4096, True, [64, 64], [1, 1])
-    assert ok == 123.0
-    assert bench.load_traffic(_Amd("other"), "onepass", 4096, True, [64, 64], [1, 1]) is None
-    assert bench.load_traffic(_Amd("abc"), "onepass", 4096, True, [64, 64], [2, 1]) is None
-    assert bench.load_traffic(_Amd("abc"), "onepass", 2048, True, [64, 64], [1, 1]) is None
-    assert bench.load_traffic(_Amd("abc"), "fused_b", 4096, True, [64, 64], [1, 1]) is None
+    assert ok == (123.0, "build")
+    assert bench.load_traffic(_Amd("other"), "onepass", 4096, True, [64, 64], [1, 1]) == (None, None)
+    assert bench.load_traffic(_Amd("abc"), "onepass", 4096, True, [64, 64], [2, 1]) == (None, None)
+    assert bench.load_traffic(_Amd("abc"), "onepass", 2048, True, [64, 64], [1, 1]) == (None, None)
+    assert bench.load_traffic(_Amd("abc"), "fused_b", 4096, True, [64, 64], [1, 1]) == (None, None)
+
+
+def test_profile_applies_to_unchanged_kernel_code(tmp_path, monkeypatch):
+    """A summary taken on another build applies when the kernel's gfx950 machine code in the loaded
+    library is byte for byte the profiled code (code_sha of the record's symbol), not otherwise."""
+    import ocean_model_arch_amd as amd
+    from ocean_model_arch_amd import _codeobj
+    lib = amd._lib.LIB_PATH
+    if not os.path.exists(lib):
+        pytest.skip("library not built")
+    sym = _codeobj.march_step_symbol("true, false, true, false, false, true, false")
+    sha = _codeobj.kernel_code_sha(lib, sym)
+    assert sha and len(sha) == 16
+
+    class _A(_Amd):
+        _lib = amd._lib
+    rec = {"build_id": "elsewhere", "box": [64, 64], "blocks": [1, 1],
+           "kernels": {"onepass2": {"cells": 4096, "compact": True, "hbm_bytes_per_launch": 7.0, "symbol": sym,
+                                    "code_sha": sha}}}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    assert bench.load_traffic(_A("other"), "onepass2", 4096, True, [64, 64], [1, 1]) == (7.0, "kernel code")
+    rec["kernels"]["onepass2"]["code_sha"] = "0" * 16
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(rec))
+    assert bench.load_traffic(_A("other"), "onepass2", 4096, True, [64, 64], [1, 1]) == (None, None)
 
 
 def test_valu_needs_matching_stamp(tmp_path, monkeypatch):
