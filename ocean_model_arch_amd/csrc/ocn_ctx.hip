@@ -213,6 +213,9 @@ struct LBlock {
     uint8_t *bits_x4 = nullptr;
     float *rows_x4 = nullptr;
     SegList save, restore;   // its save / restore runs (k_segments)
+    // x4 pairs with tracers: the first step's new ssh, sshp, ubrtr, vbrtr (based like the fields: kXRing
+    // extra rows; MarchStep::trs), the state the second tracer step reads
+    double *trs[4] = {nullptr, nullptr, nullptr, nullptr};
     template <typename T> T *f(int id) const { return (T *)ptr[field_slot(id)]; }
 };
 
@@ -631,17 +634,35 @@ static int allocate_x2(ocn_ctx *c, LBlock &b)
     HIPCHK(hipMalloc(&b.hr_x, (size_t)b.g.pitch * h * sizeof(double)));
     c->allocs.push_back(b.hr_x);
     const long per = 2L * w + 2L * (h - 2);   // rows bnd_y1, bnd_y2; columns bnd_x1, bnd_x2 between them
-    HIPCHK(hipMalloc(&b.ring2, sizeof(double) * (size_t)(6 * per)));
+    // the state's six groups, then two per tracer (ff1 / ff1n, ff1p / its second buffer: x4 pairs
+    // exchange the tracers 2 deep)
+    const int ntr = c->sw.use_tracers > 0 ? c->sw.tracer_num : 0, ngroups = 6 + 2 * ntr;
+    HIPCHK(hipMalloc(&b.ring2, sizeof(double) * (size_t)(ngroups * per)));
     c->allocs.push_back(b.ring2);
     HIPCHK(hipMalloc(&b.bits_x4, (size_t)b.g.pitch * (h + 2 * kXRing)));
     c->allocs.push_back(b.bits_x4);
     HIPCHK(hipMalloc(&b.rows_x4, row_table_size((unsigned)(h + 2 * kXRing)) * sizeof(float)));
     c->allocs.push_back(b.rows_x4);
+    if (ntr) {
+        const long xr = (long)kXRing * b.g.pitch;
+        for (double *&q : b.trs) {
+            char *d = nullptr;
+            HIPCHK(hipMalloc(&d, sizeof(double) * (size_t)(b.g.pitch * (h + 2 * kXRing)) + 512));
+            c->allocs.push_back(d);
+            q = (double *)(d + 256) + xr;
+        }
+    }
     std::vector<Seg> save, restore;
     const long p = (long)b.g.pitch;
-    for (int g = 0; g < 6; ++g) {
+    for (int g = 0; g < ngroups; ++g) {
         void *buf[2];
-        state_group(b, g, buf);
+        if (g < 6) {
+            state_group(b, g, buf);
+        } else {
+            const int t = 1 + (g - 6) / 2;
+            buf[0] = b.ptr[field_slot((g - 6) % 2 ? OCN_FF1P(t) : OCN_FF1(t))];
+            buf[1] = (g - 6) % 2 ? b.ffp_alt[(size_t)t - 1] : b.ptr[field_slot(OCN_FF1N(t))];
+        }
         double *area = b.ring2 + g * per;
         // (offset in the array, stride, count, offset in the area)
         const long runs[4][4] = {{0, 1, w, 0}, {(long)(h - 1) * p, 1, w, w}, {p, p, h - 2, 2L * w},
@@ -775,7 +796,9 @@ static void halo_layer(const ocn_block &rcv, const ocn_block &src, int d, int j,
 static bool is_tracer_field(int id) { return id >= OCN_TRACER_BASE; }
 // Depth of field id in an exchange of `depth`: the tracer fields are exchanged one point deep in
 // every exchange (one_step_x2 sends them with the state's two-deep strips: one message per peer)
-static int field_depth(int id, int depth) { return is_tracer_field(id) ? 1 : depth; }
+// tracers: 1 deep, 2 with the x4 pairs' 4-deep state (one_step_x4's first tracer step covers the halo
+// ring neighbours own)
+static int field_depth(int id, int depth) { return is_tracer_field(id) ? (depth >= 4 ? 2 : 1) : depth; }
 
 static int plan_entries(const ocn_ctx *c, const std::vector<int> &fields, std::vector<PlanEntry> &out,
                         int depth = 1)
@@ -2280,11 +2303,40 @@ static Range x4_inner(const LBlock &b)
 // priority), then the bands around it there -- the RCCL group's latency hides behind the inner
 // pair; the two launches write disjoint points of the new state (other buffers than the ones read),
 // the exchange writes halos only the bands read.
+// Tracer runs (tracer steps, c->tr_call): the exchange carries the tracers 2 deep; the pending tracer
+// step of the state before the pair (A) runs over the interior and the first halo ring neighbours own
+// (launch_tracer_step ext: as those neighbours update it), co-launched with the pair where it can be;
+// the producers also write the first step's new state (LBlock::trs), and the tracer step of that state
+// (B) runs after the pair from there -- two tracer steps per exchange, as the reference runs one per
+// step after its exchanges; the second tracer ring is saved / restored with the state's (ring2_run).
 static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
 {
     hipStream_t s = c->stream;
     ocn_ctx::Rec rec;
     c->hn_fresh = false;
+    const bool tr = c->tr_call, trA = tr && c->tr_pending;
+    const bool co = trA && c->co_launch && c->sw.tracer_num == 1 && c->batch;
+    auto tr_a = [&](const LBlock &b, int t, hipStream_t st) -> int {
+        std::vector<void *> tab = b.ptr;
+        tab[field_slot(OCN_HHQ_REST)] = b.hr_x;   // (h_r with the neighbours' second ring)
+        const Compact ct{b.bits, b.rows_x, c->march};
+        return launch_tracer_step(&b.g, tab.data(), (int)tab.size(), &ct, t, tau, c->sw.time_smooth,
+                                  (double *)b.ptr[field_slot(OCN_FF1N(t))], (double *)b.ffp_alt[(size_t)t - 1], b.own,
+                                  st, true);
+    };
+    auto tr_b = [&](const LBlock &b, int t, hipStream_t st) -> int {
+        std::vector<void *> tab = b.ptr;   // the state the pair's first step formed
+        tab[field_slot(OCN_SSH)] = b.trs[0]; tab[field_slot(OCN_SSHP)] = b.trs[1];
+        tab[field_slot(OCN_UBRTR)] = b.trs[2]; tab[field_slot(OCN_VBRTR)] = b.trs[3];
+        const Compact ct{b.bits, b.rows_x, c->march};
+        return launch_tracer_step(&b.g, tab.data(), (int)tab.size(), &ct, t, tau, c->sw.time_smooth,
+                                  (double *)b.ptr[field_slot(OCN_FF1N(t))], (double *)b.ffp_alt[(size_t)t - 1], b.own,
+                                  st, false);
+    };
+    auto tr_done = [c] {
+        swap_tracer_roles(c);
+        swap_tracer_alt(c);
+    };
     auto pair = [&](const LBlock &b, hipStream_t st, const Range *range, const Range *frame_of) -> int {
         ocn_block bx = b.g;   // the block widened by kXRing rings, the bases moved to A(bnd_x1 - kXRing, bnd_y1 - kXRing)
         bx.bnd_x1 -= kXRing; bx.bnd_x2 += kXRing; bx.bnd_y1 -= kXRing; bx.bnd_y2 += kXRing;
@@ -2292,10 +2344,12 @@ static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
         std::vector<void *> tab(b.ptr.size(), nullptr);
         for (int id = OCN_SSH; id < OCN_SSH + num_r8(c); ++id) tab[field_slot(id)] = b.f<double>(id) - sh;
         const Compact t{b.bits_x4, b.rows_x4, c->march};
+        double *trs_x[4];
+        for (int i = 0; i < 4; ++i) trs_x[i] = b.trs[i] ? b.trs[i] - sh : nullptr;
         return launch_onepass_pair_x4(&bx, tab.data(), (int)tab.size(), &t, c->sw, tau, k.check ? c->d_nbad : nullptr,
                                       k.check2 ? c->d_nbad : nullptr, (double *)b.sshp_alt - sh, (double *)b.up_alt - sh,
                                       (double *)b.vp_alt - sh, st, kc_of(c, b), b.own, range, (int)c->blocks.size(),
-                                      frame_of);
+                                      frame_of, tr ? trs_x : nullptr);
     };
     bool inner_ok = true;   // (every block keeps an inner part: the bands around it are disjoint)
     for (const LBlock &b : c->blocks) {
@@ -2317,11 +2371,12 @@ static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
         }
         HIPCHK(hipStreamWaitEvent(c->comm_stream, c->ev_fork, 0));
         if (k.x2_save) RC(ring2_run(c, true, c->comm_stream));
-        RC(run_sync(c, kStateX2, c->comm_stream, nullptr, 4));   // the state four points deep
-        RC(each_block(c, c->comm_stream, [&](const LBlock &b) -> int {
+        RC(run_sync(c, tr ? with_tracers(c, kStateX2) : kStateX2, c->comm_stream, nullptr, 4));   // the state 4 deep
+        RC(each_block(c, c->comm_stream, [&](const LBlock &b) -> int {   // the bands (+ tracer step A)
             const Range in = x4_inner(b);
-            return pair(b, c->comm_stream, nullptr, &in);
-        }));
+            RC(pair(b, c->comm_stream, nullptr, &in));
+            return co ? tr_a(b, 1, c->comm_stream) : OCN_OK;
+        }, co));
         if (xrec.b) {
             HIPCHK(hipEventRecord(xrec.b, c->comm_stream));
             c->recs.push_back(xrec);
@@ -2331,10 +2386,24 @@ static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
         RC(join_sync(c));
     } else {
         if (k.x2_save) RC(ring2_run(c, true, s));
-        RC(run_sync(c, kStateX2, s, nullptr, 4));   // the state four points deep
+        RC(run_sync(c, tr ? with_tracers(c, kStateX2) : kStateX2, s, nullptr, 4));   // the state four points deep
         RC(timer_begin(c, OCN_TIMER_ONEPASS2, rec));
-        RC(each_block(c, s, [&](const LBlock &b) { return pair(b, s, nullptr, nullptr); }));
+        RC(each_block(c, s, [&](const LBlock &b) -> int {
+            RC(pair(b, s, nullptr, nullptr));
+            return co ? tr_a(b, 1, s) : OCN_OK;
+        }, co));
         RC(timer_end(c, rec));
+    }
+    if (trA) {   // tracer step A (here when not co-launched: after the join, it reads the exchanged halos)
+        c->tr_pending = false;
+        for (int t = co ? 2 : 1; t <= c->sw.tracer_num; ++t)
+            RC(each_block(c, s, [&](const LBlock &b) { return tr_a(b, t, s); }));
+        tr_done();
+    }
+    if (tr) {   // tracer step B: the state of the pair's first step
+        for (int t = 1; t <= c->sw.tracer_num; ++t)
+            RC(each_block(c, s, [&](const LBlock &b) { return tr_b(b, t, s); }));
+        tr_done();
     }
     swap_alt3(c);
     swap_roles(c);
@@ -3434,7 +3503,9 @@ static bool x2_local(const ocn_ctx *c)
 // 4-deep strips lie in its interior) and row padding for the extra rings
 static bool x4_local(const ocn_ctx *c)
 {
-    if (!c->x4 || !c->x4_tab_ok || !c->known_const || c->r8_handed || c->sw.use_tracers > 0 || !c->march)
+    // (tracer runs: with the tracer steps, one_step_x4 runs them)
+    if (!c->x4 || !c->x4_tab_ok || !c->known_const || c->r8_handed || (c->sw.use_tracers > 0 && !c->tr_step) ||
+        !c->march)
         return false;
     for (const GBlock &g : c->gblocks)
         if (g.rank >= 0 && (g.g.nx_end - g.g.nx_start < 3 || g.g.ny_end - g.g.ny_start < 3)) return false;
@@ -3498,6 +3569,7 @@ static int complete_open(ocn_ctx *c)
         k1.flip = k1.one = k1.next_one = k1.a_done = true;
         k1.x2 = c->open_x2;   // (a pair of x2 steps: its first step again, one_step_x2)
         if (const int rc = run_step(c, c->open_tau, k1)) return finish_call(c, rc);
+        c->tr_pending = false;   // (tracer runs: the pair ran the tracer step of that state too)
     }
     StepKind k{};
     k.last = k.one_last = true;

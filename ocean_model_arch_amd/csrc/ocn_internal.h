@@ -160,11 +160,12 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
 // the state exchanged 4 deep; the known-constant variant (kc.mode OCN_KC_KNOWN); own: the halo points
 // neighbour blocks own; range: the consumers' points (nullptr: the interior), frame_of: only the bands
 // of it outside *frame_of (one launch of up to 4 rects); nblk: blocks of this size batched into the
-// launch (the tile height's cost model)
+// launch (the tile height's cost model); trs (tracer runs): four arrays (based like the fields) that get the
+// first step's new ssh, sshp, ubrtr, vbrtr on the producers' points -- the second tracer step's state
 int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                            double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
                            hipStream_t s, const OnepassKC &kc, unsigned own, const Range *range = nullptr,
-                           int nblk = 1, const Range *frame_of = nullptr);
+                           int nblk = 1, const Range *frame_of = nullptr, double *const *trs = nullptr);
 // one_step_x4's tables of block g: mask bytes over g widened by kXRing (bits4, its base at
 // A(bnd_x1 - kXRing, bnd_y1 - kXRing), pitch g->pitch) and the row table of those rows (rows4,
 // row_table_size(rows + 2 kXRing)) from the block's own tables, its ext rows and the basin mask
@@ -210,9 +211,11 @@ int launch_tracer(const ocn_block *b, void *const *ptr, int nptr, const Compact 
                   double ts, hipStream_t s);
 // the three tracer stages of tracer k as one launch in a one-pass sequence (sw_stencils.h TracerStep:
 // hh_init's hhu / hhv / hhq_p formed from the state): ffn into ffn_out, the filtered ffp into ffp_out;
-// own: the halo points neighbour blocks own (their fluxes formed here, as the exchange delivers them)
+// own: the halo points neighbour blocks own (their fluxes formed here, as the exchange delivers them);
+// ext: also the first halo ring's points neighbours own, updated as those neighbours update them (x4
+// pairs with tracers: the state 4 and the tracers 2 points deep exchanged)
 int launch_tracer_step(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int k, double tau,
-                       double ts, double *ffn_out, double *ffp_out, unsigned own, hipStream_t s);
+                       double ts, double *ffn_out, double *ffp_out, unsigned own, hipStream_t s, bool ext = false);
 // ORs 1 into *flags (device int) if a buffer pair of the role-flip step differs outside the
 // pair's write set (sw_stencils.h Coherence).
 int launch_coherence(const ocn_block *b, void *const *ptr, const uint8_t *bits, int32_t *flags, hipStream_t s);

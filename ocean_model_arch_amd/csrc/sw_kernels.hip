@@ -1916,8 +1916,9 @@ struct MarchStep {
     static constexpr int kStAux = WT ? 16 : 0;
     static constexpr bool kPair = PAIR;
     static constexpr bool kX2 = X2;
-    // the x2 single step of the known-constant variant: co-launched with a tracer step (k_march_tracer_b)
-    static constexpr bool kCoTracer = X2 && ZF && !HR && !LAST && !PAIR && !WT;
+    // the x2 single step and the x4 pair of the known-constant variant: co-launched with a tracer step
+    // (k_march_tracer_b)
+    static constexpr bool kCoTracer = X2 && ZF && !HR && !LAST && !WT;
     static constexpr int kPairCols = 116;   // PAIR: a workgroup's output columns (2 x 60 produced, less 2 each side)
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
@@ -1930,6 +1931,9 @@ struct MarchStep {
     const double *kc; const int32_t *fbz; int gate;
     unsigned own;   // X2: own_class bits of the halo points neighbour blocks own
     int32_t *nbad2 = nullptr;   // PAIR: the second step's check_ssh_err count (nbad: the first step's)
+    // PAIR + X2 with tracers (ocn_ctx.hip one_step_x4): the first step's new ssh, sshp, ubrtr, vbrtr --
+    // what the producers put into the ring -- also to these arrays (the second tracer step reads them)
+    double *trs[4] = {nullptr, nullptr, nullptr, nullptr};
     static constexpr bool kGate = true;
     // gate (OCN_KC_DEVICE): which verdict of the check (launch_fallback_check's flag word: bit 0 =
     // h_r not uniform, bit 1 = anything else) this launch is for -- 1: none, 3: h_r only, 2: bit 1
@@ -2513,6 +2517,17 @@ struct MarchStep {
         }
         if constexpr (RO == 1) {   // PAIR producer: the row goes into the ring, not to memory
             if (!WARM) pair_put<PH>(x, o, n);
+            if constexpr (X2) {   // (and to the tracer step's arrays: the lanes and rows that hold the state)
+                if (!WARM && trs[0]) {
+                    const unsigned nbytes = (unsigned)b.pitch * (unsigned)(b.bnd_y2 - b.bnd_y1 + 1) * 8u;
+                    const unsigned ci = geo(&b)(L.m, min(max(n, b.bnd_y1), b.bnd_y2)).c;
+                    const bool on = L0.out && n >= b.ny_start - 2 && n <= b.ny_end + 2;
+                    st_on(trs[0], nbytes, ci, o.lu ? o.sshn : x.ssh.s<PH>(1), on);
+                    st_on(trs[1], nbytes, ci, o.lu ? o.fx : x.shp.s<PH>(1), on);
+                    st_on(trs[2], nbytes, ci, o.cu ? o.un : x.u.s<PH>(1), on);
+                    st_on(trs[3], nbytes, ci, o.cv ? o.vn : x.v.s<PH>(1), on);
+                }
+            }
             pair_barrier();
             ++x.rn;
             fb = fbn;
@@ -3074,7 +3089,7 @@ int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Co
 int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                            double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
                            hipStream_t s, const OnepassKC &kc, unsigned own, const Range *range, int nblk,
-                           const Range *frame_of)
+                           const Range *frame_of, double *const *trs)
 {
     if (!cp || !cp->march || sw.full_free_surface != 1 || sw.trans_terms <= 0 || sw.ksw_lat <= 0 || !sshp_out ||
         !up_out || !vp_out)
@@ -3114,11 +3129,16 @@ int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, cons
         g.ntiles += g.r[g.nr - 1].tiles;
     }
     int ex;
+    auto go = [&](auto body) {
+        if (trs)
+            for (int i = 0; i < 4; ++i) body.trs[i] = trs[i];
+        return issue_march(g, body, s);
+    };
     if (std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020)   // tau = 2^k
-        return issue_march(g, MarchStep<true, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out,
-                                                                             vp_out, kc.kc, nullptr, 0, own, nbad2}, s);
-    return issue_march(g, MarchStep<false, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out,
-                                                                          vp_out, kc.kc, nullptr, 0, own, nbad2}, s);
+        return go(MarchStep<true, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out, vp_out, kc.kc,
+                                                                  nullptr, 0, own, nbad2});
+    return go(MarchStep<false, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out, vp_out, kc.kc,
+                                                               nullptr, 0, own, nbad2});
 }
 
 // mask bytes of one_step_x4 over the widened geometry bx: at the halo points neighbour blocks own
@@ -3214,7 +3234,8 @@ __device__ __forceinline__ void tracer_tile(const RangeB &R, int tile, const Bod
     sfx[ty][tx] = fxe;
     sfy[ty][tx] = fyn;
     __syncthreads();
-    if (!in || !(ld(k.W.lu, k.I(m, n)) > 0.5f)) return;
+    // (an extended range: the halo points neighbours own only -- TracerStep::in_fluxes)
+    if (!in || !k.in_fluxes(m, n) || !(ld(k.W.lu, k.I(m, n)) > 0.5f)) return;
     const double fxw = tx > 0 ? sfx[ty][tx - 1] : k.fx_at(m - 1, n);
     const double fys = ty > 0 ? sfy[ty - 1][tx] : k.fy_at(m, n - 1);
     k.finish(m, n, fxe, fxw, fyn, fys);
@@ -3348,11 +3369,17 @@ template <class Body> static int launch_tracer_tiles(const Range &r, const Body 
 }
 
 int launch_tracer_step(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, int k, double tau,
-                       double ts, double *ffn_out, double *ffp_out, unsigned own, hipStream_t s)
+                       double ts, double *ffn_out, double *ffp_out, unsigned own, hipStream_t s, bool ext)
 {
     if (!ffn_out || !ffp_out) return set_error(OCN_ERR_ARG, "tracer step: output buffers");
     RC_K(check_block(b));
-    const Range ri = range_interior(b);
+    Range ri = range_interior(b);
+    if (ext) {   // + the first halo ring where neighbours own it (the tiles skip the rest)
+        if (b->bnd_x1 > b->nx_start - 2 || b->bnd_x2 < b->nx_end + 2 || b->bnd_y1 > b->ny_start - 2 ||
+            b->bnd_y2 < b->ny_end + 2)
+            return set_error(OCN_ERR_ARG, "tracer step over the first halo ring: a 2-wide halo");
+        ri = Range{ri.m0 - 1, ri.m1 + 1, ri.n0 - 1, ri.n1 + 1};
+    }
     if (cp)
         return launch_tracer_tiles(ri, KTracerStep<true>{*b, make_tab<true>(ptr, nptr, cp->bits, cp->rows, block_rows(b), k),
                                                          tau, ts, own, ffn_out, ffp_out}, s);

@@ -63,13 +63,29 @@ def test_x4_overlapped_blocks_match_reference(amd, name, calls):
     assert any(used), used
 
 
+@pytest.mark.parametrize("name,calls", [("box70x54_b3x2_tr_s20", [2, 18]), ("box70x54_b3x2_tr_s20", [2, 5, 1, 1, 3, 8]),
+                                        ("box70x54_b3x2_tr_s20", [1] * 20), ("bs_b4x2_tr_s60", [2, 58]),
+                                        ("bs_b4x2_tr_s60", [3, 1, 1, 1, 54]), ("bs_b4x2_tr_s604", [2, 602])])
+@pytest.mark.parametrize("overlap", [None, 2])
+def test_x4_tracer_blocks_match_reference(amd, name, calls, overlap):
+    """Tracer runs with x4 pairs (one_step_x4 with tracer steps): the exchange carries the tracers 2
+    deep, the pending tracer step runs over the interior and the halo ring neighbours own (co-launched
+    with the pair), the pair's producers write the first step's state for the second tracer step --
+    two SW steps and two tracer steps per exchange, every field bitwise (control/tracer.f90:33-62 after
+    each step, leapfrog_tracer.f90:13-170)."""
+    bad, used = _run_blocks(amd, name, calls, overlap=overlap)
+    assert not bad, f"{name} {calls}: fields differ from the reference: {bad}"
+    assert any(used), used
+
+
 def test_x4_off_is_the_x2_path(amd):
     bad, used = _run_blocks(amd, "box70x54_b3x2_s20", [2, 18], x4=False)
     assert not bad and not any(used), (bad, used)
 
 
 @pytest.mark.parametrize("name,nranks,calls", [("box70x54_b3x2_s20", 6, [2, 18]), ("bs_b4x2_s60", 8, [2, 58]),
-                                               ("box40x32_b2x2_s5", 4, [2, 3]), ("box70x54_b3x2_s20", 6, [2, 7, 3, 8])])
+                                               ("box40x32_b2x2_s5", 4, [2, 3]), ("box70x54_b3x2_s20", 6, [2, 7, 3, 8]),
+                                               ("bs_b4x2_tr_s60", 8, [2, 58]), ("box70x54_b3x2_tr_s20", 6, [2, 7, 3, 8])])
 def test_x4_ranks_match_reference(amd, name, nranks, calls):
     """One block per loopback rank: the exchange is the RCCL path's (device pack / unpack, per-peer
     messages 4 deep), the decision every rank's (the vote's x4 word), every field bitwise.  (With a
