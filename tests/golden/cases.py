@@ -16,6 +16,8 @@ INIT_CASES = ["box70x54_b1x1_s0", "box48x40_cart_s0", "bs_b4x2_tr_s0"]
 # BASELINE.json configs at full size (SHA-256 digests of every field of every block only):
 # C2 1024^2 1 block, C3 2048^2 2x2 blocks, the bench workload 4096^2 1 block, C4 4096^2 4x2 blocks
 FULLSIZE_CASES = ["box1024_b1x1_s10", "box2048_b2x2_s4", "box4096_b1x1_s6", "box4096_b4x2_s4"]
+# C3 / C4 long enough for x4 pairs over ranks with the bench's cadence (tests/test_gpu_x4.py)
+FULLSIZE_RANK_CASES = ["box2048_b2x2_s10", "box4096_b4x2_s12"]
 # the reference's shipped default run (basin.par 1525 x 1115, 604 steps) on 1 and 2 x 2 blocks
 SHIPPED_CASES = ["box1521x1111_b1x1_s604", "box1521x1111_b2x2_s604"]
 # a non-uniform rest depth read from a basin.par topography file (control/init_data.f90:115-120)

@@ -286,6 +286,10 @@ CASES = {
     "box2048_b2x2_s4": (dict(BOX, nx=2052, ny=2052), SW_DEFAULT, (2, 2), 4, "sha"),        # C3
     "box4096_b1x1_s6": (dict(BOX, nx=4100, ny=4100), SW_DEFAULT, (1, 1), 6, "sha"),        # the bench workload
     "box4096_b4x2_s4": (dict(BOX, nx=4100, ny=4100), SW_DEFAULT, (4, 2), 4, "sha"),        # C4
+    # C3 / C4 long enough for pairs of x2 steps over ranks with the bench's cadence (a 2-step call
+    # that votes with the known-constant verdict, then one call of 8 or 10 steps: 4 / 5 x4 pairs)
+    "box2048_b2x2_s10": (dict(BOX, nx=2052, ny=2052), SW_DEFAULT, (2, 2), 10, "sha"),      # C3
+    "box4096_b4x2_s12": (dict(BOX, nx=4100, ny=4100), SW_DEFAULT, (4, 2), 12, "sha"),      # C4
     # the reference's shipped default run: basin.par 1525 x 1115, mask and topography none, sw.par,
     # ocean_run.par's tau = 1 s for 0.007 days = 604 steps (model.f90:135-160); one block as
     # parallel.par ships it, and 2 x 2 blocks (odd, non-64-aligned block sizes)

@@ -44,7 +44,8 @@ def _run_blocks(amd, name, calls, x4=True, overlap=None):
 @pytest.mark.parametrize("name,calls", [("box70x54_b3x2_s20", [2, 18]), ("box70x54_b3x2_s20", [2, 5, 1, 1, 3, 8]),
                                         ("box70x54_b3x2_s20", [1] * 20), ("bs_b4x2_s60", [2, 58]),
                                         ("bs_b4x2_s60", [3, 1, 1, 1, 54]), ("box40x32_b2x2_s5", [2, 3]),
-                                        ("box2048_b2x2_s4", [1, 3]), ("box4096_b4x2_s4", [1, 3])])
+                                        ("box2048_b2x2_s4", [1, 3]), ("box4096_b4x2_s4", [1, 3]),
+                                        ("box2048_b2x2_s10", [2, 8]), ("box4096_b4x2_s12", [2, 10])])
 def test_x4_blocks_match_reference(amd, name, calls):
     """Several blocks in one process (local halo copies): pairs of x2 steps inside calls and across
     calls (the reference's 1-step cadence: a pair every second call), every field bitwise."""
@@ -83,40 +84,80 @@ def test_x4_off_is_the_x2_path(amd):
     assert not bad and not any(used), (bad, used)
 
 
-@pytest.mark.parametrize("name,nranks,calls", [("box70x54_b3x2_s20", 6, [2, 18]), ("bs_b4x2_s60", 8, [2, 58]),
-                                               ("box40x32_b2x2_s5", 4, [2, 3]), ("box70x54_b3x2_s20", 6, [2, 7, 3, 8]),
-                                               ("bs_b4x2_tr_s60", 8, [2, 58]), ("box70x54_b3x2_tr_s20", 6, [2, 7, 3, 8])])
-def test_x4_ranks_match_reference(amd, name, nranks, calls):
-    """One block per loopback rank: the exchange is the RCCL path's (device pack / unpack, per-peer
-    messages 4 deep), the decision every rank's (the vote's x4 word), every field bitwise.  (With a
-    communicator a call runs pairs after a call of 2 or more steps has voted with the verdict known:
-    the full-size C3 / C4 fixtures, 4 steps, are too short for that -- their blocks run the pairs in one
-    process above, and over ranks in the random rank sequences.)"""
+def _run_ranks(amd, name, nranks, calls, overlap=None, co=None):
+    """One block per loopback rank, the bench's cadence (a first call, a synchronize: the
+    known-constant verdict reaches every host, so the next call's vote can choose the pairs), then
+    the remaining calls, complete() and a synchronize.  Returns (differing fields, per rank the
+    x4_active of each later call, per rank whether a later call co-launched a march and a tracer step)."""
     case = cases.load_e2e(name)
-    models = [build_model(amd, case, rank=r, nranks=nranks) for r in range(nranks)]
+    models = [build_model(amd, case, rank=r, nranks=nranks, overlap=overlap) for r in range(nranks)]
+    if co is not None:
+        for m in models:
+            m.set_co_launch(co)
     amd.OceanModel.attach_loopback(models)
 
     def body(m):
         m.init()
         m.step(calls[0], tau=1.0, check_every=1)
         m.synchronize()
-        used = []
+        used, co_used = [], False
         for n in calls[1:]:
             m.step(n, tau=1.0, check_every=1)
             used.append(m.x4_active)
+            co_used = co_used or m.co_launched
+        m.complete()
         m.synchronize()
-        return used
+        return used, co_used
 
     try:
-        used = amd.run_ranks(models, body)
+        res = amd.run_ranks(models, body)
         bad = []
         for m in models:
             bad += compare_case(m, case, name, whole=False)
     finally:
         for m in models:
             m.close()
+    return bad, [r[0] for r in res], [r[1] for r in res]
+
+
+@pytest.mark.parametrize("name,nranks,calls", [("box70x54_b3x2_s20", 6, [2, 18]), ("bs_b4x2_s60", 8, [2, 58]),
+                                               ("box40x32_b2x2_s5", 4, [2, 3]), ("box70x54_b3x2_s20", 6, [2, 7, 3, 8]),
+                                               ("bs_b4x2_tr_s60", 8, [2, 58]), ("box70x54_b3x2_tr_s20", 6, [2, 7, 3, 8])])
+def test_x4_ranks_match_reference(amd, name, nranks, calls):
+    """One block per loopback rank: the exchange is the RCCL path's (device pack / unpack, per-peer
+    messages 4 deep), the decision every rank's (the vote's x4 word), every field bitwise.  (With a
+    communicator a call runs pairs after a call of 2 or more steps has voted with the verdict known.)"""
+    bad, used, _ = _run_ranks(amd, name, nranks, calls)
     assert not bad, f"{name} over {nranks} ranks {calls}: fields differ from the reference: {bad}"
     assert all(any(u) for u in used) and all(u == used[0] for u in used), used
+
+
+@pytest.mark.parametrize("overlap", [1, 2])
+@pytest.mark.parametrize("name,nranks,calls", [("box2048_b2x2_s10", 4, [2, 8]), ("box4096_b4x2_s12", 8, [2, 10])])
+def test_x4_fullsize_ranks_match_reference(amd, name, nranks, calls, overlap):
+    """BASELINE configs 3 and 4 at full size, one block per loopback rank, exactly as a multi-GPU bench
+    run executes them: the warm-up call, then one long call of x4 pairs (every rank asserts it ran
+    them), complete(); overlap 2 = the inner pair beside the 4-deep exchange then the bands (the
+    default with peers), overlap 1 = exchange then the whole pair.  Every field of every block
+    bitwise against the reference's 4 / 8-block run (shared/mpp/syncborder_block2D_gen_all.fi:100-129,
+    core/kernel_interface.f90:105-117)."""
+    bad, used, _ = _run_ranks(amd, name, nranks, calls, overlap=overlap)
+    assert not bad, f"{name} over {nranks} ranks, overlap {overlap}: fields differ from the reference: {bad}"
+    assert all(all(u) for u in used), used
+
+
+@pytest.mark.parametrize("overlap", [1, 2])
+@pytest.mark.parametrize("name,calls", [("bs_b4x2_tr_s60", [2, 58]), ("bs_b4x2_tr_s604", [2, 602])])
+def test_x4_tracer_ranks_co_launch_match_reference(amd, name, calls, overlap):
+    """Config 5 (Black Sea + tracer, 8 blocks) over 8 loopback ranks with x4 pairs and the tracer steps:
+    the tracers exchanged 2 deep with the state, the pending tracer step co-launched with the pair
+    (overlap 2: in the bands' launch after the exchange; overlap 1: with the whole pair) -- every rank
+    ran the pairs and the co-launch, every field bitwise (control/tracer.f90:33-62,
+    interface/tracer/tracer_interface.f90:52-98)."""
+    bad, used, co = _run_ranks(amd, name, 8, calls, overlap=overlap, co=True)
+    assert not bad, f"{name} over 8 ranks, overlap {overlap}: fields differ from the reference: {bad}"
+    assert all(all(u) for u in used), used
+    assert all(co), co
 
 
 def test_x4_counts_blowup_like_single_launches(amd):

@@ -94,7 +94,7 @@ def build_oracle_model(case):
 
 
 @pytest.mark.parametrize("name", cases.E2E_CASES + cases.TRACER_E2E_CASES + cases.LONG_CASES + cases.INIT_CASES
-                         + cases.FULLSIZE_CASES + cases.TOPO_CASES)
+                         + cases.FULLSIZE_CASES + cases.TOPO_CASES + ["box2048_b2x2_s10"])
 def test_oracle_end_to_end_matches_reference(name):
     case = cases.load_e2e(name)
     z = case["z"]
