@@ -324,6 +324,13 @@ def rccl_report(rank_info, steps: int):
             "exposed_ms_per_step": round(max(r["exposed_ms_sum"] for r in rank_info) / steps, 4),
             "hidden_frac": round(1.0 - tot_e / tot_g, 4) if tot_g > 0 else None,
             "watchdog_s": r0["comm"]["watchdog_s"],
+            # the x2 / x4 steps' form: measured sequential vs overlapped step (or pair) times, the maxima
+            # over the ranks, and the level every rank then runs (ocn_ctx_overlap_info)
+            "overlap": ({"level": r0["overlap"]["level"], "decided": r0["overlap"]["state"] == 3,
+                         "measured_on": {2: "x2 step", 4: "x4 pair"}.get(r0["overlap"]["kind"]),
+                         "seq_ms": r0["overlap"]["seq_ms"], "overlapped_ms": r0["overlap"]["overlapped_ms"],
+                         "per_rank_level": [r["overlap"]["level"] for r in rank_info]}
+                        if r0.get("overlap") else None),
             "per_rank": [{"rank": r["rank"], "groups": r["groups"],
                           "group_ms_mean": round(r["group_ms_sum"] / r["timed_groups"], 4) if r["timed_groups"] else None,
                           "group_ms_max": round(r["group_ms_max"], 4),
@@ -444,6 +451,9 @@ def main():
     ap.add_argument("--no-lazy-tail", action="store_true",
                     help="every call forms its own tail (OCN_OPT_LAZY_TAIL off)")
     ap.add_argument("--n", type=int, default=4096, help="box interior size (N x N)")
+    ap.add_argument("--box", default=None,
+                    help="box interior WxH (overrides --n): e.g. 1024x2048, the per-GPU block of config 4 at 8 GPUs, "
+                         "timed as a lone block on one GPU")
     ap.add_argument("--basin", choices=["box", "bs", "bs_tr"], default="box",
                     help="box: the synthetic N x N box; bs / bs_tr: the reference's Black Sea basin (data/BS mask "
                          "and parameters, as stored in tests/golden), without / with the tracer (configs 1 and 5)")
@@ -513,7 +523,8 @@ def main():
             raise SystemExit("--blocks with several GPUs must give one block per GPU")
     n = args.n
     if args.basin == "box":
-        nxbox, nybox = (n, n) if args.scaling == "strong" else (n * bx, n * by)
+        nw, nh = (int(v) for v in args.box.lower().split("x")) if args.box else (n, n)
+        nxbox, nybox = (nw, nh) if args.scaling == "strong" else (nw * bx, nh * by)
         basin, sw = amd.BasinConfig(nx=nxbox + 4, ny=nybox + 4), amd.SWConfig()
         workload = f"{nxbox}x{nybox} box"
         if args.topography:   # float32 (nx-4, ny-4), Fortran order, as a basin.par topography file holds it
@@ -613,7 +624,8 @@ def main():
         ex, exp_ = stats.get("exchange", (0.0, 0, 0.0)), stats.get("exposed", (0.0, 0, 0.0))
         mine = {"rank": rank, "comm": ci, "groups": ci["exchanges"] - xchg0, "timed_groups": ex[1],
                 "group_ms_sum": ex[0], "group_ms_max": ex[2], "exposed_ms_sum": exp_[0], "exposed_n": exp_[1],
-                "stage_ms": {s: v[0] / v[1] for s, v in stats.items() if v[1]}, "cells": model.interior_cells}
+                "stage_ms": {s: v[0] / v[1] for s, v in stats.items() if v[1]}, "cells": model.interior_cells,
+                "overlap": model.overlap_info()}
         rank_info = [None] * world
         dist.all_gather_object(rank_info, mine)
 

@@ -37,7 +37,8 @@ module ocn_sw_c
                                      OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13,           &
                                      OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16,                    &
                                      OCN_OPT_TRACER_STEP = 17, OCN_OPT_MULTI_SPIN = 18, &
-                                     OCN_OPT_X4 = 19, OCN_OPT_CO_LAUNCH = 20
+                                     OCN_OPT_X4 = 19, OCN_OPT_CO_LAUNCH = 20, &
+                                     OCN_OPT_XCHG_DELAY = 21
     integer(c_int32_t), parameter :: OCN_HALO_LOCAL = 0, OCN_HALO_SEND = 1, OCN_HALO_RECV = 2
     integer, parameter :: OCN_UNIQUE_ID_BYTES = 128   ! sizeof(ncclUniqueId)
 
@@ -84,6 +85,12 @@ module ocn_sw_c
         integer(c_int32_t) :: transport, nccl_version, comm_size, comm_rank
         integer(c_int64_t) :: exchanges, exchanges_done
         real(c_double) :: watchdog_s
+    end type
+
+    ! the x2 / x4 steps' measured overlap choice (ocn_ctx_overlap_info)
+    type, bind(C) :: ocn_overlap_info
+        integer(c_int32_t) :: level, state, kind, pad
+        real(c_double) :: seq_ms, overlapped_ms
     end type
 
     interface
@@ -299,6 +306,11 @@ module ocn_sw_c
             import :: c_int, c_ptr, ocn_comm_info
             type(c_ptr), value :: ctx
             type(ocn_comm_info), intent(out) :: info
+        end function
+        integer(c_int) function ocn_ctx_overlap_info(ctx, info) bind(C, name='ocn_ctx_overlap_info')
+            import :: c_int, c_ptr, ocn_overlap_info
+            type(c_ptr), value :: ctx
+            type(ocn_overlap_info), intent(out) :: info
         end function
         integer(c_int) function ocn_ctx_set_watchdog(ctx, seconds) bind(C, name='ocn_ctx_set_watchdog')
             import :: c_int, c_double, c_ptr

@@ -275,6 +275,19 @@ typedef struct ocn_comm_info {
     double watchdog_s;
 } ocn_comm_info;
 int ocn_ctx_comm_info(ocn_ctx *ctx, ocn_comm_info *out);
+/* The x2 / x4 steps' overlap with OCN_OPT_OVERLAP auto (-1) and peers on other ranks: the first step
+ * of a sequence's kind (not the one that opens it) runs exchange-then-march, the next the inner part
+ * beside the exchange, each timed with events; the next vote max-reduces both times over the ranks
+ * and every rank keeps the faster form.  level = the OCN_OPT_OVERLAP level in effect; state 0 =
+ * nothing measured, 1 = the sequential step measured, 2 = both (not yet voted), 3 = decided; kind =
+ * the form measured (2: x2 steps, 4: x4 pairs); seq_ms / overlapped_ms = the times (after the
+ * decision: the maxima over the ranks it used).  The reference's hybrid overlap mode
+ * (core/kernel_interface.f90:105-117) has no such choice. */
+typedef struct ocn_overlap_info {
+    int32_t level, state, kind, pad;
+    double seq_ms, overlapped_ms;
+} ocn_overlap_info;
+int ocn_ctx_overlap_info(ocn_ctx *ctx, ocn_overlap_info *out);
 /* Host-side watchdog (seconds > 0; 0 = off): a thread of the context watches every call that may
  * take part in a collective (init_state, step, complete, synchronize, sync, stage, tracer_stage,
  * download, upload, output_r4).  One that has not returned after `seconds` is ended: the watchdog
@@ -411,9 +424,11 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  OCN_OPT_X4 (default 1): with halo exchanges, x2 steps run two per launch with ONE exchange of the
  *  state four points deep per two steps (the launch's first step also updates the two halo rings
  *  neighbour blocks own, as they do) -- the pair launch of single blocks (OCN_OPT_PAIR) for blocks with
- *  neighbours; the known-constant variant, no tracers, every block at least 4 x 4; two more halo rings
- *  outside the reference's arrays hold the exchanged state.  Same results bit for bit.
- *  ocn_ctx_get_option: 2 if the last ocn_ctx_step used such launches.
+ *  neighbours; the known-constant variant, every block at least 4 x 4; two more halo rings outside the
+ *  reference's arrays hold the exchanged state.  Tracer runs (tracer steps): the tracers exchanged two
+ *  deep, two tracer steps per exchange -- with 1 only where exchanges go to other ranks, with 3 always.
+ *  0 = off.  Same results bit for bit.  ocn_ctx_get_option: 2 if the last ocn_ctx_step used such
+ *  launches.
  *  OCN_OPT_CO_LAUNCH (default 1): tracer runs with x2 steps (one tracer, block batching on): each
  *  step's march -- with OCN_OPT_OVERLAP 2 the part after the exchange -- and the previous state's
  *  tracer step go as ONE launch (their workgroups in one grid) instead of two.  Same results bit for
@@ -422,6 +437,8 @@ int ocn_ctx_output_r4(ocn_ctx *ctx, int k, int field_id, float undef, float *hos
  *  barrier gives up after this many polls -- the launch's workgroups end and ocn_ctx_synchronize
  *  returns OCN_ERR_HIP instead of the device hanging if the grid was not co-resident.  Tests set it
  *  to 1 to exercise that path.
+ *  OCN_OPT_XCHG_DELAY (tests; default 0): microseconds the device waits before each exchange with
+ *  remote peers (a slow link, for the measured overlap choice: ocn_ctx_overlap_info).
  * ocn_ctx_get_option: current value; for OCN_OPT_COMPACT whether the last ocn_ctx_step used
  * the compact tables, for OCN_OPT_FLIP whether it used role-flip steps, for OCN_OPT_RECOMPUTE
  * whether it used recompute steps, for OCN_OPT_ONEPASS whether it used one-pass steps (2: with
@@ -434,7 +451,7 @@ enum { OCN_OPT_GRAPH = 1, OCN_OPT_OVERLAP = 2, OCN_OPT_STAGE_TIMING = 3, OCN_OPT
        OCN_OPT_MARCH = 6, OCN_OPT_FLIP = 7, OCN_OPT_RECOMPUTE = 8, OCN_OPT_ONEPASS = 9,
        OCN_OPT_KNOWN_CONSTANTS = 10, OCN_OPT_ONEPASS_LAST = 11, OCN_OPT_LAZY_TAIL = 12, OCN_OPT_X2 = 13,
        OCN_OPT_BATCH = 14, OCN_OPT_PAIR = 15, OCN_OPT_MULTI = 16, OCN_OPT_TRACER_STEP = 17,
-       OCN_OPT_MULTI_SPIN = 18, OCN_OPT_X4 = 19, OCN_OPT_CO_LAUNCH = 20 };
+       OCN_OPT_MULTI_SPIN = 18, OCN_OPT_X4 = 19, OCN_OPT_CO_LAUNCH = 20, OCN_OPT_XCHG_DELAY = 21 };
 
 /* Timer slots: the stage ids, then the fused groups (fused C2 is OCN_STAGE_HH_INIT), then the
  * three tracer stages (summed over tracers), then the role-flip steps' fused hh_init + next A,

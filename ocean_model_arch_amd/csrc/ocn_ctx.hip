@@ -309,6 +309,15 @@ struct ocn_ctx {
     int32_t *h_fbz = nullptr;
     bool fb_copy = false;
     int overlap = -1;            // OCN_OPT_OVERLAP: 0 none, 1 standard steps, 2 + role-flip steps, -1 auto
+    // OCN_OPT_OVERLAP auto with peers on other ranks: the x2 / x4 steps' form (inner part beside the
+    // exchange, or exchange then march) chosen from a measurement (ov_begin): ov_state 0 = nothing
+    // measured, 1 = a sequential step's events recorded, 2 = an overlapped one's too (the next vote
+    // reduces them), 3 = decided (ov_level); ov_kind = the step form measured (2: x2 steps, 4: x4 pairs);
+    // ov_ms = the two step times (this rank's, then the maxima over the ranks the decision used)
+    int ov_state = 0, ov_kind = 0, ov_level = 2;
+    hipEvent_t ov_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    double ov_ms[2] = {0.0, 0.0};
+    int xdelay_us = 0;           // OCN_OPT_XCHG_DELAY (tests): a device wait before each exchange with remote peers
     int32_t *d_nbad = nullptr;
     unsigned *d_bar = nullptr;   // the multi-step launch's grid-barrier words (kMultiBarBytes)
     ncclComm_t comm = nullptr;
@@ -422,7 +431,9 @@ struct ocn_ctx {
     // one_step_x4 (OCN_OPT_X4): pairs of x2 steps with one 4-deep exchange each; x4_tab_ok: its tables
     // were built from init_state's real(4) fields with every divisor in udiv's range; x4_dev_ok: the
     // last vote found every rank able to run them (a communicator attached); x4_used: the last call did
-    bool x4 = true, x4_tab_ok = false, x4_dev_ok = false, x4_used = false;
+    // x4: 0 off, 1 auto (tracer runs: only with peers on other ranks), 3 always
+    int x4 = 1;
+    bool x4_tab_ok = false, x4_dev_ok = false, x4_used = false;
     bool fb_x2 = false;          // the known-constant check's verdict is for the x2 range / tables
     mutable bool coherent_known = false, r8_escaped = false;
     int multi_spin = kMultiSpin;   // OCN_OPT_MULTI_SPIN (the multi-step launch's barrier bound)
@@ -991,7 +1002,42 @@ static int comm_gone(const ocn_ctx *c)
 // cost as much as the copies they hide (HISTORY.md section 5)
 static int overlap_level(const ocn_ctx *c)
 {
-    return c->overlap >= 0 ? c->overlap : has_comm(c) && c->dec.nranks > 1 ? 2 : 1;
+    if (c->overlap >= 0) return c->overlap;
+    if (!(has_comm(c) && c->dec.nranks > 1)) return 1;
+    return c->ov_state == 3 ? c->ov_level : 2;   // (measured: ov_begin, check_coherence)
+}
+
+// The form of an x2 step (kind 2) or an x4 pair (kind 4) under OCN_OPT_OVERLAP auto with peers on
+// other ranks.  Until the vote has decided, the first such step (not one that opens a sequence: its
+// ring save would be timed too) runs in sequence and the next of the same kind overlapped, each
+// between two events on the context stream (probe 1 / 2: ov_mark at its start and end); the next
+// check_coherence max-reduces both times over the ranks and keeps the faster form (ov_level) --
+// every rank the same.  Either form runs the same exchange (one group per step or pair), so ranks
+// may differ in form meanwhile; the results are the same bit for bit.
+static int ov_begin(ocn_ctx *c, int kind, bool allow, int &probe)
+{
+    probe = 0;
+    const int lv = overlap_level(c);
+    if (c->overlap >= 0 || !(has_comm(c) && c->dec.nranks > 1) || c->capturing || !allow || c->ov_state >= 2)
+        return lv;
+    for (hipEvent_t &e : c->ov_ev)
+        if (!e && hipEventCreate(&e) != hipSuccess) return lv;
+    if (c->ov_state == 0 || c->ov_kind != kind) {
+        c->ov_state = 0;
+        c->ov_kind = kind;
+        probe = 1;
+        return 1;
+    }
+    probe = 2;
+    return 2;
+}
+// probe's start (end = false) or end event on the context stream; the end advances ov_state
+static int ov_mark(ocn_ctx *c, int probe, bool end)
+{
+    if (!probe) return OCN_OK;
+    HIPCHK(hipEventRecord(c->ov_ev[2 * (probe - 1) + (end ? 1 : 0)], c->stream));
+    if (end) c->ov_state = probe;
+    return OCN_OK;
 }
 
 // a rank of a loopback group that fails releases its peers' waits at once
@@ -1284,6 +1330,22 @@ static int exchange_done(ocn_ctx *c, ocn_ctx::Rec &xrec, hipStream_t stream)
 
 // cmp != nullptr: compare the halos with what the exchange would deliver instead of writing them
 // (ORs 1 into *cmp where they differ); same messages, so every rank must take part.
+// OCN_OPT_XCHG_DELAY (tests): one wave waits c->xdelay_us on the device clock (a slow link's latency,
+// in front of an exchange with remote peers); the loop always ends
+__global__ void k_delay(unsigned long long ticks)
+{
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+static int launch_delay(ocn_ctx *c, hipStream_t s)
+{
+    int khz = 0;
+    HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dec.device));
+    const unsigned long long ticks = (unsigned long long)c->xdelay_us * (unsigned long long)(khz > 0 ? khz : 100000) / 1000ull;
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, ticks);
+    return check_launch();
+}
+
 static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stream = nullptr, int32_t *cmp = nullptr,
                     int depth = 1, int priv = 0)
 {
@@ -1301,6 +1363,7 @@ static int run_sync(ocn_ctx *c, const std::vector<int> &fields, hipStream_t stre
             HIPCHK(hipEventRecord(xrec.a, stream));
         }
         ++c->xchg;
+        if (c->xdelay_us > 0) RC(launch_delay(c, stream));
         RC(launch_segs(p->pack, stream));
         if (c->lb) {
             RC(lb_exchange(c, p, stream));
@@ -1700,7 +1763,10 @@ static bool is_flip_field(int id)
 // one-pass / hybrid decisions, so the exchange sequences of all ranks match.
 // kVoteX4: this rank cannot run one_step_x4's pairs (its tables, or the known-constant verdict its host
 // has read for the x2 range) -- every rank then runs the same steps and exchanges
-enum { kVoteIncoherent = 0, kVoteIneligible, kVoteUdiv, kVoteHhStale, kVoteX2, kVoteX4, kVoteUsed };
+// kVoteOvSeq / kVoteOvOv: the measured sequential / overlapped step times in us (ov_begin; INT32_MAX
+// from a rank that has not measured both: no decision)
+enum { kVoteIncoherent = 0, kVoteIneligible, kVoteUdiv, kVoteHhStale, kVoteX2, kVoteX4, kVoteOvSeq, kVoteOvOv,
+       kVoteUsed };
 static_assert(kVoteUsed <= kVoteWords, "vote words");
 struct VoteIn { bool eligible, udiv_ok, hh_consistent, x2_ok, x4_ok; };
 struct VoteOut { bool udiv_ok, hh_consistent, x2_ok, x4_ok; };
@@ -1768,6 +1834,17 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
     host[kVoteHhStale] = !in.hh_consistent;
     host[kVoteX2] = !in.x2_ok;
     host[kVoteX4] = !in.x4_ok;
+    host[kVoteOvSeq] = host[kVoteOvOv] = INT32_MAX;
+    if (c->ov_state == 2) {   // both probe steps recorded (ov_begin): their times, in us
+        float ms[2] = {0.f, 0.f};
+        HIPCHK(hipEventSynchronize(c->ov_ev[3]));
+        HIPCHK(hipEventElapsedTime(&ms[0], c->ov_ev[0], c->ov_ev[1]));
+        HIPCHK(hipEventElapsedTime(&ms[1], c->ov_ev[2], c->ov_ev[3]));
+        for (int i = 0; i < 2; ++i) {
+            c->ov_ms[i] = ms[i];
+            host[kVoteOvSeq + i] = (int32_t)std::min(1.0e9, std::max(1.0, std::round(1000.0 * ms[i])));
+        }
+    }
     HIPCHK(hipMemcpyAsync(c->d_flags, host, sizeof(host), hipMemcpyHostToDevice, c->stream));
     if (in.eligible)
         RC(each_block(c, c->stream, [&](const LBlock &b) { return launch_coherence(&b.g, b.ptr.data(), b.bits, c->d_flags, c->stream); }));
@@ -1796,6 +1873,14 @@ static int check_coherence(ocn_ctx *c, const VoteIn &in, VoteOut &out)
     out.x2_ok = w[kVoteX2] == 0 && exch && c->x2;
     c->x2_dev_ok = out.x2_ok;
     out.x4_ok = out.x2_ok && w[kVoteX4] == 0;
+    if (w[kVoteOvSeq] != INT32_MAX && w[kVoteOvOv] != INT32_MAX) {   // every rank measured: the faster form
+        c->ov_ms[0] = 1.0e-3 * w[kVoteOvSeq];
+        c->ov_ms[1] = 1.0e-3 * w[kVoteOvOv];
+        c->ov_level = w[kVoteOvOv] < w[kVoteOvSeq] ? 2 : 1;
+        c->ov_state = 3;
+    } else if (c->ov_state == 2) {   // another rank has not: measure again, together
+        c->ov_state = 0;
+    }
     c->x4_dev_ok = out.x4_ok;
     return OCN_OK;
 }
@@ -2181,7 +2266,10 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
         swap_tracer_roles(c);
         swap_tracer_alt(c);
     };
-    if (overlap_level(c) >= 2 && !c->capturing) {
+    int probe = 0;
+    const int lv = ov_begin(c, 2, !k.x2_save, probe);
+    RC(ov_mark(c, probe, false));
+    if (lv >= 2 && !c->capturing) {
         HIPCHK(hipEventRecord(c->ev_fork, s));
         RC(timer_begin(c, OCN_TIMER_ONEPASS, rec));
         RC(each_block(c, s, [&](const LBlock &b) -> int {
@@ -2237,6 +2325,7 @@ static int one_step_x2(ocn_ctx *c, double tau, const StepKind &k)
         }
         RC(timer_end(c, rec));
     }
+    RC(ov_mark(c, probe, true));
     // the previous state's tracer step: it reads that state (untouched by the march) and the tracers
     // with their first halo ring, both just exchanged
     RC(run_tracer_step(c, tau));
@@ -2356,7 +2445,10 @@ static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
         const Range in = x4_inner(b);
         inner_ok = inner_ok && in.m0 <= in.m1 && in.n0 <= in.n1;
     }
-    if (overlap_level(c) >= 2 && !c->capturing && inner_ok) {
+    int probe = 0;
+    const int lv = ov_begin(c, 4, !k.x2_save && inner_ok, probe);
+    RC(ov_mark(c, probe, false));
+    if (lv >= 2 && !c->capturing && inner_ok) {
         HIPCHK(hipEventRecord(c->ev_fork, s));
         RC(timer_begin(c, OCN_TIMER_ONEPASS2, rec));
         RC(each_block(c, s, [&](const LBlock &b) -> int {
@@ -2394,6 +2486,7 @@ static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
         }, co));
         RC(timer_end(c, rec));
     }
+    RC(ov_mark(c, probe, true));
     if (trA) {   // tracer step A (here when not co-launched: after the join, it reads the exchanged halos)
         c->tr_pending = false;
         for (int t = co ? 2 : 1; t <= c->sw.tracer_num; ++t)
@@ -3070,6 +3163,8 @@ int ocn_ctx_destroy(ocn_ctx *c)
     for (void *p : c->allocs) (void)hipFree(p);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    for (hipEvent_t e : c->ov_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->ev_fb) (void)hipEventDestroy(c->ev_fb);
     if (c->h_fbz) (void)hipHostFree(c->h_fbz);
@@ -3163,6 +3258,18 @@ int ocn_ctx_attach_loopback(ocn_ctx *const *ctxs, int32_t n)
     }
     if (rc) { delete L; return rc; }
     for (int i = 0; i < n; ++i) ctxs[i]->lb = L;
+    return OCN_OK;
+}
+
+int ocn_ctx_overlap_info(ocn_ctx *c, ocn_overlap_info *out)
+{
+    if (!c || !out) return set_error(OCN_ERR_ARG, "null argument");
+    *out = ocn_overlap_info{};
+    out->level = overlap_level(c);
+    out->state = c->ov_state;
+    out->kind = c->ov_kind;
+    out->seq_ms = c->ov_ms[0];
+    out->overlapped_ms = c->ov_ms[1];
     return OCN_OK;
 }
 
@@ -3503,10 +3610,14 @@ static bool x2_local(const ocn_ctx *c)
 // 4-deep strips lie in its interior) and row padding for the extra rings
 static bool x4_local(const ocn_ctx *c)
 {
-    // (tracer runs: with the tracer steps, one_step_x4 runs them)
+    // (tracer runs: with the tracer steps, one_step_x4 runs them -- by default only where exchanges go to
+    // other ranks: a pair's second tracer step is one more launch after it, which with only local copies
+    // costs more than the exchange it saves -- C5 layout on one GPU 0.0281 (x2) vs 0.0338 ms per step,
+    // profiles/r06a; over RCCL each exchange is a group's latency)
     if (!c->x4 || !c->x4_tab_ok || !c->known_const || c->r8_handed || (c->sw.use_tracers > 0 && !c->tr_step) ||
         !c->march)
         return false;
+    if (c->sw.use_tracers > 0 && c->x4 < 3 && !(has_comm(c) && c->dec.nranks > 1)) return false;
     for (const GBlock &g : c->gblocks)
         if (g.rank >= 0 && (g.g.nx_end - g.g.nx_start < 3 || g.g.ny_end - g.g.ny_start < 3)) return false;
     for (const LBlock &b : c->blocks)
@@ -4015,7 +4126,9 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
     case OCN_OPT_OVERLAP:
         if (c->overlap != value) drop_graphs(c);
         c->overlap = value < 0 ? -1 : value > 2 ? 2 : (int)value;
+        if (c->overlap < 0) c->ov_state = 0;   // (auto again: measured again)
         return OCN_OK;
+    case OCN_OPT_XCHG_DELAY: c->xdelay_us = value < 0 ? 0 : value > 1000000 ? 1000000 : (int)value; return OCN_OK;
     case OCN_OPT_MARCH:
         if (c->march != (value != 0)) drop_graphs(c);
         c->march = value != 0;
@@ -4036,7 +4149,7 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         c->coherent_known = false;
         return OCN_OK;
     case OCN_OPT_MULTI_SPIN: c->multi_spin = value < 1 ? 1 : value > kMultiSpin ? kMultiSpin : (int)value; return OCN_OK;
-    case OCN_OPT_X4: c->x4 = value != 0; c->coherent_known = false; return OCN_OK;
+    case OCN_OPT_X4: c->x4 = value <= 0 ? 0 : value >= 3 ? 3 : 1; c->coherent_known = false; return OCN_OK;
     case OCN_OPT_CO_LAUNCH: c->co_launch = value != 0; return OCN_OK;
     case OCN_OPT_BATCH:
         if (c->batch != (value != 0)) drop_graphs(c);
@@ -4080,8 +4193,9 @@ int ocn_ctx_get_option(const ocn_ctx *c, int32_t key, int64_t *value)
     case OCN_OPT_MULTI: *value = c->multi_used ? 2 : c->multi; return OCN_OK;
     case OCN_OPT_TRACER_STEP: *value = c->tr_call ? 2 : c->tr_step; return OCN_OK;
     case OCN_OPT_MULTI_SPIN: *value = c->multi_spin; return OCN_OK;
-    case OCN_OPT_X4: *value = c->x4_used ? 2 : c->x4; return OCN_OK;
+    case OCN_OPT_X4: *value = c->x4_used ? 2 : c->x4 ? 1 : 0; return OCN_OK;
     case OCN_OPT_CO_LAUNCH: *value = c->co_used ? 2 : c->co_launch; return OCN_OK;
+    case OCN_OPT_XCHG_DELAY: *value = c->xdelay_us; return OCN_OK;
     default: return set_error(OCN_ERR_ARG, "unknown option");
     }
 }

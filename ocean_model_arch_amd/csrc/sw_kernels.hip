@@ -1637,10 +1637,20 @@ template <bool HH, bool SKIP> struct MarchCA {
 // the current row is computed.
 // x of lane + dx (dx in {-1, 0, 1}); 0 in the lane without a source (bound_ctrl): the one-pass
 // march reads such values only in its halo lanes, so no old value needs to be kept
+#ifndef OCN_SHIFT_BPERM
+#define OCN_SHIFT_BPERM 0
+#endif
 __device__ __forceinline__ int dpp_shz(int x, int dx)
 {
+#if OCN_SHIFT_BPERM
+    // (the LDS crossbar instead of a VALU move: the lane without a source gets lane (l + dx) mod 64's
+    // value, which -- like bound_ctrl's 0 -- only halo lanes read)
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    return __builtin_amdgcn_ds_bpermute((lane + dx) << 2, x);
+#else
     if (dx > 0) return __builtin_amdgcn_mov_dpp(x, 0x130, 0xf, 0xf, true);   // wave_shl:1
     return __builtin_amdgcn_mov_dpp(x, 0x138, 0xf, 0xf, true);               // wave_shr:1
+#endif
 }
 __device__ __forceinline__ double shz(double x, int dx)
 {

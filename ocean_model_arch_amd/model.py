@@ -173,6 +173,21 @@ class OceanModel:
                 "exchanges": int(i.exchanges), "exchanges_done": int(i.exchanges_done),
                 "watchdog_s": float(i.watchdog_s)}
 
+    def overlap_info(self) -> dict:
+        """ocn_ctx_overlap_info: the overlap level in effect and, with OCN_OPT_OVERLAP auto and peers on
+        other ranks, the measured choice (state 3 = decided; seq_ms / overlapped_ms = the two step times
+        the vote compared, maxima over the ranks)."""
+        i = _lib.OcnOverlapInfo()
+        check(lib().ocn_ctx_overlap_info(self.ctx, C.byref(i)), "ocn_ctx_overlap_info")
+        return {"level": int(i.level), "state": int(i.state), "kind": int(i.kind),
+                "seq_ms": round(float(i.seq_ms), 4), "overlapped_ms": round(float(i.overlapped_ms), 4)}
+
+    def set_exchange_delay(self, us: int):
+        """Tests: the device waits `us` microseconds before each exchange with remote peers
+        (OCN_OPT_XCHG_DELAY: a slow link)."""
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_XCHG_DELAY, int(us)), "ocn_ctx_set_option")
+        return self
+
     def set_fused(self, on: bool = True):
         """Fused step groups (default) or the reference's 11 envoke stages; same results bit for bit."""
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_FUSED, int(on)), "ocn_ctx_set_option")
@@ -259,10 +274,12 @@ class OceanModel:
         check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_MULTI, int(on)), "ocn_ctx_set_option")
         return self
 
-    def set_x4(self, on: bool = True):
+    def set_x4(self, on=True):
         """Blocks with halo exchanges: two x2 steps per launch with one 4-deep state exchange per two
-        steps (default on, OCN_OPT_X4); same results bit for bit."""
-        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_X4, int(on)), "ocn_ctx_set_option")
+        steps (OCN_OPT_X4: True / 1 = auto, the default -- tracer runs only with peers on other ranks;
+        3 = always; False / 0 = off); same results bit for bit."""
+        mode = 3 if on == 3 else int(bool(on))
+        check(lib().ocn_ctx_set_option(self.ctx, _lib.OPT_X4, mode), "ocn_ctx_set_option")
         return self
 
     @property

@@ -19,11 +19,15 @@
 
 constexpr int ITER = 4096;
 
-enum Op { MUL64, ADD64, FMA64, DPP, CND, CMP64, ADDU32, FREXP, MIX_5F_3D, MIX_5F_3I, MIX_2F_2D, MIX_PAIR, kOps };
+enum Op { MUL64, ADD64, FMA64, DPP, CND, CMP64, ADDU32, FREXP, MIX_5F_3D, MIX_5F_3I, MIX_2F_2D, MIX_PAIR, CND_S,
+          CMP_CND, ADD64_S, BFE, kOps };
 static const char *kName[kOps] = {"v_mul_f64", "v_add_f64", "v_fma_f64", "v_mov_b32 dpp wave_shl:1", "v_cndmask_b32",
                                   "v_cmp_lt_f64", "v_add_u32", "v_frexp_exp_i32_f64",
                                   "mix 10 f64 mul + 6 dpp", "mix 10 f64 mul + 6 add_u32", "mix 8 f64 mul + 8 dpp",
-                                  "mix 10 f64 (mul/add/fma) + 2 dpp + 2 cnd + 2 u32"};
+                                  "mix 10 f64 (mul/add/fma) + 2 dpp + 2 cnd + 2 u32",
+                                  "v_cndmask_b32_e64 (SGPR-pair condition)",
+                                  "v_cmp_lt_f64 s[] + 2 v_cndmask_b32_e64 (f64 select)", "v_add_f64 (SGPR operand)",
+                                  "v_bfe_u32"};
 // instructions per block of each op (16 everywhere)
 constexpr int kPerBlock = 16;
 
@@ -35,6 +39,9 @@ __global__ __launch_bounds__(256) void k_issue(double seed, unsigned long long *
     const double k = 1.0000001, c = 0.999999;
     unsigned u0 = threadIdx.x, u1 = u0 * 3, u2 = u0 + 7, u3 = u0 ^ 5, u4 = u0 + 1, u5 = u0 * 5, u6 = u0 + 9, u7 = u0 ^ 3;
     unsigned s0 = u0 + 11, s1 = u0 + 13;   // DPP sources: not written inside the loop (no DPP read hazard)
+    const unsigned long long smask = __builtin_amdgcn_ballot_w64((threadIdx.x & 1) != 0);
+    unsigned long long sc0 = 0, sc1 = 0;
+    const double ks = seed;
     __syncthreads();
     const unsigned long long t0 = clock64(), w0 = wall_clock64();
     for (int it = 0; it < ITER; ++it) {
@@ -141,6 +148,38 @@ __global__ __launch_bounds__(256) void k_issue(double seed, unsigned long long *
                          : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7)
                          : "v"(k), "v"(c), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4), "v"(s0), "v"(s1) : "vcc");
         }
+        if constexpr (OP == CND_S) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                asm volatile("v_cndmask_b32_e64 %0, %0, %8, %9\n v_cndmask_b32_e64 %1, %1, %8, %9\n"
+                             " v_cndmask_b32_e64 %2, %2, %8, %9\n v_cndmask_b32_e64 %3, %3, %8, %9\n"
+                             " v_cndmask_b32_e64 %4, %4, %8, %9\n v_cndmask_b32_e64 %5, %5, %8, %9\n"
+                             " v_cndmask_b32_e64 %6, %6, %8, %9\n v_cndmask_b32_e64 %7, %7, %8, %9"
+                             : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "+v"(u4), "+v"(u5), "+v"(u6), "+v"(u7)
+                             : "v"(s0), "s"(smask));
+        } else if constexpr (OP == CMP_CND) {   // 4 x (compare into an SGPR pair, select both halves of an f64)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                asm volatile("v_cmp_lt_f64_e64 %8, %0, %10\n v_cndmask_b32_e64 %4, %4, %11, %8\n v_cndmask_b32_e64 %5, %5, %11, %8\n"
+                             " v_cmp_lt_f64_e64 %9, %1, %10\n v_cndmask_b32_e64 %6, %6, %11, %9\n v_cndmask_b32_e64 %7, %7, %11, %9\n"
+                             " v_mul_f64 %2, %2, %10\n v_mul_f64 %3, %3, %10"
+                             : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3),
+                               "=&s"(sc0), "=&s"(sc1)
+                             : "v"(k), "v"(s0));
+        } else if constexpr (OP == ADD64_S) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                asm volatile("v_add_f64 %0, %0, %8\n v_add_f64 %1, %1, %8\n v_add_f64 %2, %2, %8\n v_add_f64 %3, %3, %8\n"
+                             " v_add_f64 %4, %4, %8\n v_add_f64 %5, %5, %8\n v_add_f64 %6, %6, %8\n v_add_f64 %7, %7, %8"
+                             : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7) : "s"(ks));
+        } else if constexpr (OP == BFE) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                asm volatile("v_bfe_u32 %0, %8, 3, 1\n v_bfe_u32 %1, %8, 4, 1\n v_bfe_u32 %2, %8, 5, 1\n v_bfe_u32 %3, %8, 6, 1\n"
+                             " v_bfe_u32 %4, %9, 3, 1\n v_bfe_u32 %5, %9, 4, 1\n v_bfe_u32 %6, %9, 5, 1\n v_bfe_u32 %7, %9, 6, 1"
+                             : "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3), "=&v"(u4), "=&v"(u5), "=&v"(u6), "=&v"(u7)
+                             : "v"(s0), "v"(s1));
+        }
     }
     const unsigned long long t1 = clock64(), w1 = wall_clock64();
     if ((threadIdx.x & 63) == 0) {
@@ -148,7 +187,8 @@ __global__ __launch_bounds__(256) void k_issue(double seed, unsigned long long *
         cyc[wv] = t1 - t0;
         rt[wv] = w1 - w0;
     }
-    const double s = d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7 + (double)(u0 + u1 + u2 + u3 + u4 + u5 + u6 + u7);
+    const double s = d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7 + (double)(u0 + u1 + u2 + u3 + u4 + u5 + u6 + u7) +
+                     (double)(sc0 ^ sc1);
     if (s == 12345.678) sink[threadIdx.x] = s;   // (never true: keeps the chains live)
 }
 
@@ -217,6 +257,10 @@ int main()
     rc |= run_all<MIX_5F_3I>(cyc, rt, sink, hc, hr, ncu);
     rc |= run_all<MIX_2F_2D>(cyc, rt, sink, hc, hr, ncu);
     rc |= run_all<MIX_PAIR>(cyc, rt, sink, hc, hr, ncu);
+    rc |= run_all<CND_S>(cyc, rt, sink, hc, hr, ncu);
+    rc |= run_all<CMP_CND>(cyc, rt, sink, hc, hr, ncu);
+    rc |= run_all<ADD64_S>(cyc, rt, sink, hc, hr, ncu);
+    rc |= run_all<BFE>(cyc, rt, sink, hc, hr, ncu);
     CHK(hipDeviceSynchronize());
     return rc;
 }

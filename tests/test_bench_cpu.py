@@ -159,3 +159,8 @@ def test_rccl_report_from_rank_records():
     assert r["groups_per_step"] == 1.1 and r["group_ms"] == {"mean": 0.025, "max": 0.08}
     assert r["exposed_ms_per_step"] == 0.0033 and r["hidden_frac"] == 0.9
     assert [p["groups"] for p in r["per_rank"]] == [22, 22]
+    assert r["overlap"] is None
+    ov = {"level": 1, "state": 3, "kind": 2, "seq_ms": 0.11, "overlapped_ms": 0.12}
+    r = bench.rccl_report([dict(q, overlap=ov) for q in recs], 20)
+    assert r["overlap"] == {"level": 1, "decided": True, "measured_on": "x2 step", "seq_ms": 0.11,
+                            "overlapped_ms": 0.12, "per_rank_level": [1, 1]}

@@ -433,11 +433,11 @@ def _random_sequence(amd, layout, seed, ops, need_path, nops=20):
             elif op == "opt":
                 which = str(rng.choice(["onepass", "pair", "multi", "tracer_step", "lazy_tail", "flip", "x4",
                                         "co_launch"]))
-                val = int(rng.integers(0, 3 if which == "pair" else 2))
+                val = int(rng.integers(0, 3 if which in ("pair", "x4") else 2))
                 {"onepass": m.set_onepass, "multi": m.set_multi, "tracer_step": m.set_tracer_step,
                  "lazy_tail": m.set_lazy_tail, "flip": m.set_flip, "x4": m.set_x4,
                  "co_launch": m.set_co_launch}.get(which, lambda v: m.set_pair(int(v)))(
-                    val if which == "pair" else bool(val))
+                    val if which == "pair" else 3 if (which == "x4" and val == 2) else bool(val))
                 log[-1] += f"-{which}{val}"
             elif op == "graph":
                 on = bool(rng.integers(0, 2))

@@ -74,9 +74,16 @@ def test_x4_tracer_blocks_match_reference(amd, name, calls, overlap):
     with the pair), the pair's producers write the first step's state for the second tracer step --
     two SW steps and two tracer steps per exchange, every field bitwise (control/tracer.f90:33-62 after
     each step, leapfrog_tracer.f90:13-170)."""
-    bad, used = _run_blocks(amd, name, calls, overlap=overlap)
+    bad, used = _run_blocks(amd, name, calls, x4=3, overlap=overlap)
     assert not bad, f"{name} {calls}: fields differ from the reference: {bad}"
     assert any(used), used
+
+
+def test_x4_tracer_runs_in_one_process_default_to_x2(amd):
+    """OCN_OPT_X4 auto (1): a tracer run whose exchanges are all local copies keeps the x2 steps (the
+    pair's second tracer step costs a launch more than the exchange it saves), bitwise."""
+    bad, used = _run_blocks(amd, "box70x54_b3x2_tr_s20", [2, 18])
+    assert not bad and not any(used), (bad, used)
 
 
 def test_x4_off_is_the_x2_path(amd):
@@ -185,3 +192,44 @@ def test_x4_counts_blowup_like_single_launches(amd):
         m.close()
         assert used == x4
     assert msgs[0] == msgs[1], msgs
+
+
+@pytest.mark.parametrize("delay_us", [0, 600])
+def test_overlap_choice_is_measured_and_voted(amd, delay_us):
+    """OCN_OPT_OVERLAP auto with peers on other ranks (ocn_ctx.hip ov_begin): one x2 step in sequence
+    and the next overlapped, each timed; the next call's vote max-reduces both times and every rank
+    keeps the faster form.  With an injected 600 us wait before each exchange (a slow link) hiding
+    it behind the inner march wins, level 2 on every rank; either way every field bitwise against the
+    reference's 4-block run (core/kernel_interface.f90:105-117 is the reference's own overlap mode)."""
+    name, calls = "box2048_b2x2_s10", [4, 2, 4]
+    case = cases.load_e2e(name)
+    models = [build_model(amd, case, rank=r, nranks=4) for r in range(4)]
+    for m in models:
+        m.set_exchange_delay(delay_us)
+    amd.OceanModel.attach_loopback(models)
+
+    def body(m):
+        m.init()
+        infos = []
+        for n in calls:
+            m.step(n, tau=1.0, check_every=1)
+            infos.append(m.overlap_info())
+        m.complete()
+        m.synchronize()
+        return infos
+
+    try:
+        infos = amd.run_ranks(models, body)
+        bad = []
+        for m in models:
+            bad += compare_case(m, case, name, whole=False)
+    finally:
+        for m in models:
+            m.close()
+    assert not bad, f"{name} delay {delay_us}: fields differ from the reference: {bad}"
+    last = [i[-1] for i in infos]
+    print("overlap", delay_us, last)
+    assert all(i["state"] == 3 for i in last), last
+    assert len({i["level"] for i in last}) == 1 and len({(i["seq_ms"], i["overlapped_ms"]) for i in last}) == 1, last
+    if delay_us:
+        assert last[0]["level"] == 2 and last[0]["seq_ms"] > delay_us * 1e-3, last
