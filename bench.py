@@ -400,6 +400,12 @@ def load_valu(amd, stage: str, launch_ms: float, box, blocks):
                                  "wait_inst_any": round(pw["SQ_WAIT_INST_ANY"] / wc, 4),
                                  "wait_any": round(pw["SQ_WAIT_ANY"] / wc, 4)},
                "source": "profiles/sq_valu.json",
+               # the 4 cycles per wave64 VALU instruction the floor charges, measured per class at 2 waves
+               # per SIMD (scripts/issuebench.hip, profiles/r06/issuebench.txt; event-timed, launch
+               # overhead included): f64 mul / add / fma 4.48-4.54, DPP lane move 4.45, v_frexp 4.40,
+               # v_cndmask (SGPR condition) 4.54, int32 alone 2.58 but 3.9 interleaved with f64 (the
+               # 10 f64 + 6 int32 mix: 4.29 per instruction) -- the pair launch's mix issues at ~4
+               "issue_cost": {"cycles_per_inst": 4.0, "source": "profiles/r06/issuebench.txt"},
                "profile_match": match if match == "build" else
                f"{match}: profiled on build {d.get('build_id')}, the kernel's machine code unchanged"}
         clk = d["kernels"][stage].get("clock")

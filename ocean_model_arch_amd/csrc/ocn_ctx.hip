@@ -642,8 +642,15 @@ static int allocate_x2(ocn_ctx *c, LBlock &b)
     c->allocs.push_back(b.ext);
     HIPCHK(hipMalloc(&b.rows_x, nrow * sizeof(float)));
     c->allocs.push_back(b.rows_x);
-    HIPCHK(hipMalloc(&b.hr_x, (size_t)b.g.pitch * h * sizeof(double)));
-    c->allocs.push_back(b.hr_x);
+    {   // based like the real(8) fields (kXRing more rows each side): x4 pairs of the h_r-read variant
+        // read it 4 rings deep
+        char *d = nullptr;
+        const size_t nb = sizeof(double) * (size_t)(b.g.pitch * (h + 2 * kXRing)) + 512;
+        HIPCHK(hipMalloc(&d, nb));
+        c->allocs.push_back(d);
+        HIPCHK(hipMemsetAsync(d, 0, nb, c->stream));   // (rings no exchange fills: +0.0)
+        b.hr_x = (double *)(d + 256) + (long)kXRing * b.g.pitch;
+    }
     const long per = 2L * w + 2L * (h - 2);   // rows bnd_y1, bnd_y2; columns bnd_x1, bnd_x2 between them
     // the state's six groups, then two per tracer (ff1 / ff1n, ff1p / its second buffer: x4 pairs
     // exchange the tracers 2 deep)
@@ -2178,7 +2185,10 @@ static int x2_end(ocn_ctx *c, hipStream_t s)
     return run_sync(c, with_tracers(c, kStateX2), s);
 }
 
-// hr_x = h_r with the neighbours' second ring (the general variant of one_step_x2 reads it there)
+// hr_x = h_r with the neighbours' second ring (the general variant of one_step_x2 reads it there) --
+// four rings deep where x4 pairs may run (their h_r-read variant reads it on the block widened by
+// kXRing rings, as the neighbours' own h_r); x4_tables: x4 pairs may run (their tables and the option)
+static bool x4_tables(const ocn_ctx *c) { return c->x4 && c->x4_tab_ok; }
 static int refresh_hrx(ocn_ctx *c)
 {
     for (const LBlock &b : c->blocks)
@@ -2192,7 +2202,7 @@ static int refresh_hrx(ocn_ctx *c)
         }
     };
     swap_hr();
-    const int rc = run_sync(c, {OCN_HHQ_REST}, c->stream, nullptr, 2, 1);
+    const int rc = run_sync(c, {OCN_HHQ_REST}, c->stream, nullptr, x4_tables(c) ? 4 : 2, 1);
     swap_hr();
     RC(rc);
     c->hrx_ok = true;
@@ -2432,6 +2442,7 @@ static int one_step_x4(ocn_ctx *c, double tau, const StepKind &k)
         const long sh = (long)kXRing * b.g.pitch + kXRing;
         std::vector<void *> tab(b.ptr.size(), nullptr);
         for (int id = OCN_SSH; id < OCN_SSH + num_r8(c); ++id) tab[field_slot(id)] = b.f<double>(id) - sh;
+        tab[field_slot(OCN_HHQ_REST)] = b.hr_x - sh;   // (the h_r-read variant: h_r with the neighbours' 4 rings)
         const Compact t{b.bits_x4, b.rows_x4, c->march};
         double *trs_x[4];
         for (int i = 0; i < 4; ++i) trs_x[i] = b.trs[i] ? b.trs[i] - sh : nullptr;
@@ -3628,7 +3639,8 @@ static bool x4_local(const ocn_ctx *c)
 // (one process), the known-constant variant chosen on the host
 static bool x4_now(const ocn_ctx *c)
 {
-    return c->kc_mode == OCN_KC_KNOWN && (has_comm(c) ? c->x4_dev_ok : x4_local(c) && c->fb_x2);
+    return (c->kc_mode == OCN_KC_KNOWN || c->kc_mode == OCN_KC_KNOWN_HR) &&
+           (has_comm(c) ? c->x4_dev_ok : x4_local(c) && c->fb_x2);
 }
 
 // The pending tail of an open sequence: the last step run (a one-pass step) is run again from the
@@ -3767,7 +3779,7 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
     const bool x2_here = x2_local(c);
     // one_step_x4 possible on this rank: its static conditions and a known-constant verdict for the x2
     // range its host has read (the variant the pairs run; kFbZero stays put through prepare_kc(x2))
-    const bool x4_here = x2_here && x4_local(c) && c->fb_state == kFbZero && c->fb_x2;
+    const bool x4_here = x2_here && x4_local(c) && (c->fb_state == kFbZero || c->fb_state == kFbHr) && c->fb_x2;
     // a lazy call is planned as the first nsteps steps of a call of nsteps + 1 (the last deferred)
     const bool lazy_cand = eligible && c->onepass && lazy_allowed(c, x2_here);
     bool udiv_ok = c->udiv_ok, first_one = c->hh_consistent, x2_ok = x2_here && c->x2_dev_ok;
@@ -4149,7 +4161,11 @@ int ocn_ctx_set_option(ocn_ctx *c, int32_t key, int64_t value)
         c->coherent_known = false;
         return OCN_OK;
     case OCN_OPT_MULTI_SPIN: c->multi_spin = value < 1 ? 1 : value > kMultiSpin ? kMultiSpin : (int)value; return OCN_OK;
-    case OCN_OPT_X4: c->x4 = value <= 0 ? 0 : value >= 3 ? 3 : 1; c->coherent_known = false; return OCN_OK;
+    case OCN_OPT_X4:
+        c->x4 = value <= 0 ? 0 : value >= 3 ? 3 : 1;
+        c->coherent_known = false;
+        c->hrx_ok = false;   // (h_r's copy 2 or 4 rings deep: refresh_hrx)
+        return OCN_OK;
     case OCN_OPT_CO_LAUNCH: c->co_launch = value != 0; return OCN_OK;
     case OCN_OPT_BATCH:
         if (c->batch != (value != 0)) drop_graphs(c);

@@ -1770,6 +1770,15 @@ __device__ __forceinline__ double row_const(const float *rows, unsigned nrows, u
 // a / 0 are the same infinity or NaN (0 * inf, 0 / 0); c = 3 takes a division (derive).  The
 // counts are integers from the mask bits: no float sums, compares or conversions, and u / v
 // (c <= 2) need no wave-wide test.
+// rcp_count for a count of at least one (c in {1, 2, 4}): no select.  The one-pass step uses it where
+// the average is used only under llu / llv / luh, which lu_lv_init (grid_kernels.f90:40-92) sets
+// exactly where the sum of lu over the average's corners is at least one -- Prepare checks that the
+// mask bytes say so (else OCN_COMPACT_DIVISOR_RANGE: no one-pass steps); a count of 0 gives 1.0 here,
+// a value no store uses
+__device__ __forceinline__ double rcp_sea(unsigned c)
+{
+    return __builtin_bit_cast(double, (unsigned long long)(0x3ff00000u - ((c >> 1) << 20)) << 32);
+}
 __device__ __forceinline__ double rcp_count(unsigned c)
 {
     const unsigned hi = c == 0 ? 0x7ff00000u : 0x3ff00000u - ((c >> 1) << 20);
@@ -1892,6 +1901,13 @@ struct StepRegs {
     {
         return (bits.at<PH>(dx, dy) >> id) & 1u ? 1.0f : 0.0f;
     }
+    // the mask value as a double (D(mk)): 1.0 = 0x3ff00000'00000000 formed from the bit, no select or
+    // conversion
+    template <int PH> __device__ __forceinline__ double mkd(int id, int dx, int dy) const
+    {
+        const unsigned hi = ((bits.at<PH>(dx, dy) >> id) & 1u) * 0x3ff00000u;
+        return __builtin_bit_cast(double, (unsigned long long)hi << 32);
+    }
 };
 
 // metric id `id` of row n + dy as a double
@@ -1922,7 +1938,7 @@ struct StepRegs {
 template <bool P2, bool LAST = false, bool ZF = false, bool X2 = false, bool HR = false, bool PAIR = false,
           bool WT = false>
 struct MarchStep {
-    static_assert(!PAIR || !X2 || (ZF && !HR && !LAST), "two-step launches with exchanges: the known-constant variant");
+    static_assert(!PAIR || !X2 || (ZF && !LAST), "two-step launches with exchanges: the known-constant variants");
     static constexpr int kStAux = WT ? 16 : 0;
     static constexpr bool kPair = PAIR;
     static constexpr bool kX2 = X2;
@@ -2009,7 +2025,7 @@ struct MarchStep {
     {
         const int k = dy + 1;
         const double gx = x.cst<kLds>(RC_DX, dy), gy = x.cst<kLds>(RC_DY, dy);
-        const double l = D(x.mk<PH>(OCN_LU, 0, dy));
+        const double l = x.mkd<PH>(OCN_LU, 0, dy);
         // ffs = 1 (launch_onepass requires it): sh * ffs is sh bit for bit
         x.w0.s<PH>(k) = (x.hr.s<PH>(k) + x.ssh.s<PH>(k)) * gx * gy * l;
         x.w1.s<PH>(k) = (x.hr.s<PH>(k) + x.shp.s<PH>(k)) * gx * gy * l;
@@ -2096,12 +2112,12 @@ struct MarchStep {
         const double s0 = w00 + w10;
         const double rxt = x.cst<kLds>(RC_RDXT, 1), ryh = x.cst<kLds>(RC_RDYH, 1), rxh = x.cst<kLds>(RC_RDXH, 1),
                      ryt = x.cst<kLds>(RC_RDYT, 1);
-        const double ru = rcp_count(cu), rv = rcp_count(cv);
+        const double ru = rcp_sea(cu), rv = rcp_sea(cv);
         const double a_u0 = s0 * ru, a_v0 = (w00 + w01) * rv, a_u1 = (p00 + p10) * ru, a_v1 = (p00 + p01) * rv;
         // a / 3 (three sea corners): udiv by 3 (the same correctly rounded quotient: its dividend's
         // range is checked with the others below), IEEE division in the re-run -- per lane, no branch
         const double sh = s0 + w01 + w11;
-        const double a_h0 = ch == 3 ? (E ? sh / 3.0 : udiv(sh, 3.0, 1.0 / 3.0)) : sh * rcp_count(ch);
+        const double a_h0 = ch == 3 ? (E ? sh / 3.0 : udiv(sh, 3.0, 1.0 / 3.0)) : sh * rcp_sea(ch);
         if (!E) exp_check(acc, sh);
         if (!E) {   // (a / g1) / g2: a's range bounds a / g1's (|g1| <= 2^60)
             exp_check(acc, a_u0); exp_check(acc, a_v0); exp_check(acc, a_h0); exp_check(acc, a_u1);
@@ -2149,8 +2165,13 @@ struct MarchStep {
         x.rr.s<PH>(2) = rr;
         x.cx.s<PH>(2) = rr * (v_r + v_0);                                //   ... * (vbrtr(1,0) + vbrtr)
         const double hq = x.hr.s<PH>(2) + x.ssh.s<PH>(2);                    // depth.f90:48 hq = h_r + sh*ffs (ffs = 1)
-        x.dt.s<PH>(2) = x.cst<kLds>(RC_DY2, 1) * x.mu.s<PH>(2) * hq * stt;         // uv_diff2: dy**2 * mu * hq * str_t
-        x.dxq.s<PH>(2) = x.cst<kLds>(RC_DX2, 1) * x.mu.s<PH>(2) * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
+        if constexpr (kLds) {   // (the LDS rows hold dy**2 * mu, dx**2 * mu: prologue)
+            x.dt.s<PH>(2) = x.cst<kLds>(RC_DY2, 1) * hq * stt;
+            x.dxq.s<PH>(2) = x.cst<kLds>(RC_DX2, 1) * hq * stt;
+        } else {
+            x.dt.s<PH>(2) = x.cst<kLds>(RC_DY2, 1) * x.mu.s<PH>(2) * hq * stt;         // uv_diff2: dy**2 * mu * hq * str_t
+            x.dxq.s<PH>(2) = x.cst<kLds>(RC_DX2, 1) * x.mu.s<PH>(2) * hq * stt;        // uv_diff2: dx**2 * mu * hq * str_t
+        }
     }
 
     // (the warm-up row n = nb - 1, after D(nb)) the n+1 faces of row n that S(nb) takes from the
@@ -2159,13 +2180,14 @@ struct MarchStep {
     {
         const double u = x.u.s<PH>(1), v = x.v.s<PH>(1), u_n = x.u.s<PH>(2), v_n = x.v.s<PH>(2);
         const double v_r = x.vr.s<PH>(1);
-        const double pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2), luu = D(x.mk<PH>(OCN_LUU, 0, 0));
+        const double pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2), luu = x.mkd<PH>(OCN_LUU, 0, 0);
         x.fyx = (pv + shz(pv, 1)) / 2.0 * (u_n + u) / 2.0 * luu;
         x.vht = x.vh.s<PH>(1) * (v_r + v);
         x.fyy = (pv + pvn) / 2.0 * (v + v_n) / 2.0;
         if constexpr (ZF) {   // (uv_diff2_math's muh_p with mu one value: its lane shifts are the value)
             const double mu = x.mu.s<PH>(1), mu_n = x.mu.s<PH>(2), muh_p = (mu + mu + mu_n + mu_n) / 4.0;
-            x.a2t = x.cst<kLds>(RC_DXB2, 0) * muh_p * x.hh.s<PH>(1) * x.sts.s<PH>(1);
+            (void)muh_p;   // (kLds = ZF: the LDS row holds dxb**2 * muh)
+            x.a2t = x.cst<kLds>(RC_DXB2, 0) * x.hh.s<PH>(1) * x.sts.s<PH>(1);
         }
     }
 
@@ -2193,7 +2215,7 @@ struct MarchStep {
         const double u_r = shz(u, 1), u_n = x.u.s<PH>(2);
         const double v_r = x.vr.s<PH>(1), v_n = x.v.s<PH>(2);
         const double pu = x.pu.s<PH>(1), pun = x.pu.s<PH>(2), pv = x.pv.s<PH>(1), pvn = x.pv.s<PH>(2);
-        const double luu = D(x.mk<PH>(OCN_LUU, 0, 0));
+        const double luu = x.mkd<PH>(OCN_LUU, 0, 0);
         double rxa, rya;
         // each face's flux once: the m-1 face is the left lane's m+1 face and the n-1 face the row
         // before's n+1 face (carried in x, face<PH>) -- the same operands, the sums' terms swapped
@@ -2236,7 +2258,9 @@ struct MarchStep {
             double a2, a4;
             if constexpr (ZF) {
                 (void)dxb2m; (void)muh_m; (void)muh_m2;
-                const double a2p = dxb2 * muh_p * hh * sts, a4p = dyb2 * muh_p * hh * sts;
+                // (kLds = ZF: dxb2 / dyb2 are the LDS rows' dxb**2 * muh, dyb**2 * muh -- prologue)
+                (void)muh_p;
+                const double a2p = dxb2 * hh * sts, a4p = dyb2 * hh * sts;
                 a2 = a2p - x.a2t;
                 a4 = a4p - shz(a4p, -1);
                 o.a2t = a2p;
@@ -2267,7 +2291,9 @@ struct MarchStep {
                 const double bp = qtau(x, hu * dxt * dyh / 2.0);
                 const double bp0 = qtau(x, x.hu1.s<PH>(1) * dxt * dyh / 2.0);
                 const double slx = -(g * (shz(ssh, 1) - ssh) * dyh * hu);
-                const double fric = x.cst<kLds>(RC_RDSELF, 0) / 2.0 * x.up.s<PH>(1) * dxt * dyh * hu;   // (rdis + rdis) / 2
+                // (rdis + rdis) / 2 (kLds: the LDS row holds it halved)
+                const double fric = (kLds ? x.cst<kLds>(RC_RDSELF, 0) : x.cst<kLds>(RC_RDSELF, 0) / 2.0) * x.up.s<PH>(1) * dxt *
+                                    dyh * hu;
                 const double grx = x.rhsx + slx + rxd + rxa - fric + (x.cx.s<PH>(1) + x.cx.s<PH>(0)) / 4.0;
                 un = (x.up.s<PH>(1) * bp0 + grx) / (bp);
             }
@@ -2275,7 +2301,9 @@ struct MarchStep {
                 const double bp = qtau(x, hv * dyt * dxh / 2.0);
                 const double bp0 = qtau(x, x.hv1.s<PH>(1) * dyt * dxh / 2.0);
                 const double sly = -(g * (x.ssh.s<PH>(2) - ssh) * dxh * hv);
-                const double fric = x.cst<kLds>(RC_RDNEXT, 0) / 2.0 * x.vp.s<PH>(1) * dxh * dyt * hv;   // (rdis + rdis(n+1)) / 2
+                // (rdis + rdis(n+1)) / 2 (kLds: halved in the LDS row)
+                const double fric = (kLds ? x.cst<kLds>(RC_RDNEXT, 0) : x.cst<kLds>(RC_RDNEXT, 0) / 2.0) * x.vp.s<PH>(1) * dxh *
+                                    dyt * hv;
                 const double c1 = x.rr.s<PH>(1) * (u_n + u);
                 const double gry = x.rhsy + sly + ryd + rya - fric - (c1 + shz(c1, -1)) / 4.0;
                 vn = (x.vp.s<PH>(1) * bp0 + gry) / (bp);
@@ -2367,8 +2395,19 @@ struct MarchStep {
         const int ne = min(R.n1, nb + h - 1), lo = nb - (PAIR ? 5 : 2) - b.bnd_y1, i = (int)threadIdx.x;
         if (i < ne - nb + (PAIR ? 10 : 5)) {   // a thread per row
             const unsigned r = (unsigned)min(max(lo + i, 0), (int)t.nrows - 1);
+            // (the known-constant variant: mu is the one value mu0 = kc[1], so the row-uniform leading
+            // factors of four products -- dy**2 * mu, dx**2 * mu, dxb**2 * muh, dyb**2 * muh with muh
+            // = (mu + mu + mu + mu) / 4 as uv_diff2_math forms it -- and the friction's (rdis + rdis') / 2
+            // are formed here once per row: the same operations on the same operands)
+            const double mu0 = kc[1], muh = (mu0 + mu0 + mu0 + mu0) / 4.0;
 #pragma unroll
-            for (int k = 0; k < kRowC; ++k) g_step_rc[i * kRowC + k] = row_const(t.rows, t.nrows, r, k);
+            for (int k = 0; k < kRowC; ++k) {
+                double v = row_const(t.rows, t.nrows, r, k);
+                if (k == RC_DY2 || k == RC_DX2) v = v * mu0;
+                else if (k == RC_DXB2 || k == RC_DYB2) v = v * muh;
+                else if (k == RC_RDSELF || k == RC_RDNEXT) v = v / 2.0;
+                g_step_rc[i * kRowC + k] = v;
+            }
         }
         if (threadIdx.x == 0) g_step_rlo = (unsigned)lo;
         __syncthreads();
@@ -3105,8 +3144,8 @@ int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, cons
         !up_out || !vp_out)
         return set_error(OCN_ERR_ARG, "x4 two-step launch: compact tables, march, full_free_surface = 1, trans_terms "
                                       "and ksw_lat on, three second buffers");
-    if (kc.mode != OCN_KC_KNOWN || !kc.kc)
-        return set_error(OCN_ERR_ARG, "x4 two-step launch: the known-constant variant chosen on the host");
+    if ((kc.mode != OCN_KC_KNOWN && kc.mode != OCN_KC_KNOWN_HR) || !kc.kc)
+        return set_error(OCN_ERR_ARG, "x4 two-step launch: a known-constant variant chosen on the host");
     RC_K(check_block(bx));
     if (bx->bnd_x1 > bx->nx_start - 4 || bx->bnd_x2 < bx->nx_end + 4 || bx->bnd_y1 > bx->ny_start - 4 ||
         bx->bnd_y2 < bx->ny_end + 4)
@@ -3144,7 +3183,15 @@ int launch_onepass_pair_x4(const ocn_block *bx, void *const *ptr, int nptr, cons
             for (int i = 0; i < 4; ++i) body.trs[i] = trs[i];
         return issue_march(g, body, s);
     };
-    if (std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020)   // tau = 2^k
+    const bool p2 = std::frexp(tau, &ex) == 0.5 && ex > -1020 && ex < 1020;   // tau = 2^k
+    if (kc.mode == OCN_KC_KNOWN_HR) {   // h_r read (a topography: the rest depth varies), its 4 rings exchanged
+        if (p2)
+            return go(MarchStep<true, false, true, true, true, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out, vp_out,
+                                                                     kc.kc, nullptr, 0, own, nbad2});
+        return go(MarchStep<false, false, true, true, true, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out, vp_out, kc.kc,
+                                                                  nullptr, 0, own, nbad2});
+    }
+    if (p2)
         return go(MarchStep<true, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out, vp_out, kc.kc,
                                                                   nullptr, 0, own, nbad2});
     return go(MarchStep<false, false, true, true, false, true>{*bx, t, sw, tau, nbad1, sshp_out, up_out, vp_out, kc.kc,

@@ -865,7 +865,8 @@ OCN_HD inline unsigned recip_offset(unsigned nrows) { return ((unsigned)kRowTabl
 inline size_t row_table_floats(unsigned nrows) { return recip_offset(nrows) + 2u * (unsigned)kNumRecips * nrows; }
 enum { OCN_COMPACT_MASK_NOT_BINARY = 1, OCN_COMPACT_METRIC_NOT_ROW_CONSTANT = 2,
        OCN_COMPACT_RING_SEA = 4,     // not a failure: a8 / a9 write somewhere on the halo ring
-       OCN_COMPACT_DIVISOR_RANGE = 8,     // not a failure: a divisor outside [2^-60, 2^60] (no one-pass step)
+       OCN_COMPACT_DIVISOR_RANGE = 8,     // not a failure: a divisor outside [2^-60, 2^60], or llu / llv / luh
+                                          // set where lu_lv_init would not (no one-pass step)
        OCN_COMPACT_EDGE_RING_SEA = 16 };  // not a failure: a8 writes on the ring of a side no neighbour fills
 
 // Which halo points of a block a neighbour block owns (they are its interior points, filled by the
@@ -905,6 +906,7 @@ struct Prepare {
     const float *__restrict__ r4[OCN_NUM_R4];
     uint8_t *__restrict__ bits; float *__restrict__ rows; unsigned nrows; int *flags;
     unsigned own;   // halo points neighbour blocks own (own_class bits): OCN_COMPACT_EDGE_RING_SEA tests the rest
+    int bx2, by2;   // the arrays' last column / row
     OCN_HD void operator()(int m, int n) const
     {
         const Pt q = I(m, n);
@@ -917,6 +919,17 @@ struct Prepare {
         }
         st(bits, q, (uint8_t)b);
         if (bad) OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_MASK_NOT_BINARY);
+        {   // llu / llv / luh where lu_lv_init sets them (grid_kernels.f90:60-86): the one-pass step's
+            // averages divide by the sea count without a zero case (sw_kernels.hip rcp_sea)
+            auto sea = [&](int dm, int dn) {
+                const int mm = m + dm, nn = n + dn;
+                return mm <= bx2 && nn <= by2 && fbits(ld(r4[OCN_LU], I(mm, nn))) == 0x3f800000u;
+            };
+            const bool s00 = (b >> OCN_LU) & 1u, s10 = sea(1, 0), s01 = sea(0, 1), s11 = sea(1, 1);
+            if ((((b >> OCN_LLU) & 1u) && !(s00 || s10)) || (((b >> OCN_LLV) & 1u) && !(s00 || s01)) ||
+                (((b >> OCN_LUH) & 1u) && !(s00 || s10 || s01 || s11)))
+                OCN_ATOMIC_OR(flags, (int)OCN_COMPACT_DIVISOR_RANGE);
+        }
         if (m < ms || m > me || n < ns || n > ne) return;
         // a8 on the ring writes under lu / lcu / lcv; a9 (fused C1) on the outer ring e+1 under
         // lu / llu / llv / luh
@@ -1056,7 +1069,7 @@ inline Prepare make_prepare(const ocn_block *b, void *const *ptr, uint8_t *bits,
                             unsigned own = 0)
 {
     Prepare k{geo(b), b->nx_start - 1, b->nx_end + 1, b->ny_start - 1, b->ny_end + 1, {}, bits, rows,
-              block_rows(b), flags, own};
+              block_rows(b), flags, own, b->bnd_x2, b->bnd_y2};
     for (int id = 0; id < OCN_NUM_R4; ++id) k.r4[id] = (const float *)ptr[ocn_field_slot(id)];
     return k;
 }

@@ -529,4 +529,5 @@ def test_exchange_stats_and_comm_info(amd):
         # (17 one-pass steps: 8 pairs of x2 steps with one 4-deep exchange each + 1 x2 step, then the last
         # step's exchanges, the h_r refresh and the vote's two compare-mode exchanges)
         assert ex and ex[1] == groups and groups >= 10 and ex[2] >= ex[0] / ex[1] > 0, (ex, groups)
-        assert "exposed" in st and st["exposed"][1] >= 9, st.get("exposed")
+        # (overlap auto: the measured choice runs one pair of the call in sequence -- ocn_ctx.hip ov_begin)
+        assert "exposed" in st and st["exposed"][1] >= 8, st.get("exposed")

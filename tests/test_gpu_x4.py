@@ -86,6 +86,18 @@ def test_x4_tracer_runs_in_one_process_default_to_x2(amd):
     assert not bad and not any(used), (bad, used)
 
 
+@pytest.mark.parametrize("name,calls", [("box70x54_topo_b3x2_s20", [2, 18]), ("box70x54_topo_b3x2_s20", [2, 5, 1, 1, 3, 8]),
+                                        ("bs_topo_b4x2_s60", [2, 58])])
+@pytest.mark.parametrize("overlap", [None, 2])
+def test_x4_topography_blocks_match_reference(amd, name, calls, overlap):
+    """A rest depth read from a topography file (control/init_data.f90:115-120): the pairs run the
+    h_r-read variant (OCN_KC_KNOWN_HR) with h_r's copy exchanged four rings deep (refresh_hrx) -- every
+    field bitwise."""
+    bad, used = _run_blocks(amd, name, calls, overlap=overlap)
+    assert not bad, f"{name} {calls}: fields differ from the reference: {bad}"
+    assert any(used), used
+
+
 def test_x4_off_is_the_x2_path(amd):
     bad, used = _run_blocks(amd, "box70x54_b3x2_s20", [2, 18], x4=False)
     assert not bad and not any(used), (bad, used)
@@ -129,7 +141,8 @@ def _run_ranks(amd, name, nranks, calls, overlap=None, co=None):
 
 @pytest.mark.parametrize("name,nranks,calls", [("box70x54_b3x2_s20", 6, [2, 18]), ("bs_b4x2_s60", 8, [2, 58]),
                                                ("box40x32_b2x2_s5", 4, [2, 3]), ("box70x54_b3x2_s20", 6, [2, 7, 3, 8]),
-                                               ("bs_b4x2_tr_s60", 8, [2, 58]), ("box70x54_b3x2_tr_s20", 6, [2, 7, 3, 8])])
+                                               ("bs_b4x2_tr_s60", 8, [2, 58]), ("box70x54_b3x2_tr_s20", 6, [2, 7, 3, 8]),
+                                               ("box70x54_topo_b3x2_s20", 6, [2, 18]), ("bs_topo_b4x2_s60", 8, [2, 58])])
 def test_x4_ranks_match_reference(amd, name, nranks, calls):
     """One block per loopback rank: the exchange is the RCCL path's (device pack / unpack, per-peer
     messages 4 deep), the decision every rank's (the vote's x4 word), every field bitwise.  (With a

@@ -356,3 +356,18 @@ def test_tracer_step_matches_expl_tracer(hst, name, compact):
                 if got[sea].tobytes() != want[sea].tobytes():
                     bad.append(f"({blkk.bm},{blkk.bn}):{nm} {int((got[sea] != want[sea]).sum())}/{int(sea.sum())}")
     assert not bad, bad
+
+
+@pytest.mark.parametrize("which", ["llu", "llv", "luh"])
+def test_compact_tables_flag_inconsistent_sea_masks(hst, which):
+    """The one-pass step divides its hh_init averages by the sea count without a zero case
+    (sw_kernels.hip rcp_sea): Prepare flags (OCN_COMPACT_DIVISOR_RANGE: no one-pass steps) an
+    llu / llv / luh set where lu_lv_init would not set it -- no sea point among the average's
+    corners (grid_kernels.f90:60-86) -- and nothing for the masks lu_lv_init forms."""
+    om = O.OracleModel(O.BasinConfig(nx=40, ny=36), O.SWConfig(), 1, 1).init()
+    assert compact_tables(hst, om)[0][2] & 8 == 0
+    f = om.f[0]
+    for nm in ("lu", "luh", "luu", "llu", "llv", "lcu", "lcv"):   # a land square of 3 x 3 points
+        f[nm][10:13, 10:13] = 0.0
+    f[which][11, 11] = 1.0
+    assert compact_tables(hst, om)[0][2] & 8 == 8
