@@ -1712,6 +1712,9 @@ constexpr int kUdivMinExp = -899;   // frexp exponent >= -899  <=>  |x| >= 2^-90
 enum RowC { RC_DX, RC_DY, RC_DXT, RC_DYT, RC_DXH, RC_DYH, RC_DXB, RC_DYB, RC_RDXT, RC_RDYH, RC_RDXH, RC_RDYT,
             RC_RDXB, RC_RDYB, RC_RAT0, RC_RAT1, RC_RAT2, RC_RAT3, RC_RLH, RC_DY2, RC_DX2, RC_AREA, RC_RAREA,
             RC_DXB2, RC_DYB2, RC_RDSELF, RC_RDNEXT, kRowC };
+#ifndef OCN_PAIR_WAVES
+#define OCN_PAIR_WAVES OCN_STEP_WAVES   // waves per SIMD the two-step launch asks of the register allocator
+#endif
 #ifndef OCN_PAIR_MAX_ROWS
 #define OCN_PAIR_MAX_ROWS 150   // the tallest workgroup tile of the two-step launch (its rows +- 5 in LDS)
 #endif
@@ -1948,7 +1951,7 @@ struct MarchStep {
     static constexpr int kPairCols = 116;   // PAIR: a workgroup's output columns (2 x 60 produced, less 2 each side)
     static constexpr bool kAligned = false;
     static constexpr int kHalo = 2;
-    static constexpr int kWaves = OCN_STEP_WAVES;
+    static constexpr int kWaves = PAIR ? OCN_PAIR_WAVES : OCN_STEP_WAVES;
     ocn_block b; Tab<true> t; ocn_sw_params sw; double tau; int32_t *nbad;
     double *sshp_out, *up_out, *vp_out;   // a8's filtered sshp / ubrtrp / vbrtrp (the second buffers)
     // ZF: kc[0], kc[1] = the values h_r and mu hold at every point the step reads (device memory,
@@ -3073,6 +3076,8 @@ int launch_onepass_multi(const ocn_block *b, void *const *ptr, int nptr, const C
 // Rows per workgroup tile of the two-step launch: the fewest iterations in total, counting
 // ceil(waves / slots) rounds of rows + 8 iterations each (MarchStep::march); mult = blocks of this
 // size in one launch (a batch: one_step_x4 on several blocks of a device)
+// wave slots of the chip for the two-step launch: 256 CUs x 4 SIMDs x its waves per SIMD
+constexpr long kPairSlots = 256L * 4L * OCN_PAIR_WAVES;
 static int pair_rows(const Range &r, int cols, int mult = 1)
 {
     const long wx = (r.m1 - r.m0 + cols) / cols, h = r.n1 - r.n0 + 1;
@@ -3087,7 +3092,7 @@ static int pair_rows(const Range &r, int cols, int mult = 1)
     long cost = -1;
     for (int rows = 8; rows <= OCN_PAIR_MAX_ROWS; ++rows) {
         const long tiles = (h + rows - 1) / rows, waves = 4 * tiles * wx * mult,
-                   rounds = (waves + OCN_STEP_SLOTS - 1) / OCN_STEP_SLOTS, c = rounds * (rows + 8);
+                   rounds = (waves + kPairSlots - 1) / kPairSlots, c = rounds * (rows + 8);
         if (cost < 0 || c < cost) { cost = c; best = rows; }
     }
     return best;
