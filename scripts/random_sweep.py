@@ -31,7 +31,7 @@ print("failures", nfail)
 
 if len(sys.argv) > 5 and sys.argv[5] == "ranks":
     nf = 0
-    for tr in (0, 2):
+    for tr in (0, 1, 2):
         for seed in range(lo, hi):
             try:
                 _ranks_sequence(amd, seed, NOPS, tracers=tr)

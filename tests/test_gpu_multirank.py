@@ -373,7 +373,8 @@ def _ranks_sequence(amd, seed, nops=20, tracers=0, n=120, grid=(2, 2)):
             ops.append((op, str(rng.choice(["ssh", "ubrtr", "hhu_n", "hhq", "vort", "sshp", "hhq_n"]))))
         elif op == "opt":
             w = str(rng.choice(["onepass", "tracer_step", "lazy_tail", "flip", "overlap", "co_launch", "x4"]))
-            ops.append((op, w, int(rng.integers(0, 2))))
+            # (overlap: 2, 1 or auto -- the measured choice, ov_begin; x4: off, auto, always)
+            ops.append((op, w, int(rng.integers(0, 3 if w in ("overlap", "x4") else 2))))
         elif op == "kc":
             ops.append((op, int(rng.integers(0, 2))))
         else:
@@ -407,10 +408,12 @@ def _ranks_sequence(amd, seed, nops=20, tracers=0, n=120, grid=(2, 2)):
                 m.set_known_constants(bool(op[1]))
             elif op[0] == "opt":
                 if op[1] == "overlap":
-                    m.set_overlap(1 if op[2] else 2)
+                    m.set_overlap((2, 1, -1)[op[2]])
+                elif op[1] == "x4":
+                    m.set_x4((0, 1, 3)[op[2]])
                 else:
                     {"onepass": m.set_onepass, "tracer_step": m.set_tracer_step, "lazy_tail": m.set_lazy_tail,
-                     "flip": m.set_flip, "co_launch": m.set_co_launch, "x4": m.set_x4}[op[1]](bool(op[2]))
+                     "flip": m.set_flip, "co_launch": m.set_co_launch}[op[1]](bool(op[2]))
             else:
                 nm, f = fn[op[0]]
                 for b in m.blocks:
