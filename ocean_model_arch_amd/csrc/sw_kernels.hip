@@ -2413,7 +2413,10 @@ struct MarchStep {
             }
         }
         if (threadIdx.x == 0) g_step_rlo = (unsigned)lo;
-        __syncthreads();
+        // PAIR: the workgroup meets after its producers have issued their first state loads
+        // (march_role<1>, the consumers' first barrier) -- the table's and the state's memory
+        // latencies overlap instead of following each other
+        if constexpr (!PAIR) __syncthreads();
     }
 
     // PAIR (two steps in one launch, single block, a variant chosen on the host): the producer waves march the
@@ -2434,7 +2437,8 @@ struct MarchStep {
                 pair_barrier();
             } else {   // (march_role<2> has one more before its loop: after its first ring reads)
 #pragma unroll
-                for (int k = 0; k < 5; ++k) pair_barrier();
+                // (+1 with the prologue: its barrier, met by the producers after their first loads)
+                for (int k = 0; k < 5 + (kPrologue ? 1 : 0); ++k) pair_barrier();
                 march_role<2>(L, nb, ne);
             }
             return;
@@ -2448,10 +2452,7 @@ struct MarchStep {
         x.nbp = RO == 2 ? nbad2 : nbad;
         x.cnt = true;
         x.pj = L.j;
-        if (kLds) {
-            x.lds = (const __attribute__((address_space(3))) double *)g_step_rc;
-            x.rlo = g_step_rlo;
-        }
+        if (kLds) x.lds = (const __attribute__((address_space(3))) double *)g_step_rc;
         x.rows = (const __attribute__((address_space(4))) float *)t.rows;
         x.rcp = (const __attribute__((address_space(4))) double *)(t.rows + recip_offset(t.nrows));
         x.nrows = t.nrows;
@@ -2477,15 +2478,19 @@ struct MarchStep {
             }
             x.hr.s<0>(2) = ZF && !HR ? x.hr0 : ld(t.f(OCN_HHQ_REST), c1);
             x.bits.s<0>(2) = ld(t.bits, c1);
-            // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
-            x.qb = x.vp.s<0>(1) / x.cst<kLds>(RC_DXH, 0);
-            x.qc = x.up.s<0>(2) / x.cst<kLds>(RC_DXT, 1);
-            weights<0>(x, 1);
         }
         Fallback fb;
         fallback<0, RO>(x, fb, L.m, n0 + 1, 2);
         Batch q;
         load<RO>(x, q, L.m, n0);
+        // PAIR producer: the workgroup's first barrier (the row constants in LDS: prologue), its loads
+        // in flight
+        if constexpr (PAIR && RO == 1 && kPrologue) pair_barrier();
+        if (kLds) x.rlo = g_step_rlo;
+        // the shared stress quotients of rows n0 (vp/dxh) and n0+1 (up/dxt)
+        x.qb = x.vp.s<0>(1) / x.cst<kLds>(RC_DXH, 0);
+        x.qc = x.up.s<0>(2) / x.cst<kLds>(RC_DXT, 1);
+        weights<0>(x, 1);
         if (RO != 1) store_out(Out{}, 0u);   // every lane dropped: the loop entry has six stores after its loads too
         // PAIR consumer: its first ring reads (rows nb - 2 .. nb, finished by the producers 2 barriers
         // ago) precede the barrier after which the producers overwrite row nb - 2's slot with nb + 2
