@@ -3534,6 +3534,11 @@ static void learn_fb_async(ocn_ctx *c)
 // h_r with the neighbours' second ring).  A verdict for that range also holds for the hybrid
 // steps' inner range (its points and their +-2 neighbourhood lie inside what it covered, with the
 // same values there), not the other way round.
+static int kc_of_fb(const ocn_ctx *c)
+{
+    return c->fb_state == kFbZero ? OCN_KC_KNOWN : c->fb_state == kFbHr ? OCN_KC_KNOWN_HR
+         : c->fb_state == kFbGeneral ? OCN_KC_GENERAL : OCN_KC_DEVICE;
+}
 static int prepare_kc(ocn_ctx *c, bool x2 = false)
 {
     if (!c->known_const || c->r8_handed) { c->kc_mode = OCN_KC_GENERAL; return OCN_OK; }
@@ -3555,8 +3560,7 @@ static int prepare_kc(ocn_ctx *c, bool x2 = false)
         c->fb_state = kFbDevice;
         c->fb_x2 = x2;
     }
-    c->kc_mode = c->fb_state == kFbZero ? OCN_KC_KNOWN : c->fb_state == kFbHr ? OCN_KC_KNOWN_HR
-               : c->fb_state == kFbGeneral ? OCN_KC_GENERAL : OCN_KC_DEVICE;
+    c->kc_mode = kc_of_fb(c);
     return OCN_OK;
 }
 
@@ -3641,6 +3645,28 @@ static bool x4_now(const ocn_ctx *c)
 {
     return (c->kc_mode == OCN_KC_KNOWN || c->kc_mode == OCN_KC_KNOWN_HR) &&
            (has_comm(c) ? c->x4_dev_ok : x4_local(c) && c->fb_x2);
+}
+
+// The first call of a sequence long enough for pairs, right after prepare_kc issued the known-
+// constant check: wait for the check's verdict (one host wait per check -- the check's pass over
+// the fields and a 4-byte copy, behind whatever the stream holds) so that the call's steps run as
+// pairs of the host-chosen variant instead of single launches of both variants with the device
+// picking (4096^2: 0.39 ms per single step against 0.28-0.30 ms per step in pairs; the single
+// steps' HBM traffic also pulls the shader clock down, 2.25 -> 1.55 GHz over 5 ms, and the pairs'
+// clock climbs back over ~30 ms: profiles/r06/clock_*.txt).  Not while a graph is captured (no
+// host wait there), not with a communicator (the ranks' votes carry the verdicts), not for calls
+// of 1-3 steps (no pair before their deferred last steps).
+static int await_kc(ocn_ctx *c, bool x2, int nsteps)
+{
+    if (c->kc_mode != OCN_KC_DEVICE || !c->fb_copy || c->capturing || has_comm(c) || nsteps < 4) return OCN_OK;
+    c->kc_mode = OCN_KC_KNOWN;   // would the call run pairs with a host-chosen known-constant variant?
+    const bool pairs = x2 ? x4_now(c) : pair_ok(c);
+    c->kc_mode = OCN_KC_DEVICE;
+    if (!pairs) return OCN_OK;
+    HIPCHK(hipEventSynchronize(c->ev_fb));
+    learn_fb_async(c);
+    c->kc_mode = kc_of_fb(c);
+    return OCN_OK;
 }
 
 // The pending tail of an open sequence: the last step run (a one-pass step) is run again from the
@@ -3839,7 +3865,10 @@ static int step_impl(ocn_ctx *c, double tau, int32_t nsteps, int32_t check_every
         if (!c->hrx_ok || has_comm(c)) RC(refresh_hrx(c));   // (with RCCL: every rank, every call)
         RC(prebuild_x2(c));
     }
-    if (one_call) RC(prepare_kc(c, x2_call));
+    if (one_call) {
+        RC(prepare_kc(c, x2_call));
+        RC(await_kc(c, x2_call, nsteps));
+    }
     const bool rc_call = ca && c->recompute && !one_call;
     if (rc_call) c->alt_ok = false;
     if (one_call && !c->alt_ok) {   // the second buffers start as copies (they agree outside a8's write set)

@@ -455,7 +455,17 @@ __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Bo
 #endif
     int k = 0;   // workgroup-uniform
     while (k + 1 < g.nr && tile >= g.r[k].tiles) { tile -= g.r[k].tiles; ++k; }
+#if OCN_CLOCK_PROBE   // diagnostic build only (scripts/gpu_clock_probe.sh): workgroup 0's shader clock
+    const unsigned long long c0 = clock64(), w0 = wall_clock64();
+#endif
     march_tile(g.r[k], tile, body);
+#if OCN_CLOCK_PROBE
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long c1 = clock64(), w1 = wall_clock64();
+        printf("clockprobe %d %.4f GHz %.1f us\n", (int)sizeof(Body), (double)(c1 - c0) / ((double)(w1 - w0) * 10.0),
+               (double)(w1 - w0) * 0.01);
+    }
+#endif
 }
 
 // batched (ocn_internal.h Batcher): every block's rects in one grid, rect k marched with body blk[k]

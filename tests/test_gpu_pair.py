@@ -167,6 +167,27 @@ def test_pair_default_threshold(amd, name):
         assert used == (mode == 1 and name.startswith("box1024")), (mode, used)
 
 
+@pytest.mark.parametrize("name,calls,want", [("box1024_b1x1_s10", [10], [True]), ("box1024_b1x1_s10", [3, 7], [False, True]),
+                                             ("box2048_b2x2_s10", [10], [True]), ("box2048_b2x2_s10", [4, 6], [True, True])])
+def test_first_call_waits_for_the_verdict(amd, name, calls, want):
+    """A first call of 4 or more steps waits for the known-constant check's verdict (ocn_ctx.hip
+    await_kc) and runs pairs (x4 pairs with several blocks in one process) from its second step; a
+    first call of 3 leaves the variant to the device -- bitwise against the reference either way."""
+    case = cases.load_e2e(name)
+    m = build_model(amd, case).init()
+    used = []
+    try:
+        for n in calls:
+            m.step(n, tau=1.0, check_every=1)
+            used.append(m.x4_active if len(m.blocks) > 1 else m.pair_active)
+        m.synchronize()
+        bad = compare_case(m, case, name)
+    finally:
+        m.close()
+    assert not bad, f"{name} {calls}: fields differ from the reference: {bad}"
+    assert used == want, (used, want)
+
+
 def test_pair_counts_blowup_points_once(amd):
     """check_ssh_err_kernel (vel_ssh.f90:40-67) in pair launches: each step counts its points once
     (the producers count only their workgroup's own rows) -- the reported count equals the single
