@@ -1067,6 +1067,14 @@ struct MarchViewH {
 // fused C2 = a10 hh_init (sw_stencils.h HhInit) as a register march (aligned layout) over any
 // part of the whole bnd range: row n+1 is clamped to bnd_y2 (its values are used only where
 // n <= end, where it is in range)
+#ifndef OCN_HH_NT
+#define OCN_HH_NT 0   // the call tail's hh_init stores as nontemporal stores (an A/B switch)
+#endif
+template <class T> __device__ __forceinline__ void st_hh(T *__restrict__ p, Pt q, T v)
+{
+    if constexpr (OCN_HH_NT) __builtin_nontemporal_store(v, (T *)((char *)p + q.c * (unsigned)sizeof(T)));
+    else st(p, q, v);
+}
 struct MarchHhInit {
     static constexpr bool kAligned = true;
     static constexpr int kHalo = 0;
@@ -1107,13 +1115,13 @@ struct MarchHhInit {
             x.rHR.nn = q.nn[0]; x.rSH.nn = q.nn[1]; x.rSHP.nn = q.nn[2]; x.bits.nn = q.bits;
             x.rHR.enn = q.enn[0]; x.rSH.enn = q.enn[1]; x.rSHP.enn = q.enn[2]; x.bits.enn = q.ebits;
             const double r00 = x.rHR.c;
-            if (csh_dst && L.out) { st(csh_dst, c, x.rSH.c); st(cu_dst, c, x.cu); st(cv_dst, c, x.cv); }
+            if (csh_dst && L.out) { st_hh(csh_dst, c, x.rSH.c); st_hh(cu_dst, c, x.cu); st_hh(cv_dst, c, x.cv); }
             x.cu = q.uv[0]; x.cv = q.uv[1];
             if (L.out) {
-                st(k.hq, c, r00 + x.rSH.c * f);
+                st_hh(k.hq, c, r00 + x.rSH.c * f);
                 if (k.full) {
-                    st(k.hqp, c, r00 + x.rSHP.c * f);
-                    if (!keep_n) st(k.hqn, c, r00);
+                    st_hh(k.hqp, c, r00 + x.rSHP.c * f);
+                    if (!keep_n) st_hh(k.hqn, c, r00);
                 }
             }
             if (n >= k.j0 && n <= k.j1) {   // wave-uniform
@@ -1122,13 +1130,13 @@ struct MarchHhInit {
                 if (L.out && L.m >= k.i0 && L.m <= k.i1) {
                     const unsigned bc = x.bits.c;
                     const bool bu = bc & (1u << OCN_LLU), bv = bc & (1u << OCN_LLV), bh = bc & (1u << OCN_LUH);
-                    if (bu) { st(k.hu, c, o.u[0]); st(k.hup, c, o.u[1]); }
-                    if (bv) { st(k.hv, c, o.v[0]); st(k.hvp, c, o.v[1]); }
-                    if (bh) { st(k.hh, c, o.h[0]); st(k.hhp, c, o.h[1]); }
+                    if (bu) { st_hh(k.hu, c, o.u[0]); st_hh(k.hup, c, o.u[1]); }
+                    if (bv) { st_hh(k.hv, c, o.v[0]); st_hh(k.hvp, c, o.v[1]); }
+                    if (bh) { st_hh(k.hh, c, o.h[0]); st_hh(k.hhp, c, o.h[1]); }
                     if (k.full && !keep_n) {
-                        if (bu) st(k.hun, c, o.u[2]);
-                        if (bv) st(k.hvn, c, o.v[2]);
-                        if (bh) st(k.hhn, c, o.h[2]);
+                        if (bu) st_hh(k.hun, c, o.u[2]);
+                        if (bv) st_hh(k.hvn, c, o.v[2]);
+                        if (bh) st_hh(k.hhn, c, o.h[2]);
                     }
                 }
             }
