@@ -376,7 +376,7 @@ SHADER_CLOCK_GHZ = 2.4          # MI355X peak engine clock (MI355X_MICROARCH.md)
 SIMDS = 256 * 4
 
 
-def load_valu(amd, stage: str, launch_ms: float, box, blocks):
+def load_valu(amd, stage: str, launch_ms: float, box, blocks, live_clock=None):
     """The dominant kernel's VALU issue from the committed SQ counter pass (profiles/sq_valu.json,
     scripts/sq_valu.py) -- only for the one-pass launches (single and pair), and only when that pass was taken on this
     exact library build and workload.  issue_floor_ms: its VALU instructions spread over the
@@ -418,6 +418,16 @@ def load_valu(amd, stage: str, launch_ms: float, box, blocks):
                                    "; counter passes serialize dispatches)")
             out["issue_floor_ms_at_clock"] = round(floor_clk, 4)
             out["issue_frac_at_clock"] = round(floor_clk / launch_ms, 4)
+        if live_clock and live_clock.get("launches", 0) > 0 and live_clock.get("clock_ghz", 0) > 0 and stage == "onepass2":
+            # the clock the pair launches of THIS timed region ran at (ocn_ctx_clock_info: workgroup 0 of
+            # each launch counts s_memtime over 100 MHz s_memrealtime ticks) and the VALU floor at it
+            g = live_clock["clock_ghz"]
+            floor_live = pl["SQ_INSTS_VALU"] * 4.0 / SIMDS / (g * 1e9) * 1e3
+            out["live_clock_ghz"] = g
+            out["live_clock_source"] = (f"ocn_ctx_clock_info over the timed region: {live_clock['launches']} pair "
+                                        f"launches, {live_clock['sampled_ms']} ms sampled by their workgroup 0")
+            out["issue_floor_ms_at_live_clock"] = round(floor_live, 4)
+            out["issue_frac_at_live_clock"] = round(floor_live / launch_ms, 4)
         vc = d["kernels"][stage].get("valu_classes")
         if vc:   # by class (SQ_INSTS_VALU_* passes): the reference's f64 arithmetic vs everything else
             tot = pl["SQ_INSTS_VALU"]
@@ -583,6 +593,7 @@ def main():
     model.step(args.warmup, check_every=1).synchronize()
     model.set_stage_timing(not args.graph and not args.no_stage_timing)
     model.stage_times()
+    model.clock_info(reset=True)   # the pair launches' in-kernel clock counters from here on
     xchg0 = model.comm_info()["exchanges"]
 
     def barrier():
@@ -605,6 +616,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     launches = amd._lib.launch_count() - n_launch0
+    live_clock = model.clock_info()
     stats = model.stage_stats()
     times = {k: (v[0], v[1]) for k, v in stats.items()}
     compact = model.compact_active
@@ -653,11 +665,12 @@ def main():
             dom = max(stage_ms, key=lambda s: times[s][0])
             alg = kbytes[dom] * local_cells
             achieved = alg / (stage_ms[dom] * 1e-3) / 1e9
-            valu = load_valu(amd, dom, stage_ms[dom], [nxbox, nybox], [bx, by])
+            valu = load_valu(amd, dom, stage_ms[dom], [nxbox, nybox], [bx, by], live_clock)
             frac = achieved / HBM_PEAK_GBS
             # the bound: VALU issue when its floor (at the clock the counter pass measured) takes a larger
             # share of the launch than the HBM bytes do; achieved / peak / frac stay the HBM figures
-            issue = valu.get("issue_frac_at_clock", valu.get("issue_frac")) if valu else None
+            issue = (valu.get("issue_frac_at_live_clock", valu.get("issue_frac_at_clock", valu.get("issue_frac")))
+                     if valu else None)
             traffic, tmatch = load_traffic(amd, dom, local_cells, compact, [nxbox, nybox], [bx, by])
             roof = {"bound": "valu" if issue is not None and issue > frac else "hbm", "kernel": dom,
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -666,9 +679,14 @@ def main():
                     **({"traffic_match": tmatch} if tmatch else {}),
                     "valu": valu,
                     "alg_bytes_per_launch": int(alg), "launch_ms": round(stage_ms[dom], 4)}
+            if dom in ("onepass2", "onepass2_last") and live_clock.get("launches", 0) > 0:
+                # the shader clock the pair launches of this timed region ran at, measured in the kernel
+                roof["live_clock"] = {**live_clock, "source": "ocn_ctx_clock_info (workgroup 0 of each pair launch: "
+                                                              "s_memtime ticks / 100 MHz s_memrealtime ticks)"}
             if roof["bound"] == "valu":
-                roof["bound_note"] = ("VALU issue: issue_frac_at_clock (the SQ_INSTS_VALU floor at the measured clock "
-                                      "/ the launch time) exceeds the HBM fraction; frac is the HBM fraction")
+                roof["bound_note"] = ("VALU issue: issue_frac_at_live_clock (the SQ_INSTS_VALU floor at the clock "
+                                      "measured in the kernel over this timed region / the launch time; "
+                                      "issue_frac_at_clock without it) exceeds the HBM fraction; frac is the HBM fraction")
         step_gbs = B_ALG * cells * args.steps / dt / 1e9 / world
         moved = b_path * cells * args.steps / dt / 1e9 / world
         out = {"metric": METRIC, "value": value, "unit": "cell-updates/s", "n_gpus": world,

@@ -93,6 +93,12 @@ module ocn_sw_c
         real(c_double) :: seq_ms, overlapped_ms
     end type
 
+    ! the shader clock of the pair launches, measured in the kernel (ocn_ctx_clock_info)
+    type, bind(C) :: ocn_clock_info
+        integer(c_int64_t) :: launches
+        real(c_double) :: clock_ghz, sampled_ms
+    end type
+
     interface
         ! ---------------------------------------------------------------- kernel layer
         integer(c_int) function ocn_sw_update_ssh(b, tau, lu, dx, dy, dxh, dyh, hhu, hhv, sshn, sshp, ubrtr, &
@@ -311,6 +317,12 @@ module ocn_sw_c
             import :: c_int, c_ptr, ocn_overlap_info
             type(c_ptr), value :: ctx
             type(ocn_overlap_info), intent(out) :: info
+        end function
+        integer(c_int) function ocn_ctx_clock_info(ctx, reset, info) bind(C, name='ocn_ctx_clock_info')
+            import :: c_int, c_int32_t, c_ptr, ocn_clock_info
+            type(c_ptr), value :: ctx
+            integer(c_int32_t), value :: reset
+            type(ocn_clock_info), intent(out) :: info
         end function
         integer(c_int) function ocn_ctx_set_watchdog(ctx, seconds) bind(C, name='ocn_ctx_set_watchdog')
             import :: c_int, c_double, c_ptr

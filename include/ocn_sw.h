@@ -288,6 +288,17 @@ typedef struct ocn_overlap_info {
     double seq_ms, overlapped_ms;
 } ocn_overlap_info;
 int ocn_ctx_overlap_info(ocn_ctx *ctx, ocn_overlap_info *out);
+/* The shader clock the two-step launches (the dominant kernel: MarchStep pairs) ran at, measured in
+ * the kernel: workgroup 0 of every pair launch counts the s_memtime ticks and the 100 MHz
+ * s_memrealtime ticks over its tiles.  launches = pair launches sampled, clock_ghz = the ticks'
+ * ratio (0 with none), sampled_ms = the real time sampled.  Device-wide (every context on the
+ * context's device) since the last reset; reset != 0 zeroes the counters after reading them.
+ * Synchronises the context's stream.  Telemetry only: no counterpart in the reference. */
+typedef struct ocn_clock_info {
+    int64_t launches;
+    double clock_ghz, sampled_ms;
+} ocn_clock_info;
+int ocn_ctx_clock_info(ocn_ctx *ctx, int32_t reset, ocn_clock_info *out);
 /* Host-side watchdog (seconds > 0; 0 = off): a thread of the context watches every call that may
  * take part in a collective (init_state, step, complete, synchronize, sync, stage, tracer_stage,
  * download, upload, output_r4).  One that has not returned after `seconds` is ended: the watchdog

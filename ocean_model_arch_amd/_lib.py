@@ -99,7 +99,7 @@ CTX_SYMBOLS = ["ocn_decompose", "ocn_halo_schedule", "ocn_ctx_create", "ocn_ctx_
                "ocn_ctx_field", "ocn_ctx_stream", "ocn_comm_unique_id", "ocn_ctx_attach_comm", "ocn_ctx_attach_loopback",
                "ocn_ctx_set_topography", "ocn_ctx_init_state", "ocn_ctx_sync", "ocn_ctx_stage", "ocn_ctx_tracer_stage", "ocn_ctx_step", "ocn_ctx_synchronize",
                "ocn_ctx_download", "ocn_ctx_complete", "ocn_ctx_upload", "ocn_ctx_output_r4", "ocn_ctx_set_option", "ocn_ctx_get_option", "ocn_ctx_stage_times", "ocn_ctx_stage_stats",
-               "ocn_ctx_comm_info", "ocn_ctx_overlap_info", "ocn_ctx_set_watchdog", "ocn_last_error", "ocn_abi_version",
+               "ocn_ctx_comm_info", "ocn_ctx_overlap_info", "ocn_ctx_clock_info", "ocn_ctx_set_watchdog", "ocn_last_error", "ocn_abi_version",
                "ocn_build_id", "ocn_launch_count"]
 ALL_SYMBOLS = KERNEL_SYMBOLS + CTX_SYMBOLS
 
@@ -158,6 +158,10 @@ class OcnCommInfo(C.Structure):
 class OcnOverlapInfo(C.Structure):
     _fields_ = [("level", C.c_int32), ("state", C.c_int32), ("kind", C.c_int32), ("pad", C.c_int32),
                 ("seq_ms", C.c_double), ("overlapped_ms", C.c_double)]
+
+
+class OcnClockInfo(C.Structure):
+    _fields_ = [("launches", C.c_int64), ("clock_ghz", C.c_double), ("sampled_ms", C.c_double)]
 
 
 HALO_LOCAL, HALO_SEND, HALO_RECV = 0, 1, 2
@@ -220,6 +224,7 @@ def lib() -> C.CDLL:
     L.ocn_ctx_stage_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.ocn_ctx_comm_info.argtypes = [C.c_void_p, C.POINTER(OcnCommInfo)]
     L.ocn_ctx_overlap_info.argtypes = [C.c_void_p, C.POINTER(OcnOverlapInfo)]
+    L.ocn_ctx_clock_info.argtypes = [C.c_void_p, C.c_int32, C.POINTER(OcnClockInfo)]
     L.ocn_ctx_set_watchdog.argtypes = [C.c_void_p, C.c_double]
     L.ocn_ctx_attach_comm.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     L.ocn_comm_unique_id.argtypes = [C.c_void_p, C.c_int32]

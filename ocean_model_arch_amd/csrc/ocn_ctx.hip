@@ -3284,6 +3284,20 @@ int ocn_ctx_overlap_info(ocn_ctx *c, ocn_overlap_info *out)
     return OCN_OK;
 }
 
+int ocn_ctx_clock_info(ocn_ctx *c, int32_t reset, ocn_clock_info *out)
+{
+    if (!c || !out) return set_error(OCN_ERR_ARG, "null argument");
+    *out = ocn_clock_info{};
+    HIPCHK(hipSetDevice(c->dec.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    unsigned long long v[3] = {0, 0, 0};
+    RC(clock_read(reset != 0, v));
+    out->launches = (int64_t)v[2];
+    out->clock_ghz = v[1] ? (double)v[0] / ((double)v[1] * 10.0) : 0.0;
+    out->sampled_ms = (double)v[1] * 1e-5;
+    return OCN_OK;
+}
+
 int ocn_ctx_comm_info(ocn_ctx *c, ocn_comm_info *out)
 {
     if (!c || !out) return set_error(OCN_ERR_ARG, "null argument");

@@ -152,6 +152,8 @@ int launch_onepass(const ocn_block *b, void *const *ptr, int nptr, const Compact
 // a single step writes (one role flip); nbad1 / nbad2: the steps' check_ssh_err counts (null: none)
 // last: the second step is the call's last step (MarchStep LAST: the consumers also store vort, the
 // stresses and the RHS terms the reference's last step leaves)
+// the pair launches' shader-clock counters (sw_kernels.hip g_clk: ticks, 100 MHz ticks, launches)
+int clock_read(bool reset, unsigned long long out[3]);
 int launch_onepass_pair(const ocn_block *b, void *const *ptr, int nptr, const Compact *cp, const ocn_sw_params &sw,
                         double tau, int32_t *nbad1, int32_t *nbad2, double *sshp_out, double *up_out, double *vp_out,
                         hipStream_t s, const OnepassKC &kc, bool last = false);

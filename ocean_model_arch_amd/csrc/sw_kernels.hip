@@ -442,6 +442,40 @@ template <class B> struct HasGate<B, std::void_t<decltype(B::kGate)>> { static c
 
 template <class Body, bool PRO = true> __device__ __forceinline__ void march_tile(const MarchRect &R, int tile, const Body &body);
 
+// Shader-clock telemetry of the two-step launches (ocn_ctx_clock_info): workgroup 0 of every pair
+// launch adds the s_memtime ticks of its tiles, their 100 MHz s_memrealtime ticks and 1, with vector
+// atomics -- the clock the dominant kernel ran at, measured while it runs (the device's launches
+// since the last reset, every context on it)
+__device__ unsigned long long g_clk[3];
+struct ClockSample {
+    unsigned long long c0 = 0, w0 = 0;
+    __device__ __forceinline__ void begin()
+    {
+        if (blockIdx.x == 0) { c0 = clock64(); w0 = wall_clock64(); }
+    }
+    __device__ __forceinline__ void end() const
+    {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const unsigned long long c1 = clock64(), w1 = wall_clock64();
+            atomicAdd(&g_clk[0], c1 - c0);
+            atomicAdd(&g_clk[1], w1 - w0);
+            atomicAdd(&g_clk[2], 1ull);
+        }
+    }
+};
+
+int clock_read(bool reset, unsigned long long out[3])
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk), sizeof(g_clk)) != hipSuccess)
+        return set_error(OCN_ERR_HIP, "clock telemetry read");
+    if (reset) {
+        const unsigned long long z[3] = {0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_clk), z, sizeof(z)) != hipSuccess)
+            return set_error(OCN_ERR_HIP, "clock telemetry reset");
+    }
+    return OCN_OK;
+}
+
 template <class Body>
 __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Body body)
 {
@@ -458,7 +492,10 @@ __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march(MarchGrid g, Bo
 #if OCN_CLOCK_PROBE   // diagnostic build only (scripts/gpu_clock_probe.sh): workgroup 0's shader clock
     const unsigned long long c0 = clock64(), w0 = wall_clock64();
 #endif
+    ClockSample clk;
+    if constexpr (HasPair<Body>::v) clk.begin();
     march_tile(g.r[k], tile, body);
+    if constexpr (HasPair<Body>::v) clk.end();
 #if OCN_CLOCK_PROBE
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const unsigned long long c1 = clock64(), w1 = wall_clock64();
@@ -484,7 +521,10 @@ __global__ __launch_bounds__(256, WavesOf<Body>::v) void k_march_b(MarchGridB g,
     const Body &body = bodies.b[__builtin_amdgcn_readfirstlane(g.blk[k])];
     if constexpr (HasGate<Body>::v)
         if (!body.enabled()) return;
+    ClockSample clk;
+    if constexpr (HasPair<Body>::v) clk.begin();
     march_tile(g.r[k], tile, body);
+    if constexpr (HasPair<Body>::v) clk.end();
 }
 
 template <class Body> struct MarchBatch;

@@ -182,6 +182,15 @@ class OceanModel:
         return {"level": int(i.level), "state": int(i.state), "kind": int(i.kind),
                 "seq_ms": round(float(i.seq_ms), 4), "overlapped_ms": round(float(i.overlapped_ms), 4)}
 
+    def clock_info(self, reset: bool = False) -> dict:
+        """ocn_ctx_clock_info: the shader clock the pair launches ran at (measured in the kernel by
+        workgroup 0 of each launch; device-wide since the last reset -- reset=True zeroes it after
+        reading)."""
+        i = _lib.OcnClockInfo()
+        check(lib().ocn_ctx_clock_info(self.ctx, int(bool(reset)), C.byref(i)), "ocn_ctx_clock_info")
+        return {"launches": int(i.launches), "clock_ghz": round(float(i.clock_ghz), 4),
+                "sampled_ms": round(float(i.sampled_ms), 4)}
+
     def set_exchange_delay(self, us: int):
         """Tests: the device waits `us` microseconds before each exchange with remote peers
         (OCN_OPT_XCHG_DELAY: a slow link)."""

@@ -119,6 +119,25 @@ def test_valu_needs_matching_stamp(tmp_path, monkeypatch):
     assert bench.load_valu(_Amd("abc"), "hh_init", 2.0, [64, 64], [1, 1]) is None
 
 
+def test_valu_at_live_clock(tmp_path, monkeypatch):
+    """roofline.valu at the clock measured in the pair kernel over the timed region
+    (ocn_ctx_clock_info): the floor scales with 2.4 GHz / the live clock; only for the pair launch
+    and only when pair launches were sampled."""
+    per_launch = {"SQ_INSTS_VALU": 1024 * 2.4e6 / 4, "SQ_WAVES": 10}     # 1 ms of issue at 2.4 GHz
+    per_wave = {"SQ_WAVE_CYCLES": 100.0, "SQ_ACTIVE_INST_VALU": 60.0, "SQ_WAIT_INST_ANY": 30.0, "SQ_WAIT_ANY": 10.0}
+    rec = {"build_id": "abc", "box": [64, 64], "blocks": [1, 1],
+           "kernels": {"onepass2": {"per_launch": per_launch, "per_wave": per_wave}}}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "sq_valu.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    live = {"launches": 9, "clock_ghz": 1.2, "sampled_ms": 5.0}
+    v = bench.load_valu(_Amd("abc"), "onepass2", 4.0, [64, 64], [1, 1], live)
+    assert v["live_clock_ghz"] == 1.2 and v["issue_floor_ms_at_live_clock"] == 2.0
+    assert v["issue_frac_at_live_clock"] == 0.5 and "9 pair launches" in v["live_clock_source"]
+    v = bench.load_valu(_Amd("abc"), "onepass2", 4.0, [64, 64], [1, 1], {"launches": 0, "clock_ghz": 0.0})
+    assert "live_clock_ghz" not in v
+
+
 def test_hr_variant_bytes():
     """The known-constant one-pass variant that reads h_r (a topography) moves 8 B per cell more
     than the one with h_r a constant and 24 B less than the general one (101 one-pass launches in

@@ -188,6 +188,29 @@ def test_first_call_waits_for_the_verdict(amd, name, calls, want):
     assert used == want, (used, want)
 
 
+def test_pair_clock_telemetry(amd):
+    """ocn_ctx_clock_info: workgroup 0 of every pair launch counts the shader clock against the
+    100 MHz real-time counter -- one sample per pair launch, a clock within the part's range, the
+    counters zeroed by a reset; single launches add nothing."""
+    m = amd.OceanModel(amd.box_config(1024)).init()
+    try:
+        m.step(2, check_every=1).synchronize()
+        m.clock_info(reset=True)
+        m.set_pair(0)
+        m.step(4, check_every=1).synchronize()
+        assert m.clock_info()["launches"] == 0
+        m.set_pair(1)
+        m.step(7, check_every=1)
+        pairs = m.pair_active
+        c = m.clock_info(reset=True)
+        again = m.clock_info()
+    finally:
+        m.close()
+    assert pairs and c["launches"] >= 2, c
+    assert 0.5 < c["clock_ghz"] < 3.0 and c["sampled_ms"] > 0.0, c
+    assert again["launches"] == 0 and again["clock_ghz"] == 0.0, again
+
+
 def test_pair_counts_blowup_points_once(amd):
     """check_ssh_err_kernel (vel_ssh.f90:40-67) in pair launches: each step counts its points once
     (the producers count only their workgroup's own rows) -- the reported count equals the single
