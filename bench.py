@@ -241,10 +241,10 @@ def cpu_cores() -> int:
 def cpu_baseline(n_full: int = 4096):
     """The CPU path on this node's host cores: the C restatement of the reference
     (oracle/, bitwise the reference's results) timed on bounded samples of the bench workload --
-      1 core : a 2048^2 box (a quarter of the workload), 1 block, 6 timed steps;
+      1 core : a 2048^2 box (a quarter of the workload), 1 block, 24 timed steps (~8 s);
       C cores: the 4096^2 box decomposed into C blocks (MPI_Dims_create(C) grid), one block per
                core -- the reference's OpenMP-over-blocks mode (kernel_interface.f90:84-88) --
-               6 timed steps.
+               30 timed steps (~5 s on 16 cores).
     Each leg runs 1 untimed warm-up step first.  `value` is the C-core rate."""
     from oracle import oracle as O
     cores = cpu_cores()
@@ -259,13 +259,14 @@ def cpu_baseline(n_full: int = 4096):
             om.pool.shutdown()
         return n * n * steps / dt, dt
 
-    v1, t1 = leg(2048, (1, 1), 1, 6)
+    s1, sc = 24, 30
+    v1, t1 = leg(2048, (1, 1), 1, s1)
     bxy = dims_create(cores)
-    vc, tc = leg(n_full, bxy, cores, 6)
+    vc, tc = leg(n_full, bxy, cores, sc)
     return {"value": vc, "unit": "cell-updates/s", "cores": cores, "kind": "port",
-            "1core": {"value": v1, "sample": f"2048x2048 box, 1 block, 6 timed steps, {t1:.1f} s"},
+            "1core": {"value": v1, "sample": f"2048x2048 box, 1 block, {s1} timed steps, {t1:.1f} s"},
             "allcores": {"value": vc, "cores": cores,
-                         "sample": f"{n_full}x{n_full} box, {bxy[0]}x{bxy[1]} blocks on {cores} threads, 6 timed steps, "
+                         "sample": f"{n_full}x{n_full} box, {bxy[0]}x{bxy[1]} blocks on {cores} threads, {sc} timed steps, "
                                    f"{tc:.1f} s"},
             "sample": "oracle/sw_oracle.c (gcc -O2 -ffp-contract=off, bitwise the reference) on this node's host cores; "
                       "value = the all-cores leg"}
